@@ -1,0 +1,323 @@
+/*
+ * lorb_c.h -- C-ABI drop-in boundary of the MI355X-native LORB_SLAM hot path.
+ *
+ * Everything here is `extern "C"`, POD structs and plain pointers + sizes.  No torch, no
+ * OpenCV, no Ceres types cross this boundary.  Each entry point names the reference
+ * interface it replaces (paths relative to the reference repo abstract-liu/LORB_SLAM @ v0).
+ *
+ * Conventions
+ *   - Every function returns int: LORB_OK (0) or a negative LORB_E_* code.  The message of
+ *     the last error on a context is available from lorb_last_error(ctx).  No C++ exception
+ *     ever crosses the ABI.
+ *   - Functions without a `_dev` suffix take HOST pointers; they stage through device
+ *     buffers owned by the context and are synchronous.  `_dev` variants take DEVICE
+ *     pointers (allocated with lorb_malloc) and are asynchronous on the context's stream.
+ *   - The library never takes ownership of caller memory.
+ *   - One lorb_ctx per calling thread (it owns one hipStream_t).  A ctx is not thread-safe.
+ *   - Keypoint / map-point identity: the C-ABI never sees MapPoint*.  Results are returned as
+ *     per-slot "assign" codes that the C++ adapter applies to Frame::mvpMapPoints.
+ */
+#ifndef LORB_C_H
+#define LORB_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LORB_ABI_VERSION 1
+
+#define LORB_OK 0
+#define LORB_E_INVALID (-1)   /* bad argument / shape */
+#define LORB_E_DEVICE  (-2)   /* HIP runtime error (no device, launch failure, OOM) */
+#define LORB_E_NOMEM   (-3)   /* host allocation failure */
+#define LORB_E_UNSUPPORTED (-4)
+#define LORB_E_COMM    (-5)   /* RCCL error */
+
+/* Matcher constants, src/matcher.cpp:6-8 */
+#define LORB_TH_HIGH 100
+#define LORB_TH_LOW 50
+#define LORB_HISTO_LENGTH 30
+/* Frame grid, include/frame.h:13-14 */
+#define LORB_GRID_ROWS 48
+#define LORB_GRID_COLS 64
+#define LORB_DESC_BYTES 32
+#define LORB_MAX_LEVELS 16
+
+/* assign codes written per current-frame keypoint slot by the windowed matchers */
+#define LORB_ASSIGN_UNCHANGED (-1)  /* slot keeps whatever MapPoint* it held */
+#define LORB_ASSIGN_NULL      (-2)  /* slot set to NULL (rotation-consistency null-out) */
+
+/* slot state of a current-frame keypoint before a windowed match
+ * (reference test: `if(F->mvpMapPoints[i] && F->mvpMapPoints[i]->mnObs>0) continue;`,
+ *  src/matcher.cpp:149-151, 273-275) */
+#define LORB_SLOT_EMPTY   0  /* mvpMapPoints[i] == NULL            */
+#define LORB_SLOT_FREE    1  /* MapPoint present with mnObs == 0   */
+#define LORB_SLOT_LOCKED  2  /* MapPoint present with mnObs  > 0   */
+
+typedef struct lorb_ctx lorb_ctx;
+
+/* ----------------------------------------------------------------------------------------
+ * Context / runtime
+ * -------------------------------------------------------------------------------------- */
+int lorb_abi_version(void);
+int lorb_device_count(int* count);
+int lorb_create(int device, lorb_ctx** out);
+int lorb_destroy(lorb_ctx* ctx);
+const char* lorb_last_error(const lorb_ctx* ctx);
+int lorb_sync(lorb_ctx* ctx);                       /* hipStreamSynchronize(ctx stream) */
+int lorb_malloc(lorb_ctx* ctx, void** dptr, size_t bytes);
+int lorb_free(lorb_ctx* ctx, void* dptr);
+int lorb_memcpy_h2d(lorb_ctx* ctx, void* dst, const void* src, size_t bytes);  /* sync */
+int lorb_memcpy_d2h(lorb_ctx* ctx, void* dst, const void* src, size_t bytes);  /* sync */
+int lorb_memset_dev(lorb_ctx* ctx, void* dst, int value, size_t bytes);        /* async */
+/* hipEvent timer on the ctx stream: marks, then elapsed ms between two marks */
+int lorb_timer_mark(lorb_ctx* ctx, int slot);        /* slot in [0,64) */
+int lorb_timer_elapsed_ms(lorb_ctx* ctx, int slot_begin, int slot_end, float* ms);
+/* Per-kernel device timing (HIP events recorded around every launch of the named kernel
+ * family on the ctx stream).  Used by bench.py for roofline.achieved.  Kernel ids: */
+#define LORB_K_BF_SCAN_TOP2 0
+#define LORB_K_BF_SCAN_TOP1 1
+#define LORB_K_BA_SCHUR     2
+#define LORB_K_BA_LINEARIZE 3
+#define LORB_K_BA_CHOLESKY  4
+#define LORB_K_WINDOW_CAND  5
+#define LORB_K_COUNT        8
+int lorb_kernel_timing_enable(lorb_ctx* ctx, int enable);
+/* sums (and resets) the recorded launches of kernel id k: total ms and launch count */
+int lorb_kernel_timing_read(lorb_ctx* ctx, int k, double* total_ms, int* launches);
+
+/* ----------------------------------------------------------------------------------------
+ * Frame description shared by the matchers (all fields are the reference Frame's, float)
+ * -------------------------------------------------------------------------------------- */
+typedef struct lorb_frame_params {
+  float fx, fy, cx, cy;               /* Frame::fx,fy,cx,cy        include/frame.h:96 */
+  float bf, b;                        /* Frame::mbf, Frame::mb     include/frame.h:96 */
+  float min_x, max_x, min_y, max_y;   /* Frame::mnMinX..mnMaxY     include/frame.h:98-101 */
+  float grid_w_inv, grid_h_inv;       /* mfGridElementWidthInv/HeightInv, src/frame.cpp:83-84 */
+  int32_t n_levels;                   /* mnScaleLevels */
+  float log_scale_factor;             /* mfLogScaleFactor */
+  float scale_factors[LORB_MAX_LEVELS]; /* mvScaleFactors */
+} lorb_frame_params;
+
+/* SoA view of a frame's undistorted keypoints (Frame::mvKeysUn) + stereo + descriptors */
+typedef struct lorb_keypoints {
+  int32_t n;                 /* Frame::mnMapPoints */
+  const float* x;            /* mvKeysUn[i].pt.x */
+  const float* y;            /* mvKeysUn[i].pt.y */
+  const int32_t* octave;     /* mvKeysUn[i].octave */
+  const float* angle;        /* mvKeysUn[i].angle */
+  const float* u_right;      /* mvuRight[i] (NULL => all -1) */
+  const uint8_t* desc;       /* mDescriptors, n x 32 bytes row-major */
+} lorb_keypoints;
+
+/* ----------------------------------------------------------------------------------------
+ * (a2/a3) brute-force Hamming + OpenCV-3.x crossCheck + the reference's outlier filter.
+ * Replaces cv::BFMatcher(NORM_HAMMING,true).match at src/matcher.cpp:36-39 and :342-345 and
+ * the minDist filter at src/matcher.cpp:42-56 / :348-362.
+ *
+ * Batched over n_problems independent (query set, train set) pairs, concatenated:
+ *   problem p owns queries [q_off[p], q_off[p+1]) and trains [t_off[p], t_off[p+1]).
+ *   q_off / t_off are HOST arrays of n_problems+1 entries (also for the _dev variant).
+ * Outputs per query (global query index):
+ *   cc_train[q]  : OpenCV crossCheck train index (problem-local) or -1 (no DMatch emitted)
+ *   cc_dist[q]   : its Hamming distance (undefined when cc_train == -1)
+ *   match_train[q]: cc_train[q] if cc_dist <= max(2*minDist, 30) else -1   (src/matcher.cpp:52)
+ * n_matches[p] : number of accepted matches of problem p (the reference's return value).
+ * -------------------------------------------------------------------------------------- */
+int lorb_bf_match(lorb_ctx* ctx, int32_t n_problems,
+                  const uint8_t* q_desc, const int32_t* q_off,
+                  const uint8_t* t_desc, const int32_t* t_off,
+                  int32_t* cc_train, int32_t* cc_dist, int32_t* match_train,
+                  int32_t* n_matches);
+int lorb_bf_match_dev(lorb_ctx* ctx, int32_t n_problems,
+                      const uint8_t* d_q_desc, const int32_t* q_off,
+                      const uint8_t* d_t_desc, const int32_t* t_off,
+                      int32_t* d_cc_train, int32_t* d_cc_dist, int32_t* d_match_train,
+                      int32_t* d_n_matches);
+
+/* ----------------------------------------------------------------------------------------
+ * (a5 with an unbounded window; BASELINE config "2000x2000 random 256-bit, ratio test")
+ * Brute-force best/second-best with the reference's exact tie semantics
+ * (src/matcher.cpp:289-301: strict '<', first candidate in train order wins) and the
+ * level-gated ratio test + TH_HIGH acceptance (src/matcher.cpp:305-311).
+ * t_level: per-train octave (NULL => all 0, i.e. ratio test always active).
+ * Outputs per query: best_idx (-1 if none), best_dist (256 if none), best_level (-1),
+ *   second_dist (256), second_level (-1), accepted (0/1).
+ * -------------------------------------------------------------------------------------- */
+int lorb_bf_top2(lorb_ctx* ctx, int32_t n_problems,
+                 const uint8_t* q_desc, const int32_t* q_off,
+                 const uint8_t* t_desc, const int32_t* t_off, const int32_t* t_level,
+                 int32_t* best_idx, int32_t* best_dist, int32_t* best_level,
+                 int32_t* second_dist, int32_t* second_level, uint8_t* accepted);
+int lorb_bf_top2_dev(lorb_ctx* ctx, int32_t n_problems,
+                     const uint8_t* d_q_desc, const int32_t* q_off,
+                     const uint8_t* d_t_desc, const int32_t* t_off, const int32_t* d_t_level,
+                     int32_t* d_best_idx, int32_t* d_best_dist, int32_t* d_best_level,
+                     int32_t* d_second_dist, int32_t* d_second_level, uint8_t* d_accepted);
+
+/* ----------------------------------------------------------------------------------------
+ * (a4) Matcher::SearchByProjection(Frame* CurrentFrame, Frame* LastFrame, const float th)
+ *      src/matcher.cpp:64-218, incl. Frame::GetFeaturesInArea (src/frame.cpp:370-423),
+ *      the grid (src/frame.cpp:87-115) and the rotation histogram / ComputeThreeMaxima.
+ * -------------------------------------------------------------------------------------- */
+typedef struct lorb_last_frame {
+  int32_t n;                 /* LastFrame->mnMapPoints */
+  const float* Tcw;          /* LastFrame->mTcw, 4x4 row-major */
+  const uint8_t* has_mp;     /* mvpMapPoints[i] != NULL */
+  const uint8_t* outlier;    /* mvbOutlier[i] (NULL => all false) */
+  const uint8_t* mp_locked;  /* mvpMapPoints[i]->mnObs > 0 */
+  const float* mp_pos;       /* mvpMapPoints[i]->GetPos(), n x 3 */
+  const uint8_t* mp_desc;    /* mvpMapPoints[i]->GetDescriptor(), n x 32 */
+  const int32_t* octave;     /* LastFrame->mvKeys[i].octave */
+  const float* angle;        /* LastFrame->mvKeysUn[i].angle */
+} lorb_last_frame;
+
+/* assign[j] for current keypoint j: LORB_ASSIGN_UNCHANGED, LORB_ASSIGN_NULL, or i >= 0 meaning
+ * CurrentFrame->mvpMapPoints[j] = LastFrame->mvpMapPoints[i].  *nmatches = return value. */
+int lorb_search_by_projection_frame(lorb_ctx* ctx,
+                                    const lorb_frame_params* cur, const float cur_Tcw[16],
+                                    const lorb_keypoints* cur_kps, const uint8_t* cur_slot_state,
+                                    const lorb_last_frame* last, float th,
+                                    int32_t* assign, int32_t* nmatches);
+
+/* ----------------------------------------------------------------------------------------
+ * (a5) Matcher::SearchByProjection(Frame* F, const std::set<MapPoint*>&, const float th)
+ *      src/matcher.cpp:220-316.  Points are given flattened in std::set iteration order.
+ * -------------------------------------------------------------------------------------- */
+typedef struct lorb_local_points {
+  int32_t n;
+  const uint8_t* track_in_view;   /* mbTrackInView */
+  const uint8_t* is_bad;          /* IsBad() (NULL => none) */
+  const uint8_t* locked;          /* mnObs > 0 */
+  const float* proj_x;            /* mTrackProjX */
+  const float* proj_y;            /* mTrackProjY */
+  const float* proj_xr;           /* mTrackProjXR */
+  const int32_t* pred_level;      /* mnTrackScaleLevel */
+  const float* view_cos;          /* mTrackViewCos */
+  const uint8_t* desc;            /* GetDescriptor(), n x 32 */
+} lorb_local_points;
+
+/* assign[j]: LORB_ASSIGN_UNCHANGED or local point index k (F->mvpMapPoints[j] = point k). */
+int lorb_search_by_projection_local(lorb_ctx* ctx,
+                                    const lorb_frame_params* frame, const lorb_keypoints* kps,
+                                    const uint8_t* slot_state,
+                                    const lorb_local_points* pts, float th,
+                                    int32_t* assign, int32_t* nmatches);
+
+/* ----------------------------------------------------------------------------------------
+ * (a8) Frame::IsInFrustum (src/frame.cpp:425-494) + MapPoint::PredictScale
+ *      (src/map_point.cpp:267-284), batched over points.  Writes the tracking fields.
+ * -------------------------------------------------------------------------------------- */
+typedef struct lorb_frustum_points {
+  int32_t n;
+  const float* pos;        /* GetPos(), n x 3 */
+  const float* normal;     /* mNormalVector, n x 3 */
+  const float* max_dist;   /* mfMaxDistance  (GetMaxDistanceInvariance = 1.2f*mfMaxDistance) */
+  const float* min_dist;   /* mfMinDistance  (GetMinDistanceInvariance = 0.8f*mfMinDistance) */
+} lorb_frustum_points;
+int lorb_is_in_frustum(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
+                       const lorb_frustum_points* pts, float viewing_cos_limit,
+                       uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
+                       int32_t* pred_level, float* view_cos);
+
+/* (a20) Frame::UnprojectStereo, src/frame.cpp:335-356, batched over keypoints. */
+int lorb_unproject_stereo(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
+                          int32_t n, const float* x, const float* y, const float* depth,
+                          float* out_xyz);
+
+/* ----------------------------------------------------------------------------------------
+ * Bundle adjustment: Ceres-default Levenberg-Marquardt + DENSE_SCHUR restated
+ * (src/bundle_adjust.cpp:158-202 and :207-330; solver defaults in SURVEY Appendix B).
+ * -------------------------------------------------------------------------------------- */
+#define LORB_TERM_NO_CONVERGENCE 0   /* max_num_iterations reached */
+#define LORB_TERM_FUNCTION_TOL   1
+#define LORB_TERM_GRADIENT_TOL   2
+#define LORB_TERM_PARAMETER_TOL  3
+#define LORB_TERM_MIN_RADIUS     4
+#define LORB_TERM_FAILURE        5   /* too many consecutive invalid steps */
+
+typedef struct lorb_lm_options {       /* defaults == ceres::Solver::Options defaults */
+  int32_t max_num_iterations;          /* 50 */
+  double function_tolerance;           /* 1e-6 */
+  double gradient_tolerance;           /* 1e-10 */
+  double parameter_tolerance;          /* 1e-8 */
+  double initial_trust_region_radius;  /* 1e4 */
+  double max_trust_region_radius;      /* 1e16 */
+  double min_trust_region_radius;      /* 1e-32 */
+  double min_relative_decrease;        /* 1e-3 */
+  double min_lm_diagonal;              /* 1e-6 */
+  double max_lm_diagonal;              /* 1e32 */
+  int32_t max_num_consecutive_invalid_steps; /* 5 */
+  int32_t jacobi_scaling;              /* 1 */
+} lorb_lm_options;
+void lorb_lm_options_default(lorb_lm_options* opt);
+
+typedef struct lorb_ba_summary {
+  int32_t iterations;          /* LM iterations performed (successful + unsuccessful) */
+  int32_t successful_steps;
+  int32_t termination;         /* LORB_TERM_* */
+  int32_t pad_;
+  double initial_cost;         /* 0.5 * sum r^2 */
+  double final_cost;
+} lorb_ba_summary;
+
+/* (a12) BA::ProjectPoseOptimization: pose-only, one PoseCost per matched map point.
+ * The PoseCost quirk (v projected with fx, src/bundle_adjust.cpp:51) is reproduced by passing
+ * fy_eff = fx; pass the real fy to get the "fixed" projection.  Batched over frames:
+ * frame f owns residuals [res_off[f], res_off[f+1]) (HOST array).
+ * pose_init: n_frames x 6 floats = (mRvec | mTvec)  (src/bundle_adjust.cpp:163-168)
+ * pose_out:  n_frames x 6 doubles (the Ceres parameter blocks after Solve)
+ * Tcw_out (optional): n_frames x 16 floats, Frame::SetPose(T,R) write-back via Rodrigues
+ *   (src/bundle_adjust.cpp:198-201 -> src/frame.cpp:577-594). */
+typedef struct lorb_pose_problem_batch {
+  int32_t n_frames;
+  const int32_t* res_off;      /* n_frames+1 */
+  const float* intr;           /* n_frames x 4: fx, fy_eff, cx, cy */
+  const float* pose_init;      /* n_frames x 6 */
+  const float* pts3d;          /* n_res x 3 (MapPoint::GetPos) */
+  const float* obs2d;          /* n_res x 2 (Frame::GetKp2d) */
+} lorb_pose_problem_batch;
+int lorb_ba_pose_only(lorb_ctx* ctx, const lorb_pose_problem_batch* prob,
+                      const lorb_lm_options* opt, double* pose_out, float* Tcw_out,
+                      lorb_ba_summary* summaries);
+
+/* (a13) BA::LocalPoseOptimization: poses + points, MPCost for out-of-window (fixed) frames,
+ * PoseMPCost for window frames.  One window per problem; batched over windows.
+ * obs_frame[k] >= 0 : optimised pose index (PoseMPCost, src/bundle_adjust.cpp:293-301)
+ * obs_frame[k] <  0 : fixed frame index (-1 - obs_frame[k]) (MPCost, :283-290) */
+typedef struct lorb_ba_window {
+  int32_t n_poses, n_fixed, n_points, n_obs;
+  float fx, fy, cx, cy;
+  const float* pose_init;      /* n_poses x 6 (mRvec|mTvec) */
+  const float* fixed_pose;     /* n_fixed x 6 */
+  const float* point_init;     /* n_points x 3 */
+  const int32_t* obs_point;    /* n_obs */
+  const int32_t* obs_frame;    /* n_obs */
+  const float* obs_uv;         /* n_obs x 2 */
+} lorb_ba_window;
+
+int lorb_ba_local(lorb_ctx* ctx, int32_t n_windows, const lorb_ba_window* windows,
+                  const lorb_lm_options* opt, double* const* pose_out,
+                  double* const* point_out, lorb_ba_summary* summaries);
+
+/* Device-resident plan for repeated solves of the same window batch (benchmarks, LM in
+ * a captured HIP graph).  create: uploads + builds the Schur structure; solve: runs the LM
+ * from the uploaded initial values entirely on the device (async); read: copies results. */
+typedef struct lorb_ba_plan lorb_ba_plan;
+int lorb_ba_plan_create(lorb_ctx* ctx, int32_t n_windows, const lorb_ba_window* windows,
+                        lorb_ba_plan** out);
+int lorb_ba_plan_solve(lorb_ba_plan* plan, const lorb_lm_options* opt);
+int lorb_ba_plan_read(lorb_ba_plan* plan, double* const* pose_out, double* const* point_out,
+                      lorb_ba_summary* summaries);
+int lorb_ba_plan_destroy(lorb_ba_plan* plan);
+
+/* Rodrigues vector -> Tcw (float), cv::Rodrigues semantics (double internally). */
+void lorb_pose_to_Tcw(const float rvec[3], const float tvec[3], float Tcw[16]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LORB_C_H */

@@ -1,0 +1,418 @@
+// lorb_bf.hip -- brute-force ORB Hamming matching on gfx950 (MI355X).
+//
+// Replaces cv::BFMatcher(NORM_HAMMING, crossCheck=true).match (src/matcher.cpp:36-39, 342-345)
+// and the best/second-best scan of Matcher::SearchByProjection (src/matcher.cpp:289-311) for an
+// unbounded window (BASELINE config "2000x2000 random 256-bit descriptors, ratio test").
+//
+// Design (CDNA4-first, integer VALU bound -- no GEMM reshaping):
+//   * One "scan" kernel: each lane owns one descriptor of the LANE side (8 VGPRs), the wave
+//     walks the UNIFORM side in order.  Uniform descriptors are wave-uniform addresses, so they
+//     arrive through the scalar cache (s_load) straight into SGPRs -- no LDS traffic at all.
+//   * Distance: 8 x v_xor_b32 + 8 x v_bcnt_u32_b32 (popcount-accumulate).
+//   * Tie semantics are folded into one 32-bit key = (dist << 23) | uniform_index, so
+//     "strict <, first index wins" == unsigned min.  Top-2 of keys costs v_min + v_med3
+//     per pair; top-1 (cross-check reverse pass) costs one v_min.
+//   * Large problems are split into uniform-side chunks (more workgroups) and merged by a
+//     tiny deterministic merge kernel (top-2 of keys is associative).
+//   * Cross-check: the reverse pass (lanes = trains, uniform = queries) yields each train's
+//     nearest query; a 64-bit atomicMin of (dist<<32 | train) per query reproduces OpenCV's
+//     ascending-train "if (d < dist[q])" resolution exactly; a per-problem block then applies
+//     the reference's minDist / max(2*minDist, 30) filter.
+#include "lorb_internal.h"
+
+namespace {
+
+constexpr uint32_t kIdxBits = 23;
+constexpr uint32_t kIdxMask = (1u << kIdxBits) - 1u;
+constexpr uint32_t kSentinel = 256u << kIdxBits;  // "dist 256, index 0": never beaten by d=256
+
+struct BfTile {
+  int32_t lane_base;   // first lane descriptor (global index into the lane array)
+  int32_t lane_count;  // <= 256
+  int32_t uni_base;    // first uniform descriptor (global index)
+  int32_t uni_count;   // uniform descriptors in this chunk
+  int32_t uni_local0;  // problem-local index of uni_base (goes into the key)
+  int32_t out_base;    // partial-output index of lane 0 (chunk-major)
+};
+
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// popcount-accumulate chain: one v_xor_b32 + one v_bcnt_u32_b32 per 32-bit word (16 VALU/pair)
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
+  uint32_t r;
+  asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+  return r;
+}
+
+__device__ __forceinline__ uint32_t hamming256(const uint4& a0, const uint4& a1, const uint4& b0,
+                                               const uint4& b1) {
+  uint32_t d = __builtin_popcount(a0.x ^ b0.x);
+  d = bcnt_acc(a0.y ^ b0.y, d);
+  d = bcnt_acc(a0.z ^ b0.z, d);
+  d = bcnt_acc(a0.w ^ b0.w, d);
+  d = bcnt_acc(a1.x ^ b1.x, d);
+  d = bcnt_acc(a1.y ^ b1.y, d);
+  d = bcnt_acc(a1.z ^ b1.z, d);
+  d = bcnt_acc(a1.w ^ b1.w, d);
+  return d;
+}
+
+template <bool TOP2>
+__global__ __launch_bounds__(256) void k_bf_scan(const uint4* __restrict__ lane_desc,
+                                                 const uint4* __restrict__ uni_desc,
+                                                 const BfTile* __restrict__ tiles,
+                                                 uint32_t* __restrict__ k1_out,
+                                                 uint32_t* __restrict__ k2_out) {
+  const BfTile tl = tiles[blockIdx.x];
+  const int l = threadIdx.x;
+  const bool active = l < tl.lane_count;
+  uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+  if (active) {
+    a0 = lane_desc[2 * (size_t)(tl.lane_base + l)];
+    a1 = lane_desc[2 * (size_t)(tl.lane_base + l) + 1];
+  }
+  uint32_t k1 = kSentinel, k2 = kSentinel;
+  const uint4* __restrict__ u = uni_desc + 2 * (size_t)tl.uni_base;
+  const uint32_t kb = (uint32_t)tl.uni_local0;
+  const int n = tl.uni_count;
+  int j = 0;
+  for (; j + 4 <= n; j += 4) {
+    uint4 b[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) b[s] = u[2 * j + s];  // 4 descriptors -> SGPRs (s_load) up front
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t key = (hamming256(a0, a1, b[2 * s], b[2 * s + 1]) << kIdxBits) + kb + (uint32_t)(j + s);
+      if (TOP2) k2 = umed3(k1, key, k2);
+      k1 = min(k1, key);
+    }
+  }
+  for (; j < n; ++j) {
+    const uint4 b0 = u[2 * j], b1 = u[2 * j + 1];
+    const uint32_t key = (hamming256(a0, a1, b0, b1) << kIdxBits) + kb + (uint32_t)j;
+    if (TOP2) k2 = umed3(k1, key, k2);
+    k1 = min(k1, key);
+  }
+  if (active) {
+    k1_out[tl.out_base + l] = k1;
+    if (TOP2) k2_out[tl.out_base + l] = k2;
+  }
+}
+
+// merge chunk partials: part[c * n + i] -> out[i]
+template <bool TOP2>
+__global__ __launch_bounds__(256) void k_bf_merge(const uint32_t* __restrict__ k1p,
+                                                  const uint32_t* __restrict__ k2p, int n,
+                                                  int n_chunks, uint32_t* __restrict__ k1o,
+                                                  uint32_t* __restrict__ k2o) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k1 = kSentinel, k2 = kSentinel;
+  for (int c = 0; c < n_chunks; ++c) {
+    const uint32_t a = k1p[(size_t)c * n + i];
+    if (TOP2) k2 = umed3(k1, a, k2);
+    k1 = min(k1, a);
+    if (TOP2) {
+      const uint32_t b = k2p[(size_t)c * n + i];
+      k2 = umed3(k1, b, k2);
+      k1 = min(k1, b);
+    }
+  }
+  k1o[i] = k1;
+  if (TOP2) k2o[i] = k2;
+}
+
+__device__ __forceinline__ int find_problem(const int32_t* __restrict__ off, int np, int i) {
+  int lo = 0, hi = np - 1;  // largest p with off[p] <= i
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// decode top-2 keys + level-gated ratio test (src/matcher.cpp:305-311)
+__global__ __launch_bounds__(256) void k_top2_finalize(
+    const uint32_t* __restrict__ k1, const uint32_t* __restrict__ k2, int nq,
+    const int32_t* __restrict__ q_off, const int32_t* __restrict__ t_off, int np,
+    const int32_t* __restrict__ t_level, int32_t* __restrict__ best_idx,
+    int32_t* __restrict__ best_dist, int32_t* __restrict__ best_level,
+    int32_t* __restrict__ second_dist, int32_t* __restrict__ second_level,
+    uint8_t* __restrict__ accepted) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nq) return;
+  const int p = find_problem(q_off, np, i);
+  const int tb = t_off[p];
+  const bool has_t = t_off[p + 1] > tb;
+  const uint32_t a = has_t ? k1[i] : kSentinel, b = has_t ? k2[i] : kSentinel;
+  const int d1 = (int)(a >> kIdxBits), d2 = (int)(b >> kIdxBits);
+  const int i1 = d1 < 256 ? (int)(a & kIdxMask) : -1;
+  const int i2 = d2 < 256 ? (int)(b & kIdxMask) : -1;
+  const int l1 = i1 >= 0 ? (t_level ? t_level[tb + i1] : 0) : -1;
+  const int l2 = i2 >= 0 ? (t_level ? t_level[tb + i2] : 0) : -1;
+  int acc = 0;
+  if (d1 <= LORB_TH_HIGH) {
+    acc = 1;
+    if (l1 == l2 && (double)d1 > 0.8 * (double)d2) acc = 0;
+  }
+  best_idx[i] = i1;
+  best_dist[i] = d1;
+  best_level[i] = l1;
+  second_dist[i] = d2;
+  second_level[i] = l2;
+  accepted[i] = (uint8_t)acc;
+}
+
+// cross-check resolution: per train, offer (dist, train) to its nearest query
+__global__ __launch_bounds__(256) void k_cc_scatter(const uint32_t* __restrict__ tkey, int nt,
+                                                    const int32_t* __restrict__ q_off,
+                                                    const int32_t* __restrict__ t_off, int np,
+                                                    unsigned long long* __restrict__ qkey) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nt) return;
+  const int p = find_problem(t_off, np, t);
+  if (q_off[p + 1] == q_off[p]) return;
+  const uint32_t k = tkey[t];
+  const uint32_t q = k & kIdxMask, d = k >> kIdxBits;
+  const unsigned long long v = ((unsigned long long)d << 32) | (unsigned)(t - t_off[p]);
+  atomicMin(&qkey[q_off[p] + q], v);
+}
+
+// one workgroup per problem: DMatch list + minDist filter (src/matcher.cpp:42-56)
+__global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* __restrict__ qkey,
+                                                     const int32_t* __restrict__ q_off,
+                                                     const int32_t* __restrict__ t_off,
+                                                     int32_t* __restrict__ cc_train,
+                                                     int32_t* __restrict__ cc_dist,
+                                                     int32_t* __restrict__ match_train,
+                                                     int32_t* __restrict__ n_matches) {
+  const int p = blockIdx.x;
+  const int q0 = q_off[p], q1 = q_off[p + 1];
+  const bool has_t = t_off[p + 1] > t_off[p];
+  __shared__ int s_min[256];
+  __shared__ int s_cnt[256];
+  int mn = 0x7fffffff;
+  for (int q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+    const unsigned long long v = has_t ? qkey[q] : ~0ull;
+    if (v != ~0ull) {
+      const int d = (int)(v >> 32);
+      cc_train[q] = (int)(v & 0xffffffffu);
+      cc_dist[q] = d;
+      mn = min(mn, d);
+    } else {
+      cc_train[q] = -1;
+      cc_dist[q] = 0;
+    }
+  }
+  s_min[threadIdx.x] = mn;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) s_min[threadIdx.x] = min(s_min[threadIdx.x], s_min[threadIdx.x + s]);
+    __syncthreads();
+  }
+  const int minDist = s_min[0];
+  const int thr = max(2 * minDist, 30);  // d > max(2*minDist, 30.0) rejects (exact in integers)
+  int cnt = 0;
+  for (int q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
+    const unsigned long long v = has_t ? qkey[q] : ~0ull;
+    int m = -1;
+    if (v != ~0ull && (int)(v >> 32) <= thr) { m = (int)(v & 0xffffffffu); cnt++; }
+    match_train[q] = m;
+  }
+  s_cnt[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) s_cnt[threadIdx.x] += s_cnt[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) n_matches[p] = s_cnt[0];
+}
+
+// Host: tile table for "lanes = L side, uniform = U side" with a fixed number of U chunks.
+int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_off,
+                std::vector<BfTile>& tiles, int* n_chunks_out) {
+  const int64_t nl_total = l_off[np] - l_off[0];
+  int64_t max_u = 0, lane_tiles = 0;
+  for (int p = 0; p < np; p++) {
+    const int64_t nl = l_off[p + 1] - l_off[p], nu = u_off[p + 1] - u_off[p];
+    if (nl < 0 || nu < 0) return lorb::set_error(ctx, LORB_E_INVALID, "offsets not monotone at problem %d", p);
+    if (nu > (int64_t)kIdxMask) return lorb::set_error(ctx, LORB_E_INVALID, "problem %d: %lld uniform items > 2^23-1", p, (long long)nu);
+    if (nu > 0) lane_tiles += (nl + 255) / 256;
+    max_u = std::max<int64_t>(max_u, nu);
+  }
+  // enough workgroups to fill 256 CUs x ~8, but keep >= 128 uniform items per chunk
+  int n_chunks = 1;
+  if (lane_tiles > 0) {
+    const int64_t want = (2048 + lane_tiles - 1) / lane_tiles;
+    const int64_t cap = std::max<int64_t>(1, max_u / 128);
+    n_chunks = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::min<int64_t>(cap, 64)));
+  }
+  tiles.clear();
+  for (int p = 0; p < np; p++) {
+    const int l0 = l_off[p] - l_off[0], nl = l_off[p + 1] - l_off[p];
+    const int u0 = u_off[p] - u_off[0], nu = u_off[p + 1] - u_off[p];
+    if (nu == 0 || nl == 0) continue;
+    for (int c = 0; c < n_chunks; c++) {
+      const int a = (int)((int64_t)nu * c / n_chunks), b = (int)((int64_t)nu * (c + 1) / n_chunks);
+      for (int t = 0; t < nl; t += 256) {
+        BfTile tl;
+        tl.lane_base = l0 + t;
+        tl.lane_count = std::min(256, nl - t);
+        tl.uni_base = u0 + a;
+        tl.uni_count = b - a;
+        tl.uni_local0 = a;
+        tl.out_base = (int)((int64_t)c * nl_total + l0 + t);
+        tiles.push_back(tl);
+      }
+    }
+  }
+  *n_chunks_out = n_chunks;
+  return LORB_OK;
+}
+
+// scan + merge; final keys land in k1/k2 (n_lanes entries)
+template <bool TOP2>
+int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, const uint8_t* d_uni,
+         const int32_t* u_off, uint32_t** k1_final, uint32_t** k2_final) {
+  std::vector<BfTile> tiles;
+  int n_chunks = 1;
+  LORB_TRY(build_tiles(ctx, np, l_off, u_off, tiles, &n_chunks));
+  const int nl = l_off[np] - l_off[0];
+  BfTile* d_tiles = nullptr;
+  uint32_t *k1 = nullptr, *k2 = nullptr, *m1 = nullptr, *m2 = nullptr;
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_K1, (size_t)nl * n_chunks, &k1));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_K2, (size_t)nl * (TOP2 ? n_chunks : 1), &k2));
+  if (!tiles.empty()) {
+    LORB_TRY(lorb::upload_t(ctx, S_BF_TILES, tiles.data(), tiles.size(), &d_tiles));
+    lorb::KernelTimer kt(ctx, TOP2 ? LORB_K_BF_SCAN_TOP2 : LORB_K_BF_SCAN_TOP1);
+    hipLaunchKernelGGL(k_bf_scan<TOP2>, dim3((unsigned)tiles.size()), dim3(256), 0, ctx->stream,
+                       reinterpret_cast<const uint4*>(d_lane), reinterpret_cast<const uint4*>(d_uni),
+                       d_tiles, k1, k2);
+    LORB_CHECK_LAUNCH(ctx);
+  }
+  if (n_chunks > 1 && nl > 0) {
+    LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT4, (size_t)nl, &m1));
+    LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT5, (size_t)nl, &m2));
+    hipLaunchKernelGGL(k_bf_merge<TOP2>, dim3(lorb::ceil_div(nl, 256)), dim3(256), 0, ctx->stream,
+                       k1, k2, nl, n_chunks, m1, m2);
+    LORB_CHECK_LAUNCH(ctx);
+    *k1_final = m1;
+    *k2_final = m2;
+  } else {
+    *k1_final = k1;
+    *k2_final = k2;
+  }
+  return LORB_OK;
+}
+
+int check_offsets(lorb_ctx* ctx, int np, const int32_t* a, const int32_t* b) {
+  if (!ctx) return LORB_E_INVALID;
+  if (np < 0 || (np > 0 && (!a || !b))) return lorb::set_error(ctx, LORB_E_INVALID, "bad problem offsets");
+  if (np > 0 && (a[0] != 0 || b[0] != 0)) return lorb::set_error(ctx, LORB_E_INVALID, "offsets must start at 0");
+  return LORB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lorb_bf_top2_dev(lorb_ctx* ctx, int32_t np, const uint8_t* d_q, const int32_t* q_off,
+                     const uint8_t* d_t, const int32_t* t_off, const int32_t* d_t_level,
+                     int32_t* d_best_idx, int32_t* d_best_dist, int32_t* d_best_level,
+                     int32_t* d_second_dist, int32_t* d_second_level, uint8_t* d_accepted) {
+  LORB_TRY(check_offsets(ctx, np, q_off, t_off));
+  if (np == 0 || q_off[np] == 0) return LORB_OK;
+  uint32_t *k1 = nullptr, *k2 = nullptr;
+  LORB_TRY(scan<true>(ctx, np, d_q, q_off, d_t, t_off, &k1, &k2));
+  int32_t* d_off = nullptr;
+  std::vector<int32_t> offs(q_off, q_off + np + 1);
+  offs.insert(offs.end(), t_off, t_off + np + 1);
+  LORB_TRY(lorb::upload_t(ctx, S_BF_OFF, offs.data(), offs.size(), &d_off));
+  const int nq = q_off[np];
+  hipLaunchKernelGGL(k_top2_finalize, dim3(lorb::ceil_div(nq, 256)), dim3(256), 0, ctx->stream, k1,
+                     k2, nq, d_off, d_off + np + 1, np, d_t_level, d_best_idx, d_best_dist,
+                     d_best_level, d_second_dist, d_second_level, d_accepted);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
+int lorb_bf_top2(lorb_ctx* ctx, int32_t np, const uint8_t* q, const int32_t* q_off,
+                 const uint8_t* t, const int32_t* t_off, const int32_t* t_level,
+                 int32_t* best_idx, int32_t* best_dist, int32_t* best_level, int32_t* second_dist,
+                 int32_t* second_level, uint8_t* accepted) {
+  LORB_TRY(check_offsets(ctx, np, q_off, t_off));
+  if (np == 0) return LORB_OK;
+  const int nq = q_off[np], nt = t_off[np];
+  if (nq == 0) return LORB_OK;
+  uint8_t *dq = nullptr, *dt = nullptr;
+  int32_t *dl = nullptr, *o = nullptr;
+  uint8_t* dacc = nullptr;
+  LORB_TRY(lorb::upload_t(ctx, S_BF_Q, q, (size_t)nq * 32, &dq));
+  if (nt > 0) LORB_TRY(lorb::upload_t(ctx, S_BF_T, t, (size_t)nt * 32, &dt));
+  if (t_level && nt > 0) LORB_TRY(lorb::upload_t(ctx, S_BF_TL, t_level, (size_t)nt, &dl));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT0, (size_t)nq * 5, &o));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT1, (size_t)nq, &dacc));
+  LORB_TRY(lorb_bf_top2_dev(ctx, np, dq, q_off, dt, t_off, dl, o, o + nq, o + 2 * nq, o + 3 * nq,
+                            o + 4 * nq, dacc));
+  int32_t* outs[5] = {best_idx, best_dist, best_level, second_dist, second_level};
+  for (int k = 0; k < 5; k++)
+    LORB_HIP(ctx, hipMemcpyAsync(outs[k], o + (size_t)k * nq, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(accepted, dacc, nq, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_bf_match_dev(lorb_ctx* ctx, int32_t np, const uint8_t* d_q, const int32_t* q_off,
+                      const uint8_t* d_t, const int32_t* t_off, int32_t* d_cc_train,
+                      int32_t* d_cc_dist, int32_t* d_match_train, int32_t* d_n_matches) {
+  LORB_TRY(check_offsets(ctx, np, q_off, t_off));
+  if (np == 0) return LORB_OK;
+  const int nq = q_off[np], nt = t_off[np];
+  uint32_t *k1 = nullptr, *k2 = nullptr;
+  unsigned long long* qkey = nullptr;
+  int32_t* d_off = nullptr;
+  std::vector<int32_t> offs(q_off, q_off + np + 1);
+  offs.insert(offs.end(), t_off, t_off + np + 1);
+  LORB_TRY(lorb::upload_t(ctx, S_BF_OFF, offs.data(), offs.size(), &d_off));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_QKEY, (size_t)std::max(nq, 1), &qkey));
+  if (nq > 0) LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, ctx->stream));
+  if (nt > 0 && nq > 0) {
+    // reverse pass: lanes = trains, uniform = queries  -> nearest query per train
+    LORB_TRY(scan<false>(ctx, np, d_t, t_off, d_q, q_off, &k1, &k2));
+    hipLaunchKernelGGL(k_cc_scatter, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, k1,
+                       nt, d_off, d_off + np + 1, np, qkey);
+    LORB_CHECK_LAUNCH(ctx);
+  }
+  hipLaunchKernelGGL(k_cc_finalize, dim3(np), dim3(256), 0, ctx->stream, qkey, d_off,
+                     d_off + np + 1, d_cc_train, d_cc_dist, d_match_train, d_n_matches);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
+int lorb_bf_match(lorb_ctx* ctx, int32_t np, const uint8_t* q, const int32_t* q_off,
+                  const uint8_t* t, const int32_t* t_off, int32_t* cc_train, int32_t* cc_dist,
+                  int32_t* match_train, int32_t* n_matches) {
+  LORB_TRY(check_offsets(ctx, np, q_off, t_off));
+  if (np == 0) return LORB_OK;
+  const int nq = q_off[np], nt = t_off[np];
+  uint8_t *dq = nullptr, *dt = nullptr;
+  int32_t* o = nullptr;
+  if (nq > 0) LORB_TRY(lorb::upload_t(ctx, S_BF_Q, q, (size_t)nq * 32, &dq));
+  if (nt > 0) LORB_TRY(lorb::upload_t(ctx, S_BF_T, t, (size_t)nt * 32, &dt));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT0, (size_t)nq * 3 + np, &o));
+  LORB_TRY(lorb_bf_match_dev(ctx, np, dq, q_off, dt, t_off, o, o + nq, o + 2 * nq, o + 3 * nq));
+  if (nq > 0) {
+    LORB_HIP(ctx, hipMemcpyAsync(cc_train, o, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(cc_dist, o + nq, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(match_train, o + 2 * nq, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  LORB_HIP(ctx, hipMemcpyAsync(n_matches, o + 3 * nq, sizeof(int32_t) * np, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+}  // extern "C"

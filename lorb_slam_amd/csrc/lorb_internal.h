@@ -1,0 +1,92 @@
+// lorb_internal.h -- shared internals of liblorb.so (HIP runtime for gfx950 / MI355X).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/lorb_c.h"
+
+struct lorb_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  hipEvent_t ev[64] = {};
+  // grow-only device scratch buffers, one per slot
+  static constexpr int kScratch = 24;
+  void* scratch[kScratch] = {};
+  size_t scratch_sz[kScratch] = {};
+  // per-kernel event timing
+  bool ktime = false;
+  std::vector<hipEvent_t> kev_pool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> kev[LORB_K_COUNT];
+  // pinned host staging
+  void* pinned = nullptr;
+  size_t pinned_sz = 0;
+};
+
+namespace lorb {
+
+int set_error(lorb_ctx* ctx, int code, const char* fmt, ...);
+
+#define LORB_HIP(ctx, call)                                                              \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return ::lorb::set_error((ctx), LORB_E_DEVICE, "%s failed: %s (%s:%d)", #call,    \
+                               hipGetErrorString(e_), __FILE__, __LINE__);               \
+  } while (0)
+
+#define LORB_CHECK_LAUNCH(ctx) LORB_HIP(ctx, hipGetLastError())
+
+#define LORB_TRY(expr)          \
+  do {                          \
+    int rc_ = (expr);           \
+    if (rc_ != LORB_OK) return rc_; \
+  } while (0)
+
+// grow-only scratch: returns device pointer in *out
+int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out);
+template <typename T>
+int scratch_t(lorb_ctx* ctx, int slot, size_t count, T** out) {
+  void* p = nullptr;
+  int rc = scratch(ctx, slot, count * sizeof(T) + 16, &p);
+  *out = static_cast<T*>(p);
+  return rc;
+}
+
+// H2D into scratch slot (sync w.r.t. host buffer: uses hipMemcpyAsync + stream sync at end
+// of the calling API).
+int upload(lorb_ctx* ctx, int slot, const void* host, size_t bytes, void** dev);
+template <typename T>
+int upload_t(lorb_ctx* ctx, int slot, const T* host, size_t count, T** dev) {
+  void* p = nullptr;
+  if (host == nullptr || count == 0) { *dev = nullptr; return scratch(ctx, slot, 16, &p) == LORB_OK ? (*dev = nullptr, LORB_OK) : LORB_E_DEVICE; }
+  int rc = upload(ctx, slot, host, count * sizeof(T), &p);
+  *dev = static_cast<T*>(p);
+  return rc;
+}
+
+// brackets one kernel launch with events when ctx->ktime is set
+struct KernelTimer {
+  lorb_ctx* ctx; int k; hipEvent_t b = nullptr, e = nullptr;
+  KernelTimer(lorb_ctx* c, int kid);
+  ~KernelTimer();
+};
+
+inline unsigned ceil_div(size_t a, size_t b) { return static_cast<unsigned>((a + b - 1) / b); }
+
+}  // namespace lorb
+
+// scratch slot plan (per API family; calls on one ctx are serialized)
+enum {
+  S_BF_Q = 0, S_BF_T, S_BF_TL, S_BF_TILES, S_BF_K1, S_BF_K2, S_BF_QKEY, S_BF_OUT0, S_BF_OUT1,
+  S_BF_OUT2, S_BF_OUT3, S_BF_OUT4, S_BF_OUT5, S_BF_OFF,
+  S_W0 = 14, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7, S_W8, S_W9
+};

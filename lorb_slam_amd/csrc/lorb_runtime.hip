@@ -1,0 +1,204 @@
+// lorb_runtime.hip -- context, memory and timer entry points of the C-ABI (include/lorb_c.h).
+#include "lorb_internal.h"
+
+namespace lorb {
+
+int set_error(lorb_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return code;
+}
+
+int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out) {
+  if (slot < 0 || slot >= lorb_ctx::kScratch) return set_error(ctx, LORB_E_INVALID, "bad scratch slot %d", slot);
+  if (bytes == 0) bytes = 16;
+  if (ctx->scratch_sz[slot] < bytes) {
+    if (ctx->scratch[slot]) {
+      LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      LORB_HIP(ctx, hipFree(ctx->scratch[slot]));
+      ctx->scratch[slot] = nullptr;
+      ctx->scratch_sz[slot] = 0;
+    }
+    size_t want = bytes + bytes / 4;
+    LORB_HIP(ctx, hipMalloc(&ctx->scratch[slot], want));
+    ctx->scratch_sz[slot] = want;
+  }
+  *out = ctx->scratch[slot];
+  return LORB_OK;
+}
+
+int upload(lorb_ctx* ctx, int slot, const void* host, size_t bytes, void** dev) {
+  LORB_TRY(scratch(ctx, slot, bytes, dev));
+  if (bytes) LORB_HIP(ctx, hipMemcpyAsync(*dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return LORB_OK;
+}
+
+static hipEvent_t pool_get(lorb_ctx* ctx) {
+  if (!ctx->kev_pool.empty()) { hipEvent_t e = ctx->kev_pool.back(); ctx->kev_pool.pop_back(); return e; }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+KernelTimer::KernelTimer(lorb_ctx* c, int kid) : ctx(c), k(kid) {
+  if (!ctx->ktime || k < 0 || k >= LORB_K_COUNT) return;
+  b = pool_get(ctx); e = pool_get(ctx);
+  if (b) (void)hipEventRecord(b, ctx->stream);
+}
+KernelTimer::~KernelTimer() {
+  if (!b || !e) return;
+  (void)hipEventRecord(e, ctx->stream);
+  ctx->kev[k].emplace_back(b, e);
+}
+
+}  // namespace lorb
+
+using namespace lorb;
+
+extern "C" {
+
+int lorb_abi_version(void) { return LORB_ABI_VERSION; }
+
+int lorb_device_count(int* count) {
+  if (!count) return LORB_E_INVALID;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) { *count = 0; return LORB_E_DEVICE; }
+  *count = n;
+  return LORB_OK;
+}
+
+int lorb_create(int device, lorb_ctx** out) {
+  if (!out) return LORB_E_INVALID;
+  *out = nullptr;
+  lorb_ctx* ctx = new (std::nothrow) lorb_ctx();
+  if (!ctx) return LORB_E_NOMEM;
+  ctx->device = device;
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  for (int i = 0; i < 64 && e == hipSuccess; i++) e = hipEventCreate(&ctx->ev[i]);
+  if (e != hipSuccess) {
+    delete ctx;
+    return LORB_E_DEVICE;
+  }
+  *out = ctx;
+  return LORB_OK;
+}
+
+int lorb_destroy(lorb_ctx* ctx) {
+  if (!ctx) return LORB_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (int i = 0; i < lorb_ctx::kScratch; i++)
+    if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  for (int i = 0; i < 64; i++)
+    if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
+  for (int k = 0; k < LORB_K_COUNT; k++)
+    for (auto& pr : ctx->kev[k]) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+  for (auto e : ctx->kev_pool) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return LORB_OK;
+}
+
+const char* lorb_last_error(const lorb_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int lorb_sync(lorb_ctx* ctx) {
+  if (!ctx) return LORB_E_INVALID;
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_malloc(lorb_ctx* ctx, void** dptr, size_t bytes) {
+  if (!ctx || !dptr) return LORB_E_INVALID;
+  LORB_HIP(ctx, hipMalloc(dptr, bytes ? bytes : 16));
+  return LORB_OK;
+}
+
+int lorb_free(lorb_ctx* ctx, void* dptr) {
+  if (!ctx) return LORB_E_INVALID;
+  if (dptr) LORB_HIP(ctx, hipFree(dptr));
+  return LORB_OK;
+}
+
+int lorb_memcpy_h2d(lorb_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return LORB_E_INVALID;
+  if (!bytes) return LORB_OK;
+  LORB_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_memcpy_d2h(lorb_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return LORB_E_INVALID;
+  if (!bytes) return LORB_OK;
+  LORB_HIP(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_memset_dev(lorb_ctx* ctx, void* dst, int value, size_t bytes) {
+  if (!ctx) return LORB_E_INVALID;
+  if (!bytes) return LORB_OK;
+  LORB_HIP(ctx, hipMemsetAsync(dst, value, bytes, ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_timer_mark(lorb_ctx* ctx, int slot) {
+  if (!ctx || slot < 0 || slot >= 64) return LORB_E_INVALID;
+  LORB_HIP(ctx, hipEventRecord(ctx->ev[slot], ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_timer_elapsed_ms(lorb_ctx* ctx, int a, int b, float* ms) {
+  if (!ctx || !ms || a < 0 || a >= 64 || b < 0 || b >= 64) return LORB_E_INVALID;
+  LORB_HIP(ctx, hipEventSynchronize(ctx->ev[b]));
+  LORB_HIP(ctx, hipEventElapsedTime(ms, ctx->ev[a], ctx->ev[b]));
+  return LORB_OK;
+}
+
+int lorb_kernel_timing_enable(lorb_ctx* ctx, int enable) {
+  if (!ctx) return LORB_E_INVALID;
+  ctx->ktime = enable != 0;
+  return LORB_OK;
+}
+
+int lorb_kernel_timing_read(lorb_ctx* ctx, int k, double* total_ms, int* launches) {
+  if (!ctx || k < 0 || k >= LORB_K_COUNT || !total_ms || !launches) return LORB_E_INVALID;
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  double tot = 0.0;
+  for (auto& pr : ctx->kev[k]) {
+    float ms = 0.f;
+    LORB_HIP(ctx, hipEventElapsedTime(&ms, pr.first, pr.second));
+    tot += ms;
+    ctx->kev_pool.push_back(pr.first);
+    ctx->kev_pool.push_back(pr.second);
+  }
+  *launches = (int)ctx->kev[k].size();
+  ctx->kev[k].clear();
+  *total_ms = tot;
+  return LORB_OK;
+}
+
+void lorb_lm_options_default(lorb_lm_options* o) {
+  if (!o) return;
+  o->max_num_iterations = 50;
+  o->function_tolerance = 1e-6;
+  o->gradient_tolerance = 1e-10;
+  o->parameter_tolerance = 1e-8;
+  o->initial_trust_region_radius = 1e4;
+  o->max_trust_region_radius = 1e16;
+  o->min_trust_region_radius = 1e-32;
+  o->min_relative_decrease = 1e-3;
+  o->min_lm_diagonal = 1e-6;
+  o->max_lm_diagonal = 1e32;
+  o->max_num_consecutive_invalid_steps = 5;
+  o->jacobi_scaling = 1;
+}
+
+}  // extern "C"

@@ -1,0 +1,164 @@
+"""Loader + thin ctypes bindings of liblorb.so (include/lorb_c.h).
+
+The product path is the HIP library.  There is no CPU fallback: if liblorb.so is missing
+or no MI355X is visible, every call raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblorb.so")
+_lib = None
+
+
+class LorbError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load the in-tree liblorb.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LorbError(f"{LIB_PATH} not built: run `make -C lorb_slam_amd/csrc` (hipcc, gfx950)")
+        L = C.CDLL(LIB_PATH)
+        L.lorb_last_error.restype = C.c_char_p
+        L.lorb_last_error.argtypes = [C.c_void_p]
+        for name in ("lorb_create", "lorb_destroy", "lorb_sync", "lorb_malloc", "lorb_free",
+                     "lorb_memcpy_h2d", "lorb_memcpy_d2h", "lorb_memset_dev", "lorb_timer_mark",
+                     "lorb_timer_elapsed_ms", "lorb_device_count", "lorb_abi_version"):
+            getattr(L, name).restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def device_count():
+    n = C.c_int(0)
+    rc = lib().lorb_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+class Context:
+    """One lorb_ctx (one HIP stream) on one device.  Not thread-safe (one per thread)."""
+
+    def __init__(self, device=0):
+        self._p = C.c_void_p()
+        rc = lib().lorb_create(C.c_int(device), C.byref(self._p))
+        if rc != 0:
+            raise LorbError(f"lorb_create(device={device}) failed rc={rc}: no usable HIP device")
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._p
+
+    def check(self, rc, what):
+        if rc != 0:
+            msg = lib().lorb_last_error(self._p)
+            raise LorbError(f"{what} failed rc={rc}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if self._p:
+            lib().lorb_destroy(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        self.check(lib().lorb_sync(self._p), "lorb_sync")
+
+    # device memory -----------------------------------------------------------------------
+    def malloc(self, nbytes):
+        p = C.c_void_p()
+        self.check(lib().lorb_malloc(self._p, C.byref(p), C.c_size_t(nbytes)), "lorb_malloc")
+        return p
+
+    def free(self, p):
+        self.check(lib().lorb_free(self._p, p), "lorb_free")
+
+    def to_device(self, arr):
+        arr = np.ascontiguousarray(arr)
+        p = self.malloc(max(arr.nbytes, 16))
+        self.check(lib().lorb_memcpy_h2d(self._p, p, arr.ctypes.data_as(C.c_void_p), C.c_size_t(arr.nbytes)), "h2d")
+        return DeviceArray(self, p, arr.shape, arr.dtype)
+
+    def empty(self, shape, dtype):
+        dt = np.dtype(dtype)
+        n = int(np.prod(shape)) * dt.itemsize
+        return DeviceArray(self, self.malloc(max(n, 16)), tuple(np.atleast_1d(shape)) if np.ndim(shape) else (int(shape),), dt)
+
+    def timer_mark(self, slot):
+        self.check(lib().lorb_timer_mark(self._p, C.c_int(slot)), "timer_mark")
+
+    def timer_ms(self, a, b):
+        ms = C.c_float(0)
+        self.check(lib().lorb_timer_elapsed_ms(self._p, C.c_int(a), C.c_int(b), C.byref(ms)), "timer")
+        return ms.value
+
+    # matcher -------------------------------------------------------------------------------
+    def bf_top2(self, q_list, t_list, t_level_list=None):
+        """Batched a5-with-unbounded-window: lists of (Nq_i x 32) / (Nt_i x 32) uint8 arrays."""
+        q = np.ascontiguousarray(np.concatenate(q_list) if len(q_list) else np.zeros((0, 32), np.uint8), np.uint8)
+        t = np.ascontiguousarray(np.concatenate(t_list) if len(t_list) else np.zeros((0, 32), np.uint8), np.uint8)
+        q_off = np.concatenate([[0], np.cumsum([len(a) for a in q_list])]).astype(np.int32)
+        t_off = np.concatenate([[0], np.cumsum([len(a) for a in t_list])]).astype(np.int32)
+        tl = None
+        if t_level_list is not None:
+            tl = np.ascontiguousarray(np.concatenate(t_level_list), np.int32)
+        nq = len(q)
+        out = {k: np.zeros(max(nq, 1), np.int32) for k in ("best_idx", "best_dist", "best_level", "second_dist", "second_level")}
+        acc = np.zeros(max(nq, 1), np.uint8)
+        self.check(lib().lorb_bf_top2(
+            self._p, C.c_int32(len(q_list)), A.ptr(q, C.c_uint8), A.ptr(q_off, C.c_int32), A.ptr(t, C.c_uint8),
+            A.ptr(t_off, C.c_int32), A.ptr(tl, C.c_int32), A.ptr(out["best_idx"], C.c_int32),
+            A.ptr(out["best_dist"], C.c_int32), A.ptr(out["best_level"], C.c_int32),
+            A.ptr(out["second_dist"], C.c_int32), A.ptr(out["second_level"], C.c_int32),
+            A.ptr(acc, C.c_uint8)), "lorb_bf_top2")
+        out["accepted"] = acc
+        return {k: v[:nq] for k, v in out.items()}, q_off
+
+    def bf_match(self, q_list, t_list):
+        q = np.ascontiguousarray(np.concatenate(q_list) if len(q_list) else np.zeros((0, 32), np.uint8), np.uint8)
+        t = np.ascontiguousarray(np.concatenate(t_list) if len(t_list) else np.zeros((0, 32), np.uint8), np.uint8)
+        q_off = np.concatenate([[0], np.cumsum([len(a) for a in q_list])]).astype(np.int32)
+        t_off = np.concatenate([[0], np.cumsum([len(a) for a in t_list])]).astype(np.int32)
+        nq = len(q)
+        cc_t = np.zeros(max(nq, 1), np.int32); cc_d = np.zeros(max(nq, 1), np.int32); mt = np.zeros(max(nq, 1), np.int32)
+        nm = np.zeros(max(len(q_list), 1), np.int32)
+        self.check(lib().lorb_bf_match(
+            self._p, C.c_int32(len(q_list)), A.ptr(q, C.c_uint8), A.ptr(q_off, C.c_int32), A.ptr(t, C.c_uint8),
+            A.ptr(t_off, C.c_int32), A.ptr(cc_t, C.c_int32), A.ptr(cc_d, C.c_int32), A.ptr(mt, C.c_int32),
+            A.ptr(nm, C.c_int32)), "lorb_bf_match")
+        return dict(cc_train=cc_t[:nq], cc_dist=cc_d[:nq], match_train=mt[:nq], n_matches=nm[: len(q_list)]), q_off
+
+
+class DeviceArray:
+    def __init__(self, ctx, ptr_, shape, dtype):
+        self.ctx, self.ptr, self.shape, self.dtype = ctx, ptr_, tuple(shape), np.dtype(dtype)
+
+    @property
+    def nbytes(self):
+        return int(np.prod(self.shape)) * self.dtype.itemsize
+
+    def numpy(self):
+        out = np.empty(self.shape, self.dtype)
+        if self.nbytes:
+            self.ctx.check(lib().lorb_memcpy_d2h(self.ctx.handle, out.ctypes.data_as(C.c_void_p), self.ptr,
+                                                 C.c_size_t(self.nbytes)), "d2h")
+        return out
+
+    def free(self):
+        if self.ptr:
+            self.ctx.free(self.ptr)
+            self.ptr = None
+
+    def as_ptr(self, ctype):
+        return C.cast(self.ptr, C.POINTER(ctype))

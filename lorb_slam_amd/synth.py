@@ -1,0 +1,260 @@
+"""Seeded synthetic workloads for the LORB_SLAM hot path.
+
+No dataset ships with the reference and there is no network, so every benchmark
+and parity test runs on these generators.  Geometry follows the EuRoC-like intrinsics the
+reference reads from EuRoC.yaml (src/camera.cpp:38-42); ORB level statistics follow
+ORBextractor's per-level feature split (src/ORBextractor.cpp:412-485).
+"""
+import math
+
+import numpy as np
+
+W, H = 752, 480
+FX = FY = 435.2
+CX, CY = 367.5, 252.2
+BF = 47.9
+N_LEVELS = 8
+SCALE = 1.2
+
+
+def scale_factors(n_levels=N_LEVELS, scale=SCALE):
+    sf = [np.float32(1.0)]
+    for _ in range(1, n_levels):
+        sf.append(np.float32(sf[-1] * np.float32(scale)))  # ORBextractor: float recurrence
+    return np.array(sf, np.float32)
+
+
+def frame_params(fx=FX, fy=FY, cx=CX, cy=CY, bf=BF, width=W, height=H):
+    """Frame fields as ComputeImageBounds / the Frame ctor set them (src/frame.cpp:31-36, 67-85)."""
+    f32 = np.float32
+    min_x, max_x, min_y, max_y = f32(0), f32(width), f32(0), f32(height)
+    return dict(fx=f32(fx), fy=f32(fy), cx=f32(cx), cy=f32(cy), bf=f32(bf), b=f32(f32(bf) / f32(fx)),
+                min_x=min_x, max_x=max_x, min_y=min_y, max_y=max_y,
+                grid_w_inv=f32(f32(64) / (max_x - min_x)), grid_h_inv=f32(f32(48) / (max_y - min_y)),
+                n_levels=N_LEVELS, log_scale_factor=np.float32(math.log(np.float32(SCALE))),
+                scale_factors=scale_factors())
+
+
+def level_probs(n_levels=N_LEVELS, scale=SCALE):
+    f = 1.0 / scale
+    w = np.array([f ** l for l in range(n_levels)])
+    return w / w.sum()
+
+
+def random_desc(rng, n):
+    return rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+
+
+def flip_bits(rng, desc, max_flips):
+    """copy of desc with U{0..max_flips} random distinct bit flips per row"""
+    out = desc.copy()
+    n = len(desc)
+    nf = rng.integers(0, max_flips + 1, size=n)
+    for i in range(n):
+        if nf[i]:
+            bits = rng.choice(256, size=nf[i], replace=False)
+            for b in bits:
+                out[i, b >> 3] ^= np.uint8(1 << (b & 7))
+    return out
+
+
+def bf_problem(seed=2, nq=2000, nt=2000, n_planted=1000, max_flips=32, random_levels=False):
+    """BASELINE config 1: Nq=Nt=2000 random 256-bit descriptors, n_planted trains are bit-flipped
+    copies of random queries."""
+    rng = np.random.default_rng(seed)
+    q = random_desc(rng, nq)
+    t = random_desc(rng, nt)
+    src = rng.choice(nq, size=min(n_planted, nt), replace=False)
+    dst = rng.choice(nt, size=len(src), replace=False)
+    t[dst] = flip_bits(rng, q[src], max_flips)
+    lev = rng.choice(N_LEVELS, size=nt, p=level_probs()).astype(np.int32) if random_levels else np.zeros(nt, np.int32)
+    return q, t, lev
+
+
+def rodrigues(aa):
+    aa = np.asarray(aa, np.float64)
+    th = np.linalg.norm(aa)
+    if th < 1e-300:
+        return np.eye(3)
+    k = aa / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + math.sin(th) * K + (1 - math.cos(th)) * K @ K
+
+
+def Tcw_from(aa, t):
+    T = np.eye(4, dtype=np.float32)
+    T[:3, :3] = rodrigues(aa)
+    T[:3, 3] = t
+    return T
+
+
+# ------------------------------------------------------------------------------------------
+def ba_window(seed=3, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400, obs_lens=(7, 8),
+              noise_px=0.5, fx=FX, fy=FY, cx=CX, cy=CY, pert=(2e-3, 2e-2, 5e-2)):
+    """Local-BA window.  KF i: camera centre (0.1 i, 0, 0), yaw 0.01 i.
+    Each point is seen by a contiguous KF range of length obs_lens[p % len]; n_fixed extra
+    out-of-window KFs (MPCost, fixed pose) each observe ~fixed_obs_per_kf points to fix the gauge.
+    Returns the problem dict consumed by lorb_ba_local / or_ba_local plus ground truth."""
+    rng = np.random.default_rng(seed)
+
+    def pose_of(i):
+        aa = np.array([0.0, 0.01 * i, 0.0])
+        R = rodrigues(aa)
+        C = np.array([0.1 * i, 0.0, 0.0])
+        return aa, -R @ C
+
+    true_poses = np.array([np.concatenate(pose_of(i)) for i in range(n_kf)])
+    fixed = np.array([np.concatenate(pose_of(-1 - j)) for j in range(n_fixed)]).reshape(-1, 6)
+    pts = np.stack([rng.uniform(-6, 8, n_pts), rng.uniform(-3, 3, n_pts), rng.uniform(4, 20, n_pts)], 1)
+    obs_p, obs_f = [], []
+    for p in range(n_pts):
+        k = obs_lens[p % len(obs_lens)]
+        k = min(k, n_kf)
+        s = rng.integers(0, n_kf - k + 1)
+        for f in range(s, s + k):
+            obs_p.append(p); obs_f.append(f)
+    for j in range(n_fixed):
+        sel = rng.choice(n_pts, size=min(fixed_obs_per_kf, n_pts), replace=False)
+        for p in np.sort(sel):
+            obs_p.append(p); obs_f.append(-1 - j)
+    obs_p = np.array(obs_p, np.int32); obs_f = np.array(obs_f, np.int32)
+    allposes = np.concatenate([true_poses, fixed], 0)
+    fidx = np.where(obs_f >= 0, obs_f, n_kf + (-1 - obs_f))
+    uv = np.zeros((len(obs_p), 2))
+    Rs = [rodrigues(allposes[i, :3]) for i in range(len(allposes))]
+    for k in range(len(obs_p)):
+        pp = Rs[fidx[k]] @ pts[obs_p[k]] + allposes[fidx[k], 3:]
+        uv[k] = (fx * pp[0] / pp[2] + cx, fy * pp[1] / pp[2] + cy)
+    uv += rng.normal(0, noise_px, uv.shape)
+    pose_init = true_poses.copy()
+    pose_init[:, :3] += rng.normal(0, pert[0], (n_kf, 3))
+    pose_init[:, 3:] += rng.normal(0, pert[1], (n_kf, 3))
+    point_init = pts + rng.normal(0, pert[2], pts.shape)
+    return dict(pose_init=pose_init.astype(np.float32), fixed_pose=fixed.astype(np.float32),
+                point_init=point_init.astype(np.float32), obs_point=obs_p, obs_frame=obs_f,
+                obs_uv=uv.astype(np.float32), intr=(np.float32(fx), np.float32(fy), np.float32(cx), np.float32(cy)),
+                true_poses=true_poses, true_points=pts)
+
+
+def pose_only_batch(seed=1, n_frames=1, n_res=200, fx=FX, fy=FY, cx=CX, cy=CY, quirk=True, noise_px=0.5):
+    """BA::ProjectPoseOptimization problems: n_res matched map points per frame,
+    observation = reprojection + N(0, noise_px).  quirk=True passes fy_eff = fx (PoseCost uses fx
+    for v, src/bundle_adjust.cpp:51) to the solver, as the reference does."""
+    rng = np.random.default_rng(seed)
+    res_off = [0]
+    intr, pose_init, pts3d, obs2d = [], [], [], []
+    for f in range(n_frames):
+        aa = np.array([0.01, -0.005, 0.002]) + rng.normal(0, 0.01, 3)
+        t = np.array([0.05, 0.0, 0.02]) + rng.normal(0, 0.05, 3)
+        R = rodrigues(aa)
+        X = np.stack([rng.uniform(-4, 4, n_res), rng.uniform(-2.5, 2.5, n_res), rng.uniform(2, 10, n_res)], 1)
+        Xc = X @ R.T + t
+        fyv = fx if quirk else fy
+        uv = np.stack([fx * Xc[:, 0] / Xc[:, 2] + cx, fyv * Xc[:, 1] / Xc[:, 2] + cy], 1)
+        uv += rng.normal(0, noise_px, uv.shape)
+        pi = np.concatenate([aa + rng.normal(0, 5e-3, 3), t + rng.normal(0, 3e-2, 3)])
+        intr.append([fx, fyv, cx, cy]); pose_init.append(pi); pts3d.append(X); obs2d.append(uv)
+        res_off.append(res_off[-1] + n_res)
+    return dict(res_off=np.array(res_off, np.int32), intr=np.array(intr, np.float32),
+                pose_init=np.array(pose_init, np.float32), pts3d=np.concatenate(pts3d).astype(np.float32),
+                obs2d=np.concatenate(obs2d).astype(np.float32))
+
+
+# ------------------------------------------------------------------------------------------
+def _project(T, X, fp):
+    Xc = (T[:3, :3].astype(np.float64) @ X.T).T + T[:3, 3]
+    u = fp["fx"] * Xc[:, 0] / Xc[:, 2] + fp["cx"]
+    v = fp["fy"] * Xc[:, 1] / Xc[:, 2] + fp["cy"]
+    return np.stack([u, v], 1), Xc[:, 2]
+
+
+def two_frames(seed=1, n_kps=500, n_shared=200, locked_frac=0.5, with_stereo=True, prefilled=0):
+    """frame A (last) and B (current), n_kps each, n_shared map points of A are
+    re-observed in B (reprojection + N(0,0.5px), descriptor with U{0..12} bit flips).
+    Returns inputs for Matcher::SearchByProjection(curr, last, th) (a4) and the BF match (a2)."""
+    rng = np.random.default_rng(seed)
+    fp = frame_params()
+    TA = Tcw_from([0, 0, 0], [0, 0, 0])
+    TB = Tcw_from([0.01, -0.005, 0.002], [0.05, 0.0, 0.02])
+    probs = level_probs()
+    # last frame
+    descA = random_desc(rng, n_kps)
+    octA = rng.choice(N_LEVELS, size=n_kps, p=probs).astype(np.int32)
+    angA = rng.uniform(0, 360, n_kps).astype(np.float32)
+    has_mp = np.zeros(n_kps, np.uint8)
+    mp_idx = rng.choice(n_kps, size=n_shared, replace=False)
+    has_mp[mp_idx] = 1
+    # extra map points in A that are NOT observed in B (plenty of non-matches)
+    extra = rng.choice(np.setdiff1d(np.arange(n_kps), mp_idx), size=min(n_kps - n_shared, n_shared // 2), replace=False)
+    has_mp[extra] = 1
+    Xw = np.stack([rng.uniform(-5, 5, n_kps), rng.uniform(-3, 3, n_kps), rng.uniform(2, 10, n_kps)], 1).astype(np.float32)
+    mp_locked = (rng.uniform(size=n_kps) < locked_frac).astype(np.uint8)
+    outlier = (rng.uniform(size=n_kps) < 0.02).astype(np.uint8)
+    # current frame
+    uvB, zB = _project(TB, Xw[mp_idx].astype(np.float64), fp)
+    uvB += rng.normal(0, 0.5, uvB.shape)
+    xB = rng.uniform(0, W, n_kps).astype(np.float32)
+    yB = rng.uniform(0, H, n_kps).astype(np.float32)
+    descB = random_desc(rng, n_kps)
+    octB = rng.choice(N_LEVELS, size=n_kps, p=probs).astype(np.int32)
+    angB = rng.uniform(0, 360, n_kps).astype(np.float32)
+    slots = rng.choice(n_kps, size=n_shared, replace=False)
+    xB[slots] = np.clip(uvB[:, 0], 0, W - 1e-3); yB[slots] = np.clip(uvB[:, 1], 0, H - 1e-3)
+    descB[slots] = flip_bits(rng, descA[mp_idx], 12)
+    octB[slots] = np.clip(octA[mp_idx] + rng.integers(-1, 2, n_shared), 0, N_LEVELS - 1)
+    angB[slots] = np.mod(angA[mp_idx] - rng.normal(5.0, 3.0, n_shared), 360).astype(np.float32)
+    uR = np.full(n_kps, -1.0, np.float32)
+    if with_stereo:
+        has_st = rng.uniform(size=n_kps) < 0.6
+        depth = rng.uniform(2, 10, n_kps).astype(np.float32)
+        depth[slots] = zB.astype(np.float32)
+        uR[has_st] = (xB[has_st] - fp["bf"] / depth[has_st]).astype(np.float32)
+    slot_state = np.zeros(n_kps, np.uint8)
+    if prefilled:
+        pf = rng.choice(n_kps, size=prefilled, replace=False)
+        slot_state[pf] = rng.integers(1, 3, size=prefilled).astype(np.uint8)
+    cur_kps = dict(x=xB, y=yB, octave=octB, angle=angB, u_right=uR, desc=descB)
+    last = dict(Tcw=TA, has_mp=has_mp, outlier=outlier, mp_locked=mp_locked, mp_pos=Xw,
+                mp_desc=descA, octave=octA, angle=angA)
+    return dict(fp=fp, cur_Tcw=TB, cur_kps=cur_kps, slot_state=slot_state, last=last)
+
+
+def local_points_problem(seed=5, n_kps=2000, n_pts=3000, n_true=1500, locked_frac=0.8, slot_prefill=100):
+    """Inputs of Matcher::SearchByProjection(F, set<MapPoint*>, th) (a5): a frame with n_kps
+    keypoints and n_pts local map points already projected by IsInFrustum (the tracking
+    fields), n_true of them re-observing a keypoint (bit-flipped descriptor)."""
+    rng = np.random.default_rng(seed)
+    fp = frame_params()
+    probs = level_probs()
+    x = rng.uniform(0, W, n_kps).astype(np.float32)
+    y = rng.uniform(0, H, n_kps).astype(np.float32)
+    octv = rng.choice(N_LEVELS, size=n_kps, p=probs).astype(np.int32)
+    ang = rng.uniform(0, 360, n_kps).astype(np.float32)
+    desc = random_desc(rng, n_kps)
+    uR = np.full(n_kps, -1.0, np.float32)
+    st = rng.uniform(size=n_kps) < 0.5
+    uR[st] = (x[st] - rng.uniform(3, 20, st.sum())).astype(np.float32)
+    pdesc = random_desc(rng, n_pts)
+    px = rng.uniform(0, W, n_pts).astype(np.float32)
+    py = rng.uniform(0, H, n_pts).astype(np.float32)
+    plev = rng.choice(N_LEVELS, size=n_pts, p=probs).astype(np.int32)
+    tk = rng.choice(n_kps, size=n_true, replace=False)
+    tp = rng.choice(n_pts, size=n_true, replace=False)
+    px[tp] = x[tk] + rng.normal(0, 1.0, n_true).astype(np.float32)
+    py[tp] = y[tk] + rng.normal(0, 1.0, n_true).astype(np.float32)
+    plev[tp] = np.clip(octv[tk] + rng.integers(0, 2, n_true), 0, N_LEVELS - 1)
+    pdesc[tp] = flip_bits(rng, desc[tk], 20)
+    pxr = (px - rng.uniform(3, 20, n_pts)).astype(np.float32)
+    pxr[tp] = np.where(uR[tk] > 0, uR[tk] + rng.normal(0, 1.0, n_true), pxr[tp]).astype(np.float32)
+    vc = rng.uniform(0.5, 1.0, n_pts).astype(np.float32)
+    vc[rng.uniform(size=n_pts) < 0.3] = np.float32(0.9995)
+    pts = dict(track_in_view=(rng.uniform(size=n_pts) < 0.95).astype(np.uint8),
+               is_bad=(rng.uniform(size=n_pts) < 0.01).astype(np.uint8),
+               locked=(rng.uniform(size=n_pts) < locked_frac).astype(np.uint8),
+               proj_x=px, proj_y=py, proj_xr=pxr, pred_level=plev, view_cos=vc, desc=pdesc)
+    slot_state = np.zeros(n_kps, np.uint8)
+    if slot_prefill:
+        pf = rng.choice(n_kps, size=slot_prefill, replace=False)
+        slot_state[pf] = rng.integers(1, 3, size=slot_prefill).astype(np.uint8)
+    kps = dict(x=x, y=y, octave=octv, angle=ang, u_right=uR, desc=desc)
+    return dict(fp=fp, kps=kps, slot_state=slot_state, pts=pts)

@@ -1,0 +1,193 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper of the CPU restatement (liblorb_oracle.so).
+
+Parity vs the real reference is UNPINNED (the reference needs OpenCV/Ceres and cannot be
+built here; it ships no golden vectors).  See oracle/lorb_oracle.h.  Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from lorb_slam_amd import _abi as A
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liblorb_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = C.CDLL(_LIB_PATH)
+        _lib.or_descriptor_distance.restype = C.c_int
+        _lib.or_radius_by_viewing_cos.restype = C.c_float
+        _lib.or_radius_by_viewing_cos.argtypes = [C.c_float]
+    return _lib
+
+
+def descriptor_distance(a, b):
+    a = A.u8(a); b = A.u8(b)
+    return lib().or_descriptor_distance(A.ptr(a, C.c_uint8), A.ptr(b, C.c_uint8))
+
+
+def radius_by_viewing_cos(c):
+    return lib().or_radius_by_viewing_cos(C.c_float(c))
+
+
+def compute_three_maxima(hist):
+    h = A.i32(hist)
+    i1, i2, i3 = C.c_int(-1), C.c_int(-1), C.c_int(-1)
+    lib().or_compute_three_maxima(A.ptr(h, C.c_int32), C.c_int(len(h)), C.byref(i1), C.byref(i2), C.byref(i3))
+    return i1.value, i2.value, i3.value
+
+
+def bf_match(q, t):
+    q = A.u8(q).reshape(-1, 32); t = A.u8(t).reshape(-1, 32)
+    nq = len(q)
+    cc_t = np.empty(nq, np.int32); cc_d = np.empty(nq, np.int32); mt = np.empty(nq, np.int32)
+    n = lib().or_bf_match(A.ptr(q, C.c_uint8), C.c_int(nq), A.ptr(t, C.c_uint8), C.c_int(len(t)),
+                          A.ptr(cc_t, C.c_int32), A.ptr(cc_d, C.c_int32), A.ptr(mt, C.c_int32))
+    return {"cc_train": cc_t, "cc_dist": cc_d, "match_train": mt, "n_matches": n}
+
+
+def bf_top2(q, t, t_level=None, threads=1):
+    q = A.u8(q).reshape(-1, 32); t = A.u8(t).reshape(-1, 32)
+    nq = len(q)
+    out = {k: np.empty(nq, np.int32) for k in ("best_idx", "best_dist", "best_level", "second_dist", "second_level")}
+    acc = np.empty(nq, np.uint8)
+    tl = A.i32(t_level) if t_level is not None else None
+    args = [A.ptr(q, C.c_uint8), C.c_int(nq), A.ptr(t, C.c_uint8), C.c_int(len(t)), A.ptr(tl, C.c_int32),
+            A.ptr(out["best_idx"], C.c_int32), A.ptr(out["best_dist"], C.c_int32), A.ptr(out["best_level"], C.c_int32),
+            A.ptr(out["second_dist"], C.c_int32), A.ptr(out["second_level"], C.c_int32), A.ptr(acc, C.c_uint8)]
+    if threads > 1:
+        lib().or_bf_top2_mt(*args, C.c_int(threads))
+    else:
+        lib().or_bf_top2(*args)
+    out["accepted"] = acc
+    return out
+
+
+def features_in_area(fp, kps, x, y, r, min_level=-1, max_level=-1):
+    keep = A.KeepAlive()
+    fps = A.make_frame_params(fp)
+    k = A.make_keypoints(kps, keep)
+
+    class Grid(C.Structure):
+        _fields_ = [("cell_off", C.c_int32 * (A.LORB_GRID_COLS * A.LORB_GRID_ROWS + 1)), ("idx", A.i32p)]
+
+    g = Grid()
+    L = lib()
+    L.or_grid_build(C.byref(fps), C.byref(k), C.byref(g))
+    out = np.empty(max(1, k.n), np.int32)
+    n = L.or_features_in_area(C.byref(fps), C.byref(k), C.byref(g), C.c_float(x), C.c_float(y), C.c_float(r),
+                              C.c_int(min_level), C.c_int(max_level), A.ptr(out, C.c_int32))
+    L.or_grid_free(C.byref(g))
+    return out[:n].copy()
+
+
+def search_by_projection_frame(fp, cur_Tcw, cur_kps, cur_slot_state, last, th):
+    keep = A.KeepAlive()
+    fps = A.make_frame_params(fp)
+    k = A.make_keypoints(cur_kps, keep)
+    lf = A.make_last_frame(last, keep)
+    T = keep.keep(A.f32(cur_Tcw).reshape(16))
+    ss = keep.keep(A.u8(cur_slot_state)) if cur_slot_state is not None else None
+    assign = np.empty(max(1, k.n), np.int32)
+    nm = C.c_int32(0)
+    lib().or_search_by_projection_frame(C.byref(fps), A.ptr(T, C.c_float), C.byref(k), A.ptr(ss, C.c_uint8),
+                                        C.byref(lf), C.c_float(th), A.ptr(assign, C.c_int32), C.byref(nm))
+    return assign[: k.n].copy(), nm.value
+
+
+def search_by_projection_local(fp, kps, slot_state, pts, th):
+    keep = A.KeepAlive()
+    fps = A.make_frame_params(fp)
+    k = A.make_keypoints(kps, keep)
+    lp = A.make_local_points(pts, keep)
+    ss = keep.keep(A.u8(slot_state)) if slot_state is not None else None
+    assign = np.empty(max(1, k.n), np.int32)
+    nm = C.c_int32(0)
+    lib().or_search_by_projection_local(C.byref(fps), C.byref(k), A.ptr(ss, C.c_uint8), C.byref(lp), C.c_float(th),
+                                        A.ptr(assign, C.c_int32), C.byref(nm))
+    return assign[: k.n].copy(), nm.value
+
+
+def is_in_frustum(fp, Tcw, fpts, cos_limit=0.5):
+    keep = A.KeepAlive()
+    fps = A.make_frame_params(fp)
+    p = A.make_frustum_points(fpts, keep)
+    T = keep.keep(A.f32(Tcw).reshape(16))
+    n = p.n
+    out = dict(in_view=np.zeros(n, np.uint8), proj_x=np.zeros(n, np.float32), proj_y=np.zeros(n, np.float32),
+               proj_xr=np.zeros(n, np.float32), pred_level=np.zeros(n, np.int32), view_cos=np.zeros(n, np.float32))
+    lib().or_is_in_frustum(C.byref(fps), A.ptr(T, C.c_float), C.byref(p), C.c_float(cos_limit),
+                           A.ptr(out["in_view"], C.c_uint8), A.ptr(out["proj_x"], C.c_float),
+                           A.ptr(out["proj_y"], C.c_float), A.ptr(out["proj_xr"], C.c_float),
+                           A.ptr(out["pred_level"], C.c_int32), A.ptr(out["view_cos"], C.c_float))
+    return out
+
+
+def unproject_stereo(fp, Tcw, x, y, depth):
+    fps = A.make_frame_params(fp)
+    T = A.f32(Tcw).reshape(16)
+    x = A.f32(x); y = A.f32(y); d = A.f32(depth)
+    out = np.zeros((len(x), 3), np.float32)
+    lib().or_unproject_stereo(C.byref(fps), A.ptr(T, C.c_float), C.c_int(len(x)), A.ptr(x, C.c_float),
+                              A.ptr(y, C.c_float), A.ptr(d, C.c_float), A.ptr(out, C.c_float))
+    return out
+
+
+def inv4_f32(M):
+    M = A.f32(M).reshape(16)
+    out = np.zeros(16, np.float32)
+    ok = lib().or_inv4_f32(A.ptr(M, C.c_float), A.ptr(out, C.c_float))
+    return out.reshape(4, 4), ok
+
+
+def pose_to_Tcw(rvec, tvec):
+    r = A.f32(rvec); t = A.f32(tvec)
+    out = np.zeros(16, np.float32)
+    lib().or_pose_to_Tcw(A.ptr(r, C.c_float), A.ptr(t, C.c_float), A.ptr(out, C.c_float))
+    return out.reshape(4, 4)
+
+
+def residual_jet(kind, X, pose, fx, fy, cx, cy, u, v):
+    X = np.ascontiguousarray(X, np.float64); pose = np.ascontiguousarray(pose, np.float64)
+    res = np.zeros(2); np_ = {0: 6, 1: 3, 2: 9}[kind]
+    jac = np.zeros(2 * np_)
+    lib().or_residual_jet(C.c_int(kind), A.ptr(X, C.c_double), A.ptr(pose, C.c_double), C.c_double(fx),
+                          C.c_double(fy), C.c_double(cx), C.c_double(cy), C.c_double(u), C.c_double(v),
+                          A.ptr(res, C.c_double), A.ptr(jac, C.c_double))
+    return res, jac.reshape(2, np_)
+
+
+def ba_pose_only(pb, opt=None):
+    keep = A.KeepAlive()
+    s = A.make_pose_batch(pb, keep)
+    opt = opt or A.LMOptions.default()
+    nf = s.n_frames
+    pose = np.zeros((nf, 6)); T = np.zeros((nf, 4, 4), np.float32)
+    summ = (A.BASummary * max(1, nf))()
+    lib().or_ba_pose_only(C.byref(s), C.byref(opt), A.ptr(pose, C.c_double), A.ptr(T, C.c_float), summ)
+    return pose, T, [summ[i].as_dict() for i in range(nf)]
+
+
+def ba_local(wins, opt=None):
+    keep = A.KeepAlive()
+    arr = A.make_windows(wins, keep)
+    opt = opt or A.LMOptions.default()
+    poses = [np.zeros((len(w["pose_init"]), 6)) for w in wins]
+    pts = [np.zeros((len(w["point_init"]), 3)) for w in wins]
+    pp = (A.f64p * max(1, len(wins)))(*[A.ptr(p, C.c_double) for p in poses])
+    qp = (A.f64p * max(1, len(wins)))(*[A.ptr(p, C.c_double) for p in pts])
+    summ = (A.BASummary * max(1, len(wins)))()
+    lib().or_ba_local(C.c_int(len(wins)), arr, C.byref(opt), pp, qp, summ)
+    return poses, pts, [summ[i].as_dict() for i in range(len(wins))]
