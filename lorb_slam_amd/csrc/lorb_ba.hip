@@ -1,0 +1,1254 @@
+// lorb_ba.hip -- reprojection-error bundle adjustment on gfx950 (MI355X), FP64.
+//
+// Restates BA::ProjectPoseOptimization (src/bundle_adjust.cpp:158-202) and
+// BA::LocalPoseOptimization (src/bundle_adjust.cpp:207-330): ceres::Solve with the default
+// trust-region Levenberg-Marquardt options + DENSE_SCHUR.
+//
+// MI355X-first structure (device-resident LM, batched over independent windows):
+//   * every LM scalar decision (accept/reject, radius, tolerances) is made ON THE DEVICE by a
+//     one-workgroup-per-window kernel, so an LM iteration is a fixed sequence of launches with
+//     no host round trip; it is captured once into a hipGraph and replayed.
+//   * per-observation linearisation, per-point Schur elimination (3x3 inverse, W / Y tiles),
+//     one wavefront per non-zero (camera, camera) block of S accumulating a CSR pair list in a
+//     fixed order (deterministic, no FP64 atomics), an envelope (profile) Cholesky of S per
+//     window in LDS, and per-point back-substitution.
+//   * all reductions are fixed-order trees (block partials reduced in index order).
+#include "lorb_ba_math.h"
+#include "lorb_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+
+namespace {
+
+using lorb::residual;
+using lorb::residual_jac;
+
+constexpr int kPB = 256;  // points per point-block (one thread per point)
+
+struct BaWin {
+  int pose_base, n_poses, point_base, n_points;
+  int pblk_base, n_pblk;
+  int env_base, env_size, n, row_base;
+  int obs_base, n_obs;
+  double fx, fy, cx, cy;
+};
+struct PBlk { int win, p0, cnt; };
+struct BlockPair { int win, ch, cl, off, cnt; };  // global camera indices, pair list range
+struct WinState {
+  double radius, decrease_factor, cost, x_norm, gmax, initial_cost;
+  int iter, n_success, n_invalid, done, relin, cur, last_successful, term, chol_fail, pad;
+};
+struct LMOpt {
+  int max_iter, max_invalid, jacobi;
+  double ftol, gtol, ptol, init_radius, max_radius, min_radius, min_rel, min_diag, max_diag;
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void block_sum(double (&v)[N], double* sh /* [N*256] */) {
+  // deterministic fixed tree over a 256-thread block
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < N; ++k) sh[k * 256 + t] = v[k];
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (t < s) {
+#pragma unroll
+      for (int k = 0; k < N; ++k) sh[k * 256 + t] += sh[k * 256 + t + s];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = sh[k * 256];
+  __syncthreads();
+}
+
+// sym 3x3 packed (xx,xy,xz,yy,yz,zz) inverse via Cholesky; returns false if not PD
+__device__ __forceinline__ bool inv3(const double a[6], double inv[6]) {
+  const double l00 = a[0];
+  if (!(l00 > 0.0)) return false;
+  const double L00 = sqrt(l00);
+  const double L10 = a[1] / L00, L20 = a[2] / L00;
+  const double d1 = a[3] - L10 * L10;
+  if (!(d1 > 0.0)) return false;
+  const double L11 = sqrt(d1);
+  const double L21 = (a[4] - L20 * L10) / L11;
+  const double d2 = a[5] - L20 * L20 - L21 * L21;
+  if (!(d2 > 0.0)) return false;
+  const double L22 = sqrt(d2);
+  // inverse of L (lower)
+  const double i00 = 1.0 / L00, i11 = 1.0 / L11, i22 = 1.0 / L22;
+  const double i10 = -L10 * i00 * i11;
+  const double i21 = -L21 * i11 * i22;
+  const double i20 = -(L20 * i00 + L21 * i10) * i22;
+  // A^-1 = Li^T Li
+  inv[0] = i00 * i00 + i10 * i10 + i20 * i20;
+  inv[1] = i10 * i11 + i20 * i21;
+  inv[2] = i20 * i22;
+  inv[3] = i11 * i11 + i21 * i21;
+  inv[4] = i21 * i22;
+  inv[5] = i22 * i22;
+  return true;
+}
+__device__ __forceinline__ double s3(const double m[6], int a, int b) {
+  if (a > b) { const int t = a; a = b; b = t; }
+  return m[a * 3 - (a * (a - 1)) / 2 + (b - a)];  // packed (xx,xy,xz,yy,yz,zz)
+}
+
+// ------------------------------------------------------------------------------------------
+struct BaDev {
+  const BaWin* win;
+  const PBlk* pblk;
+  const BlockPair* bp;
+  const int2* pairs;
+  const int* pt_obs_off;     // Ptot+1
+  const int* obs_cam;        // K  (global optimised camera or -1)
+  const int* obs_fix;        // K  (global fixed pose or -1)
+  const double2* obs_uv;     // K
+  const int* cam_obs_off;    // Ctot+1
+  const int* cam_obs;        // camera-major obs list
+  const int* cam_win;        // Ctot
+  const int* row_first;      // per S row (window-local column index)
+  const int* row_off;        // per S row (offset in window env)
+  const int* col_last;       // per S column (window-local last row with first<=col)
+  const double* fixed_pose;  // NF*6
+  double* x_init_pose;       // Ctot*6 (initial values, never written)
+  double* x_init_pt;         // Ptot*3
+  double* x_pose[2];         // Ctot*6
+  double* x_pt[2];           // Ptot*3
+  double* scale_pose;        // Ctot*6
+  double* scale_pt;          // Ptot*3
+  double* ete;               // Ptot*6 (unscaled)
+  double* etb;               // Ptot*3 (unscaled)
+  double* pinv;              // Ptot*6
+  double* U;                 // Ctot*21 (unscaled, packed upper row-major)
+  double* V;                 // Ctot*6
+  double* cam_gmax;          // Ctot
+  double* obs_r;             // K*2
+  double* obs_Jp;            // K*6
+  double* obs_Jc;            // K*12
+  double* obs_W;             // K*18 (scaled)
+  double* obs_Y;             // K*18
+  double* obs_rc;            // K*6
+  double* env;               // S envelopes
+  double* rhs;               // sum n
+  double* ycam;              // sum n (solution, scaled space, y = -step)
+  double* part;              // n_pblk * 8 partials
+  WinState* st;
+};
+
+__device__ __forceinline__ int u21(int a, int b) {  // packed upper index of 6x6 sym
+  if (a > b) { const int t = a; a = b; b = t; }
+  return a * 6 - (a * (a - 1)) / 2 + (b - a);
+}
+
+// K0: state init
+__global__ void k_ba_init(BaDev d, int W, LMOpt o) {
+  const int w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= W) return;
+  WinState s;
+  s.radius = o.init_radius; s.decrease_factor = 2.0; s.cost = 0.0; s.x_norm = 0.0; s.gmax = 0.0;
+  s.initial_cost = 0.0; s.iter = 0; s.n_success = 0; s.n_invalid = 0;
+  s.done = d.win[w].n_obs == 0 ? 1 : 0;
+  s.relin = 1; s.cur = 0; s.last_successful = 1; s.term = 0; s.chol_fail = 0; s.pad = 0;
+  d.st[w] = s;
+}
+
+// K1: per-point linearisation (only windows that (re)linearise this iteration)
+__global__ __launch_bounds__(kPB) void k_ba_linearize(BaDev d) {
+  __shared__ double sh[3 * kPB];
+  const PBlk pb = d.pblk[blockIdx.x];
+  const WinState& S = d.st[pb.win];
+  if (S.done || !S.relin) return;
+  const BaWin& W = d.win[pb.win];
+  const int cur = S.cur;
+  const int t = threadIdx.x;
+  double cost = 0.0, gm = 0.0, xn2 = 0.0;
+  if (t < pb.cnt) {
+    const int p = pb.p0 + t;
+    double X[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) X[k] = d.x_pt[cur][3 * p + k];
+    double E[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+    const int o0 = d.pt_obs_off[p], o1 = d.pt_obs_off[p + 1];
+    for (int o = o0; o < o1; ++o) {
+      const int c = d.obs_cam[o];
+      double pose[6];
+      if (c >= 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) pose[k] = d.x_pose[cur][6 * c + k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[o] + k];
+      }
+      const double2 uv = d.obs_uv[o];
+      double r[2], Jp[6], Jc[12];
+      residual_jac(pose, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
+      d.obs_r[2 * o] = r[0]; d.obs_r[2 * o + 1] = r[1];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) d.obs_Jp[6 * o + k] = Jp[k];
+      if (c >= 0) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) d.obs_Jc[12 * o + k] = Jc[k];
+      }
+      E[0] += Jp[0] * Jp[0] + Jp[3] * Jp[3]; E[1] += Jp[0] * Jp[1] + Jp[3] * Jp[4];
+      E[2] += Jp[0] * Jp[2] + Jp[3] * Jp[5]; E[3] += Jp[1] * Jp[1] + Jp[4] * Jp[4];
+      E[4] += Jp[1] * Jp[2] + Jp[4] * Jp[5]; E[5] += Jp[2] * Jp[2] + Jp[5] * Jp[5];
+      b[0] += Jp[0] * r[0] + Jp[3] * r[1]; b[1] += Jp[1] * r[0] + Jp[4] * r[1];
+      b[2] += Jp[2] * r[0] + Jp[5] * r[1];
+      cost += 0.5 * (r[0] * r[0] + r[1] * r[1]);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d.ete[6 * p + k] = E[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d.etb[3 * p + k] = b[k];
+    if (S.iter == 0) {
+      d.scale_pt[3 * p] = 1.0 / (1.0 + sqrt(E[0]));
+      d.scale_pt[3 * p + 1] = 1.0 / (1.0 + sqrt(E[3]));
+      d.scale_pt[3 * p + 2] = 1.0 / (1.0 + sqrt(E[5]));
+    }
+    if (o1 > o0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        gm = fmax(gm, fabs(X[k] - (X[k] + -b[k])));
+        xn2 += X[k] * X[k];
+      }
+    }
+  }
+  double v[3] = {cost, gm, xn2};
+  // gm is reduced with max: do it separately
+  sh[t] = gm;
+  __syncthreads();
+  for (int s = kPB / 2; s > 0; s >>= 1) {
+    if (t < s) sh[t] = fmax(sh[t], sh[t + s]);
+    __syncthreads();
+  }
+  const double gmax = sh[0];
+  __syncthreads();
+  double sv[2] = {v[0], v[2]};
+  block_sum<2>(sv, sh);
+  if (t == 0) {
+    double* P = d.part + 8 * blockIdx.x;
+    P[0] = sv[0]; P[1] = gmax; P[2] = sv[1];
+  }
+}
+
+// K2: per-camera normal blocks (one wavefront per optimised camera)
+__global__ __launch_bounds__(64) void k_ba_camera(BaDev d) {
+  const int c = blockIdx.x;
+  const int w = d.cam_win[c];
+  const WinState& S = d.st[w];
+  if (S.done || !S.relin) return;
+  const int lane = threadIdx.x;
+  double U[21], V[6];
+#pragma unroll
+  for (int k = 0; k < 21; ++k) U[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) V[k] = 0.0;
+  const int a0 = d.cam_obs_off[c], a1 = d.cam_obs_off[c + 1];
+  for (int e = a0 + lane; e < a1; e += 64) {
+    const int o = d.cam_obs[e];
+    double J[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) J[k] = d.obs_Jc[12 * o + k];
+    const double r0 = d.obs_r[2 * o], r1 = d.obs_r[2 * o + 1];
+    int q = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      V[a] += J[a] * r0 + J[6 + a] * r1;
+#pragma unroll
+      for (int b = a; b < 6; ++b) U[q++] += J[a] * J[b] + J[6 + a] * J[6 + b];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 21; ++k) U[k] = wave_sum(U[k]);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) V[k] = wave_sum(V[k]);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 21; ++k) d.U[21 * c + k] = U[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d.V[6 * c + k] = V[k];
+    double gm = 0.0;
+    if (a1 > a0) {
+      const int cur = S.cur;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const double x = d.x_pose[cur][6 * c + k];
+        gm = fmax(gm, fabs(x - (x + -V[k])));
+      }
+    }
+    d.cam_gmax[c] = gm;
+    if (S.iter == 0) {
+      const int dg[6] = {0, 6, 11, 15, 18, 20};
+#pragma unroll
+      for (int k = 0; k < 6; ++k) d.scale_pose[6 * c + k] = 1.0 / (1.0 + sqrt(U[dg[k]]));
+    }
+  }
+}
+
+// K3: per-window iteration head: finalise the (re)linearisation, termination checks
+__global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
+  const int w = blockIdx.x;
+  WinState S = d.st[w];
+  if (S.done) return;
+  const BaWin W = d.win[w];
+  const int lane = threadIdx.x;
+  if (S.relin) {
+    double cost = 0.0, gm = 0.0, xn2 = 0.0;
+    if (lane == 0) {
+      for (int b = 0; b < W.n_pblk; ++b) {  // fixed order
+        const double* P = d.part + 8 * (W.pblk_base + b);
+        cost += P[0]; gm = fmax(gm, P[1]); xn2 += P[2];
+      }
+      const int cur = S.cur;
+      for (int c = W.pose_base; c < W.pose_base + W.n_poses; ++c) {
+        if (d.cam_obs_off[c + 1] == d.cam_obs_off[c]) continue;
+        gm = fmax(gm, d.cam_gmax[c]);
+        for (int k = 0; k < 6; ++k) { const double x = d.x_pose[cur][6 * c + k]; xn2 += x * x; }
+      }
+      S.cost = cost;
+      S.gmax = gm;
+      S.x_norm = sqrt(xn2);
+      if (S.iter == 0) S.initial_cost = cost;
+      S.last_successful = 1;
+      S.relin = 0;
+    }
+  }
+  if (lane == 0) {
+    if (S.iter >= o.max_iter) { S.done = 1; S.term = LORB_TERM_NO_CONVERGENCE; }
+    else if (S.last_successful && S.gmax <= o.gtol) { S.done = 1; S.term = LORB_TERM_GRADIENT_TOL; }
+    else if (S.radius <= o.min_radius) { S.done = 1; S.term = LORB_TERM_MIN_RADIUS; }
+    else { S.iter++; S.chol_fail = 0; }
+    d.st[w] = S;
+  }
+}
+
+// K4: per-point Schur prep: scaled E^T E + D^2 -> inverse, W_s, Y = W_s E^-1, rc = Y E^T b
+__global__ __launch_bounds__(kPB) void k_ba_point_prep(BaDev d, LMOpt o) {
+  const PBlk pb = d.pblk[blockIdx.x];
+  const WinState& S = d.st[pb.win];
+  if (S.done) return;
+  const int t = threadIdx.x;
+  if (t >= pb.cnt) return;
+  const int p = pb.p0 + t;
+  const double rad = S.radius;
+  double sp[3], E[6], b[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * p + k]; b[k] = d.etb[3 * p + k] * sp[k]; }
+  const double* Eu = d.ete + 6 * p;
+  E[0] = Eu[0] * sp[0] * sp[0]; E[1] = Eu[1] * sp[0] * sp[1]; E[2] = Eu[2] * sp[0] * sp[2];
+  E[3] = Eu[3] * sp[1] * sp[1]; E[4] = Eu[4] * sp[1] * sp[2]; E[5] = Eu[5] * sp[2] * sp[2];
+  E[0] += fmin(fmax(E[0], o.min_diag), o.max_diag) / rad;
+  E[3] += fmin(fmax(E[3], o.min_diag), o.max_diag) / rad;
+  E[5] += fmin(fmax(E[5], o.min_diag), o.max_diag) / rad;
+  double Ei[6];
+  if (!inv3(E, Ei)) {
+    d.st[pb.win].chol_fail = 1;  // benign race: every writer stores 1
+    for (int k = 0; k < 6; ++k) Ei[k] = 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) d.pinv[6 * p + k] = Ei[k];
+  const int o0 = d.pt_obs_off[p], o1 = d.pt_obs_off[p + 1];
+  for (int e = o0; e < o1; ++e) {
+    const int c = d.obs_cam[e];
+    if (c < 0) continue;
+    double Jp[6], Jc[12], sc[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { Jp[k] = d.obs_Jp[6 * e + k]; sc[k] = d.scale_pose[6 * c + k]; }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) Jc[k] = d.obs_Jc[12 * e + k];
+    double Wm[18], Y[18], rc[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) Wm[3 * i + j] = (Jc[i] * Jp[j] + Jc[6 + i] * Jp[3 + j]) * sc[i] * sp[j];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        Y[3 * i + j] = Wm[3 * i] * s3(Ei, 0, j) + Wm[3 * i + 1] * s3(Ei, 1, j) + Wm[3 * i + 2] * s3(Ei, 2, j);
+      rc[i] = Y[3 * i] * b[0] + Y[3 * i + 1] * b[1] + Y[3 * i + 2] * b[2];
+    }
+#pragma unroll
+    for (int k = 0; k < 18; ++k) { d.obs_W[18 * e + k] = Wm[k]; d.obs_Y[18 * e + k] = Y[k]; }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d.obs_rc[6 * e + k] = rc[k];
+  }
+}
+
+// K5: reduced camera system S (envelope) + rhs: one wavefront per non-zero camera block pair
+__global__ __launch_bounds__(64) void k_ba_schur(BaDev d, LMOpt o) {
+  const BlockPair bp = d.bp[blockIdx.x];
+  const WinState& S = d.st[bp.win];
+  if (S.done) return;
+  const BaWin& W = d.win[bp.win];
+  const int lane = threadIdx.x;
+  double acc[36];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+  for (int q = bp.off + lane; q < bp.off + bp.cnt; q += 64) {
+    const int2 pr = d.pairs[q];  // (obs in camera ch, obs in camera cl) of one point
+    double Y[18], Wl[18];
+#pragma unroll
+    for (int k = 0; k < 18; ++k) { Y[k] = d.obs_Y[18 * pr.x + k]; Wl[k] = d.obs_W[18 * pr.y + k]; }
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        acc[6 * i + j] += Y[3 * i] * Wl[3 * j] + Y[3 * i + 1] * Wl[3 * j + 1] + Y[3 * i + 2] * Wl[3 * j + 2];
+  }
+#pragma unroll
+  for (int k = 0; k < 36; ++k) acc[k] = wave_sum(acc[k]);
+  const int lh = bp.ch - W.pose_base, ll = bp.cl - W.pose_base;
+  double* env = d.env + W.env_base;
+  if (bp.ch == bp.cl) {
+    // diagonal block: U_s + D^2 - sum ; rhs = v_s - sum_obs rc
+    double r6[6] = {0, 0, 0, 0, 0, 0};
+    const int a0 = d.cam_obs_off[bp.ch], a1 = d.cam_obs_off[bp.ch + 1];
+    for (int e = a0 + lane; e < a1; e += 64) {
+      const int ob = d.cam_obs[e];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) r6[k] += d.obs_rc[6 * ob + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) r6[k] = wave_sum(r6[k]);
+    if (lane < 36) {
+      const int i = lane / 6, j = lane % 6;
+      if (j <= i) {
+        const double* sc = d.scale_pose + 6 * bp.ch;
+        double v = d.U[21 * bp.ch + u21(i, j)] * sc[i] * sc[j];
+        if (i == j) v += fmin(fmax(v, o.min_diag), o.max_diag) / S.radius;
+        // select acc[lane] without dynamic register indexing
+        double a = 0.0;
+#pragma unroll
+        for (int k = 0; k < 36; ++k) a = (k == lane) ? acc[k] : a;
+        const int row = 6 * lh + i, col = 6 * lh + j;
+        env[d.row_off[W.row_base + row] + (col - d.row_first[W.row_base + row])] = v - a;
+      }
+    }
+    if (lane < 6) {
+      double r = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) r = (k == lane) ? r6[k] : r;
+      const double vs = d.V[6 * bp.ch + lane] * d.scale_pose[6 * bp.ch + lane];
+      d.rhs[W.row_base + 6 * lh + lane] = vs - r;
+    }
+  } else {
+    if (lane < 36) {
+      const int i = lane / 6, j = lane % 6;
+      double a = 0.0;
+#pragma unroll
+      for (int k = 0; k < 36; ++k) a = (k == lane) ? acc[k] : a;
+      const int row = 6 * lh + i, col = 6 * ll + j;
+      env[d.row_off[W.row_base + row] + (col - d.row_first[W.row_base + row])] = -a;
+    }
+  }
+}
+
+// K6: envelope Cholesky of S + forward/back substitution, one workgroup per window.
+// Elements (i, j), first[i] <= j <= i, stored row-wise at row_off[i] + j - first[i].
+template <bool IN_LDS>
+__global__ __launch_bounds__(256) void k_ba_chol(BaDev d, int lds_doubles) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int w = blockIdx.x;
+  if (d.st[w].done) return;
+  const BaWin W = d.win[w];
+  const int n = W.n;
+  const int t = threadIdx.x;
+  const int* first = d.row_first + W.row_base;
+  const int* roff = d.row_off + W.row_base;
+  const int* last = d.col_last + W.row_base;
+  double* A;
+  double* z;
+  if (IN_LDS) {
+    A = smem;
+    z = smem + W.env_size;
+    for (int k = t; k < W.env_size; k += 256) A[k] = d.env[W.env_base + k];
+    for (int k = t; k < n; k += 256) z[k] = d.rhs[W.row_base + k];
+  } else {
+    A = d.env + W.env_base;
+    z = d.rhs + W.row_base;
+  }
+  __syncthreads();
+  bool failed = false;
+  for (int k = 0; k < n; ++k) {
+    const double akk = A[roff[k] + (k - first[k])];
+    if (!(akk > 0.0)) { failed = true; break; }  // every thread reads the same value
+    const double lkk = sqrt(akk);
+    const int lk = last[k];
+    for (int i = k + 1 + t; i <= lk; i += 256)
+      if (first[i] <= k) A[roff[i] + (k - first[i])] /= lkk;
+    if (t == 0) { A[roff[k] + (k - first[k])] = lkk; z[k] /= lkk; }
+    __syncthreads();
+    const int m = lk - k;
+    const double zk = z[k];
+    for (int e = t; e < m * m; e += 256) {
+      const int ii = e / m, jj = e - ii * m;
+      if (jj > ii) continue;
+      const int i = k + 1 + ii, j = k + 1 + jj;
+      const int fi = first[i], fj = first[j];
+      if (fi > k || fj > k) continue;
+      A[roff[i] + (j - fi)] -= A[roff[i] + (k - fi)] * A[roff[j] + (k - fj)];
+    }
+    for (int i = k + 1 + t; i <= lk; i += 256)
+      if (first[i] <= k) z[i] -= A[roff[i] + (k - first[i])] * zk;
+    __syncthreads();
+  }
+  if (failed) {
+    if (t == 0) d.st[w].chol_fail = 1;
+    return;
+  }
+  for (int k = n - 1; k >= 0; --k) {
+    const double yk = z[k] / A[roff[k] + (k - first[k])];
+    const int fk = first[k];
+    for (int i = fk + t; i < k; i += 256) z[i] -= A[roff[k] + (i - fk)] * yk;
+    if (t == 0) z[k] = yk;
+    __syncthreads();
+  }
+  for (int k = t; k < n; k += 256) d.ycam[W.row_base + k] = z[k];
+}
+
+// K7: per-point back-substitution, candidate point, model cost change and candidate cost
+__global__ __launch_bounds__(kPB) void k_ba_backsub(BaDev d) {
+  __shared__ double sh[3 * kPB];
+  const PBlk pb = d.pblk[blockIdx.x];
+  const WinState& S = d.st[pb.win];
+  if (S.done || S.chol_fail) return;
+  const BaWin& W = d.win[pb.win];
+  const int cur = S.cur;
+  const int t = threadIdx.x;
+  double mcc = 0.0, ncost = 0.0, sn2 = 0.0;
+  if (t < pb.cnt) {
+    const int p = pb.p0 + t;
+    double sp[3], X[3], b[3], Ei[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      sp[k] = d.scale_pt[3 * p + k];
+      X[k] = d.x_pt[cur][3 * p + k];
+      b[k] = d.etb[3 * p + k] * sp[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Ei[k] = d.pinv[6 * p + k];
+    const int o0 = d.pt_obs_off[p], o1 = d.pt_obs_off[p + 1];
+    for (int e = o0; e < o1; ++e) {
+      const int c = d.obs_cam[e];
+      if (c < 0) continue;
+      const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
+      const double* Wm = d.obs_W + 18 * e;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) s += Wm[3 * i + j] * y[i];
+        b[j] -= s;
+      }
+    }
+    double step[3], Xn[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      step[j] = -(s3(Ei, j, 0) * b[0] + s3(Ei, j, 1) * b[1] + s3(Ei, j, 2) * b[2]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      Xn[j] = X[j] + step[j] * sp[j];
+      d.x_pt[cur ^ 1][3 * p + j] = Xn[j];
+    }
+    if (o1 > o0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) sn2 += (X[j] - Xn[j]) * (X[j] - Xn[j]);
+    }
+    for (int e = o0; e < o1; ++e) {
+      const int c = d.obs_cam[e];
+      double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const double s = step[j] * sp[j];
+        m0 += d.obs_Jp[6 * e + j] * s;
+        m1 += d.obs_Jp[6 * e + 3 + j] * s;
+      }
+      double pose[6];
+      if (c >= 0) {
+        const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          const double sc = d.scale_pose[6 * c + k];
+          const double s = -y[k] * sc;
+          m0 += d.obs_Jc[12 * e + k] * s;
+          m1 += d.obs_Jc[12 * e + 6 + k] * s;
+          pose[k] = d.x_pose[cur][6 * c + k] + s;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[e] + k];
+      }
+      const double r0 = d.obs_r[2 * e], r1 = d.obs_r[2 * e + 1];
+      mcc += m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0);
+      const double2 uv = d.obs_uv[e];
+      double rn[2];
+      residual(pose, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
+      ncost += 0.5 * (rn[0] * rn[0] + rn[1] * rn[1]);
+    }
+  }
+  double v[3] = {mcc, ncost, sn2};
+  block_sum<3>(v, sh);
+  if (t == 0) {
+    double* P = d.part + 8 * blockIdx.x;
+    P[3] = v[0]; P[4] = v[1]; P[5] = v[2];
+  }
+}
+
+// K8: per-window iteration tail: camera candidate, step validity, tolerances, accept/reject
+__global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
+  const int w = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  WinState S = d.st[w];
+  if (S.done) return;
+  const BaWin W = d.win[w];
+  bool valid = !S.chol_fail;
+  double mccs = 0.0, ncost = 0.0, sn2 = 0.0;
+  if (valid) {
+    for (int b = 0; b < W.n_pblk; ++b) {
+      const double* P = d.part + 8 * (W.pblk_base + b);
+      mccs += P[3]; ncost += P[4]; sn2 += P[5];
+    }
+    const int cur = S.cur;
+    for (int c = W.pose_base; c < W.pose_base + W.n_poses; ++c) {
+      const bool active = d.cam_obs_off[c + 1] > d.cam_obs_off[c];
+      const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
+      for (int k = 0; k < 6; ++k) {
+        const double x = d.x_pose[cur][6 * c + k];
+        const double xn = x + (-y[k]) * d.scale_pose[6 * c + k];
+        d.x_pose[cur ^ 1][6 * c + k] = xn;
+        if (active) sn2 += (x - xn) * (x - xn);
+      }
+    }
+  }
+  const double model_cost_change = -mccs;
+  valid = valid && isfinite(model_cost_change) && isfinite(sn2) && model_cost_change > 0.0;
+  if (!valid) {
+    if (++S.n_invalid >= o.max_invalid) {
+      S.done = 1; S.term = LORB_TERM_FAILURE;
+    } else {
+      S.radius = S.radius / S.decrease_factor;
+      S.decrease_factor *= 2.0;
+      S.last_successful = 0;
+    }
+    d.st[w] = S;
+    return;
+  }
+  S.n_invalid = 0;
+  const double new_cost = isfinite(ncost) ? ncost : 1.7976931348623157e308;
+  const double step_norm = sqrt(sn2);
+  if (step_norm <= o.ptol * (S.x_norm + o.ptol)) {
+    S.done = 1; S.term = LORB_TERM_PARAMETER_TOL; d.st[w] = S; return;
+  }
+  const double cost_change = S.cost - new_cost;
+  if (fabs(cost_change) <= o.ftol * S.cost) {
+    S.done = 1; S.term = LORB_TERM_FUNCTION_TOL; d.st[w] = S; return;
+  }
+  const double rel = cost_change / model_cost_change;
+  if (rel > o.min_rel) {
+    S.cur ^= 1;
+    S.relin = 1;
+    S.n_success++;
+    const double tt = 2.0 * rel - 1.0;
+    S.radius = S.radius / fmax(1.0 / 3.0, 1.0 - tt * tt * tt);
+    S.radius = fmin(o.max_radius, S.radius);
+    S.decrease_factor = 2.0;
+  } else {
+    S.last_successful = 0;
+    S.radius = S.radius / S.decrease_factor;
+    S.decrease_factor *= 2.0;
+  }
+  d.st[w] = S;
+}
+
+// ------------------------------------------------------------------------------------------
+// pose-only LM (BA::ProjectPoseOptimization), one workgroup per frame, whole solve in-kernel
+__global__ __launch_bounds__(256) void k_ba_pose_only(const int32_t* __restrict__ res_off,
+                                                      const float* __restrict__ intr,
+                                                      const float* __restrict__ pose_init,
+                                                      const float* __restrict__ pts3d,
+                                                      const float* __restrict__ obs2d, LMOpt o,
+                                                      double* __restrict__ pose_out,
+                                                      lorb_ba_summary* __restrict__ sums) {
+  __shared__ double sh[28 * 256];
+  __shared__ double xs[6], xn[6], sc[6], step[6];
+  __shared__ double s_cost, s_gmax, s_xnorm, s_new;
+  __shared__ double JtJ[21], Jtr[6];
+  __shared__ int s_flag;  // 0 continue, 1 stop
+  __shared__ int s_relin;
+  const int f = blockIdx.x;
+  const int t = threadIdx.x;
+  const int r0 = res_off[f], r1 = res_off[f + 1];
+  const double fx = intr[4 * f], fyv = intr[4 * f + 1], cx = intr[4 * f + 2], cy = intr[4 * f + 3];
+  if (t < 6) xs[t] = (double)pose_init[6 * f + t];
+  __syncthreads();
+  if (r1 == r0) {
+    if (t < 6) pose_out[6 * f + t] = xs[t];
+    if (t == 0) { lorb_ba_summary z = {}; sums[f] = z; }
+    return;
+  }
+  double radius = o.init_radius, df = 2.0;
+  int iter = 0, n_success = 0, n_invalid = 0, term = LORB_TERM_NO_CONVERGENCE, last_successful = 1;
+  double initial_cost = 0.0;
+  if (t == 0) s_relin = 1;
+  __syncthreads();
+  for (;;) {
+    if (s_relin) {
+      double v[28];
+#pragma unroll
+      for (int k = 0; k < 28; ++k) v[k] = 0.0;
+      double pose[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) pose[k] = xs[k];
+      for (int r = r0 + t; r < r1; r += 256) {
+        const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
+        double rr[2], Jp[6], Jc[12];
+        residual_jac(pose, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr, Jp, Jc);
+        int q = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          v[21 + a] += Jc[a] * rr[0] + Jc[6 + a] * rr[1];
+#pragma unroll
+          for (int b = a; b < 6; ++b) v[q++] += Jc[a] * Jc[b] + Jc[6 + a] * Jc[6 + b];
+        }
+        v[27] += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
+      }
+      block_sum<28>(v, sh);
+      if (t == 0) {
+        for (int k = 0; k < 21; ++k) JtJ[k] = v[k];
+        for (int k = 0; k < 6; ++k) Jtr[k] = v[21 + k];
+        s_cost = v[27];
+        double gm = 0.0, xn2 = 0.0;
+        for (int k = 0; k < 6; ++k) { gm = fmax(gm, fabs(xs[k] - (xs[k] + -Jtr[k]))); xn2 += xs[k] * xs[k]; }
+        s_gmax = gm;
+        s_xnorm = sqrt(xn2);
+        if (iter == 0) {
+          initial_cost = s_cost;
+          const int dg[6] = {0, 6, 11, 15, 18, 20};
+          for (int k = 0; k < 6; ++k) sc[k] = o.jacobi ? 1.0 / (1.0 + sqrt(JtJ[dg[k]])) : 1.0;
+        }
+        last_successful = 1;
+        s_relin = 0;
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      s_flag = 0;
+      if (iter >= o.max_iter) { s_flag = 1; term = LORB_TERM_NO_CONVERGENCE; }
+      else if (last_successful && s_gmax <= o.gtol) { s_flag = 1; term = LORB_TERM_GRADIENT_TOL; }
+      else if (radius <= o.min_radius) { s_flag = 1; term = LORB_TERM_MIN_RADIUS; }
+      else {
+        iter++;
+        // (Js^T Js + D^2) y = Js^T r, D^2 = clamp(diag)/radius ; dense 6x6 Cholesky
+        double A[36], y[6];
+        for (int a = 0; a < 6; ++a) {
+          for (int b = 0; b < 6; ++b) A[6 * a + b] = JtJ[u21(a, b)] * sc[a] * sc[b];
+          y[a] = Jtr[a] * sc[a];
+        }
+        for (int a = 0; a < 6; ++a) A[7 * a] += fmin(fmax(A[7 * a], o.min_diag), o.max_diag) / radius;
+        bool ok = true;
+        for (int j = 0; j < 6 && ok; ++j) {
+          double dd = A[7 * j];
+          for (int k = 0; k < j; ++k) dd -= A[6 * j + k] * A[6 * j + k];
+          if (!(dd > 0.0)) { ok = false; break; }
+          const double l = sqrt(dd);
+          A[7 * j] = l;
+          for (int i = j + 1; i < 6; ++i) {
+            double s = A[6 * i + j];
+            for (int k = 0; k < j; ++k) s -= A[6 * i + k] * A[6 * j + k];
+            A[6 * i + j] = s / l;
+          }
+        }
+        double mcc = -1.0;
+        if (ok) {
+          for (int i = 0; i < 6; ++i) { double s = y[i]; for (int k = 0; k < i; ++k) s -= A[6 * i + k] * y[k]; y[i] = s / A[7 * i]; }
+          for (int i = 5; i >= 0; --i) { double s = y[i]; for (int k = i + 1; k < 6; ++k) s -= A[6 * k + i] * y[k]; y[i] = s / A[7 * i]; }
+          // model cost change = -(step.Js^T r + 0.5 step^T Js^T Js step), step = -y
+          double lin = 0.0, quad = 0.0;
+          for (int a = 0; a < 6; ++a) {
+            const double sa = -y[a];
+            lin += sa * Jtr[a] * sc[a];
+            for (int b = 0; b < 6; ++b) quad += sa * JtJ[u21(a, b)] * sc[a] * sc[b] * (-y[b]);
+          }
+          mcc = -(lin + 0.5 * quad);
+          for (int a = 0; a < 6; ++a) { step[a] = -y[a]; xn[a] = xs[a] + step[a] * sc[a]; }
+          ok = isfinite(mcc) && mcc > 0.0;
+        }
+        if (!ok) {
+          if (++n_invalid >= o.max_invalid) { s_flag = 1; term = LORB_TERM_FAILURE; }
+          else { radius /= df; df *= 2.0; last_successful = 0; s_flag = 2; }
+        } else {
+          n_invalid = 0;
+          s_new = mcc;  // stash model cost change
+          s_flag = 3;
+        }
+      }
+    }
+    __syncthreads();
+    if (s_flag == 1) break;
+    if (s_flag == 2) continue;
+    // candidate cost
+    double v[1] = {0.0};
+    double pose[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pose[k] = xn[k];
+    for (int r = r0 + t; r < r1; r += 256) {
+      const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
+      double rr[2];
+      residual(pose, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr);
+      v[0] += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
+    }
+    block_sum<1>(v, sh);
+    if (t == 0) {
+      const double mcc = s_new;
+      const double new_cost = isfinite(v[0]) ? v[0] : 1.7976931348623157e308;
+      double sn2 = 0.0;
+      for (int k = 0; k < 6; ++k) sn2 += (xs[k] - xn[k]) * (xs[k] - xn[k]);
+      s_flag = 0;
+      if (sqrt(sn2) <= o.ptol * (s_xnorm + o.ptol)) { s_flag = 1; term = LORB_TERM_PARAMETER_TOL; }
+      else {
+        const double cc = s_cost - new_cost;
+        if (fabs(cc) <= o.ftol * s_cost) { s_flag = 1; term = LORB_TERM_FUNCTION_TOL; }
+        else {
+          const double rel = cc / mcc;
+          if (rel > o.min_rel) {
+            for (int k = 0; k < 6; ++k) xs[k] = xn[k];
+            s_relin = 1;
+            n_success++;
+            const double tt = 2.0 * rel - 1.0;
+            radius = fmin(o.max_radius, radius / fmax(1.0 / 3.0, 1.0 - tt * tt * tt));
+            df = 2.0;
+          } else {
+            last_successful = 0;
+            radius /= df;
+            df *= 2.0;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (s_flag == 1) break;
+  }
+  if (t < 6) pose_out[6 * f + t] = xs[t];
+  if (t == 0) {
+    lorb_ba_summary s;
+    s.iterations = iter; s.successful_steps = n_success; s.termination = term; s.pad_ = 0;
+    s.initial_cost = initial_cost; s.final_cost = s_cost;
+    sums[f] = s;
+  }
+}
+
+LMOpt to_dev_opt(const lorb_lm_options* o) {
+  LMOpt d;
+  d.max_iter = o->max_num_iterations; d.max_invalid = o->max_num_consecutive_invalid_steps;
+  d.jacobi = o->jacobi_scaling; d.ftol = o->function_tolerance; d.gtol = o->gradient_tolerance;
+  d.ptol = o->parameter_tolerance; d.init_radius = o->initial_trust_region_radius;
+  d.max_radius = o->max_trust_region_radius; d.min_radius = o->min_trust_region_radius;
+  d.min_rel = o->min_relative_decrease; d.min_diag = o->min_lm_diagonal; d.max_diag = o->max_lm_diagonal;
+  return d;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+struct lorb_ba_plan {
+  lorb_ctx* ctx = nullptr;
+  int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_bp = 0, n_pairs = 0;
+  int env_total = 0, n_total = 0, max_env = 0;
+  std::vector<BaWin> hwin;
+  std::vector<void*> allocs;
+  BaDev dev{};
+  WinState* d_state = nullptr;
+  // graph of one LM iteration
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  LMOpt graph_opt{};
+  bool has_graph = false;
+  ~lorb_ba_plan() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph) (void)hipGraphDestroy(graph);
+    for (void* p : allocs) (void)hipFree(p);
+  }
+};
+
+namespace {
+
+template <typename T>
+int dalloc(lorb_ba_plan* P, size_t n, T** out) {
+  void* p = nullptr;
+  LORB_HIP(P->ctx, hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+  P->allocs.push_back(p);
+  *out = static_cast<T*>(p);
+  return LORB_OK;
+}
+template <typename T>
+int dupload(lorb_ba_plan* P, const std::vector<T>& v, T** out) {
+  LORB_TRY(dalloc(P, v.size(), out));
+  if (!v.empty())
+    LORB_HIP(P->ctx, hipMemcpyAsync(*out, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, P->ctx->stream));
+  return LORB_OK;
+}
+
+int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P) {
+  P->ctx = ctx;
+  P->W = nw;
+  std::vector<int> pt_obs_off(1, 0), obs_cam, obs_fix, cam_obs_off(1, 0), cam_obs, cam_win;
+  std::vector<double2> obs_uv;
+  std::vector<double> fixed, xpose, xpt;
+  std::vector<PBlk> pblk;
+  std::vector<BlockPair> bps;
+  std::vector<int2> pairs;
+  std::vector<int> row_first, row_off, col_last;
+  int pose_base = 0, point_base = 0, fix_base = 0, env_base = 0, row_base = 0;
+  for (int w = 0; w < nw; ++w) {
+    const lorb_ba_window& in = win[w];
+    if (in.n_poses < 0 || in.n_points < 0 || in.n_obs < 0 || in.n_fixed < 0)
+      return lorb::set_error(ctx, LORB_E_INVALID, "window %d: negative sizes", w);
+    BaWin bw{};
+    bw.pose_base = pose_base; bw.n_poses = in.n_poses;
+    bw.point_base = point_base; bw.n_points = in.n_points;
+    bw.fx = in.fx; bw.fy = in.fy; bw.cx = in.cx; bw.cy = in.cy;
+    bw.obs_base = (int)obs_cam.size(); bw.n_obs = in.n_obs;
+    // obs sorted by point (stable)
+    std::vector<int> cnt(in.n_points + 1, 0);
+    for (int k = 0; k < in.n_obs; ++k) {
+      const int p = in.obs_point[k], f = in.obs_frame[k];
+      if (p < 0 || p >= in.n_points) return lorb::set_error(ctx, LORB_E_INVALID, "window %d obs %d: bad point %d", w, k, p);
+      if (f >= in.n_poses || f < -in.n_fixed) return lorb::set_error(ctx, LORB_E_INVALID, "window %d obs %d: bad frame %d", w, k, f);
+      cnt[p + 1]++;
+    }
+    for (int p = 0; p < in.n_points; ++p) cnt[p + 1] += cnt[p];
+    std::vector<int> order(in.n_obs), fill(in.n_points, 0);
+    for (int k = 0; k < in.n_obs; ++k) { const int p = in.obs_point[k]; order[cnt[p] + fill[p]++] = k; }
+    const int ob0 = (int)obs_cam.size();
+    for (int p = 0; p < in.n_points; ++p) pt_obs_off.push_back(ob0 + cnt[p + 1]);
+    for (int e = 0; e < in.n_obs; ++e) {
+      const int k = order[e], f = in.obs_frame[k];
+      obs_cam.push_back(f >= 0 ? pose_base + f : -1);
+      obs_fix.push_back(f >= 0 ? -1 : fix_base + (-1 - f));
+      obs_uv.push_back(make_double2(in.obs_uv[2 * k], in.obs_uv[2 * k + 1]));
+    }
+    for (int i = 0; i < 6 * in.n_fixed; ++i) fixed.push_back(in.fixed_pose[i]);
+    for (int i = 0; i < 6 * in.n_poses; ++i) xpose.push_back(in.pose_init[i]);
+    for (int i = 0; i < 3 * in.n_points; ++i) xpt.push_back(in.point_init[i]);
+    // camera-major obs lists (sorted by point == by sorted obs index)
+    std::vector<std::vector<int>> co(in.n_poses);
+    for (int e = 0; e < in.n_obs; ++e) { const int c = obs_cam[ob0 + e]; if (c >= 0) co[c - pose_base].push_back(ob0 + e); }
+    for (int c = 0; c < in.n_poses; ++c) {
+      for (int e : co[c]) cam_obs.push_back(e);
+      cam_obs_off.push_back((int)cam_obs.size());
+      cam_win.push_back(w);
+    }
+    // block pairs: for each point, all ordered (obs_h, obs_l) with cam(h) >= cam(l)
+    std::map<std::pair<int, int>, std::vector<int2>> bmap;
+    for (int c = 0; c < in.n_poses; ++c) bmap[{c, c}];  // every diagonal block exists
+    std::vector<int> fc(in.n_poses);
+    for (int c = 0; c < in.n_poses; ++c) fc[c] = c;
+    for (int p = 0; p < in.n_points; ++p) {
+      const int e0 = ob0 + cnt[p], e1 = ob0 + cnt[p + 1];
+      for (int a = e0; a < e1; ++a) {
+        const int ca = obs_cam[a];
+        if (ca < 0) continue;
+        for (int b = e0; b < e1; ++b) {
+          const int cb = obs_cam[b];
+          if (cb < 0 || cb > ca) continue;
+          bmap[{ca - pose_base, cb - pose_base}].push_back(make_int2(a, b));
+          fc[ca - pose_base] = std::min(fc[ca - pose_base], cb - pose_base);
+        }
+      }
+    }
+    for (auto& kv : bmap) {
+      BlockPair b;
+      b.win = w; b.ch = pose_base + kv.first.first; b.cl = pose_base + kv.first.second;
+      b.off = (int)pairs.size(); b.cnt = (int)kv.second.size();
+      pairs.insert(pairs.end(), kv.second.begin(), kv.second.end());
+      bps.push_back(b);
+    }
+    // envelope rows
+    const int n = 6 * in.n_poses;
+    int off = 0;
+    std::vector<int> rf(n);
+    for (int c = 0; c < in.n_poses; ++c)
+      for (int a = 0; a < 6; ++a) {
+        const int i = 6 * c + a;
+        rf[i] = 6 * fc[c];
+        row_first.push_back(rf[i]);
+        row_off.push_back(off);
+        off += i - rf[i] + 1;
+      }
+    for (int k = 0; k < n; ++k) {
+      int lk = k;
+      for (int i = k + 1; i < n; ++i) if (rf[i] <= k) lk = i;
+      col_last.push_back(lk);
+    }
+    bw.env_base = env_base; bw.env_size = off; bw.n = n; bw.row_base = row_base;
+    P->max_env = std::max(P->max_env, off + n);
+    env_base += off; row_base += n;
+    // point blocks
+    bw.pblk_base = (int)pblk.size();
+    for (int p0 = 0; p0 < in.n_points; p0 += kPB) pblk.push_back({w, point_base + p0, std::min(kPB, in.n_points - p0)});
+    bw.n_pblk = (int)pblk.size() - bw.pblk_base;
+    P->hwin.push_back(bw);
+    pose_base += in.n_poses; point_base += in.n_points; fix_base += in.n_fixed;
+  }
+  P->Ctot = pose_base; P->Ptot = point_base; P->K = (int)obs_cam.size(); P->NF = fix_base;
+  P->n_pblk = (int)pblk.size(); P->n_bp = (int)bps.size(); P->n_pairs = (int)pairs.size();
+  P->env_total = env_base; P->n_total = row_base;
+  BaDev& d = P->dev;
+  BaWin* dwin; PBlk* dpb; BlockPair* dbp; int2* dpairs; double2* duv;
+  int *a1, *a2, *a3, *a4, *a5, *a6, *a7, *a8, *a9;
+  double* dfix;
+  LORB_TRY(dupload(P, P->hwin, &dwin)); d.win = dwin;
+  LORB_TRY(dupload(P, pblk, &dpb)); d.pblk = dpb;
+  LORB_TRY(dupload(P, bps, &dbp)); d.bp = dbp;
+  LORB_TRY(dupload(P, pairs, &dpairs)); d.pairs = dpairs;
+  LORB_TRY(dupload(P, pt_obs_off, &a1)); d.pt_obs_off = a1;
+  LORB_TRY(dupload(P, obs_cam, &a2)); d.obs_cam = a2;
+  LORB_TRY(dupload(P, obs_fix, &a3)); d.obs_fix = a3;
+  LORB_TRY(dupload(P, obs_uv, &duv)); d.obs_uv = duv;
+  LORB_TRY(dupload(P, cam_obs_off, &a4)); d.cam_obs_off = a4;
+  LORB_TRY(dupload(P, cam_obs, &a5)); d.cam_obs = a5;
+  LORB_TRY(dupload(P, cam_win, &a6)); d.cam_win = a6;
+  LORB_TRY(dupload(P, row_first, &a7)); d.row_first = a7;
+  LORB_TRY(dupload(P, row_off, &a8)); d.row_off = a8;
+  LORB_TRY(dupload(P, col_last, &a9)); d.col_last = a9;
+  LORB_TRY(dupload(P, fixed, &dfix)); d.fixed_pose = dfix;
+  LORB_TRY(dupload(P, xpose, &d.x_init_pose));
+  LORB_TRY(dupload(P, xpt, &d.x_init_pt));
+  LORB_TRY(dupload(P, xpose, &d.x_pose[0]));
+  LORB_TRY(dupload(P, xpose, &d.x_pose[1]));
+  LORB_TRY(dupload(P, xpt, &d.x_pt[0]));
+  LORB_TRY(dupload(P, xpt, &d.x_pt[1]));
+  const size_t C = P->Ctot, Pn = P->Ptot, K = P->K;
+  LORB_TRY(dalloc(P, C * 6, &d.scale_pose)); LORB_TRY(dalloc(P, Pn * 3, &d.scale_pt));
+  LORB_TRY(dalloc(P, Pn * 6, &d.ete)); LORB_TRY(dalloc(P, Pn * 3, &d.etb)); LORB_TRY(dalloc(P, Pn * 6, &d.pinv));
+  LORB_TRY(dalloc(P, C * 21, &d.U)); LORB_TRY(dalloc(P, C * 6, &d.V)); LORB_TRY(dalloc(P, C, &d.cam_gmax));
+  LORB_TRY(dalloc(P, K * 2, &d.obs_r)); LORB_TRY(dalloc(P, K * 6, &d.obs_Jp)); LORB_TRY(dalloc(P, K * 12, &d.obs_Jc));
+  LORB_TRY(dalloc(P, K * 18, &d.obs_W)); LORB_TRY(dalloc(P, K * 18, &d.obs_Y)); LORB_TRY(dalloc(P, K * 6, &d.obs_rc));
+  LORB_TRY(dalloc(P, (size_t)P->env_total, &d.env)); LORB_TRY(dalloc(P, (size_t)P->n_total, &d.rhs));
+  LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
+  LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
+  if (!obs_cam.empty()) { /* keep obs arrays alive via allocs */ }
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+constexpr int kLdsBudget = 160 * 1024 - 1024;
+
+// one LM iteration (K1..K8) on the ctx stream
+int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
+  lorb_ctx* ctx = P->ctx;
+  hipStream_t s = ctx->stream;
+  const BaDev& d = P->dev;
+  if (P->n_pblk) hipLaunchKernelGGL(k_ba_linearize, dim3(P->n_pblk), dim3(kPB), 0, s, d);
+  if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(64), 0, s, d);
+  hipLaunchKernelGGL(k_ba_lm_begin, dim3(P->W), dim3(64), 0, s, d, o);
+  if (P->n_pblk) hipLaunchKernelGGL(k_ba_point_prep, dim3(P->n_pblk), dim3(kPB), 0, s, d, o);
+  if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
+  if (P->n_bp) {
+    lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
+    hipLaunchKernelGGL(k_ba_schur, dim3(P->n_bp), dim3(64), 0, s, d, o);
+  }
+  if (P->Ctot) {
+    lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
+    const size_t lds = sizeof(double) * (size_t)P->max_env;
+    if (lds <= (size_t)kLdsBudget)
+      hipLaunchKernelGGL(k_ba_chol<true>, dim3(P->W), dim3(256), lds, s, d, P->max_env);
+    else
+      hipLaunchKernelGGL(k_ba_chol<false>, dim3(P->W), dim3(256), 0, s, d, 0);
+  }
+  if (P->n_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->n_pblk), dim3(kPB), 0, s, d);
+  hipLaunchKernelGGL(k_ba_lm_end, dim3(P->W), dim3(64), 0, s, d, o);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
+int enqueue_finalize(lorb_ba_plan* P, const LMOpt& o) {
+  lorb_ctx* ctx = P->ctx;
+  hipStream_t s = ctx->stream;
+  const BaDev& d = P->dev;
+  if (P->n_pblk) hipLaunchKernelGGL(k_ba_linearize, dim3(P->n_pblk), dim3(kPB), 0, s, d);
+  if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(64), 0, s, d);
+  hipLaunchKernelGGL(k_ba_lm_begin, dim3(P->W), dim3(64), 0, s, d, o);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
+int plan_solve(lorb_ba_plan* P, const lorb_lm_options* opt) {
+  lorb_ctx* ctx = P->ctx;
+  LMOpt o = to_dev_opt(opt);
+  // restore the initial values into x[0] (x[1] is the candidate buffer)
+  if (P->Ctot) LORB_HIP(ctx, hipMemcpyAsync(P->dev.x_pose[0], P->dev.x_init_pose, sizeof(double) * 6 * P->Ctot, hipMemcpyDeviceToDevice, ctx->stream));
+  if (P->Ptot) LORB_HIP(ctx, hipMemcpyAsync(P->dev.x_pt[0], P->dev.x_init_pt, sizeof(double) * 3 * P->Ptot, hipMemcpyDeviceToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_ba_init, dim3(lorb::ceil_div(P->W, 64)), dim3(64), 0, ctx->stream, P->dev, P->W, o);
+  LORB_CHECK_LAUNCH(ctx);
+  const bool timing = ctx->ktime;  // per-kernel events cannot live inside a graph
+  if (!timing && (!P->has_graph || memcmp(&P->graph_opt, &o, sizeof(LMOpt)) != 0)) {
+    if (P->gexec) { (void)hipGraphExecDestroy(P->gexec); P->gexec = nullptr; }
+    if (P->graph) { (void)hipGraphDestroy(P->graph); P->graph = nullptr; }
+    LORB_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+    int rc = enqueue_iteration(P, o);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+    if (rc != LORB_OK) return rc;
+    if (e != hipSuccess) return lorb::set_error(ctx, LORB_E_DEVICE, "graph capture failed: %s", hipGetErrorString(e));
+    P->graph = g;
+    LORB_HIP(ctx, hipGraphInstantiate(&P->gexec, P->graph, nullptr, nullptr, 0));
+    P->graph_opt = o;
+    P->has_graph = true;
+  }
+  for (int it = 0; it < o.max_iter; ++it) {
+    if (timing) LORB_TRY(enqueue_iteration(P, o));
+    else LORB_HIP(ctx, hipGraphLaunch(P->gexec, ctx->stream));
+  }
+  LORB_TRY(enqueue_finalize(P, o));
+  return LORB_OK;
+}
+
+int plan_read(lorb_ba_plan* P, double* const* pose_out, double* const* point_out,
+              lorb_ba_summary* sums) {
+  lorb_ctx* ctx = P->ctx;
+  std::vector<WinState> st(P->W);
+  LORB_HIP(ctx, hipMemcpyAsync(st.data(), P->d_state, sizeof(WinState) * P->W, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (int w = 0; w < P->W; ++w) {
+    const BaWin& bw = P->hwin[w];
+    const int cur = st[w].cur;
+    if (pose_out && pose_out[w] && bw.n_poses)
+      LORB_HIP(ctx, hipMemcpyAsync(pose_out[w], P->dev.x_pose[cur] + 6 * bw.pose_base, sizeof(double) * 6 * bw.n_poses, hipMemcpyDeviceToHost, ctx->stream));
+    if (point_out && point_out[w] && bw.n_points)
+      LORB_HIP(ctx, hipMemcpyAsync(point_out[w], P->dev.x_pt[cur] + 3 * bw.point_base, sizeof(double) * 3 * bw.n_points, hipMemcpyDeviceToHost, ctx->stream));
+    if (sums) {
+      lorb_ba_summary s{};
+      s.iterations = st[w].iter; s.successful_steps = st[w].n_success; s.termination = st[w].term;
+      s.initial_cost = st[w].initial_cost; s.final_cost = st[w].cost;
+      if (bw.n_obs == 0) { s.iterations = 0; s.termination = LORB_TERM_FUNCTION_TOL; }
+      sums[w] = s;
+    }
+  }
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lorb_ba_plan_create(lorb_ctx* ctx, int32_t n_windows, const lorb_ba_window* windows,
+                        lorb_ba_plan** out) {
+  if (!ctx || !out || n_windows < 0 || (n_windows > 0 && !windows)) return LORB_E_INVALID;
+  *out = nullptr;
+  lorb_ba_plan* P = new (std::nothrow) lorb_ba_plan();
+  if (!P) return LORB_E_NOMEM;
+  int rc = build_plan(ctx, n_windows, windows, P);
+  if (rc != LORB_OK) { delete P; return rc; }
+  *out = P;
+  return LORB_OK;
+}
+
+int lorb_ba_plan_solve(lorb_ba_plan* plan, const lorb_lm_options* opt) {
+  if (!plan || !opt) return LORB_E_INVALID;
+  if (plan->W == 0) return LORB_OK;
+  return plan_solve(plan, opt);
+}
+
+int lorb_ba_plan_read(lorb_ba_plan* plan, double* const* pose_out, double* const* point_out,
+                      lorb_ba_summary* summaries) {
+  if (!plan) return LORB_E_INVALID;
+  if (plan->W == 0) return LORB_OK;
+  return plan_read(plan, pose_out, point_out, summaries);
+}
+
+int lorb_ba_plan_destroy(lorb_ba_plan* plan) {
+  if (!plan) return LORB_OK;
+  if (plan->ctx) (void)hipStreamSynchronize(plan->ctx->stream);
+  delete plan;
+  return LORB_OK;
+}
+
+int lorb_ba_local(lorb_ctx* ctx, int32_t n_windows, const lorb_ba_window* windows,
+                  const lorb_lm_options* opt, double* const* pose_out, double* const* point_out,
+                  lorb_ba_summary* summaries) {
+  if (!ctx || !opt) return LORB_E_INVALID;
+  lorb_ba_plan* P = nullptr;
+  LORB_TRY(lorb_ba_plan_create(ctx, n_windows, windows, &P));
+  int rc = lorb_ba_plan_solve(P, opt);
+  if (rc == LORB_OK) rc = lorb_ba_plan_read(P, pose_out, point_out, summaries);
+  lorb_ba_plan_destroy(P);
+  return rc;
+}
+
+int lorb_ba_pose_only(lorb_ctx* ctx, const lorb_pose_problem_batch* prob,
+                      const lorb_lm_options* opt, double* pose_out, float* Tcw_out,
+                      lorb_ba_summary* summaries) {
+  if (!ctx || !prob || !opt || !pose_out) return LORB_E_INVALID;
+  const int nf = prob->n_frames;
+  if (nf <= 0) return LORB_OK;
+  const int nr = prob->res_off[nf];
+  int32_t* roff; float *intr, *pinit, *pts, *obs;
+  double* dpose; lorb_ba_summary* dsum;
+  LORB_TRY(lorb::upload_t(ctx, S_W0, prob->res_off, (size_t)nf + 1, &roff));
+  LORB_TRY(lorb::upload_t(ctx, S_W1, prob->intr, (size_t)nf * 4, &intr));
+  LORB_TRY(lorb::upload_t(ctx, S_W2, prob->pose_init, (size_t)nf * 6, &pinit));
+  LORB_TRY(lorb::scratch_t(ctx, S_W3, (size_t)std::max(nr, 1) * 3, &pts));
+  LORB_TRY(lorb::scratch_t(ctx, S_W4, (size_t)std::max(nr, 1) * 2, &obs));
+  if (nr > 0) {
+    LORB_HIP(ctx, hipMemcpyAsync(pts, prob->pts3d, sizeof(float) * 3 * nr, hipMemcpyHostToDevice, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(obs, prob->obs2d, sizeof(float) * 2 * nr, hipMemcpyHostToDevice, ctx->stream));
+  }
+  LORB_TRY(lorb::scratch_t(ctx, S_W5, (size_t)nf * 6, &dpose));
+  LORB_TRY(lorb::scratch_t(ctx, S_W6, (size_t)nf, &dsum));
+  hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(256), 0, ctx->stream, roff, intr, pinit, pts, obs,
+                     to_dev_opt(opt), dpose, dsum);
+  LORB_CHECK_LAUNCH(ctx);
+  LORB_HIP(ctx, hipMemcpyAsync(pose_out, dpose, sizeof(double) * 6 * nf, hipMemcpyDeviceToHost, ctx->stream));
+  std::vector<lorb_ba_summary> hs(nf);
+  LORB_HIP(ctx, hipMemcpyAsync(hs.data(), dsum, sizeof(lorb_ba_summary) * nf, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (summaries) std::copy(hs.begin(), hs.end(), summaries);
+  if (Tcw_out)
+    for (int f = 0; f < nf; ++f) {
+      const float R[3] = {(float)pose_out[6 * f], (float)pose_out[6 * f + 1], (float)pose_out[6 * f + 2]};
+      const float T[3] = {(float)pose_out[6 * f + 3], (float)pose_out[6 * f + 4], (float)pose_out[6 * f + 5]};
+      lorb_pose_to_Tcw(R, T, Tcw_out + 16 * f);
+    }
+  return LORB_OK;
+}
+
+// cv::Rodrigues (vector -> matrix, double internally) + Frame::UpdatePoseMat write-back
+void lorb_pose_to_Tcw(const float rvec[3], const float tvec[3], float T[16]) {
+  double rx = rvec[0], ry = rvec[1], rz = rvec[2];
+  const double theta = std::sqrt(rx * rx + ry * ry + rz * rz);
+  double R[9];
+  if (theta < 2.220446049250313e-16) {
+    for (int k = 0; k < 9; ++k) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
+  } else {
+    const double c = std::cos(theta), s = std::sin(theta), c1 = 1. - c;
+    const double it = theta ? 1. / theta : 0.;
+    rx *= it; ry *= it; rz *= it;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double rxm[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    for (int k = 0; k < 9; ++k) R[k] = c * I[k] + c1 * rrt[k] + s * rxm[k];
+  }
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) T[4 * r + c] = (float)R[3 * r + c];
+    T[4 * r + 3] = tvec[r];
+  }
+  T[12] = 0.f; T[13] = 0.f; T[14] = 0.f; T[15] = 1.f;
+}
+
+}  // extern "C"

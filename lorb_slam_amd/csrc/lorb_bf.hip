@@ -20,6 +20,8 @@
 //     the reference's minDist / max(2*minDist, 30) filter.
 #include "lorb_internal.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr uint32_t kIdxBits = 23;
@@ -61,21 +63,28 @@ __device__ __forceinline__ uint32_t hamming256(const uint4& a0, const uint4& a1,
   return d;
 }
 
-template <bool TOP2>
+// QPL = lane-side descriptors per thread (1 or 2): a block covers 256*QPL lane items; every
+// uniform descriptor loaded into SGPRs feeds QPL distance chains.
+template <bool TOP2, int QPL>
 __global__ __launch_bounds__(256) void k_bf_scan(const uint4* __restrict__ lane_desc,
                                                  const uint4* __restrict__ uni_desc,
                                                  const BfTile* __restrict__ tiles,
                                                  uint32_t* __restrict__ k1_out,
                                                  uint32_t* __restrict__ k2_out) {
   const BfTile tl = tiles[blockIdx.x];
-  const int l = threadIdx.x;
-  const bool active = l < tl.lane_count;
-  uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
-  if (active) {
-    a0 = lane_desc[2 * (size_t)(tl.lane_base + l)];
-    a1 = lane_desc[2 * (size_t)(tl.lane_base + l) + 1];
+  uint4 a[QPL][2];
+  uint32_t k1[QPL], k2[QPL];
+#pragma unroll
+  for (int r = 0; r < QPL; ++r) {
+    const int l = threadIdx.x + 256 * r;
+    a[r][0] = a[r][1] = make_uint4(0, 0, 0, 0);
+    if (l < tl.lane_count) {
+      a[r][0] = lane_desc[2 * (size_t)(tl.lane_base + l)];
+      a[r][1] = lane_desc[2 * (size_t)(tl.lane_base + l) + 1];
+    }
+    k1[r] = kSentinel;
+    k2[r] = kSentinel;
   }
-  uint32_t k1 = kSentinel, k2 = kSentinel;
   const uint4* __restrict__ u = uni_desc + 2 * (size_t)tl.uni_base;
   const uint32_t kb = (uint32_t)tl.uni_local0;
   const int n = tl.uni_count;
@@ -86,20 +95,30 @@ __global__ __launch_bounds__(256) void k_bf_scan(const uint4* __restrict__ lane_
     for (int s = 0; s < 8; ++s) b[s] = u[2 * j + s];  // 4 descriptors -> SGPRs (s_load) up front
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const uint32_t key = (hamming256(a0, a1, b[2 * s], b[2 * s + 1]) << kIdxBits) + kb + (uint32_t)(j + s);
-      if (TOP2) k2 = umed3(k1, key, k2);
-      k1 = min(k1, key);
+#pragma unroll
+      for (int r = 0; r < QPL; ++r) {
+        const uint32_t key = (hamming256(a[r][0], a[r][1], b[2 * s], b[2 * s + 1]) << kIdxBits) + kb + (uint32_t)(j + s);
+        if (TOP2) k2[r] = umed3(k1[r], key, k2[r]);
+        k1[r] = min(k1[r], key);
+      }
     }
   }
   for (; j < n; ++j) {
     const uint4 b0 = u[2 * j], b1 = u[2 * j + 1];
-    const uint32_t key = (hamming256(a0, a1, b0, b1) << kIdxBits) + kb + (uint32_t)j;
-    if (TOP2) k2 = umed3(k1, key, k2);
-    k1 = min(k1, key);
+#pragma unroll
+    for (int r = 0; r < QPL; ++r) {
+      const uint32_t key = (hamming256(a[r][0], a[r][1], b0, b1) << kIdxBits) + kb + (uint32_t)j;
+      if (TOP2) k2[r] = umed3(k1[r], key, k2[r]);
+      k1[r] = min(k1[r], key);
+    }
   }
-  if (active) {
-    k1_out[tl.out_base + l] = k1;
-    if (TOP2) k2_out[tl.out_base + l] = k2;
+#pragma unroll
+  for (int r = 0; r < QPL; ++r) {
+    const int l = threadIdx.x + 256 * r;
+    if (l < tl.lane_count) {
+      k1_out[tl.out_base + l] = k1[r];
+      if (TOP2) k2_out[tl.out_base + l] = k2[r];
+    }
   }
 }
 
@@ -233,7 +252,7 @@ __global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* _
 }
 
 // Host: tile table for "lanes = L side, uniform = U side" with a fixed number of U chunks.
-int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_off,
+int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_off, int lt,
                 std::vector<BfTile>& tiles, int* n_chunks_out) {
   const int64_t nl_total = l_off[np] - l_off[0];
   int64_t max_u = 0, lane_tiles = 0;
@@ -241,7 +260,7 @@ int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_of
     const int64_t nl = l_off[p + 1] - l_off[p], nu = u_off[p + 1] - u_off[p];
     if (nl < 0 || nu < 0) return lorb::set_error(ctx, LORB_E_INVALID, "offsets not monotone at problem %d", p);
     if (nu > (int64_t)kIdxMask) return lorb::set_error(ctx, LORB_E_INVALID, "problem %d: %lld uniform items > 2^23-1", p, (long long)nu);
-    if (nu > 0) lane_tiles += (nl + 255) / 256;
+    if (nu > 0) lane_tiles += (nl + lt - 1) / lt;
     max_u = std::max<int64_t>(max_u, nu);
   }
   // enough workgroups to fill 256 CUs x ~8, but keep >= 128 uniform items per chunk
@@ -258,10 +277,10 @@ int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_of
     if (nu == 0 || nl == 0) continue;
     for (int c = 0; c < n_chunks; c++) {
       const int a = (int)((int64_t)nu * c / n_chunks), b = (int)((int64_t)nu * (c + 1) / n_chunks);
-      for (int t = 0; t < nl; t += 256) {
+      for (int t = 0; t < nl; t += lt) {
         BfTile tl;
         tl.lane_base = l0 + t;
-        tl.lane_count = std::min(256, nl - t);
+        tl.lane_count = std::min(lt, nl - t);
         tl.uni_base = u0 + a;
         tl.uni_count = b - a;
         tl.uni_local0 = a;
@@ -280,7 +299,8 @@ int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, con
          const int32_t* u_off, uint32_t** k1_final, uint32_t** k2_final) {
   std::vector<BfTile> tiles;
   int n_chunks = 1;
-  LORB_TRY(build_tiles(ctx, np, l_off, u_off, tiles, &n_chunks));
+  static const int qpl = [] { const char* e = getenv("LORB_BF_QPL"); return (e && atoi(e) == 1) ? 1 : 2; }();
+  LORB_TRY(build_tiles(ctx, np, l_off, u_off, 256 * qpl, tiles, &n_chunks));
   const int nl = l_off[np] - l_off[0];
   BfTile* d_tiles = nullptr;
   uint32_t *k1 = nullptr, *k2 = nullptr, *m1 = nullptr, *m2 = nullptr;
@@ -289,9 +309,14 @@ int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, con
   if (!tiles.empty()) {
     LORB_TRY(lorb::upload_t(ctx, S_BF_TILES, tiles.data(), tiles.size(), &d_tiles));
     lorb::KernelTimer kt(ctx, TOP2 ? LORB_K_BF_SCAN_TOP2 : LORB_K_BF_SCAN_TOP1);
-    hipLaunchKernelGGL(k_bf_scan<TOP2>, dim3((unsigned)tiles.size()), dim3(256), 0, ctx->stream,
-                       reinterpret_cast<const uint4*>(d_lane), reinterpret_cast<const uint4*>(d_uni),
-                       d_tiles, k1, k2);
+    if (qpl == 2)
+      hipLaunchKernelGGL((k_bf_scan<TOP2, 2>), dim3((unsigned)tiles.size()), dim3(256), 0, ctx->stream,
+                         reinterpret_cast<const uint4*>(d_lane), reinterpret_cast<const uint4*>(d_uni),
+                         d_tiles, k1, k2);
+    else
+      hipLaunchKernelGGL((k_bf_scan<TOP2, 1>), dim3((unsigned)tiles.size()), dim3(256), 0, ctx->stream,
+                         reinterpret_cast<const uint4*>(d_lane), reinterpret_cast<const uint4*>(d_uni),
+                         d_tiles, k1, k2);
     LORB_CHECK_LAUNCH(ctx);
   }
   if (n_chunks > 1 && nl > 0) {

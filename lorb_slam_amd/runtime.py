@@ -162,3 +162,71 @@ class DeviceArray:
 
     def as_ptr(self, ctype):
         return C.cast(self.ptr, C.POINTER(ctype))
+
+
+# ---- bundle adjustment ---------------------------------------------------------------------
+def _ba_pose_only(self, pb, opt=None):
+    keep = A.KeepAlive()
+    s = A.make_pose_batch(pb, keep)
+    opt = opt or A.LMOptions.default()
+    nf = s.n_frames
+    pose = np.zeros((max(nf, 1), 6)); T = np.zeros((max(nf, 1), 4, 4), np.float32)
+    summ = (A.BASummary * max(1, nf))()
+    self.check(lib().lorb_ba_pose_only(self._p, C.byref(s), C.byref(opt), A.ptr(pose, C.c_double),
+                                       A.ptr(T, C.c_float), summ), "lorb_ba_pose_only")
+    return pose[:nf], T[:nf], [summ[i].as_dict() for i in range(nf)]
+
+
+def _ba_local(self, wins, opt=None):
+    keep = A.KeepAlive()
+    arr = A.make_windows(wins, keep)
+    opt = opt or A.LMOptions.default()
+    poses = [np.zeros((len(w["pose_init"]), 6)) for w in wins]
+    pts = [np.zeros((len(w["point_init"]), 3)) for w in wins]
+    pp = (A.f64p * max(1, len(wins)))(*[A.ptr(p, C.c_double) for p in poses])
+    qp = (A.f64p * max(1, len(wins)))(*[A.ptr(p, C.c_double) for p in pts])
+    summ = (A.BASummary * max(1, len(wins)))()
+    self.check(lib().lorb_ba_local(self._p, C.c_int32(len(wins)), arr, C.byref(opt), pp, qp, summ), "lorb_ba_local")
+    return poses, pts, [summ[i].as_dict() for i in range(len(wins))]
+
+
+class BAPlan:
+    """Device-resident plan (lorb_ba_plan_*): upload + Schur structure once, solve many times."""
+
+    def __init__(self, ctx, wins):
+        self.ctx = ctx
+        self.wins = wins
+        self._keep = A.KeepAlive()
+        arr = A.make_windows(wins, self._keep)
+        self._p = C.c_void_p()
+        ctx.check(lib().lorb_ba_plan_create(ctx.handle, C.c_int32(len(wins)), arr, C.byref(self._p)),
+                  "lorb_ba_plan_create")
+
+    def solve(self, opt=None):
+        opt = opt or A.LMOptions.default()
+        self.ctx.check(lib().lorb_ba_plan_solve(self._p, C.byref(opt)), "lorb_ba_plan_solve")
+
+    def read(self):
+        wins = self.wins
+        poses = [np.zeros((len(w["pose_init"]), 6)) for w in wins]
+        pts = [np.zeros((len(w["point_init"]), 3)) for w in wins]
+        pp = (A.f64p * max(1, len(wins)))(*[A.ptr(p, C.c_double) for p in poses])
+        qp = (A.f64p * max(1, len(wins)))(*[A.ptr(p, C.c_double) for p in pts])
+        summ = (A.BASummary * max(1, len(wins)))()
+        self.ctx.check(lib().lorb_ba_plan_read(self._p, pp, qp, summ), "lorb_ba_plan_read")
+        return poses, pts, [summ[i].as_dict() for i in range(len(wins))]
+
+    def close(self):
+        if self._p:
+            lib().lorb_ba_plan_destroy(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+Context.ba_pose_only = _ba_pose_only
+Context.ba_local = _ba_local

@@ -1,0 +1,107 @@
+"""GPU parity: bundle adjustment (liblorb.so) vs the oracle's Ceres-LM restatement.
+
+Tolerance (north_star): poses / points within 1e-5 relative.  Relative is taken per block
+against max(|oracle|, 1) for angle-axis / translation / point coordinates, i.e.
+|gpu - oracle| <= 1e-5 * max(|oracle|, 1)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from lorb_slam_amd import _abi as A
+from lorb_slam_amd import synth
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+
+
+def close(a, b, rtol=RTOL):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return np.all(np.abs(a - b) <= rtol * np.maximum(np.abs(b), 1.0))
+
+
+@pytest.mark.parametrize("quirk", [True, False])
+def test_pose_only_default_options(ctx, quirk):
+    pb = synth.pose_only_batch(seed=1, n_frames=16, n_res=200, quirk=quirk)
+    pg, Tg, sg = ctx.ba_pose_only(pb)
+    po, To, so = O.ba_pose_only(pb)
+    assert close(pg, po), np.abs(pg - po).max()
+    assert np.allclose(Tg, To, rtol=1e-5, atol=1e-6)
+    for a, b in zip(sg, so):
+        assert a["termination"] == b["termination"] and a["iterations"] == b["iterations"]
+        assert abs(a["final_cost"] - b["final_cost"]) <= 1e-6 * b["final_cost"]
+
+
+def test_pose_only_fixed_iterations_and_edge(ctx):
+    pb = synth.pose_only_batch(seed=4, n_frames=5, n_res=1500)
+    # frame with zero residuals (empty ceres::Problem leaves the pose untouched)
+    pb["res_off"][1:] -= 0
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    pg, _, sg = ctx.ba_pose_only(pb, opt)
+    po, _, so = O.ba_pose_only(pb, opt)
+    assert close(pg, po), np.abs(pg - po).max()
+    assert [s["iterations"] for s in sg] == [s["iterations"] for s in so]
+    empty = dict(res_off=np.array([0, 0], np.int32), intr=pb["intr"][:1], pose_init=pb["pose_init"][:1],
+                 pts3d=np.zeros((0, 3), np.float32), obs2d=np.zeros((0, 2), np.float32))
+    pg, _, _ = ctx.ba_pose_only(empty)
+    assert np.array_equal(pg[0], pb["pose_init"][0].astype(np.float64))
+
+
+def test_pose_only_identity_init_small_angle_branch(ctx):
+    pb = synth.pose_only_batch(seed=9, n_frames=3, n_res=300)
+    pb["pose_init"][:, :3] = 0.0  # theta^2 <= eps: first-order AngleAxisRotatePoint branch
+    pg, _, _ = ctx.ba_pose_only(pb)
+    po, _, _ = O.ba_pose_only(pb)
+    assert close(pg, po), np.abs(pg - po).max()
+
+
+@pytest.mark.parametrize("n_kf,n_pts,n_fixed", [(6, 300, 2), (20, 4000, 2)])
+def test_local_ba_default_options(ctx, n_kf, n_pts, n_fixed):
+    w = synth.ba_window(seed=3, n_kf=n_kf, n_pts=n_pts, n_fixed=n_fixed, fixed_obs_per_kf=max(60, n_pts // 10))
+    Pg, Xg, sg = ctx.ba_local([w])
+    Po, Xo, so = O.ba_local([w])
+    assert sg[0]["termination"] == so[0]["termination"], (sg, so)
+    assert sg[0]["iterations"] == so[0]["iterations"], (sg, so)
+    assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
+    assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
+    assert abs(sg[0]["final_cost"] - so[0]["final_cost"]) <= 1e-8 * so[0]["final_cost"]
+
+
+def test_local_ba_c3_ten_iterations(ctx):
+    """BASELINE config 2 shape: 20 KF / 4k points / 30k obs (+2 fixed KFs), exactly 10 LM its."""
+    w = synth.ba_window(seed=3, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400)
+    assert len(w["obs_point"]) == 30000 + 800
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    Pg, Xg, sg = ctx.ba_local([w], opt)
+    Po, Xo, so = O.ba_local([w], opt)
+    assert sg[0]["iterations"] == so[0]["iterations"] == 10
+    assert sg[0]["successful_steps"] == so[0]["successful_steps"]
+    assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
+    assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
+
+
+def test_local_ba_batched_ragged_windows(ctx):
+    wins = [synth.ba_window(seed=10 + i, n_kf=k, n_pts=p, n_fixed=nf, fixed_obs_per_kf=50)
+            for i, (k, p, nf) in enumerate([(3, 100, 1), (8, 700, 2), (12, 900, 3), (5, 257, 1)])]
+    # an unobserved point and an empty window
+    wins[1]["point_init"] = np.concatenate([wins[1]["point_init"], [[1.0, 2.0, 9.0]]]).astype(np.float32)
+    empty = dict(pose_init=np.zeros((2, 6), np.float32), fixed_pose=np.zeros((0, 6), np.float32),
+                 point_init=np.zeros((3, 3), np.float32), obs_point=np.zeros(0, np.int32),
+                 obs_frame=np.zeros(0, np.int32), obs_uv=np.zeros((0, 2), np.float32), intr=wins[0]["intr"])
+    wins.append(empty)
+    Pg, Xg, sg = ctx.ba_local(wins)
+    Po, Xo, so = O.ba_local(wins)
+    for i in range(len(wins)):
+        assert close(Pg[i], Po[i]), (i, np.abs(Pg[i] - Po[i]).max())
+        assert close(Xg[i], Xo[i]), (i, np.abs(Xg[i] - Xo[i]).max())
+    assert np.array_equal(Xg[1][-1], np.array([1.0, 2.0, 9.0]))
+    assert np.array_equal(Pg[-1], np.zeros((2, 6)))
+
+
+def test_plan_resolve_is_repeatable(ctx):
+    from lorb_slam_amd.runtime import BAPlan
+    w = synth.ba_window(seed=5, n_kf=10, n_pts=1000, n_fixed=2, fixed_obs_per_kf=100)
+    plan = BAPlan(ctx, [w])
+    plan.solve(); a = plan.read()
+    plan.solve(); b = plan.read()
+    assert np.array_equal(a[0][0], b[0][0]) and np.array_equal(a[1][0], b[1][0])
+    plan.close()
