@@ -25,16 +25,18 @@ namespace {
 using lorb::residual;
 using lorb::residual_jac;
 
-constexpr int kPB = 256;  // points per point-block (one thread per point)
+constexpr int kPB = 64;   // points per point-block (one thread per point, 1 wave)
+constexpr int kOB = 256;  // observations per obs-block (one thread per observation)
 
 struct BaWin {
   int pose_base, n_poses, point_base, n_points;
   int pblk_base, n_pblk;
-  int env_base, env_size, n, row_base;
+  int oblk_base, n_oblk;
+  int env_base, env_size, n, row_base, bw;  // S band: row i holds cols [i-bw, i]
   int obs_base, n_obs;
   double fx, fy, cx, cy;
 };
-struct PBlk { int win, p0, cnt; };
+struct PBlk { int win, p0, cnt; };   // also used for obs blocks (o0, cnt)
 struct BlockPair { int win, ch, cl, off, cnt; };  // global camera indices, pair list range
 struct WinState {
   double radius, decrease_factor, cost, x_norm, gmax, initial_cost;
@@ -110,6 +112,8 @@ __device__ __forceinline__ double s3(const double m[6], int a, int b) {
 struct BaDev {
   const BaWin* win;
   const PBlk* pblk;
+  const PBlk* oblk;
+  const int* obs_pt;         // K  (global point of each observation)
   const BlockPair* bp;
   const int2* pairs;
   const int* pt_obs_off;     // Ptot+1
@@ -119,9 +123,6 @@ struct BaDev {
   const int* cam_obs_off;    // Ctot+1
   const int* cam_obs;        // camera-major obs list
   const int* cam_win;        // Ctot
-  const int* row_first;      // per S row (window-local column index)
-  const int* row_off;        // per S row (offset in window env)
-  const int* col_last;       // per S column (window-local last row with first<=col)
   const double* fixed_pose;  // NF*6
   double* x_init_pose;       // Ctot*6 (initial values, never written)
   double* x_init_pt;         // Ptot*3
@@ -145,6 +146,7 @@ struct BaDev {
   double* rhs;               // sum n
   double* ycam;              // sum n (solution, scaled space, y = -step)
   double* part;              // n_pblk * 8 partials
+  double* opart;             // n_oblk * 4 partials
   WinState* st;
 };
 
@@ -165,49 +167,73 @@ __global__ void k_ba_init(BaDev d, int W, LMOpt o) {
   d.st[w] = s;
 }
 
-// K1: per-point linearisation (only windows that (re)linearise this iteration)
-__global__ __launch_bounds__(kPB) void k_ba_linearize(BaDev d) {
-  __shared__ double sh[3 * kPB];
+// K1: per-observation linearisation (windows that (re)linearise this iteration)
+__global__ __launch_bounds__(kOB) void k_ba_lin_obs(BaDev d) {
+  __shared__ double sh[kOB];
+  const PBlk ob = d.oblk[blockIdx.x];
+  const WinState& S = d.st[ob.win];
+  if (S.done || !S.relin) return;
+  const BaWin& W = d.win[ob.win];
+  const int cur = S.cur;
+  const int t = threadIdx.x;
+  double cost = 0.0;
+  if (t < ob.cnt) {
+    const int o = ob.p0 + t;
+    const int p = d.obs_pt[o];
+    const int c = d.obs_cam[o];
+    double X[3], pose[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) X[k] = d.x_pt[cur][3 * p + k];
+    if (c >= 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) pose[k] = d.x_pose[cur][6 * c + k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[o] + k];
+    }
+    const double2 uv = d.obs_uv[o];
+    double r[2], Jp[6], Jc[12];
+    residual_jac(pose, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
+    d.obs_r[2 * o] = r[0]; d.obs_r[2 * o + 1] = r[1];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d.obs_Jp[6 * o + k] = Jp[k];
+    if (c >= 0) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) d.obs_Jc[12 * o + k] = Jc[k];
+    }
+    cost = 0.5 * (r[0] * r[0] + r[1] * r[1]);
+  }
+  // deterministic block sum
+  sh[t] = cost;
+  __syncthreads();
+  for (int s = kOB / 2; s > 0; s >>= 1) {
+    if (t < s) sh[t] += sh[t + s];
+    __syncthreads();
+  }
+  if (t == 0) d.opart[4 * blockIdx.x] = sh[0];
+}
+
+// K1b: per-point E^T E, E^T r (unscaled), Jacobi scale (iteration 0), gradient / norm partials
+__global__ __launch_bounds__(kPB) void k_ba_lin_point(BaDev d) {
   const PBlk pb = d.pblk[blockIdx.x];
   const WinState& S = d.st[pb.win];
   if (S.done || !S.relin) return;
-  const BaWin& W = d.win[pb.win];
   const int cur = S.cur;
   const int t = threadIdx.x;
-  double cost = 0.0, gm = 0.0, xn2 = 0.0;
+  double gm = 0.0, xn2 = 0.0;
   if (t < pb.cnt) {
     const int p = pb.p0 + t;
-    double X[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) X[k] = d.x_pt[cur][3 * p + k];
     double E[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
     const int o0 = d.pt_obs_off[p], o1 = d.pt_obs_off[p + 1];
     for (int o = o0; o < o1; ++o) {
-      const int c = d.obs_cam[o];
-      double pose[6];
-      if (c >= 0) {
+      double Jp[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) pose[k] = d.x_pose[cur][6 * c + k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[o] + k];
-      }
-      const double2 uv = d.obs_uv[o];
-      double r[2], Jp[6], Jc[12];
-      residual_jac(pose, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
-      d.obs_r[2 * o] = r[0]; d.obs_r[2 * o + 1] = r[1];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) d.obs_Jp[6 * o + k] = Jp[k];
-      if (c >= 0) {
-#pragma unroll
-        for (int k = 0; k < 12; ++k) d.obs_Jc[12 * o + k] = Jc[k];
-      }
+      for (int k = 0; k < 6; ++k) Jp[k] = d.obs_Jp[6 * o + k];
+      const double r0 = d.obs_r[2 * o], r1 = d.obs_r[2 * o + 1];
       E[0] += Jp[0] * Jp[0] + Jp[3] * Jp[3]; E[1] += Jp[0] * Jp[1] + Jp[3] * Jp[4];
       E[2] += Jp[0] * Jp[2] + Jp[3] * Jp[5]; E[3] += Jp[1] * Jp[1] + Jp[4] * Jp[4];
       E[4] += Jp[1] * Jp[2] + Jp[4] * Jp[5]; E[5] += Jp[2] * Jp[2] + Jp[5] * Jp[5];
-      b[0] += Jp[0] * r[0] + Jp[3] * r[1]; b[1] += Jp[1] * r[0] + Jp[4] * r[1];
-      b[2] += Jp[2] * r[0] + Jp[5] * r[1];
-      cost += 0.5 * (r[0] * r[0] + r[1] * r[1]);
+      b[0] += Jp[0] * r0 + Jp[3] * r1; b[1] += Jp[1] * r0 + Jp[4] * r1; b[2] += Jp[2] * r0 + Jp[5] * r1;
     }
 #pragma unroll
     for (int k = 0; k < 6; ++k) d.ete[6 * p + k] = E[k];
@@ -221,27 +247,15 @@ __global__ __launch_bounds__(kPB) void k_ba_linearize(BaDev d) {
     if (o1 > o0) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        gm = fmax(gm, fabs(X[k] - (X[k] + -b[k])));
-        xn2 += X[k] * X[k];
+        const double X = d.x_pt[cur][3 * p + k];
+        gm = fmax(gm, fabs(X - (X + -b[k])));
+        xn2 += X * X;
       }
     }
   }
-  double v[3] = {cost, gm, xn2};
-  // gm is reduced with max: do it separately
-  sh[t] = gm;
-  __syncthreads();
-  for (int s = kPB / 2; s > 0; s >>= 1) {
-    if (t < s) sh[t] = fmax(sh[t], sh[t + s]);
-    __syncthreads();
-  }
-  const double gmax = sh[0];
-  __syncthreads();
-  double sv[2] = {v[0], v[2]};
-  block_sum<2>(sv, sh);
-  if (t == 0) {
-    double* P = d.part + 8 * blockIdx.x;
-    P[0] = sv[0]; P[1] = gmax; P[2] = sv[1];
-  }
+  gm = wave_max(gm);
+  xn2 = wave_sum(xn2);
+  if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[1] = gm; P[2] = xn2; }
 }
 
 // K2: per-camera normal blocks (one wavefront per optimised camera)
@@ -301,30 +315,32 @@ __global__ __launch_bounds__(64) void k_ba_camera(BaDev d) {
 // K3: per-window iteration head: finalise the (re)linearisation, termination checks
 __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
   const int w = blockIdx.x;
-  WinState S = d.st[w];
-  if (S.done) return;
+  const WinState* Sp = d.st + w;
+  if (Sp->done) return;
+  WinState S = *Sp;
   const BaWin W = d.win[w];
   const int lane = threadIdx.x;
   if (S.relin) {
+    // fixed lane assignment + fixed butterfly => deterministic
     double cost = 0.0, gm = 0.0, xn2 = 0.0;
-    if (lane == 0) {
-      for (int b = 0; b < W.n_pblk; ++b) {  // fixed order
-        const double* P = d.part + 8 * (W.pblk_base + b);
-        cost += P[0]; gm = fmax(gm, P[1]); xn2 += P[2];
-      }
-      const int cur = S.cur;
-      for (int c = W.pose_base; c < W.pose_base + W.n_poses; ++c) {
-        if (d.cam_obs_off[c + 1] == d.cam_obs_off[c]) continue;
-        gm = fmax(gm, d.cam_gmax[c]);
-        for (int k = 0; k < 6; ++k) { const double x = d.x_pose[cur][6 * c + k]; xn2 += x * x; }
-      }
-      S.cost = cost;
-      S.gmax = gm;
-      S.x_norm = sqrt(xn2);
-      if (S.iter == 0) S.initial_cost = cost;
-      S.last_successful = 1;
-      S.relin = 0;
+    for (int b = lane; b < W.n_oblk; b += 64) cost += d.opart[4 * (W.oblk_base + b)];
+    for (int b = lane; b < W.n_pblk; b += 64) {
+      const double* P = d.part + 8 * (W.pblk_base + b);
+      gm = fmax(gm, P[1]); xn2 += P[2];
     }
+    const int cur = S.cur;
+    for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64) {
+      if (d.cam_obs_off[c + 1] == d.cam_obs_off[c]) continue;
+      gm = fmax(gm, d.cam_gmax[c]);
+      for (int k = 0; k < 6; ++k) { const double x = d.x_pose[cur][6 * c + k]; xn2 += x * x; }
+    }
+    cost = wave_sum(cost); gm = wave_max(gm); xn2 = wave_sum(xn2);
+    S.cost = cost;
+    S.gmax = gm;
+    S.x_norm = sqrt(xn2);
+    if (S.iter == 0) S.initial_cost = cost;
+    S.last_successful = 1;
+    S.relin = 0;
   }
   if (lane == 0) {
     if (S.iter >= o.max_iter) { S.done = 1; S.term = LORB_TERM_NO_CONVERGENCE; }
@@ -388,17 +404,23 @@ __global__ __launch_bounds__(kPB) void k_ba_point_prep(BaDev d, LMOpt o) {
   }
 }
 
-// K5: reduced camera system S (envelope) + rhs: one wavefront per non-zero camera block pair
-__global__ __launch_bounds__(64) void k_ba_schur(BaDev d, LMOpt o) {
+__device__ __forceinline__ double& band(double* A, int bw, int i, int j) {
+  return A[(size_t)i * (bw + 1) + (j - i + bw)];
+}
+
+// K5: reduced camera system S (band storage) + rhs: one 256-thread workgroup per non-zero
+// camera block pair; lanes stride the pair list, fixed-order wave + LDS reduction.
+__global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
+  __shared__ double red[4][37];
   const BlockPair bp = d.bp[blockIdx.x];
   const WinState& S = d.st[bp.win];
   if (S.done) return;
   const BaWin& W = d.win[bp.win];
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   double acc[36];
 #pragma unroll
   for (int k = 0; k < 36; ++k) acc[k] = 0.0;
-  for (int q = bp.off + lane; q < bp.off + bp.cnt; q += 64) {
+  for (int q = bp.off + t; q < bp.off + bp.cnt; q += 256) {
     const int2 pr = d.pairs[q];  // (obs in camera ch, obs in camera cl) of one point
     double Y[18], Wl[18];
 #pragma unroll
@@ -409,120 +431,159 @@ __global__ __launch_bounds__(64) void k_ba_schur(BaDev d, LMOpt o) {
       for (int j = 0; j < 6; ++j)
         acc[6 * i + j] += Y[3 * i] * Wl[3 * j] + Y[3 * i + 1] * Wl[3 * j + 1] + Y[3 * i + 2] * Wl[3 * j + 2];
   }
-#pragma unroll
-  for (int k = 0; k < 36; ++k) acc[k] = wave_sum(acc[k]);
-  const int lh = bp.ch - W.pose_base, ll = bp.cl - W.pose_base;
-  double* env = d.env + W.env_base;
-  if (bp.ch == bp.cl) {
-    // diagonal block: U_s + D^2 - sum ; rhs = v_s - sum_obs rc
-    double r6[6] = {0, 0, 0, 0, 0, 0};
+  const bool diag = bp.ch == bp.cl;
+  double r6[6] = {0, 0, 0, 0, 0, 0};
+  if (diag) {
     const int a0 = d.cam_obs_off[bp.ch], a1 = d.cam_obs_off[bp.ch + 1];
-    for (int e = a0 + lane; e < a1; e += 64) {
+    for (int e = a0 + t; e < a1; e += 256) {
       const int ob = d.cam_obs[e];
 #pragma unroll
       for (int k = 0; k < 6; ++k) r6[k] += d.obs_rc[6 * ob + k];
     }
+  }
 #pragma unroll
-    for (int k = 0; k < 6; ++k) r6[k] = wave_sum(r6[k]);
-    if (lane < 36) {
-      const int i = lane / 6, j = lane % 6;
+  for (int k = 0; k < 36; ++k) {
+    const double v = wave_sum(acc[k]);
+    if (lane == 0) red[wv][k] = v;
+  }
+  __syncthreads();
+  if (t < 36) {
+    const double a = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    const int i = t / 6, j = t % 6;
+    const int lh = bp.ch - W.pose_base, ll = bp.cl - W.pose_base;
+    double* A = d.env + W.env_base;
+    if (diag) {
       if (j <= i) {
         const double* sc = d.scale_pose + 6 * bp.ch;
         double v = d.U[21 * bp.ch + u21(i, j)] * sc[i] * sc[j];
         if (i == j) v += fmin(fmax(v, o.min_diag), o.max_diag) / S.radius;
-        // select acc[lane] without dynamic register indexing
-        double a = 0.0;
-#pragma unroll
-        for (int k = 0; k < 36; ++k) a = (k == lane) ? acc[k] : a;
-        const int row = 6 * lh + i, col = 6 * lh + j;
-        env[d.row_off[W.row_base + row] + (col - d.row_first[W.row_base + row])] = v - a;
+        band(A, W.bw, 6 * lh + i, 6 * lh + j) = v - a;
       }
+    } else {
+      band(A, W.bw, 6 * lh + i, 6 * ll + j) = -a;
     }
-    if (lane < 6) {
-      double r = 0.0;
+  }
+  if (diag) {
+    __syncthreads();
 #pragma unroll
-      for (int k = 0; k < 6; ++k) r = (k == lane) ? r6[k] : r;
-      const double vs = d.V[6 * bp.ch + lane] * d.scale_pose[6 * bp.ch + lane];
-      d.rhs[W.row_base + 6 * lh + lane] = vs - r;
+    for (int k = 0; k < 6; ++k) {
+      const double v = wave_sum(r6[k]);
+      if (lane == 0) red[wv][k] = v;
     }
-  } else {
-    if (lane < 36) {
-      const int i = lane / 6, j = lane % 6;
-      double a = 0.0;
-#pragma unroll
-      for (int k = 0; k < 36; ++k) a = (k == lane) ? acc[k] : a;
-      const int row = 6 * lh + i, col = 6 * ll + j;
-      env[d.row_off[W.row_base + row] + (col - d.row_first[W.row_base + row])] = -a;
+    __syncthreads();
+    if (t < 6) {
+      const double r = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+      const double vs = d.V[6 * bp.ch + t] * d.scale_pose[6 * bp.ch + t];
+      d.rhs[W.row_base + 6 * (bp.ch - W.pose_base) + t] = vs - r;
     }
   }
 }
 
-// K6: envelope Cholesky of S + forward/back substitution, one workgroup per window.
-// Elements (i, j), first[i] <= j <= i, stored row-wise at row_off[i] + j - first[i].
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ double rsqrt_refined(double a) {
+  double y = __builtin_amdgcn_rsq(a);
+  double e = fma(-a * y, y, 1.0);
+  y = fma(0.5 * y, e, y);
+  e = fma(-a * y, y, 1.0);
+  y = fma(0.5 * y, e, y);
+  return y;
+}
+
+// K6: banded Cholesky of S + forward/back substitution; one 256-thread workgroup per window.
+// Right-looking, panel width NB: wave 0 factors the panel (wave-synchronous, rsqrt-refined,
+// no IEEE div/sqrt on the critical path) and runs the fused forward substitution; all four
+// waves apply the rank-NB trailing update.  Band stays in LDS when it fits.
+constexpr int NB = 16;
 template <bool IN_LDS>
-__global__ __launch_bounds__(256) void k_ba_chol(BaDev d, int lds_doubles) {
+__global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int s_fail;
   const int w = blockIdx.x;
   if (d.st[w].done) return;
   const BaWin W = d.win[w];
-  const int n = W.n;
-  const int t = threadIdx.x;
-  const int* first = d.row_first + W.row_base;
-  const int* roff = d.row_off + W.row_base;
-  const int* last = d.col_last + W.row_base;
-  double* A;
-  double* z;
+  const int n = W.n, bw = W.bw;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double *A, *z, *invd;
   if (IN_LDS) {
     A = smem;
-    z = smem + W.env_size;
-    for (int k = t; k < W.env_size; k += 256) A[k] = d.env[W.env_base + k];
+    z = smem + (size_t)n * (bw + 1);
+    invd = z + n;
+    const double* src = d.env + W.env_base;
+    for (int k = t; k < n * (bw + 1); k += 256) A[k] = src[k];
     for (int k = t; k < n; k += 256) z[k] = d.rhs[W.row_base + k];
   } else {
     A = d.env + W.env_base;
     z = d.rhs + W.row_base;
+    invd = d.ycam + W.row_base;  // scratch, overwritten with the solution at the end
   }
+  if (t == 0) s_fail = 0;
   __syncthreads();
-  bool failed = false;
-  for (int k = 0; k < n; ++k) {
-    const double akk = A[roff[k] + (k - first[k])];
-    if (!(akk > 0.0)) { failed = true; break; }  // every thread reads the same value
-    const double lkk = sqrt(akk);
-    const int lk = last[k];
-    for (int i = k + 1 + t; i <= lk; i += 256)
-      if (first[i] <= k) A[roff[i] + (k - first[i])] /= lkk;
-    if (t == 0) { A[roff[k] + (k - first[k])] = lkk; z[k] /= lkk; }
-    __syncthreads();
-    const int m = lk - k;
-    const double zk = z[k];
-    for (int e = t; e < m * m; e += 256) {
-      const int ii = e / m, jj = e - ii * m;
-      if (jj > ii) continue;
-      const int i = k + 1 + ii, j = k + 1 + jj;
-      const int fi = first[i], fj = first[j];
-      if (fi > k || fj > k) continue;
-      A[roff[i] + (j - fi)] -= A[roff[i] + (k - fi)] * A[roff[j] + (k - fj)];
+  for (int kb = 0; kb < n; kb += NB) {
+    const int ke = min(kb + NB, n);
+    if (wv == 0) {
+      bool bad = false;
+      for (int k = kb; k < ke; ++k) {
+        const double akk = band(A, bw, k, k);
+        if (!(akk > 0.0)) { bad = true; break; }
+        const double y = rsqrt_refined(akk);
+        const int ie = min(n - 1, k + bw);
+        for (int i = k + 1 + lane; i <= ie; i += 64) band(A, bw, i, k) *= y;
+        if (lane == 0) { band(A, bw, k, k) = akk * y; invd[k] = y; z[k] *= y; }
+        wave_sync_lds();
+        const double zk = z[k];
+        // rank-1 update of the rest of the panel + fused forward substitution
+        for (int i = k + 1 + lane; i <= ie; i += 64) {
+          const double lik = band(A, bw, i, k);
+          const int je = min(ke - 1, i);
+          for (int j = k + 1; j <= je; ++j) band(A, bw, i, j) -= lik * band(A, bw, j, k);
+          z[i] -= lik * zk;
+        }
+        wave_sync_lds();
+      }
+      if (bad && lane == 0) s_fail = 1;
     }
-    for (int i = k + 1 + t; i <= lk; i += 256)
-      if (first[i] <= k) z[i] -= A[roff[i] + (k - first[i])] * zk;
+    __syncthreads();
+    if (s_fail) break;
+    // trailing update: rows i, cols j in [ke, min(n-1, ke-1+bw)], j <= i, k in [max(kb, i-bw), ke)
+    const int re = min(n - 1, ke - 1 + bw);
+    for (int i = ke + (t >> 2); i <= re; i += 64) {
+      const int k0 = max(kb, i - bw);
+      double li[NB];
+#pragma unroll
+      for (int q = 0; q < NB; ++q) li[q] = (kb + q >= k0 && kb + q < ke) ? band(A, bw, i, kb + q) : 0.0;
+      for (int j = ke + (t & 3); j <= i; j += 4) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q)
+          if (kb + q >= k0 && kb + q < ke) acc += li[q] * band(A, bw, j, kb + q);
+        band(A, bw, i, j) -= acc;
+      }
+    }
     __syncthreads();
   }
-  if (failed) {
+  if (s_fail) {
     if (t == 0) d.st[w].chol_fail = 1;
     return;
   }
-  for (int k = n - 1; k >= 0; --k) {
-    const double yk = z[k] / A[roff[k] + (k - first[k])];
-    const int fk = first[k];
-    for (int i = fk + t; i < k; i += 256) z[i] -= A[roff[k] + (i - fk)] * yk;
-    if (t == 0) z[k] = yk;
-    __syncthreads();
+  // back substitution L^T y = z (wave 0)
+  if (wv == 0) {
+    for (int k = n - 1; k >= 0; --k) {
+      const double yk = z[k] * invd[k];
+      for (int i = max(0, k - bw) + lane; i < k; i += 64) z[i] -= band(A, bw, k, i) * yk;
+      if (lane == 0) z[k] = yk;
+      wave_sync_lds();
+    }
   }
+  __syncthreads();
   for (int k = t; k < n; k += 256) d.ycam[W.row_base + k] = z[k];
 }
 
 // K7: per-point back-substitution, candidate point, model cost change and candidate cost
 __global__ __launch_bounds__(kPB) void k_ba_backsub(BaDev d) {
-  __shared__ double sh[3 * kPB];
   const PBlk pb = d.pblk[blockIdx.x];
   const WinState& S = d.st[pb.win];
   if (S.done || S.chol_fail) return;
@@ -600,30 +661,30 @@ __global__ __launch_bounds__(kPB) void k_ba_backsub(BaDev d) {
       ncost += 0.5 * (rn[0] * rn[0] + rn[1] * rn[1]);
     }
   }
-  double v[3] = {mcc, ncost, sn2};
-  block_sum<3>(v, sh);
+  mcc = wave_sum(mcc); ncost = wave_sum(ncost); sn2 = wave_sum(sn2);
   if (t == 0) {
     double* P = d.part + 8 * blockIdx.x;
-    P[3] = v[0]; P[4] = v[1]; P[5] = v[2];
+    P[3] = mcc; P[4] = ncost; P[5] = sn2;
   }
 }
 
 // K8: per-window iteration tail: camera candidate, step validity, tolerances, accept/reject
 __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
   const int w = blockIdx.x;
-  if (threadIdx.x != 0) return;
-  WinState S = d.st[w];
-  if (S.done) return;
+  const WinState* Sp = d.st + w;
+  if (Sp->done) return;
+  WinState S = *Sp;
   const BaWin W = d.win[w];
+  const int lane = threadIdx.x;
   bool valid = !S.chol_fail;
   double mccs = 0.0, ncost = 0.0, sn2 = 0.0;
   if (valid) {
-    for (int b = 0; b < W.n_pblk; ++b) {
+    for (int b = lane; b < W.n_pblk; b += 64) {
       const double* P = d.part + 8 * (W.pblk_base + b);
       mccs += P[3]; ncost += P[4]; sn2 += P[5];
     }
     const int cur = S.cur;
-    for (int c = W.pose_base; c < W.pose_base + W.n_poses; ++c) {
+    for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64) {
       const bool active = d.cam_obs_off[c + 1] > d.cam_obs_off[c];
       const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
       for (int k = 0; k < 6; ++k) {
@@ -633,7 +694,9 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
         if (active) sn2 += (x - xn) * (x - xn);
       }
     }
+    mccs = wave_sum(mccs); ncost = wave_sum(ncost); sn2 = wave_sum(sn2);
   }
+  if (lane != 0) return;
   const double model_cost_change = -mccs;
   valid = valid && isfinite(model_cost_change) && isfinite(sn2) && model_cost_change > 0.0;
   if (!valid) {
@@ -866,7 +929,7 @@ LMOpt to_dev_opt(const lorb_lm_options* o) {
 // ------------------------------------------------------------------------------------------
 struct lorb_ba_plan {
   lorb_ctx* ctx = nullptr;
-  int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_bp = 0, n_pairs = 0;
+  int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_oblk = 0, n_bp = 0, n_pairs = 0;
   int env_total = 0, n_total = 0, max_env = 0;
   std::vector<BaWin> hwin;
   std::vector<void*> allocs;
@@ -905,13 +968,13 @@ int dupload(lorb_ba_plan* P, const std::vector<T>& v, T** out) {
 int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P) {
   P->ctx = ctx;
   P->W = nw;
-  std::vector<int> pt_obs_off(1, 0), obs_cam, obs_fix, cam_obs_off(1, 0), cam_obs, cam_win;
+  std::vector<int> pt_obs_off(1, 0), obs_cam, obs_fix, obs_pt, cam_obs_off(1, 0), cam_obs, cam_win;
+  std::vector<PBlk> oblk;
   std::vector<double2> obs_uv;
   std::vector<double> fixed, xpose, xpt;
   std::vector<PBlk> pblk;
   std::vector<BlockPair> bps;
   std::vector<int2> pairs;
-  std::vector<int> row_first, row_off, col_last;
   int pose_base = 0, point_base = 0, fix_base = 0, env_base = 0, row_base = 0;
   for (int w = 0; w < nw; ++w) {
     const lorb_ba_window& in = win[w];
@@ -938,6 +1001,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     for (int e = 0; e < in.n_obs; ++e) {
       const int k = order[e], f = in.obs_frame[k];
       obs_cam.push_back(f >= 0 ? pose_base + f : -1);
+      obs_pt.push_back(point_base + in.obs_point[k]);
       obs_fix.push_back(f >= 0 ? -1 : fix_base + (-1 - f));
       obs_uv.push_back(make_double2(in.obs_uv[2 * k], in.obs_uv[2 * k + 1]));
     }
@@ -977,26 +1041,18 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
       pairs.insert(pairs.end(), kv.second.begin(), kv.second.end());
       bps.push_back(b);
     }
-    // envelope rows
+    // uniform band of S: bw = max_i (i - first_nonzero_col(i)); exact for Cholesky (no fill
+    // outside the envelope, and the zero padding never changes a value)
     const int n = 6 * in.n_poses;
-    int off = 0;
-    std::vector<int> rf(n);
-    for (int c = 0; c < in.n_poses; ++c)
-      for (int a = 0; a < 6; ++a) {
-        const int i = 6 * c + a;
-        rf[i] = 6 * fc[c];
-        row_first.push_back(rf[i]);
-        row_off.push_back(off);
-        off += i - rf[i] + 1;
-      }
-    for (int k = 0; k < n; ++k) {
-      int lk = k;
-      for (int i = k + 1; i < n; ++i) if (rf[i] <= k) lk = i;
-      col_last.push_back(lk);
-    }
-    bw.env_base = env_base; bw.env_size = off; bw.n = n; bw.row_base = row_base;
-    P->max_env = std::max(P->max_env, off + n);
-    env_base += off; row_base += n;
+    int bwid = 0;
+    for (int c = 0; c < in.n_poses; ++c) bwid = std::max(bwid, 6 * c + 5 - 6 * fc[c]);
+    if (n == 0) bwid = 0;
+    bw.env_base = env_base; bw.env_size = n * (bwid + 1); bw.n = n; bw.row_base = row_base; bw.bw = bwid;
+    P->max_env = std::max(P->max_env, bw.env_size + 2 * n);
+    env_base += bw.env_size; row_base += n;
+    bw.oblk_base = (int)oblk.size();
+    for (int o0 = 0; o0 < in.n_obs; o0 += kOB) oblk.push_back({w, bw.obs_base + o0, std::min(kOB, in.n_obs - o0)});
+    bw.n_oblk = (int)oblk.size() - bw.oblk_base;
     // point blocks
     bw.pblk_base = (int)pblk.size();
     for (int p0 = 0; p0 < in.n_points; p0 += kPB) pblk.push_back({w, point_base + p0, std::min(kPB, in.n_points - p0)});
@@ -1005,14 +1061,17 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     pose_base += in.n_poses; point_base += in.n_points; fix_base += in.n_fixed;
   }
   P->Ctot = pose_base; P->Ptot = point_base; P->K = (int)obs_cam.size(); P->NF = fix_base;
-  P->n_pblk = (int)pblk.size(); P->n_bp = (int)bps.size(); P->n_pairs = (int)pairs.size();
+  P->n_pblk = (int)pblk.size(); P->n_oblk = (int)oblk.size(); P->n_bp = (int)bps.size(); P->n_pairs = (int)pairs.size();
   P->env_total = env_base; P->n_total = row_base;
   BaDev& d = P->dev;
   BaWin* dwin; PBlk* dpb; BlockPair* dbp; int2* dpairs; double2* duv;
-  int *a1, *a2, *a3, *a4, *a5, *a6, *a7, *a8, *a9;
+  int *a1, *a2, *a3, *a4, *a5, *a6;
   double* dfix;
   LORB_TRY(dupload(P, P->hwin, &dwin)); d.win = dwin;
   LORB_TRY(dupload(P, pblk, &dpb)); d.pblk = dpb;
+  PBlk* dob; int* dopt;
+  LORB_TRY(dupload(P, oblk, &dob)); d.oblk = dob;
+  LORB_TRY(dupload(P, obs_pt, &dopt)); d.obs_pt = dopt;
   LORB_TRY(dupload(P, bps, &dbp)); d.bp = dbp;
   LORB_TRY(dupload(P, pairs, &dpairs)); d.pairs = dpairs;
   LORB_TRY(dupload(P, pt_obs_off, &a1)); d.pt_obs_off = a1;
@@ -1022,9 +1081,6 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   LORB_TRY(dupload(P, cam_obs_off, &a4)); d.cam_obs_off = a4;
   LORB_TRY(dupload(P, cam_obs, &a5)); d.cam_obs = a5;
   LORB_TRY(dupload(P, cam_win, &a6)); d.cam_win = a6;
-  LORB_TRY(dupload(P, row_first, &a7)); d.row_first = a7;
-  LORB_TRY(dupload(P, row_off, &a8)); d.row_off = a8;
-  LORB_TRY(dupload(P, col_last, &a9)); d.col_last = a9;
   LORB_TRY(dupload(P, fixed, &dfix)); d.fixed_pose = dfix;
   LORB_TRY(dupload(P, xpose, &d.x_init_pose));
   LORB_TRY(dupload(P, xpt, &d.x_init_pt));
@@ -1040,35 +1096,47 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   LORB_TRY(dalloc(P, K * 18, &d.obs_W)); LORB_TRY(dalloc(P, K * 18, &d.obs_Y)); LORB_TRY(dalloc(P, K * 6, &d.obs_rc));
   LORB_TRY(dalloc(P, (size_t)P->env_total, &d.env)); LORB_TRY(dalloc(P, (size_t)P->n_total, &d.rhs));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
+  LORB_TRY(dalloc(P, (size_t)P->n_oblk * 4, &d.opart));
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
   if (!obs_cam.empty()) { /* keep obs arrays alive via allocs */ }
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return LORB_OK;
 }
 
-constexpr int kLdsBudget = 160 * 1024 - 1024;
+constexpr int kLdsBudget = 160 * 1024 - 2048;
 
 // one LM iteration (K1..K8) on the ctx stream
+void enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
+  hipStream_t s = P->ctx->stream;
+  const BaDev& d = P->dev;
+  if (P->n_oblk) {
+    lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
+    hipLaunchKernelGGL(k_ba_lin_obs, dim3(P->n_oblk), dim3(kOB), 0, s, d);
+  }
+  if (P->n_pblk) hipLaunchKernelGGL(k_ba_lin_point, dim3(P->n_pblk), dim3(kPB), 0, s, d);
+  if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(64), 0, s, d);
+  hipLaunchKernelGGL(k_ba_lm_begin, dim3(P->W), dim3(64), 0, s, d, o);
+}
+
+// one LM iteration on the ctx stream
 int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   lorb_ctx* ctx = P->ctx;
   hipStream_t s = ctx->stream;
   const BaDev& d = P->dev;
-  if (P->n_pblk) hipLaunchKernelGGL(k_ba_linearize, dim3(P->n_pblk), dim3(kPB), 0, s, d);
-  if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(64), 0, s, d);
-  hipLaunchKernelGGL(k_ba_lm_begin, dim3(P->W), dim3(64), 0, s, d, o);
+  enqueue_linearize(P, o);
   if (P->n_pblk) hipLaunchKernelGGL(k_ba_point_prep, dim3(P->n_pblk), dim3(kPB), 0, s, d, o);
   if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   if (P->n_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
-    hipLaunchKernelGGL(k_ba_schur, dim3(P->n_bp), dim3(64), 0, s, d, o);
+    hipLaunchKernelGGL(k_ba_schur, dim3(P->n_bp), dim3(256), 0, s, d, o);
   }
   if (P->Ctot) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
     const size_t lds = sizeof(double) * (size_t)P->max_env;
     if (lds <= (size_t)kLdsBudget)
-      hipLaunchKernelGGL(k_ba_chol<true>, dim3(P->W), dim3(256), lds, s, d, P->max_env);
+      hipLaunchKernelGGL(k_ba_chol<true>, dim3(P->W), dim3(256), lds, s, d);
     else
-      hipLaunchKernelGGL(k_ba_chol<false>, dim3(P->W), dim3(256), 0, s, d, 0);
+      hipLaunchKernelGGL(k_ba_chol<false>, dim3(P->W), dim3(256), 0, s, d);
   }
   if (P->n_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->n_pblk), dim3(kPB), 0, s, d);
   hipLaunchKernelGGL(k_ba_lm_end, dim3(P->W), dim3(64), 0, s, d, o);
@@ -1077,13 +1145,8 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
 }
 
 int enqueue_finalize(lorb_ba_plan* P, const LMOpt& o) {
-  lorb_ctx* ctx = P->ctx;
-  hipStream_t s = ctx->stream;
-  const BaDev& d = P->dev;
-  if (P->n_pblk) hipLaunchKernelGGL(k_ba_linearize, dim3(P->n_pblk), dim3(kPB), 0, s, d);
-  if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(64), 0, s, d);
-  hipLaunchKernelGGL(k_ba_lm_begin, dim3(P->W), dim3(64), 0, s, d, o);
-  LORB_CHECK_LAUNCH(ctx);
+  enqueue_linearize(P, o);
+  LORB_CHECK_LAUNCH(P->ctx);
   return LORB_OK;
 }
 
