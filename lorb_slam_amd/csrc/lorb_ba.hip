@@ -493,12 +493,21 @@ __device__ __forceinline__ double rsqrt_refined(double a) {
   return y;
 }
 
+// broadcast lane `l` (wave-uniform) of a double through two v_readlane_b32
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffu), l);
+  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
 // K6: banded Cholesky of S + forward/back substitution; one 256-thread workgroup per window.
-// Right-looking, panel width NB: wave 0 factors the panel (wave-synchronous, rsqrt-refined,
-// no IEEE div/sqrt on the critical path) and runs the fused forward substitution; all four
-// waves apply the rank-NB trailing update.  Band stays in LDS when it fits.
+// Right-looking with panel width NB.  Wave 0 factors the panel entirely in registers (lane l
+// owns panel rows kb+l+64r, r < RPL; the pivot column is broadcast with v_readlane), with the
+// forward substitution fused in; rsqrt-refined pivots keep IEEE div/sqrt off the critical
+// path.  All four waves then apply the rank-NB trailing update from LDS.
 constexpr int NB = 16;
-template <bool IN_LDS>
+template <bool IN_LDS, int RPL>
 __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_fail;
@@ -524,33 +533,72 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   __syncthreads();
   for (int kb = 0; kb < n; kb += NB) {
     const int ke = min(kb + NB, n);
+    const int rlast = min(n - 1, ke - 1 + bw);
     if (wv == 0) {
-      bool bad = false;
-      for (int k = kb; k < ke; ++k) {
-        const double akk = band(A, bw, k, k);
-        if (!(akk > 0.0)) { bad = true; break; }
-        const double y = rsqrt_refined(akk);
-        const int ie = min(n - 1, k + bw);
-        for (int i = k + 1 + lane; i <= ie; i += 64) band(A, bw, i, k) *= y;
-        if (lane == 0) { band(A, bw, k, k) = akk * y; invd[k] = y; z[k] *= y; }
-        wave_sync_lds();
-        const double zk = z[k];
-        // rank-1 update of the rest of the panel + fused forward substitution
-        for (int i = k + 1 + lane; i <= ie; i += 64) {
-          const double lik = band(A, bw, i, k);
-          const int je = min(ke - 1, i);
-          for (int j = k + 1; j <= je; ++j) band(A, bw, i, j) -= lik * band(A, bw, j, k);
-          z[i] -= lik * zk;
+      double P[RPL][NB], zr[RPL];
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        const int row = kb + lane + 64 * r;
+        const bool vr = row <= rlast;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          const int col = kb + q;
+          P[r][q] = (vr && col < ke && col <= row && row - col <= bw) ? band(A, bw, row, col) : 0.0;
         }
-        wave_sync_lds();
+        zr[r] = vr ? z[row] : 0.0;
+      }
+      bool bad = false;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int k = kb + q;
+        if (k < ke && !bad) {
+          const double akk = readlane_d(P[0][q], q);
+          if (!(akk > 0.0)) {
+            bad = true;
+          } else {
+            const double y = rsqrt_refined(akk);
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) {
+              const int row = kb + lane + 64 * r;
+              if (row > k) P[r][q] *= y;
+            }
+            if (lane == q) { P[0][q] = akk * y; zr[0] *= y; invd[k] = y; }
+            const double zk = readlane_d(zr[0], q);
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) {
+              const int row = kb + lane + 64 * r;
+              if (row > k) zr[r] -= P[r][q] * zk;
+            }
+#pragma unroll
+            for (int q2 = q + 1; q2 < NB; ++q2) {
+              const double l = readlane_d(P[0][q], q2);  // L(kb+q2, k)
+#pragma unroll
+              for (int r = 0; r < RPL; ++r) {
+                const int row = kb + lane + 64 * r;
+                if (row >= kb + q2) P[r][q2] -= P[r][q] * l;
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        const int row = kb + lane + 64 * r;
+        if (row <= rlast) {
+#pragma unroll
+          for (int q = 0; q < NB; ++q) {
+            const int col = kb + q;
+            if (col < ke && col <= row && row - col <= bw) band(A, bw, row, col) = P[r][q];
+          }
+          z[row] = zr[r];
+        }
       }
       if (bad && lane == 0) s_fail = 1;
     }
     __syncthreads();
     if (s_fail) break;
-    // trailing update: rows i, cols j in [ke, min(n-1, ke-1+bw)], j <= i, k in [max(kb, i-bw), ke)
-    const int re = min(n - 1, ke - 1 + bw);
-    for (int i = ke + (t >> 2); i <= re; i += 64) {
+    // trailing update: rows i, cols j in [ke, rlast], j <= i, k in [max(kb, i-bw), ke)
+    for (int i = ke + (t >> 2); i <= rlast; i += 64) {
       const int k0 = max(kb, i - bw);
       double li[NB];
 #pragma unroll
@@ -569,12 +617,27 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
     if (t == 0) d.st[w].chol_fail = 1;
     return;
   }
-  // back substitution L^T y = z (wave 0)
+  // back substitution L^T y = z, 64-row register blocks from the bottom (wave 0)
   if (wv == 0) {
-    for (int k = n - 1; k >= 0; --k) {
-      const double yk = z[k] * invd[k];
-      for (int i = max(0, k - bw) + lane; i < k; i += 64) z[i] -= band(A, bw, k, i) * yk;
-      if (lane == 0) z[k] = yk;
+    for (int bb = ((n - 1) / 64) * 64; bb >= 0; bb -= 64) {
+      const int row = bb + lane;
+      const int be = min(n - 1, bb + 63);
+      double zr = row < n ? z[row] : 0.0;
+      for (int k = be; k >= bb; --k) {
+        const double lk = (row < k && k - row <= bw) ? band(A, bw, k, row) : 0.0;
+        const double yk = readlane_d(zr, k - bb) * invd[k];
+        if (lane == k - bb) zr = yk;
+        if (row < k) zr -= lk * yk;
+      }
+      if (row < n) z[row] = zr;
+      wave_sync_lds();
+      // rows above the block: z_i -= sum_k L(k, i) y_k, k in [bb, be], k - i <= bw
+      for (int i = max(0, bb - bw) + lane; i < bb; i += 64) {
+        double acc = 0.0;
+        const int kend = min(be, i + bw);
+        for (int k = bb; k <= kend; ++k) acc += band(A, bw, k, i) * z[k];
+        z[i] -= acc;
+      }
       wave_sync_lds();
     }
   }
@@ -930,7 +993,7 @@ LMOpt to_dev_opt(const lorb_lm_options* o) {
 struct lorb_ba_plan {
   lorb_ctx* ctx = nullptr;
   int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_oblk = 0, n_bp = 0, n_pairs = 0;
-  int env_total = 0, n_total = 0, max_env = 0;
+  int env_total = 0, n_total = 0, max_env = 0, max_bw = 0;
   std::vector<BaWin> hwin;
   std::vector<void*> allocs;
   BaDev dev{};
@@ -1049,6 +1112,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     if (n == 0) bwid = 0;
     bw.env_base = env_base; bw.env_size = n * (bwid + 1); bw.n = n; bw.row_base = row_base; bw.bw = bwid;
     P->max_env = std::max(P->max_env, bw.env_size + 2 * n);
+    P->max_bw = std::max(P->max_bw, bwid);
     env_base += bw.env_size; row_base += n;
     bw.oblk_base = (int)oblk.size();
     for (int o0 = 0; o0 < in.n_obs; o0 += kOB) oblk.push_back({w, bw.obs_base + o0, std::min(kOB, in.n_obs - o0)});
@@ -1133,10 +1197,13 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   if (P->Ctot) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
     const size_t lds = sizeof(double) * (size_t)P->max_env;
-    if (lds <= (size_t)kLdsBudget)
-      hipLaunchKernelGGL(k_ba_chol<true>, dim3(P->W), dim3(256), lds, s, d);
-    else
-      hipLaunchKernelGGL(k_ba_chol<false>, dim3(P->W), dim3(256), 0, s, d);
+    const bool in_lds = lds <= (size_t)kLdsBudget;
+    const int rows = NB + P->max_bw;  // panel rows held in registers by wave 0
+    const int rpl = rows <= 64 ? 1 : rows <= 128 ? 2 : rows <= 256 ? 4 : 8;
+#define LORB_CHOL(L, R) hipLaunchKernelGGL((k_ba_chol<L, R>), dim3(P->W), dim3(256), L ? lds : 0, s, d)
+    if (in_lds) { if (rpl == 1) LORB_CHOL(true, 1); else if (rpl == 2) LORB_CHOL(true, 2); else if (rpl == 4) LORB_CHOL(true, 4); else LORB_CHOL(true, 8); }
+    else { if (rpl == 1) LORB_CHOL(false, 1); else if (rpl == 2) LORB_CHOL(false, 2); else if (rpl == 4) LORB_CHOL(false, 4); else LORB_CHOL(false, 8); }
+#undef LORB_CHOL
   }
   if (P->n_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->n_pblk), dim3(kPB), 0, s, d);
   hipLaunchKernelGGL(k_ba_lm_end, dim3(P->W), dim3(64), 0, s, d, o);

@@ -106,3 +106,16 @@ def test_plan_resolve_is_repeatable(ctx):
     plan.solve(); b = plan.read()
     assert np.array_equal(a[0][0], b[0][0]) and np.array_equal(a[1][0], b[1][0])
     plan.close()
+
+
+@pytest.mark.parametrize("n_kf,n_pts", [(10, 300), (30, 400), (54, 300)])
+def test_local_ba_dense_covisibility(ctx, n_kf, n_pts):
+    """Every point seen by every window KF: S is fully dense (band = n-1).  Covers the
+    multi-row-per-lane register panel and the global-memory (band > LDS) Cholesky path."""
+    w = synth.ba_window(seed=21, n_kf=n_kf, n_pts=n_pts, n_fixed=1, fixed_obs_per_kf=50, obs_lens=(n_kf,))
+    opt = A.LMOptions.default(max_num_iterations=6)
+    Pg, Xg, sg = ctx.ba_local([w], opt)
+    Po, Xo, so = O.ba_local([w], opt)
+    assert sg[0]["iterations"] == so[0]["iterations"]
+    assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
+    assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
