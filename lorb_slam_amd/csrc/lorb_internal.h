@@ -19,7 +19,7 @@ struct lorb_ctx {
   std::string err;
   hipEvent_t ev[64] = {};
   // grow-only device scratch buffers, one per slot
-  static constexpr int kScratch = 24;
+  static constexpr int kScratch = 48;
   void* scratch[kScratch] = {};
   size_t scratch_sz[kScratch] = {};
   // per-kernel event timing
@@ -88,5 +88,7 @@ inline unsigned ceil_div(size_t a, size_t b) { return static_cast<unsigned>((a +
 enum {
   S_BF_Q = 0, S_BF_T, S_BF_TL, S_BF_TILES, S_BF_K1, S_BF_K2, S_BF_QKEY, S_BF_OUT0, S_BF_OUT1,
   S_BF_OUT2, S_BF_OUT3, S_BF_OUT4, S_BF_OUT5, S_BF_OFF,
-  S_W0 = 14, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7, S_W8, S_W9
+  S_W0 = 14, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7, S_W8, S_W9,
+  S_KP = 24,   /* 10 slots: keypoint upload + grid */
+  S_WX = 34    /* 8 slots: windowed-matcher scratch */
 };

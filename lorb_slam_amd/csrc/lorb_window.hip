@@ -1,0 +1,667 @@
+// lorb_window.hip -- windowed (projection) ORB matching on gfx950 + its frame-side callees.
+//
+// (a4) Matcher::SearchByProjection(Frame*, Frame*, th)          src/matcher.cpp:64-218
+// (a5) Matcher::SearchByProjection(Frame*, set<MapPoint*>, th)  src/matcher.cpp:220-316
+// (a7) Frame::AssignFeaturesToGrid / GetFeaturesInArea          src/frame.cpp:87-115, 370-423
+// (a8) Frame::IsInFrustum + MapPoint::PredictScale              src/frame.cpp:425-494, map_point.cpp:267-284
+// (a20) Frame::UnprojectStereo                                  src/frame.cpp:335-356
+//
+// The reference resolves map points sequentially: a keypoint slot already holding a map point
+// with mnObs>0 is skipped by every LATER point (src/matcher.cpp:149-151, 273-275).  That order
+// dependence is reproduced exactly and in parallel by a Jacobi fixpoint:
+//   round r: every point picks best/second over its candidate list, skipping slots that were
+//            locked before the call or claimed (accepted + mnObs>0) by an EARLIER point in
+//            round r-1's results;  claims = min point index per slot.
+// Point 0 is exact in round 1, point j depends only on points < j, so after round k points
+// 0..k-1 are final; a round with no change is the unique sequential answer.  Rounds are bounded
+// by n+1 and in practice end after a handful.  All float expressions follow the reference's
+// operation order (built with -ffp-contract=off) so candidate sets are bit-identical.
+#include "lorb_internal.h"
+
+#include <cmath>
+
+namespace {
+
+constexpr int kCells = LORB_GRID_COLS * LORB_GRID_ROWS;
+constexpr uint32_t kNoClaim = 0x7fffffff;
+
+struct WinParams {  // per-call scalars (device copy of lorb_frame_params)
+  lorb_frame_params fp;
+  float th;
+  int mode_forward, mode_backward;  // a4 only
+  float Rcw[9], tcw[3];             // a4 only
+};
+
+__device__ __forceinline__ int hamming(const uint4* a, const uint4* b) {
+  const uint4 a0 = a[0], a1 = a[1], b0 = b[0], b1 = b[1];
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// (a7) grid: one workgroup; cell = PosInGrid; per-cell lists in keypoint (insertion) order
+__global__ __launch_bounds__(1024) void k_grid_build(const float* __restrict__ x, const float* __restrict__ y,
+                                                     int n, lorb_frame_params fp,
+                                                     int* __restrict__ cell_off,  // kCells+1
+                                                     int* __restrict__ cell_idx, int* __restrict__ kp_cell) {
+  __shared__ int cnt[kCells];
+  __shared__ int cur[kCells];
+  const int t = threadIdx.x;
+  for (int c = t; c < kCells; c += 1024) cnt[c] = 0;
+  __syncthreads();
+  for (int i = t; i < n; i += 1024) {
+    const int px = (int)roundf((x[i] - fp.min_x) * fp.grid_w_inv);
+    const int py = (int)roundf((y[i] - fp.min_y) * fp.grid_h_inv);
+    int c = -1;
+    if (!(px < 0 || px >= LORB_GRID_COLS || py < 0 || py >= LORB_GRID_ROWS)) c = px * LORB_GRID_ROWS + py;
+    kp_cell[i] = c;
+    if (c >= 0) atomicAdd(&cnt[c], 1);
+  }
+  __syncthreads();
+  if (t == 0) {  // 3072-entry scan (tiny)
+    int acc = 0;
+    for (int c = 0; c < kCells; ++c) { cell_off[c] = acc; cur[c] = acc; acc += cnt[c]; }
+    cell_off[kCells] = acc;
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += 1024) {
+    const int c = kp_cell[i];
+    if (c >= 0) cell_idx[atomicAdd(&cur[c], 1)] = i;
+  }
+  __syncthreads();
+  // restore insertion (index) order inside every cell: cells hold a handful of entries
+  for (int c = t; c < kCells; c += 1024) {
+    const int a = cell_off[c], b = cell_off[c + 1];
+    for (int i = a + 1; i < b; ++i) {
+      const int v = cell_idx[i];
+      int j = i - 1;
+      while (j >= a && cell_idx[j] > v) { cell_idx[j + 1] = cell_idx[j]; --j; }
+      cell_idx[j + 1] = v;
+    }
+  }
+}
+
+struct FeatArea {  // Frame::GetFeaturesInArea window
+  int x0, x1, y0, y1;
+  bool empty;
+};
+__device__ __forceinline__ FeatArea feat_area(const lorb_frame_params& fp, float x, float y, float r) {
+  FeatArea a;
+  a.empty = true;
+  a.x0 = max(0, (int)floorf((x - fp.min_x - r) * fp.grid_w_inv));
+  if (a.x0 >= LORB_GRID_COLS) return a;
+  a.x1 = min(LORB_GRID_COLS - 1, (int)ceilf((x - fp.min_x + r) * fp.grid_w_inv));
+  if (a.x1 < 0) return a;
+  a.y0 = max(0, (int)floorf((y - fp.min_y - r) * fp.grid_h_inv));
+  if (a.y0 >= LORB_GRID_ROWS) return a;
+  a.y1 = min(LORB_GRID_ROWS - 1, (int)ceilf((y - fp.min_y + r) * fp.grid_h_inv));
+  if (a.y1 < 0) return a;
+  a.empty = false;
+  return a;
+}
+
+struct KpDev {
+  const float *x, *y, *angle, *uR;
+  const int* octave;
+  const uint4* desc;
+  const uint8_t* slot_state;
+  const int *cell_off, *cell_idx;
+  int n;
+};
+
+// Walk GetFeaturesInArea in reference order (ix outer, iy inner, cell insertion order) and
+// apply the level / window / stereo filters.  WRITE=false counts, WRITE=true emits
+// (keypoint, distance) in order.
+template <bool WRITE>
+__device__ __forceinline__ int walk_candidates(const KpDev& K, const lorb_frame_params& fp, float x,
+                                               float y, float r, int minLevel, int maxLevel,
+                                               float stereo_u, float stereo_r, const uint4* qdesc,
+                                               int2* out) {
+  const FeatArea a = feat_area(fp, x, y, r);
+  if (a.empty) return 0;
+  const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+  int n = 0;
+  for (int ix = a.x0; ix <= a.x1; ++ix)
+    for (int iy = a.y0; iy <= a.y1; ++iy) {
+      const int c = ix * LORB_GRID_ROWS + iy;
+      for (int e = K.cell_off[c]; e < K.cell_off[c + 1]; ++e) {
+        const int j = K.cell_idx[e];
+        const int oc = K.octave[j];
+        if (bCheckLevels) {
+          if (oc < minLevel) continue;
+          if (maxLevel >= 0 && oc > maxLevel) continue;
+        }
+        const float distx = K.x[j] - x;
+        const float disty = K.y[j] - y;
+        if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+        if (K.uR && K.uR[j] > 0) {  // stereo consistency (checked after occupancy in the reference;
+                                    // both are pure filters so the order is immaterial)
+          const float er = fabsf(stereo_u - K.uR[j]);
+          if (er > stereo_r) continue;
+        }
+        if (WRITE) out[n] = make_int2(j, hamming(qdesc, K.desc + 2 * (size_t)j));
+        ++n;
+      }
+    }
+  return n;
+}
+
+// (a5) candidates of each local map point
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_cand_local(KpDev K, WinParams P, int np,
+                                                    const uint8_t* __restrict__ in_view,
+                                                    const uint8_t* __restrict__ is_bad,
+                                                    const float* __restrict__ px, const float* __restrict__ py,
+                                                    const float* __restrict__ pxr, const int* __restrict__ plev,
+                                                    const float* __restrict__ vcos, const uint4* __restrict__ pdesc,
+                                                    int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
+                                                    int2* __restrict__ cand) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= np) return;
+  int cnt = 0;
+  if (in_view[m] && !(is_bad && is_bad[m])) {
+    const int lev = plev[m];
+    float r = ((double)vcos[m] > 0.998) ? 2.5f : 4.0f;  // RadiusByViewingCos
+    if (P.th != 1.0f) r *= P.th;
+    const float rs = r * P.fp.scale_factors[lev];
+    cnt = walk_candidates<WRITE>(K, P.fp, px[m], py[m], rs, lev - 1, lev, pxr[m], rs, pdesc + 2 * (size_t)m,
+                                 WRITE ? cand + cand_off[m] : nullptr);
+  }
+  if (!WRITE) cand_cnt[m] = cnt;
+}
+
+// (a4) projection of last-frame map points + candidates
+__device__ __forceinline__ float gemv3(const float* R, float a, float b, float c, float t) {
+  const double s = (double)R[0] * (double)a + (double)R[1] * (double)b + (double)R[2] * (double)c;
+  return (float)(s + (double)t);
+}
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_cand_frame(KpDev K, WinParams P, int nl,
+                                                    const uint8_t* __restrict__ has_mp,
+                                                    const uint8_t* __restrict__ outlier,
+                                                    const float* __restrict__ pos,
+                                                    const int* __restrict__ loct,
+                                                    const uint4* __restrict__ ldesc,
+                                                    int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
+                                                    int2* __restrict__ cand) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nl) return;
+  int cnt = 0;
+  if (has_mp[i] && !(outlier && outlier[i])) {
+    const float X = pos[3 * i], Y = pos[3 * i + 1], Z = pos[3 * i + 2];
+    const float xc = gemv3(P.Rcw + 0, X, Y, Z, P.tcw[0]);
+    const float yc = gemv3(P.Rcw + 3, X, Y, Z, P.tcw[1]);
+    const float zc = gemv3(P.Rcw + 6, X, Y, Z, P.tcw[2]);
+    const float invzc = (float)(1.0 / (double)zc);
+    if (!(invzc < 0)) {
+      const float u = P.fp.fx * xc * invzc + P.fp.cx;
+      const float v = P.fp.fy * yc * invzc + P.fp.cy;
+      if (!(u < P.fp.min_x || u > P.fp.max_x) && !(v < P.fp.min_y || v > P.fp.max_y)) {
+        const int o = loct[i];
+        const float radius = P.th * P.fp.scale_factors[o];
+        int mn, mx;
+        if (P.mode_forward) { mn = o; mx = -1; }
+        else if (P.mode_backward) { mn = 0; mx = o; }
+        else { mn = o - 1; mx = o + 1; }
+        const float ur = u - P.fp.bf * invzc;
+        cnt = walk_candidates<WRITE>(K, P.fp, u, v, radius, mn, mx, ur, radius, ldesc + 2 * (size_t)i,
+                                     WRITE ? cand + cand_off[i] : nullptr);
+      }
+    }
+  }
+  if (!WRITE) cand_cnt[i] = cnt;
+}
+
+// exclusive scan of candidate counts (one workgroup, chunked)
+__global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ cnt, int n, int* __restrict__ off) {
+  __shared__ int s[1024];
+  __shared__ int carry;
+  const int t = threadIdx.x;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 1024) {
+    const int v = base + t < n ? cnt[base + t] : 0;
+    s[t] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int a = t >= o ? s[t - o] : 0;
+      __syncthreads();
+      s[t] += a;
+      __syncthreads();
+    }
+    if (base + t < n) off[base + t] = carry + s[t] - v;
+    __syncthreads();
+    if (t == 1023) carry += s[1023];
+    __syncthreads();
+  }
+  if (t == 0) off[n] = carry;
+}
+
+// Jacobi fixpoint resolver (one workgroup per call).  MODE 0 = a5 (best/second + ratio test),
+// MODE 1 = a4 (best only + rotation histogram / ComputeThreeMaxima null-out).
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __restrict__ cand_off,
+                                                  const int2* __restrict__ cand,
+                                                  const int* __restrict__ kp_octave,
+                                                  const uint8_t* __restrict__ slot_state,
+                                                  const uint8_t* __restrict__ pt_locked,
+                                                  const float* __restrict__ last_angle,
+                                                  const float* __restrict__ cur_angle,
+                                                  int* __restrict__ res,     // np: accepted slot or -1
+                                                  int* __restrict__ claim,   // nk (global scratch)
+                                                  int* __restrict__ assign,  // nk output
+                                                  int* __restrict__ bins,    // np scratch (MODE 1)
+                                                  int* __restrict__ nulls,   // nk scratch (MODE 1)
+                                                  int* __restrict__ nmatches) {
+  __shared__ int s_changed, s_rounds;
+  __shared__ int hist[LORB_HISTO_LENGTH];
+  __shared__ int s_ind[3];
+  __shared__ int s_acc, s_rej;
+  const int t = threadIdx.x;
+  for (int c = t; c < nk; c += 1024) claim[c] = kNoClaim;
+  for (int m = t; m < np; m += 1024) res[m] = -2;  // "never computed"
+  if (t == 0) { s_rounds = 0; s_acc = 0; s_rej = 0; }
+  __syncthreads();
+  for (int round = 0; round <= np; ++round) {
+    if (t == 0) s_changed = 0;
+    __syncthreads();
+    for (int m = t; m < np; m += 1024) {
+      const int a = cand_off[m], b = cand_off[m + 1];
+      int bestDist = 256, bestIdx = -1;
+      int bestLevel = -1, bestDist2 = 256, bestLevel2 = -1;
+      for (int e = a; e < b; ++e) {
+        const int2 cd = cand[e];
+        const int j = cd.x;
+        if (slot_state[j] == LORB_SLOT_LOCKED) continue;
+        if ((int)claim[j] < m) continue;  // locked by an earlier point during this call
+        const int dist = cd.y;
+        if (MODE == 0) {
+          if (dist < bestDist) {
+            bestDist2 = bestDist; bestDist = dist;
+            bestLevel2 = bestLevel; bestLevel = kp_octave[j]; bestIdx = j;
+          } else if (dist < bestDist2) {
+            bestLevel2 = kp_octave[j]; bestDist2 = dist;
+          }
+        } else {
+          if (dist < bestDist) { bestDist = dist; bestIdx = j; }
+        }
+      }
+      int r = -1;
+      if (bestDist <= LORB_TH_HIGH) {
+        r = bestIdx;
+        if (MODE == 0 && bestLevel == bestLevel2 && (double)bestDist > 0.8 * (double)bestDist2) r = -1;
+      }
+      if (r != res[m]) { res[m] = r; s_changed = 1; }
+    }
+    __syncthreads();
+    if (!s_changed) break;
+    for (int c = t; c < nk; c += 1024) claim[c] = kNoClaim;
+    __syncthreads();
+    for (int m = t; m < np; m += 1024)
+      if (res[m] >= 0 && pt_locked[m]) atomicMin(&claim[res[m]], m);
+    __syncthreads();
+  }
+  // final slot assignment: last accepted writer per slot
+  for (int c = t; c < nk; c += 1024) { assign[c] = LORB_ASSIGN_UNCHANGED; if (MODE == 1) nulls[c] = 0; }
+  if (MODE == 1 && t < LORB_HISTO_LENGTH) hist[t] = 0;
+  __syncthreads();
+  for (int m = t; m < np; m += 1024) {
+    const int r = res[m];
+    if (r >= 0) {
+      atomicMax(&assign[r], m);
+      atomicAdd(&s_acc, 1);
+      if (MODE == 1) {
+        float rot = last_angle[m] - cur_angle[r];
+        if (rot < 0.0) rot += 360.0f;
+        const float factor = LORB_HISTO_LENGTH / 360.0f;
+        int bin = (int)roundf(rot * factor);
+        if (bin == LORB_HISTO_LENGTH) bin = 0;
+        bins[m] = bin;
+        atomicAdd(&hist[bin], 1);
+      }
+    }
+  }
+  __syncthreads();
+  if (MODE == 1) {
+    if (t == 0) {  // Matcher::ComputeThreeMaxima, src/matcher.cpp:387-428
+      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+      for (int i = 0; i < LORB_HISTO_LENGTH; i++) {
+        const int s = hist[i];
+        if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+        else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+        else if (s > max3) { max3 = s; ind3 = i; }
+      }
+      if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+      else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
+      s_ind[0] = ind1; s_ind[1] = ind2; s_ind[2] = ind3;
+    }
+    __syncthreads();
+    for (int m = t; m < np; m += 1024) {
+      const int r = res[m];
+      if (r >= 0) {
+        const int b = bins[m];
+        if (b != s_ind[0] && b != s_ind[1] && b != s_ind[2]) { nulls[r] = 1; atomicAdd(&s_rej, 1); }
+      }
+    }
+    __syncthreads();
+    for (int c = t; c < nk; c += 1024)
+      if (nulls[c]) assign[c] = LORB_ASSIGN_NULL;
+  }
+  __syncthreads();
+  if (t == 0) *nmatches = s_acc - s_rej;
+}
+
+// (a8) Frame::IsInFrustum + PredictScale, one thread per map point
+__global__ __launch_bounds__(256) void k_frustum(lorb_frame_params fp, const float* __restrict__ T,
+                                                 const float* __restrict__ Ow, int n,
+                                                 const float* __restrict__ pos, const float* __restrict__ nrm,
+                                                 const float* __restrict__ maxd, const float* __restrict__ mind,
+                                                 float cos_limit, uint8_t* __restrict__ in_view,
+                                                 float* __restrict__ ox, float* __restrict__ oy,
+                                                 float* __restrict__ oxr, int* __restrict__ olev,
+                                                 float* __restrict__ ocos) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= n) return;
+  in_view[m] = 0;
+  const float P0 = pos[3 * m], P1 = pos[3 * m + 1], P2 = pos[3 * m + 2];
+  float Pc[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const double s = (double)T[4 * r] * P0 + (double)T[4 * r + 1] * P1 + (double)T[4 * r + 2] * P2 + (double)T[4 * r + 3] * 1.0f;
+    Pc[r] = (float)s;
+  }
+  if (Pc[2] < 0.0f) return;
+  const float invz = 1.0f / Pc[2];
+  const float u = fp.fx * Pc[0] * invz + fp.cx;
+  const float v = fp.fy * Pc[1] * invz + fp.cy;
+  if (u < fp.min_x || u > fp.max_x) return;
+  if (v < fp.min_y || v > fp.max_y) return;
+  const float maxDistance = 1.2f * maxd[m];
+  const float minDistance = 0.8f * mind[m];
+  const float PO0 = P0 - Ow[0], PO1 = P1 - Ow[1], PO2 = P2 - Ow[2];
+  const float dist = (float)sqrt((double)PO0 * PO0 + (double)PO1 * PO1 + (double)PO2 * PO2);
+  if (dist < minDistance || dist > maxDistance) return;
+  const float dot = PO0 * nrm[3 * m] + PO1 * nrm[3 * m + 1] + PO2 * nrm[3 * m + 2];
+  const float viewCos = dot / dist;
+  if (viewCos < cos_limit) return;
+  const float ratio = maxd[m] / dist;
+  int nScale = (int)ceilf((float)log((double)ratio) / fp.log_scale_factor);
+  if (nScale < 0) nScale = 0;
+  else if (nScale >= fp.n_levels) nScale = fp.n_levels - 1;
+  in_view[m] = 1;
+  ox[m] = u;
+  oxr[m] = u - fp.bf * invz;
+  oy[m] = v;
+  olev[m] = nScale;
+  ocos[m] = viewCos;
+}
+
+// (a20) Frame::UnprojectStereo, one thread per keypoint; Twc = mTcw.inv() given
+__global__ __launch_bounds__(256) void k_unproject(lorb_frame_params fp, const float* __restrict__ Twc, int n,
+                                                   const float* __restrict__ x, const float* __restrict__ y,
+                                                   const float* __restrict__ depth, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float z = depth[i];
+  if (z > 0) {
+    const float xx = (x[i] - fp.cx) * z / fp.fx;
+    const float yy = (y[i] - fp.cy) * z / fp.fy;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const double s = (double)Twc[4 * r] * xx + (double)Twc[4 * r + 1] * yy + (double)Twc[4 * r + 2] * z + (double)Twc[4 * r + 3] * 1.0f;
+      out[3 * i + r] = (float)s;
+    }
+  } else {
+    out[3 * i] = 0.0f; out[3 * i + 1] = 0.0f; out[3 * i + 2] = 0.0f;
+  }
+}
+
+// cv::Mat::inv() for 4x4 CV_32F: hal::LU32f (partial pivoting, float), host side
+bool inv4_lu32f(const float* Ain, float* out) {
+  float A[16], b[16];
+  memcpy(A, Ain, sizeof(A));
+  for (int i = 0; i < 16; i++) b[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+  const float eps = 1.1920928955078125e-07f * 10;
+  for (int i = 0; i < 4; i++) {
+    int k = i;
+    for (int j = i + 1; j < 4; j++)
+      if (std::fabs(A[j * 4 + i]) > std::fabs(A[k * 4 + i])) k = j;
+    if (std::fabs(A[k * 4 + i]) < eps) { memset(out, 0, 16 * sizeof(float)); return false; }
+    if (k != i) {
+      for (int j = i; j < 4; j++) std::swap(A[i * 4 + j], A[k * 4 + j]);
+      for (int j = 0; j < 4; j++) std::swap(b[i * 4 + j], b[k * 4 + j]);
+    }
+    const float dd = -1 / A[i * 4 + i];
+    for (int j = i + 1; j < 4; j++) {
+      const float alpha = A[j * 4 + i] * dd;
+      for (int kk = i + 1; kk < 4; kk++) A[j * 4 + kk] += alpha * A[i * 4 + kk];
+      for (int kk = 0; kk < 4; kk++) b[j * 4 + kk] += alpha * b[i * 4 + kk];
+    }
+  }
+  for (int i = 3; i >= 0; i--)
+    for (int j = 0; j < 4; j++) {
+      float s = b[i * 4 + j];
+      for (int k = i + 1; k < 4; k++) s -= A[i * 4 + k] * b[k * 4 + j];
+      b[i * 4 + j] = s / A[i * 4 + i];
+    }
+  memcpy(out, b, sizeof(b));
+  return true;
+}
+
+int upload_kps(lorb_ctx* ctx, const lorb_keypoints* k, const uint8_t* slot_state, int slot0, KpDev* K,
+               const lorb_frame_params* fp) {
+  const int n = k->n;
+  float *x, *y, *ang, *ur = nullptr;
+  int* oc;
+  uint8_t *desc, *ss;
+  LORB_TRY(lorb::upload_t(ctx, slot0 + 0, k->x, n, &x));
+  LORB_TRY(lorb::upload_t(ctx, slot0 + 1, k->y, n, &y));
+  LORB_TRY(lorb::upload_t(ctx, slot0 + 2, k->angle, n, &ang));
+  LORB_TRY(lorb::upload_t(ctx, slot0 + 3, k->octave, n, &oc));
+  LORB_TRY(lorb::upload_t(ctx, slot0 + 4, k->desc, (size_t)n * 32, &desc));
+  if (k->u_right) LORB_TRY(lorb::upload_t(ctx, slot0 + 5, k->u_right, n, &ur));
+  std::vector<uint8_t> zeros;
+  if (!slot_state) { zeros.assign(n, 0); slot_state = zeros.data(); }
+  LORB_TRY(lorb::upload_t(ctx, slot0 + 6, slot_state, n, &ss));
+  int *cell_off, *cell_idx, *kp_cell;
+  LORB_TRY(lorb::scratch_t(ctx, slot0 + 7, kCells + 1, &cell_off));
+  LORB_TRY(lorb::scratch_t(ctx, slot0 + 8, (size_t)std::max(n, 1), &cell_idx));
+  LORB_TRY(lorb::scratch_t(ctx, slot0 + 9, (size_t)std::max(n, 1), &kp_cell));
+  hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, ctx->stream, x, y, n, *fp, cell_off, cell_idx, kp_cell);
+  LORB_CHECK_LAUNCH(ctx);
+  K->x = x; K->y = y; K->angle = ang; K->uR = ur; K->octave = oc;
+  K->desc = reinterpret_cast<const uint4*>(desc); K->slot_state = ss;
+  K->cell_off = cell_off; K->cell_idx = cell_idx; K->n = n;
+  return LORB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* frame, const lorb_keypoints* kps,
+                                    const uint8_t* slot_state, const lorb_local_points* pts, float th,
+                                    int32_t* assign, int32_t* nmatches) {
+  if (!ctx || !frame || !kps || !pts || !assign || !nmatches) return LORB_E_INVALID;
+  const int nk = kps->n, np = pts->n;
+  if (nk < 0 || np < 0) return lorb::set_error(ctx, LORB_E_INVALID, "negative sizes");
+  if (nk == 0) { *nmatches = 0; return LORB_OK; }
+  for (int i = 0; i < np; ++i)
+    if (pts->pred_level[i] < 0 || pts->pred_level[i] >= LORB_MAX_LEVELS)
+      return lorb::set_error(ctx, LORB_E_INVALID, "point %d: predicted level %d out of range", i, pts->pred_level[i]);
+  KpDev K;
+  LORB_TRY(upload_kps(ctx, kps, slot_state, S_KP, &K, frame));
+  uint8_t *iv, *bad = nullptr, *lk;
+  float *px, *py, *pxr, *vc;
+  int* pl;
+  uint8_t* pd;
+  LORB_TRY(lorb::upload_t(ctx, S_W0, pts->track_in_view, np, &iv));
+  if (pts->is_bad) LORB_TRY(lorb::upload_t(ctx, S_W1, pts->is_bad, np, &bad));
+  LORB_TRY(lorb::upload_t(ctx, S_W2, pts->locked, np, &lk));
+  LORB_TRY(lorb::upload_t(ctx, S_W3, pts->proj_x, np, &px));
+  LORB_TRY(lorb::upload_t(ctx, S_W4, pts->proj_y, np, &py));
+  LORB_TRY(lorb::upload_t(ctx, S_W5, pts->proj_xr, np, &pxr));
+  LORB_TRY(lorb::upload_t(ctx, S_W6, pts->pred_level, np, &pl));
+  LORB_TRY(lorb::upload_t(ctx, S_W7, pts->view_cos, np, &vc));
+  LORB_TRY(lorb::upload_t(ctx, S_W8, pts->desc, (size_t)np * 32, &pd));
+  WinParams P{};
+  P.fp = *frame;
+  P.th = th;
+  int *cnt, *off, *res, *claim, *dassign, *dnm;
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 0, (size_t)np + 1, &cnt));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 1, (size_t)np + 1, &off));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 2, (size_t)np + 1, &res));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 3, (size_t)nk + 1, &claim));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 4, (size_t)nk + 2, &dassign));
+  dnm = dassign + nk;
+  const unsigned g = lorb::ceil_div(std::max(np, 1), 256);
+  if (np > 0) {
+    lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
+    hipLaunchKernelGGL(k_cand_local<false>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
+                       reinterpret_cast<const uint4*>(pd), cnt, (const int*)nullptr, (int2*)nullptr);
+  }
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, np, off);
+  int total = 0;
+  LORB_HIP(ctx, hipMemcpyAsync(&total, off + np, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  int2* cand;
+  LORB_TRY(lorb::scratch_t(ctx, S_W9, (size_t)std::max(total, 1), &cand));
+  if (np > 0)
+    hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
+                       reinterpret_cast<const uint4*>(pd), cnt, off, cand);
+  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), 0, ctx->stream, np, nk, off, cand, K.octave, K.slot_state, lk,
+                     (const float*)nullptr, (const float*)nullptr, res, claim, dassign, (int*)nullptr, (int*)nullptr, dnm);
+  LORB_CHECK_LAUNCH(ctx);
+  LORB_HIP(ctx, hipMemcpyAsync(assign, dassign, sizeof(int) * nk, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(nmatches, dnm, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur, const float cur_Tcw[16],
+                                    const lorb_keypoints* cur_kps, const uint8_t* cur_slot_state,
+                                    const lorb_last_frame* last, float th, int32_t* assign, int32_t* nmatches) {
+  if (!ctx || !cur || !cur_Tcw || !cur_kps || !last || !assign || !nmatches) return LORB_E_INVALID;
+  const int nk = cur_kps->n, nl = last->n;
+  if (nk < 0 || nl < 0) return lorb::set_error(ctx, LORB_E_INVALID, "negative sizes");
+  if (nk == 0) { *nmatches = 0; return LORB_OK; }
+  for (int i = 0; i < nl; ++i)
+    if (last->has_mp[i] && (last->octave[i] < 0 || last->octave[i] >= LORB_MAX_LEVELS))
+      return lorb::set_error(ctx, LORB_E_INVALID, "last keypoint %d: octave %d out of range", i, last->octave[i]);
+  // src/matcher.cpp:74-87: motion direction from the two poses (cv::gemm: double accumulation)
+  WinParams P{};
+  P.fp = *cur;
+  P.th = th;
+  const float* T = cur_Tcw;
+  const float Rcw[9] = {T[0], T[1], T[2], T[4], T[5], T[6], T[8], T[9], T[10]};
+  const float tcw[3] = {T[3], T[7], T[11]};
+  memcpy(P.Rcw, Rcw, sizeof(Rcw));
+  memcpy(P.tcw, tcw, sizeof(tcw));
+  float twc[3];
+  for (int i = 0; i < 3; i++) {
+    const double s = (double)Rcw[i] * tcw[0] + (double)Rcw[3 + i] * tcw[1] + (double)Rcw[6 + i] * tcw[2];
+    twc[i] = (float)(-s);
+  }
+  const float* L = last->Tcw;
+  const double s2 = (double)L[8] * twc[0] + (double)L[9] * twc[1] + (double)L[10] * twc[2];
+  const float tlc2 = (float)(s2 + (double)L[11]);
+  P.mode_forward = tlc2 > cur->b;
+  P.mode_backward = -tlc2 > cur->b;
+  KpDev K;
+  LORB_TRY(upload_kps(ctx, cur_kps, cur_slot_state, S_KP, &K, cur));
+  uint8_t *hm, *ol = nullptr, *lk, *ld;
+  float *pos, *la;
+  int* lo;
+  LORB_TRY(lorb::upload_t(ctx, S_W0, last->has_mp, nl, &hm));
+  if (last->outlier) LORB_TRY(lorb::upload_t(ctx, S_W1, last->outlier, nl, &ol));
+  LORB_TRY(lorb::upload_t(ctx, S_W2, last->mp_locked, nl, &lk));
+  LORB_TRY(lorb::upload_t(ctx, S_W3, last->mp_pos, (size_t)nl * 3, &pos));
+  LORB_TRY(lorb::upload_t(ctx, S_W4, last->mp_desc, (size_t)nl * 32, &ld));
+  LORB_TRY(lorb::upload_t(ctx, S_W5, last->octave, nl, &lo));
+  LORB_TRY(lorb::upload_t(ctx, S_W6, last->angle, nl, &la));
+  int *cnt, *off, *res, *claim, *dassign, *dnm, *bins, *nulls;
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 0, (size_t)nl + 1, &cnt));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 1, (size_t)nl + 1, &off));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 2, (size_t)nl + 1, &res));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 3, (size_t)nk + 1, &claim));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 4, (size_t)nk + 2, &dassign));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 5, (size_t)nl + 1, &bins));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 6, (size_t)nk + 1, &nulls));
+  dnm = dassign + nk;
+  const unsigned g = lorb::ceil_div(std::max(nl, 1), 256);
+  if (nl > 0) {
+    lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
+    hipLaunchKernelGGL(k_cand_frame<false>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
+                       reinterpret_cast<const uint4*>(ld), cnt, (const int*)nullptr, (int2*)nullptr);
+  }
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, nl, off);
+  int total = 0;
+  LORB_HIP(ctx, hipMemcpyAsync(&total, off + nl, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  int2* cand;
+  LORB_TRY(lorb::scratch_t(ctx, S_W9, (size_t)std::max(total, 1), &cand));
+  if (nl > 0)
+    hipLaunchKernelGGL(k_cand_frame<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
+                       reinterpret_cast<const uint4*>(ld), cnt, off, cand);
+  hipLaunchKernelGGL(k_resolve<1>, dim3(1), dim3(1024), 0, ctx->stream, nl, nk, off, cand, K.octave, K.slot_state, lk,
+                     la, K.angle, res, claim, dassign, bins, nulls, dnm);
+  LORB_CHECK_LAUNCH(ctx);
+  LORB_HIP(ctx, hipMemcpyAsync(assign, dassign, sizeof(int) * nk, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(nmatches, dnm, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_is_in_frustum(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
+                       const lorb_frustum_points* pts, float viewing_cos_limit, uint8_t* in_view,
+                       float* proj_x, float* proj_y, float* proj_xr, int32_t* pred_level, float* view_cos) {
+  if (!ctx || !frame || !Tcw || !pts) return LORB_E_INVALID;
+  const int n = pts->n;
+  if (n <= 0) return LORB_OK;
+  float Twc[16];
+  inv4_lu32f(Tcw, Twc);
+  const float Ow[3] = {Twc[3], Twc[7], Twc[11]};
+  float *dT, *dO, *pos, *nrm, *mx, *mn, *outf;
+  uint8_t* iv;
+  int* lev;
+  LORB_TRY(lorb::upload_t(ctx, S_W0, Tcw, 16, &dT));
+  LORB_TRY(lorb::upload_t(ctx, S_W1, Ow, 3, &dO));
+  LORB_TRY(lorb::upload_t(ctx, S_W2, pts->pos, (size_t)n * 3, &pos));
+  LORB_TRY(lorb::upload_t(ctx, S_W3, pts->normal, (size_t)n * 3, &nrm));
+  LORB_TRY(lorb::upload_t(ctx, S_W4, pts->max_dist, n, &mx));
+  LORB_TRY(lorb::upload_t(ctx, S_W5, pts->min_dist, n, &mn));
+  LORB_TRY(lorb::scratch_t(ctx, S_W6, (size_t)n * 4, &outf));
+  LORB_TRY(lorb::scratch_t(ctx, S_W7, (size_t)n, &iv));
+  LORB_TRY(lorb::scratch_t(ctx, S_W8, (size_t)n, &lev));
+  hipLaunchKernelGGL(k_frustum, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, *frame, dT, dO, n, pos, nrm, mx,
+                     mn, viewing_cos_limit, iv, outf, outf + n, outf + 2 * n, lev, outf + 3 * n);
+  LORB_CHECK_LAUNCH(ctx);
+  LORB_HIP(ctx, hipMemcpyAsync(in_view, iv, n, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(proj_x, outf, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(proj_y, outf + n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(proj_xr, outf + 2 * n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(view_cos, outf + 3 * n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(pred_level, lev, sizeof(int) * n, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_unproject_stereo(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16], int32_t n,
+                          const float* x, const float* y, const float* depth, float* out_xyz) {
+  if (!ctx || !frame || !Tcw) return LORB_E_INVALID;
+  if (n <= 0) return LORB_OK;
+  float Twc[16];
+  inv4_lu32f(Tcw, Twc);
+  float *dT, *dx, *dy, *dd, *o;
+  LORB_TRY(lorb::upload_t(ctx, S_W0, Twc, 16, &dT));
+  LORB_TRY(lorb::upload_t(ctx, S_W1, x, n, &dx));
+  LORB_TRY(lorb::upload_t(ctx, S_W2, y, n, &dy));
+  LORB_TRY(lorb::upload_t(ctx, S_W3, depth, n, &dd));
+  LORB_TRY(lorb::scratch_t(ctx, S_W4, (size_t)n * 3, &o));
+  hipLaunchKernelGGL(k_unproject, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, *frame, dT, n, dx, dy, dd, o);
+  LORB_CHECK_LAUNCH(ctx);
+  LORB_HIP(ctx, hipMemcpyAsync(out_xyz, o, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+}  // extern "C"

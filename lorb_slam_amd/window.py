@@ -1,0 +1,70 @@
+"""ctypes bindings of the windowed matchers and frame callees (a4, a5, a8, a20) of liblorb.so."""
+import ctypes as C
+
+import numpy as np
+
+from . import _abi as A
+from .runtime import Context, lib
+
+
+def _search_by_projection_frame(self, fp, cur_Tcw, cur_kps, cur_slot_state, last, th):
+    keep = A.KeepAlive()
+    fps = A.make_frame_params(fp)
+    k = A.make_keypoints(cur_kps, keep)
+    lf = A.make_last_frame(last, keep)
+    T = keep.keep(A.f32(cur_Tcw).reshape(16))
+    ss = keep.keep(A.u8(cur_slot_state)) if cur_slot_state is not None else None
+    assign = np.empty(max(1, k.n), np.int32)
+    nm = C.c_int32(0)
+    self.check(lib().lorb_search_by_projection_frame(
+        self.handle, C.byref(fps), A.ptr(T, C.c_float), C.byref(k), A.ptr(ss, C.c_uint8), C.byref(lf),
+        C.c_float(th), A.ptr(assign, C.c_int32), C.byref(nm)), "lorb_search_by_projection_frame")
+    return assign[: k.n].copy(), nm.value
+
+
+def _search_by_projection_local(self, fp, kps, slot_state, pts, th):
+    keep = A.KeepAlive()
+    fps = A.make_frame_params(fp)
+    k = A.make_keypoints(kps, keep)
+    lp = A.make_local_points(pts, keep)
+    ss = keep.keep(A.u8(slot_state)) if slot_state is not None else None
+    assign = np.empty(max(1, k.n), np.int32)
+    nm = C.c_int32(0)
+    self.check(lib().lorb_search_by_projection_local(
+        self.handle, C.byref(fps), C.byref(k), A.ptr(ss, C.c_uint8), C.byref(lp), C.c_float(th),
+        A.ptr(assign, C.c_int32), C.byref(nm)), "lorb_search_by_projection_local")
+    return assign[: k.n].copy(), nm.value
+
+
+def _is_in_frustum(self, fp, Tcw, fpts, cos_limit=0.5):
+    keep = A.KeepAlive()
+    fps = A.make_frame_params(fp)
+    p = A.make_frustum_points(fpts, keep)
+    T = keep.keep(A.f32(Tcw).reshape(16))
+    n = p.n
+    out = dict(in_view=np.zeros(max(n, 1), np.uint8), proj_x=np.zeros(max(n, 1), np.float32),
+               proj_y=np.zeros(max(n, 1), np.float32), proj_xr=np.zeros(max(n, 1), np.float32),
+               pred_level=np.zeros(max(n, 1), np.int32), view_cos=np.zeros(max(n, 1), np.float32))
+    self.check(lib().lorb_is_in_frustum(
+        self.handle, C.byref(fps), A.ptr(T, C.c_float), C.byref(p), C.c_float(cos_limit),
+        A.ptr(out["in_view"], C.c_uint8), A.ptr(out["proj_x"], C.c_float), A.ptr(out["proj_y"], C.c_float),
+        A.ptr(out["proj_xr"], C.c_float), A.ptr(out["pred_level"], C.c_int32),
+        A.ptr(out["view_cos"], C.c_float)), "lorb_is_in_frustum")
+    return {k_: v[:n] for k_, v in out.items()}
+
+
+def _unproject_stereo(self, fp, Tcw, x, y, depth):
+    fps = A.make_frame_params(fp)
+    T = A.f32(Tcw).reshape(16)
+    x = A.f32(x); y = A.f32(y); d = A.f32(depth)
+    out = np.zeros((max(len(x), 1), 3), np.float32)
+    self.check(lib().lorb_unproject_stereo(self.handle, C.byref(fps), A.ptr(T, C.c_float), C.c_int32(len(x)),
+                                           A.ptr(x, C.c_float), A.ptr(y, C.c_float), A.ptr(d, C.c_float),
+                                           A.ptr(out, C.c_float)), "lorb_unproject_stereo")
+    return out[: len(x)]
+
+
+Context.search_by_projection_frame = _search_by_projection_frame
+Context.search_by_projection_local = _search_by_projection_local
+Context.is_in_frustum = _is_in_frustum
+Context.unproject_stereo = _unproject_stereo

@@ -1,0 +1,49 @@
+"""CPU: oracle windowed matchers pinned against the independent pure-Python restatement."""
+import numpy as np
+import pytest
+
+import oracle as O
+import pyref
+from lorb_slam_amd import synth
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_local_points_oracle_vs_pyref(seed):
+    pr = synth.local_points_problem(seed=seed, n_kps=400, n_pts=500, n_true=250)
+    a, n = O.search_by_projection_local(pr["fp"], pr["kps"], pr["slot_state"], pr["pts"], 1.0)
+    b, m = pyref.search_by_projection_local(pr["fp"], pr["kps"], pr["slot_state"], pr["pts"], 1.0)
+    assert n == m
+    assert np.array_equal(np.where(a >= 0, a, -1), b)
+
+
+def test_features_in_area_vs_pyref():
+    pr = synth.local_points_problem(seed=3, n_kps=600, n_pts=10, n_true=5)
+    fp, kps = pr["fp"], pr["kps"]
+    grid = pyref.build_grid(fp, kps)
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        x, y = rng.uniform(-20, 780), rng.uniform(-20, 500)
+        r = float(np.float32(rng.uniform(1, 30)))
+        lo, hi = int(rng.integers(-1, 4)), int(rng.integers(-1, 8))
+        got = O.features_in_area(fp, kps, np.float32(x), np.float32(y), np.float32(r), lo, hi)
+        ref = pyref.features_in_area(fp, kps, grid, x, y, r, lo, hi)
+        assert list(got) == ref
+
+
+def test_frame_match_oracle_runs():
+    s = synth.two_frames(seed=1)
+    a, n = O.search_by_projection_frame(s["fp"], s["cur_Tcw"], s["cur_kps"], s["slot_state"], s["last"], 15.0)
+    assert n > 100  # most of the 200 shared points are recovered at th=15
+    assert (a >= -2).all()
+
+
+def test_inv4_and_unproject():
+    T = synth.Tcw_from([0.1, -0.2, 0.05], [0.3, -0.1, 0.5])
+    Ti, ok = O.inv4_f32(T)
+    assert ok and np.allclose(Ti @ T, np.eye(4), atol=1e-6)
+    fp = synth.frame_params()
+    out = O.unproject_stereo(fp, T, [100.0, 300.0], [50.0, 200.0], [2.0, -1.0])
+    assert np.array_equal(out[1], np.zeros(3, np.float32))
+    Xc = T.astype(np.float64) @ np.array([*out[0], 1.0])   # back into the camera frame
+    assert abs(Xc[2] - 2.0) < 1e-5
+    assert abs(Xc[0] - (100.0 - fp["cx"]) * 2.0 / fp["fx"]) < 1e-4
