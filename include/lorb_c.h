@@ -227,6 +227,10 @@ int lorb_is_in_frustum(lorb_ctx* ctx, const lorb_frame_params* frame, const floa
 int lorb_unproject_stereo(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
                           int32_t n, const float* x, const float* y, const float* depth,
                           float* out_xyz);
+/* device-pointer variant (async on the ctx stream); frame / Tcw are host values */
+int lorb_unproject_stereo_dev(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
+                              int32_t n, const float* d_x, const float* d_y, const float* d_depth,
+                              float* d_out_xyz);
 
 /* ----------------------------------------------------------------------------------------
  * Bundle adjustment: Ceres-default Levenberg-Marquardt + DENSE_SCHUR restated

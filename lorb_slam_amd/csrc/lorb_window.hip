@@ -645,6 +645,20 @@ int lorb_is_in_frustum(lorb_ctx* ctx, const lorb_frame_params* frame, const floa
   return LORB_OK;
 }
 
+int lorb_unproject_stereo_dev(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16], int32_t n,
+                              const float* d_x, const float* d_y, const float* d_depth, float* d_out) {
+  if (!ctx || !frame || !Tcw) return LORB_E_INVALID;
+  if (n <= 0) return LORB_OK;
+  float Twc[16];
+  inv4_lu32f(Tcw, Twc);
+  float* dT;
+  LORB_TRY(lorb::upload_t(ctx, S_WX + 7, Twc, 16, &dT));
+  hipLaunchKernelGGL(k_unproject, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, *frame, dT, n, d_x, d_y,
+                     d_depth, d_out);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
 int lorb_unproject_stereo(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16], int32_t n,
                           const float* x, const float* y, const float* depth, float* out_xyz) {
   if (!ctx || !frame || !Tcw) return LORB_E_INVALID;

@@ -258,3 +258,27 @@ def local_points_problem(seed=5, n_kps=2000, n_pts=3000, n_true=1500, locked_fra
         slot_state[pf] = rng.integers(1, 3, size=slot_prefill).astype(np.uint8)
     kps = dict(x=x, y=y, octave=octv, angle=ang, u_right=uR, desc=desc)
     return dict(fp=fp, kps=kps, slot_state=slot_state, pts=pts)
+
+
+def local_mapping_step(seed=4, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400, n_kps=2000,
+                       n_reobs=1500, max_flips=20):
+    """BASELINE config "full local_mapping step -- match + triangulate + BA on a 50-KF / 10k-point
+    window" (SURVEY §8d C4): the window (ba_window), the window map points' descriptors, and a
+    new keyframe with n_kps keypoints of which n_reobs re-observe window map points (bit-flipped
+    descriptors) and the rest are new with stereo depth (to be unprojected)."""
+    win = ba_window(seed=seed, n_kf=n_kf, n_pts=n_pts, n_fixed=n_fixed, fixed_obs_per_kf=fixed_obs_per_kf)
+    rng = np.random.default_rng(seed + 7777)
+    mp_desc = random_desc(rng, n_pts)
+    kf_desc = random_desc(rng, n_kps)
+    re = rng.choice(n_pts, size=n_reobs, replace=False)
+    slots = rng.choice(n_kps, size=n_reobs, replace=False)
+    kf_desc[slots] = flip_bits(rng, mp_desc[re], max_flips)
+    x = rng.uniform(0, W, n_kps).astype(np.float32)
+    y = rng.uniform(0, H, n_kps).astype(np.float32)
+    depth = np.full(n_kps, -1.0, np.float32)
+    new = np.setdiff1d(np.arange(n_kps), slots)
+    depth[new] = rng.uniform(2, 20, len(new)).astype(np.float32)
+    last = win["true_poses"][-1]
+    Tcw = Tcw_from(last[:3], last[3:])
+    return dict(window=win, mp_desc=mp_desc, kf_desc=kf_desc, kf_x=x, kf_y=y, kf_depth=depth, kf_Tcw=Tcw,
+                reobs_slot=slots, reobs_point=re)
