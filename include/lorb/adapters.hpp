@@ -1,0 +1,353 @@
+// lorb/adapters.hpp -- C++ host layer between the reference's class interfaces
+// (Simple_ORB_SLAM::Matcher / BA / LocalMapping) and the C-ABI of lorb_c.h.
+//
+// The functions here are templates over the caller's Frame / MapPoint types and reach their
+// fields only through FrameTraits<> / PointTraits<> specialisations.  The drop-in build
+// (integration/Simple_ORB_SLAM/) specialises them for the reference's OpenCV-based Frame and
+// MapPoint; tests/cpp specialises them for plain test frames.  Every function gathers the
+// fields the reference reads into SoA arrays, calls liblorb.so (HIP kernels on the MI355X),
+// and applies the results back exactly as the reference writes them (file:line per function).
+//
+// Error behaviour: the reference never fails (it returns counts / void).  A C-ABI error is
+// raised as lorb::Error (std::runtime_error) -- there is deliberately no CPU fallback.
+#pragma once
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../lorb_c.h"
+
+namespace lorb {
+
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// Specialise for the caller's types.  Required members are listed in integration/.
+template <class FrameT> struct FrameTraits;
+template <class PointT> struct PointTraits;
+
+// One lorb_ctx (one HIP stream) per calling thread (SURVEY §8b "Threading").
+inline lorb_ctx* thread_ctx(int device = 0) {
+  struct Holder {
+    lorb_ctx* ctx = nullptr;
+    ~Holder() { if (ctx) lorb_destroy(ctx); }
+  };
+  thread_local Holder h;
+  if (!h.ctx && lorb_create(device, &h.ctx) != LORB_OK)
+    throw Error("lorb_create failed: no usable MI355X (liblorb.so has no CPU fallback)");
+  return h.ctx;
+}
+
+inline void check(lorb_ctx* ctx, int rc, const char* what) {
+  if (rc != LORB_OK) throw Error(std::string(what) + " failed: " + lorb_last_error(ctx));
+}
+
+// SoA gather of a frame's keypoints (Frame::mvKeysUn, mvuRight, mDescriptors)
+struct KeypointsSoA {
+  std::vector<float> x, y, angle, uR;
+  std::vector<int32_t> octave;
+  std::vector<uint8_t> desc;
+  lorb_keypoints view() const {
+    lorb_keypoints k;
+    k.n = (int32_t)x.size(); k.x = x.data(); k.y = y.data(); k.octave = octave.data(); k.angle = angle.data();
+    k.u_right = uR.empty() ? nullptr : uR.data(); k.desc = desc.data();
+    return k;
+  }
+};
+
+template <class FrameT>
+KeypointsSoA gather_keypoints(FrameT* F) {
+  using FT = FrameTraits<FrameT>;
+  KeypointsSoA s;
+  const size_t n = FT::num_keypoints(F);
+  s.x.resize(n); s.y.resize(n); s.angle.resize(n); s.octave.resize(n); s.desc.resize(32 * n);
+  for (size_t i = 0; i < n; ++i) {
+    FT::keypoint(F, i, &s.x[i], &s.y[i], &s.octave[i], &s.angle[i]);
+    FT::descriptor(F, i, &s.desc[32 * i]);
+  }
+  if (FT::has_right(F)) {
+    s.uR.resize(n);
+    for (size_t i = 0; i < n; ++i) s.uR[i] = FT::u_right(F, i);
+  }
+  return s;
+}
+
+// slot state of F->mvpMapPoints (src/matcher.cpp:149-151 occupancy test)
+template <class FrameT>
+std::vector<uint8_t> gather_slot_state(FrameT* F) {
+  using FT = FrameTraits<FrameT>;
+  using PT = PointTraits<typename FT::point_type>;
+  const size_t n = FT::num_keypoints(F);
+  std::vector<uint8_t> st(n, LORB_SLOT_EMPTY);
+  for (size_t i = 0; i < n; ++i) {
+    auto* p = FT::map_point(F, i);
+    if (p) st[i] = PT::num_obs(p) > 0 ? LORB_SLOT_LOCKED : LORB_SLOT_FREE;
+  }
+  return st;
+}
+
+// ---- Matcher::SearchByProjection(Frame* curr, Frame* prev), src/matcher.cpp:13-62 ----------
+template <class FrameT>
+size_t SearchByProjectionBF(lorb_ctx* ctx, FrameT* curr, FrameT* prev) {
+  using FT = FrameTraits<FrameT>;
+  using P = typename FT::point_type;
+  using PT = PointTraits<P>;
+  std::vector<P*> prevMPs;
+  std::vector<uint8_t> tdesc;
+  for (size_t i = 0; i < FT::num_keypoints(prev); ++i) {
+    P* p = FT::map_point(prev, i);
+    if (!p) continue;
+    prevMPs.push_back(p);
+    tdesc.resize(tdesc.size() + 32);
+    PT::descriptor(p, &tdesc[tdesc.size() - 32]);
+  }
+  KeypointsSoA k = gather_keypoints(curr);
+  const int32_t nq = (int32_t)FT::num_keypoints(curr), nt = (int32_t)prevMPs.size();
+  const int32_t q_off[2] = {0, nq}, t_off[2] = {0, nt};
+  std::vector<int32_t> cc_t(nq + 1), cc_d(nq + 1), mt(nq + 1);
+  int32_t nm = 0;
+  check(ctx, lorb_bf_match(ctx, 1, k.desc.data(), q_off, tdesc.data(), t_off, cc_t.data(), cc_d.data(), mt.data(), &nm),
+        "lorb_bf_match");
+  for (int32_t q = 0; q < nq; ++q)
+    if (mt[q] >= 0) FT::set_map_point(curr, q, prevMPs[mt[q]]);
+  return (size_t)nm;
+}
+
+// ---- Matcher::SearchLocalPoints(Frame* curr, std::set<MapPoint*>), src/matcher.cpp:319-366 -
+template <class FrameT, class PointT>
+size_t SearchLocalPoints(lorb_ctx* ctx, FrameT* curr, const std::set<PointT*>& vpMPs) {
+  using FT = FrameTraits<FrameT>;
+  using PT = PointTraits<PointT>;
+  std::vector<PointT*> mps;
+  std::vector<uint8_t> tdesc;
+  for (PointT* p : vpMPs) {  // std::set iteration order (pointer order), src/matcher.cpp:327
+    if (!p) continue;
+    mps.push_back(p);
+    tdesc.resize(tdesc.size() + 32);
+    PT::descriptor(p, &tdesc[tdesc.size() - 32]);
+  }
+  KeypointsSoA k = gather_keypoints(curr);
+  const int32_t nq = (int32_t)FT::num_keypoints(curr), nt = (int32_t)mps.size();
+  const int32_t q_off[2] = {0, nq}, t_off[2] = {0, nt};
+  std::vector<int32_t> cc_t(nq + 1), cc_d(nq + 1), mt(nq + 1);
+  int32_t nm = 0;
+  check(ctx, lorb_bf_match(ctx, 1, k.desc.data(), q_off, tdesc.data(), t_off, cc_t.data(), cc_d.data(), mt.data(), &nm),
+        "lorb_bf_match");
+  for (int32_t q = 0; q < nq; ++q)
+    if (mt[q] >= 0) FT::set_map_point(curr, q, mps[mt[q]]);
+  return (size_t)nm;
+}
+
+template <class FrameT>
+lorb_frame_params frame_params(FrameT* F) {
+  using FT = FrameTraits<FrameT>;
+  lorb_frame_params fp;
+  std::memset(&fp, 0, sizeof(fp));
+  FT::params(F, &fp);
+  return fp;
+}
+
+// ---- Matcher::SearchByProjection(Frame* Cur, Frame* Last, const float th), src/matcher.cpp:64-218
+template <class FrameT>
+size_t SearchByProjectionFrame(lorb_ctx* ctx, FrameT* cur, FrameT* last, float th) {
+  using FT = FrameTraits<FrameT>;
+  using P = typename FT::point_type;
+  using PT = PointTraits<P>;
+  lorb_frame_params fp = frame_params(cur);
+  float Tcur[16], Tlast[16];
+  FT::Tcw(cur, Tcur);
+  FT::Tcw(last, Tlast);
+  KeypointsSoA k = gather_keypoints(cur);
+  std::vector<uint8_t> st = gather_slot_state(cur);
+  const size_t nl = FT::num_keypoints(last);
+  std::vector<uint8_t> has(nl, 0), out(nl, 0), lk(nl, 0), ldesc(32 * nl, 0);
+  std::vector<float> pos(3 * nl, 0.f), ang(nl, 0.f);
+  std::vector<int32_t> oct(nl, 0);
+  std::vector<P*> mps(nl, nullptr);
+  for (size_t i = 0; i < nl; ++i) {
+    P* p = FT::map_point(last, i);
+    float kx, ky;
+    FT::keypoint(last, i, &kx, &ky, &oct[i], &ang[i]);  // mvKeys == mvKeysUn (src/frame.cpp:358-362)
+    if (!p) continue;
+    mps[i] = p; has[i] = 1; out[i] = FT::outlier(last, i) ? 1 : 0;
+    lk[i] = PT::num_obs(p) > 0 ? 1 : 0;
+    PT::pos(p, &pos[3 * i]);
+    PT::descriptor(p, &ldesc[32 * i]);
+  }
+  lorb_last_frame L;
+  L.n = (int32_t)nl; L.Tcw = Tlast; L.has_mp = has.data(); L.outlier = out.data(); L.mp_locked = lk.data();
+  L.mp_pos = pos.data(); L.mp_desc = ldesc.data(); L.octave = oct.data(); L.angle = ang.data();
+  lorb_keypoints kv = k.view();
+  std::vector<int32_t> assign(kv.n + 1);
+  int32_t nm = 0;
+  check(ctx, lorb_search_by_projection_frame(ctx, &fp, Tcur, &kv, st.data(), &L, th, assign.data(), &nm),
+        "lorb_search_by_projection_frame");
+  for (int32_t j = 0; j < kv.n; ++j) {
+    if (assign[j] == LORB_ASSIGN_NULL) FT::set_map_point(cur, j, (P*)nullptr);
+    else if (assign[j] >= 0) FT::set_map_point(cur, j, mps[assign[j]]);
+  }
+  return (size_t)nm;
+}
+
+// ---- Matcher::SearchByProjection(Frame* F, const set<MapPoint*>&, th), src/matcher.cpp:220-316
+template <class FrameT, class PointT>
+size_t SearchByProjectionLocal(lorb_ctx* ctx, FrameT* F, const std::set<PointT*>& vpMapPoints, float th) {
+  using FT = FrameTraits<FrameT>;
+  using PT = PointTraits<PointT>;
+  lorb_frame_params fp = frame_params(F);
+  KeypointsSoA k = gather_keypoints(F);
+  std::vector<uint8_t> st = gather_slot_state(F);
+  const size_t n = vpMapPoints.size();
+  std::vector<PointT*> mps;
+  mps.reserve(n);
+  std::vector<uint8_t> iv, bad, lk, desc;
+  std::vector<float> px, py, pxr, vc;
+  std::vector<int32_t> lev;
+  for (PointT* p : vpMapPoints) {  // std::set iteration order, src/matcher.cpp:226
+    mps.push_back(p);
+    iv.push_back(PT::track_in_view(p) ? 1 : 0);
+    bad.push_back(PT::is_bad(p) ? 1 : 0);
+    lk.push_back(PT::num_obs(p) > 0 ? 1 : 0);
+    float t[5];
+    int l;
+    PT::tracking(p, t, &l);  // mTrackProjX/Y/XR, mTrackViewCos ; mnTrackScaleLevel
+    px.push_back(t[0]); py.push_back(t[1]); pxr.push_back(t[2]); vc.push_back(t[3]);
+    lev.push_back(iv.back() ? l : 0);
+    desc.resize(desc.size() + 32);
+    PT::descriptor(p, &desc[desc.size() - 32]);
+  }
+  lorb_local_points L;
+  L.n = (int32_t)n; L.track_in_view = iv.data(); L.is_bad = bad.data(); L.locked = lk.data();
+  L.proj_x = px.data(); L.proj_y = py.data(); L.proj_xr = pxr.data(); L.pred_level = lev.data();
+  L.view_cos = vc.data(); L.desc = desc.data();
+  lorb_keypoints kv = k.view();
+  std::vector<int32_t> assign(kv.n + 1);
+  int32_t nm = 0;
+  check(ctx, lorb_search_by_projection_local(ctx, &fp, &kv, st.data(), &L, th, assign.data(), &nm),
+        "lorb_search_by_projection_local");
+  for (int32_t j = 0; j < kv.n; ++j)
+    if (assign[j] >= 0) FT::set_map_point(F, j, mps[assign[j]]);
+  return (size_t)nm;
+}
+
+// ---- BA::ProjectPoseOptimization(Frame*), src/bundle_adjust.cpp:158-202 -------------------
+template <class FrameT>
+void ProjectPoseOptimization(lorb_ctx* ctx, FrameT* F) {
+  using FT = FrameTraits<FrameT>;
+  using P = typename FT::point_type;
+  using PT = PointTraits<P>;
+  std::vector<float> pts, obs;
+  for (size_t i = 0; i < FT::num_keypoints(F); ++i) {
+    P* p = FT::map_point(F, i);
+    if (!p) continue;
+    float X[3], x, y, a;
+    int o;
+    PT::pos(p, X);
+    FT::keypoint(F, i, &x, &y, &o, &a);  // GetKp2d(i) = mvKeysUn[i].pt
+    pts.insert(pts.end(), X, X + 3);
+    obs.push_back(x);
+    obs.push_back(y);
+  }
+  lorb_frame_params fp = frame_params(F);
+  float rt[6];
+  FT::pose_vectors(F, rt, rt + 3);  // mRvec, mTvec
+  const float intr[4] = {fp.fx, fp.fx /* PoseCost quirk: v uses fx, src/bundle_adjust.cpp:51 */, fp.cx, fp.cy};
+  const int32_t res_off[2] = {0, (int32_t)(obs.size() / 2)};
+  lorb_pose_problem_batch b;
+  b.n_frames = 1; b.res_off = res_off; b.intr = intr; b.pose_init = rt; b.pts3d = pts.data(); b.obs2d = obs.data();
+  lorb_lm_options opt;
+  lorb_lm_options_default(&opt);
+  double pose[6];
+  lorb_ba_summary s;
+  check(ctx, lorb_ba_pose_only(ctx, &b, &opt, pose, nullptr, &s), "lorb_ba_pose_only");
+  const float R[3] = {(float)pose[0], (float)pose[1], (float)pose[2]};
+  const float T[3] = {(float)pose[3], (float)pose[4], (float)pose[5]};
+  FT::set_pose(F, T, R);  // Frame::SetPose(T, R) -> Rodrigues -> mTcw (src/frame.cpp:577-594)
+}
+
+// ---- BA::LocalPoseOptimization(Frame*), src/bundle_adjust.cpp:207-330 ---------------------
+// Observation source: the reference reads GetKps2d()[idx] (src/bundle_adjust.cpp:285,295),
+// which is empty on the live path (UB); we use GetKp2d(idx) as ProjectPoseOptimization does
+// (the one intentional divergence).
+template <class FrameT>
+void LocalPoseOptimization(lorb_ctx* ctx, FrameT* cur) {
+  using FT = FrameTraits<FrameT>;
+  using P = typename FT::point_type;
+  using PT = PointTraits<P>;
+  std::vector<FrameT*> frames{cur};
+  for (FrameT* f : FT::covisible_frames(cur))
+    if (!FT::is_bad(f)) frames.push_back(f);
+  std::map<FrameT*, int> frame_idx;
+  for (size_t i = 0; i < frames.size(); ++i) frame_idx.emplace(frames[i], (int)i);
+  std::vector<P*> points;  // union in first-seen order (std::find dedup, :224-241)
+  std::set<P*> seen;
+  for (FrameT* f : frames)
+    for (size_t i = 0; i < FT::num_keypoints(f); ++i) {
+      P* p = FT::map_point(f, i);
+      if (!p || PT::is_bad(p)) continue;
+      if (seen.insert(p).second) points.push_back(p);
+    }
+  std::vector<float> pose_init(6 * frames.size()), point_init(3 * points.size()), fixed, uv;
+  for (size_t i = 0; i < frames.size(); ++i) FT::pose_vectors(frames[i], &pose_init[6 * i], &pose_init[6 * i + 3]);
+  std::vector<int32_t> op, of;
+  std::map<FrameT*, int> fixed_idx;
+  for (size_t pi = 0; pi < points.size(); ++pi) {
+    P* p = points[pi];
+    PT::pos(p, &point_init[3 * pi]);
+    for (auto& ob : PT::observations(p)) {  // std::map<Frame*, size_t> order
+      FrameT* f = ob.first;
+      if (FT::is_bad(f)) continue;
+      float x, y, a;
+      int o;
+      FT::keypoint(f, ob.second, &x, &y, &o, &a);
+      auto it = frame_idx.find(f);
+      int code;
+      if (it != frame_idx.end()) {
+        code = it->second;
+      } else {
+        auto jt = fixed_idx.find(f);
+        if (jt == fixed_idx.end()) {
+          jt = fixed_idx.emplace(f, (int)fixed_idx.size()).first;
+          fixed.resize(fixed.size() + 6);
+          FT::pose_vectors(f, &fixed[fixed.size() - 6], &fixed[fixed.size() - 3]);
+        }
+        code = -1 - jt->second;
+      }
+      op.push_back((int32_t)pi);
+      of.push_back(code);
+      uv.push_back(x);
+      uv.push_back(y);
+    }
+  }
+  lorb_frame_params fp = frame_params(cur);
+  lorb_ba_window w;
+  w.n_poses = (int32_t)frames.size(); w.n_fixed = (int32_t)fixed_idx.size();
+  w.n_points = (int32_t)points.size(); w.n_obs = (int32_t)op.size();
+  w.fx = fp.fx; w.fy = fp.fy; w.cx = fp.cx; w.cy = fp.cy;
+  w.pose_init = pose_init.data(); w.fixed_pose = fixed.data(); w.point_init = point_init.data();
+  w.obs_point = op.data(); w.obs_frame = of.data(); w.obs_uv = uv.data();
+  lorb_lm_options opt;
+  lorb_lm_options_default(&opt);
+  std::vector<double> po(6 * frames.size() + 1), pt(3 * points.size() + 1);
+  double* pp = po.data();
+  double* qq = pt.data();
+  lorb_ba_summary s;
+  check(ctx, lorb_ba_local(ctx, 1, &w, &opt, &pp, &qq, &s), "lorb_ba_local");
+  for (size_t i = 0; i < frames.size(); ++i) {  // float write-back, :317-329
+    const float R[3] = {(float)po[6 * i], (float)po[6 * i + 1], (float)po[6 * i + 2]};
+    const float T[3] = {(float)po[6 * i + 3], (float)po[6 * i + 4], (float)po[6 * i + 5]};
+    FT::set_pose(frames[i], T, R);
+  }
+  for (size_t i = 0; i < points.size(); ++i) {
+    const float X[3] = {(float)pt[3 * i], (float)pt[3 * i + 1], (float)pt[3 * i + 2]};
+    PT::set_pos(points[i], X);
+  }
+}
+
+}  // namespace lorb

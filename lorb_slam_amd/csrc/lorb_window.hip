@@ -486,7 +486,8 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
   if (nk < 0 || np < 0) return lorb::set_error(ctx, LORB_E_INVALID, "negative sizes");
   if (nk == 0) { *nmatches = 0; return LORB_OK; }
   for (int i = 0; i < np; ++i)
-    if (pts->pred_level[i] < 0 || pts->pred_level[i] >= LORB_MAX_LEVELS)
+    if (pts->track_in_view[i] && !(pts->is_bad && pts->is_bad[i]) &&
+        (pts->pred_level[i] < 0 || pts->pred_level[i] >= LORB_MAX_LEVELS))
       return lorb::set_error(ctx, LORB_E_INVALID, "point %d: predicted level %d out of range", i, pts->pred_level[i]);
   KpDev K;
   LORB_TRY(upload_kps(ctx, kps, slot_state, S_KP, &K, frame));

@@ -1,0 +1,297 @@
+// tests/cpp/test_adapters.cpp -- the C++ host layer (include/lorb/adapters.hpp,
+// local_mapping.hpp) driven exactly like the reference's VisualOdometry drives Matcher / BA /
+// LocalMapping, with plain test frames standing in for Simple_ORB_SLAM::Frame/MapPoint.  Every
+// GPU result is checked against the oracle (test infrastructure, linked only here).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <set>
+#include <thread>
+#include <vector>
+
+#include "../../include/lorb/adapters.hpp"
+#include "../../include/lorb/local_mapping.hpp"
+#include "../../oracle/lorb_oracle.h"
+
+struct MiniFrame;
+struct MiniPoint {
+  float pos[3];
+  uint8_t desc[32];
+  size_t nobs = 0;
+  bool bad = false;
+  bool in_view = false;
+  float proj[4] = {0, 0, 0, 0};  // x, y, xr, viewcos
+  int level = 0;
+  std::map<MiniFrame*, size_t> obs;
+  size_t first_id = 0;
+};
+struct MiniFrame {
+  size_t id = 0;
+  std::vector<float> x, y, angle, uR;
+  std::vector<int> octave;
+  std::vector<uint8_t> desc;
+  std::vector<MiniPoint*> mps;
+  std::vector<bool> outlier;
+  float Tcw[16];
+  float rvec[3] = {0, 0, 0}, tvec[3] = {0, 0, 0};
+  lorb_frame_params fp;
+  std::vector<MiniFrame*> covis;
+  bool bad = false;
+};
+struct MiniMap {
+  std::vector<MiniFrame*> frames;
+};
+
+namespace lorb {
+template <> struct FrameTraits<MiniFrame> {
+  using point_type = MiniPoint;
+  static size_t num_keypoints(MiniFrame* f) { return f->x.size(); }
+  static void keypoint(MiniFrame* f, size_t i, float* x, float* y, int* o, float* a) {
+    *x = f->x[i]; *y = f->y[i]; *o = f->octave[i]; *a = f->angle[i];
+  }
+  static void descriptor(MiniFrame* f, size_t i, uint8_t* d) { memcpy(d, &f->desc[32 * i], 32); }
+  static bool has_right(MiniFrame* f) { return !f->uR.empty(); }
+  static float u_right(MiniFrame* f, size_t i) { return f->uR[i]; }
+  static MiniPoint* map_point(MiniFrame* f, size_t i) { return f->mps[i]; }
+  static void set_map_point(MiniFrame* f, size_t i, MiniPoint* p) { f->mps[i] = p; }
+  static bool outlier(MiniFrame* f, size_t i) { return f->outlier[i]; }
+  static void params(MiniFrame* f, lorb_frame_params* fp) { *fp = f->fp; }
+  static void Tcw(MiniFrame* f, float* T) { memcpy(T, f->Tcw, sizeof(f->Tcw)); }
+  static void pose_vectors(MiniFrame* f, float* r, float* t) { memcpy(r, f->rvec, 12); memcpy(t, f->tvec, 12); }
+  static void set_pose(MiniFrame* f, const float* t, const float* r) {
+    memcpy(f->rvec, r, 12); memcpy(f->tvec, t, 12);
+    lorb_pose_to_Tcw(r, t, f->Tcw);
+  }
+  static std::vector<MiniFrame*> covisible_frames(MiniFrame* f) { return f->covis; }
+  static bool is_bad(MiniFrame* f) { return f->bad; }
+  static size_t id(MiniFrame* f) { return f->id; }
+  static void update_connections(MiniFrame*) {}
+  static void map_add_frame(MiniMap* m, MiniFrame* f) { m->frames.push_back(f); }
+};
+template <> struct PointTraits<MiniPoint> {
+  static size_t num_obs(MiniPoint* p) { return p->nobs; }
+  static void descriptor(MiniPoint* p, uint8_t* d) { memcpy(d, p->desc, 32); }
+  static void pos(MiniPoint* p, float* X) { memcpy(X, p->pos, 12); }
+  static void set_pos(MiniPoint* p, const float* X) { memcpy(p->pos, X, 12); }
+  static bool is_bad(MiniPoint* p) { return p->bad; }
+  static bool track_in_view(MiniPoint* p) { return p->in_view; }
+  static void tracking(MiniPoint* p, float* t, int* l) { memcpy(t, p->proj, 16); *l = p->level; }
+  static std::map<MiniFrame*, size_t> observations(MiniPoint* p) { return p->obs; }
+  static bool is_in_frame(MiniPoint* p, MiniFrame* f) { return p->obs.count(f) > 0; }
+  static void add_observation(MiniPoint* p, MiniFrame* f, size_t i) {
+    if (p->obs.count(f)) return;
+    p->obs[f] = i; p->nobs++;
+  }
+  static float found_ratio(MiniPoint*) { return 1.0f; }
+  static void set_bad(MiniPoint* p) { p->bad = true; }
+  static size_t first_frame_id(MiniPoint* p) { return p->first_id; }
+};
+}  // namespace lorb
+
+static uint64_t s_rng = 0x9E3779B97F4A7C15ull;
+static uint32_t rnd() { s_rng ^= s_rng << 13; s_rng ^= s_rng >> 7; s_rng ^= s_rng << 17; return (uint32_t)(s_rng >> 11); }
+static float urand(float a, float b) { return a + (b - a) * (float)(rnd() & 0xffffff) / 16777216.0f; }
+
+static lorb_frame_params make_fp() {
+  lorb_frame_params fp;
+  memset(&fp, 0, sizeof(fp));
+  fp.fx = fp.fy = 435.2f; fp.cx = 367.5f; fp.cy = 252.2f; fp.bf = 47.9f; fp.b = fp.bf / fp.fx;
+  fp.min_x = 0; fp.max_x = 752; fp.min_y = 0; fp.max_y = 480;
+  fp.grid_w_inv = 64.0f / 752.0f; fp.grid_h_inv = 48.0f / 480.0f;
+  fp.n_levels = 8; fp.log_scale_factor = logf(1.2f);
+  float s = 1.0f;
+  for (int i = 0; i < 8; i++) { fp.scale_factors[i] = s; s *= 1.2f; }
+  return fp;
+}
+
+static void project(const float* T, const float* X, const lorb_frame_params& fp, float* u, float* v) {
+  float Xc[3];
+  for (int r = 0; r < 3; r++) Xc[r] = T[4 * r] * X[0] + T[4 * r + 1] * X[1] + T[4 * r + 2] * X[2] + T[4 * r + 3];
+  *u = fp.fx * Xc[0] / Xc[2] + fp.cx;
+  *v = fp.fy * Xc[1] / Xc[2] + fp.cy;
+}
+
+static MiniFrame* make_frame(size_t id, int n, const float r[3], const float t[3]) {
+  MiniFrame* f = new MiniFrame();
+  f->id = id;
+  f->fp = make_fp();
+  memcpy(f->rvec, r, 12); memcpy(f->tvec, t, 12);
+  lorb_pose_to_Tcw(r, t, f->Tcw);
+  for (int i = 0; i < n; i++) {
+    f->x.push_back(urand(0, 752)); f->y.push_back(urand(0, 480));
+    f->angle.push_back(urand(0, 360)); f->octave.push_back((int)(rnd() % 8) < 4 ? 0 : (int)(rnd() % 8));
+    f->uR.push_back(rnd() % 3 == 0 ? f->x.back() - urand(3, 20) : -1.0f);
+    for (int b = 0; b < 32; b++) f->desc.push_back((uint8_t)rnd());
+  }
+  f->mps.assign(n, nullptr);
+  f->outlier.assign(n, false);
+  return f;
+}
+
+static int g_fail = 0;
+#define EXPECT(c, ...) do { if (!(c)) { printf("FAIL %s:%d: ", __FILE__, __LINE__); printf(__VA_ARGS__); printf("\n"); g_fail++; } } while (0)
+
+int main() {
+  lorb_ctx* ctx = lorb::thread_ctx(0);
+  const int N = 800;
+  const float r0[3] = {0, 0, 0}, t0[3] = {0, 0, 0};
+  const float r1[3] = {0.01f, -0.005f, 0.002f}, t1[3] = {0.05f, 0.0f, 0.02f};
+  MiniFrame* last = make_frame(1, N, r0, t0);
+  // map points in the last frame, re-observed in the current one
+  std::vector<MiniPoint*> pts;
+  for (int i = 0; i < N; i++) {
+    if (rnd() % 2) continue;
+    MiniPoint* p = new MiniPoint();
+    p->pos[0] = urand(-5, 5); p->pos[1] = urand(-3, 3); p->pos[2] = urand(2, 10);
+    memcpy(p->desc, &last->desc[32 * i], 32);
+    p->nobs = rnd() % 2;
+    p->obs[last] = (size_t)i;
+    last->mps[i] = p;
+    float u, v;
+    project(last->Tcw, p->pos, last->fp, &u, &v);
+    last->x[i] = u; last->y[i] = v;
+    pts.push_back(p);
+  }
+  MiniFrame* cur = make_frame(2, N, r1, t1);
+  int k = 0;
+  for (MiniPoint* p : pts) {
+    float u, v;
+    project(cur->Tcw, p->pos, cur->fp, &u, &v);
+    if (u < 0 || u >= 752 || v < 0 || v >= 480 || k >= N) continue;
+    cur->x[k] = u + urand(-0.5f, 0.5f); cur->y[k] = v + urand(-0.5f, 0.5f);
+    memcpy(&cur->desc[32 * k], p->desc, 32);
+    cur->desc[32 * k + (rnd() % 32)] ^= (uint8_t)(1u << (rnd() % 8));
+    k++;
+  }
+
+  // ---- Matcher::SearchByProjection(curr, last, 15): adapter (GPU) vs oracle -------------
+  {
+    lorb::KeypointsSoA ks = lorb::gather_keypoints(cur);
+    lorb_keypoints kv = ks.view();
+    std::vector<uint8_t> st = lorb::gather_slot_state(cur);
+    const size_t nl = last->x.size();
+    std::vector<uint8_t> has(nl), out(nl, 0), lk(nl), ld(32 * nl);
+    std::vector<float> pos(3 * nl), ang(last->angle);
+    std::vector<int32_t> oct(last->octave.begin(), last->octave.end());
+    for (size_t i = 0; i < nl; i++) {
+      MiniPoint* p = last->mps[i];
+      has[i] = p != nullptr;
+      if (!p) continue;
+      lk[i] = p->nobs > 0;
+      memcpy(&pos[3 * i], p->pos, 12);
+      memcpy(&ld[32 * i], p->desc, 32);
+    }
+    lorb_last_frame L{(int32_t)nl, last->Tcw, has.data(), out.data(), lk.data(), pos.data(), ld.data(), oct.data(), ang.data()};
+    std::vector<int32_t> assign(N);
+    int32_t nm_o = 0;
+    or_search_by_projection_frame(&cur->fp, cur->Tcw, &kv, st.data(), &L, 15.0f, assign.data(), &nm_o);
+    const size_t nm_g = lorb::SearchByProjectionFrame(ctx, cur, last, 15.0f);
+    EXPECT((int)nm_g == nm_o, "frame match count gpu %zu oracle %d", nm_g, nm_o);
+    int mism = 0;
+    for (int j = 0; j < N; j++) {
+      MiniPoint* want = assign[j] >= 0 ? last->mps[assign[j]] : nullptr;
+      if (cur->mps[j] != want) mism++;
+    }
+    EXPECT(mism == 0, "frame match: %d slot mismatches", mism);
+    printf("SearchByProjection(frame): %zu matches\n", nm_g);
+  }
+
+  // ---- BA::ProjectPoseOptimization(curr) -------------------------------------------------
+  {
+    std::vector<float> P3, P2;
+    for (int j = 0; j < N; j++)
+      if (cur->mps[j]) { P3.insert(P3.end(), cur->mps[j]->pos, cur->mps[j]->pos + 3); P2.push_back(cur->x[j]); P2.push_back(cur->y[j]); }
+    float pinit[6] = {0, 0, 0, 0, 0, 0};  // the caller's initial pose (prev pose * motion model)
+    memcpy(cur->rvec, pinit, 12); memcpy(cur->tvec, pinit + 3, 12);
+    const float intr[4] = {cur->fp.fx, cur->fp.fx, cur->fp.cx, cur->fp.cy};
+    const int32_t ro[2] = {0, (int32_t)(P2.size() / 2)};
+    lorb_pose_problem_batch b{1, ro, intr, pinit, P3.data(), P2.data()};
+    lorb_lm_options opt;
+    lorb_lm_options_default(&opt);
+    double po[6];
+    float To[16];
+    or_ba_pose_only(&b, &opt, po, To, nullptr);
+    lorb::ProjectPoseOptimization(ctx, cur);
+    double md = 0;
+    for (int i = 0; i < 3; i++) {
+      md = std::max(md, (double)fabsf(cur->rvec[i] - (float)po[i]) / std::max(1.0, fabs(po[i])));
+      md = std::max(md, (double)fabsf(cur->tvec[i] - (float)po[3 + i]) / std::max(1.0, fabs(po[3 + i])));
+    }
+    EXPECT(md <= 1e-5, "pose-only BA rel diff %g", md);
+    printf("ProjectPoseOptimization: t = %.5f %.5f %.5f (max rel diff %.2e)\n", cur->tvec[0], cur->tvec[1], cur->tvec[2], md);
+  }
+
+  // ---- LocalMapping: queue processed by the mapper thread, reference wiring --------------
+  {
+    MiniMap map;
+    lorb::LocalMapping<MiniFrame, MiniMap> lm(&map);
+    std::thread th([&] { lm.Run(); });
+    lm.InsertKeyFrame(last);
+    lm.InsertKeyFrame(cur);
+    for (int i = 0; i < 2000 && lm.processed() < 2; i++) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    lm.RequestFinish();
+    th.join();
+    EXPECT(map.frames.size() == 2 && map.frames[0] == last && map.frames[1] == cur, "LocalMapping queue order");
+    printf("LocalMapping: processed %zu keyframes\n", lm.processed());
+  }
+
+  // ---- BA::LocalPoseOptimization(curr) through the covisibility window --------------------
+  {
+    // every point observed by both frames; last is fixed (not covisible => MPCost)
+    for (int j = 0; j < N; j++) {
+      MiniPoint* p = cur->mps[j];
+      if (p && !p->obs.count(cur)) { p->obs[cur] = (size_t)j; p->nobs++; }
+    }
+    cur->covis.clear();
+    // oracle: gather the same window by hand
+    std::vector<MiniPoint*> wp;
+    std::set<MiniPoint*> seen;
+    for (int j = 0; j < N; j++)
+      if (cur->mps[j] && seen.insert(cur->mps[j]).second) wp.push_back(cur->mps[j]);
+    std::vector<float> pi(cur->rvec, cur->rvec + 3), fx(last->rvec, last->rvec + 3), X, uv;
+    pi.insert(pi.end(), cur->tvec, cur->tvec + 3);
+    fx.insert(fx.end(), last->tvec, last->tvec + 3);
+    std::vector<int32_t> op, of;
+    for (size_t q = 0; q < wp.size(); q++) {
+      X.insert(X.end(), wp[q]->pos, wp[q]->pos + 3);
+      for (auto& ob : wp[q]->obs) {
+        op.push_back((int32_t)q);
+        of.push_back(ob.first == cur ? 0 : -1);
+        uv.push_back(ob.first->x[ob.second]); uv.push_back(ob.first->y[ob.second]);
+      }
+    }
+    lorb_ba_window w{1, 1, (int32_t)wp.size(), (int32_t)op.size(), cur->fp.fx, cur->fp.fy, cur->fp.cx, cur->fp.cy,
+                     pi.data(), fx.data(), X.data(), op.data(), of.data(), uv.data()};
+    lorb_lm_options opt;
+    lorb_lm_options_default(&opt);
+    std::vector<double> po(6), ppt(3 * wp.size());
+    double* a = po.data();
+    double* bpt = ppt.data();
+    or_ba_local(1, &w, &opt, &a, &bpt, nullptr);
+    lorb::LocalPoseOptimization(ctx, cur);
+    double md = 0;
+    for (size_t q = 0; q < wp.size(); q++)
+      for (int i = 0; i < 3; i++)
+        md = std::max(md, fabs((double)wp[q]->pos[i] - (double)(float)ppt[3 * q + i]) / std::max(1.0, fabs(ppt[3 * q + i])));
+    EXPECT(md <= 1e-5, "local BA point rel diff %g", md);
+    printf("LocalPoseOptimization: %zu points, %zu obs (max rel diff %.2e)\n", wp.size(), op.size(), md);
+  }
+
+  // ---- Matcher::SearchLocalPoints(curr, set) ------------------------------------------------
+  {
+    std::set<MiniPoint*> s(pts.begin(), pts.end());
+    std::vector<uint8_t> tdesc;
+    for (MiniPoint* p : s) tdesc.insert(tdesc.end(), p->desc, p->desc + 32);
+    lorb::KeypointsSoA ks = lorb::gather_keypoints(cur);
+    std::vector<int32_t> a(N), b(N), c(N);
+    const int no = or_bf_match(ks.desc.data(), N, tdesc.data(), (int)s.size(), a.data(), b.data(), c.data());
+    for (auto& mp : cur->mps) mp = nullptr;
+    const size_t ng = lorb::SearchLocalPoints(ctx, cur, s);
+    EXPECT((int)ng == no, "SearchLocalPoints gpu %zu oracle %d", ng, no);
+    printf("SearchLocalPoints: %zu matches\n", ng);
+  }
+
+  printf(g_fail ? "RESULT FAIL (%d)\n" : "RESULT PASS\n", g_fail);
+  return g_fail ? 1 : 0;
+}
