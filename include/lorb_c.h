@@ -317,6 +317,8 @@ int lorb_ba_plan_solve(lorb_ba_plan* plan, const lorb_lm_options* opt);
 int lorb_ba_plan_read(lorb_ba_plan* plan, double* const* pose_out, double* const* point_out,
                       lorb_ba_summary* summaries);
 int lorb_ba_plan_destroy(lorb_ba_plan* plan);
+/* diagnostics: Cholesky phase stamps of window 0 (non-zero only in LORB_CHOL_STAMPS builds) */
+int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8);
 
 /* Rodrigues vector -> Tcw (float), cv::Rodrigues semantics (double internally). */
 void lorb_pose_to_Tcw(const float rvec[3], const float tvec[3], float Tcw[16]);

@@ -146,6 +146,7 @@ struct BaDev {
   double* rhs;               // sum n
   double* ycam;              // sum n (solution, scaled space, y = -step)
   double* part;              // n_pblk * 8 partials
+  unsigned long long* dbg;   // diagnostic stamps (LORB_CHOL_STAMPS builds only)
   double* opart;             // n_oblk * 4 partials
   WinState* st;
 };
@@ -511,6 +512,7 @@ template <bool IN_LDS, int RPL>
 __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_fail;
+  __shared__ __attribute__((aligned(16))) double s_col[80];
   const int w = blockIdx.x;
   if (d.st[w].done) return;
   const BaWin W = d.win[w];
@@ -531,7 +533,14 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   }
   if (t == 0) s_fail = 0;
   __syncthreads();
+#ifdef LORB_CHOL_STAMPS
+  const unsigned long long T0 = __builtin_amdgcn_s_memtime();
+  unsigned long long tst0 = 0, tst_panel = 0, tst_trail = 0;
+#endif
   for (int kb = 0; kb < n; kb += NB) {
+#ifdef LORB_CHOL_STAMPS
+    if (t == 0 && kb == 0) { d.dbg[8 * w] = __builtin_amdgcn_s_memtime() - T0; tst0 = __builtin_amdgcn_s_memtime(); }
+#endif
     const int ke = min(kb + NB, n);
     const int rlast = min(n - 1, ke - 1 + bw);
     if (wv == 0) {
@@ -562,8 +571,14 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
               const int row = kb + lane + 64 * r;
               if (row > k) P[r][q] *= y;
             }
-            if (lane == q) { P[0][q] = akk * y; zr[0] *= y; invd[k] = y; }
-            const double zk = readlane_d(zr[0], q);
+            if (lane == q) { P[0][q] = akk * y; zr[0] *= y; invd[k] = y; s_col[64] = zr[0]; }
+            // broadcast the column head L(kb+q2, k) and z_k through LDS (one write, wide reads)
+            s_col[lane] = P[0][q];
+            wave_sync_lds();
+            const double zk = s_col[64];
+            double l[NB];
+#pragma unroll
+            for (int q2 = q + 1; q2 < NB; ++q2) l[q2] = s_col[q2];
 #pragma unroll
             for (int r = 0; r < RPL; ++r) {
               const int row = kb + lane + 64 * r;
@@ -571,13 +586,13 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
             }
 #pragma unroll
             for (int q2 = q + 1; q2 < NB; ++q2) {
-              const double l = readlane_d(P[0][q], q2);  // L(kb+q2, k)
 #pragma unroll
               for (int r = 0; r < RPL; ++r) {
                 const int row = kb + lane + 64 * r;
-                if (row >= kb + q2) P[r][q2] -= P[r][q] * l;
+                if (row >= kb + q2) P[r][q2] -= P[r][q] * l[q2];
               }
             }
+            wave_sync_lds();  // all reads of s_col done before the next column overwrites it
           }
         }
       }
@@ -597,26 +612,43 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
     }
     __syncthreads();
     if (s_fail) break;
+#ifdef LORB_CHOL_STAMPS
+    if (t == 0) { const unsigned long long q_ = __builtin_amdgcn_s_memtime(); tst_panel += q_ - tst0; tst0 = q_; }
+#endif
     // trailing update: rows i, cols j in [ke, rlast], j <= i, k in [max(kb, i-bw), ke)
+    // Branch-free: li[q] = 0 wherever L(i, kb+q) is outside the band or the panel, and every
+    // band(A, j, kb+q) read is an in-bounds finite entry (a neighbouring band element when the
+    // pair is outside the band), so the masked terms contribute exactly 0.  Only full panels
+    // have trailing rows (the last panel ends at n).
     for (int i = ke + (t >> 2); i <= rlast; i += 64) {
       const int k0 = max(kb, i - bw);
       double li[NB];
 #pragma unroll
-      for (int q = 0; q < NB; ++q) li[q] = (kb + q >= k0 && kb + q < ke) ? band(A, bw, i, kb + q) : 0.0;
+      for (int q = 0; q < NB; ++q) {
+        const bool ok = kb + q >= k0 && kb + q < ke;
+        li[q] = band(A, bw, i, ok ? kb + q : i);
+        li[q] = ok ? li[q] : 0.0;
+      }
       for (int j = ke + (t & 3); j <= i; j += 4) {
+        const double* Aj = A + (size_t)j * (bw + 1) + (kb - j + bw);
         double acc = 0.0;
 #pragma unroll
-        for (int q = 0; q < NB; ++q)
-          if (kb + q >= k0 && kb + q < ke) acc += li[q] * band(A, bw, j, kb + q);
+        for (int q = 0; q < NB; ++q) acc += li[q] * Aj[q];
         band(A, bw, i, j) -= acc;
       }
     }
     __syncthreads();
+#ifdef LORB_CHOL_STAMPS
+    if (t == 0) { const unsigned long long q_ = __builtin_amdgcn_s_memtime(); tst_trail += q_ - tst0; tst0 = q_; }
+#endif
   }
   if (s_fail) {
     if (t == 0) d.st[w].chol_fail = 1;
     return;
   }
+#ifdef LORB_CHOL_STAMPS
+  if (t == 0) { d.dbg[8 * w + 2] = tst_trail; d.dbg[8 * w + 1] = tst_panel; }
+#endif
   // back substitution L^T y = z, 64-row register blocks from the bottom (wave 0)
   if (wv == 0) {
     for (int bb = ((n - 1) / 64) * 64; bb >= 0; bb -= 64) {
@@ -643,6 +675,9 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   }
   __syncthreads();
   for (int k = t; k < n; k += 256) d.ycam[W.row_base + k] = z[k];
+#ifdef LORB_CHOL_STAMPS
+  if (t == 0) { d.dbg[8 * w + 3] = __builtin_amdgcn_s_memtime() - T0 - d.dbg[8*w] - d.dbg[8*w+1] - d.dbg[8*w+2]; }
+#endif
 }
 
 // K7: per-point back-substitution, candidate point, model cost change and candidate cost
@@ -1161,6 +1196,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   LORB_TRY(dalloc(P, (size_t)P->env_total, &d.env)); LORB_TRY(dalloc(P, (size_t)P->n_total, &d.rhs));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
   LORB_TRY(dalloc(P, (size_t)P->n_oblk * 4, &d.opart));
+  LORB_TRY(dalloc(P, (size_t)nw * 8, &d.dbg));
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
   if (!obs_cam.empty()) { /* keep obs arrays alive via allocs */ }
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -1300,6 +1336,14 @@ int lorb_ba_plan_read(lorb_ba_plan* plan, double* const* pose_out, double* const
   if (!plan) return LORB_E_INVALID;
   if (plan->W == 0) return LORB_OK;
   return plan_read(plan, pose_out, point_out, summaries);
+}
+
+// diagnostic: copy the Cholesky phase stamps of window 0 (LORB_CHOL_STAMPS builds)
+int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8) {
+  if (!plan || !out8) return LORB_E_INVALID;
+  LORB_HIP(plan->ctx, hipMemcpyAsync(out8, plan->dev.dbg, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, plan->ctx->stream));
+  LORB_HIP(plan->ctx, hipStreamSynchronize(plan->ctx->stream));
+  return LORB_OK;
 }
 
 int lorb_ba_plan_destroy(lorb_ba_plan* plan) {

@@ -11,7 +11,7 @@ import numpy as np
 from . import _abi as A
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblorb.so")
+LIB_PATH = os.environ.get("LORB_LIB_PATH") or os.path.join(_HERE, "liblorb.so")  # override: diagnostics only
 _lib = None
 
 
