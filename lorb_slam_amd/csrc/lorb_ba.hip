@@ -405,6 +405,8 @@ __global__ __launch_bounds__(kPB) void k_ba_point_prep(BaDev d, LMOpt o) {
   }
 }
 
+typedef double v4d __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ double& band(double* A, int bw, int i, int j) {
   return A[(size_t)i * (bw + 1) + (j - i + bw)];
 }
@@ -508,6 +510,40 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // forward substitution fused in; rsqrt-refined pivots keep IEEE div/sqrt off the critical
 // path.  All four waves then apply the rank-NB trailing update from LDS.
 constexpr int NB = 16;
+
+// One 16x16 tile (I, J) of the panel's trailing update (SYRK): A(i, j) -= sum_k L(i, k) L(j, k)
+// for ke <= j <= i <= rlast, k in [kb, kb + NB), on v_mfma_f64_16x16x4f64 (K = NB = 4 MFMAs).
+// Operand lane l holds row (l & 15), k = l >> 4; accumulator register r holds row
+// 4r + (l >> 4), column l & 15.  Entries outside the band / triangle are fed as 0 and never
+// stored.
+__device__ __forceinline__ void chol_trail_tile(double* A, int bw, int kb, int ke, int rlast,
+                                                int I, int J, int lane) {
+  if (16 * (I - J) - 15 > bw) return;  // tile entirely outside the band
+  const int ci = lane & 15, ck = lane >> 4;
+  const int i0 = ke + 16 * I, j0 = ke + 16 * J;
+  v4d acc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + ck + 4 * r, j = j0 + ci;
+    const bool ok = i <= rlast && j <= i && i - j <= bw;
+    const double v = band(A, bw, ok ? i : ke, ok ? j : ke);
+    acc[r] = ok ? v : 0.0;
+  }
+#pragma unroll
+  for (int kk = 0; kk < NB / 4; ++kk) {
+    const int k = kb + 4 * kk + ck;
+    const int ia = i0 + ci, jb = j0 + ci;
+    const bool oka = ia <= rlast && ia - k <= bw, okb = jb <= rlast && jb - k <= bw;
+    const double a = band(A, bw, oka ? ia : k, k), b = band(A, bw, okb ? jb : k, k);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(oka ? -a : 0.0, okb ? b : 0.0, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + ck + 4 * r, j = j0 + ci;
+    if (i <= rlast && j <= i && i - j <= bw) band(A, bw, i, j) = acc[r];
+  }
+}
+
 template <bool IN_LDS, int RPL>
 __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -537,12 +573,24 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   const unsigned long long T0 = __builtin_amdgcn_s_memtime();
   unsigned long long tst0 = 0, tst_panel = 0, tst_trail = 0;
 #endif
+  // Lookahead: panel p's trailing update is split into the tiles covering panel p+1's columns
+  // (J = 0, all four waves, before panel p+1) and the rest (J >= 1), which waves 1-3 apply
+  // while wave 0 factors panel p+1 -- they touch disjoint columns.
+  int pkb = -1, pke = 0, prl = 0;  // previous panel (deferred tiles), pkb < 0: none
   for (int kb = 0; kb < n; kb += NB) {
 #ifdef LORB_CHOL_STAMPS
     if (t == 0 && kb == 0) { d.dbg[8 * w] = __builtin_amdgcn_s_memtime() - T0; tst0 = __builtin_amdgcn_s_memtime(); }
 #endif
     const int ke = min(kb + NB, n);
     const int rlast = min(n - 1, ke - 1 + bw);
+    if (wv != 0 && pkb >= 0) {
+      const int m = ((prl - pke + 1 + 15) >> 4) - 1;  // J >= 1 tiles: triangle of side m
+      for (int tt = wv - 1; tt < m * (m + 1) / 2; tt += 3) {
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= tt) ++I;
+        chol_trail_tile(A, bw, pkb, pke, prl, I + 1, tt - I * (I + 1) / 2 + 1, lane);
+      }
+    }
     if (wv == 0) {
       double P[RPL][NB], zr[RPL];
 #pragma unroll
@@ -557,6 +605,34 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
         zr[r] = vr ? z[row] : 0.0;
       }
       bool bad = false;
+      if (ke - kb == NB) {
+        // Full panel: one basic block (no per-column branches, pivots via v_readlane), so the
+        // compiler can overlap column q+1's pivot chain with column q's bulk updates.  A
+        // non-positive pivot turns into NaNs that are never stored: `bad` aborts below.
+        // Lanes l < q hold finished or upper-triangle garbage in P[0][q..]; those entries are
+        // never read as a pivot/head and never stored, so only z needs masking.
+        double yq = 0.0;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          const double akk = readlane_d(P[0][q], q);
+          bad |= !(akk > 0.0);
+          const double y = rsqrt_refined(akk);
+#pragma unroll
+          for (int r = 0; r < RPL; ++r) P[r][q] *= y;  // lane q: akk * y = L(k, k)
+          yq = lane == q ? y : yq;
+          const double zk = readlane_d(zr[0], q) * y;
+          zr[0] = lane > q ? fma(-P[0][q], zk, zr[0]) : (lane == q ? zk : zr[0]);
+#pragma unroll
+          for (int r = 1; r < RPL; ++r) zr[r] = fma(-P[r][q], zk, zr[r]);
+#pragma unroll
+          for (int q2 = q + 1; q2 < NB; ++q2) {
+            const double l = readlane_d(P[0][q], q2);
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) P[r][q2] = fma(-P[r][q], l, P[r][q2]);
+          }
+        }
+        if (lane < NB) invd[kb + lane] = yq;
+      } else {
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
         const int k = kb + q;
@@ -596,6 +672,7 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
           }
         }
       }
+      }
 #pragma unroll
       for (int r = 0; r < RPL; ++r) {
         const int row = kb + lane + 64 * r;
@@ -615,27 +692,11 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
 #ifdef LORB_CHOL_STAMPS
     if (t == 0) { const unsigned long long q_ = __builtin_amdgcn_s_memtime(); tst_panel += q_ - tst0; tst0 = q_; }
 #endif
-    // trailing update: rows i, cols j in [ke, rlast], j <= i, k in [max(kb, i-bw), ke)
-    // Branch-free: li[q] = 0 wherever L(i, kb+q) is outside the band or the panel, and every
-    // band(A, j, kb+q) read is an in-bounds finite entry (a neighbouring band element when the
-    // pair is outside the band), so the masked terms contribute exactly 0.  Only full panels
-    // have trailing rows (the last panel ends at n).
-    for (int i = ke + (t >> 2); i <= rlast; i += 64) {
-      const int k0 = max(kb, i - bw);
-      double li[NB];
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const bool ok = kb + q >= k0 && kb + q < ke;
-        li[q] = band(A, bw, i, ok ? kb + q : i);
-        li[q] = ok ? li[q] : 0.0;
-      }
-      for (int j = ke + (t & 3); j <= i; j += 4) {
-        const double* Aj = A + (size_t)j * (bw + 1) + (kb - j + bw);
-        double acc = 0.0;
-#pragma unroll
-        for (int q = 0; q < NB; ++q) acc += li[q] * Aj[q];
-        band(A, bw, i, j) -= acc;
-      }
+    // trailing tiles over panel p+1's columns (J = 0); the rest is deferred (see above)
+    {
+      const int nt = (rlast - ke + 1 + 15) >> 4;
+      for (int I = wv; I < nt; I += 4) chol_trail_tile(A, bw, kb, ke, rlast, I, 0, lane);
+      pkb = kb; pke = ke; prl = rlast;
     }
     __syncthreads();
 #ifdef LORB_CHOL_STAMPS
@@ -655,11 +716,27 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
       const int row = bb + lane;
       const int be = min(n - 1, bb + 63);
       double zr = row < n ? z[row] : 0.0;
-      for (int k = be; k >= bb; --k) {
-        const double lk = (row < k && k - row <= bw) ? band(A, bw, k, row) : 0.0;
-        const double yk = readlane_d(zr, k - bb) * invd[k];
-        if (lane == k - bb) zr = yk;
-        if (row < k) zr -= lk * yk;
+      // 8-row chunks: the chunk's L(k, row) and 1/L(k, k) are loaded before the serial
+      // readlane chain so LDS/global latency is paid once per chunk, not once per row.
+      constexpr int BC = 8;
+      for (int k0 = be; k0 >= bb; k0 -= BC) {
+        double lk[BC], iv[BC];
+#pragma unroll
+        for (int u = 0; u < BC; ++u) {
+          const int k = max(k0 - u, bb);
+          const bool ok = k0 - u >= bb && row < k && k - row <= bw;
+          lk[u] = band(A, bw, k, ok ? row : k);
+          lk[u] = ok ? lk[u] : 0.0;
+          iv[u] = invd[k];
+        }
+#pragma unroll
+        for (int u = 0; u < BC; ++u) {
+          const int k = k0 - u;
+          if (k >= bb) {
+            const double yk = readlane_d(zr, k - bb) * iv[u];
+            zr = lane == k - bb ? yk : fma(-lk[u], yk, zr);
+          }
+        }
       }
       if (row < n) z[row] = zr;
       wave_sync_lds();
@@ -667,7 +744,17 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
       for (int i = max(0, bb - bw) + lane; i < bb; i += 64) {
         double acc = 0.0;
         const int kend = min(be, i + bw);
-        for (int k = bb; k <= kend; ++k) acc += band(A, bw, k, i) * z[k];
+        for (int k = bb; k <= kend; k += BC) {
+          double a[BC], zk[BC];
+#pragma unroll
+          for (int u = 0; u < BC; ++u) {
+            const int kk = min(k + u, kend);
+            a[u] = band(A, bw, kk, i);
+            zk[u] = z[kk];
+          }
+#pragma unroll
+          for (int u = 0; u < BC; ++u) acc = fma(k + u <= kend ? a[u] : 0.0, zk[u], acc);
+        }
         z[i] -= acc;
       }
       wave_sync_lds();
