@@ -223,6 +223,21 @@ def workload_c2(ctx, args, rank):
                 config={"workload": "c2_bf_top2_ratio", "pairs_per_gpu": B, "nq": 2000, "nt": 2000}, cpu=cpu)
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (FETCH_SIZE and
+    WRITE_SIZE collected in separate runs, gfx950 FETCH_SIZE x2 correction; tools/pmc_traffic.py).
+    PMC counters cannot be read live from inside the timed process, so this is the profiled
+    value of the same command; null when no summary is committed."""
+    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
+    try:
+        with open(path) as f:
+            tab = json.load(f)
+    except (OSError, ValueError):
+        return None
+    ent = tab.get("kernels", {}).get(kernel)
+    return None if ent is None else ent.get("hbm_bytes_per_launch")
+
+
 def roofline_entry(kt, wl, steps):
     """Dominant kernel (largest total device time in the profile pass) vs its roofline."""
     best = max(kt.items(), key=lambda kv: kv[1][0]) if kt else None
@@ -236,11 +251,14 @@ def roofline_entry(kt, wl, steps):
         bound, peak, unit = "valu_int32", INT32_VALU_PEAK, "Tops/s"
     else:
         kind, amount, unit = wl["kspec"][k]
-        bound, peak = ("hbm", HBM_PEAK) if kind == "hbm" else ("valu_fp64", FP64_PEAK)
+        # FP64 kernels (the Cholesky's SYRK runs on v_mfma_f64_16x16x4f64) are priced against the
+        # dense FP64 peak, which is the same for MFMA and VALU on MI355X
+        bound, peak = ("hbm", HBM_PEAK) if kind == "hbm" else ("mfma", FP64_PEAK)
     achieved = amount / avg_s
     scale = 1e9 if unit == "GB/s" else 1e12
+    name = K_NAMES.get(k, str(k))
     return {"bound": bound, "achieved": achieved / scale, "peak": peak / scale, "unit": unit,
-            "frac": achieved / peak, "traffic": None, "kernel": K_NAMES.get(k, str(k)),
+            "frac": achieved / peak, "traffic": pmc_traffic(name), "kernel": name,
             "algorithmic_per_launch": amount, "avg_kernel_us": avg_s * 1e6, "launches_per_step": per_step,
             "all_kernels_ms_per_step": {K_NAMES.get(kk, str(kk)): v[0] / steps for kk, v in kt.items()}}
 
