@@ -122,6 +122,10 @@ struct BaDev {
   const double2* obs_uv;     // K
   const int* cam_obs_off;    // Ctot+1
   const int* cam_obs;        // camera-major obs list
+  const int* obs_cm;         // K: camera-major slot of an optimised obs (-1: fixed camera).
+                             //    Camera-side tiles (obs_Jc, cam_r, obs_Jps, obs_Q, obs_g) are
+                             //    stored in camera-major order so camera and Schur kernels
+                             //    read contiguous runs.
   const int* cam_win;        // Ctot
   const double* fixed_pose;  // NF*6
   double* x_init_pose;       // Ctot*6 (initial values, never written)
@@ -138,10 +142,12 @@ struct BaDev {
   double* cam_gmax;          // Ctot
   double* obs_r;             // K*2
   double* obs_Jp;            // K*6
-  double* obs_Jc;            // K*12
-  double* obs_W;             // K*18 (scaled)
-  double* obs_Y;             // K*18
-  double* obs_rc;            // K*6
+  double* obs_Jc;            // K*12, camera-major slots
+  double* cam_r;             // K*2: residuals in camera-major slots
+  double* obs_Jps;           // K*6: Jp scaled by the point's Jacobi scale (2x3)
+  double* obs_Q;             // K*6: Q = Jps E^-1 (2x3); W = Jcs^T Jps is rank 2, so the Schur
+                             //      block Y_h W_l^T = Jcs_h^T (Q_h Jps_l^T) Jcs_l
+  double* obs_g;             // K*2: g = Q b_p  (rhs: Y_h b_p = Jcs_h^T g)
   double* env;               // S envelopes
   double* rhs;               // sum n
   double* ycam;              // sum n (solution, scaled space, y = -step)
@@ -199,8 +205,10 @@ __global__ __launch_bounds__(kOB) void k_ba_lin_obs(BaDev d) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) d.obs_Jp[6 * o + k] = Jp[k];
     if (c >= 0) {
+      const int m = d.obs_cm[o];
 #pragma unroll
-      for (int k = 0; k < 12; ++k) d.obs_Jc[12 * o + k] = Jc[k];
+      for (int k = 0; k < 12; ++k) d.obs_Jc[12 * m + k] = Jc[k];
+      d.cam_r[2 * m] = r[0]; d.cam_r[2 * m + 1] = r[1];
     }
     cost = 0.5 * (r[0] * r[0] + r[1] * r[1]);
   }
@@ -260,24 +268,24 @@ __global__ __launch_bounds__(kPB) void k_ba_lin_point(BaDev d) {
 }
 
 // K2: per-camera normal blocks (one wavefront per optimised camera)
-__global__ __launch_bounds__(64) void k_ba_camera(BaDev d) {
+__global__ __launch_bounds__(256) void k_ba_camera(BaDev d) {
+  __shared__ double red[4][27];
   const int c = blockIdx.x;
   const int w = d.cam_win[c];
   const WinState& S = d.st[w];
   if (S.done || !S.relin) return;
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   double U[21], V[6];
 #pragma unroll
   for (int k = 0; k < 21; ++k) U[k] = 0.0;
 #pragma unroll
   for (int k = 0; k < 6; ++k) V[k] = 0.0;
   const int a0 = d.cam_obs_off[c], a1 = d.cam_obs_off[c + 1];
-  for (int e = a0 + lane; e < a1; e += 64) {
-    const int o = d.cam_obs[e];
+  for (int e = a0 + t; e < a1; e += 256) {
     double J[12];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) J[k] = d.obs_Jc[12 * o + k];
-    const double r0 = d.obs_r[2 * o], r1 = d.obs_r[2 * o + 1];
+    for (int k = 0; k < 12; ++k) J[k] = d.obs_Jc[12 * e + k];
+    const double r0 = d.cam_r[2 * e], r1 = d.cam_r[2 * e + 1];
     int q = 0;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
@@ -287,10 +295,21 @@ __global__ __launch_bounds__(64) void k_ba_camera(BaDev d) {
     }
   }
 #pragma unroll
-  for (int k = 0; k < 21; ++k) U[k] = wave_sum(U[k]);
+  for (int k = 0; k < 21; ++k) {
+    const double v = wave_sum(U[k]);
+    if (lane == 0) red[wv][k] = v;
+  }
 #pragma unroll
-  for (int k = 0; k < 6; ++k) V[k] = wave_sum(V[k]);
-  if (lane == 0) {
+  for (int k = 0; k < 6; ++k) {
+    const double v = wave_sum(V[k]);
+    if (lane == 0) red[wv][21 + k] = v;
+  }
+  __syncthreads();
+  if (t == 0) {
+#pragma unroll
+    for (int k = 0; k < 21; ++k) U[k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) V[k] = ((red[0][21 + k] + red[1][21 + k]) + red[2][21 + k]) + red[3][21 + k];
 #pragma unroll
     for (int k = 0; k < 21; ++k) d.U[21 * c + k] = U[k];
 #pragma unroll
@@ -379,29 +398,20 @@ __global__ __launch_bounds__(kPB) void k_ba_point_prep(BaDev d, LMOpt o) {
   for (int k = 0; k < 6; ++k) d.pinv[6 * p + k] = Ei[k];
   const int o0 = d.pt_obs_off[p], o1 = d.pt_obs_off[p + 1];
   for (int e = o0; e < o1; ++e) {
-    const int c = d.obs_cam[e];
-    if (c < 0) continue;
-    double Jp[6], Jc[12], sc[6];
+    const int m = d.obs_cm[e];
+    if (m < 0) continue;
+    double Jps[6], Q[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) { Jp[k] = d.obs_Jp[6 * e + k]; sc[k] = d.scale_pose[6 * c + k]; }
+    for (int k = 0; k < 6; ++k) Jps[k] = d.obs_Jp[6 * e + k] * sp[k % 3];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) Jc[k] = d.obs_Jc[12 * e + k];
-    double Wm[18], Y[18], rc[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) Wm[3 * i + j] = (Jc[i] * Jp[j] + Jc[6 + i] * Jp[3 + j]) * sc[i] * sp[j];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
+    for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int j = 0; j < 3; ++j)
-        Y[3 * i + j] = Wm[3 * i] * s3(Ei, 0, j) + Wm[3 * i + 1] * s3(Ei, 1, j) + Wm[3 * i + 2] * s3(Ei, 2, j);
-      rc[i] = Y[3 * i] * b[0] + Y[3 * i + 1] * b[1] + Y[3 * i + 2] * b[2];
-    }
+        Q[3 * r + j] = Jps[3 * r] * s3(Ei, 0, j) + Jps[3 * r + 1] * s3(Ei, 1, j) + Jps[3 * r + 2] * s3(Ei, 2, j);
 #pragma unroll
-    for (int k = 0; k < 18; ++k) { d.obs_W[18 * e + k] = Wm[k]; d.obs_Y[18 * e + k] = Y[k]; }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) d.obs_rc[6 * e + k] = rc[k];
+    for (int k = 0; k < 6; ++k) { d.obs_Jps[6 * m + k] = Jps[k]; d.obs_Q[6 * m + k] = Q[k]; }
+    d.obs_g[2 * m] = Q[0] * b[0] + Q[1] * b[1] + Q[2] * b[2];
+    d.obs_g[2 * m + 1] = Q[3] * b[0] + Q[4] * b[1] + Q[5] * b[2];
   }
 }
 
@@ -412,10 +422,20 @@ __device__ __forceinline__ double& band(double* A, int bw, int i, int j) {
 }
 
 // K5: reduced camera system S (band storage) + rhs: one 256-thread workgroup per non-zero
-// camera block pair; lanes stride the pair list, fixed-order wave + LDS reduction.
-__global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
+// camera block pair; lanes stride the pair list, fixed-order wave + LDS reduction.  Each
+// (obs_h, obs_l) term is Jc_h^T M Jc_l with the 2x2 M = Q_h Jps_l^T (108 FMA, 36 doubles read);
+// the camera Jacobi scales are applied once per block.  Block pairs are sorted by camera and
+// remapped so that each XCD (blockIdx % 8 group) takes a contiguous run: the tiles of a camera
+// are re-read from that XCD's L2 instead of from the fabric.
+__global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o, int n_bp) {
   __shared__ double red[4][37];
-  const BlockPair bp = d.bp[blockIdx.x];
+  int bid;
+  {
+    const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = blockIdx.x % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
+  }
+  if (bid >= n_bp) return;
+  const BlockPair bp = d.bp[bid];
   const WinState& S = d.st[bp.win];
   if (S.done) return;
   const BaWin& W = d.win[bp.win];
@@ -424,24 +444,35 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
 #pragma unroll
   for (int k = 0; k < 36; ++k) acc[k] = 0.0;
   for (int q = bp.off + t; q < bp.off + bp.cnt; q += 256) {
-    const int2 pr = d.pairs[q];  // (obs in camera ch, obs in camera cl) of one point
-    double Y[18], Wl[18];
+    const int2 pr = d.pairs[q];  // camera-major slots (obs in camera ch, obs in camera cl) of one point
+    double Qh[6], Jl[6], Ch[12], Cl[12];
 #pragma unroll
-    for (int k = 0; k < 18; ++k) { Y[k] = d.obs_Y[18 * pr.x + k]; Wl[k] = d.obs_W[18 * pr.y + k]; }
+    for (int k = 0; k < 6; ++k) { Qh[k] = d.obs_Q[6 * pr.x + k]; Jl[k] = d.obs_Jps[6 * pr.y + k]; }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) { Ch[k] = d.obs_Jc[12 * pr.x + k]; Cl[k] = d.obs_Jc[12 * pr.y + k]; }
+    double M[4], N[12];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        M[2 * r + s] = Qh[3 * r] * Jl[3 * s] + Qh[3 * r + 1] * Jl[3 * s + 1] + Qh[3 * r + 2] * Jl[3 * s + 2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) N[6 * r + j] = M[2 * r] * Cl[j] + M[2 * r + 1] * Cl[6 + j];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
-      for (int j = 0; j < 6; ++j)
-        acc[6 * i + j] += Y[3 * i] * Wl[3 * j] + Y[3 * i + 1] * Wl[3 * j + 1] + Y[3 * i + 2] * Wl[3 * j + 2];
+      for (int j = 0; j < 6; ++j) acc[6 * i + j] += Ch[i] * N[j] + Ch[6 + i] * N[6 + j];
   }
   const bool diag = bp.ch == bp.cl;
   double r6[6] = {0, 0, 0, 0, 0, 0};
   if (diag) {
     const int a0 = d.cam_obs_off[bp.ch], a1 = d.cam_obs_off[bp.ch + 1];
     for (int e = a0 + t; e < a1; e += 256) {
-      const int ob = d.cam_obs[e];
+      const double g0 = d.obs_g[2 * e], g1 = d.obs_g[2 * e + 1];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) r6[k] += d.obs_rc[6 * ob + k];
+      for (int k = 0; k < 6; ++k) r6[k] += d.obs_Jc[12 * e + k] * g0 + d.obs_Jc[12 * e + 6 + k] * g1;
     }
   }
 #pragma unroll
@@ -451,8 +482,9 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
   }
   __syncthreads();
   if (t < 36) {
-    const double a = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
     const int i = t / 6, j = t % 6;
+    const double a = (((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]) *
+                     d.scale_pose[6 * bp.ch + i] * d.scale_pose[6 * bp.cl + j];
     const int lh = bp.ch - W.pose_base, ll = bp.cl - W.pose_base;
     double* A = d.env + W.env_base;
     if (diag) {
@@ -475,7 +507,7 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
     }
     __syncthreads();
     if (t < 6) {
-      const double r = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+      const double r = (((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]) * d.scale_pose[6 * bp.ch + t];
       const double vs = d.V[6 * bp.ch + t] * d.scale_pose[6 * bp.ch + t];
       d.rhs[W.row_base + 6 * (bp.ch - W.pose_base) + t] = vs - r;
     }
@@ -791,15 +823,18 @@ __global__ __launch_bounds__(kPB) void k_ba_backsub(BaDev d) {
     for (int e = o0; e < o1; ++e) {
       const int c = d.obs_cam[e];
       if (c < 0) continue;
+      // W^T y = Jps^T (Jcs y), W = Jcs^T Jps
       const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
-      const double* Wm = d.obs_W + 18 * e;
+      const int m = d.obs_cm[e];
+      double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        double s = 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) s += Wm[3 * i + j] * y[i];
-        b[j] -= s;
+      for (int i = 0; i < 6; ++i) {
+        const double ys = y[i] * d.scale_pose[6 * c + i];
+        a0 += d.obs_Jc[12 * m + i] * ys;
+        a1 += d.obs_Jc[12 * m + 6 + i] * ys;
       }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) b[j] -= d.obs_Jps[6 * m + j] * a0 + d.obs_Jps[6 * m + 3 + j] * a1;
     }
     double step[3], Xn[3];
 #pragma unroll
@@ -830,8 +865,8 @@ __global__ __launch_bounds__(kPB) void k_ba_backsub(BaDev d) {
         for (int k = 0; k < 6; ++k) {
           const double sc = d.scale_pose[6 * c + k];
           const double s = -y[k] * sc;
-          m0 += d.obs_Jc[12 * e + k] * s;
-          m1 += d.obs_Jc[12 * e + 6 + k] * s;
+          m0 += d.obs_Jc[12 * d.obs_cm[e] + k] * s;
+          m1 += d.obs_Jc[12 * d.obs_cm[e] + 6 + k] * s;
           pose[k] = d.x_pose[cur][6 * c + k] + s;
         }
       } else {
@@ -1153,7 +1188,7 @@ int dupload(lorb_ba_plan* P, const std::vector<T>& v, T** out) {
 int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P) {
   P->ctx = ctx;
   P->W = nw;
-  std::vector<int> pt_obs_off(1, 0), obs_cam, obs_fix, obs_pt, cam_obs_off(1, 0), cam_obs, cam_win;
+  std::vector<int> pt_obs_off(1, 0), obs_cam, obs_fix, obs_pt, cam_obs_off(1, 0), cam_obs, cam_win, obs_cm;
   std::vector<PBlk> oblk;
   std::vector<double2> obs_uv;
   std::vector<double> fixed, xpose, xpt;
@@ -1196,8 +1231,9 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     // camera-major obs lists (sorted by point == by sorted obs index)
     std::vector<std::vector<int>> co(in.n_poses);
     for (int e = 0; e < in.n_obs; ++e) { const int c = obs_cam[ob0 + e]; if (c >= 0) co[c - pose_base].push_back(ob0 + e); }
+    obs_cm.resize(obs_cam.size(), -1);
     for (int c = 0; c < in.n_poses; ++c) {
-      for (int e : co[c]) cam_obs.push_back(e);
+      for (int e : co[c]) { obs_cm[e] = (int)cam_obs.size(); cam_obs.push_back(e); }
       cam_obs_off.push_back((int)cam_obs.size());
       cam_win.push_back(w);
     }
@@ -1214,7 +1250,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
         for (int b = e0; b < e1; ++b) {
           const int cb = obs_cam[b];
           if (cb < 0 || cb > ca) continue;
-          bmap[{ca - pose_base, cb - pose_base}].push_back(make_int2(a, b));
+          bmap[{ca - pose_base, cb - pose_base}].push_back(make_int2(obs_cm[a], obs_cm[b]));
           fc[ca - pose_base] = std::min(fc[ca - pose_base], cb - pose_base);
         }
       }
@@ -1266,6 +1302,8 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   LORB_TRY(dupload(P, obs_uv, &duv)); d.obs_uv = duv;
   LORB_TRY(dupload(P, cam_obs_off, &a4)); d.cam_obs_off = a4;
   LORB_TRY(dupload(P, cam_obs, &a5)); d.cam_obs = a5;
+  int* acm = nullptr;
+  LORB_TRY(dupload(P, obs_cm, &acm)); d.obs_cm = acm;
   LORB_TRY(dupload(P, cam_win, &a6)); d.cam_win = a6;
   LORB_TRY(dupload(P, fixed, &dfix)); d.fixed_pose = dfix;
   LORB_TRY(dupload(P, xpose, &d.x_init_pose));
@@ -1279,7 +1317,8 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   LORB_TRY(dalloc(P, Pn * 6, &d.ete)); LORB_TRY(dalloc(P, Pn * 3, &d.etb)); LORB_TRY(dalloc(P, Pn * 6, &d.pinv));
   LORB_TRY(dalloc(P, C * 21, &d.U)); LORB_TRY(dalloc(P, C * 6, &d.V)); LORB_TRY(dalloc(P, C, &d.cam_gmax));
   LORB_TRY(dalloc(P, K * 2, &d.obs_r)); LORB_TRY(dalloc(P, K * 6, &d.obs_Jp)); LORB_TRY(dalloc(P, K * 12, &d.obs_Jc));
-  LORB_TRY(dalloc(P, K * 18, &d.obs_W)); LORB_TRY(dalloc(P, K * 18, &d.obs_Y)); LORB_TRY(dalloc(P, K * 6, &d.obs_rc));
+  LORB_TRY(dalloc(P, K * 2, &d.cam_r));
+  LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
   LORB_TRY(dalloc(P, (size_t)P->env_total, &d.env)); LORB_TRY(dalloc(P, (size_t)P->n_total, &d.rhs));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
   LORB_TRY(dalloc(P, (size_t)P->n_oblk * 4, &d.opart));
@@ -1301,7 +1340,7 @@ void enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
     hipLaunchKernelGGL(k_ba_lin_obs, dim3(P->n_oblk), dim3(kOB), 0, s, d);
   }
   if (P->n_pblk) hipLaunchKernelGGL(k_ba_lin_point, dim3(P->n_pblk), dim3(kPB), 0, s, d);
-  if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(64), 0, s, d);
+  if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_ba_lm_begin, dim3(P->W), dim3(64), 0, s, d, o);
 }
 
@@ -1315,7 +1354,7 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   if (P->n_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
-    hipLaunchKernelGGL(k_ba_schur, dim3(P->n_bp), dim3(256), 0, s, d, o);
+    hipLaunchKernelGGL(k_ba_schur, dim3(P->n_bp), dim3(256), 0, s, d, o, P->n_bp);
   }
   if (P->Ctot) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
