@@ -24,19 +24,19 @@ namespace {
 
 using lorb::residual;
 using lorb::residual_jac;
+using lorb::residual_jac_s;
+using lorb::residual_s;
 
-constexpr int kPB = 64;   // points per point-block (one thread per point, 1 wave)
-constexpr int kOB = 256;  // observations per obs-block (one thread per observation)
+constexpr int kGB = 256;  // observations per point group (one workgroup), see K1
 
 struct BaWin {
   int pose_base, n_poses, point_base, n_points;
   int pblk_base, n_pblk;
-  int oblk_base, n_oblk;
   int env_base, env_size, n, row_base, bw;  // S band: row i holds cols [i-bw, i]
   int obs_base, n_obs;
   double fx, fy, cx, cy;
 };
-struct PBlk { int win, p0, cnt; };   // also used for obs blocks (o0, cnt)
+struct PBlk { int win, p0, cnt, o0, no; };  // point group: points [p0, p0+cnt), obs [o0, o0+no)
 struct BlockPair { int win, ch, cl, off, cnt; };  // global camera indices, pair list range
 struct WinState {
   double radius, decrease_factor, cost, x_norm, gmax, initial_cost;
@@ -110,9 +110,10 @@ __device__ __forceinline__ double s3(const double m[6], int a, int b) {
 
 // ------------------------------------------------------------------------------------------
 struct BaDev {
+  lorb::RotJet* rot_lin;           // Ctot: rotation state (with d/daa) of x_pose[cur], per linearisation
+  lorb::RotVal* rot_cand;          // Ctot: rotation state of the candidate pose x_pose[cur ^ 1]
   const BaWin* win;
   const PBlk* pblk;
-  const PBlk* oblk;
   const int* obs_pt;         // K  (global point of each observation)
   const BlockPair* bp;
   const int2* pairs;
@@ -153,7 +154,6 @@ struct BaDev {
   double* ycam;              // sum n (solution, scaled space, y = -step)
   double* part;              // n_pblk * 8 partials
   unsigned long long* dbg;   // diagnostic stamps (LORB_CHOL_STAMPS builds only)
-  double* opart;             // n_oblk * 4 partials
   WinState* st;
 };
 
@@ -174,76 +174,105 @@ __global__ void k_ba_init(BaDev d, int W, LMOpt o) {
   d.st[w] = s;
 }
 
-// K1: per-observation linearisation (windows that (re)linearise this iteration)
-__global__ __launch_bounds__(kOB) void k_ba_lin_obs(BaDev d) {
-  __shared__ double sh[kOB];
-  const PBlk ob = d.oblk[blockIdx.x];
-  const WinState& S = d.st[ob.win];
+// K0: per-camera rotation state of the linearisation point (transcendentals once per camera)
+__global__ __launch_bounds__(64) void k_ba_rot_lin(BaDev d, int ctot) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= ctot) return;
+  const WinState& S = d.st[d.cam_win[c]];
   if (S.done || !S.relin) return;
-  const BaWin& W = d.win[ob.win];
+  d.rot_lin[c] = lorb::rot_jet(d.x_pose[S.cur] + 6 * c);
+}
+
+// Point groups (PBlk): consecutive points of one window whose observations (contiguous, sorted
+// by point) number <= kGB, processed by one 256-thread workgroup: observation-parallel phases
+// (thread = observation, coalesced, no serial load chains) alternate with point phases (thread =
+// point) that reduce their observations from LDS serially in observation order -- the same
+// summation order as a point-serial loop.  A point with more than kGB observations gets a group
+// of its own and the observation phases loop over chunks.
+
+// deterministic workgroup reductions (fixed butterfly per wave, fixed wave order)
+__device__ __forceinline__ double block_sum256(double v, double* red4) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return ((red4[0] + red4[1]) + red4[2]) + red4[3];
+}
+__device__ __forceinline__ double block_max256(double v, double* red4) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
+}
+
+// K1: linearisation of a point group (windows that (re)linearise this iteration): per
+// observation residual + Jacobians, per point E^T E / E^T r (unscaled), Jacobi scale
+// (iteration 0), gradient-max / point-norm / cost partials.
+__global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
+  __shared__ double sh[kGB][9];
+  __shared__ double red4[4];
+  const PBlk g = d.pblk[blockIdx.x];
+  const WinState& S = d.st[g.win];
+  if (S.done || !S.relin) return;
+  const BaWin& W = d.win[g.win];
   const int cur = S.cur;
   const int t = threadIdx.x;
   double cost = 0.0;
-  if (t < ob.cnt) {
-    const int o = ob.p0 + t;
-    const int p = d.obs_pt[o];
-    const int c = d.obs_cam[o];
-    double X[3], pose[6];
+  double E[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+  int po0 = 0, po1 = 0;
+  if (t < g.cnt) { po0 = d.pt_obs_off[g.p0 + t]; po1 = d.pt_obs_off[g.p0 + t + 1]; }
+  for (int c0 = 0; c0 < g.no; c0 += kGB) {
+    if (c0 + t < g.no) {
+      const int o = g.o0 + c0 + t;
+      const int p = d.obs_pt[o];
+      const int c = d.obs_cam[o];
+      double X[3], pose[6];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) X[k] = d.x_pt[cur][3 * p + k];
-    if (c >= 0) {
+      for (int k = 0; k < 3; ++k) X[k] = d.x_pt[cur][3 * p + k];
+      if (c >= 0) {
 #pragma unroll
-      for (int k = 0; k < 6; ++k) pose[k] = d.x_pose[cur][6 * c + k];
-    } else {
+        for (int k = 0; k < 6; ++k) pose[k] = d.x_pose[cur][6 * c + k];
+      } else {
 #pragma unroll
-      for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[o] + k];
+        for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[o] + k];
+      }
+      const double2 uv = d.obs_uv[o];
+      double r[2], Jp[6], Jc[12];
+      if (c >= 0) residual_jac_s(d.rot_lin[c], pose + 3, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
+      else residual_jac(pose, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
+      d.obs_r[2 * o] = r[0]; d.obs_r[2 * o + 1] = r[1];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) d.obs_Jp[6 * o + k] = Jp[k];
+      if (c >= 0) {
+        const int m = d.obs_cm[o];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) d.obs_Jc[12 * m + k] = Jc[k];
+        d.cam_r[2 * m] = r[0]; d.cam_r[2 * m + 1] = r[1];
+      }
+      cost += 0.5 * (r[0] * r[0] + r[1] * r[1]);
+      sh[t][0] = Jp[0] * Jp[0] + Jp[3] * Jp[3]; sh[t][1] = Jp[0] * Jp[1] + Jp[3] * Jp[4];
+      sh[t][2] = Jp[0] * Jp[2] + Jp[3] * Jp[5]; sh[t][3] = Jp[1] * Jp[1] + Jp[4] * Jp[4];
+      sh[t][4] = Jp[1] * Jp[2] + Jp[4] * Jp[5]; sh[t][5] = Jp[2] * Jp[2] + Jp[5] * Jp[5];
+      sh[t][6] = Jp[0] * r[0] + Jp[3] * r[1]; sh[t][7] = Jp[1] * r[0] + Jp[4] * r[1];
+      sh[t][8] = Jp[2] * r[0] + Jp[5] * r[1];
     }
-    const double2 uv = d.obs_uv[o];
-    double r[2], Jp[6], Jc[12];
-    residual_jac(pose, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
-    d.obs_r[2 * o] = r[0]; d.obs_r[2 * o + 1] = r[1];
+    __syncthreads();
+    if (t < g.cnt) {
+      const int a = max(po0, g.o0 + c0), z = min(po1, g.o0 + c0 + kGB);
+      for (int e = a; e < z; ++e) {
+        const double* v = sh[e - g.o0 - c0];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) d.obs_Jp[6 * o + k] = Jp[k];
-    if (c >= 0) {
-      const int m = d.obs_cm[o];
+        for (int k = 0; k < 6; ++k) E[k] += v[k];
 #pragma unroll
-      for (int k = 0; k < 12; ++k) d.obs_Jc[12 * m + k] = Jc[k];
-      d.cam_r[2 * m] = r[0]; d.cam_r[2 * m + 1] = r[1];
+        for (int k = 0; k < 3; ++k) b[k] += v[6 + k];
+      }
     }
-    cost = 0.5 * (r[0] * r[0] + r[1] * r[1]);
-  }
-  // deterministic block sum
-  sh[t] = cost;
-  __syncthreads();
-  for (int s = kOB / 2; s > 0; s >>= 1) {
-    if (t < s) sh[t] += sh[t + s];
     __syncthreads();
   }
-  if (t == 0) d.opart[4 * blockIdx.x] = sh[0];
-}
-
-// K1b: per-point E^T E, E^T r (unscaled), Jacobi scale (iteration 0), gradient / norm partials
-__global__ __launch_bounds__(kPB) void k_ba_lin_point(BaDev d) {
-  const PBlk pb = d.pblk[blockIdx.x];
-  const WinState& S = d.st[pb.win];
-  if (S.done || !S.relin) return;
-  const int cur = S.cur;
-  const int t = threadIdx.x;
   double gm = 0.0, xn2 = 0.0;
-  if (t < pb.cnt) {
-    const int p = pb.p0 + t;
-    double E[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-    const int o0 = d.pt_obs_off[p], o1 = d.pt_obs_off[p + 1];
-    for (int o = o0; o < o1; ++o) {
-      double Jp[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) Jp[k] = d.obs_Jp[6 * o + k];
-      const double r0 = d.obs_r[2 * o], r1 = d.obs_r[2 * o + 1];
-      E[0] += Jp[0] * Jp[0] + Jp[3] * Jp[3]; E[1] += Jp[0] * Jp[1] + Jp[3] * Jp[4];
-      E[2] += Jp[0] * Jp[2] + Jp[3] * Jp[5]; E[3] += Jp[1] * Jp[1] + Jp[4] * Jp[4];
-      E[4] += Jp[1] * Jp[2] + Jp[4] * Jp[5]; E[5] += Jp[2] * Jp[2] + Jp[5] * Jp[5];
-      b[0] += Jp[0] * r0 + Jp[3] * r1; b[1] += Jp[1] * r0 + Jp[4] * r1; b[2] += Jp[2] * r0 + Jp[5] * r1;
-    }
+  if (t < g.cnt) {
+    const int p = g.p0 + t;
 #pragma unroll
     for (int k = 0; k < 6; ++k) d.ete[6 * p + k] = E[k];
 #pragma unroll
@@ -253,7 +282,7 @@ __global__ __launch_bounds__(kPB) void k_ba_lin_point(BaDev d) {
       d.scale_pt[3 * p + 1] = 1.0 / (1.0 + sqrt(E[3]));
       d.scale_pt[3 * p + 2] = 1.0 / (1.0 + sqrt(E[5]));
     }
-    if (o1 > o0) {
+    if (po1 > po0) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const double X = d.x_pt[cur][3 * p + k];
@@ -262,9 +291,10 @@ __global__ __launch_bounds__(kPB) void k_ba_lin_point(BaDev d) {
       }
     }
   }
-  gm = wave_max(gm);
-  xn2 = wave_sum(xn2);
-  if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[1] = gm; P[2] = xn2; }
+  cost = block_sum256(cost, red4);
+  gm = block_max256(gm, red4);
+  xn2 = block_sum256(xn2, red4);
+  if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[0] = cost; P[1] = gm; P[2] = xn2; }
 }
 
 // K2: per-camera normal blocks (one wavefront per optimised camera)
@@ -343,10 +373,9 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
   if (S.relin) {
     // fixed lane assignment + fixed butterfly => deterministic
     double cost = 0.0, gm = 0.0, xn2 = 0.0;
-    for (int b = lane; b < W.n_oblk; b += 64) cost += d.opart[4 * (W.oblk_base + b)];
     for (int b = lane; b < W.n_pblk; b += 64) {
       const double* P = d.part + 8 * (W.pblk_base + b);
-      gm = fmax(gm, P[1]); xn2 += P[2];
+      cost += P[0]; gm = fmax(gm, P[1]); xn2 += P[2];
     }
     const int cur = S.cur;
     for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64) {
@@ -371,38 +400,47 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
   }
 }
 
-// K4: per-point Schur prep: scaled E^T E + D^2 -> inverse, W_s, Y = W_s E^-1, rc = Y E^T b
-__global__ __launch_bounds__(kPB) void k_ba_point_prep(BaDev d, LMOpt o) {
-  const PBlk pb = d.pblk[blockIdx.x];
-  const WinState& S = d.st[pb.win];
+// K4: point-group Schur prep: scaled E^T E + D^2 -> inverse (point phase), then per optimised
+// observation Jps (scaled Jp), Q = Jps E^-1 and g = Q b (observation phase).
+__global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
+  __shared__ double sEi[kGB][6], sb[kGB][3], ssp[kGB][3];
+  const PBlk g = d.pblk[blockIdx.x];
+  const WinState& S = d.st[g.win];
   if (S.done) return;
   const int t = threadIdx.x;
-  if (t >= pb.cnt) return;
-  const int p = pb.p0 + t;
-  const double rad = S.radius;
-  double sp[3], E[6], b[3];
+  if (t < g.cnt) {
+    const int p = g.p0 + t;
+    const double rad = S.radius;
+    double sp[3], E[6], b[3];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * p + k]; b[k] = d.etb[3 * p + k] * sp[k]; }
-  const double* Eu = d.ete + 6 * p;
-  E[0] = Eu[0] * sp[0] * sp[0]; E[1] = Eu[1] * sp[0] * sp[1]; E[2] = Eu[2] * sp[0] * sp[2];
-  E[3] = Eu[3] * sp[1] * sp[1]; E[4] = Eu[4] * sp[1] * sp[2]; E[5] = Eu[5] * sp[2] * sp[2];
-  E[0] += fmin(fmax(E[0], o.min_diag), o.max_diag) / rad;
-  E[3] += fmin(fmax(E[3], o.min_diag), o.max_diag) / rad;
-  E[5] += fmin(fmax(E[5], o.min_diag), o.max_diag) / rad;
-  double Ei[6];
-  if (!inv3(E, Ei)) {
-    d.st[pb.win].chol_fail = 1;  // benign race: every writer stores 1
-    for (int k = 0; k < 6; ++k) Ei[k] = 0.0;
+    for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * p + k]; b[k] = d.etb[3 * p + k] * sp[k]; }
+    const double* Eu = d.ete + 6 * p;
+    E[0] = Eu[0] * sp[0] * sp[0]; E[1] = Eu[1] * sp[0] * sp[1]; E[2] = Eu[2] * sp[0] * sp[2];
+    E[3] = Eu[3] * sp[1] * sp[1]; E[4] = Eu[4] * sp[1] * sp[2]; E[5] = Eu[5] * sp[2] * sp[2];
+    E[0] += fmin(fmax(E[0], o.min_diag), o.max_diag) / rad;
+    E[3] += fmin(fmax(E[3], o.min_diag), o.max_diag) / rad;
+    E[5] += fmin(fmax(E[5], o.min_diag), o.max_diag) / rad;
+    double Ei[6];
+    if (!inv3(E, Ei)) {
+      d.st[g.win].chol_fail = 1;  // benign race: every writer stores 1
+      for (int k = 0; k < 6; ++k) Ei[k] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { d.pinv[6 * p + k] = Ei[k]; sEi[t][k] = Ei[k]; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sb[t][k] = b[k]; ssp[t][k] = sp[k]; }
   }
-#pragma unroll
-  for (int k = 0; k < 6; ++k) d.pinv[6 * p + k] = Ei[k];
-  const int o0 = d.pt_obs_off[p], o1 = d.pt_obs_off[p + 1];
-  for (int e = o0; e < o1; ++e) {
+  __syncthreads();
+  for (int c0 = t; c0 < g.no; c0 += kGB) {
+    const int e = g.o0 + c0;
     const int m = d.obs_cm[e];
     if (m < 0) continue;
+    const int lp = d.obs_pt[e] - g.p0;
+    const double* Ei = sEi[lp];
+    const double* b = sb[lp];
     double Jps[6], Q[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) Jps[k] = d.obs_Jp[6 * e + k] * sp[k % 3];
+    for (int k = 0; k < 6; ++k) Jps[k] = d.obs_Jp[6 * e + k] * ssp[lp][k % 3];
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -799,93 +837,139 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
 #endif
 }
 
-// K7: per-point back-substitution, candidate point, model cost change and candidate cost
-__global__ __launch_bounds__(kPB) void k_ba_backsub(BaDev d) {
-  const PBlk pb = d.pblk[blockIdx.x];
-  const WinState& S = d.st[pb.win];
+// K7: point-group back-substitution: b_p -= sum_e W_e^T y_c(e) (observation phase + ordered
+// point reduction), point step / candidate (point phase), model cost change and candidate cost
+// per observation (observation phase).
+__global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
+  __shared__ double sh[kGB][3], sst[kGB][3], sxn[kGB][3];
+  __shared__ double red4[4];
+  const PBlk g = d.pblk[blockIdx.x];
+  const WinState& S = d.st[g.win];
   if (S.done || S.chol_fail) return;
-  const BaWin& W = d.win[pb.win];
+  const BaWin& W = d.win[g.win];
   const int cur = S.cur;
   const int t = threadIdx.x;
-  double mcc = 0.0, ncost = 0.0, sn2 = 0.0;
-  if (t < pb.cnt) {
-    const int p = pb.p0 + t;
-    double sp[3], X[3], b[3], Ei[6];
+  double b[3] = {0, 0, 0};
+  int po0 = 0, po1 = 0;
+  if (t < g.cnt) {
+    const int p = g.p0 + t;
+    po0 = d.pt_obs_off[p]; po1 = d.pt_obs_off[p + 1];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      sp[k] = d.scale_pt[3 * p + k];
-      X[k] = d.x_pt[cur][3 * p + k];
-      b[k] = d.etb[3 * p + k] * sp[k];
+    for (int k = 0; k < 3; ++k) b[k] = d.etb[3 * p + k] * d.scale_pt[3 * p + k];
+  }
+  for (int c0 = 0; c0 < g.no; c0 += kGB) {
+    if (c0 + t < g.no) {
+      const int e = g.o0 + c0 + t;
+      const int c = d.obs_cam[e];
+      if (c >= 0) {
+        // W^T y = Jps^T (Jcs y), W = Jcs^T Jps
+        const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
+        const int m = d.obs_cm[e];
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const double ys = y[i] * d.scale_pose[6 * c + i];
+          a0 += d.obs_Jc[12 * m + i] * ys;
+          a1 += d.obs_Jc[12 * m + 6 + i] * ys;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j) sh[t][j] = d.obs_Jps[6 * m + j] * a0 + d.obs_Jps[6 * m + 3 + j] * a1;
+      } else {
+        sh[t][0] = sh[t][1] = sh[t][2] = 0.0;
+      }
     }
+    __syncthreads();
+    if (t < g.cnt) {
+      const int a = max(po0, g.o0 + c0), z = min(po1, g.o0 + c0 + kGB);
+      for (int e = a; e < z; ++e) {
+        if (d.obs_cam[e] < 0) continue;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) b[j] -= sh[e - g.o0 - c0][j];
+      }
+    }
+    __syncthreads();
+  }
+  double sn2 = 0.0;
+  if (t < g.cnt) {
+    const int p = g.p0 + t;
+    double sp[3], X[3], Ei[6], step[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * p + k]; X[k] = d.x_pt[cur][3 * p + k]; }
 #pragma unroll
     for (int k = 0; k < 6; ++k) Ei[k] = d.pinv[6 * p + k];
-    const int o0 = d.pt_obs_off[p], o1 = d.pt_obs_off[p + 1];
-    for (int e = o0; e < o1; ++e) {
-      const int c = d.obs_cam[e];
-      if (c < 0) continue;
-      // W^T y = Jps^T (Jcs y), W = Jcs^T Jps
-      const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
-      const int m = d.obs_cm[e];
-      double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const double ys = y[i] * d.scale_pose[6 * c + i];
-        a0 += d.obs_Jc[12 * m + i] * ys;
-        a1 += d.obs_Jc[12 * m + 6 + i] * ys;
-      }
-#pragma unroll
-      for (int j = 0; j < 3; ++j) b[j] -= d.obs_Jps[6 * m + j] * a0 + d.obs_Jps[6 * m + 3 + j] * a1;
-    }
-    double step[3], Xn[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       step[j] = -(s3(Ei, j, 0) * b[0] + s3(Ei, j, 1) * b[1] + s3(Ei, j, 2) * b[2]);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      Xn[j] = X[j] + step[j] * sp[j];
-      d.x_pt[cur ^ 1][3 * p + j] = Xn[j];
-    }
-    if (o1 > o0) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) sn2 += (X[j] - Xn[j]) * (X[j] - Xn[j]);
-    }
-    for (int e = o0; e < o1; ++e) {
-      const int c = d.obs_cam[e];
-      double m0 = 0.0, m1 = 0.0;
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const double s = step[j] * sp[j];
-        m0 += d.obs_Jp[6 * e + j] * s;
-        m1 += d.obs_Jp[6 * e + 3 + j] * s;
-      }
-      double pose[6];
-      if (c >= 0) {
-        const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          const double sc = d.scale_pose[6 * c + k];
-          const double s = -y[k] * sc;
-          m0 += d.obs_Jc[12 * d.obs_cm[e] + k] * s;
-          m1 += d.obs_Jc[12 * d.obs_cm[e] + 6 + k] * s;
-          pose[k] = d.x_pose[cur][6 * c + k] + s;
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[e] + k];
-      }
-      const double r0 = d.obs_r[2 * e], r1 = d.obs_r[2 * e + 1];
-      mcc += m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0);
-      const double2 uv = d.obs_uv[e];
-      double rn[2];
-      residual(pose, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
-      ncost += 0.5 * (rn[0] * rn[0] + rn[1] * rn[1]);
+      const double xn = X[j] + step[j] * sp[j];
+      d.x_pt[cur ^ 1][3 * p + j] = xn;
+      sxn[t][j] = xn;
+      sst[t][j] = step[j] * sp[j];
+      if (po1 > po0) sn2 += (X[j] - xn) * (X[j] - xn);
     }
   }
-  mcc = wave_sum(mcc); ncost = wave_sum(ncost); sn2 = wave_sum(sn2);
+  __syncthreads();
+  double mcc = 0.0, ncost = 0.0;
+  for (int c0 = t; c0 < g.no; c0 += kGB) {
+    const int e = g.o0 + c0;
+    const int c = d.obs_cam[e];
+    const int lp = d.obs_pt[e] - g.p0;
+    const double Xn[3] = {sxn[lp][0], sxn[lp][1], sxn[lp][2]};
+    double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      m0 += d.obs_Jp[6 * e + j] * sst[lp][j];
+      m1 += d.obs_Jp[6 * e + 3 + j] * sst[lp][j];
+    }
+    const double2 uv = d.obs_uv[e];
+    double rn[2];
+    if (c >= 0) {
+      const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
+      const int m = d.obs_cm[e];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const double s = -y[k] * d.scale_pose[6 * c + k];
+        m0 += d.obs_Jc[12 * m + k] * s;
+        m1 += d.obs_Jc[12 * m + 6 + k] * s;
+      }
+      // candidate camera (k_ba_cand): x_pose[cur ^ 1] with its rotation state
+      residual_s(d.rot_cand[c], d.x_pose[cur ^ 1] + 6 * c + 3, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
+    } else {
+      double pose[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[e] + k];
+      residual(pose, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
+    }
+    const double r0 = d.obs_r[2 * e], r1 = d.obs_r[2 * e + 1];
+    mcc += m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0);
+    ncost += 0.5 * (rn[0] * rn[0] + rn[1] * rn[1]);
+  }
+  mcc = block_sum256(mcc, red4);
+  ncost = block_sum256(ncost, red4);
+  sn2 = block_sum256(sn2, red4);
   if (t == 0) {
     double* P = d.part + 8 * blockIdx.x;
     P[3] = mcc; P[4] = ncost; P[5] = sn2;
   }
+}
+
+// K7b: per-camera candidate pose x + D^-1 delta (into x_pose[cur ^ 1]) and its rotation state
+__global__ __launch_bounds__(64) void k_ba_cand(BaDev d, int ctot) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= ctot) return;
+  const int w = d.cam_win[c];
+  const WinState& S = d.st[w];
+  if (S.done || S.chol_fail) return;
+  const BaWin& W = d.win[w];
+  const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
+  double xn[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    xn[k] = d.x_pose[S.cur][6 * c + k] + (-y[k]) * d.scale_pose[6 * c + k];
+    d.x_pose[S.cur ^ 1][6 * c + k] = xn[k];
+  }
+  d.rot_cand[c] = lorb::rot_val(xn);
 }
 
 // K8: per-window iteration tail: camera candidate, step validity, tolerances, accept/reject
@@ -909,8 +993,7 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
       const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
       for (int k = 0; k < 6; ++k) {
         const double x = d.x_pose[cur][6 * c + k];
-        const double xn = x + (-y[k]) * d.scale_pose[6 * c + k];
-        d.x_pose[cur ^ 1][6 * c + k] = xn;
+        const double xn = d.x_pose[cur ^ 1][6 * c + k];  // written by k_ba_cand
         if (active) sn2 += (x - xn) * (x - xn);
       }
     }
@@ -996,10 +1079,11 @@ __global__ __launch_bounds__(256) void k_ba_pose_only(const int32_t* __restrict_
       double pose[6];
 #pragma unroll
       for (int k = 0; k < 6; ++k) pose[k] = xs[k];
+      const lorb::RotJet R = lorb::rot_jet(pose);  // one frame: rotation state hoisted
       for (int r = r0 + t; r < r1; r += 256) {
         const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
         double rr[2], Jp[6], Jc[12];
-        residual_jac(pose, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr, Jp, Jc);
+        residual_jac_s(R, pose + 3, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr, Jp, Jc);
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
@@ -1088,10 +1172,11 @@ __global__ __launch_bounds__(256) void k_ba_pose_only(const int32_t* __restrict_
     double pose[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) pose[k] = xn[k];
+    const lorb::RotVal R = lorb::rot_val(pose);
     for (int r = r0 + t; r < r1; r += 256) {
       const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
       double rr[2];
-      residual(pose, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr);
+      residual_s(R, pose + 3, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr);
       v[0] += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
     }
     block_sum<1>(v, sh);
@@ -1149,7 +1234,7 @@ LMOpt to_dev_opt(const lorb_lm_options* o) {
 // ------------------------------------------------------------------------------------------
 struct lorb_ba_plan {
   lorb_ctx* ctx = nullptr;
-  int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_oblk = 0, n_bp = 0, n_pairs = 0;
+  int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_bp = 0, n_pairs = 0;
   int env_total = 0, n_total = 0, max_env = 0, max_bw = 0;
   std::vector<BaWin> hwin;
   std::vector<void*> allocs;
@@ -1189,7 +1274,6 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   P->ctx = ctx;
   P->W = nw;
   std::vector<int> pt_obs_off(1, 0), obs_cam, obs_fix, obs_pt, cam_obs_off(1, 0), cam_obs, cam_win, obs_cm;
-  std::vector<PBlk> oblk;
   std::vector<double2> obs_uv;
   std::vector<double> fixed, xpose, xpt;
   std::vector<PBlk> pblk;
@@ -1272,18 +1356,23 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     P->max_env = std::max(P->max_env, bw.env_size + 2 * n);
     P->max_bw = std::max(P->max_bw, bwid);
     env_base += bw.env_size; row_base += n;
-    bw.oblk_base = (int)oblk.size();
-    for (int o0 = 0; o0 < in.n_obs; o0 += kOB) oblk.push_back({w, bw.obs_base + o0, std::min(kOB, in.n_obs - o0)});
-    bw.n_oblk = (int)oblk.size() - bw.oblk_base;
-    // point blocks
+    // point groups: consecutive points with <= kGB observations (and <= kGB points) in total
     bw.pblk_base = (int)pblk.size();
-    for (int p0 = 0; p0 < in.n_points; p0 += kPB) pblk.push_back({w, point_base + p0, std::min(kPB, in.n_points - p0)});
+    for (int p = 0; p < in.n_points;) {
+      PBlk g{w, point_base + p, 0, ob0 + cnt[p], 0};
+      while (p < in.n_points && g.cnt < kGB) {
+        const int k = cnt[p + 1] - cnt[p];
+        if (g.cnt > 0 && g.no + k > kGB) break;
+        g.cnt++; g.no += k; ++p;
+      }
+      pblk.push_back(g);
+    }
     bw.n_pblk = (int)pblk.size() - bw.pblk_base;
     P->hwin.push_back(bw);
     pose_base += in.n_poses; point_base += in.n_points; fix_base += in.n_fixed;
   }
   P->Ctot = pose_base; P->Ptot = point_base; P->K = (int)obs_cam.size(); P->NF = fix_base;
-  P->n_pblk = (int)pblk.size(); P->n_oblk = (int)oblk.size(); P->n_bp = (int)bps.size(); P->n_pairs = (int)pairs.size();
+  P->n_pblk = (int)pblk.size(); P->n_bp = (int)bps.size(); P->n_pairs = (int)pairs.size();
   P->env_total = env_base; P->n_total = row_base;
   BaDev& d = P->dev;
   BaWin* dwin; PBlk* dpb; BlockPair* dbp; int2* dpairs; double2* duv;
@@ -1291,8 +1380,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   double* dfix;
   LORB_TRY(dupload(P, P->hwin, &dwin)); d.win = dwin;
   LORB_TRY(dupload(P, pblk, &dpb)); d.pblk = dpb;
-  PBlk* dob; int* dopt;
-  LORB_TRY(dupload(P, oblk, &dob)); d.oblk = dob;
+  int* dopt;
   LORB_TRY(dupload(P, obs_pt, &dopt)); d.obs_pt = dopt;
   LORB_TRY(dupload(P, bps, &dbp)); d.bp = dbp;
   LORB_TRY(dupload(P, pairs, &dpairs)); d.pairs = dpairs;
@@ -1318,10 +1406,11 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   LORB_TRY(dalloc(P, C * 21, &d.U)); LORB_TRY(dalloc(P, C * 6, &d.V)); LORB_TRY(dalloc(P, C, &d.cam_gmax));
   LORB_TRY(dalloc(P, K * 2, &d.obs_r)); LORB_TRY(dalloc(P, K * 6, &d.obs_Jp)); LORB_TRY(dalloc(P, K * 12, &d.obs_Jc));
   LORB_TRY(dalloc(P, K * 2, &d.cam_r));
+  LORB_TRY(dalloc(P, (size_t)P->Ctot, &d.rot_lin));
+  LORB_TRY(dalloc(P, (size_t)P->Ctot, &d.rot_cand));
   LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
   LORB_TRY(dalloc(P, (size_t)P->env_total, &d.env)); LORB_TRY(dalloc(P, (size_t)P->n_total, &d.rhs));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
-  LORB_TRY(dalloc(P, (size_t)P->n_oblk * 4, &d.opart));
   LORB_TRY(dalloc(P, (size_t)nw * 8, &d.dbg));
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
   if (!obs_cam.empty()) { /* keep obs arrays alive via allocs */ }
@@ -1335,11 +1424,11 @@ constexpr int kLdsBudget = 160 * 1024 - 2048;
 void enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = P->ctx->stream;
   const BaDev& d = P->dev;
-  if (P->n_oblk) {
+  if (P->Ctot) hipLaunchKernelGGL(k_ba_rot_lin, dim3(lorb::ceil_div(P->Ctot, 64)), dim3(64), 0, s, d, P->Ctot);
+  if (P->n_pblk) {
     lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-    hipLaunchKernelGGL(k_ba_lin_obs, dim3(P->n_oblk), dim3(kOB), 0, s, d);
+    hipLaunchKernelGGL(k_ba_lin, dim3(P->n_pblk), dim3(kGB), 0, s, d);
   }
-  if (P->n_pblk) hipLaunchKernelGGL(k_ba_lin_point, dim3(P->n_pblk), dim3(kPB), 0, s, d);
   if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(256), 0, s, d);
   hipLaunchKernelGGL(k_ba_lm_begin, dim3(P->W), dim3(64), 0, s, d, o);
 }
@@ -1350,7 +1439,7 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = ctx->stream;
   const BaDev& d = P->dev;
   enqueue_linearize(P, o);
-  if (P->n_pblk) hipLaunchKernelGGL(k_ba_point_prep, dim3(P->n_pblk), dim3(kPB), 0, s, d, o);
+  if (P->n_pblk) hipLaunchKernelGGL(k_ba_point_prep, dim3(P->n_pblk), dim3(kGB), 0, s, d, o);
   if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   if (P->n_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
@@ -1367,7 +1456,8 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
     else { if (rpl == 1) LORB_CHOL(false, 1); else if (rpl == 2) LORB_CHOL(false, 2); else if (rpl == 4) LORB_CHOL(false, 4); else LORB_CHOL(false, 8); }
 #undef LORB_CHOL
   }
-  if (P->n_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->n_pblk), dim3(kPB), 0, s, d);
+  if (P->Ctot) hipLaunchKernelGGL(k_ba_cand, dim3(lorb::ceil_div(P->Ctot, 64)), dim3(64), 0, s, d, P->Ctot);
+  if (P->n_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->n_pblk), dim3(kGB), 0, s, d);
   hipLaunchKernelGGL(k_ba_lm_end, dim3(P->W), dim3(64), 0, s, d, o);
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;

@@ -22,11 +22,57 @@ __device__ __forceinline__ Dual3 operator*(Dual3 f, Dual3 g) {
 }
 __device__ __forceinline__ Dual3 operator*(Dual3 f, double s) { return {f.a * s, f.v0 * s, f.v1 * s, f.v2 * s}; }
 
-// ceres::AngleAxisRotatePoint value + d(out)/d(aa) (3x3, row = output coord) + d(out)/d(pt) (3x3)
-__device__ __forceinline__ void aarp_jac(const double aa[3], const double pt[3], double out[3],
-                                         double dO_daa[9], double dO_dpt[9]) {
+// ceres::AngleAxisRotatePoint is split into a per-rotation part (theta, cos, sin, unit axis --
+// the transcendentals) and a per-point part, so that kernels evaluating many points under one
+// camera compute the former once per camera.  The per-point operation sequence is unchanged,
+// so split and fused evaluation give bit-identical results.
+constexpr double kAarpEps = 2.220446049250313e-16;  // std::numeric_limits<double>::epsilon()
+
+struct RotVal {  // value-only rotation state
+  double cs, sn, w0, w1, w2, aa0, aa1, aa2;
+  int big;  // theta^2 > eps (else first-order branch)
+};
+__device__ __forceinline__ RotVal rot_val(const double aa[3]) {
+  RotVal R;
+  R.aa0 = aa[0]; R.aa1 = aa[1]; R.aa2 = aa[2];
   const double theta2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
-  if (theta2 > 2.220446049250313e-16) {
+  R.big = theta2 > kAarpEps;
+  if (R.big) {
+    const double th = sqrt(theta2);
+    sincos(th, &R.sn, &R.cs);
+    const double ti = 1.0 / th;
+    R.w0 = aa[0] * ti; R.w1 = aa[1] * ti; R.w2 = aa[2] * ti;
+  } else {
+    R.sn = R.cs = R.w0 = R.w1 = R.w2 = 0.0;
+  }
+  return R;
+}
+__device__ __forceinline__ void aarp_s(const RotVal& R, const double pt[3], double out[3]) {
+  if (R.big) {
+    const double w0 = R.w0, w1 = R.w1, w2 = R.w2, cs = R.cs, sn = R.sn;
+    const double x0 = w1 * pt[2] - w2 * pt[1], x1 = w2 * pt[0] - w0 * pt[2], x2 = w0 * pt[1] - w1 * pt[0];
+    const double tmp = (w0 * pt[0] + w1 * pt[1] + w2 * pt[2]) * (1.0 - cs);
+    out[0] = pt[0] * cs + x0 * sn + w0 * tmp;
+    out[1] = pt[1] * cs + x1 * sn + w1 * tmp;
+    out[2] = pt[2] * cs + x2 * sn + w2 * tmp;
+  } else {
+    out[0] = pt[0] + (R.aa1 * pt[2] - R.aa2 * pt[1]);
+    out[1] = pt[1] + (R.aa2 * pt[0] - R.aa0 * pt[2]);
+    out[2] = pt[2] + (R.aa0 * pt[1] - R.aa1 * pt[0]);
+  }
+}
+
+struct RotJet {  // rotation state with d/d(aa) (forward-mode duals)
+  Dual3 c, s, w0, w1, w2;
+  double aa0, aa1, aa2;
+  int big;
+};
+__device__ __forceinline__ RotJet rot_jet(const double aa[3]) {
+  RotJet R;
+  R.aa0 = aa[0]; R.aa1 = aa[1]; R.aa2 = aa[2];
+  const double theta2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
+  R.big = theta2 > kAarpEps;
+  if (R.big) {
     const Dual3 A0 = {aa[0], 1.0, 0.0, 0.0}, A1 = {aa[1], 0.0, 1.0, 0.0}, A2 = {aa[2], 0.0, 0.0, 1.0};
     const Dual3 t2 = A0 * A0 + A1 * A1 + A2 * A2;
     const double th = sqrt(t2.a);
@@ -34,12 +80,22 @@ __device__ __forceinline__ void aarp_jac(const double aa[3], const double pt[3],
     const Dual3 theta = {th, t2.v0 * hinv, t2.v1 * hinv, t2.v2 * hinv};
     double sn, cs;
     sincos(th, &sn, &cs);
-    const Dual3 c = {cs, -sn * theta.v0, -sn * theta.v1, -sn * theta.v2};
-    const Dual3 s = {sn, cs * theta.v0, cs * theta.v1, cs * theta.v2};
+    R.c = {cs, -sn * theta.v0, -sn * theta.v1, -sn * theta.v2};
+    R.s = {sn, cs * theta.v0, cs * theta.v1, cs * theta.v2};
     const double ti = 1.0 / th;
     const double dti = -ti * ti;
     const Dual3 tinv = {ti, dti * theta.v0, dti * theta.v1, dti * theta.v2};
-    const Dual3 w0 = A0 * tinv, w1 = A1 * tinv, w2 = A2 * tinv;
+    R.w0 = A0 * tinv; R.w1 = A1 * tinv; R.w2 = A2 * tinv;
+  } else {
+    R.c = R.s = R.w0 = R.w1 = R.w2 = dconst(0.0);
+  }
+  return R;
+}
+// value + d(out)/d(aa) (3x3, row = output coord) + d(out)/d(pt) (3x3)
+__device__ __forceinline__ void aarp_jac_s(const RotJet& R, const double pt[3], double out[3],
+                                           double dO_daa[9], double dO_dpt[9]) {
+  if (R.big) {
+    const Dual3 c = R.c, s = R.s, w0 = R.w0, w1 = R.w1, w2 = R.w2;
     const Dual3 p0 = dconst(pt[0]), p1 = dconst(pt[1]), p2 = dconst(pt[2]);
     const Dual3 x0 = w1 * p2 - w2 * p1, x1 = w2 * p0 - w0 * p2, x2 = w0 * p1 - w1 * p0;
     const Dual3 omc = dconst(1.0) - c;
@@ -52,11 +108,13 @@ __device__ __forceinline__ void aarp_jac(const double aa[3], const double pt[3],
     dO_daa[3] = o1.v0; dO_daa[4] = o1.v1; dO_daa[5] = o1.v2;
     dO_daa[6] = o2.v0; dO_daa[7] = o2.v1; dO_daa[8] = o2.v2;
     // R = c I + s [w]x + (1-c) w w^T
+    const double cs = c.a, sn = s.a;
     const double W0 = w0.a, W1 = w1.a, W2 = w2.a, oc = omc.a;
     dO_dpt[0] = cs + oc * W0 * W0;      dO_dpt[1] = -sn * W2 + oc * W0 * W1; dO_dpt[2] = sn * W1 + oc * W0 * W2;
     dO_dpt[3] = sn * W2 + oc * W1 * W0; dO_dpt[4] = cs + oc * W1 * W1;       dO_dpt[5] = -sn * W0 + oc * W1 * W2;
     dO_dpt[6] = -sn * W1 + oc * W2 * W0; dO_dpt[7] = sn * W0 + oc * W2 * W1; dO_dpt[8] = cs + oc * W2 * W2;
   } else {
+    const double aa[3] = {R.aa0, R.aa1, R.aa2};
     // first-order branch: out = pt + aa x pt
     out[0] = pt[0] + (aa[1] * pt[2] - aa[2] * pt[1]);
     out[1] = pt[1] + (aa[2] * pt[0] - aa[0] * pt[2]);
@@ -72,25 +130,14 @@ __device__ __forceinline__ void aarp_jac(const double aa[3], const double pt[3],
   }
 }
 
+__device__ __forceinline__ void aarp_jac(const double aa[3], const double pt[3], double out[3],
+                                         double dO_daa[9], double dO_dpt[9]) {
+  aarp_jac_s(rot_jet(aa), pt, out, dO_daa, dO_dpt);
+}
+
 // plain double ceres::AngleAxisRotatePoint
 __device__ __forceinline__ void aarp(const double aa[3], const double pt[3], double out[3]) {
-  const double theta2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
-  if (theta2 > 2.220446049250313e-16) {
-    const double th = sqrt(theta2);
-    double sn, cs;
-    sincos(th, &sn, &cs);
-    const double ti = 1.0 / th;
-    const double w0 = aa[0] * ti, w1 = aa[1] * ti, w2 = aa[2] * ti;
-    const double x0 = w1 * pt[2] - w2 * pt[1], x1 = w2 * pt[0] - w0 * pt[2], x2 = w0 * pt[1] - w1 * pt[0];
-    const double tmp = (w0 * pt[0] + w1 * pt[1] + w2 * pt[2]) * (1.0 - cs);
-    out[0] = pt[0] * cs + x0 * sn + w0 * tmp;
-    out[1] = pt[1] * cs + x1 * sn + w1 * tmp;
-    out[2] = pt[2] * cs + x2 * sn + w2 * tmp;
-  } else {
-    out[0] = pt[0] + (aa[1] * pt[2] - aa[2] * pt[1]);
-    out[1] = pt[1] + (aa[2] * pt[0] - aa[0] * pt[2]);
-    out[2] = pt[2] + (aa[0] * pt[1] - aa[1] * pt[0]);
-  }
+  aarp_s(rot_val(aa), pt, out);
 }
 
 __device__ __forceinline__ void residual(const double pose[6], const double X[3], double fx,
@@ -104,12 +151,12 @@ __device__ __forceinline__ void residual(const double pose[6], const double X[3]
 }
 
 // residual + Jp (2x3, d/dX) + Jc (2x6, d/d(aa,t))
-__device__ __forceinline__ void residual_jac(const double pose[6], const double X[3], double fx,
-                                             double fyv, double cx, double cy, double u, double v,
-                                             double r[2], double Jp[6], double Jc[12]) {
+__device__ __forceinline__ void residual_jac_s(const RotJet& R, const double t[3], const double X[3],
+                                               double fx, double fyv, double cx, double cy, double u,
+                                               double v, double r[2], double Jp[6], double Jc[12]) {
   double p[3], daa[9], dpt[9];
-  aarp_jac(pose, X, p, daa, dpt);
-  p[0] += pose[3]; p[1] += pose[4]; p[2] += pose[5];
+  aarp_jac_s(R, X, p, daa, dpt);
+  p[0] += t[0]; p[1] += t[1]; p[2] += t[2];
   const double iz = 1.0 / p[2];
   r[0] = p[0] / p[2] * fx + cx - u;
   r[1] = p[1] / p[2] * fyv + cy - v;
@@ -125,6 +172,23 @@ __device__ __forceinline__ void residual_jac(const double pose[6], const double 
   }
   Jc[3] = a0; Jc[4] = 0.0; Jc[5] = a2;
   Jc[9] = 0.0; Jc[10] = b1; Jc[11] = b2;
+}
+
+__device__ __forceinline__ void residual_jac(const double pose[6], const double X[3], double fx,
+                                             double fyv, double cx, double cy, double u, double v,
+                                             double r[2], double Jp[6], double Jc[12]) {
+  residual_jac_s(rot_jet(pose), pose + 3, X, fx, fyv, cx, cy, u, v, r, Jp, Jc);
+}
+
+// residual with a precomputed rotation state (t = pose[3..5])
+__device__ __forceinline__ void residual_s(const RotVal& R, const double t[3], const double X[3],
+                                           double fx, double fyv, double cx, double cy, double u,
+                                           double v, double r[2]) {
+  double p[3];
+  aarp_s(R, X, p);
+  p[0] += t[0]; p[1] += t[1]; p[2] += t[2];
+  r[0] = p[0] / p[2] * fx + cx - u;
+  r[1] = p[1] / p[2] * fyv + cy - v;
 }
 
 }  // namespace lorb
