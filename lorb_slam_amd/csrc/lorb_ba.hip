@@ -832,6 +832,20 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   }
   __syncthreads();
   for (int k = t; k < n; k += 256) d.ycam[W.row_base + k] = z[k];
+  // candidate cameras x + D^-1 delta (into x_pose[cur ^ 1]) and their rotation states
+  {
+    const int cur = d.st[w].cur;
+    for (int ci = t; ci < W.n_poses; ci += 256) {
+      const int c = W.pose_base + ci;
+      double xn[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        xn[k] = d.x_pose[cur][6 * c + k] + (-z[6 * ci + k]) * d.scale_pose[6 * c + k];
+        d.x_pose[cur ^ 1][6 * c + k] = xn[k];
+      }
+      d.rot_cand[c] = lorb::rot_val(xn);
+    }
+  }
 #ifdef LORB_CHOL_STAMPS
   if (t == 0) { d.dbg[8 * w + 3] = __builtin_amdgcn_s_memtime() - T0 - d.dbg[8*w] - d.dbg[8*w+1] - d.dbg[8*w+2]; }
 #endif
@@ -933,7 +947,7 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
         m0 += d.obs_Jc[12 * m + k] * s;
         m1 += d.obs_Jc[12 * m + 6 + k] * s;
       }
-      // candidate camera (k_ba_cand): x_pose[cur ^ 1] with its rotation state
+      // candidate camera (end of k_ba_chol): x_pose[cur ^ 1] with its rotation state
       residual_s(d.rot_cand[c], d.x_pose[cur ^ 1] + 6 * c + 3, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
     } else {
       double pose[6];
@@ -954,22 +968,48 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
   }
 }
 
-// K7b: per-camera candidate pose x + D^-1 delta (into x_pose[cur ^ 1]) and its rotation state
-__global__ __launch_bounds__(64) void k_ba_cand(BaDev d, int ctot) {
-  const int c = blockIdx.x * 64 + threadIdx.x;
-  if (c >= ctot) return;
-  const int w = d.cam_win[c];
-  const WinState& S = d.st[w];
-  if (S.done || S.chol_fail) return;
-  const BaWin& W = d.win[w];
-  const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
-  double xn[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    xn[k] = d.x_pose[S.cur][6 * c + k] + (-y[k]) * d.scale_pose[6 * c + k];
-    d.x_pose[S.cur ^ 1][6 * c + k] = xn[k];
+// K8 decision (lane 0): step validity, tolerances, accept/reject; returns 1 if accepted
+__device__ int lm_decide(BaDev d, const LMOpt& o, int w, WinState S, bool valid, double mccs,
+                         double ncost, double sn2) {
+  const double model_cost_change = -mccs;
+  valid = valid && isfinite(model_cost_change) && isfinite(sn2) && model_cost_change > 0.0;
+  if (!valid) {
+    if (++S.n_invalid >= o.max_invalid) {
+      S.done = 1; S.term = LORB_TERM_FAILURE;
+    } else {
+      S.radius = S.radius / S.decrease_factor;
+      S.decrease_factor *= 2.0;
+      S.last_successful = 0;
+    }
+    d.st[w] = S;
+    return 0;
   }
-  d.rot_cand[c] = lorb::rot_val(xn);
+  S.n_invalid = 0;
+  const double new_cost = isfinite(ncost) ? ncost : 1.7976931348623157e308;
+  const double step_norm = sqrt(sn2);
+  if (step_norm <= o.ptol * (S.x_norm + o.ptol)) {
+    S.done = 1; S.term = LORB_TERM_PARAMETER_TOL; d.st[w] = S; return 0;
+  }
+  const double cost_change = S.cost - new_cost;
+  if (fabs(cost_change) <= o.ftol * S.cost) {
+    S.done = 1; S.term = LORB_TERM_FUNCTION_TOL; d.st[w] = S; return 0;
+  }
+  const double rel = cost_change / model_cost_change;
+  if (rel > o.min_rel) {
+    S.cur ^= 1;
+    S.relin = 1;
+    S.n_success++;
+    const double tt = 2.0 * rel - 1.0;
+    S.radius = S.radius / fmax(1.0 / 3.0, 1.0 - tt * tt * tt);
+    S.radius = fmin(o.max_radius, S.radius);
+    S.decrease_factor = 2.0;
+  } else {
+    S.last_successful = 0;
+    S.radius = S.radius / S.decrease_factor;
+    S.decrease_factor *= 2.0;
+  }
+  d.st[w] = S;
+  return rel > o.min_rel;
 }
 
 // K8: per-window iteration tail: camera candidate, step validity, tolerances, accept/reject
@@ -990,54 +1030,21 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
     const int cur = S.cur;
     for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64) {
       const bool active = d.cam_obs_off[c + 1] > d.cam_obs_off[c];
-      const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
       for (int k = 0; k < 6; ++k) {
         const double x = d.x_pose[cur][6 * c + k];
-        const double xn = d.x_pose[cur ^ 1][6 * c + k];  // written by k_ba_cand
+        const double xn = d.x_pose[cur ^ 1][6 * c + k];  // written by k_ba_chol
         if (active) sn2 += (x - xn) * (x - xn);
       }
     }
     mccs = wave_sum(mccs); ncost = wave_sum(ncost); sn2 = wave_sum(sn2);
   }
-  if (lane != 0) return;
-  const double model_cost_change = -mccs;
-  valid = valid && isfinite(model_cost_change) && isfinite(sn2) && model_cost_change > 0.0;
-  if (!valid) {
-    if (++S.n_invalid >= o.max_invalid) {
-      S.done = 1; S.term = LORB_TERM_FAILURE;
-    } else {
-      S.radius = S.radius / S.decrease_factor;
-      S.decrease_factor *= 2.0;
-      S.last_successful = 0;
-    }
-    d.st[w] = S;
-    return;
-  }
-  S.n_invalid = 0;
-  const double new_cost = isfinite(ncost) ? ncost : 1.7976931348623157e308;
-  const double step_norm = sqrt(sn2);
-  if (step_norm <= o.ptol * (S.x_norm + o.ptol)) {
-    S.done = 1; S.term = LORB_TERM_PARAMETER_TOL; d.st[w] = S; return;
-  }
-  const double cost_change = S.cost - new_cost;
-  if (fabs(cost_change) <= o.ftol * S.cost) {
-    S.done = 1; S.term = LORB_TERM_FUNCTION_TOL; d.st[w] = S; return;
-  }
-  const double rel = cost_change / model_cost_change;
-  if (rel > o.min_rel) {
-    S.cur ^= 1;
-    S.relin = 1;
-    S.n_success++;
-    const double tt = 2.0 * rel - 1.0;
-    S.radius = S.radius / fmax(1.0 / 3.0, 1.0 - tt * tt * tt);
-    S.radius = fmin(o.max_radius, S.radius);
-    S.decrease_factor = 2.0;
-  } else {
-    S.last_successful = 0;
-    S.radius = S.radius / S.decrease_factor;
-    S.decrease_factor *= 2.0;
-  }
-  d.st[w] = S;
+  __shared__ int s_accept;
+  if (lane == 0) s_accept = lm_decide(d, o, w, S, valid, mccs, ncost, sn2);
+  __syncthreads();
+  // accepted: the candidate is the new linearisation point -> its rotation states for k_ba_lin
+  if (s_accept)
+    for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64)
+      d.rot_lin[c] = lorb::rot_jet(d.x_pose[S.cur ^ 1] + 6 * c);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1410,6 +1417,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   LORB_TRY(dalloc(P, (size_t)P->Ctot, &d.rot_cand));
   LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
   LORB_TRY(dalloc(P, (size_t)P->env_total, &d.env)); LORB_TRY(dalloc(P, (size_t)P->n_total, &d.rhs));
+  if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, ctx->stream));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
   LORB_TRY(dalloc(P, (size_t)nw * 8, &d.dbg));
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
@@ -1424,7 +1432,6 @@ constexpr int kLdsBudget = 160 * 1024 - 2048;
 void enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = P->ctx->stream;
   const BaDev& d = P->dev;
-  if (P->Ctot) hipLaunchKernelGGL(k_ba_rot_lin, dim3(lorb::ceil_div(P->Ctot, 64)), dim3(64), 0, s, d, P->Ctot);
   if (P->n_pblk) {
     lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
     hipLaunchKernelGGL(k_ba_lin, dim3(P->n_pblk), dim3(kGB), 0, s, d);
@@ -1440,7 +1447,11 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   const BaDev& d = P->dev;
   enqueue_linearize(P, o);
   if (P->n_pblk) hipLaunchKernelGGL(k_ba_point_prep, dim3(P->n_pblk), dim3(kGB), 0, s, d, o);
-  if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
+  // The LDS Cholesky never writes env, and k_ba_schur rewrites every stored entry of every
+  // block each iteration, so the band's structural zeros (set at plan creation) persist; the
+  // in-place global variant needs them restored.
+  const bool chol_in_lds = sizeof(double) * (size_t)P->max_env <= (size_t)kLdsBudget;
+  if (P->env_total && !chol_in_lds) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   if (P->n_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
     hipLaunchKernelGGL(k_ba_schur, dim3(P->n_bp), dim3(256), 0, s, d, o, P->n_bp);
@@ -1448,7 +1459,7 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   if (P->Ctot) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
     const size_t lds = sizeof(double) * (size_t)P->max_env;
-    const bool in_lds = lds <= (size_t)kLdsBudget;
+    const bool in_lds = chol_in_lds;
     const int rows = NB + P->max_bw;  // panel rows held in registers by wave 0
     const int rpl = rows <= 64 ? 1 : rows <= 128 ? 2 : rows <= 256 ? 4 : 8;
 #define LORB_CHOL(L, R) hipLaunchKernelGGL((k_ba_chol<L, R>), dim3(P->W), dim3(256), L ? lds : 0, s, d)
@@ -1456,7 +1467,6 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
     else { if (rpl == 1) LORB_CHOL(false, 1); else if (rpl == 2) LORB_CHOL(false, 2); else if (rpl == 4) LORB_CHOL(false, 4); else LORB_CHOL(false, 8); }
 #undef LORB_CHOL
   }
-  if (P->Ctot) hipLaunchKernelGGL(k_ba_cand, dim3(lorb::ceil_div(P->Ctot, 64)), dim3(64), 0, s, d, P->Ctot);
   if (P->n_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->n_pblk), dim3(kGB), 0, s, d);
   hipLaunchKernelGGL(k_ba_lm_end, dim3(P->W), dim3(64), 0, s, d, o);
   LORB_CHECK_LAUNCH(ctx);
@@ -1476,6 +1486,8 @@ int plan_solve(lorb_ba_plan* P, const lorb_lm_options* opt) {
   if (P->Ctot) LORB_HIP(ctx, hipMemcpyAsync(P->dev.x_pose[0], P->dev.x_init_pose, sizeof(double) * 6 * P->Ctot, hipMemcpyDeviceToDevice, ctx->stream));
   if (P->Ptot) LORB_HIP(ctx, hipMemcpyAsync(P->dev.x_pt[0], P->dev.x_init_pt, sizeof(double) * 3 * P->Ptot, hipMemcpyDeviceToDevice, ctx->stream));
   hipLaunchKernelGGL(k_ba_init, dim3(lorb::ceil_div(P->W, 64)), dim3(64), 0, ctx->stream, P->dev, P->W, o);
+  // rotation states of the initial linearisation point (later ones: k_ba_lm_end on acceptance)
+  if (P->Ctot) hipLaunchKernelGGL(k_ba_rot_lin, dim3(lorb::ceil_div(P->Ctot, 64)), dim3(64), 0, ctx->stream, P->dev, P->Ctot);
   LORB_CHECK_LAUNCH(ctx);
   const bool timing = ctx->ktime;  // per-kernel events cannot live inside a graph
   if (!timing && (!P->has_graph || memcmp(&P->graph_opt, &o, sizeof(LMOpt)) != 0)) {
