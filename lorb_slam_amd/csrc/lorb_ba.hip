@@ -851,6 +851,211 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
 #endif
 }
 
+// K6w: banded Cholesky for band <= 48 on ONE wavefront per window, no workgroup barrier.
+// The active 64 x 64 trailing window (rows/cols kb .. kb+63) lives in registers as ten 16 x 16
+// tiles (I, J), J <= I < 4, in the v_mfma_f64_16x16x4f64 accumulator layout (register r of
+// lane l: row 4r + (l >> 4), column l & 15).  Per 16-column panel:
+//   1. the panel tiles (I, 0) go through a 64 x 17 LDS exchange to lane = row layout;
+//   2. the 64 x 16 panel is factored in registers (v_readlane pivots, rsqrt + Newton, the
+//      forward substitution fused);
+//   3. L is stored into the LDS band (for the back-substitution) and re-read as MFMA operands
+//      (A and B fragments of a tile are the same registers: B = L_J^T);
+//   4. the rank-16 trailing update of tiles (I, J >= 1) runs as 24 MFMAs;
+//   5. the window slides by 16: tiles move up-left, and the new bottom tile row comes straight
+//      from S, because no earlier panel reaches it (L(i, k) = 0 for i - k > bw <= 48).
+// Rows n .. n16-1 are an identity pad, so every panel is full; the next bottom tile row is
+// prefetched one panel ahead.
+__device__ __forceinline__ constexpr int tri4(int I, int J) { return I * (I + 1) / 2 + J; }
+
+__global__ __launch_bounds__(256) void k_ba_chol_w(BaDev d) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int w = blockIdx.x;
+  if (d.st[w].done) return;
+  const BaWin W = d.win[w];
+  const int n = W.n, bw = W.bw;
+  const int n16 = (n + 15) & ~15;
+  const int t = threadIdx.x, lane = t & 63, ci = lane & 15, ck = lane >> 4;
+  double* A = smem;                          // S band, overwritten in place by L: n16 x (bw + 1)
+  double* z = A + (size_t)n16 * (bw + 1);    // rhs, overwritten by the forward substitution
+  double* invd = z + n16;                    // n16
+  double* xch = invd + n16;                  // 64 x 17 exchange
+  const int dummy = (int)(xch + 64 * 17 + lane - A);  // 64 per-lane dummy slots after xch
+  {  // stage S (+ identity pad rows) and rhs with all four waves, then wave 0 works alone
+    const double* __restrict__ S = d.env + W.env_base;
+    const int ne = n * (bw + 1);
+    for (int k = t; k < ne; k += 256) A[k] = S[k];
+    for (int k = ne + t; k < n16 * (bw + 1); k += 256) A[k] = (k % (bw + 1)) == bw ? 1.0 : 0.0;
+    for (int k = t; k < n16; k += 256) z[k] = k < n ? d.rhs[W.row_base + k] : 0.0;
+  }
+  __syncthreads();
+  if (t >= 64) return;
+#ifdef LORB_CHOL_STAMPS
+  unsigned long long T0 = __builtin_amdgcn_s_memtime(), tq = T0, ph[5] = {0, 0, 0, 0, 0};
+#define CW_STAMP(k) do { const unsigned long long q_ = __builtin_amdgcn_s_memtime(); ph[k] += q_ - tq; tq = q_; } while (0)
+#else
+#define CW_STAMP(k) do {} while (0)
+#endif
+  auto sget = [&](int i, int j) -> double {  // band entry (i, j) of the staged matrix; branch-free
+    const bool ok = j <= i && i - j <= bw && i < n16;
+    const double v = A[ok ? i * (bw + 1) + (j - i + bw) : 0];
+    return ok ? v : 0.0;
+  };
+  v4d T[10], Tn[4];
+#pragma unroll
+  for (int I = 0; I < 4; ++I)
+#pragma unroll
+    for (int J = 0; J <= I; ++J)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[tri4(I, J)][r] = sget(16 * I + ck + 4 * r, 16 * J + ci);
+  double zr = z[lane];
+  bool bad = false;
+  for (int kb = 0; kb < n16; kb += 16) {
+    // the tile row that enters at the end of this panel (rows kb+64 .. kb+79): untouched S
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Tn[J][r] = sget(kb + 64 + ck + 4 * r, kb + 16 + 16 * J + ci);
+    const double zin = kb + 16 + lane < n16 ? z[kb + 16 + lane] : 0.0;  // used by lanes >= 48
+    // 1. panel tiles -> lane = row
+#pragma unroll
+    for (int I = 0; I < 4; ++I)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xch[(16 * I + ck + 4 * r) * 17 + ci] = T[tri4(I, 0)][r];
+    wave_sync_lds();
+    double P[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) P[q] = xch[lane * 17 + q];
+    wave_sync_lds();
+    CW_STAMP(0);
+    // 2. factor the panel (lane = row kb + lane; entries above the diagonal are never stored)
+    double yq = 0.0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const double akk = readlane_d(P[q], q);
+      bad |= !(akk > 0.0);
+      const double y = rsqrt_refined(akk);
+      P[q] *= y;  // lane q: akk * y = L(k, k)
+      yq = lane == q ? y : yq;
+      const double zk = readlane_d(zr, q) * y;
+      zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
+#pragma unroll
+      for (int q2 = q + 1; q2 < NB; ++q2) {
+        const double l = readlane_d(P[q], q2);
+        P[q2] = fma(-P[q], l, P[q2]);
+      }
+    }
+    CW_STAMP(1);
+    // 3. L into the band (rows kb .. kb+63 have left S's use) + exchange; final z of the panel
+    {
+      const int row = kb + lane;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int col = kb + q;
+        // branch-free: entries outside the band / above the diagonal go to a per-lane dummy slot
+        const bool ok = row < n16 && col <= row && row - col <= bw;
+        A[ok ? row * (bw + 1) + (col - row + bw) : dummy] = P[q];
+        xch[lane * 17 + q] = P[q];
+      }
+      if (lane < NB) { z[row] = zr; invd[row] = yq; }
+    }
+    wave_sync_lds();
+    double opA[4][4];  // [I][kk] = L(kb + 16 I + ci, kb + 4 kk + ck), I >= 1
+#pragma unroll
+    for (int I = 1; I < 4; ++I)
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) opA[I][kk] = xch[(16 * I + ci) * 17 + 4 * kk + ck];
+    CW_STAMP(2);
+    // 4. rank-16 trailing update (J = 1 first: it is the next panel)
+#pragma unroll
+    for (int J = 1; J < 4; ++J)
+#pragma unroll
+      for (int I = J; I < 4; ++I)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          T[tri4(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[J][kk], T[tri4(I, J)], 0, 0, 0);
+    // 5. slide the window by 16 rows / columns
+    {
+      const double zs = __shfl_down(zr, 16, 64);  // rows kb+16 .. kb+63 move up
+      zr = lane < 48 ? zs : zin;                  // rows kb+64 .. kb+79 enter (raw rhs)
+    }
+    T[tri4(0, 0)] = T[tri4(1, 1)];
+    T[tri4(1, 0)] = T[tri4(2, 1)]; T[tri4(1, 1)] = T[tri4(2, 2)];
+    T[tri4(2, 0)] = T[tri4(3, 1)]; T[tri4(2, 1)] = T[tri4(3, 2)]; T[tri4(2, 2)] = T[tri4(3, 3)];
+#pragma unroll
+    for (int J = 0; J < 4; ++J) T[tri4(3, J)] = Tn[J];
+    CW_STAMP(3);
+  }
+  if (bad) {
+#ifdef LORB_CHOL_STAMPS
+    if (lane == 0) for (int k = 0; k < 5; ++k) d.dbg[8 * w + k] = ph[k];
+#endif
+    if (lane == 0) d.st[w].chol_fail = 1;
+    return;
+  }
+  wave_sync_lds();
+  // back substitution L^T y = z by 16-row blocks from the bottom.  Lane (g, j) = (lane >> 4,
+  // lane & 15): the block's column j gathers sum_i L(i, j) y_i over the rows below (split over
+  // the four lane groups, butterfly-reduced), then the 16 x 16 triangle is solved with
+  // v_readlane broadcasts.
+  {
+    const int jc = lane & 15, g = lane >> 4;
+    for (int c0 = n16 - 16; c0 >= 0; c0 -= 16) {
+      const int j = c0 + jc;
+      double lk[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {  // L(c0 + k, j), k > jc
+        const bool ok = k > jc;
+        const double v = A[ok ? (c0 + k) * (bw + 1) + (j - (c0 + k) + bw) : 0];
+        lk[k] = ok ? v : 0.0;
+      }
+      // rows i = c0+16+g+4u (u < 16) cover every row below the block that reaches column j
+      // (i - j <= bw <= 48); all loads are issued before the FMAs, four independent chains
+      const int iend = min(n16 - 1, j + bw);
+      double av[16], zv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = c0 + 16 + g + 4 * u;
+        const bool ok = i <= iend;
+        av[u] = A[ok ? i * (bw + 1) + (j - i + bw) : 0];
+        zv[u] = z[ok ? i : 0];
+        av[u] = ok ? av[u] : 0.0;
+      }
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a4[u & 3] = fma(av[u], zv[u], a4[u & 3]);
+      double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      acc += __shfl_xor(acc, 16, 64);
+      acc += __shfl_xor(acc, 32, 64);
+      double zb = z[j] - acc;
+      const double iv = invd[j];
+#pragma unroll
+      for (int k = NB - 1; k >= 0; --k) {
+        const double yk = readlane_d(zb, k) * readlane_d(iv, k);
+        zb = jc == k ? yk : fma(-lk[k], yk, zb);
+      }
+      if (g == 0) z[j] = zb;
+      wave_sync_lds();
+    }
+  }
+  CW_STAMP(4);
+#ifdef LORB_CHOL_STAMPS
+  if (lane == 0) for (int k = 0; k < 5; ++k) d.dbg[8 * w + k] = ph[k];
+#endif
+#undef CW_STAMP
+  for (int k = lane; k < n; k += 64) d.ycam[W.row_base + k] = z[k];
+  const int cur = d.st[w].cur;
+  for (int ci2 = lane; ci2 < W.n_poses; ci2 += 64) {
+    const int c = W.pose_base + ci2;
+    double xn[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      xn[k] = d.x_pose[cur][6 * c + k] + (-z[6 * ci2 + k]) * d.scale_pose[6 * c + k];
+      d.x_pose[cur ^ 1][6 * c + k] = xn[k];
+    }
+    d.rot_cand[c] = lorb::rot_val(xn);
+  }
+}
+
 // K7: point-group back-substitution: b_p -= sum_e W_e^T y_c(e) (observation phase + ordered
 // point reduction), point step / candidate (point phase), model cost change and candidate cost
 // per observation (observation phase).
@@ -1242,7 +1447,7 @@ LMOpt to_dev_opt(const lorb_lm_options* o) {
 struct lorb_ba_plan {
   lorb_ctx* ctx = nullptr;
   int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_bp = 0, n_pairs = 0;
-  int env_total = 0, n_total = 0, max_env = 0, max_bw = 0;
+  int env_total = 0, n_total = 0, max_env = 0, max_bw = 0, max_env_w = 0;
   std::vector<BaWin> hwin;
   std::vector<void*> allocs;
   BaDev dev{};
@@ -1362,6 +1567,10 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     bw.env_base = env_base; bw.env_size = n * (bwid + 1); bw.n = n; bw.row_base = row_base; bw.bw = bwid;
     P->max_env = std::max(P->max_env, bw.env_size + 2 * n);
     P->max_bw = std::max(P->max_bw, bwid);
+    {
+      const int n16 = (n + 15) & ~15;
+      P->max_env_w = std::max(P->max_env_w, n16 * (bwid + 1) + 2 * n16 + 64 * 18);
+    }
     env_base += bw.env_size; row_base += n;
     // point groups: consecutive points with <= kGB observations (and <= kGB points) in total
     bw.pblk_base = (int)pblk.size();
@@ -1456,7 +1665,12 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
     hipLaunchKernelGGL(k_ba_schur, dim3(P->n_bp), dim3(256), 0, s, d, o, P->n_bp);
   }
-  if (P->Ctot) {
+  static const bool force_old = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'o'; }();
+  const bool chol_w = !force_old && P->max_bw <= 48 && sizeof(double) * (size_t)P->max_env_w <= (size_t)kLdsBudget;
+  if (P->Ctot && chol_w) {
+    lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
+    hipLaunchKernelGGL(k_ba_chol_w, dim3(P->W), dim3(256), sizeof(double) * (size_t)P->max_env_w, s, d);
+  } else if (P->Ctot) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
     const size_t lds = sizeof(double) * (size_t)P->max_env;
     const bool in_lds = chol_in_lds;

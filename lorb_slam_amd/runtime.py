@@ -230,3 +230,5 @@ class BAPlan:
 
 Context.ba_pose_only = _ba_pose_only
 Context.ba_local = _ba_local
+
+from . import window as _window  # noqa: E402,F401  (binds the windowed-matcher methods onto Context)
