@@ -320,6 +320,44 @@ int lorb_ba_plan_destroy(lorb_ba_plan* plan);
 /* diagnostics: Cholesky phase stamps of window 0 (non-zero only in LORB_CHOL_STAMPS builds) */
 int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8);
 
+/* ----------------------------------------------------------------------------------------
+ * Multi-GPU: point-partitioned ("sharded") local BA.  No reference counterpart:
+ * the reference is single-process (its Ceres solve is src/bundle_adjust.cpp:308-314).
+ *
+ * One process (or thread) per GPU, each with its own lorb_ctx.  Every rank passes the SAME
+ * window poses / fixed poses / intrinsics and only ITS points with all of their observations
+ * (every observation of a point on the rank that owns the point).  Per LM iteration the ranks
+ * all-reduce (i) the camera normal blocks, cost and gradient norms of the linearisation,
+ * (ii) the reduced camera system S and its right-hand side, (iii) the model/candidate cost
+ * and step norms.  The Cholesky of S and every LM decision are replicated, so all ranks hold
+ * identical poses; each rank holds its own points.
+ *
+ * Communicators: RCCL (ncclAllReduce on the ctx stream, capturable in the LM hipGraph) or a
+ * host callback (any host transport, e.g. gloo in tests; the plan then runs eagerly).
+ * -------------------------------------------------------------------------------------- */
+#define LORB_OP_SUM 0
+#define LORB_OP_MAX 1
+#define LORB_OP_MIN 2
+#define LORB_UNIQUE_ID_BYTES 128
+typedef struct lorb_comm lorb_comm;
+/* host all-reduce over all ranks, in place on `buf` (count doubles); returns 0 on success */
+typedef int (*lorb_host_allreduce_fn)(void* user, double* buf, int64_t count, int32_t op);
+
+int lorb_comm_unique_id(void* id_out /* LORB_UNIQUE_ID_BYTES */);        /* rank 0 only */
+int lorb_comm_init_rccl(lorb_ctx* ctx, int32_t nranks, int32_t rank, const void* unique_id,
+                        lorb_comm** out);
+int lorb_comm_init_host(lorb_ctx* ctx, int32_t nranks, int32_t rank, lorb_host_allreduce_fn fn,
+                        void* user, lorb_comm** out);
+int lorb_comm_destroy(lorb_comm* comm);
+/* all-reduce of device doubles on the ctx stream (send == recv allowed) */
+int lorb_comm_allreduce_f64(lorb_comm* comm, const double* d_send, double* d_recv, int64_t count,
+                            int32_t op);
+
+/* plan over this rank's shard of each window; solve / read / destroy as lorb_ba_plan_*.
+ * read returns the (replicated) poses and this rank's points. */
+int lorb_ba_plan_create_sharded(lorb_ctx* ctx, lorb_comm* comm, int32_t n_windows,
+                                const lorb_ba_window* shards, lorb_ba_plan** out);
+
 /* Rodrigues vector -> Tcw (float), cv::Rodrigues semantics (double internally). */
 void lorb_pose_to_Tcw(const float rvec[3], const float tvec[3], float Tcw[16]);
 

@@ -34,6 +34,7 @@ struct BaWin {
   int pblk_base, n_pblk;
   int env_base, env_size, n, row_base, bw;  // S band: row i holds cols [i-bw, i]
   int obs_base, n_obs;
+  int n_obs_all;  // observations of the window over all ranks (== n_obs unless sharded)
   double fx, fy, cx, cy;
 };
 struct PBlk { int win, p0, cnt, o0, no; };  // point group: points [p0, p0+cnt), obs [o0, o0+no)
@@ -149,8 +150,17 @@ struct BaDev {
   double* obs_Q;             // K*6: Q = Jps E^-1 (2x3); W = Jcs^T Jps is rank 2, so the Schur
                              //      block Y_h W_l^T = Jcs_h^T (Q_h Jps_l^T) Jcs_l
   double* obs_g;             // K*2: g = Q b_p  (rhs: Y_h b_p = Jcs_h^T g)
-  double* env;               // S envelopes
+  double* env;               // S envelopes (all-reduced when sharded)
   double* rhs;               // sum n
+  // sharded plans: kernels write the *_part buffers, the all-reduce produces the
+  // global ones (unsharded: *_part == global).  Contiguous per exchange:
+  //   lin   [U | V | wlin (2W: cost, point |x|^2)]  sum;   wmax (W: point gradient max)  max
+  //   solve [env | rhs | wfail (W)]                 sum
+  //   step  wstep (3W: model cost change, candidate cost, point |step|^2)  sum
+  double *U_part, *V_part, *wlin, *wlin_part, *wmax, *wmax_part;
+  double *env_part, *rhs_part, *wfail, *wfail_part, *wstep, *wstep_part;
+  const int* cam_active;     // Ctot: camera observed by some rank
+  int sharded, rank0;
   double* ycam;              // sum n (solution, scaled space, y = -step)
   double* part;              // n_pblk * 8 partials
   unsigned long long* dbg;   // diagnostic stamps (LORB_CHOL_STAMPS builds only)
@@ -169,7 +179,7 @@ __global__ void k_ba_init(BaDev d, int W, LMOpt o) {
   WinState s;
   s.radius = o.init_radius; s.decrease_factor = 2.0; s.cost = 0.0; s.x_norm = 0.0; s.gmax = 0.0;
   s.initial_cost = 0.0; s.iter = 0; s.n_success = 0; s.n_invalid = 0;
-  s.done = d.win[w].n_obs == 0 ? 1 : 0;
+  s.done = d.win[w].n_obs_all == 0 ? 1 : 0;
   s.relin = 1; s.cur = 0; s.last_successful = 1; s.term = 0; s.chol_fail = 0; s.pad = 0;
   d.st[w] = s;
 }
@@ -341,28 +351,39 @@ __global__ __launch_bounds__(256) void k_ba_camera(BaDev d) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) V[k] = ((red[0][21 + k] + red[1][21 + k]) + red[2][21 + k]) + red[3][21 + k];
 #pragma unroll
-    for (int k = 0; k < 21; ++k) d.U[21 * c + k] = U[k];
+    for (int k = 0; k < 21; ++k) d.U_part[21 * c + k] = U[k];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) d.V[6 * c + k] = V[k];
-    double gm = 0.0;
-    if (a1 > a0) {
-      const int cur = S.cur;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const double x = d.x_pose[cur][6 * c + k];
-        gm = fmax(gm, fabs(x - (x + -V[k])));
-      }
-    }
-    d.cam_gmax[c] = gm;
-    if (S.iter == 0) {
-      const int dg[6] = {0, 6, 11, 15, 18, 20};
-#pragma unroll
-      for (int k = 0; k < 6; ++k) d.scale_pose[6 * c + k] = 1.0 / (1.0 + sqrt(U[dg[k]]));
-    }
+    for (int k = 0; k < 6; ++k) d.V_part[6 * c + k] = V[k];
+  }
+}
+
+// K2b (sharded plans): per-window reduction of the point-group partials of one phase into the
+// exchange buffers (PH 0: cost, point |x|^2 (sum) and point gradient max; PH 1: model cost
+// change, candidate cost, point |step|^2), fixed lane order + butterfly.
+template <int PH>
+__global__ __launch_bounds__(64) void k_ba_win_reduce(BaDev d) {
+  const int w = blockIdx.x;
+  if (d.st[w].done) return;
+  const BaWin& W = d.win[w];
+  const int lane = threadIdx.x;
+  double a = 0.0, b = 0.0, c = 0.0;
+  for (int g = lane; g < W.n_pblk; g += 64) {
+    const double* P = d.part + 8 * (W.pblk_base + g);
+    if (PH == 0) { a += P[0]; b += P[2]; c = fmax(c, P[1]); }
+    else { a += P[3]; b += P[4]; c += P[5]; }
+  }
+  a = wave_sum(a); b = wave_sum(b);
+  c = PH == 0 ? wave_max(c) : wave_sum(c);
+  if (lane == 0) {
+    if (PH == 0) { d.wlin_part[2 * w] = a; d.wlin_part[2 * w + 1] = b; d.wmax_part[w] = c; }
+    else { d.wstep_part[3 * w] = a; d.wstep_part[3 * w + 1] = b; d.wstep_part[3 * w + 2] = c; }
   }
 }
 
 // K3: per-window iteration head: finalise the (re)linearisation, termination checks
+// Camera terms (gradient max, |x|^2, iteration-0 Jacobi scale) come from the (all-reduced)
+// U / V blocks; point terms from the point-group partials (SH: from the exchange buffers).
+template <bool SH>
 __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
   const int w = blockIdx.x;
   const WinState* Sp = d.st + w;
@@ -370,20 +391,31 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
   WinState S = *Sp;
   const BaWin W = d.win[w];
   const int lane = threadIdx.x;
+  if (SH && lane == 0) d.wfail_part[w] = 0.0;  // point-block failures of this iteration (K4)
   if (S.relin) {
     // fixed lane assignment + fixed butterfly => deterministic
     double cost = 0.0, gm = 0.0, xn2 = 0.0;
-    for (int b = lane; b < W.n_pblk; b += 64) {
-      const double* P = d.part + 8 * (W.pblk_base + b);
-      cost += P[0]; gm = fmax(gm, P[1]); xn2 += P[2];
+    if (!SH) {
+      for (int b = lane; b < W.n_pblk; b += 64) {
+        const double* P = d.part + 8 * (W.pblk_base + b);
+        cost += P[0]; gm = fmax(gm, P[1]); xn2 += P[2];
+      }
     }
     const int cur = S.cur;
     for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64) {
-      if (d.cam_obs_off[c + 1] == d.cam_obs_off[c]) continue;
-      gm = fmax(gm, d.cam_gmax[c]);
-      for (int k = 0; k < 6; ++k) { const double x = d.x_pose[cur][6 * c + k]; xn2 += x * x; }
+      if (S.iter == 0) {
+        const int dg[6] = {0, 6, 11, 15, 18, 20};
+        for (int k = 0; k < 6; ++k) d.scale_pose[6 * c + k] = 1.0 / (1.0 + sqrt(d.U[21 * c + dg[k]]));
+      }
+      if (!d.cam_active[c]) continue;
+      for (int k = 0; k < 6; ++k) {
+        const double x = d.x_pose[cur][6 * c + k];
+        gm = fmax(gm, fabs(x - (x + -d.V[6 * c + k])));
+        xn2 += x * x;
+      }
     }
     cost = wave_sum(cost); gm = wave_max(gm); xn2 = wave_sum(xn2);
+    if (SH) { cost += d.wlin[2 * w]; xn2 += d.wlin[2 * w + 1]; gm = fmax(gm, d.wmax[w]); }
     S.cost = cost;
     S.gmax = gm;
     S.x_norm = sqrt(xn2);
@@ -422,7 +454,9 @@ __global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
     E[5] += fmin(fmax(E[5], o.min_diag), o.max_diag) / rad;
     double Ei[6];
     if (!inv3(E, Ei)) {
-      d.st[g.win].chol_fail = 1;  // benign race: every writer stores 1
+      // benign race: every writer stores the same value; sharded plans reduce the flag (K5)
+      if (d.sharded) d.wfail_part[g.win] = 1.0;
+      else d.st[g.win].chol_fail = 1;
       for (int k = 0; k < 6; ++k) Ei[k] = 0.0;
     }
 #pragma unroll
@@ -524,12 +558,15 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o, int n_bp) {
     const double a = (((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]) *
                      d.scale_pose[6 * bp.ch + i] * d.scale_pose[6 * bp.cl + j];
     const int lh = bp.ch - W.pose_base, ll = bp.cl - W.pose_base;
-    double* A = d.env + W.env_base;
+    double* A = d.env_part + W.env_base;
     if (diag) {
       if (j <= i) {
-        const double* sc = d.scale_pose + 6 * bp.ch;
-        double v = d.U[21 * bp.ch + u21(i, j)] * sc[i] * sc[j];
-        if (i == j) v += fmin(fmax(v, o.min_diag), o.max_diag) / S.radius;
+        double v = 0.0;
+        if (d.rank0) {  // camera block J^T J + D^2 once (sharded: U is already global)
+          const double* sc = d.scale_pose + 6 * bp.ch;
+          v = d.U[21 * bp.ch + u21(i, j)] * sc[i] * sc[j];
+          if (i == j) v += fmin(fmax(v, o.min_diag), o.max_diag) / S.radius;
+        }
         band(A, W.bw, 6 * lh + i, 6 * lh + j) = v - a;
       }
     } else {
@@ -546,8 +583,8 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o, int n_bp) {
     __syncthreads();
     if (t < 6) {
       const double r = (((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]) * d.scale_pose[6 * bp.ch + t];
-      const double vs = d.V[6 * bp.ch + t] * d.scale_pose[6 * bp.ch + t];
-      d.rhs[W.row_base + 6 * (bp.ch - W.pose_base) + t] = vs - r;
+      const double vs = d.rank0 ? d.V[6 * bp.ch + t] * d.scale_pose[6 * bp.ch + t] : 0.0;
+      d.rhs_part[W.row_base + 6 * (bp.ch - W.pose_base) + t] = vs - r;
     }
   }
 }
@@ -621,6 +658,10 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   __shared__ __attribute__((aligned(16))) double s_col[80];
   const int w = blockIdx.x;
   if (d.st[w].done) return;
+  if (d.sharded && d.wfail[w] > 0.0) {  // a rank's point block was not PD: the step is invalid
+    if (threadIdx.x == 0) d.st[w].chol_fail = 1;
+    return;
+  }
   const BaWin W = d.win[w];
   const int n = W.n, bw = W.bw;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -871,6 +912,10 @@ __global__ __launch_bounds__(256) void k_ba_chol_w(BaDev d) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int w = blockIdx.x;
   if (d.st[w].done) return;
+  if (d.sharded && d.wfail[w] > 0.0) {  // a rank's point block was not PD: the step is invalid
+    if (threadIdx.x == 0) d.st[w].chol_fail = 1;
+    return;
+  }
   const BaWin W = d.win[w];
   const int n = W.n, bw = W.bw;
   const int n16 = (n + 15) & ~15;
@@ -1218,6 +1263,7 @@ __device__ int lm_decide(BaDev d, const LMOpt& o, int w, WinState S, bool valid,
 }
 
 // K8: per-window iteration tail: camera candidate, step validity, tolerances, accept/reject
+template <bool SH>
 __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
   const int w = blockIdx.x;
   const WinState* Sp = d.st + w;
@@ -1228,13 +1274,15 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
   bool valid = !S.chol_fail;
   double mccs = 0.0, ncost = 0.0, sn2 = 0.0;
   if (valid) {
-    for (int b = lane; b < W.n_pblk; b += 64) {
-      const double* P = d.part + 8 * (W.pblk_base + b);
-      mccs += P[3]; ncost += P[4]; sn2 += P[5];
+    if (!SH) {
+      for (int b = lane; b < W.n_pblk; b += 64) {
+        const double* P = d.part + 8 * (W.pblk_base + b);
+        mccs += P[3]; ncost += P[4]; sn2 += P[5];
+      }
     }
     const int cur = S.cur;
     for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64) {
-      const bool active = d.cam_obs_off[c + 1] > d.cam_obs_off[c];
+      const bool active = d.cam_active[c];
       for (int k = 0; k < 6; ++k) {
         const double x = d.x_pose[cur][6 * c + k];
         const double xn = d.x_pose[cur ^ 1][6 * c + k];  // written by k_ba_chol
@@ -1242,6 +1290,7 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
       }
     }
     mccs = wave_sum(mccs); ncost = wave_sum(ncost); sn2 = wave_sum(sn2);
+    if (SH) { mccs += d.wstep[3 * w]; ncost += d.wstep[3 * w + 1]; sn2 += d.wstep[3 * w + 2]; }
   }
   __shared__ int s_accept;
   if (lane == 0) s_accept = lm_decide(d, o, w, S, valid, mccs, ncost, sn2);
@@ -1457,6 +1506,7 @@ struct lorb_ba_plan {
   hipGraphExec_t gexec = nullptr;
   LMOpt graph_opt{};
   bool has_graph = false;
+  lorb_comm* comm = nullptr;  // sharded plan (not owned)
   ~lorb_ba_plan() {
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -1485,6 +1535,45 @@ int dupload(lorb_ba_plan* P, const std::vector<T>& v, T** out) {
 int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P) {
   P->ctx = ctx;
   P->W = nw;
+  lorb_comm* comm = P->comm;
+  // sharded: band structure, camera activity and observation counts are global -- reduce the
+  // per-window first-coupled camera (min), per-camera and per-window observation counts (sum)
+  std::vector<std::vector<int>> g_fc(nw);
+  std::vector<std::vector<int>> g_cam_obs(nw);
+  std::vector<int> g_obs(nw, 0);
+  if (comm) {
+    size_t nfc = 0;
+    for (int w = 0; w < nw; ++w) nfc += (size_t)std::max(win[w].n_poses, 0);
+    std::vector<double> hmin(nfc), hsum(nfc + nw);
+    size_t o = 0;
+    for (int w = 0; w < nw; ++w) {
+      const lorb_ba_window& in = win[w];
+      std::vector<int> fc(std::max(in.n_poses, 0)), cobs(std::max(in.n_poses, 0), 0);
+      for (int c = 0; c < in.n_poses; ++c) fc[c] = c;
+      std::vector<std::vector<int>> pf(std::max(in.n_points, 0));
+      for (int k = 0; k < in.n_obs; ++k) {
+        const int p = in.obs_point[k], f = in.obs_frame[k];
+        if (p < 0 || p >= in.n_points || f >= in.n_poses || f < -in.n_fixed) continue;  // rejected below
+        if (f >= 0) { pf[p].push_back(f); cobs[f]++; }
+      }
+      for (auto& v : pf)
+        for (int a : v)
+          for (int b : v) fc[a] = std::min(fc[a], b);
+      for (int c = 0; c < in.n_poses; ++c) { hmin[o + c] = fc[c]; hsum[o + c] = cobs[c]; }
+      hsum[nfc + w] = in.n_obs;
+      o += in.n_poses;
+    }
+    LORB_TRY(lorb::comm_allreduce_host(comm, hmin.data(), hmin.size(), LORB_OP_MIN));
+    LORB_TRY(lorb::comm_allreduce_host(comm, hsum.data(), hsum.size(), LORB_OP_SUM));
+    o = 0;
+    for (int w = 0; w < nw; ++w) {
+      g_fc[w].resize(win[w].n_poses); g_cam_obs[w].resize(win[w].n_poses);
+      for (int c = 0; c < win[w].n_poses; ++c) { g_fc[w][c] = (int)hmin[o + c]; g_cam_obs[w][c] = (int)hsum[o + c]; }
+      g_obs[w] = (int)hsum[nfc + w];
+      o += win[w].n_poses;
+    }
+  }
+  std::vector<int> cam_active;
   std::vector<int> pt_obs_off(1, 0), obs_cam, obs_fix, obs_pt, cam_obs_off(1, 0), cam_obs, cam_win, obs_cm;
   std::vector<double2> obs_uv;
   std::vector<double> fixed, xpose, xpt;
@@ -1501,6 +1590,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     bw.point_base = point_base; bw.n_points = in.n_points;
     bw.fx = in.fx; bw.fy = in.fy; bw.cx = in.cx; bw.cy = in.cy;
     bw.obs_base = (int)obs_cam.size(); bw.n_obs = in.n_obs;
+    bw.n_obs_all = comm ? g_obs[w] : in.n_obs;
     // obs sorted by point (stable)
     std::vector<int> cnt(in.n_points + 1, 0);
     for (int k = 0; k < in.n_obs; ++k) {
@@ -1532,6 +1622,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
       for (int e : co[c]) { obs_cm[e] = (int)cam_obs.size(); cam_obs.push_back(e); }
       cam_obs_off.push_back((int)cam_obs.size());
       cam_win.push_back(w);
+      cam_active.push_back(comm ? (g_cam_obs[w][c] > 0) : !co[c].empty());
     }
     // block pairs: for each point, all ordered (obs_h, obs_l) with cam(h) >= cam(l)
     std::map<std::pair<int, int>, std::vector<int2>> bmap;
@@ -1561,6 +1652,8 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     // uniform band of S: bw = max_i (i - first_nonzero_col(i)); exact for Cholesky (no fill
     // outside the envelope, and the zero padding never changes a value)
     const int n = 6 * in.n_poses;
+    if (comm)
+      for (int c = 0; c < in.n_poses; ++c) fc[c] = std::min(fc[c], g_fc[w][c]);
     int bwid = 0;
     for (int c = 0; c < in.n_poses; ++c) bwid = std::max(bwid, 6 * c + 5 - 6 * fc[c]);
     if (n == 0) bwid = 0;
@@ -1619,13 +1712,34 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
   const size_t C = P->Ctot, Pn = P->Ptot, K = P->K;
   LORB_TRY(dalloc(P, C * 6, &d.scale_pose)); LORB_TRY(dalloc(P, Pn * 3, &d.scale_pt));
   LORB_TRY(dalloc(P, Pn * 6, &d.ete)); LORB_TRY(dalloc(P, Pn * 3, &d.etb)); LORB_TRY(dalloc(P, Pn * 6, &d.pinv));
-  LORB_TRY(dalloc(P, C * 21, &d.U)); LORB_TRY(dalloc(P, C * 6, &d.V)); LORB_TRY(dalloc(P, C, &d.cam_gmax));
+  int* dact = nullptr;
+  LORB_TRY(dupload(P, cam_active, &dact)); d.cam_active = dact;
+  // exchange buffers (see BaDev); unsharded plans alias *_part to the global buffers
+  const size_t W8 = (size_t)nw, lin_n = C * 27 + 2 * W8, solve_n = (size_t)P->env_total + P->n_total + W8;
+  double *lin, *linp, *mx, *mxp, *sol, *solp, *stp, *stpp;
+  LORB_TRY(dalloc(P, lin_n, &lin)); LORB_TRY(dalloc(P, W8, &mx));
+  LORB_TRY(dalloc(P, solve_n, &sol)); LORB_TRY(dalloc(P, 3 * W8, &stp));
+  if (comm) {
+    LORB_TRY(dalloc(P, lin_n, &linp)); LORB_TRY(dalloc(P, W8, &mxp));
+    LORB_TRY(dalloc(P, solve_n, &solp)); LORB_TRY(dalloc(P, 3 * W8, &stpp));
+    LORB_HIP(ctx, hipMemsetAsync(solp, 0, sizeof(double) * solve_n, ctx->stream));
+    LORB_HIP(ctx, hipMemsetAsync(linp, 0, sizeof(double) * lin_n, ctx->stream));
+  } else {
+    linp = lin; mxp = mx; solp = sol; stpp = stp;
+  }
+  d.U = lin; d.V = lin + C * 21; d.wlin = lin + C * 27; d.wmax = mx;
+  d.U_part = linp; d.V_part = linp + C * 21; d.wlin_part = linp + C * 27; d.wmax_part = mxp;
+  d.env = sol; d.rhs = sol + P->env_total; d.wfail = sol + P->env_total + P->n_total;
+  d.env_part = solp; d.rhs_part = solp + P->env_total; d.wfail_part = solp + P->env_total + P->n_total;
+  d.wstep = stp; d.wstep_part = stpp;
+  d.sharded = comm ? 1 : 0;
+  d.rank0 = comm ? (comm->rank == 0) : 1;
+  LORB_TRY(dalloc(P, C, &d.cam_gmax));
   LORB_TRY(dalloc(P, K * 2, &d.obs_r)); LORB_TRY(dalloc(P, K * 6, &d.obs_Jp)); LORB_TRY(dalloc(P, K * 12, &d.obs_Jc));
   LORB_TRY(dalloc(P, K * 2, &d.cam_r));
   LORB_TRY(dalloc(P, (size_t)P->Ctot, &d.rot_lin));
   LORB_TRY(dalloc(P, (size_t)P->Ctot, &d.rot_cand));
   LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
-  LORB_TRY(dalloc(P, (size_t)P->env_total, &d.env)); LORB_TRY(dalloc(P, (size_t)P->n_total, &d.rhs));
   if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, ctx->stream));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
   LORB_TRY(dalloc(P, (size_t)nw * 8, &d.dbg));
@@ -1638,7 +1752,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
 constexpr int kLdsBudget = 160 * 1024 - 2048;
 
 // one LM iteration (K1..K8) on the ctx stream
-void enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
+int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = P->ctx->stream;
   const BaDev& d = P->dev;
   if (P->n_pblk) {
@@ -1646,7 +1760,15 @@ void enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
     hipLaunchKernelGGL(k_ba_lin, dim3(P->n_pblk), dim3(kGB), 0, s, d);
   }
   if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(256), 0, s, d);
-  hipLaunchKernelGGL(k_ba_lm_begin, dim3(P->W), dim3(64), 0, s, d, o);
+  if (P->comm) {  // exchange 1: camera blocks + cost / |x|^2 (sum), gradient max (max)
+    hipLaunchKernelGGL(k_ba_win_reduce<0>, dim3(P->W), dim3(64), 0, s, d);
+    LORB_TRY(lorb::comm_allreduce(P->comm, d.U_part, d.U, (size_t)P->Ctot * 27 + 2 * P->W, LORB_OP_SUM));
+    LORB_TRY(lorb::comm_allreduce(P->comm, d.wmax_part, d.wmax, (size_t)P->W, LORB_OP_MAX));
+    hipLaunchKernelGGL(k_ba_lm_begin<true>, dim3(P->W), dim3(64), 0, s, d, o);
+  } else {
+    hipLaunchKernelGGL(k_ba_lm_begin<false>, dim3(P->W), dim3(64), 0, s, d, o);
+  }
+  return LORB_OK;
 }
 
 // one LM iteration on the ctx stream
@@ -1654,17 +1776,19 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   lorb_ctx* ctx = P->ctx;
   hipStream_t s = ctx->stream;
   const BaDev& d = P->dev;
-  enqueue_linearize(P, o);
+  LORB_TRY(enqueue_linearize(P, o));
   if (P->n_pblk) hipLaunchKernelGGL(k_ba_point_prep, dim3(P->n_pblk), dim3(kGB), 0, s, d, o);
   // The LDS Cholesky never writes env, and k_ba_schur rewrites every stored entry of every
   // block each iteration, so the band's structural zeros (set at plan creation) persist; the
   // in-place global variant needs them restored.
   const bool chol_in_lds = sizeof(double) * (size_t)P->max_env <= (size_t)kLdsBudget;
-  if (P->env_total && !chol_in_lds) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
+  if (P->env_total && !chol_in_lds && !P->comm) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   if (P->n_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
     hipLaunchKernelGGL(k_ba_schur, dim3(P->n_bp), dim3(256), 0, s, d, o, P->n_bp);
   }
+  if (P->comm)  // exchange 2: reduced camera system, rhs, point-block failure flags
+    LORB_TRY(lorb::comm_allreduce(P->comm, d.env_part, d.env, (size_t)P->env_total + P->n_total + P->W, LORB_OP_SUM));
   static const bool force_old = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'o'; }();
   const bool chol_w = !force_old && P->max_bw <= 48 && sizeof(double) * (size_t)P->max_env_w <= (size_t)kLdsBudget;
   if (P->Ctot && chol_w) {
@@ -1682,13 +1806,19 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
 #undef LORB_CHOL
   }
   if (P->n_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->n_pblk), dim3(kGB), 0, s, d);
-  hipLaunchKernelGGL(k_ba_lm_end, dim3(P->W), dim3(64), 0, s, d, o);
+  if (P->comm) {  // exchange 3: model cost change, candidate cost, point |step|^2
+    hipLaunchKernelGGL(k_ba_win_reduce<1>, dim3(P->W), dim3(64), 0, s, d);
+    LORB_TRY(lorb::comm_allreduce(P->comm, d.wstep_part, d.wstep, 3 * (size_t)P->W, LORB_OP_SUM));
+    hipLaunchKernelGGL(k_ba_lm_end<true>, dim3(P->W), dim3(64), 0, s, d, o);
+  } else {
+    hipLaunchKernelGGL(k_ba_lm_end<false>, dim3(P->W), dim3(64), 0, s, d, o);
+  }
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
 }
 
 int enqueue_finalize(lorb_ba_plan* P, const LMOpt& o) {
-  enqueue_linearize(P, o);
+  LORB_TRY(enqueue_linearize(P, o));
   LORB_CHECK_LAUNCH(P->ctx);
   return LORB_OK;
 }
@@ -1703,7 +1833,9 @@ int plan_solve(lorb_ba_plan* P, const lorb_lm_options* opt) {
   // rotation states of the initial linearisation point (later ones: k_ba_lm_end on acceptance)
   if (P->Ctot) hipLaunchKernelGGL(k_ba_rot_lin, dim3(lorb::ceil_div(P->Ctot, 64)), dim3(64), 0, ctx->stream, P->dev, P->Ctot);
   LORB_CHECK_LAUNCH(ctx);
-  const bool timing = ctx->ktime;  // per-kernel events cannot live inside a graph
+  // per-kernel events cannot live inside a graph, and neither can a host-transport exchange
+  static const bool no_graph = [] { const char* e = getenv("LORB_NO_GRAPH"); return e && e[0] == '1'; }();
+  const bool timing = ctx->ktime || no_graph || (P->comm && !P->comm->rccl);
   if (!timing && (!P->has_graph || memcmp(&P->graph_opt, &o, sizeof(LMOpt)) != 0)) {
     if (P->gexec) { (void)hipGraphExecDestroy(P->gexec); P->gexec = nullptr; }
     if (P->graph) { (void)hipGraphDestroy(P->graph); P->graph = nullptr; }
@@ -1762,6 +1894,20 @@ int lorb_ba_plan_create(lorb_ctx* ctx, int32_t n_windows, const lorb_ba_window* 
   lorb_ba_plan* P = new (std::nothrow) lorb_ba_plan();
   if (!P) return LORB_E_NOMEM;
   int rc = build_plan(ctx, n_windows, windows, P);
+  if (rc != LORB_OK) { delete P; return rc; }
+  *out = P;
+  return LORB_OK;
+}
+
+int lorb_ba_plan_create_sharded(lorb_ctx* ctx, lorb_comm* comm, int32_t n_windows,
+                                const lorb_ba_window* shards, lorb_ba_plan** out) {
+  if (!ctx || !comm || !out || n_windows < 0 || (n_windows > 0 && !shards)) return LORB_E_INVALID;
+  if (comm->ctx != ctx) return lorb::set_error(ctx, LORB_E_INVALID, "communicator belongs to another context");
+  *out = nullptr;
+  lorb_ba_plan* P = new (std::nothrow) lorb_ba_plan();
+  if (!P) return LORB_E_NOMEM;
+  P->comm = comm;
+  int rc = build_plan(ctx, n_windows, shards, P);
   if (rc != LORB_OK) { delete P; return rc; }
   *out = P;
   return LORB_OK;

@@ -31,9 +31,25 @@ struct lorb_ctx {
   size_t pinned_sz = 0;
 };
 
+// multi-GPU communicator (lorb_comm.hip): RCCL over xGMI, or a host callback transport
+struct lorb_comm {
+  lorb_ctx* ctx = nullptr;
+  int nranks = 1, rank = 0;
+  bool rccl = false;
+  void* nccl = nullptr;                    // ncclComm_t
+  lorb_host_allreduce_fn fn = nullptr;     // host transport
+  void* user = nullptr;
+  double* pinned = nullptr;                // host staging for the callback transport
+  size_t pinned_n = 0;
+};
+
 namespace lorb {
 
 int set_error(lorb_ctx* ctx, int code, const char* fmt, ...);
+// stream-ordered all-reduce of device doubles on comm->ctx->stream (send may equal recv)
+int comm_allreduce(lorb_comm* comm, const double* d_send, double* d_recv, size_t n, int op);
+// blocking all-reduce of a host array (plan construction)
+int comm_allreduce_host(lorb_comm* comm, double* h_buf, size_t n, int op);
 
 #define LORB_HIP(ctx, call)                                                              \
   do {                                                                                   \

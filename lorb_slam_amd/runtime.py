@@ -190,17 +190,80 @@ def _ba_local(self, wins, opt=None):
     return poses, pts, [summ[i].as_dict() for i in range(len(wins))]
 
 
-class BAPlan:
-    """Device-resident plan (lorb_ba_plan_*): upload + Schur structure once, solve many times."""
+HOST_ALLREDUCE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_int32)
+OP_SUM, OP_MAX, OP_MIN = 0, 1, 2
 
-    def __init__(self, ctx, wins):
+
+def unique_id():
+    """RCCL unique id (bytes) -- create on rank 0, distribute out of band."""
+    buf = (C.c_uint8 * 128)()
+    rc = lib().lorb_comm_unique_id(buf)
+    if rc != 0:
+        raise LorbError(f"lorb_comm_unique_id failed rc={rc}")
+    return bytes(buf)
+
+
+class Comm:
+    """lorb_comm: the multi-GPU exchange of the sharded local BA (include/lorb_c.h).
+
+    Comm.rccl(ctx, world, rank, uid): ncclAllReduce on the context stream (one process per GPU).
+    Comm.host(ctx, world, rank, fn):  fn(np.ndarray float64 view, op) all-reduces in place over
+    the ranks by any host transport (tests: torch.distributed gloo)."""
+
+    def __init__(self, ctx, handle, keep=None):
+        self.ctx, self._p, self._keep = ctx, handle, keep
+
+    @classmethod
+    def rccl(cls, ctx, world, rank, uid):
+        h = C.c_void_p()
+        idb = (C.c_uint8 * 128).from_buffer_copy(uid)
+        ctx.check(lib().lorb_comm_init_rccl(ctx.handle, C.c_int32(world), C.c_int32(rank), idb, C.byref(h)),
+                  "lorb_comm_init_rccl")
+        return cls(ctx, h)
+
+    @classmethod
+    def host(cls, ctx, world, rank, fn):
+        def cb(_user, buf, n, op):
+            try:
+                fn(np.ctypeslib.as_array(buf, shape=(int(n),)), int(op))
+                return 0
+            except Exception:  # noqa: BLE001 -- reported to the library as a transport failure
+                import traceback
+                traceback.print_exc()
+                return 1
+        cfn = HOST_ALLREDUCE(cb)
+        h = C.c_void_p()
+        ctx.check(lib().lorb_comm_init_host(ctx.handle, C.c_int32(world), C.c_int32(rank), cfn, None, C.byref(h)),
+                  "lorb_comm_init_host")
+        return cls(ctx, h, keep=cfn)
+
+    @property
+    def handle(self):
+        return self._p
+
+    def close(self):
+        if self._p:
+            lib().lorb_comm_destroy(self._p)
+            self._p = C.c_void_p()
+
+
+class BAPlan:
+    """Device-resident plan (lorb_ba_plan_*): upload + Schur structure once, solve many times.
+    With `comm`, `wins` are this rank's shards (lorb_ba_plan_create_sharded)."""
+
+    def __init__(self, ctx, wins, comm=None):
         self.ctx = ctx
         self.wins = wins
+        self.comm = comm
         self._keep = A.KeepAlive()
         arr = A.make_windows(wins, self._keep)
         self._p = C.c_void_p()
-        ctx.check(lib().lorb_ba_plan_create(ctx.handle, C.c_int32(len(wins)), arr, C.byref(self._p)),
-                  "lorb_ba_plan_create")
+        if comm is None:
+            ctx.check(lib().lorb_ba_plan_create(ctx.handle, C.c_int32(len(wins)), arr, C.byref(self._p)),
+                      "lorb_ba_plan_create")
+        else:
+            ctx.check(lib().lorb_ba_plan_create_sharded(ctx.handle, comm.handle, C.c_int32(len(wins)), arr,
+                                                        C.byref(self._p)), "lorb_ba_plan_create_sharded")
 
     def solve(self, opt=None):
         opt = opt or A.LMOptions.default()

@@ -1,0 +1,68 @@
+"""One rank of the point-partitioned local BA for tests/test_gpu_shard.py.
+
+    python tests/shard_rank.py RANK WORLD PORT OUT.npz
+
+Builds the rank's shard of a synthetic window, joins a 2-rank host all-reduce over a local
+socket (commutative ops, so both ranks hold bit-identical reduced values), runs the sharded
+plan on GPU 0 (several ranks share the one GPU of the test box) and saves poses + its points."""
+import os
+import sys
+from multiprocessing.connection import Client, Listener
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from lorb_slam_amd import _abi as A  # noqa: E402
+from lorb_slam_amd import shard, synth  # noqa: E402
+from lorb_slam_amd.runtime import BAPlan, Comm, Context  # noqa: E402
+
+WINDOWS = [dict(seed=3, n_kf=12, n_pts=1500, n_fixed=2, fixed_obs_per_kf=150),
+           dict(seed=7, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400)]
+
+
+def main():
+    rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    assert world == 2
+    if rank == 0:
+        conn = Listener(("127.0.0.1", port), authkey=b"lorb").accept()
+    else:
+        conn = Client(("127.0.0.1", port), authkey=b"lorb")
+
+    def allreduce(buf, op):
+        conn.send_bytes(buf.tobytes())
+        other = np.frombuffer(conn.recv_bytes(), dtype=np.float64)
+        if op == 0:
+            buf += other
+        elif op == 1:
+            np.maximum(buf, other, out=buf)
+        else:
+            np.minimum(buf, other, out=buf)
+
+    wins = [synth.ba_window(**kw) for kw in WINDOWS]
+    shards = [shard.shard_window(w, rank, world) for w in wins]
+    ctx = Context(0)
+    comm = Comm.host(ctx, world, rank, allreduce)
+    res = {}
+    for name, opt in (("default", A.LMOptions.default()),
+                      ("ten", A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0,
+                                                  gradient_tolerance=0.0, parameter_tolerance=0.0))):
+        plan = BAPlan(ctx, shards, comm=comm)
+        plan.solve(opt)
+        P, X, S = plan.read()
+        plan.close()
+        for i in range(len(wins)):
+            res[f"{name}_pose{i}"] = P[i]
+            res[f"{name}_pts{i}"] = X[i]
+            res[f"{name}_range{i}"] = np.array(shards[i]["point_range"])
+            res[f"{name}_iters{i}"] = np.array([S[i]["iterations"], S[i]["successful_steps"]])
+            res[f"{name}_cost{i}"] = np.array([S[i]["final_cost"]])
+    comm.close()
+    ctx.close()
+    np.savez(out, **res)
+    conn.close()
+
+
+if __name__ == "__main__":
+    main()

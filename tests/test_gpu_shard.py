@@ -1,0 +1,77 @@
+"""GPU: point-partitioned local BA through lorb_ba_plan_create_sharded.
+
+* world 1 over RCCL (the communicator, the captured exchanges) == the unsharded plan;
+* world 2, two processes sharing the test box's GPU, host all-reduce transport: poses and each
+  rank's points == the unsharded solve within the north_star tolerance (1e-5 relative; the
+  exchange only reorders sums, so the agreement is ~1e-10 in practice), same iteration counts."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle as O
+from lorb_slam_amd import _abi as A
+from lorb_slam_amd import synth
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-5
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import shard_rank  # noqa: E402
+
+
+def close(a, b, rtol=RTOL):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return np.all(np.abs(a - b) <= rtol * np.maximum(np.abs(b), 1.0))
+
+
+OPTS = {"default": A.LMOptions.default(),
+        "ten": A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                                   parameter_tolerance=0.0)}
+
+
+def test_sharded_rccl_world1_matches_unsharded(ctx):
+    from lorb_slam_amd.runtime import BAPlan, Comm, unique_id
+    wins = [synth.ba_window(**kw) for kw in shard_rank.WINDOWS]
+    comm = Comm.rccl(ctx, 1, 0, unique_id())
+    try:
+        for opt in OPTS.values():
+            ref = BAPlan(ctx, wins); ref.solve(opt); Pr, Xr, Sr = ref.read(); ref.close()
+            pl = BAPlan(ctx, wins, comm=comm); pl.solve(opt); pl.solve(opt); Ps, Xs, Ss = pl.read(); pl.close()
+            for i in range(len(wins)):
+                assert close(Ps[i], Pr[i], 1e-9) and close(Xs[i], Xr[i], 1e-9)
+                assert Ss[i]["iterations"] == Sr[i]["iterations"]
+    finally:
+        comm.close()
+
+
+def test_sharded_two_ranks_host_transport(ctx, tmp_path):
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    outs = [str(tmp_path / f"r{r}.npz") for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "shard_rank.py"), str(r), "2", str(port), outs[r]])
+             for r in range(2)]
+    try:
+        rcs = [p.wait(timeout=100) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert rcs == [0, 0], rcs
+    R = [np.load(o) for o in outs]
+    wins = [synth.ba_window(**kw) for kw in shard_rank.WINDOWS]
+    for name, opt in OPTS.items():
+        Pg, Xg, Sg = ctx.ba_local(wins, opt)
+        Po, Xo, So = O.ba_local(wins, opt)
+        for i in range(len(wins)):
+            # poses are replicated bit-identically on both ranks
+            assert np.array_equal(R[0][f"{name}_pose{i}"], R[1][f"{name}_pose{i}"])
+            assert close(R[0][f"{name}_pose{i}"], Pg[i]) and close(R[0][f"{name}_pose{i}"], Po[i])
+            X = np.zeros_like(Xg[i])
+            for r in range(2):
+                a, b = R[r][f"{name}_range{i}"]
+                X[a:b] = R[r][f"{name}_pts{i}"]
+            assert close(X, Xg[i]) and close(X, Xo[i])
+            assert list(R[0][f"{name}_iters{i}"]) == [Sg[i]["iterations"], Sg[i]["successful_steps"]]
