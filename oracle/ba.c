@@ -225,6 +225,17 @@ static int inv3_spd(const double* A, double* inv) {
   return 1;
 }
 
+/* Point-partitioned solve (the multi-GPU design): every rank holds all poses and
+ * its own points.  R == NULL: single process.  Otherwise every quantity that sums over
+ * residuals is all-reduced through R->fn, exactly where the GPU path exchanges. */
+typedef struct {
+  or_allreduce_fn fn;
+  void* user;
+  int rank;
+} or_reducer;
+static int ar(const or_reducer* R, double* buf, int64_t n, int op) { return R ? R->fn(R->user, buf, n, op) : 0; }
+static double ar1(const or_reducer* R, double v, int op) { if (R) R->fn(R->user, &v, 1, op); return v; }
+
 typedef struct {
   double *r, *Jp, *Jc;           /* current residuals and SCALED jacobians */
   int* pt_res_off; int* pt_res;  /* residuals of each point (CSR) */
@@ -232,7 +243,7 @@ typedef struct {
 
 /* Solve (Js^T Js + D^2) y = Js^T r by Schur elimination of the point blocks
  * (ceres SchurEliminator + DenseSchurComplementSolver).  Returns 0 on failure. */
-static int schur_solve(const or_prob* P, const lin_state* L, const double* D, double* y) {
+static int schur_solve(const or_prob* P, const lin_state* L, const double* D, double* y, const or_reducer* R) {
   const int nc = 6 * P->n_pose;
   double* S = (double*)calloc((size_t)nc * nc + 1, sizeof(double));
   double* rhs = (double*)calloc((size_t)nc + 1, sizeof(double));
@@ -248,7 +259,8 @@ static int schur_solve(const or_prob* P, const lin_state* L, const double* D, do
       for (int b = 0; b < 6; b++) S[(c0 + a) * nc + c0 + b] += J[a] * J[b] + J[6 + a] * J[6 + b];
     }
   }
-  for (int i = 0; i < nc; i++) S[i * nc + i] += D[i] * D[i];
+  if (!R || R->rank == 0)
+    for (int i = 0; i < nc; i++) S[i * nc + i] += D[i] * D[i];
   /* eliminate every point block */
   double* ete_inv = (double*)malloc(sizeof(double) * 9 * (size_t)(P->n_point > 0 ? P->n_point : 1));
   double* etb = (double*)malloc(sizeof(double) * 3 * (size_t)(P->n_point > 0 ? P->n_point : 1));
@@ -264,7 +276,7 @@ static int schur_solve(const or_prob* P, const lin_state* L, const double* D, do
     }
     const double* Dp = D + nc + 3 * p;
     for (int a = 0; a < 3; a++) ete[4 * a] += Dp[a] * Dp[a];
-    if (!inv3_spd(ete, ete_inv + 9 * p)) { ok = 0; break; }
+    if (!inv3_spd(ete, ete_inv + 9 * p)) { ok = 0; if (!R) break; continue; }
     memcpy(etb + 3 * p, b, sizeof(b));
     const double* Ei = ete_inv + 9 * p;
     /* W_a = Jc_a^T Jp_a (6x3); Y_a = W_a Ei */
@@ -292,6 +304,11 @@ static int schur_solve(const or_prob* P, const lin_state* L, const double* D, do
       }
     }
   }
+  if (R) {  /* exchange 2: S, rhs and the point-block failure flag */
+    ok = ar1(R, ok ? 0.0 : 1.0, LORB_OP_MAX) == 0.0;
+    ar(R, S, (int64_t)nc * nc, LORB_OP_SUM);
+    ar(R, rhs, nc, LORB_OP_SUM);
+  }
   if (ok && nc > 0) {
     ok = chol(S, nc);
     if (ok) chol_solve(S, nc, rhs);
@@ -317,13 +334,15 @@ static int schur_solve(const or_prob* P, const lin_state* L, const double* D, do
     }
     const int np = nc + 3 * P->n_point;
     for (int i = 0; i < np; i++) if (!isfinite(y[i])) { ok = 0; break; }
+    if (R) ok = ar1(R, ok ? 0.0 : 1.0, LORB_OP_MAX) == 0.0;
   }
   free(S); free(rhs); free(ete_inv); free(etb);
   return ok;
 }
 
 /* The Ceres TrustRegionMinimizer + LevenbergMarquardtStrategy loop (Appendix B). */
-static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_ba_summary* sum) {
+static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_ba_summary* sum,
+                    const or_reducer* R) {
   const int nc = 6 * P->n_pose;
   const int np = nc + 3 * P->n_point;
   const int nr = P->n_res;
@@ -344,6 +363,13 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
   for (int k = 0; k < nr; k++) {
     if (P->res[k].pose >= 0) memset(active + 6 * P->res[k].pose, 1, 6);
     if (P->res[k].point >= 0) memset(active + nc + 3 * P->res[k].point, 1, 3);
+  }
+  if (R && nc > 0) {  /* a pose is active if any rank observes it */
+    double* a = (double*)malloc(sizeof(double) * (size_t)nc);
+    for (int i = 0; i < nc; i++) a[i] = active[i];
+    ar(R, a, nc, LORB_OP_MAX);
+    for (int i = 0; i < nc; i++) active[i] = a[i] > 0.0;
+    free(a);
   }
   double* scale = (double*)malloc(sizeof(double) * (size_t)(np + 1));
   double* diag = (double*)malloc(sizeof(double) * (size_t)(np + 1));
@@ -374,12 +400,24 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
     }                                                                                     \
   } while (0)
 
+  /* exchange 1 (per linearisation): cost, pose column norms and gradient (sum), gradient max */
+#define LIN_EXCHANGE()                                                                    \
+  do {                                                                                    \
+    if (R) { cost = ar1(R, cost, LORB_OP_SUM); ar(R, diag, nc, LORB_OP_SUM); ar(R, g, nc, LORB_OP_SUM); } \
+  } while (0)
+#define GMAX()                                                                            \
+  do {                                                                                    \
+    gmax = 0.0;                                                                           \
+    for (int i = 0; i < np; i++) if (active[i]) { const double d = fabs(x[i] - (x[i] + -g[i])); if (d > gmax) gmax = d; } \
+    gmax = ar1(R, gmax, LORB_OP_MAX);                                                     \
+  } while (0)
   double cost = eval_jac(P, x, L.r, L.Jp, L.Jc);
-  sum->initial_cost = cost;
   COLS_AND_GRAD(diag, g);
+  LIN_EXCHANGE();
+  sum->initial_cost = cost;
   for (int i = 0; i < np; i++) scale[i] = o->jacobi_scaling ? 1.0 / (1.0 + sqrt(diag[i])) : 1.0;
   double gmax = 0.0;
-  for (int i = 0; i < np; i++) if (active[i]) { const double d = fabs(x[i] - (x[i] + -g[i])); if (d > gmax) gmax = d; }
+  GMAX();
 #define SCALE_J()                                                                         \
   do {                                                                                    \
     for (int k = 0; k < nr; k++) {                                                        \
@@ -391,9 +429,16 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
     }                                                                                     \
   } while (0)
   SCALE_J();
+  /* |x|: poses are replicated, points are rank-local */
+#define XNORM()                                                                           \
+  do {                                                                                    \
+    double xp = 0.0, xq = 0.0;                                                            \
+    for (int i = 0; i < nc; i++) if (active[i]) xp += x[i] * x[i];                        \
+    for (int i = nc; i < np; i++) if (active[i]) xq += x[i] * x[i];                       \
+    x_norm = sqrt(xp + ar1(R, xq, LORB_OP_SUM));                                          \
+  } while (0)
   double x_norm = 0.0;
-  for (int i = 0; i < np; i++) if (active[i]) x_norm += x[i] * x[i];
-  x_norm = sqrt(x_norm);
+  XNORM();
 
   double radius = o->initial_trust_region_radius, decrease_factor = 2.0;
   int reuse_diagonal = 0, n_invalid = 0, iter = 0, n_success = 0;
@@ -415,10 +460,11 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
         if (q->pose >= 0) for (int j = 0; j < 6; j++) { const double a = L.Jc[12 * k + j], b = L.Jc[12 * k + 6 + j]; colsq[6 * q->pose + j] += a * a + b * b; }
         if (q->point >= 0) for (int j = 0; j < 3; j++) { const double a = L.Jp[6 * k + j], b = L.Jp[6 * k + 3 + j]; colsq[nc + 3 * q->point + j] += a * a + b * b; }
       }
+      ar(R, diag, nc, LORB_OP_SUM);
       for (int i = 0; i < np; i++) diag[i] = fmin(fmax(diag[i], o->min_lm_diagonal), o->max_lm_diagonal);
     }
     for (int i = 0; i < np; i++) D[i] = sqrt(diag[i] / radius);
-    int solved = schur_solve(P, &L, D, y);
+    int solved = schur_solve(P, &L, D, y, R);
     reuse_diagonal = 1;
     double model_cost_change = 0.0;
     int valid = 0;
@@ -432,7 +478,7 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
         if (q->pose >= 0) for (int j = 0; j < 6; j++) { const double s = y[6 * q->pose + j]; m0 += L.Jc[12 * k + j] * s; m1 += L.Jc[12 * k + 6 + j] * s; }
         mcc += m0 * (L.r[2 * k] + m0 / 2.0) + m1 * (L.r[2 * k + 1] + m1 / 2.0);
       }
-      model_cost_change = -mcc;
+      model_cost_change = -ar1(R, mcc, LORB_OP_SUM);  /* exchange 3 */
       valid = model_cost_change > 0.0;
     }
     if (!valid) {
@@ -446,10 +492,11 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
     }
     n_invalid = 0;
     for (int i = 0; i < np; i++) xn[i] = x[i] + y[i] * scale[i];
-    const double new_cost = eval_cost(P, xn);
-    double step_norm = 0.0;
-    for (int i = 0; i < np; i++) if (active[i]) { const double d = x[i] - xn[i]; step_norm += d * d; }
-    step_norm = sqrt(step_norm);
+    const double new_cost = ar1(R, eval_cost(P, xn), LORB_OP_SUM);
+    double sp = 0.0, sq = 0.0;
+    for (int i = 0; i < nc; i++) if (active[i]) { const double d = x[i] - xn[i]; sp += d * d; }
+    for (int i = nc; i < np; i++) if (active[i]) { const double d = x[i] - xn[i]; sq += d * d; }
+    const double step_norm = sqrt(sp + ar1(R, sq, LORB_OP_SUM));
     if (step_norm <= o->parameter_tolerance * (x_norm + o->parameter_tolerance)) { term = LORB_TERM_PARAMETER_TOL; break; }
     const double cost_change = cost - new_cost;
     if (fabs(cost_change) <= o->function_tolerance * cost) { term = LORB_TERM_FUNCTION_TOL; break; }
@@ -457,13 +504,11 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
     if (relative_decrease > o->min_relative_decrease) {
       /* HandleSuccessfulStep */
       memcpy(x, xn, sizeof(double) * (size_t)np);
-      x_norm = 0.0;
-      for (int i = 0; i < np; i++) if (active[i]) x_norm += x[i] * x[i];
-      x_norm = sqrt(x_norm);
+      XNORM();
       cost = eval_jac(P, x, L.r, L.Jp, L.Jc);
       COLS_AND_GRAD(D, g);   /* D used as scratch for the (unused) unscaled column norms */
-      gmax = 0.0;
-      for (int i = 0; i < np; i++) if (active[i]) { const double d = fabs(x[i] - (x[i] + -g[i])); if (d > gmax) gmax = d; }
+      if (R) { cost = ar1(R, cost, LORB_OP_SUM); ar(R, g, nc, LORB_OP_SUM); }
+      GMAX();
       SCALE_J();
       n_success++;
       last_successful = 1;
@@ -489,6 +534,9 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
   return LORB_OK;
 #undef COLS_AND_GRAD
 #undef SCALE_J
+#undef LIN_EXCHANGE
+#undef GMAX
+#undef XNORM
 }
 
 /* (a12) BA::ProjectPoseOptimization, src/bundle_adjust.cpp:158-202 */
@@ -511,7 +559,7 @@ int or_ba_pose_only(const lorb_pose_problem_batch* prob, const lorb_lm_options* 
     for (int i = 0; i < 6; i++) x[i] = prob->pose_init[6 * f + i];
     lorb_ba_summary s;
     memset(&s, 0, sizeof(s));
-    if (P.n_res > 0) lm_solve(&P, opt, x, &s);  /* an empty ceres::Problem leaves the pose untouched */
+    if (P.n_res > 0) lm_solve(&P, opt, x, &s, NULL);  /* an empty ceres::Problem leaves the pose untouched */
     for (int i = 0; i < 6; i++) pose_out[6 * f + i] = x[i];
     if (Tcw_out) {
       const float R[3] = {(float)x[0], (float)x[1], (float)x[2]};
@@ -547,7 +595,42 @@ int or_ba_local(int n_windows, const lorb_ba_window* W, const lorb_lm_options* o
     for (int i = 0; i < 3 * P.n_point; i++) x[6 * P.n_pose + i] = win->point_init[i];
     lorb_ba_summary s;
     memset(&s, 0, sizeof(s));
-    if (P.n_res > 0) lm_solve(&P, opt, x, &s);
+    if (P.n_res > 0) lm_solve(&P, opt, x, &s, NULL);
+    memcpy(pose_out[w], x, sizeof(double) * 6 * (size_t)P.n_pose);
+    memcpy(point_out[w], x + 6 * P.n_pose, sizeof(double) * 3 * (size_t)P.n_point);
+    if (summaries) summaries[w] = s;
+    free(x); free(P.res);
+  }
+  return LORB_OK;
+}
+
+/* Point-partitioned variant of or_ba_local: `shards` holds this rank's points and
+ * all of their observations; poses, fixed poses and intrinsics are identical on every rank. */
+int or_ba_local_sharded(int n_windows, const lorb_ba_window* W, const lorb_lm_options* opt, int rank,
+                        or_allreduce_fn fn, void* user, double* const* pose_out, double* const* point_out,
+                        lorb_ba_summary* summaries) {
+  const or_reducer R = {fn, user, rank};
+  for (int w = 0; w < n_windows; w++) {
+    const lorb_ba_window* win = &W[w];
+    or_prob P;
+    P.n_pose = win->n_poses; P.n_point = win->n_points; P.n_res = win->n_obs;
+    P.res = (or_res*)calloc((size_t)(P.n_res > 0 ? P.n_res : 1), sizeof(or_res));
+    for (int k = 0; k < P.n_res; k++) {
+      or_res* q = &P.res[k];
+      q->point = win->obs_point[k];
+      const int f = win->obs_frame[k];
+      if (f >= 0) { q->kind = 2; q->pose = f; }
+      else { q->kind = 1; q->pose = -1; for (int i = 0; i < 6; i++) q->fpose[i] = win->fixed_pose[6 * (size_t)(-1 - f) + i]; }
+      q->fx = win->fx; q->fy = win->fy; q->cx = win->cx; q->cy = win->cy;
+      q->u = win->obs_uv[2 * (size_t)k]; q->v = win->obs_uv[2 * (size_t)k + 1];
+    }
+    const int np = 6 * P.n_pose + 3 * P.n_point;
+    double* x = (double*)malloc(sizeof(double) * (size_t)(np + 1));
+    for (int i = 0; i < 6 * P.n_pose; i++) x[i] = win->pose_init[i];
+    for (int i = 0; i < 3 * P.n_point; i++) x[6 * P.n_pose + i] = win->point_init[i];
+    lorb_ba_summary s;
+    memset(&s, 0, sizeof(s));
+    if (ar1(&R, (double)P.n_res, LORB_OP_SUM) > 0.0) lm_solve(&P, opt, x, &s, &R);
     memcpy(pose_out[w], x, sizeof(double) * 6 * (size_t)P.n_pose);
     memcpy(point_out[w], x + 6 * P.n_pose, sizeof(double) * 3 * (size_t)P.n_point);
     if (summaries) summaries[w] = s;

@@ -83,6 +83,12 @@ int or_ba_pose_only(const lorb_pose_problem_batch* prob, const lorb_lm_options* 
                     double* pose_out, float* Tcw_out, lorb_ba_summary* summaries);
 int or_ba_local(int n_windows, const lorb_ba_window* windows, const lorb_lm_options* opt,
                 double* const* pose_out, double* const* point_out, lorb_ba_summary* summaries);
+/* Point-partitioned local BA (the multi-GPU exchange pattern of SURVEY §8e, restated on the
+ * CPU): each rank passes its shard; fn all-reduces `count` doubles in place (op LORB_OP_*). */
+typedef int (*or_allreduce_fn)(void* user, double* buf, int64_t count, int32_t op);
+int or_ba_local_sharded(int n_windows, const lorb_ba_window* shards, const lorb_lm_options* opt, int rank,
+                        or_allreduce_fn fn, void* user, double* const* pose_out, double* const* point_out,
+                        lorb_ba_summary* summaries);
 /* Residual + Jacobian of one observation by Ceres-style Jets (AutoDiffCostFunction).
  * kind 0 = PoseCost (params aa,t ; v uses fy_eff), 1 = MPCost (params X), 2 = PoseMPCost
  * (params X, pose).  jac: 2 x nparams row-major (nparams 6 / 3 / 9). */

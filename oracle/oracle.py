@@ -191,3 +191,32 @@ def ba_local(wins, opt=None):
     summ = (A.BASummary * max(1, len(wins)))()
     lib().or_ba_local(C.c_int(len(wins)), arr, C.byref(opt), pp, qp, summ)
     return poses, pts, [summ[i].as_dict() for i in range(len(wins))]
+
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_int32)
+
+
+def ba_local_sharded(shards, rank, allreduce, opt=None):
+    """Point-partitioned local BA on this rank's shards; allreduce(np.ndarray view, op) reduces
+    in place over all ranks (op 0 sum, 1 max, 2 min)."""
+    keep = A.KeepAlive()
+    arr = A.make_windows(shards, keep)
+    opt = opt or A.LMOptions.default()
+
+    def cb(_u, buf, n, op):
+        try:
+            allreduce(np.ctypeslib.as_array(buf, shape=(int(n),)), int(op))
+            return 0
+        except Exception:  # noqa: BLE001
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    cfn = ALLREDUCE_FN(cb)
+    poses = [np.zeros((len(w["pose_init"]), 6)) for w in shards]
+    pts = [np.zeros((max(len(w["point_init"]), 1), 3)) for w in shards]
+    pp = (A.f64p * max(1, len(shards)))(*[A.ptr(p, C.c_double) for p in poses])
+    qp = (A.f64p * max(1, len(shards)))(*[A.ptr(p, C.c_double) for p in pts])
+    summ = (A.BASummary * max(1, len(shards)))()
+    lib().or_ba_local_sharded(C.c_int(len(shards)), arr, C.byref(opt), C.c_int(rank), cfn, None, pp, qp, summ)
+    return poses, [p[: len(w["point_init"])] for p, w in zip(pts, shards)], [summ[i].as_dict() for i in range(len(shards))]
