@@ -358,6 +358,16 @@ int lorb_comm_allreduce_f64(lorb_comm* comm, const double* d_send, double* d_rec
 int lorb_ba_plan_create_sharded(lorb_ctx* ctx, lorb_comm* comm, int32_t n_windows,
                                 const lorb_ba_window* shards, lorb_ba_plan** out);
 
+/* (a2/a3) with query rows split over ranks.  This rank holds queries
+ * [q_base[p], q_base[p] + q_off[p+1] - q_off[p]) of problem p (global numbering) and ALL of its
+ * trains.  Outputs as lorb_bf_match_dev for the local queries (global train indices);
+ * n_matches[p] is the count over all ranks.  q_off / t_off / q_base are HOST arrays. */
+int lorb_bf_match_sharded_dev(lorb_ctx* ctx, lorb_comm* comm, int32_t n_problems,
+                              const uint8_t* d_q_desc, const int32_t* q_off, const int32_t* q_base,
+                              const uint8_t* d_t_desc, const int32_t* t_off,
+                              int32_t* d_cc_train, int32_t* d_cc_dist, int32_t* d_match_train,
+                              int32_t* d_n_matches);
+
 /* Rodrigues vector -> Tcw (float), cv::Rodrigues semantics (double internally). */
 void lorb_pose_to_Tcw(const float rvec[3], const float tvec[3], float Tcw[16]);
 

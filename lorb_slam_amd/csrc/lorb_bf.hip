@@ -187,34 +187,50 @@ __global__ __launch_bounds__(256) void k_top2_finalize(
 }
 
 // cross-check resolution: per train, offer (dist, train) to its nearest query
+// (sharded rows: keys carry GLOBAL query numbers, q_base[p] = this rank's first query of
+// problem p; only trains whose nearest query is local are offered)
 __global__ __launch_bounds__(256) void k_cc_scatter(const uint32_t* __restrict__ tkey, int nt,
                                                     const int32_t* __restrict__ q_off,
                                                     const int32_t* __restrict__ t_off, int np,
+                                                    const int32_t* __restrict__ q_base,
                                                     unsigned long long* __restrict__ qkey) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nt) return;
   const int p = find_problem(t_off, np, t);
-  if (q_off[p + 1] == q_off[p]) return;
   const uint32_t k = tkey[t];
-  const uint32_t q = k & kIdxMask, d = k >> kIdxBits;
+  if (k >= kSentinel) return;  // no query anywhere
+  uint32_t q = k & kIdxMask;
+  const uint32_t d = k >> kIdxBits;
+  if (q_base) {
+    if ((int)q < q_base[p] || (int)q >= q_base[p] + (q_off[p + 1] - q_off[p])) return;
+    q -= (uint32_t)q_base[p];
+  } else if (q_off[p + 1] == q_off[p]) {
+    return;
+  }
   const unsigned long long v = ((unsigned long long)d << 32) | (unsigned)(t - t_off[p]);
   atomicMin(&qkey[q_off[p] + q], v);
 }
 
 // one workgroup per problem: DMatch list + minDist filter (src/matcher.cpp:42-56)
+// MODE 0: whole problem on this device.  Sharded rows: MODE 1 writes the local DMatches and the
+// local minDist (ex[p], as double) for an all-reduce(min); MODE 2 filters with the global
+// minDist and writes the local count (ex[np + p]) for an all-reduce(sum).
+template <int MODE>
 __global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* __restrict__ qkey,
                                                      const int32_t* __restrict__ q_off,
                                                      const int32_t* __restrict__ t_off,
                                                      int32_t* __restrict__ cc_train,
                                                      int32_t* __restrict__ cc_dist,
                                                      int32_t* __restrict__ match_train,
-                                                     int32_t* __restrict__ n_matches) {
+                                                     int32_t* __restrict__ n_matches,
+                                                     double* __restrict__ ex, int np) {
   const int p = blockIdx.x;
   const int q0 = q_off[p], q1 = q_off[p + 1];
   const bool has_t = t_off[p + 1] > t_off[p];
   __shared__ int s_min[256];
   __shared__ int s_cnt[256];
   int mn = 0x7fffffff;
+  if (MODE != 2) {
   for (int q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
     const unsigned long long v = has_t ? qkey[q] : ~0ull;
     if (v != ~0ull) {
@@ -233,7 +249,12 @@ __global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* _
     if (threadIdx.x < s) s_min[threadIdx.x] = min(s_min[threadIdx.x], s_min[threadIdx.x + s]);
     __syncthreads();
   }
-  const int minDist = s_min[0];
+  }
+  if (MODE == 1) {
+    if (threadIdx.x == 0) ex[p] = (double)s_min[0];
+    return;
+  }
+  const int minDist = MODE == 2 ? (int)ex[p] : s_min[0];
   const int thr = max(2 * minDist, 30);  // d > max(2*minDist, 30.0) rejects (exact in integers)
   int cnt = 0;
   for (int q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
@@ -248,12 +269,34 @@ __global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* _
     if (threadIdx.x < s) s_cnt[threadIdx.x] += s_cnt[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) n_matches[p] = s_cnt[0];
+  if (threadIdx.x == 0) {
+    if (MODE == 2) ex[np + p] = (double)s_cnt[0];
+    else n_matches[p] = s_cnt[0];
+  }
+}
+
+// train keys <-> doubles for the all-reduce(min) (keys < 2^32 are exact in double); trains of
+// problems without local queries were not scanned and offer the sentinel
+__global__ void k_u32_f64(const uint32_t* __restrict__ a, double* __restrict__ b, int n, int dir,
+                          uint32_t* __restrict__ c, const int32_t* __restrict__ q_off,
+                          const int32_t* __restrict__ t_off, int np) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (dir == 0) {
+    const int p = find_problem(t_off, np, i);
+    b[i] = q_off[p + 1] > q_off[p] ? (double)a[i] : (double)kSentinel;
+  } else {
+    c[i] = (uint32_t)b[i];
+  }
+}
+__global__ void k_counts_out(const double* __restrict__ ex, int np, int32_t* __restrict__ n_matches) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < np) n_matches[p] = (int32_t)ex[np + p];
 }
 
 // Host: tile table for "lanes = L side, uniform = U side" with a fixed number of U chunks.
 int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_off, int lt,
-                std::vector<BfTile>& tiles, int* n_chunks_out) {
+                std::vector<BfTile>& tiles, int* n_chunks_out, const int32_t* u_base = nullptr) {
   const int64_t nl_total = l_off[np] - l_off[0];
   int64_t max_u = 0, lane_tiles = 0;
   for (int p = 0; p < np; p++) {
@@ -283,7 +326,7 @@ int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_of
         tl.lane_count = std::min(lt, nl - t);
         tl.uni_base = u0 + a;
         tl.uni_count = b - a;
-        tl.uni_local0 = a;
+        tl.uni_local0 = a + (u_base ? u_base[p] : 0);
         tl.out_base = (int)((int64_t)c * nl_total + l0 + t);
         tiles.push_back(tl);
       }
@@ -296,11 +339,11 @@ int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_of
 // scan + merge; final keys land in k1/k2 (n_lanes entries)
 template <bool TOP2>
 int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, const uint8_t* d_uni,
-         const int32_t* u_off, uint32_t** k1_final, uint32_t** k2_final) {
+         const int32_t* u_off, uint32_t** k1_final, uint32_t** k2_final, const int32_t* u_base = nullptr) {
   std::vector<BfTile> tiles;
   int n_chunks = 1;
   static const int qpl = [] { const char* e = getenv("LORB_BF_QPL"); return (e && atoi(e) == 1) ? 1 : 2; }();
-  LORB_TRY(build_tiles(ctx, np, l_off, u_off, 256 * qpl, tiles, &n_chunks));
+  LORB_TRY(build_tiles(ctx, np, l_off, u_off, 256 * qpl, tiles, &n_chunks, u_base));
   const int nl = l_off[np] - l_off[0];
   BfTile* d_tiles = nullptr;
   uint32_t *k1 = nullptr, *k2 = nullptr, *m1 = nullptr, *m2 = nullptr;
@@ -409,11 +452,66 @@ int lorb_bf_match_dev(lorb_ctx* ctx, int32_t np, const uint8_t* d_q, const int32
     // reverse pass: lanes = trains, uniform = queries  -> nearest query per train
     LORB_TRY(scan<false>(ctx, np, d_t, t_off, d_q, q_off, &k1, &k2));
     hipLaunchKernelGGL(k_cc_scatter, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, k1,
-                       nt, d_off, d_off + np + 1, np, qkey);
+                       nt, d_off, d_off + np + 1, np, (const int32_t*)nullptr, qkey);
     LORB_CHECK_LAUNCH(ctx);
   }
-  hipLaunchKernelGGL(k_cc_finalize, dim3(np), dim3(256), 0, ctx->stream, qkey, d_off,
-                     d_off + np + 1, d_cc_train, d_cc_dist, d_match_train, d_n_matches);
+  hipLaunchKernelGGL(k_cc_finalize<0>, dim3(np), dim3(256), 0, ctx->stream, qkey, d_off,
+                     d_off + np + 1, d_cc_train, d_cc_dist, d_match_train, d_n_matches, (double*)nullptr, np);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
+// Query rows sharded over ranks: reverse pass over the LOCAL queries with global
+// query numbers in the keys, all-reduce(min) of the per-train keys, local resolution, then the
+// global minDist (min) and match count (sum).  Three exchanges of Nt + 2 np doubles in total.
+int lorb_bf_match_sharded_dev(lorb_ctx* ctx, lorb_comm* comm, int32_t np, const uint8_t* d_q,
+                              const int32_t* q_off, const int32_t* q_base, const uint8_t* d_t,
+                              const int32_t* t_off, int32_t* d_cc_train, int32_t* d_cc_dist,
+                              int32_t* d_match_train, int32_t* d_n_matches) {
+  LORB_TRY(check_offsets(ctx, np, q_off, t_off));
+  if (!comm || !q_base || comm->ctx != ctx) return lorb::set_error(ctx, LORB_E_INVALID, "bad communicator / q_base");
+  for (int p = 0; p < np; ++p)
+    if (q_base[p] < 0 || (int64_t)q_base[p] + (q_off[p + 1] - q_off[p]) > (int64_t)kIdxMask)
+      return lorb::set_error(ctx, LORB_E_INVALID, "problem %d: global query index out of range", p);
+  if (np == 0) return LORB_OK;
+  const int nq = q_off[np], nt = t_off[np];
+  uint32_t *k1 = nullptr, *k2 = nullptr, *kt = nullptr;
+  unsigned long long* qkey = nullptr;
+  int32_t* d_off = nullptr;
+  double *kd = nullptr, *ex = nullptr;
+  std::vector<int32_t> offs(q_off, q_off + np + 1);
+  offs.insert(offs.end(), t_off, t_off + np + 1);
+  offs.insert(offs.end(), q_base, q_base + np);
+  LORB_TRY(lorb::upload_t(ctx, S_BF_OFF, offs.data(), offs.size(), &d_off));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_QKEY, (size_t)std::max(nq, 1), &qkey));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT2, (size_t)std::max(nt, 1), &kd));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT3, (size_t)std::max(nt, 1), &kt));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT1, (size_t)2 * np, &ex));
+  if (nq > 0) LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, ctx->stream));
+  if (nt > 0) {
+    if (nq > 0) {
+      LORB_TRY(scan<false>(ctx, np, d_t, t_off, d_q, q_off, &k1, &k2, q_base));
+      hipLaunchKernelGGL(k_u32_f64, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, k1, kd, nt, 0,
+                         (uint32_t*)nullptr, (const int32_t*)d_off, (const int32_t*)(d_off + np + 1), np);
+    } else {
+      std::vector<double> sent(nt, (double)kSentinel);
+      LORB_HIP(ctx, hipMemcpyAsync(kd, sent.data(), sizeof(double) * nt, hipMemcpyHostToDevice, ctx->stream));
+      LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    LORB_TRY(lorb::comm_allreduce(comm, kd, kd, (size_t)nt, LORB_OP_MIN));
+    hipLaunchKernelGGL(k_u32_f64, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, (const uint32_t*)nullptr, kd, nt, 1,
+                       kt, (const int32_t*)d_off, (const int32_t*)(d_off + np + 1), np);
+    hipLaunchKernelGGL(k_cc_scatter, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, kt, nt, d_off,
+                       d_off + np + 1, np, (const int32_t*)(d_off + 2 * np + 2), qkey);
+    LORB_CHECK_LAUNCH(ctx);
+  }
+  hipLaunchKernelGGL(k_cc_finalize<1>, dim3(np), dim3(256), 0, ctx->stream, qkey, d_off, d_off + np + 1, d_cc_train,
+                     d_cc_dist, d_match_train, d_n_matches, ex, np);
+  LORB_TRY(lorb::comm_allreduce(comm, ex, ex, (size_t)np, LORB_OP_MIN));
+  hipLaunchKernelGGL(k_cc_finalize<2>, dim3(np), dim3(256), 0, ctx->stream, qkey, d_off, d_off + np + 1, d_cc_train,
+                     d_cc_dist, d_match_train, d_n_matches, ex, np);
+  LORB_TRY(lorb::comm_allreduce(comm, ex + np, ex + np, (size_t)np, LORB_OP_SUM));
+  hipLaunchKernelGGL(k_counts_out, dim3(lorb::ceil_div(np, 256)), dim3(256), 0, ctx->stream, ex, np, d_n_matches);
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
 }

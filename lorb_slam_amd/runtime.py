@@ -140,6 +140,32 @@ class Context:
         return dict(cc_train=cc_t[:nq], cc_dist=cc_d[:nq], match_train=mt[:nq], n_matches=nm[: len(q_list)]), q_off
 
 
+def _bf_match_sharded(self, comm, q_list, q_base, t_list):
+    """lorb_bf_match_sharded_dev: this rank's query rows of every problem (q_list[p] starts at
+    global query q_base[p]) against all trains; returns local outputs + global match counts."""
+    q = np.ascontiguousarray(np.concatenate(q_list) if len(q_list) else np.zeros((0, 32), np.uint8), np.uint8)
+    t = np.ascontiguousarray(np.concatenate(t_list) if len(t_list) else np.zeros((0, 32), np.uint8), np.uint8)
+    q_off = np.concatenate([[0], np.cumsum([len(a) for a in q_list])]).astype(np.int32)
+    t_off = np.concatenate([[0], np.cumsum([len(a) for a in t_list])]).astype(np.int32)
+    qb = np.ascontiguousarray(q_base, np.int32)
+    nq, npb = len(q), len(q_list)
+    dq, dt = self.to_device(q if nq else np.zeros((1, 32), np.uint8)), self.to_device(t if len(t) else np.zeros((1, 32), np.uint8))
+    outs = [self.empty(max(nq, 1), np.int32) for _ in range(3)]
+    nm = self.empty(max(npb, 1), np.int32)
+    self.check(lib().lorb_bf_match_sharded_dev(
+        self._p, comm.handle, C.c_int32(npb), dq.as_ptr(C.c_uint8), A.ptr(q_off, C.c_int32), A.ptr(qb, C.c_int32),
+        dt.as_ptr(C.c_uint8), A.ptr(t_off, C.c_int32), *[o.as_ptr(C.c_int32) for o in outs], nm.as_ptr(C.c_int32)),
+        "lorb_bf_match_sharded_dev")
+    res = dict(cc_train=outs[0].numpy()[:nq], cc_dist=outs[1].numpy()[:nq], match_train=outs[2].numpy()[:nq],
+               n_matches=nm.numpy()[:npb])
+    for a in (dq, dt, nm, *outs):
+        a.free()
+    return res
+
+
+Context.bf_match_sharded = _bf_match_sharded
+
+
 class DeviceArray:
     def __init__(self, ctx, ptr_, shape, dtype):
         self.ctx, self.ptr, self.shape, self.dtype = ctx, ptr_, tuple(shape), np.dtype(dtype)

@@ -22,13 +22,36 @@ WINDOWS = [dict(seed=3, n_kf=12, n_pts=1500, n_fixed=2, fixed_obs_per_kf=150),
            dict(seed=7, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400)]
 
 
+def match_problems():
+    """brute-force crossCheck problems: one with a planted majority, one ragged, one with no trains,
+    one whose queries all fall on a single rank"""
+    out = []
+    for seed, nq, nt in ((21, 1500, 2000), (22, 333, 517), (23, 40, 0), (24, 1, 300)):
+        q, t, _ = synth.bf_problem(seed=seed, nq=nq, nt=max(nt, 1), n_planted=min(nq, nt) // 2)
+        out.append((q, t[:nt]))
+    return out
+
+
+def row_range(n, rank, world):
+    return n * rank // world, n * (rank + 1) // world
+
+
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
     assert world == 2
     if rank == 0:
         conn = Listener(("127.0.0.1", port), authkey=b"lorb").accept()
     else:
-        conn = Client(("127.0.0.1", port), authkey=b"lorb")
+        import time
+        t0 = time.time()
+        while True:  # rank 0 may not be listening yet
+            try:
+                conn = Client(("127.0.0.1", port), authkey=b"lorb")
+                break
+            except ConnectionRefusedError:
+                if time.time() - t0 > 60:
+                    raise
+                time.sleep(0.1)
 
     def allreduce(buf, op):
         conn.send_bytes(buf.tobytes())
@@ -40,11 +63,20 @@ def main():
         else:
             np.minimum(buf, other, out=buf)
 
-    wins = [synth.ba_window(**kw) for kw in WINDOWS]
-    shards = [shard.shard_window(w, rank, world) for w in wins]
     ctx = Context(0)
     comm = Comm.host(ctx, world, rank, allreduce)
     res = {}
+    # matcher: query rows split over the ranks, trains replicated
+    probs = match_problems()
+    ql, qb, tl = [], [], []
+    for q, t in probs:
+        a, b = row_range(len(q), rank, world)
+        ql.append(q[a:b]); qb.append(a); tl.append(t)
+    m = ctx.bf_match_sharded(comm, ql, qb, tl)
+    for k, v in m.items():
+        res[f"match_{k}"] = v
+    wins = [synth.ba_window(**kw) for kw in WINDOWS]
+    shards = [shard.shard_window(w, rank, world) for w in wins]
     for name, opt in (("default", A.LMOptions.default()),
                       ("ten", A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0,
                                                   gradient_tolerance=0.0, parameter_tolerance=0.0))):

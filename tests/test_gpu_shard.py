@@ -61,6 +61,23 @@ def test_sharded_two_ranks_host_transport(ctx, tmp_path):
                 p.kill()
     assert rcs == [0, 0], rcs
     R = [np.load(o) for o in outs]
+    # matcher rows: bit-exact vs the unsharded kernel (and the oracle)
+    probs = shard_rank.match_problems()
+    ref, _ = ctx.bf_match([q for q, _ in probs], [t for _, t in probs])
+    def gather(k):  # rank r holds rows row_range(nq_p, r, 2) of every problem p, problems concatenated
+        parts, off = [[], []], [0, 0]
+        for q, _ in probs:
+            for r in range(2):
+                a, b = shard_rank.row_range(len(q), r, 2)
+                parts[r].append(R[r][f"match_{k}"][off[r]:off[r] + b - a]); off[r] += b - a
+        return np.concatenate([np.concatenate([parts[0][p], parts[1][p]]) for p in range(len(probs))])
+    for k in ("cc_train", "match_train"):
+        assert np.array_equal(gather(k), ref[k]), k
+    has = ref["cc_train"] >= 0
+    assert np.array_equal(gather("cc_dist")[has], ref["cc_dist"][has])
+    assert np.array_equal(R[0]["match_n_matches"], ref["n_matches"]) and np.array_equal(R[1]["match_n_matches"], ref["n_matches"])
+    for (q, t), n in zip(probs, ref["n_matches"]):
+        assert O.bf_match(q, t)["n_matches"] == n
     wins = [synth.ba_window(**kw) for kw in shard_rank.WINDOWS]
     for name, opt in OPTS.items():
         Pg, Xg, Sg = ctx.ba_local(wins, opt)
