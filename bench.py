@@ -41,7 +41,10 @@ INT32_VALU_PEAK = 256 * 4 * 32 * CLOCK      # lane-ops/s: 256 CU x 4 SIMD32 (MI3
 FP64_PEAK = 78.6e12                          # FP64 vector/matrix dense, MI355X spec
 HBM_PEAK = 8.0e12                            # HBM3E spec (MI355X_MICROARCH)
 OPS_PER_PAIR = 16                            # 8 x v_xor_b32 + 8 x v_bcnt_u32_b32 per 256-bit pair
-K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_schur", 3: "k_ba_lin_obs", 4: "k_ba_chol"}
+K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_w"}
+# rocprofv3 short names (tools/pmc_traffic.py) of the same kernels, for the PMC traffic lookup
+K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_w"}
+TRAFFIC = os.path.join(ROOT, "profiles", "r01", "traffic.json")
 METRIC = "ORB matches/sec + local-BA iterations/sec (50 KF, 10k pts) at 1/2/4/8 MI355X"
 
 
@@ -68,6 +71,14 @@ class Dist:
         t = torch.tensor([float(v)], dtype=torch.float64)
         self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op))
         return float(t.item())
+
+    def broadcast_bytes(self, b):
+        """rank 0's bytes to every rank (the RCCL unique id), over gloo"""
+        if not self.dist:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
 
     def close(self):
         if self.dist:
@@ -185,6 +196,75 @@ def cpu_baseline_c4(st, budget_s=12.0):
                       f"(Ceres default num_threads=1), {dt:.1f}s"}
 
 
+def workload_shared(ctx, args, rank, D):
+    """BASELINE C5 shared-window variant: ONE 50-KF window with 80,000 points
+    (~600,000 observations) point-partitioned over the N ranks, 10 LM iterations per step with
+    the three RCCL all-reduces per iteration; plus the new keyframe's 2,000 descriptors matched
+    (crossCheck) against the window's 80,000 map-point descriptors with the query rows split over
+    the ranks.  Strong scaling: total work is fixed as N grows."""
+    from lorb_slam_amd import shard
+    from lorb_slam_amd.runtime import Comm, unique_id
+    world = D.world
+    win = synth.ba_window(seed=11, n_kf=50, n_pts=args.shared_points, n_fixed=5, fixed_obs_per_kf=400)
+    sh = shard.shard_window(win, rank, world)
+    uid = unique_id() if rank == 0 else None
+    uid = D.broadcast_bytes(uid)
+    comm = Comm.rccl(ctx, world, rank, uid)
+    t0 = time.perf_counter()
+    plan = BAPlan(ctx, [sh], comm=comm)
+    plan_ms = (time.perf_counter() - t0) * 1e3
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    rng = np.random.default_rng(12)
+    nq, nt = 2000, args.shared_points
+    mp_desc = synth.random_desc(rng, nt)
+    kf_desc = synth.random_desc(rng, nq)
+    a, b = nq * rank // world, nq * (rank + 1) // world
+    dq, dt = ctx.to_device(kf_desc[a:b] if b > a else kf_desc[:1]), ctx.to_device(mp_desc)
+    q_off = np.array([0, b - a], np.int32)
+    q_base = np.array([a], np.int32)
+    t_off = np.array([0, nt], np.int32)
+    outs = [ctx.empty(max(b - a, 1), np.int32) for _ in range(3)]
+    nm = ctx.empty(1, np.int32)
+    L = lib()
+
+    def step():
+        ctx.check(L.lorb_bf_match_sharded_dev(ctx.handle, comm.handle, C.c_int32(1), dq.as_ptr(C.c_uint8),
+                                              A.ptr(q_off, C.c_int32), A.ptr(q_base, C.c_int32), dt.as_ptr(C.c_uint8),
+                                              A.ptr(t_off, C.c_int32), *[o.as_ptr(C.c_int32) for o in outs],
+                                              nm.as_ptr(C.c_int32)), "lorb_bf_match_sharded_dev")
+        plan.solve(opt)
+
+    def check():
+        _, _, summ = plan.read()
+        return {"n_matches": int(nm.numpy()[0]), "ba_final_cost": summ[0]["final_cost"],
+                "ba_iterations": summ[0]["iterations"]}
+
+    def cleanup():
+        plan.close()
+        comm.close()
+
+    n_obs = len(win["obs_point"])
+    kp = np.bincount(sh["obs_point"][sh["obs_frame"] >= 0])
+    pt_flops = float(np.sum(60 + 108 * kp + 108 * kp * (kp + 1)))
+    pair_cnt = float(np.sum(kp * (kp + 1) // 2))
+    opt_obs = int((sh["obs_frame"] >= 0).sum())
+    bw = 6 * 8 - 1
+    kspec = {
+        2: ("hbm", opt_obs * 36 * 8.0 + (6 * 50) * (bw + 1) * 8.0, "GB/s"),
+        3: ("hbm", len(sh["obs_point"]) * (20 * 8.0 + 16 + 8), "GB/s"),
+        4: ("fp64", (6 * 50) * bw * bw + 4.0 * (6 * 50) * bw, "TFLOP/s"),
+    }
+    del pair_cnt, pt_flops
+    # whole-job units: the shared window's iterations / matches are counted once (rank 0 only)
+    return dict(step=step, check=check, ba_iters=10.0 if rank == 0 else 0.0, matches=float(nq) if rank == 0 else 0.0,
+                pairs=float(b - a) * nt, it_flops=0.0, plan_ms=plan_ms, cleanup=cleanup, kspec=kspec,
+                config={"workload": "c5_shared_window", "kf": 50, "fixed_kf": 5, "points": len(win["point_init"]),
+                        "observations": n_obs, "lm_iterations": 10, "new_kf_keypoints": nq,
+                        "match": f"{nq}x{nt} bf crossCheck, query rows sharded", "points_this_rank": len(sh["point_init"])},
+                cpu=None, scaling="strong")
+
+
 def workload_c2(ctx, args, rank):
     """BASELINE config 1: brute-force Hamming 2000x2000 random 256-bit + ratio test, batched
     over `pairs` independent frame pairs per GPU."""
@@ -228,9 +308,8 @@ def pmc_traffic(kernel):
     WRITE_SIZE collected in separate runs, gfx950 FETCH_SIZE x2 correction; tools/pmc_traffic.py).
     PMC counters cannot be read live from inside the timed process, so this is the profiled
     value of the same command; null when no summary is committed."""
-    path = os.path.join(ROOT, "profiles", "r01_traffic.json")
     try:
-        with open(path) as f:
+        with open(TRAFFIC) as f:
             tab = json.load(f)
     except (OSError, ValueError):
         return None
@@ -258,7 +337,7 @@ def roofline_entry(kt, wl, steps):
     scale = 1e9 if unit == "GB/s" else 1e12
     name = K_NAMES.get(k, str(k))
     return {"bound": bound, "achieved": achieved / scale, "peak": peak / scale, "unit": unit,
-            "frac": achieved / peak, "traffic": pmc_traffic(name), "kernel": name,
+            "frac": achieved / peak, "traffic": pmc_traffic(K_PROF.get(k, name)), "kernel": name,
             "algorithmic_per_launch": amount, "avg_kernel_us": avg_s * 1e6, "launches_per_step": per_step,
             "all_kernels_ms_per_step": {K_NAMES.get(kk, str(kk)): v[0] / steps for kk, v in kt.items()}}
 
@@ -268,7 +347,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c2"])
+    ap.add_argument("--workload", default="c4", choices=["c4", "c2", "shared"])
+    ap.add_argument("--shared-points", type=int, default=80000)
     ap.add_argument("--windows", type=int, default=1)
     ap.add_argument("--pairs", type=int, default=256)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -276,7 +356,10 @@ def main():
 
     D = Dist()
     ctx = Context(D.local_rank)
-    wl = (workload_c4 if args.workload == "c4" else workload_c2)(ctx, args, D.rank)
+    if args.workload == "shared":
+        wl = workload_shared(ctx, args, D.rank, D)
+    else:
+        wl = (workload_c4 if args.workload == "c4" else workload_c2)(ctx, args, D.rank)
     for _ in range(args.warmup):
         wl["step"]()
     ctx.sync()
@@ -302,9 +385,9 @@ def main():
     L.lorb_kernel_timing_enable(ctx.handle, 0)
     total_iters = D.reduce(wl["ba_iters"] * args.steps, "SUM")
     total_matches = D.reduce(wl["matches"] * args.steps, "SUM")
-    cpu = wl["cpu"]() if (D.rank == 0 and not args.no_cpu_baseline and D.world == 1) else None
+    cpu = wl["cpu"]() if (D.rank == 0 and not args.no_cpu_baseline and D.world == 1 and wl["cpu"]) else None
     if D.rank == 0:
-        if args.workload == "c4":
+        if args.workload in ("c4", "shared"):
             value, unit = total_iters / elapsed, "BA iterations/s"
         else:
             value, unit = total_matches / elapsed, "matches/s"
@@ -312,8 +395,9 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": unit, "n_gpus": D.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64+u8", "data": "synthetic",
-            "config": dict(wl["config"], parallelism=f"independent windows x{D.world}"),
+            "scaling": wl.get("scaling", "weak"), "vs_baseline": None, "dtype": "f64+u8", "data": "synthetic",
+            "config": dict(wl["config"], parallelism=(f"point-partitioned window over {D.world} ranks (RCCL)"
+                                                      if args.workload == "shared" else f"independent windows x{D.world}")),
             "matches_per_sec": total_matches / elapsed, "plan_build_ms": wl["plan_ms"],
             "roofline": rf, "cpu_baseline": cpu, "check": check,
         }
