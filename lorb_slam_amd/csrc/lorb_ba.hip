@@ -1101,6 +1101,243 @@ __global__ __launch_bounds__(256) void k_ba_chol_w(BaDev d) {
   }
 }
 
+// K6t: two-sided ("twisted") banded Cholesky for band <= 48 and n >= 128.  The chain of
+// dependent panels is the cost of K6w (one wavefront is latency/issue bound), so the matrix is
+// split into T = [0, m), M = [m, m+48) and B = [m+48, n16): T and B do not couple (band <= 48).
+// Wave 0 eliminates T top-down and wave 1 eliminates B bottom-up (the reversed matrix, whose
+// band is the same) concurrently with the K6w panel machinery; their windows end on M holding
+// S_MM - L_MT L_MT^T and S_MM - L_MB L_MB^T, which wave 0 combines (minus S_MM) and factors
+// (3 panels).  Back-substitution: M, then T (wave 0) and B (wave 1) concurrently.  L of both
+// sides lives in the band storage of S in LDS (wave 1 writes L'(i', j') into the slot of the
+// original lower entry it equals); the only LDS data both sides read is S_MM, which neither
+// overwrites.  Rows n .. n16-1 are an identity pad.
+template <bool REV>
+struct TwoSide {
+  double* A; double* z; double* invd; double* xch;
+  int n16, bw, rlim, dummy, lane;
+  // processing-space index -> storage index of rows (z, invd)
+  __device__ __forceinline__ int o(int i) const { return REV ? n16 - 1 - i : i; }
+  // band slot of processing-space entry (i, j), j <= i, i - j <= bw
+  __device__ __forceinline__ int slot(int i, int j) const {
+    return REV ? (n16 - 1 - j) * (bw + 1) + (j - i + bw) : i * (bw + 1) + (j - i + bw);
+  }
+  __device__ __forceinline__ double get(int i, int j) const {  // branch-free; 0 outside band / rlim
+    const bool ok = j <= i && i - j <= bw && i < rlim;
+    const double v = A[ok ? slot(i, j) : 0];
+    return ok ? v : 0.0;
+  }
+  __device__ __forceinline__ void init(v4d (&T)[10], double& zr) const {
+#pragma unroll
+    for (int I = 0; I < 4; ++I)
+#pragma unroll
+      for (int J = 0; J <= I; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) T[tri4(I, J)][r] = get(16 * I + (lane >> 4) + 4 * r, 16 * J + (lane & 15));
+    zr = lane < rlim ? z[o(lane)] : 0.0;
+  }
+  // panels kb = kb0, kb0+16, ... < kend (processing space)
+  __device__ __forceinline__ void panels(v4d (&T)[10], double& zr, bool& bad, int kb0, int kend) const {
+    const int ci = lane & 15, ck = lane >> 4;
+    v4d Tn[4];
+    for (int kb = kb0; kb < kend; kb += 16) {
+#pragma unroll
+      for (int J = 0; J < 4; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Tn[J][r] = get(kb + 64 + ck + 4 * r, kb + 16 + 16 * J + ci);
+      const double zin = kb + 16 + lane < rlim ? z[o(kb + 16 + lane)] : 0.0;
+#pragma unroll
+      for (int I = 0; I < 4; ++I)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xch[(16 * I + ck + 4 * r) * 17 + ci] = T[tri4(I, 0)][r];
+      wave_sync_lds();
+      double P[NB];
+#pragma unroll
+      for (int q = 0; q < NB; ++q) P[q] = xch[lane * 17 + q];
+      wave_sync_lds();
+      double yq = 0.0;
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const double akk = readlane_d(P[q], q);
+        bad |= !(akk > 0.0);
+        const double y = rsqrt_refined(akk);
+        P[q] *= y;
+        yq = lane == q ? y : yq;
+        const double zk = readlane_d(zr, q) * y;
+        zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
+#pragma unroll
+        for (int q2 = q + 1; q2 < NB; ++q2) {
+          const double l = readlane_d(P[q], q2);
+          P[q2] = fma(-P[q], l, P[q2]);
+        }
+      }
+      {
+        const int row = kb + lane;
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          const int col = kb + q;
+          const bool ok = row < rlim && col <= row && row - col <= bw;
+          A[ok ? slot(row, col) : dummy] = P[q];
+          xch[lane * 17 + q] = P[q];
+        }
+        if (lane < NB) { z[o(row)] = zr; invd[o(row)] = yq; }
+      }
+      wave_sync_lds();
+      double opA[4][4];
+#pragma unroll
+      for (int I = 1; I < 4; ++I)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) opA[I][kk] = xch[(16 * I + ci) * 17 + 4 * kk + ck];
+#pragma unroll
+      for (int J = 1; J < 4; ++J)
+#pragma unroll
+        for (int I = J; I < 4; ++I)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            T[tri4(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[J][kk], T[tri4(I, J)], 0, 0, 0);
+      const double zs = __shfl_down(zr, 16, 64);
+      zr = lane < 48 ? zs : zin;
+      T[tri4(0, 0)] = T[tri4(1, 1)];
+      T[tri4(1, 0)] = T[tri4(2, 1)]; T[tri4(1, 1)] = T[tri4(2, 2)];
+      T[tri4(2, 0)] = T[tri4(3, 1)]; T[tri4(2, 1)] = T[tri4(3, 2)]; T[tri4(2, 2)] = T[tri4(3, 3)];
+#pragma unroll
+      for (int J = 0; J < 4; ++J) T[tri4(3, J)] = Tn[J];
+    }
+  }
+  // L^T y = z for the 16-row blocks c0 = c_hi, c_hi-16, ..., c_lo (processing space); rows below
+  // a block are gathered up to rlim-1
+  __device__ __forceinline__ void backsub(int c_hi, int c_lo) const {
+    const int jc = lane & 15, g = lane >> 4;
+    for (int c0 = c_hi; c0 >= c_lo; c0 -= 16) {
+      const int j = c0 + jc;
+      double lk[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        const bool ok = k > jc;
+        const double v = A[ok ? slot(c0 + k, j) : 0];
+        lk[k] = ok ? v : 0.0;
+      }
+      const int iend = min(rlim - 1, j + bw);
+      double av[16], zv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = c0 + 16 + g + 4 * u;
+        const bool ok = i <= iend;
+        av[u] = A[ok ? slot(i, j) : 0];
+        zv[u] = z[ok ? o(i) : 0];
+        av[u] = ok ? av[u] : 0.0;
+      }
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a4[u & 3] = fma(av[u], zv[u], a4[u & 3]);
+      double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      acc += __shfl_xor(acc, 16, 64);
+      acc += __shfl_xor(acc, 32, 64);
+      double zb = z[o(j)] - acc;
+      const double iv = invd[o(j)];
+#pragma unroll
+      for (int k = NB - 1; k >= 0; --k) {
+        const double yk = readlane_d(zb, k) * readlane_d(iv, k);
+        zb = jc == k ? yk : fma(-lk[k], yk, zb);
+      }
+      if (g == 0) z[o(j)] = zb;
+      wave_sync_lds();
+    }
+  }
+};
+
+__global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int s_bad;
+  const int w = blockIdx.x;
+  if (d.st[w].done) return;
+  if (d.sharded && d.wfail[w] > 0.0) {
+    if (threadIdx.x == 0) d.st[w].chol_fail = 1;
+    return;
+  }
+  const BaWin W = d.win[w];
+  const int n = W.n, bw = W.bw;
+  const int n16 = (n + 15) & ~15;
+  const int m = 16 * ((n16 - 48) / 32);  // T = [0, m), M = [m, m+48), B = [m+48, n16)
+  const int nB = n16 - m - 48;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double* A = smem;
+  double* z = A + (size_t)n16 * (bw + 1);
+  double* invd = z + n16;
+  double* xch = invd + n16;       // 2 x (64 x 18): per side exchange + dummy slots; X (48 x 48) later
+  double* zX = xch + 2 * 64 * 18;  // 48
+  {
+    const double* __restrict__ S = d.env + W.env_base;
+    const int ne = n * (bw + 1);
+    for (int k = t; k < ne; k += 256) A[k] = S[k];
+    for (int k = ne + t; k < n16 * (bw + 1); k += 256) A[k] = (k % (bw + 1)) == bw ? 1.0 : 0.0;
+    for (int k = t; k < n16; k += 256) z[k] = k < n ? d.rhs[W.row_base + k] : 0.0;
+    if (t == 0) s_bad = 0;
+  }
+  __syncthreads();
+  const TwoSide<false> top{A, z, invd, xch, n16, bw, m + 48, (int)(xch + 64 * 17 + lane - A), lane};
+  const TwoSide<true> bot{A, z, invd, xch + 64 * 18, n16, bw, nB + 48, (int)(xch + 64 * 18 + 64 * 17 + lane - A), lane};
+  v4d T[10];
+  double zr = 0.0;
+  bool bad = false;
+  if (wv == 0) { top.init(T, zr); top.panels(T, zr, bad, 0, m); }
+  else if (wv == 1) { bot.init(T, zr); bot.panels(T, zr, bad, 0, nB); }
+  __syncthreads();  // both sides done reading S_MM / xch
+  double* X = xch;  // 48 x 48, original M-relative (row, col), lower
+  if (wv == 1) {
+#pragma unroll
+    for (int I = 0; I < 3; ++I)
+#pragma unroll
+      for (int J = 0; J <= I; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rho = 16 * I + (lane >> 4) + 4 * r, kap = 16 * J + (lane & 15);
+          if (kap <= rho) X[(47 - kap) * 48 + (47 - rho)] = T[tri4(I, J)][r];
+        }
+    if (lane < 48) zX[47 - lane] = zr;
+    if (bad) s_bad = 1;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    // S_M = (S_MM - L_MT L_MT^T) + (S_MM - L_MB L_MB^T) - S_MM ; rows >= m+48 leave the window
+#pragma unroll
+    for (int I = 0; I < 3; ++I)
+#pragma unroll
+      for (int J = 0; J <= I; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rho = 16 * I + (lane >> 4) + 4 * r, kap = 16 * J + (lane & 15);
+          if (kap <= rho) T[tri4(I, J)][r] += X[rho * 48 + kap] - top.get(m + rho, m + kap);
+        }
+#pragma unroll
+    for (int J = 0; J < 4; ++J) T[tri4(3, J)] = v4d{0.0, 0.0, 0.0, 0.0};
+    zr = lane < 48 ? zr + zX[lane] - z[m + lane] : 0.0;
+    top.panels(T, zr, bad, m, m + 48);
+    if (bad) s_bad = 1;
+  }
+  __syncthreads();
+  if (s_bad) {
+    if (t == 0) d.st[w].chol_fail = 1;
+    return;
+  }
+  if (wv == 0) top.backsub(m + 32, m);  // y_M
+  __syncthreads();
+  if (wv == 0) top.backsub(m - 16, 0);  // y_T
+  else if (wv == 1) bot.backsub(nB - 16, 0);  // y_B (reversed)
+  __syncthreads();
+  for (int k = t; k < n; k += 256) d.ycam[W.row_base + k] = z[k];
+  const int cur = d.st[w].cur;
+  for (int ci2 = t; ci2 < W.n_poses; ci2 += 256) {
+    const int c = W.pose_base + ci2;
+    double xn[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      xn[k] = d.x_pose[cur][6 * c + k] + (-z[6 * ci2 + k]) * d.scale_pose[6 * c + k];
+      d.x_pose[cur ^ 1][6 * c + k] = xn[k];
+    }
+    d.rot_cand[c] = lorb::rot_val(xn);
+  }
+}
+
 // K7: point-group back-substitution: b_p -= sum_e W_e^T y_c(e) (observation phase + ordered
 // point reduction), point step / candidate (point phase), model cost change and candidate cost
 // per observation (observation phase).
@@ -1496,7 +1733,7 @@ LMOpt to_dev_opt(const lorb_lm_options* o) {
 struct lorb_ba_plan {
   lorb_ctx* ctx = nullptr;
   int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_bp = 0, n_pairs = 0;
-  int env_total = 0, n_total = 0, max_env = 0, max_bw = 0, max_env_w = 0;
+  int env_total = 0, n_total = 0, max_env = 0, max_bw = 0, max_env_w = 0, min_n16 = 1 << 30;
   std::vector<BaWin> hwin;
   std::vector<void*> allocs;
   BaDev dev{};
@@ -1662,7 +1899,8 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     P->max_bw = std::max(P->max_bw, bwid);
     {
       const int n16 = (n + 15) & ~15;
-      P->max_env_w = std::max(P->max_env_w, n16 * (bwid + 1) + 2 * n16 + 64 * 18);
+      P->max_env_w = std::max(P->max_env_w, n16 * (bwid + 1) + 2 * n16 + 2 * 64 * 18 + 48);
+      if (n16 > 0) P->min_n16 = std::min(P->min_n16, n16);
     }
     env_base += bw.env_size; row_base += n;
     // point groups: consecutive points with <= kGB observations (and <= kGB points) in total
@@ -1791,7 +2029,12 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
     LORB_TRY(lorb::comm_allreduce(P->comm, d.env_part, d.env, (size_t)P->env_total + P->n_total + P->W, LORB_OP_SUM));
   static const bool force_old = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'o'; }();
   const bool chol_w = !force_old && P->max_bw <= 48 && sizeof(double) * (size_t)P->max_env_w <= (size_t)kLdsBudget;
-  if (P->Ctot && chol_w) {
+  static const bool no_2s = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'w'; }();
+  const bool chol_2s = chol_w && !no_2s && P->min_n16 >= 128;
+  if (P->Ctot && chol_2s) {
+    lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
+    hipLaunchKernelGGL(k_ba_chol_2s, dim3(P->W), dim3(256), sizeof(double) * (size_t)P->max_env_w, s, d);
+  } else if (P->Ctot && chol_w) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
     hipLaunchKernelGGL(k_ba_chol_w, dim3(P->W), dim3(256), sizeof(double) * (size_t)P->max_env_w, s, d);
   } else if (P->Ctot) {
