@@ -1104,26 +1104,22 @@ __global__ __launch_bounds__(256) void k_ba_chol_w(BaDev d) {
 // K6t: two-sided ("twisted") banded Cholesky for band <= 48 and n >= 128.  The chain of
 // dependent panels is the cost of K6w (one wavefront is latency/issue bound), so the matrix is
 // split into T = [0, m), M = [m, m+48) and B = [m+48, n16): T and B do not couple (band <= 48).
-// Wave 0 eliminates T top-down and wave 1 eliminates B bottom-up (the reversed matrix, whose
-// band is the same) concurrently with the K6w panel machinery; their windows end on M holding
-// S_MM - L_MT L_MT^T and S_MM - L_MB L_MB^T, which wave 0 combines (minus S_MM) and factors
-// (3 panels).  Back-substitution: M, then T (wave 0) and B (wave 1) concurrently.  L of both
-// sides lives in the band storage of S in LDS (wave 1 writes L'(i', j') into the slot of the
-// original lower entry it equals); the only LDS data both sides read is S_MM, which neither
-// overwrites.  Rows n .. n16-1 are an identity pad.
-template <bool REV>
-struct TwoSide {
-  double* A; double* z; double* invd; double* xch;
-  int n16, bw, rlim, dummy, lane;
-  // processing-space index -> storage index of rows (z, invd)
-  __device__ __forceinline__ int o(int i) const { return REV ? n16 - 1 - i : i; }
-  // band slot of processing-space entry (i, j), j <= i, i - j <= bw
-  __device__ __forceinline__ int slot(int i, int j) const {
-    return REV ? (n16 - 1 - j) * (bw + 1) + (j - i + bw) : i * (bw + 1) + (j - i + bw);
-  }
-  __device__ __forceinline__ double get(int i, int j) const {  // branch-free; 0 outside band / rlim
-    const bool ok = j <= i && i - j <= bw && i < rlim;
-    const double v = A[ok ? slot(i, j) : 0];
+// Wave 0 eliminates T top-down and wave 1 eliminates B bottom-up concurrently: the bottom part
+// is staged REVERSED (row i' = n16-1-i; the band of the reversed matrix is the same), so both
+// waves run the identical panel code on their own LDS band.  Their windows end on M holding
+// S_MM - L_MT L_MT^T and S_MM - L_MB L_MB^T; wave 0 combines them (minus S_MM) and factors M
+// (3 panels).  Back-substitution: M, then T (wave 0) and B (wave 1) concurrently.  Rows
+// n .. n16-1 are an identity pad.
+struct BandSide {
+  double* A;     // band storage, rows x (bw + 1), row i holds cols i-bw .. i; the diagonal slot
+                 // holds 1 / L(i, i) (the only use of the diagonal is the back-substitution)
+  double* z;     // rows: rhs -> forward substitution -> solution
+  double* xch;   // 64 x 17 exchange (column 16 of each row: dummy store slot of that lane)
+  int rows, bw, lane;
+
+  __device__ __forceinline__ double get(int i, int j) const {  // branch-free; 0 outside band / rows
+    const bool ok = j <= i && i - j <= bw && i < rows;
+    const double v = A[ok ? i * (bw + 1) + (j - i + bw) : 0];
     return ok ? v : 0.0;
   }
   __device__ __forceinline__ void init(v4d (&T)[10], double& zr) const {
@@ -1133,18 +1129,47 @@ struct TwoSide {
       for (int J = 0; J <= I; ++J)
 #pragma unroll
         for (int r = 0; r < 4; ++r) T[tri4(I, J)][r] = get(16 * I + (lane >> 4) + 4 * r, 16 * J + (lane & 15));
-    zr = lane < rlim ? z[o(lane)] : 0.0;
+    zr = lane < rows ? z[lane] : 0.0;
   }
-  // panels kb = kb0, kb0+16, ... < kend (processing space)
+  // panels kb = kb0, kb0+16, ... < kend.  Per-lane addresses are linear in kb; band validity is
+  // static per lane and element, only the row limit varies.  The pivot and next-column
+  // multipliers use v_readlane (the dependency chain); the other multipliers of a column go
+  // through LDS broadcast reads, off the chain.
   __device__ __forceinline__ void panels(v4d (&T)[10], double& zr, bool& bad, int kb0, int kend) const {
     const int ci = lane & 15, ck = lane >> 4;
-    v4d Tn[4];
+    const int B1 = bw + 1;
+    int tn_addr = (kb0 + 64 + ck) * B1 + (16 + ci - 64 - ck + bw) ;  // entering tile (J, r) adds 16 J - 4 r bw ... (below)
+    unsigned tn_ok = 0;
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 64 + ck + 4 * r, j = 16 + 16 * J + ci;
+        tn_ok |= (unsigned)(j <= i && i - j <= bw) << (4 * J + r);
+      }
+    unsigned l_ok = 0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) l_ok |= (unsigned)(q <= lane && lane - q <= bw) << q;
+    int l_base = (kb0 + lane) * B1 + (bw - lane);  // slot of (kb0 + lane, kb0 + q) = l_base + q
+    double* colbuf = xch;  // 16 x 64 during the factorization (xch is idle then)
+    double* dummy = xch + lane * 17 + 16;
     for (int kb = kb0; kb < kend; kb += 16) {
+      // Opaque per-iteration copies of the lane constants: otherwise every lane comparison of the
+      // unrolled panel is hoisted out of the loop as an SGPR mask and the masks spill.
+      int lane = this->lane, lok = (int)l_ok, tok = (int)tn_ok;
+      asm volatile("" : "+v"(lane), "+v"(lok), "+v"(tok));
+      v4d Tn[4];
 #pragma unroll
       for (int J = 0; J < 4; ++J)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) Tn[J][r] = get(kb + 64 + ck + 4 * r, kb + 16 + 16 * J + ci);
-      const double zin = kb + 16 + lane < rlim ? z[o(kb + 16 + lane)] : 0.0;
+        for (int r = 0; r < 4; ++r) {
+          // (kb+64+ck+4r, kb+16+16J+ci): row offset 4r, column offset 16J relative to tn_addr
+          const bool ok = (((unsigned)tok >> (4 * J + r)) & 1u) && kb + 64 + ck + 4 * r < rows;
+          const double v = A[ok ? tn_addr + 4 * r * B1 + 16 * J - 4 * r : 0];
+          Tn[J][r] = ok ? v : 0.0;
+        }
+      tn_addr += 16 * B1;
+      const double zin = kb + 16 + lane < rows ? z[kb + 16 + lane] : 0.0;
 #pragma unroll
       for (int I = 0; I < 4; ++I)
 #pragma unroll
@@ -1152,7 +1177,7 @@ struct TwoSide {
       wave_sync_lds();
       double P[NB];
 #pragma unroll
-      for (int q = 0; q < NB; ++q) P[q] = xch[lane * 17 + q];
+      for (int q = 0; q < NB; ++q) P[q] = xch[lane * 17 + q];  // lanes < q: upper garbage, never used
       wave_sync_lds();
       double yq = 0.0;
 #pragma unroll
@@ -1160,26 +1185,29 @@ struct TwoSide {
         const double akk = readlane_d(P[q], q);
         bad |= !(akk > 0.0);
         const double y = rsqrt_refined(akk);
-        P[q] *= y;
+        P[q] *= y;  // lane q: akk * y = L(k, k)
         yq = lane == q ? y : yq;
         const double zk = readlane_d(zr, q) * y;
         zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
+        if (q + 1 < NB) {
+          colbuf[q * 64 + lane] = P[q];
+          const double l1 = readlane_d(P[q], q + 1);
+          P[q + 1] = fma(-P[q], l1, P[q + 1]);
 #pragma unroll
-        for (int q2 = q + 1; q2 < NB; ++q2) {
-          const double l = readlane_d(P[q], q2);
-          P[q2] = fma(-P[q], l, P[q2]);
+          for (int q2 = q + 2; q2 < NB; ++q2) P[q2] = fma(-P[q], colbuf[q * 64 + q2], P[q2]);
         }
       }
+      wave_sync_lds();  // colbuf reads done before xch is rewritten
       {
-        const int row = kb + lane;
+        const bool rowvalid = kb + lane < rows;
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-          const int col = kb + q;
-          const bool ok = row < rlim && col <= row && row - col <= bw;
-          A[ok ? slot(row, col) : dummy] = P[q];
+          const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
+          *(ok ? A + l_base + q : dummy) = q == lane ? yq : P[q];
           xch[lane * 17 + q] = P[q];
         }
-        if (lane < NB) { z[o(row)] = zr; invd[o(row)] = yq; }
+        l_base += 16 * B1;
+        if (lane < NB) z[kb + lane] = zr;
       }
       wave_sync_lds();
       double opA[4][4];
@@ -1187,12 +1215,14 @@ struct TwoSide {
       for (int I = 1; I < 4; ++I)
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) opA[I][kk] = xch[(16 * I + ci) * 17 + 4 * kk + ck];
+      // k-step outer: the six tiles' accumulation chains interleave, so consecutive MFMAs are
+      // independent and the matrix pipe stays full
 #pragma unroll
-      for (int J = 1; J < 4; ++J)
+      for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-        for (int I = J; I < 4; ++I)
+        for (int J = 1; J < 4; ++J)
 #pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
+          for (int I = J; I < 4; ++I)
             T[tri4(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[J][kk], T[tri4(I, J)], 0, 0, 0);
       const double zs = __shfl_down(zr, 16, 64);
       zr = lane < 48 ? zs : zin;
@@ -1203,8 +1233,8 @@ struct TwoSide {
       for (int J = 0; J < 4; ++J) T[tri4(3, J)] = Tn[J];
     }
   }
-  // L^T y = z for the 16-row blocks c0 = c_hi, c_hi-16, ..., c_lo (processing space); rows below
-  // a block are gathered up to rlim-1
+  // L^T y = z for the 16-row blocks c0 = c_hi, c_hi-16, ..., c_lo; rows below a block are
+  // gathered up to rows-1
   __device__ __forceinline__ void backsub(int c_hi, int c_lo) const {
     const int jc = lane & 15, g = lane >> 4;
     for (int c0 = c_hi; c0 >= c_lo; c0 -= 16) {
@@ -1213,17 +1243,17 @@ struct TwoSide {
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         const bool ok = k > jc;
-        const double v = A[ok ? slot(c0 + k, j) : 0];
+        const double v = A[ok ? (c0 + k) * (bw + 1) + (j - (c0 + k) + bw) : 0];
         lk[k] = ok ? v : 0.0;
       }
-      const int iend = min(rlim - 1, j + bw);
+      const int iend = min(rows - 1, j + bw);
       double av[16], zv[16];
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int i = c0 + 16 + g + 4 * u;
         const bool ok = i <= iend;
-        av[u] = A[ok ? slot(i, j) : 0];
-        zv[u] = z[ok ? o(i) : 0];
+        av[u] = A[ok ? i * (bw + 1) + (j - i + bw) : 0];
+        zv[u] = z[ok ? i : 0];
         av[u] = ok ? av[u] : 0.0;
       }
       double a4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1232,14 +1262,14 @@ struct TwoSide {
       double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
       acc += __shfl_xor(acc, 16, 64);
       acc += __shfl_xor(acc, 32, 64);
-      double zb = z[o(j)] - acc;
-      const double iv = invd[o(j)];
+      double zb = z[j] - acc;
+      const double iv = A[j * (bw + 1) + bw];  // 1 / L(j, j)
 #pragma unroll
       for (int k = NB - 1; k >= 0; --k) {
         const double yk = readlane_d(zb, k) * readlane_d(iv, k);
         zb = jc == k ? yk : fma(-lk[k], yk, zb);
       }
-      if (g == 0) z[o(j)] = zb;
+      if (g == 0) z[j] = zb;
       wave_sync_lds();
     }
   }
@@ -1255,34 +1285,54 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
     return;
   }
   const BaWin W = d.win[w];
-  const int n = W.n, bw = W.bw;
+  const int n = W.n, bw = W.bw, B1 = bw + 1;
   const int n16 = (n + 15) & ~15;
   const int m = 16 * ((n16 - 48) / 32);  // T = [0, m), M = [m, m+48), B = [m+48, n16)
   const int nB = n16 - m - 48;
+  const int rt = m + 48, rb = nB + 48;    // rows of the top / reversed-bottom bands
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  double* A = smem;
-  double* z = A + (size_t)n16 * (bw + 1);
-  double* invd = z + n16;
-  double* xch = invd + n16;       // 2 x (64 x 18): per side exchange + dummy slots; X (48 x 48) later
-  double* zX = xch + 2 * 64 * 18;  // 48
+  double* At = smem;
+  double* Ab = At + rt * B1;
+  double* zt = Ab + rb * B1;
+  double* zb = zt + rt;
+  double* xt = zb + rb;       // 64 x 18 per side (rows of 17); both together hold X (48 x 48)
+  double* xb = xt + 64 * 18;
+  double* zX = xb + 64 * 18;  // 48
   {
     const double* __restrict__ S = d.env + W.env_base;
-    const int ne = n * (bw + 1);
-    for (int k = t; k < ne; k += 256) A[k] = S[k];
-    for (int k = ne + t; k < n16 * (bw + 1); k += 256) A[k] = (k % (bw + 1)) == bw ? 1.0 : 0.0;
-    for (int k = t; k < n16; k += 256) z[k] = k < n ? d.rhs[W.row_base + k] : 0.0;
+    for (int k = t; k < rt * B1; k += 256) {  // top: rows 0 .. m+47 as they are (m + 48 <= n)
+      const int i = k / B1, off = k - i * B1;
+      At[k] = i - (bw - off) >= 0 ? S[k] : 0.0;
+    }
+    for (int k = t; k < rb * B1; k += 256) {  // bottom reversed: (i', j' = i' + off - bw)
+      const int ip = k / B1, off = k - ip * B1;
+      const int jp = ip + off - bw;
+      const int row = n16 - 1 - jp, col = n16 - 1 - ip;  // original lower entry, row >= col
+      double v = 0.0;
+      if (jp >= 0) v = row >= n ? (row == col ? 1.0 : 0.0) : S[row * B1 + (col - row + bw)];
+      Ab[k] = v;
+    }
+    for (int k = t; k < rt; k += 256) zt[k] = d.rhs[W.row_base + k];
+    for (int k = t; k < rb; k += 256) { const int row = n16 - 1 - k; zb[k] = row < n ? d.rhs[W.row_base + row] : 0.0; }
     if (t == 0) s_bad = 0;
   }
   __syncthreads();
-  const TwoSide<false> top{A, z, invd, xch, n16, bw, m + 48, (int)(xch + 64 * 17 + lane - A), lane};
-  const TwoSide<true> bot{A, z, invd, xch + 64 * 18, n16, bw, nB + 48, (int)(xch + 64 * 18 + 64 * 17 + lane - A), lane};
+  const BandSide top{At, zt, xt, rt, bw, lane};
+  const BandSide bot{Ab, zb, xb, rb, bw, lane};
+  const BandSide& me = wv == 0 ? top : bot;
   v4d T[10];
   double zr = 0.0;
   bool bad = false;
-  if (wv == 0) { top.init(T, zr); top.panels(T, zr, bad, 0, m); }
-  else if (wv == 1) { bot.init(T, zr); bot.panels(T, zr, bad, 0, nB); }
-  __syncthreads();  // both sides done reading S_MM / xch
-  double* X = xch;  // 48 x 48, original M-relative (row, col), lower
+#ifdef LORB_CHOL_STAMPS
+  const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+#define C2_STAMP(k) do { if (lane == 0 && wv < 2) d.dbg[8 * w + (k) + 4 * wv] = __builtin_amdgcn_s_memtime() - st0; } while (0)
+#else
+#define C2_STAMP(k) do {} while (0)
+#endif
+  if (wv < 2) { me.init(T, zr); me.panels(T, zr, bad, 0, wv == 0 ? m : nB); }
+  C2_STAMP(0);
+  __syncthreads();
+  double* X = xt;  // 48 x 48 in the two exchanges (idle now), original M orientation
   if (wv == 1) {
 #pragma unroll
     for (int I = 0; I < 3; ++I)
@@ -1310,28 +1360,37 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
         }
 #pragma unroll
     for (int J = 0; J < 4; ++J) T[tri4(3, J)] = v4d{0.0, 0.0, 0.0, 0.0};
-    zr = lane < 48 ? zr + zX[lane] - z[m + lane] : 0.0;
+    zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
+    C2_STAMP(1);
     top.panels(T, zr, bad, m, m + 48);
     if (bad) s_bad = 1;
+    C2_STAMP(2);
   }
   __syncthreads();
   if (s_bad) {
     if (t == 0) d.st[w].chol_fail = 1;
     return;
   }
-  if (wv == 0) top.backsub(m + 32, m);  // y_M
+  if (wv == 0) {
+    top.backsub(m + 32, m);                      // y_M
+    if (lane < 48) zb[nB + 47 - lane] = zt[m + lane];  // into the reversed bottom rows
+  }
   __syncthreads();
-  if (wv == 0) top.backsub(m - 16, 0);  // y_T
-  else if (wv == 1) bot.backsub(nB - 16, 0);  // y_B (reversed)
+  if (wv == 0) top.backsub(m - 16, 0);           // y_T
+  else if (wv == 1) bot.backsub(nB - 16, 0);     // y_B (reversed)
+  C2_STAMP(3);
   __syncthreads();
-  for (int k = t; k < n; k += 256) d.ycam[W.row_base + k] = z[k];
+#undef C2_STAMP
+  for (int k = t; k < n; k += 256) d.ycam[W.row_base + k] = k < rt ? zt[k] : zb[n16 - 1 - k];
   const int cur = d.st[w].cur;
   for (int ci2 = t; ci2 < W.n_poses; ci2 += 256) {
     const int c = W.pose_base + ci2;
     double xn[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      xn[k] = d.x_pose[cur][6 * c + k] + (-z[6 * ci2 + k]) * d.scale_pose[6 * c + k];
+      const int row = 6 * ci2 + k;
+      const double y = row < rt ? zt[row] : zb[n16 - 1 - row];
+      xn[k] = d.x_pose[cur][6 * c + k] + (-y) * d.scale_pose[6 * c + k];
       d.x_pose[cur ^ 1][6 * c + k] = xn[k];
     }
     d.rot_cand[c] = lorb::rot_val(xn);
@@ -1899,7 +1958,10 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P
     P->max_bw = std::max(P->max_bw, bwid);
     {
       const int n16 = (n + 15) & ~15;
-      P->max_env_w = std::max(P->max_env_w, n16 * (bwid + 1) + 2 * n16 + 2 * 64 * 18 + 48);
+      // one-sided K6w: band + z + invd + exchange; two-sided K6t: (n16 + 48) band rows, z, invd,
+      // two exchanges, zX -- the larger of the two
+      P->max_env_w = std::max(P->max_env_w, std::max(n16 * (bwid + 1) + 2 * n16 + 64 * 18,
+                                                      (n16 + 48) * (bwid + 2) + 2 * 64 * 18 + 48));
       if (n16 > 0) P->min_n16 = std::min(P->min_n16, n16);
     }
     env_base += bw.env_size; row_base += n;

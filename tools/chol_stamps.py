@@ -13,5 +13,5 @@ for kw in [dict(n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400), dict(n_k
     ctx.sync()
     out = (C.c_ulonglong * 8)()
     lib().lorb_ba_plan_debug_stamps(plan._p, out)
-    print(kw["n_kf"], "stamps", list(out[:5]), "total", sum(out[:5]))
+    print(kw["n_kf"], "stamps", list(out[:8]))
     plan.close()
