@@ -27,7 +27,10 @@ using lorb::residual_jac;
 using lorb::residual_jac_s;
 using lorb::residual_s;
 
-constexpr int kGB = 256;  // observations per point group (one workgroup), see K1
+#ifndef LORB_KGB
+#define LORB_KGB 256
+#endif
+constexpr int kGB = LORB_KGB;  // observations per point group (one workgroup), see K1
 
 struct BaWin {
   int pose_base, n_poses, point_base, n_points;
@@ -200,20 +203,30 @@ __global__ __launch_bounds__(64) void k_ba_rot_lin(BaDev d, int ctot) {
 // summation order as a point-serial loop.  A point with more than kGB observations gets a group
 // of its own and the observation phases loop over chunks.
 
-// deterministic workgroup reductions (fixed butterfly per wave, fixed wave order)
+// deterministic point-group reductions (fixed butterfly per wave, fixed wave order) over the
+// kGB / 64 waves of a point-group workgroup
+constexpr int kGW = kGB / 64;
 __device__ __forceinline__ double block_sum256(double v, double* red4) {
   v = wave_sum(v);
+  if (kGW == 1) return v;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
   __syncthreads();
-  return ((red4[0] + red4[1]) + red4[2]) + red4[3];
+  double s = red4[0];
+#pragma unroll
+  for (int k = 1; k < kGW; ++k) s += red4[k];
+  return s;
 }
 __device__ __forceinline__ double block_max256(double v, double* red4) {
   v = wave_max(v);
+  if (kGW == 1) return v;
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
   __syncthreads();
-  return fmax(fmax(red4[0], red4[1]), fmax(red4[2], red4[3]));
+  double s = red4[0];
+#pragma unroll
+  for (int k = 1; k < kGW; ++k) s = fmax(s, red4[k]);
+  return s;
 }
 
 // K1: linearisation of a point group (windows that (re)linearise this iteration): per
