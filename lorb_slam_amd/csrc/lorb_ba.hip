@@ -512,6 +512,35 @@ __device__ __forceinline__ double& band(double* A, int bw, int i, int j) {
 // the camera Jacobi scales are applied once per block.  Block pairs are sorted by camera and
 // remapped so that each XCD (blockIdx % 8 group) takes a contiguous run: the tiles of a camera
 // are re-read from that XCD's L2 instead of from the fabric.
+__device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc)[36]) {
+  double Qh[6], Jl[6], Ch[12], Cl[12];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { Qh[k] = d.obs_Q[6 * pr.x + k]; Jl[k] = d.obs_Jps[6 * pr.y + k]; }
+#pragma unroll
+  for (int k = 0; k < 12; ++k) { Ch[k] = d.obs_Jc[12 * pr.x + k]; Cl[k] = d.obs_Jc[12 * pr.y + k]; }
+  double M[4], N[12];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+      M[2 * r + s] = Qh[3 * r] * Jl[3 * s] + Qh[3 * r + 1] * Jl[3 * s + 1] + Qh[3 * r + 2] * Jl[3 * s + 2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) N[6 * r + j] = M[2 * r] * Cl[j] + M[2 * r + 1] * Cl[6 + j];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[6 * i + j] += Ch[i] * N[j] + Ch[6 + i] * N[6 + j];
+}
+
+// K5: reduced camera system S (band storage) + rhs: one 256-thread workgroup per non-zero camera
+// block pair; threads stride the pair list two pairs at a time (both pairs' loads are in flight
+// before either is accumulated: the loop is load-latency bound), fixed-order wave + LDS
+// reduction.  Each (obs_h, obs_l) term is Jc_h^T M Jc_l with the 2x2 M = Q_h Jps_l^T (108 FMA,
+// 36 doubles read); the camera Jacobi scales are applied once per block.  Block pairs are sorted
+// by camera and remapped so that each XCD (blockIdx % 8 group) takes a contiguous run: the tiles
+// of a camera are re-read from that XCD's L2 instead of from the fabric.
 __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o, int n_bp) {
   __shared__ double red[4][37];
   int bid;
@@ -528,27 +557,13 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o, int n_bp) {
   double acc[36];
 #pragma unroll
   for (int k = 0; k < 36; ++k) acc[k] = 0.0;
-  for (int q = bp.off + t; q < bp.off + bp.cnt; q += 256) {
-    const int2 pr = d.pairs[q];  // camera-major slots (obs in camera ch, obs in camera cl) of one point
-    double Qh[6], Jl[6], Ch[12], Cl[12];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { Qh[k] = d.obs_Q[6 * pr.x + k]; Jl[k] = d.obs_Jps[6 * pr.y + k]; }
-#pragma unroll
-    for (int k = 0; k < 12; ++k) { Ch[k] = d.obs_Jc[12 * pr.x + k]; Cl[k] = d.obs_Jc[12 * pr.y + k]; }
-    double M[4], N[12];
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-        M[2 * r + s] = Qh[3 * r] * Jl[3 * s] + Qh[3 * r + 1] * Jl[3 * s + 1] + Qh[3 * r + 2] * Jl[3 * s + 2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) N[6 * r + j] = M[2 * r] * Cl[j] + M[2 * r + 1] * Cl[6 + j];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) acc[6 * i + j] += Ch[i] * N[j] + Ch[6 + i] * N[6 + j];
+  const int end = bp.off + bp.cnt;
+  for (int q = bp.off + t; q < end; q += 512) {
+    const int2 p0 = d.pairs[q];  // camera-major slots (obs in camera ch, obs in camera cl) of one point
+    const bool two = q + 256 < end;
+    const int2 p1 = d.pairs[two ? q + 256 : q];
+    schur_pair(d, p0, acc);
+    if (two) schur_pair(d, p1, acc);
   }
   const bool diag = bp.ch == bp.cl;
   double r6[6] = {0, 0, 0, 0, 0, 0};
