@@ -41,9 +41,11 @@ INT32_VALU_PEAK = 256 * 4 * 32 * CLOCK      # lane-ops/s: 256 CU x 4 SIMD32 (MI3
 FP64_PEAK = 78.6e12                          # FP64 vector/matrix dense, MI355X spec
 HBM_PEAK = 8.0e12                            # HBM3E spec (MI355X_MICROARCH)
 OPS_PER_PAIR = 16                            # 8 x v_xor_b32 + 8 x v_bcnt_u32_b32 per 256-bit pair
-K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_w"}
+# the Cholesky id covers three kernels chosen by band shape; C3/C4/C5 windows
+# (band 47, n >= 128) run the two-sided k_ba_chol_2s
+K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_2s"}
 # rocprofv3 short names (tools/pmc_traffic.py) of the same kernels, for the PMC traffic lookup
-K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_w"}
+K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_2s"}
 TRAFFIC = os.path.join(ROOT, "profiles", "r01", "traffic.json")
 METRIC = "ORB matches/sec + local-BA iterations/sec (50 KF, 10k pts) at 1/2/4/8 MI355X"
 
