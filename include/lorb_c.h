@@ -368,6 +368,19 @@ int lorb_bf_match_sharded_dev(lorb_ctx* ctx, lorb_comm* comm, int32_t n_problems
                               int32_t* d_cc_train, int32_t* d_cc_dist, int32_t* d_match_train,
                               int32_t* d_n_matches);
 
+/* MapPoint::ComputeDescriptor (src/map_point.cpp:69-129; called at src/visual_odometry.cpp:94,392),
+ * batched over map points.  Point p's candidate descriptors -- its observations in
+ * std::map<Frame*, size_t> order, bad frames skipped (:74-81) -- are rows [d_off[p], d_off[p+1]) of
+ * desc (32 bytes each).  best[p] = index within the point's list of the descriptor whose median
+ * Hamming distance to the list (self included; element floor((n-1)/2) of the sorted row) is
+ * smallest, first index on ties; -1 for an empty list (the reference indexes an empty vector
+ * there).  out_desc (optional, n_points x 32) receives the chosen descriptor (zeros when -1).
+ * d_off is a HOST array for lorb_compute_descriptor and a DEVICE array for the _dev variant. */
+int lorb_compute_descriptor(lorb_ctx* ctx, int32_t n_points, const int32_t* d_off,
+                            const uint8_t* desc, int32_t* best, uint8_t* out_desc);
+int lorb_compute_descriptor_dev(lorb_ctx* ctx, int32_t n_points, const int32_t* d_off,
+                                const uint8_t* d_desc, int32_t* d_best, uint8_t* d_out_desc);
+
 /* Rodrigues vector -> Tcw (float), cv::Rodrigues semantics (double internally). */
 void lorb_pose_to_Tcw(const float rvec[3], const float tvec[3], float Tcw[16]);
 

@@ -294,6 +294,57 @@ __global__ void k_counts_out(const double* __restrict__ ex, int np, int32_t* __r
   if (p < np) n_matches[p] = (int32_t)ex[np + p];
 }
 
+
+// MapPoint::ComputeDescriptor (src/map_point.cpp:69-129), one wavefront per map point: lane i
+// owns candidate descriptor i (rows i, i+64, ... for long lists).  The median of row i of the
+// all-pairs Hamming matrix (self-distance 0 included, element floor((n-1)/2) of the sorted row,
+// src/map_point.cpp:115-118) is found by a 9-step binary search over the value range [0, 256]
+// counting #{j : d(i, j) <= v}; the other candidates are wave-uniform loads (scalar cache).
+// The smallest median wins, first index on ties (strict '<', :119).
+__global__ __launch_bounds__(256) void k_compute_descriptor(const uint4* __restrict__ desc,
+                                                            const int32_t* __restrict__ d_off,
+                                                            int np, int32_t* __restrict__ best,
+                                                            uint4* __restrict__ out_desc) {
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= np) return;
+  const int lane = threadIdx.x & 63;
+  const int o0 = d_off[p], n = d_off[p + 1] - o0;
+  if (n <= 0) {
+    if (lane == 0) best[p] = -1;
+    return;
+  }
+  const int k = (n - 1) / 2;  // vDist[0.5 * (n - 1)]: the double index truncates
+  const uint4* __restrict__ D = desc + 2 * (size_t)o0;
+  unsigned long long bestkey = ~0ull;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const bool act = i < n;
+    const uint4 a0 = act ? D[2 * i] : make_uint4(0, 0, 0, 0), a1 = act ? D[2 * i + 1] : make_uint4(0, 0, 0, 0);
+    // the median is the smallest v in [0, 256] with #{j : d(i, j) <= v} > k (at most 9 steps)
+    int lo = 0, hi = act ? 256 : 0;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      int cnt = 0;
+      for (int j = 0; j < n; ++j) cnt += (int)(hamming256(a0, a1, D[2 * j], D[2 * j + 1]) <= (uint32_t)mid);
+      if (cnt > k) hi = mid;
+      else lo = mid + 1;
+    }
+    if (act) {
+      const unsigned long long key = ((unsigned long long)lo << 32) | (unsigned)i;
+      bestkey = key < bestkey ? key : bestkey;
+    }
+  }
+  // first index with the smallest median: min over (median, index)
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(bestkey, off, 64);
+    bestkey = o < bestkey ? o : bestkey;
+  }
+  const int bi = (int)(bestkey & 0xffffffffu);
+  if (lane == 0) best[p] = bi;
+  if (out_desc && lane < 2) out_desc[2 * (size_t)p + lane] = D[2 * bi + lane];
+}
+
 // Host: tile table for "lanes = L side, uniform = U side" with a fixed number of U chunks.
 int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_off, int lt,
                 std::vector<BfTile>& tiles, int* n_chunks_out, const int32_t* u_base = nullptr) {
@@ -513,6 +564,41 @@ int lorb_bf_match_sharded_dev(lorb_ctx* ctx, lorb_comm* comm, int32_t np, const 
   LORB_TRY(lorb::comm_allreduce(comm, ex + np, ex + np, (size_t)np, LORB_OP_SUM));
   hipLaunchKernelGGL(k_counts_out, dim3(lorb::ceil_div(np, 256)), dim3(256), 0, ctx->stream, ex, np, d_n_matches);
   LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
+int lorb_compute_descriptor_dev(lorb_ctx* ctx, int32_t n_points, const int32_t* d_off,
+                                const uint8_t* d_desc, int32_t* d_best, uint8_t* d_out_desc) {
+  if (!ctx || n_points < 0 || (n_points > 0 && (!d_off || !d_best))) return LORB_E_INVALID;
+  if (n_points == 0) return LORB_OK;
+  hipLaunchKernelGGL(k_compute_descriptor, dim3(lorb::ceil_div(n_points, 4)), dim3(256), 0, ctx->stream,
+                     reinterpret_cast<const uint4*>(d_desc), d_off, n_points, d_best,
+                     reinterpret_cast<uint4*>(d_out_desc));
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
+int lorb_compute_descriptor(lorb_ctx* ctx, int32_t n_points, const int32_t* d_off_h,
+                            const uint8_t* desc, int32_t* best, uint8_t* out_desc) {
+  if (!ctx || n_points < 0 || (n_points > 0 && (!d_off_h || !best))) return LORB_E_INVALID;
+  if (n_points == 0) return LORB_OK;
+  const int nd = d_off_h[n_points];
+  for (int p = 0; p < n_points; ++p)
+    if (d_off_h[p + 1] < d_off_h[p]) return lorb::set_error(ctx, LORB_E_INVALID, "offsets not monotone at point %d", p);
+  if (d_off_h[0] != 0) return lorb::set_error(ctx, LORB_E_INVALID, "offsets must start at 0");
+  int32_t *doff = nullptr, *dbest = nullptr;
+  uint8_t *dd = nullptr, *dout = nullptr;
+  LORB_TRY(lorb::upload_t(ctx, S_BF_OFF, d_off_h, (size_t)n_points + 1, &doff));
+  if (nd > 0) LORB_TRY(lorb::upload_t(ctx, S_BF_Q, desc, (size_t)nd * 32, &dd));
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT0, (size_t)n_points, &dbest));
+  if (out_desc) LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT1, (size_t)n_points * 32, &dout));
+  LORB_TRY(lorb_compute_descriptor_dev(ctx, n_points, doff, dd, dbest, dout));
+  LORB_HIP(ctx, hipMemcpyAsync(best, dbest, sizeof(int32_t) * n_points, hipMemcpyDeviceToHost, ctx->stream));
+  if (out_desc) LORB_HIP(ctx, hipMemcpyAsync(out_desc, dout, (size_t)n_points * 32, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (out_desc)  // points without candidates keep whatever the caller had: mark them unchanged
+    for (int p = 0; p < n_points; ++p)
+      if (best[p] < 0) memset(out_desc + 32 * (size_t)p, 0, 32);
   return LORB_OK;
 }
 

@@ -166,6 +166,22 @@ def _bf_match_sharded(self, comm, q_list, q_base, t_list):
 Context.bf_match_sharded = _bf_match_sharded
 
 
+def _compute_descriptor(self, d_off, desc):
+    """lorb_compute_descriptor: best candidate index per map point (-1: empty) + its descriptor."""
+    d_off = np.ascontiguousarray(d_off, np.int32)
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    n = len(d_off) - 1
+    best = np.zeros(max(n, 1), np.int32)
+    out = np.zeros((max(n, 1), 32), np.uint8)
+    self.check(lib().lorb_compute_descriptor(self._p, C.c_int32(n), A.ptr(d_off, C.c_int32),
+                                             A.ptr(desc if len(desc) else np.zeros((1, 32), np.uint8), C.c_uint8),
+                                             A.ptr(best, C.c_int32), A.ptr(out, C.c_uint8)), "lorb_compute_descriptor")
+    return best[:n], out[:n]
+
+
+Context.compute_descriptor = _compute_descriptor
+
+
 class DeviceArray:
     def __init__(self, ctx, ptr_, shape, dtype):
         self.ctx, self.ptr, self.shape, self.dtype = ctx, ptr_, tuple(shape), np.dtype(dtype)

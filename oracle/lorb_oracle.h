@@ -43,6 +43,9 @@ void or_bf_top2_mt(const uint8_t* q, int nq, const uint8_t* t, int nt, const int
                    int32_t* best_idx, int32_t* best_dist, int32_t* best_level,
                    int32_t* second_dist, int32_t* second_level, uint8_t* accepted, int threads);
 
+/* MapPoint::ComputeDescriptor, src/map_point.cpp:69-129, batched (CSR d_off); best -1 if empty */
+void or_compute_descriptor(int n_points, const int32_t* d_off, const uint8_t* desc, int32_t* best);
+
 /* Frame grid: src/frame.cpp:87-115 (AssignFeaturesToGrid / PosInGrid) and
  * GetFeaturesInArea src/frame.cpp:370-423.  Grid stored as CSR over cells, cell = ix*ROWS+iy. */
 typedef struct or_grid {

@@ -512,3 +512,33 @@ void or_pose_to_Tcw(const float rvec[3], const float tvec[3], float T[16]) {
   }
   T[12] = 0.0f; T[13] = 0.0f; T[14] = 0.0f; T[15] = 1.0f;
 }
+
+/* MapPoint::ComputeDescriptor, src/map_point.cpp:69-129: all-pairs distance matrix (:84-109),
+ * per row a sorted copy and its element 0.5*(n-1) truncated (:113-118), strict '<' on the
+ * median (:119).  Batched over points (CSR d_off); best = -1 for an empty list. */
+static int or_cmp_int(const void* a, const void* b) { return (*(const int*)a > *(const int*)b) - (*(const int*)a < *(const int*)b); }
+void or_compute_descriptor(int n_points, const int32_t* d_off, const uint8_t* desc, int32_t* best) {
+  for (int p = 0; p < n_points; p++) {
+    const int o0 = d_off[p], n = d_off[p + 1] - o0;
+    if (n <= 0) { best[p] = -1; continue; }
+    int* dist = (int*)malloc(sizeof(int) * (size_t)n * (size_t)n);
+    int* row = (int*)malloc(sizeof(int) * (size_t)n);
+    for (int i = 0; i < n; i++) {
+      dist[i * n + i] = 0;
+      for (int j = i + 1; j < n; j++) {
+        const int d = or_descriptor_distance(desc + 32 * (size_t)(o0 + i), desc + 32 * (size_t)(o0 + j));
+        dist[i * n + j] = d;
+        dist[j * n + i] = d;
+      }
+    }
+    int bestIdx = 0, bestMedian = 0x7fffffff;
+    for (int i = 0; i < n; i++) {
+      memcpy(row, dist + (size_t)i * n, sizeof(int) * (size_t)n);
+      qsort(row, (size_t)n, sizeof(int), or_cmp_int);
+      const int median = row[(size_t)(0.5 * (n - 1))];
+      if (median < bestMedian) { bestMedian = median; bestIdx = i; }
+    }
+    best[p] = bestIdx;
+    free(dist); free(row);
+  }
+}

@@ -220,3 +220,11 @@ def ba_local_sharded(shards, rank, allreduce, opt=None):
     summ = (A.BASummary * max(1, len(shards)))()
     lib().or_ba_local_sharded(C.c_int(len(shards)), arr, C.byref(opt), C.c_int(rank), cfn, None, pp, qp, summ)
     return poses, [p[: len(w["point_init"])] for p, w in zip(pts, shards)], [summ[i].as_dict() for i in range(len(shards))]
+
+
+def compute_descriptor(d_off, desc):
+    d_off = A.i32(d_off); desc = A.u8(desc).reshape(-1, 32)
+    n = len(d_off) - 1
+    best = np.empty(max(n, 1), np.int32)
+    lib().or_compute_descriptor(C.c_int(n), A.ptr(d_off, C.c_int32), A.ptr(desc, C.c_uint8), A.ptr(best, C.c_int32))
+    return best[:n]
