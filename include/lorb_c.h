@@ -223,6 +223,31 @@ int lorb_is_in_frustum(lorb_ctx* ctx, const lorb_frame_params* frame, const floa
                        uint8_t* in_view, float* proj_x, float* proj_y, float* proj_xr,
                        int32_t* pred_level, float* view_cos);
 
+/* device-resident local-map tracking -- VisualOdometry::EstimatePoseLocal's
+ * sequence (src/visual_odometry.cpp:173-201): IsInFrustum(MP, viewing_cos_limit) for every local
+ * map point that is neither already matched in the frame (mnLastFrameSeen == frame id) nor bad,
+ * then SearchByProjection(F, localMPs, th), with frame and map data resident on the device.
+ * All pointers below are DEVICE pointers (a lorb_keypoints whose arrays live on the device);
+ * frame / Tcw are host values.  Outputs: d_in_view (mbTrackInView), d_track (n x 4 as four
+ * planes: mTrackProjX, mTrackProjY, mTrackProjXR, mTrackViewCos), d_level (mnTrackScaleLevel),
+ * d_assign / d_nmatches as lorb_search_by_projection_local. */
+typedef struct lorb_map_points_dev {
+  int32_t n;
+  const float* pos;          /* GetPos(), n x 3 */
+  const float* normal;       /* mNormalVector, n x 3 */
+  const float* max_dist;     /* mfMaxDistance */
+  const float* min_dist;     /* mfMinDistance */
+  const uint8_t* desc;       /* GetDescriptor(), n x 32 */
+  const uint8_t* locked;     /* mnObs > 0 */
+  const uint8_t* is_bad;     /* IsBad() (NULL => none) */
+  const uint8_t* in_frame;   /* mnLastFrameSeen == frame id (NULL => none) */
+} lorb_map_points_dev;
+int lorb_track_local_map_dev(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
+                             const lorb_keypoints* d_kps, const uint8_t* d_slot_state,
+                             const lorb_map_points_dev* pts, float viewing_cos_limit, float th,
+                             uint8_t* d_in_view, float* d_track, int32_t* d_level,
+                             int32_t* d_assign, int32_t* d_nmatches);
+
 /* (a20) Frame::UnprojectStereo, src/frame.cpp:335-356, batched over keypoints. */
 int lorb_unproject_stereo(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
                           int32_t n, const float* x, const float* y, const float* depth,

@@ -58,6 +58,17 @@ class FrustumPoints(C.Structure):
                 ("min_dist", f32p)]
 
 
+class MapPointsDev(C.Structure):
+    _fields_ = [("n", C.c_int32), ("pos", C.c_void_p), ("normal", C.c_void_p), ("max_dist", C.c_void_p),
+                ("min_dist", C.c_void_p), ("desc", C.c_void_p), ("locked", C.c_void_p), ("is_bad", C.c_void_p),
+                ("in_frame", C.c_void_p)]
+
+
+class KeypointsDev(C.Structure):  # lorb_keypoints with device pointers
+    _fields_ = [("n", C.c_int32), ("x", C.c_void_p), ("y", C.c_void_p), ("octave", C.c_void_p),
+                ("angle", C.c_void_p), ("u_right", C.c_void_p), ("desc", C.c_void_p)]
+
+
 class LMOptions(C.Structure):
     _fields_ = [("max_num_iterations", C.c_int32), ("function_tolerance", C.c_double),
                 ("gradient_tolerance", C.c_double), ("parameter_tolerance", C.c_double),

@@ -358,10 +358,15 @@ __global__ __launch_bounds__(256) void k_frustum(lorb_frame_params fp, const flo
                                                  float cos_limit, uint8_t* __restrict__ in_view,
                                                  float* __restrict__ ox, float* __restrict__ oy,
                                                  float* __restrict__ oxr, int* __restrict__ olev,
-                                                 float* __restrict__ ocos) {
+                                                 float* __restrict__ ocos,
+                                                 const uint8_t* __restrict__ skip_a,
+                                                 const uint8_t* __restrict__ skip_b) {
   const int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= n) return;
   in_view[m] = 0;
+  // EstimatePoseLocal skips points already matched in the frame and bad points before calling
+  // IsInFrustum (src/visual_odometry.cpp:181-184); they leave tracking with mbTrackInView false
+  if ((skip_a && skip_a[m]) || (skip_b && skip_b[m])) return;
   const float P0 = pos[3 * m], P1 = pos[3 * m + 1], P2 = pos[3 * m + 2];
   float Pc[3];
 #pragma unroll
@@ -634,7 +639,8 @@ int lorb_is_in_frustum(lorb_ctx* ctx, const lorb_frame_params* frame, const floa
   LORB_TRY(lorb::scratch_t(ctx, S_W7, (size_t)n, &iv));
   LORB_TRY(lorb::scratch_t(ctx, S_W8, (size_t)n, &lev));
   hipLaunchKernelGGL(k_frustum, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, *frame, dT, dO, n, pos, nrm, mx,
-                     mn, viewing_cos_limit, iv, outf, outf + n, outf + 2 * n, lev, outf + 3 * n);
+                     mn, viewing_cos_limit, iv, outf, outf + n, outf + 2 * n, lev, outf + 3 * n,
+                     (const uint8_t*)nullptr, (const uint8_t*)nullptr);
   LORB_CHECK_LAUNCH(ctx);
   LORB_HIP(ctx, hipMemcpyAsync(in_view, iv, n, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, hipMemcpyAsync(proj_x, outf, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
@@ -643,6 +649,84 @@ int lorb_is_in_frustum(lorb_ctx* ctx, const lorb_frame_params* frame, const floa
   LORB_HIP(ctx, hipMemcpyAsync(view_cos, outf + 3 * n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, hipMemcpyAsync(pred_level, lev, sizeof(int) * n, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+// the tracking sequence of VisualOdometry::EstimatePoseLocal
+// (src/visual_odometry.cpp:173-201) on device-resident frame and map data: IsInFrustum for every
+// local map point not already in the frame and not bad, then SearchByProjection(F, localMPs, th).
+int lorb_track_local_map_dev(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
+                             const lorb_keypoints* d_kps, const uint8_t* d_slot_state,
+                             const lorb_map_points_dev* pts, float viewing_cos_limit, float th,
+                             uint8_t* d_in_view, float* d_track, int32_t* d_level,
+                             int32_t* d_assign, int32_t* d_nmatches) {
+  if (!ctx || !frame || !Tcw || !d_kps || !pts || !d_in_view || !d_track || !d_level || !d_assign || !d_nmatches)
+    return LORB_E_INVALID;
+  const int nk = d_kps->n, np = pts->n;
+  if (nk < 0 || np < 0) return lorb::set_error(ctx, LORB_E_INVALID, "negative sizes");
+  if (frame->n_levels < 1 || frame->n_levels > LORB_MAX_LEVELS)
+    return lorb::set_error(ctx, LORB_E_INVALID, "n_levels %d out of range", frame->n_levels);
+  float Twc[16];
+  inv4_lu32f(Tcw, Twc);
+  const float TO[19] = {Tcw[0], Tcw[1], Tcw[2], Tcw[3], Tcw[4], Tcw[5], Tcw[6], Tcw[7], Tcw[8], Tcw[9],
+                        Tcw[10], Tcw[11], Tcw[12], Tcw[13], Tcw[14], Tcw[15], Twc[3], Twc[7], Twc[11]};
+  float* dTO;
+  LORB_TRY(lorb::upload_t(ctx, S_WX + 7, TO, 19, &dTO));
+  if (np > 0)
+    hipLaunchKernelGGL(k_frustum, dim3(lorb::ceil_div(np, 256)), dim3(256), 0, ctx->stream, *frame, dTO, dTO + 16, np,
+                       pts->pos, pts->normal, pts->max_dist, pts->min_dist, viewing_cos_limit, d_in_view, d_track,
+                       d_track + np, d_track + 2 * np, d_level, d_track + 3 * np, pts->in_frame, pts->is_bad);
+  if (nk == 0) {
+    LORB_HIP(ctx, hipMemsetAsync(d_nmatches, 0, sizeof(int32_t), ctx->stream));
+    LORB_CHECK_LAUNCH(ctx);
+    return LORB_OK;
+  }
+  // keypoint grid of the frame, from the device keypoints (src/frame.cpp:87-115)
+  KpDev K;
+  int *cell_off, *cell_idx, *kp_cell;
+  LORB_TRY(lorb::scratch_t(ctx, S_KP + 7, kCells + 1, &cell_off));
+  LORB_TRY(lorb::scratch_t(ctx, S_KP + 8, (size_t)nk, &cell_idx));
+  LORB_TRY(lorb::scratch_t(ctx, S_KP + 9, (size_t)nk, &kp_cell));
+  hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, ctx->stream, d_kps->x, d_kps->y, nk, *frame, cell_off, cell_idx,
+                     kp_cell);
+  uint8_t* ss = const_cast<uint8_t*>(d_slot_state);
+  if (!ss) {
+    LORB_TRY(lorb::scratch_t(ctx, S_KP + 6, (size_t)nk, &ss));
+    LORB_HIP(ctx, hipMemsetAsync(ss, 0, nk, ctx->stream));
+  }
+  K.x = d_kps->x; K.y = d_kps->y; K.angle = d_kps->angle; K.uR = d_kps->u_right; K.octave = d_kps->octave;
+  K.desc = reinterpret_cast<const uint4*>(d_kps->desc); K.slot_state = ss;
+  K.cell_off = cell_off; K.cell_idx = cell_idx; K.n = nk;
+  WinParams P{};
+  P.fp = *frame;
+  P.th = th;
+  int *cnt, *off, *res, *claim;
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 0, (size_t)np + 1, &cnt));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 1, (size_t)np + 1, &off));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 2, (size_t)np + 1, &res));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 3, (size_t)nk + 1, &claim));
+  const unsigned g = lorb::ceil_div(std::max(np, 1), 256);
+  const float* tx = d_track;
+  if (np > 0) {
+    lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
+    hipLaunchKernelGGL(k_cand_local<false>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, d_in_view, pts->is_bad, tx,
+                       tx + np, tx + 2 * np, d_level, tx + 3 * np, reinterpret_cast<const uint4*>(pts->desc), cnt,
+                       (const int*)nullptr, (int2*)nullptr);
+  }
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, np, off);
+  int total = 0;  // candidate-list size: the one device -> host word of the call
+  LORB_HIP(ctx, hipMemcpyAsync(&total, off + np, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  int2* cand;
+  LORB_TRY(lorb::scratch_t(ctx, S_W9, (size_t)std::max(total, 1), &cand));
+  if (np > 0)
+    hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, d_in_view, pts->is_bad, tx,
+                       tx + np, tx + 2 * np, d_level, tx + 3 * np, reinterpret_cast<const uint4*>(pts->desc), cnt, off,
+                       cand);
+  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), 0, ctx->stream, np, nk, off, cand, K.octave, K.slot_state,
+                     pts->locked, (const float*)nullptr, (const float*)nullptr, res, claim, d_assign, (int*)nullptr,
+                     (int*)nullptr, d_nmatches);
+  LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
 }
 

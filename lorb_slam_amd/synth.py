@@ -282,3 +282,53 @@ def local_mapping_step(seed=4, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf
     Tcw = Tcw_from(last[:3], last[3:])
     return dict(window=win, mp_desc=mp_desc, kf_desc=kf_desc, kf_x=x, kf_y=y, kf_depth=depth, kf_Tcw=Tcw,
                 reobs_slot=slots, reobs_point=re)
+
+
+def local_map_problem(seed=7, n_kps=2000, n_pts=3000, n_true=1200, n_in_frame=150, bad_frac=0.01):
+    """VisualOdometry::EstimatePoseLocal inputs (SURVEY §8f row 1): a frame with n_kps keypoints
+    and n_pts local map points (position, mean viewing normal, scale-invariance distances,
+    descriptor, mnObs>0 flag, bad flag, already-matched-in-frame flag); n_true points re-observe a
+    keypoint at their projection (bit-flipped descriptor, octave at the predicted level)."""
+    rng = np.random.default_rng(seed)
+    fp = frame_params()
+    T = Tcw_from([0.01, -0.02, 0.005], [0.1, -0.05, 0.2])
+    R, t = T[:3, :3].astype(np.float64), T[:3, 3].astype(np.float64)
+    Ow = -R.T @ t
+    x = rng.uniform(0, W, n_kps).astype(np.float32)
+    y = rng.uniform(0, H, n_kps).astype(np.float32)
+    octv = rng.choice(N_LEVELS, size=n_kps, p=level_probs()).astype(np.int32)
+    ang = rng.uniform(0, 360, n_kps).astype(np.float32)
+    desc = random_desc(rng, n_kps)
+    uR = np.full(n_kps, -1.0, np.float32)
+    # map points: mostly in front of the camera, some behind / outside the image
+    Xc = np.stack([rng.uniform(-6, 6, n_pts), rng.uniform(-4, 4, n_pts), rng.uniform(-1, 15, n_pts)], 1)
+    pos = ((Xc - t) @ R).astype(np.float32)  # world = R^T (Xc - t)
+    dist = np.linalg.norm(pos.astype(np.float64) - Ow, axis=1)
+    nrm = (pos - Ow) / np.maximum(dist[:, None], 1e-9)
+    nrm = (nrm + rng.normal(0, 0.3, nrm.shape) * (rng.uniform(size=(n_pts, 1)) < 0.2)).astype(np.float32)
+    maxd = (dist * rng.uniform(1.0, 3.0, n_pts)).astype(np.float32)
+    mind = (maxd / np.float32(SCALE ** (N_LEVELS - 1))).astype(np.float32)
+    pdesc = random_desc(rng, n_pts)
+    # planted re-observations of in-view points
+    front = np.where(Xc[:, 2] > 0.5)[0]
+    uv = np.stack([FX * Xc[:, 0] / Xc[:, 2] + CX, FY * Xc[:, 1] / Xc[:, 2] + CY], 1)
+    inimg = front[(uv[front, 0] > 1) & (uv[front, 0] < W - 1) & (uv[front, 1] > 1) & (uv[front, 1] < H - 1)]
+    tp = rng.choice(inimg, size=min(n_true, len(inimg)), replace=False)
+    tk = rng.choice(n_kps, size=len(tp), replace=False)
+    x[tk] = (uv[tp, 0] + rng.normal(0, 0.7, len(tp))).astype(np.float32)
+    y[tk] = (uv[tp, 1] + rng.normal(0, 0.7, len(tp))).astype(np.float32)
+    lev = np.clip(np.ceil(np.log(maxd[tp] / dist[tp]) / math.log(SCALE)), 0, N_LEVELS - 1).astype(np.int32)
+    octv[tk] = np.clip(lev - rng.integers(0, 2, len(tp)), 0, N_LEVELS - 1)
+    desc[tk] = flip_bits(rng, pdesc[tp], 20)
+    st = rng.uniform(size=n_kps) < 0.5
+    uR[st] = (x[st] - rng.uniform(3, 20, st.sum())).astype(np.float32)
+    in_frame = np.zeros(n_pts, np.uint8)
+    in_frame[rng.choice(n_pts, size=n_in_frame, replace=False)] = 1
+    slot_state = np.zeros(n_kps, np.uint8)
+    pf = rng.choice(n_kps, size=100, replace=False)
+    slot_state[pf] = rng.integers(1, 3, size=100).astype(np.uint8)
+    pts = dict(pos=pos, normal=nrm, max_dist=maxd, min_dist=mind, desc=pdesc,
+               locked=(rng.uniform(size=n_pts) < 0.8).astype(np.uint8),
+               is_bad=(rng.uniform(size=n_pts) < bad_frac).astype(np.uint8), in_frame=in_frame)
+    kps = dict(x=x, y=y, octave=octv, angle=ang, u_right=uR, desc=desc)
+    return dict(fp=fp, Tcw=T, kps=kps, slot_state=slot_state, pts=pts)

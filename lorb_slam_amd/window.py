@@ -64,6 +64,41 @@ def _unproject_stereo(self, fp, Tcw, x, y, depth):
     return out[: len(x)]
 
 
+def _track_local_map(self, fp, Tcw, kps, slot_state, pts, cos_limit=0.5, th=1.0):
+    """lorb_track_local_map_dev on device copies of the inputs (they stay resident for the call)."""
+    keep = []
+
+    def dev(a, dtype):
+        d = self.to_device(np.ascontiguousarray(a, dtype))
+        keep.append(d)
+        return d.ptr
+
+    nk, npt = len(kps["x"]), len(pts["max_dist"])
+    k = A.KeypointsDev(nk, dev(kps["x"], np.float32), dev(kps["y"], np.float32), dev(kps["octave"], np.int32),
+                       dev(kps["angle"], np.float32),
+                       dev(kps["u_right"], np.float32) if kps.get("u_right") is not None else None,
+                       dev(kps["desc"], np.uint8))
+    m = A.MapPointsDev(npt, dev(pts["pos"], np.float32), dev(pts["normal"], np.float32), dev(pts["max_dist"], np.float32),
+                       dev(pts["min_dist"], np.float32), dev(pts["desc"], np.uint8), dev(pts["locked"], np.uint8),
+                       dev(pts["is_bad"], np.uint8) if pts.get("is_bad") is not None else None,
+                       dev(pts["in_frame"], np.uint8) if pts.get("in_frame") is not None else None)
+    ss = dev(slot_state, np.uint8) if slot_state is not None else None
+    iv, tr, lv = self.empty(max(npt, 1), np.uint8), self.empty((4, max(npt, 1)), np.float32), self.empty(max(npt, 1), np.int32)
+    asg, nm = self.empty(max(nk, 1), np.int32), self.empty(1, np.int32)
+    fps = A.make_frame_params(fp)
+    T = A.f32(Tcw).reshape(16)
+    self.check(lib().lorb_track_local_map_dev(self._p, C.byref(fps), A.ptr(T, C.c_float), C.byref(k), ss, C.byref(m),
+                                              C.c_float(cos_limit), C.c_float(th), iv.ptr, tr.ptr, lv.ptr, asg.ptr, nm.ptr),
+               "lorb_track_local_map_dev")
+    trk = tr.numpy().reshape(4, -1)[:, :npt] if npt else np.zeros((4, 0), np.float32)
+    out = dict(in_view=iv.numpy()[:npt], proj_x=trk[0], proj_y=trk[1], proj_xr=trk[2], view_cos=trk[3],
+               pred_level=lv.numpy()[:npt], assign=asg.numpy()[:nk], nmatches=int(nm.numpy()[0]))
+    for a in keep + [iv, tr, lv, asg, nm]:
+        a.free()
+    return out
+
+
+Context.track_local_map = _track_local_map
 Context.search_by_projection_frame = _search_by_projection_frame
 Context.search_by_projection_local = _search_by_projection_local
 Context.is_in_frustum = _is_in_frustum

@@ -228,3 +228,25 @@ def compute_descriptor(d_off, desc):
     best = np.empty(max(n, 1), np.int32)
     lib().or_compute_descriptor(C.c_int(n), A.ptr(d_off, C.c_int32), A.ptr(desc, C.c_uint8), A.ptr(best, C.c_int32))
     return best[:n]
+
+
+def track_local_map(fp, Tcw, kps, slot_state, pts, cos_limit=0.5, th=1.0):
+    """The sequence of VisualOdometry::EstimatePoseLocal, src/visual_odometry.cpp:173-201: skip points
+    already matched in the frame (mnLastFrameSeen == id, whose mbTrackInView was cleared at :168) and
+    bad points, IsInFrustum(pMP, 0.5) for the rest, then SearchByProjection(F, localMPs, th).  A bad
+    point keeps a stale mbTrackInView in the reference; SearchByProjection skips it for IsBad() first
+    (src/matcher.cpp:229-236), so in_view = 0 is equivalent."""
+    n = len(pts["max_dist"])
+    fr = is_in_frustum(fp, Tcw, pts, cos_limit)
+    skip = np.zeros(n, bool)
+    for k in ("in_frame", "is_bad"):
+        if pts.get(k) is not None:
+            skip |= np.asarray(pts[k]).astype(bool)
+    fr["in_view"] = np.where(skip, 0, fr["in_view"]).astype(np.uint8)
+    lp = dict(track_in_view=fr["in_view"], is_bad=pts.get("is_bad"), locked=pts["locked"], proj_x=fr["proj_x"],
+              proj_y=fr["proj_y"], proj_xr=fr["proj_xr"], pred_level=fr["pred_level"], view_cos=fr["view_cos"],
+              desc=pts["desc"])
+    if int(fr["in_view"].sum()) == 0:  # nToMatch == 0: no search (src/visual_odometry.cpp:197-201)
+        return fr, np.full(len(kps["x"]), -1, np.int32), 0
+    assign, nm = search_by_projection_local(fp, kps, slot_state, lp, th)
+    return fr, assign, nm

@@ -85,3 +85,42 @@ def test_unproject_stereo(ctx):
     x = rng.uniform(0, 752, n).astype(np.float32); y = rng.uniform(0, 480, n).astype(np.float32)
     d = rng.uniform(-1, 12, n).astype(np.float32)
     assert np.array_equal(ctx.unproject_stereo(fp, T, x, y, d), O.unproject_stereo(fp, T, x, y, d))
+
+
+@pytest.mark.parametrize("seed,cos_limit,th", [(11, 0.5, 1.0), (12, 0.5, 3.0), (13, 0.8, 1.0)])
+def test_track_local_map(ctx, seed, cos_limit, th):
+    """lorb_track_local_map_dev vs the oracle chain of EstimatePoseLocal
+    (src/visual_odometry.cpp:173-201) -- tracking fields and assignments bit-exact."""
+    pr = synth.local_map_problem(seed=seed, bad_frac=0.02)
+    g = ctx.track_local_map(pr["fp"], pr["Tcw"], pr["kps"], pr["slot_state"], pr["pts"], cos_limit, th)
+    fr, assign, nm = O.track_local_map(pr["fp"], pr["Tcw"], pr["kps"], pr["slot_state"], pr["pts"], cos_limit, th)
+    assert np.array_equal(g["in_view"], fr["in_view"])
+    m = fr["in_view"].astype(bool)
+    assert m.sum() > 500
+    for k in ("proj_x", "proj_y", "proj_xr", "view_cos", "pred_level"):
+        assert np.array_equal(g[k][m], fr[k][m]), k
+    assert g["nmatches"] == nm and nm > 100
+    assert np.array_equal(g["assign"], assign)
+
+
+def test_track_local_map_edges(ctx):
+    pr = synth.local_map_problem(seed=14, n_kps=300, n_pts=400, n_true=100)
+    fp, T, kps, pts = pr["fp"], pr["Tcw"], pr["kps"], pr["pts"]
+    # every point already matched in the frame: nothing in view, no search, nothing assigned
+    allin = dict(pts, in_frame=np.ones(400, np.uint8))
+    g = ctx.track_local_map(fp, T, kps, None, allin)
+    assert g["in_view"].sum() == 0 and g["nmatches"] == 0 and (g["assign"] == -1).all()
+    # no map points at all
+    empty = {k: v[:0] for k, v in pts.items()}
+    g = ctx.track_local_map(fp, T, kps, None, empty)
+    assert g["nmatches"] == 0 and (g["assign"] == -1).all()
+    # no keypoints: tracking fields still computed
+    nok = {k: v[:0] for k, v in kps.items()}
+    g = ctx.track_local_map(fp, T, nok, None, pts)
+    fr, _, _ = O.track_local_map(fp, T, kps, None, pts)
+    assert g["nmatches"] == 0 and np.array_equal(g["in_view"], fr["in_view"])
+    # no skip masks (NULL pointers)
+    bare = dict(pts, in_frame=None, is_bad=None)
+    g = ctx.track_local_map(fp, T, kps, pr["slot_state"], bare)
+    fr, assign, nm = O.track_local_map(fp, T, kps, pr["slot_state"], bare)
+    assert g["nmatches"] == nm and np.array_equal(g["assign"], assign)

@@ -47,3 +47,15 @@ def test_inv4_and_unproject():
     Xc = T.astype(np.float64) @ np.array([*out[0], 1.0])   # back into the camera frame
     assert abs(Xc[2] - 2.0) < 1e-5
     assert abs(Xc[0] - (100.0 - fp["cx"]) * 2.0 / fp["fx"]) < 1e-4
+
+
+def test_track_local_map_oracle_chain():
+    """The EstimatePoseLocal chain (frustum → skip mask → local search) on the synthetic local map is
+    non-trivial: many points in view, skipped points masked, many matches."""
+    pr = synth.local_map_problem(seed=11)
+    fr, assign, nm = O.track_local_map(pr["fp"], pr["Tcw"], pr["kps"], pr["slot_state"], pr["pts"], 0.5, 1.0)
+    skip = pr["pts"]["in_frame"].astype(bool) | pr["pts"]["is_bad"].astype(bool)
+    assert fr["in_view"][skip].sum() == 0
+    assert fr["in_view"].sum() > 1000
+    assert nm > 300
+    assert (assign >= 0).sum() == nm
