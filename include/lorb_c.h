@@ -84,6 +84,7 @@ int lorb_timer_elapsed_ms(lorb_ctx* ctx, int slot_begin, int slot_end, float* ms
 #define LORB_K_BA_LINEARIZE 3
 #define LORB_K_BA_CHOLESKY  4
 #define LORB_K_WINDOW_CAND  5
+#define LORB_K_STEREO       6
 #define LORB_K_COUNT        8
 int lorb_kernel_timing_enable(lorb_ctx* ctx, int enable);
 /* sums (and resets) the recorded launches of kernel id k: total ms and launch count */
@@ -256,6 +257,38 @@ int lorb_unproject_stereo(lorb_ctx* ctx, const lorb_frame_params* frame, const f
 int lorb_unproject_stereo_dev(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
                               int32_t n, const float* d_x, const float* d_y, const float* d_depth,
                               float* d_out_xyz);
+
+/* Frame::ComputeStereoMatches, src/frame.cpp:125-333 -- per left keypoint the
+ * best right keypoint in its row band (Hamming < (TH_HIGH+TH_LOW)/2, octave within +-1, disparity in
+ * [0, bf/b]), 11x11 SAD refinement over +-5 columns on the keypoint's pyramid level, parabola
+ * sub-pixel fit, and the 2.1 x median SAD outlier rejection.  One image pyramid per camera
+ * (ORBextractor::mvImagePyramid): level l is rows[l] x cols[l] u8 pixels at data + offset[l],
+ * step[l] bytes per row. */
+typedef struct lorb_image_pyramid {
+  int32_t n_levels;
+  const uint8_t* data;
+  int64_t offset[LORB_MAX_LEVELS];
+  int32_t rows[LORB_MAX_LEVELS], cols[LORB_MAX_LEVELS], step[LORB_MAX_LEVELS];
+} lorb_image_pyramid;
+/* SoA view of one camera's distorted keypoints (Frame::mvKeys / mvKeysRight) + descriptors */
+typedef struct lorb_stereo_keys {
+  int32_t n;
+  const float* x;            /* kp.pt.x */
+  const float* y;            /* kp.pt.y */
+  const int32_t* octave;     /* kp.octave */
+  const uint8_t* desc;       /* mDescriptors / mDescriptorsRight, n x 32 */
+} lorb_stereo_keys;
+/* Outputs mvuRight / mvDepth (n_left floats each, -1 where no depth).  Host pointers. */
+int lorb_compute_stereo_matches(lorb_ctx* ctx, const lorb_frame_params* frame,
+                                const lorb_stereo_keys* left, const lorb_stereo_keys* right,
+                                const lorb_image_pyramid* left_pyr, const lorb_image_pyramid* right_pyr,
+                                float* u_right, float* depth);
+/* device-pointer variant: every array (keys, pyramid data, outputs) lives on the device; the structs
+ * themselves and frame are host values.  Async on the ctx stream. */
+int lorb_compute_stereo_matches_dev(lorb_ctx* ctx, const lorb_frame_params* frame,
+                                    const lorb_stereo_keys* d_left, const lorb_stereo_keys* d_right,
+                                    const lorb_image_pyramid* d_left_pyr, const lorb_image_pyramid* d_right_pyr,
+                                    float* d_u_right, float* d_depth);
 
 /* ----------------------------------------------------------------------------------------
  * Bundle adjustment: Ceres-default Levenberg-Marquardt + DENSE_SCHUR restated

@@ -58,6 +58,38 @@ class FrustumPoints(C.Structure):
                 ("min_dist", f32p)]
 
 
+class ImagePyramid(C.Structure):
+    _fields_ = [("n_levels", C.c_int32), ("data", C.c_void_p), ("offset", C.c_int64 * LORB_MAX_LEVELS),
+                ("rows", C.c_int32 * LORB_MAX_LEVELS), ("cols", C.c_int32 * LORB_MAX_LEVELS),
+                ("step", C.c_int32 * LORB_MAX_LEVELS)]
+
+
+class StereoKeys(C.Structure):
+    _fields_ = [("n", C.c_int32), ("x", C.c_void_p), ("y", C.c_void_p), ("octave", C.c_void_p), ("desc", C.c_void_p)]
+
+
+def pack_pyramid(levels):
+    """list of 2-D uint8 images -> (one contiguous byte buffer, ImagePyramid with data=None)."""
+    p = ImagePyramid()
+    p.n_levels = len(levels)
+    off = 0
+    for l, im in enumerate(levels):
+        p.offset[l], p.rows[l], p.cols[l], p.step[l] = off, im.shape[0], im.shape[1], im.shape[1]
+        off += im.size
+    buf = np.concatenate([np.ascontiguousarray(im, np.uint8).reshape(-1) for im in levels]) if levels else np.zeros(1, np.uint8)
+    return buf, p
+
+
+def make_stereo_keys(k, keep):
+    s = StereoKeys()
+    s.n = int(len(k["x"]))
+    s.x = keep.keep(f32(k["x"])).ctypes.data
+    s.y = keep.keep(f32(k["y"])).ctypes.data
+    s.octave = keep.keep(i32(k["octave"])).ctypes.data
+    s.desc = keep.keep(u8(k["desc"])).ctypes.data
+    return s
+
+
 class MapPointsDev(C.Structure):
     _fields_ = [("n", C.c_int32), ("pos", C.c_void_p), ("normal", C.c_void_p), ("max_dist", C.c_void_p),
                 ("min_dist", C.c_void_p), ("desc", C.c_void_p), ("locked", C.c_void_p), ("is_bad", C.c_void_p),

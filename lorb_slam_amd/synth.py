@@ -332,3 +332,59 @@ def local_map_problem(seed=7, n_kps=2000, n_pts=3000, n_true=1200, n_in_frame=15
                is_bad=(rng.uniform(size=n_pts) < bad_frac).astype(np.uint8), in_frame=in_frame)
     kps = dict(x=x, y=y, octave=octv, angle=ang, u_right=uR, desc=desc)
     return dict(fp=fp, Tcw=T, kps=kps, slot_state=slot_state, pts=pts)
+
+
+def _bilinear(img, x, y):
+    h, w = img.shape
+    x = np.clip(x, 0, w - 1.001); y = np.clip(y, 0, h - 1.001)
+    x0 = np.floor(x).astype(np.int64); y0 = np.floor(y).astype(np.int64)
+    fx, fy = x - x0, y - y0
+    a = img[y0, x0] * (1 - fx) + img[y0, x0 + 1] * fx
+    b = img[y0 + 1, x0] * (1 - fx) + img[y0 + 1, x0 + 1] * fx
+    return a * (1 - fy) + b * fy
+
+
+def stereo_problem(seed=21, n_left=2000, n_distract=800, frac_true=0.75, width=W, height=H, border=24):
+    """Frame::ComputeStereoMatches inputs (SURVEY §8f row 2): a textured scene seen by a rectified pair
+    with a smooth disparity field D(x, y) (level-0 pixels), both image pyramids (level l samples the
+    scene at scale_factors[l]; right(x, y) = left(x + D, y)), left keypoints with descriptors and
+    right keypoints at (x - D, y) + noise with bit-flipped descriptors, plus distractors."""
+    rng = np.random.default_rng(seed)
+    sf = scale_factors()
+    noise = rng.normal(0, 1, (height + 8, width + 80))
+    k = np.exp(-0.5 * (np.arange(-4, 5) / 1.4) ** 2); k /= k.sum()
+    tex = np.apply_along_axis(lambda r: np.convolve(r, k, "same"), 1, noise)
+    tex = np.apply_along_axis(lambda c: np.convolve(c, k, "same"), 0, tex)
+    tex = (tex - tex.min()) / (tex.max() - tex.min()) * 255.0
+
+    def disp(x, y):
+        return 25.0 + 12.0 * np.sin(x / 90.0) + 8.0 * np.cos(y / 70.0)
+
+    pyr_l, pyr_r = [], []
+    for l in range(N_LEVELS):
+        s = float(sf[l])
+        h, w = int(round(height / s)), int(round(width / s))
+        yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+        X, Y = xx * s + 40.0, yy * s + 4.0
+        pyr_l.append(np.clip(np.round(_bilinear(tex, X, Y)), 0, 255).astype(np.uint8))
+        pyr_r.append(np.clip(np.round(_bilinear(tex, X + disp(xx * s, yy * s), Y)), 0, 255).astype(np.uint8))
+    octv = rng.choice(N_LEVELS, size=n_left, p=level_probs()).astype(np.int32)
+    bx = border * sf[octv]
+    x = rng.uniform(bx + 40, width - bx).astype(np.float32)
+    y = rng.uniform(bx, height - bx).astype(np.float32)
+    desc = random_desc(rng, n_left)
+    nt = int(n_left * frac_true)
+    d = disp(x[:nt].astype(np.float64), y[:nt].astype(np.float64))
+    rx = (x[:nt] - d + rng.normal(0, 0.4, nt)).astype(np.float32)
+    ry = (y[:nt] + rng.normal(0, 0.6, nt)).astype(np.float32)
+    ro = np.clip(octv[:nt] + rng.choice([-1, 0, 0, 0, 1], nt), 0, N_LEVELS - 1).astype(np.int32)
+    rdesc = flip_bits(rng, desc[:nt], 30)
+    dox = rng.choice(N_LEVELS, size=n_distract, p=level_probs()).astype(np.int32)
+    dbx = border * sf[dox]
+    right = dict(x=np.concatenate([rx, rng.uniform(dbx, width - dbx).astype(np.float32)]),
+                 y=np.concatenate([ry, rng.uniform(dbx, height - dbx).astype(np.float32)]),
+                 octave=np.concatenate([ro, dox]), desc=np.concatenate([rdesc, random_desc(rng, n_distract)]))
+    perm = rng.permutation(len(right["x"]))
+    right = {k_: v[perm] for k_, v in right.items()}
+    left = dict(x=x, y=y, octave=octv, desc=desc)
+    return dict(fp=frame_params(width=width, height=height), left=left, right=right, pyr_l=pyr_l, pyr_r=pyr_r)

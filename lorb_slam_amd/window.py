@@ -98,6 +98,46 @@ def _track_local_map(self, fp, Tcw, kps, slot_state, pts, cos_limit=0.5, th=1.0)
     return out
 
 
+def _compute_stereo_matches(self, fp, left, right, pyr_l, pyr_r, device_resident=False):
+    """Frame::ComputeStereoMatches -> (u_right, depth).  device_resident=True stages every input in
+    device memory first and calls lorb_compute_stereo_matches_dev (the async form)."""
+    fps = A.make_frame_params(fp)
+    n = len(left["x"])
+    bl, pl = A.pack_pyramid(pyr_l)
+    br, pr = A.pack_pyramid(pyr_r)
+    if not device_resident:
+        keep = A.KeepAlive()
+        kl, kr = A.make_stereo_keys(left, keep), A.make_stereo_keys(right, keep)
+        pl.data, pr.data = bl.ctypes.data, br.ctypes.data
+        ur, dp = np.empty(max(n, 1), np.float32), np.empty(max(n, 1), np.float32)
+        self.check(lib().lorb_compute_stereo_matches(self._p, C.byref(fps), C.byref(kl), C.byref(kr), C.byref(pl),
+                                                     C.byref(pr), A.ptr(ur, C.c_float), A.ptr(dp, C.c_float)),
+                   "lorb_compute_stereo_matches")
+        return ur[:n].copy(), dp[:n].copy()
+    keep = []
+
+    def dev(a, dtype):
+        d = self.to_device(np.ascontiguousarray(a, dtype))
+        keep.append(d)
+        return d.ptr
+
+    def keys(k):
+        return A.StereoKeys(len(k["x"]), dev(k["x"], np.float32), dev(k["y"], np.float32), dev(k["octave"], np.int32),
+                            dev(k["desc"], np.uint8))
+
+    kl, kr = keys(left), keys(right)
+    pl.data, pr.data = dev(bl, np.uint8), dev(br, np.uint8)
+    ur, dp = self.empty(max(n, 1), np.float32), self.empty(max(n, 1), np.float32)
+    keep += [ur, dp]
+    self.check(lib().lorb_compute_stereo_matches_dev(self._p, C.byref(fps), C.byref(kl), C.byref(kr), C.byref(pl),
+                                                     C.byref(pr), ur.ptr, dp.ptr), "lorb_compute_stereo_matches_dev")
+    out = ur.numpy()[:n], dp.numpy()[:n]
+    for a in keep:
+        a.free()
+    return out
+
+
+Context.compute_stereo_matches = _compute_stereo_matches
 Context.track_local_map = _track_local_map
 Context.search_by_projection_frame = _search_by_projection_frame
 Context.search_by_projection_local = _search_by_projection_local

@@ -100,6 +100,11 @@ void or_residual_jet(int kind, const double* X, const double* pose, double fx, d
 /* AngleAxisRotatePoint (ceres/rotation.h) in double */
 void or_angle_axis_rotate_point(const double aa[3], const double pt[3], double out[3]);
 
+/* src/frame.cpp:125-333 (stereo.c).  Returns the number of pairs before the median rejection. */
+int or_compute_stereo_matches(const lorb_frame_params* fp, const lorb_stereo_keys* L, const lorb_stereo_keys* R,
+                              const lorb_image_pyramid* PL, const lorb_image_pyramid* PR, float* u_right,
+                              float* depth);
+
 #ifdef __cplusplus
 }
 #endif

@@ -250,3 +250,19 @@ def track_local_map(fp, Tcw, kps, slot_state, pts, cos_limit=0.5, th=1.0):
         return fr, np.full(len(kps["x"]), -1, np.int32), 0
     assign, nm = search_by_projection_local(fp, kps, slot_state, lp, th)
     return fr, assign, nm
+
+
+def compute_stereo_matches(fp, left, right, pyr_l, pyr_r):
+    """Frame::ComputeStereoMatches (src/frame.cpp:125-333) -> (u_right, depth, n_pairs_before_rejection).
+    left/right: dicts x, y, octave, desc (distorted keypoints); pyr_l/pyr_r: lists of 2-D uint8 levels."""
+    keep = A.KeepAlive()
+    fps = A.make_frame_params(fp)
+    kl, kr = A.make_stereo_keys(left, keep), A.make_stereo_keys(right, keep)
+    bl, pl = A.pack_pyramid(pyr_l)
+    br, pr = A.pack_pyramid(pyr_r)
+    pl.data, pr.data = bl.ctypes.data, br.ctypes.data
+    n = kl.n
+    ur, dp = np.empty(max(n, 1), np.float32), np.empty(max(n, 1), np.float32)
+    npair = lib().or_compute_stereo_matches(C.byref(fps), C.byref(kl), C.byref(kr), C.byref(pl), C.byref(pr),
+                                            A.ptr(ur, C.c_float), A.ptr(dp, C.c_float))
+    return ur[:n].copy(), dp[:n].copy(), npair

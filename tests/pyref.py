@@ -88,3 +88,79 @@ def search_by_projection_local(fp, kps, slot_state, pts, th):  # src/matcher.cpp
             state[bi] = 2 if pts["locked"][m] else 1
             nm += 1
     return assign, nm
+
+
+def compute_stereo_matches(fp, left, right, pyr_l, pyr_r):  # src/frame.cpp:125-333
+    """Pure-Python ComputeStereoMatches with the same defined behaviour at the edges as oracle/stereo.c
+    (clipped bands, out-of-image windows => no depth, empty => no rejection).  Windows via numpy."""
+    nL = len(left["x"])
+    ur = np.full(nL, -1.0, np.float32); dp = np.full(nL, -1.0, np.float32)
+    sf = [f32(s) for s in fp["scale_factors"]]
+    nRows = pyr_l[0].shape[0]
+    rows = [[] for _ in range(nRows)]
+    for iR in range(len(right["x"])):  # :147-161
+        kpY = f32(right["y"][iR]); r = f32(2.0) * sf[int(right["octave"][iR])]
+        for yi in range(max(int(math.floor(f32(kpY - r))), 0), min(int(math.ceil(f32(kpY + r))), nRows - 1) + 1):
+            rows[yi].append(iR)
+    maxD = f32(fp["bf"]) / f32(fp["b"])
+    pairs = []
+    for iL in range(nL):  # :176-315
+        lv = int(left["octave"][iL]); vL = f32(left["y"][iL]); uL = f32(left["x"][iL])
+        if not (0 <= vL < nRows):
+            continue
+        cand = rows[int(vL)]
+        if not cand:
+            continue
+        minU = f32(uL - maxD); maxU = uL
+        if maxU < 0:
+            continue
+        best, bi = 100, 0
+        for iR in cand:
+            o = int(right["octave"][iR])
+            if o < lv - 1 or o > lv + 1:
+                continue
+            uR = f32(right["x"][iR])
+            if minU <= uR <= maxU:
+                d = descriptor_distance(left["desc"][iL], right["desc"][iR])
+                if d < best:
+                    best, bi = d, iR
+        if best >= 75:
+            continue
+        inv = f32(1.0) / sf[lv]
+        su = int(np.round(f32(uL * inv))); sv = int(np.round(f32(vL * inv)))
+        sr = int(np.round(f32(f32(right["x"][bi]) * inv)))
+        IL, IR = pyr_l[lv].astype(np.int64), pyr_r[lv].astype(np.int64)
+        h, w = IL.shape
+        if sv - 5 < 0 or sv + 6 > h or su - 5 < 0 or su + 6 > w:
+            continue
+        if sr < 0 or sr + 11 >= pyr_r[lv].shape[1] or sr - 10 < 0:
+            continue
+        a = IL[sv - 5:sv + 6, su - 5:su + 6]; a = a - a[5, 5]
+        dists = []
+        for inc in range(-5, 6):
+            b = IR[sv - 5:sv + 6, sr + inc - 5:sr + inc + 6]; b = b - b[5, 5]
+            dists.append(int(np.abs(a - b).sum()))
+        binc = int(np.argmin(dists)) - 5
+        if binc in (-5, 5):
+            continue
+        d1, d2, d3 = f32(dists[binc + 4]), f32(dists[binc + 5]), f32(dists[binc + 6])
+        with np.errstate(all="ignore"):
+            delta = f32(f32(d1 - d3) / f32(f32(2.0) * f32(f32(d1 + d3) - f32(f32(2.0) * d2))))
+        if delta < -1 or delta > 1 or np.isnan(delta):
+            if not np.isnan(delta):
+                continue
+        bu = f32(sf[lv] * f32(f32(f32(sr) + f32(binc)) + delta))
+        disp = f32(uL - bu)
+        if disp >= 0 and disp < maxD:
+            if disp <= 0:
+                disp = f32(0.01); bu = f32(float(uL) - 0.01)
+            dp[iL] = f32(f32(fp["bf"]) / disp); ur[iL] = bu
+            pairs.append((dists[binc + 5], iL))
+    if pairs:  # :319-332
+        pairs.sort()
+        th = f32(f32(f32(1.5) * f32(1.4)) * f32(pairs[len(pairs) // 2][0]))
+        for d, i in reversed(pairs):
+            if f32(d) < th:
+                break
+            ur[i] = -1; dp[i] = -1
+    return ur, dp, len(pairs)

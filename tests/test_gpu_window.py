@@ -124,3 +124,33 @@ def test_track_local_map_edges(ctx):
     g = ctx.track_local_map(fp, T, kps, pr["slot_state"], bare)
     fr, assign, nm = O.track_local_map(fp, T, kps, pr["slot_state"], bare)
     assert g["nmatches"] == nm and np.array_equal(g["assign"], assign)
+
+
+@pytest.mark.parametrize("seed,n_left,n_distract,border,dev", [(21, 2000, 800, 24, False), (22, 2000, 800, 24, True),
+                                                               (23, 300, 50, 4, False), (24, 6000, 3000, 10, True)])
+def test_compute_stereo_matches(ctx, seed, n_left, n_distract, border, dev):
+    """ComputeStereoMatches (src/frame.cpp:125-333) bit-exact vs the oracle, incl.
+    keypoints whose SAD windows leave the image (border=4) and the median rejection."""
+    pr = synth.stereo_problem(seed=seed, n_left=n_left, n_distract=n_distract, border=border)
+    ur, dp = ctx.compute_stereo_matches(pr["fp"], pr["left"], pr["right"], pr["pyr_l"], pr["pyr_r"], device_resident=dev)
+    our, odp, npair = O.compute_stereo_matches(pr["fp"], pr["left"], pr["right"], pr["pyr_l"], pr["pyr_r"])
+    assert npair > n_left // 3
+    assert np.array_equal(ur, our) and np.array_equal(dp, odp)
+    assert (ur >= 0).sum() < npair  # the median cut removed some
+
+
+def test_compute_stereo_matches_edges(ctx):
+    pr = synth.stereo_problem(seed=25, n_left=200, n_distract=20)
+    fp, L, R, pl, prr = pr["fp"], pr["left"], pr["right"], pr["pyr_l"], pr["pyr_r"]
+    # no right keypoints: nothing matched
+    noR = {k: v[:0] for k, v in R.items()}
+    ur, dp = ctx.compute_stereo_matches(fp, L, noR, pl, prr)
+    assert (ur == -1).all() and (dp == -1).all()
+    # no left keypoints
+    ur, dp = ctx.compute_stereo_matches(fp, {k: v[:0] for k, v in L.items()}, R, pl, prr)
+    assert len(ur) == 0
+    # a single accepted pair: the median is itself, 2.1 x median keeps it
+    one = {k: v[:1] for k, v in L.items()}
+    ur, dp = ctx.compute_stereo_matches(fp, one, R, pl, prr)
+    o = O.compute_stereo_matches(fp, one, R, pl, prr)
+    assert np.array_equal(ur, o[0]) and np.array_equal(dp, o[1])

@@ -59,3 +59,13 @@ def test_track_local_map_oracle_chain():
     assert fr["in_view"].sum() > 1000
     assert nm > 300
     assert (assign >= 0).sum() == nm
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_stereo_oracle_vs_pyref(seed):
+    """ComputeStereoMatches: C restatement == independent pure-Python restatement, bit for bit."""
+    pr = synth.stereo_problem(seed=seed, n_left=300, n_distract=150, border=4 if seed == 22 else 24)
+    a = O.compute_stereo_matches(pr["fp"], pr["left"], pr["right"], pr["pyr_l"], pr["pyr_r"])
+    b = pyref.compute_stereo_matches(pr["fp"], pr["left"], pr["right"], pr["pyr_l"], pr["pyr_r"])
+    assert a[2] == b[2] and a[2] > 100
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
