@@ -98,6 +98,32 @@ struct KernelTimer {
 
 inline unsigned ceil_div(size_t a, size_t b) { return static_cast<unsigned>((a + b - 1) / b); }
 
+// Exclusive scan of one int per thread across a 1024-thread workgroup (16 wavefronts): wave
+// inclusive scan with DPP-lowered shuffles, then the 16 wave totals from LDS.  Returns the
+// exclusive prefix of this thread; *total = the workgroup sum.  wsum: __shared__ int[16].
+// Every thread of the workgroup must call it (two barriers).
+__device__ __forceinline__ int block_excl_scan_1024(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) {
+    const int s = wsum[w];
+    pre += w < wv ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + incl - v;
+}
+
 }  // namespace lorb
 
 // scratch slot plan (per API family; calls on one ctx are serialized)

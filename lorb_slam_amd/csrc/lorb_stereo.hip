@@ -74,21 +74,10 @@ __global__ __launch_bounds__(1024) void k_st_rows(Keys R, Scales S, int n_levels
   const int b0 = t * per, b1 = min(b0 + per, nRows);
   int s = 0;
   for (int i = b0; i < b1; i++) s += cnt[i];
-  // block-wide exclusive scan of the per-thread sums (16 waves x 64 lanes)
-  int incl = s;
-  const int lane = t & 63, wv = t >> 6;
-  for (int o = 1; o < 64; o <<= 1) {
-    const int v = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += v;
-  }
-  if (lane == 63) wsum[wv] = incl;
-  __syncthreads();
-  int wpre = 0;
-  for (int w = 0; w < wv; w++) wpre += wsum[w];
-  int run = wpre + incl - s;
-  __syncthreads();
+  int tot;
+  int run = lorb::block_excl_scan_1024(s, wsum, &tot);
   for (int i = b0; i < b1; i++) { const int c = cnt[i]; cnt[i] = run; row_off[i] = run; run += c; }
-  if (t == 1023) { int tot = 0; for (int w = 0; w < 16; w++) tot += wsum[w]; row_off[nRows] = tot; }
+  if (t == 1023) row_off[nRows] = tot;
   __syncthreads();
   for (int iR = t; iR < R.n; iR += 1024) {
     int lo, hi;
@@ -212,6 +201,27 @@ __global__ __launch_bounds__(64 * kStWaves) void k_st_match(Keys L, Keys R, Pyr 
   if (lane == 0) { u_right[iL] = ur_o; depth[iL] = dp_o; sad_out[iL] = sad_o; }
 }
 
+// wave 0: the 256-bin histogram bucket b holding 0-based rank k, and the rank r within it
+__device__ __forceinline__ void select_bucket(const int* hist, int k, int& b, int& r) {
+  const int lane = threadIdx.x & 63;
+  const int h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+  const int s = h0 + h1 + h2 + h3;
+  int incl = s;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  const int ex = incl - s;
+  // the owning lane: ex <= k < incl (exactly one lane)
+  const unsigned long long m = __ballot(ex <= k && k < incl);
+  const int src = __ffsll((long long)m) - 1;
+  int kk = k - ex, bb = 4 * lane;
+  if (kk >= h0) { kk -= h0; bb++; if (kk >= h1) { kk -= h1; bb++; if (kk >= h2) { kk -= h2; bb++; } } }
+  b = __shfl(bb, src, 64);
+  r = __shfl(kk, src, 64);
+}
+
 __global__ __launch_bounds__(1024) void k_st_reject(int n, const int* __restrict__ sad, float* __restrict__ u_right,
                                                     float* __restrict__ depth) {
   __shared__ int hist[256];
@@ -229,10 +239,10 @@ __global__ __launch_bounds__(1024) void k_st_reject(int n, const int* __restrict
   __syncthreads();
   const int cnt = s_n;
   if (cnt == 0) return;                                                       // empty: no rejection
-  if (t == 0) {
-    int k = cnt / 2, hi = 0;                                                  // :320 vDistIdx[size/2]
-    while (k >= hist[hi]) { k -= hist[hi]; hi++; }
-    s_hi = hi; s_rank = k;
+  if (t < 64) {  // :320 vDistIdx[size/2]: the bucket holding rank cnt/2
+    int b, r;
+    select_bucket(hist, cnt / 2, b, r);
+    if (t == 0) { s_hi = b; s_rank = r; }
   }
   __syncthreads();
   if (t < 256) hist[t] = 0;
@@ -243,10 +253,10 @@ __global__ __launch_bounds__(1024) void k_st_reject(int n, const int* __restrict
     if (v >= 0 && (v >> 8) == hsel) atomicAdd(&hist[v & 255], 1);
   }
   __syncthreads();
-  if (t == 0) {
-    int k = s_rank, lo = 0;
-    while (k >= hist[lo]) { k -= hist[lo]; lo++; }
-    s_med = (hsel << 8) | lo;
+  if (t < 64) {
+    int b, r;
+    select_bucket(hist, s_rank, b, r);
+    if (t == 0) s_med = (hsel << 8) | b;
   }
   __syncthreads();
   const float median = (float)s_med;

@@ -57,10 +57,16 @@ __global__ __launch_bounds__(1024) void k_grid_build(const float* __restrict__ x
     if (c >= 0) atomicAdd(&cnt[c], 1);
   }
   __syncthreads();
-  if (t == 0) {  // 3072-entry scan (tiny)
-    int acc = 0;
-    for (int c = 0; c < kCells; ++c) { cell_off[c] = acc; cur[c] = acc; acc += cnt[c]; }
-    cell_off[kCells] = acc;
+  {  // 3072-entry exclusive scan: three consecutive cells per thread
+    static_assert(kCells == 3 * 1024, "grid scan assumes 64 x 48 cells");
+    __shared__ int wsum[16];
+    const int c0 = 3 * t;
+    const int a = cnt[c0], b = cnt[c0 + 1], c = cnt[c0 + 2];
+    int tot;
+    const int ex = lorb::block_excl_scan_1024(a + b + c, wsum, &tot);
+    cell_off[c0] = ex; cell_off[c0 + 1] = ex + a; cell_off[c0 + 2] = ex + a + b;
+    cur[c0] = ex; cur[c0 + 1] = ex + a; cur[c0 + 2] = ex + a + b;
+    if (t == 1023) cell_off[kCells] = tot;
   }
   __syncthreads();
   for (int i = t; i < n; i += 1024) {
@@ -108,46 +114,83 @@ struct KpDev {
   int n;
 };
 
-// Walk GetFeaturesInArea in reference order (ix outer, iy inner, cell insertion order) and
-// apply the level / window / stereo filters.  WRITE=false counts, WRITE=true emits
-// (keypoint, distance) in order.
+// Walk GetFeaturesInArea in reference order (ix outer, iy inner, cell insertion order) and apply
+// the level / window / stereo filters -- one WAVEFRONT per query.  The window's cells are taken 64
+// at a time (lane = cell); a wave scan of their sizes flattens the cell lists into one entry
+// sequence in reference order, the entries are taken 64 at a time (lane = entry, owner cell by a
+// 6-step binary search over the scanned sizes), and survivors are compacted with a ballot, so
+// candidate k of the query is the k-th survivor of the reference's loop.  WRITE=false counts,
+// WRITE=true emits (keypoint, distance | octave << 16).  All arguments are wave-uniform; returns the count.
 template <bool WRITE>
-__device__ __forceinline__ int walk_candidates(const KpDev& K, const lorb_frame_params& fp, float x,
-                                               float y, float r, int minLevel, int maxLevel,
-                                               float stereo_u, float stereo_r, const uint4* qdesc,
-                                               int2* out) {
+__device__ __forceinline__ int walk_candidates_wave(const KpDev& K, const lorb_frame_params& fp, float x,
+                                                    float y, float r, int minLevel, int maxLevel,
+                                                    float stereo_u, float stereo_r, const uint4* qdesc,
+                                                    int2* out) {
   const FeatArea a = feat_area(fp, x, y, r);
   if (a.empty) return 0;
+  const int lane = threadIdx.x & 63;
   const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+  const int ny = a.y1 - a.y0 + 1;
+  const int ncell = (a.x1 - a.x0 + 1) * ny;
+  const unsigned long long lt = (1ull << lane) - 1ull;
   int n = 0;
-  for (int ix = a.x0; ix <= a.x1; ++ix)
-    for (int iy = a.y0; iy <= a.y1; ++iy) {
-      const int c = ix * LORB_GRID_ROWS + iy;
-      for (int e = K.cell_off[c]; e < K.cell_off[c + 1]; ++e) {
-        const int j = K.cell_idx[e];
-        const int oc = K.octave[j];
-        if (bCheckLevels) {
-          if (oc < minLevel) continue;
-          if (maxLevel >= 0 && oc > maxLevel) continue;
-        }
+  for (int cb = 0; cb < ncell; cb += 64) {
+    const int ci = cb + lane;
+    int beg = 0, len = 0;
+    if (ci < ncell) {
+      const int c = (a.x0 + ci / ny) * LORB_GRID_ROWS + (a.y0 + ci % ny);
+      beg = K.cell_off[c];
+      len = K.cell_off[c + 1] - beg;
+    }
+    int incl = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    const int ex = incl - len;
+    const int total = __shfl(incl, 63, 64);
+    for (int eb = 0; eb < total; eb += 64) {
+      const int e = eb + lane;
+      int src = 0;  // last lane (cell) whose first entry is <= e: the owner (ex is non-decreasing)
+#pragma unroll
+      for (int st = 32; st >= 1; st >>= 1) {
+        const int cand = src + st;
+        const int exc = __shfl(ex, cand & 63, 64);
+        if (cand < 64 && exc <= e) src = cand;
+      }
+      const int sbeg = __shfl(beg, src, 64), sex = __shfl(ex, src, 64);
+      bool pass = false;
+      int j = 0, oc = 0;
+      if (e < total) {
+        j = K.cell_idx[sbeg + (e - sex)];
+        oc = K.octave[j];
+        // slots locked before the call (mnObs > 0) are skipped by every point (src/matcher.cpp:
+        // 149-151, 273-275): a pure filter, applied here once instead of in every resolver round
+        pass = K.slot_state[j] != LORB_SLOT_LOCKED;
+        pass = pass && !(bCheckLevels && (oc < minLevel || (maxLevel >= 0 && oc > maxLevel)));
         const float distx = K.x[j] - x;
         const float disty = K.y[j] - y;
-        if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
-        if (K.uR && K.uR[j] > 0) {  // stereo consistency (checked after occupancy in the reference;
-                                    // both are pure filters so the order is immaterial)
-          const float er = fabsf(stereo_u - K.uR[j]);
-          if (er > stereo_r) continue;
+        pass = pass && (fabsf(distx) < r && fabsf(disty) < r);
+        if (pass && K.uR) {  // stereo consistency (checked after occupancy in the reference;
+                             // both are pure filters so the order is immaterial)
+          const float uRj = K.uR[j];
+          if (uRj > 0) pass = !(fabsf(stereo_u - uRj) > stereo_r);
         }
-        if (WRITE) out[n] = make_int2(j, hamming(qdesc, K.desc + 2 * (size_t)j));
-        ++n;
       }
+      const unsigned long long m = __ballot(pass);
+      if (WRITE && pass) out[n + __popcll(m & lt)] = make_int2(j, hamming(qdesc, K.desc + 2 * (size_t)j) | (oc << 16));
+      n += __popcll(m);
     }
+  }
   return n;
 }
 
-// (a5) candidates of each local map point
+constexpr int kCandWaves = 4;  // queries (wavefronts) per 256-thread workgroup
+
+// (a5) candidates of each local map point, one wavefront per point
 template <bool WRITE>
-__global__ __launch_bounds__(256) void k_cand_local(KpDev K, WinParams P, int np,
+__global__ __launch_bounds__(64 * kCandWaves) void k_cand_local(KpDev K, WinParams P, int np,
                                                     const uint8_t* __restrict__ in_view,
                                                     const uint8_t* __restrict__ is_bad,
                                                     const float* __restrict__ px, const float* __restrict__ py,
@@ -155,7 +198,7 @@ __global__ __launch_bounds__(256) void k_cand_local(KpDev K, WinParams P, int np
                                                     const float* __restrict__ vcos, const uint4* __restrict__ pdesc,
                                                     int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
                                                     int2* __restrict__ cand) {
-  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  const int m = blockIdx.x * kCandWaves + (threadIdx.x >> 6);
   if (m >= np) return;
   int cnt = 0;
   if (in_view[m] && !(is_bad && is_bad[m])) {
@@ -163,19 +206,19 @@ __global__ __launch_bounds__(256) void k_cand_local(KpDev K, WinParams P, int np
     float r = ((double)vcos[m] > 0.998) ? 2.5f : 4.0f;  // RadiusByViewingCos
     if (P.th != 1.0f) r *= P.th;
     const float rs = r * P.fp.scale_factors[lev];
-    cnt = walk_candidates<WRITE>(K, P.fp, px[m], py[m], rs, lev - 1, lev, pxr[m], rs, pdesc + 2 * (size_t)m,
-                                 WRITE ? cand + cand_off[m] : nullptr);
+    cnt = walk_candidates_wave<WRITE>(K, P.fp, px[m], py[m], rs, lev - 1, lev, pxr[m], rs, pdesc + 2 * (size_t)m,
+                                      WRITE ? cand + cand_off[m] : nullptr);
   }
-  if (!WRITE) cand_cnt[m] = cnt;
+  if (!WRITE && (threadIdx.x & 63) == 0) cand_cnt[m] = cnt;
 }
 
-// (a4) projection of last-frame map points + candidates
+// (a4) projection of last-frame map points + candidates, one wavefront per point
 __device__ __forceinline__ float gemv3(const float* R, float a, float b, float c, float t) {
   const double s = (double)R[0] * (double)a + (double)R[1] * (double)b + (double)R[2] * (double)c;
   return (float)(s + (double)t);
 }
 template <bool WRITE>
-__global__ __launch_bounds__(256) void k_cand_frame(KpDev K, WinParams P, int nl,
+__global__ __launch_bounds__(64 * kCandWaves) void k_cand_frame(KpDev K, WinParams P, int nl,
                                                     const uint8_t* __restrict__ has_mp,
                                                     const uint8_t* __restrict__ outlier,
                                                     const float* __restrict__ pos,
@@ -183,7 +226,7 @@ __global__ __launch_bounds__(256) void k_cand_frame(KpDev K, WinParams P, int nl
                                                     const uint4* __restrict__ ldesc,
                                                     int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
                                                     int2* __restrict__ cand) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * kCandWaves + (threadIdx.x >> 6);
   if (i >= nl) return;
   int cnt = 0;
   if (has_mp[i] && !(outlier && outlier[i])) {
@@ -203,37 +246,33 @@ __global__ __launch_bounds__(256) void k_cand_frame(KpDev K, WinParams P, int nl
         else if (P.mode_backward) { mn = 0; mx = o; }
         else { mn = o - 1; mx = o + 1; }
         const float ur = u - P.fp.bf * invzc;
-        cnt = walk_candidates<WRITE>(K, P.fp, u, v, radius, mn, mx, ur, radius, ldesc + 2 * (size_t)i,
-                                     WRITE ? cand + cand_off[i] : nullptr);
+        cnt = walk_candidates_wave<WRITE>(K, P.fp, u, v, radius, mn, mx, ur, radius, ldesc + 2 * (size_t)i,
+                                          WRITE ? cand + cand_off[i] : nullptr);
       }
     }
   }
-  if (!WRITE) cand_cnt[i] = cnt;
+  if (!WRITE && (threadIdx.x & 63) == 0) cand_cnt[i] = cnt;
 }
 
 // exclusive scan of candidate counts (one workgroup, chunked)
 __global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ cnt, int n, int* __restrict__ off) {
-  __shared__ int s[1024];
-  __shared__ int carry;
-  const int t = threadIdx.x;
-  if (t == 0) carry = 0;
-  __syncthreads();
+  __shared__ int wsum[16];
+  int carry = 0;
   for (int base = 0; base < n; base += 1024) {
-    const int v = base + t < n ? cnt[base + t] : 0;
-    s[t] = v;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-      const int a = t >= o ? s[t - o] : 0;
-      __syncthreads();
-      s[t] += a;
-      __syncthreads();
-    }
-    if (base + t < n) off[base + t] = carry + s[t] - v;
-    __syncthreads();
-    if (t == 1023) carry += s[1023];
-    __syncthreads();
+    const int i = base + (int)threadIdx.x;
+    const int v = i < n ? cnt[i] : 0;
+    int tot;
+    const int ex = lorb::block_excl_scan_1024(v, wsum, &tot);
+    if (i < n) off[i] = carry + ex;
+    carry += tot;
   }
-  if (t == 0) off[n] = carry;
+  if (threadIdx.x == 0) off[n] = carry;
+}
+
+// resolver state in LDS when claim + res fit (nk + np ints <= 120 KiB)
+inline size_t resolve_lds_bytes(int np, int nk) {
+  const size_t b = sizeof(int) * ((size_t)np + (size_t)nk);
+  return b <= 120 * 1024 ? b : 0;
 }
 
 // Jacobi fixpoint resolver (one workgroup per call).  MODE 0 = a5 (best/second + ratio test),
@@ -251,15 +290,18 @@ __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __r
                                                   int* __restrict__ assign,  // nk output
                                                   int* __restrict__ bins,    // np scratch (MODE 1)
                                                   int* __restrict__ nulls,   // nk scratch (MODE 1)
-                                                  int* __restrict__ nmatches) {
-  __shared__ int s_changed, s_rounds;
+                                                  int* __restrict__ nmatches, int use_lds) {
+  // claim (nk) and res (np) live in LDS when they fit (dynamic shared memory), else in global
+  extern __shared__ int s_dyn[];
+  if (use_lds) { claim = s_dyn; res = s_dyn + nk; }
+  __shared__ int s_changed;
   __shared__ int hist[LORB_HISTO_LENGTH];
   __shared__ int s_ind[3];
   __shared__ int s_acc, s_rej;
   const int t = threadIdx.x;
   for (int c = t; c < nk; c += 1024) claim[c] = kNoClaim;
   for (int m = t; m < np; m += 1024) res[m] = -2;  // "never computed"
-  if (t == 0) { s_rounds = 0; s_acc = 0; s_rej = 0; }
+  if (t == 0) { s_acc = 0; s_rej = 0; }
   __syncthreads();
   for (int round = 0; round <= np; ++round) {
     if (t == 0) s_changed = 0;
@@ -269,17 +311,17 @@ __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __r
       int bestDist = 256, bestIdx = -1;
       int bestLevel = -1, bestDist2 = 256, bestLevel2 = -1;
       for (int e = a; e < b; ++e) {
-        const int2 cd = cand[e];
+        const int2 cd = cand[e];  // (slot, distance | octave << 16); pre-call locked slots removed
         const int j = cd.x;
-        if (slot_state[j] == LORB_SLOT_LOCKED) continue;
         if ((int)claim[j] < m) continue;  // locked by an earlier point during this call
-        const int dist = cd.y;
+        const int dist = cd.y & 0xffff;
         if (MODE == 0) {
+          const int oc = cd.y >> 16;
           if (dist < bestDist) {
             bestDist2 = bestDist; bestDist = dist;
-            bestLevel2 = bestLevel; bestLevel = kp_octave[j]; bestIdx = j;
+            bestLevel2 = bestLevel; bestLevel = oc; bestIdx = j;
           } else if (dist < bestDist2) {
-            bestLevel2 = kp_octave[j]; bestDist2 = dist;
+            bestLevel2 = oc; bestDist2 = dist;
           }
         } else {
           if (dist < bestDist) { bestDist = dist; bestIdx = j; }
@@ -519,7 +561,7 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 3, (size_t)nk + 1, &claim));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 4, (size_t)nk + 2, &dassign));
   dnm = dassign + nk;
-  const unsigned g = lorb::ceil_div(std::max(np, 1), 256);
+  const unsigned g = lorb::ceil_div(std::max(np, 1), kCandWaves);
   if (np > 0) {
     lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
     hipLaunchKernelGGL(k_cand_local<false>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
@@ -534,8 +576,9 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
   if (np > 0)
     hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
                        reinterpret_cast<const uint4*>(pd), cnt, off, cand);
-  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), 0, ctx->stream, np, nk, off, cand, K.octave, K.slot_state, lk,
-                     (const float*)nullptr, (const float*)nullptr, res, claim, dassign, (int*)nullptr, (int*)nullptr, dnm);
+  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), resolve_lds_bytes(np, nk), ctx->stream, np, nk, off, cand, K.octave, K.slot_state, lk,
+                     (const float*)nullptr, (const float*)nullptr, res, claim, dassign, (int*)nullptr, (int*)nullptr, dnm,
+                     (int)(resolve_lds_bytes(np, nk) > 0));
   LORB_CHECK_LAUNCH(ctx);
   LORB_HIP(ctx, hipMemcpyAsync(assign, dassign, sizeof(int) * nk, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, hipMemcpyAsync(nmatches, dnm, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
@@ -593,7 +636,7 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 5, (size_t)nl + 1, &bins));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 6, (size_t)nk + 1, &nulls));
   dnm = dassign + nk;
-  const unsigned g = lorb::ceil_div(std::max(nl, 1), 256);
+  const unsigned g = lorb::ceil_div(std::max(nl, 1), kCandWaves);
   if (nl > 0) {
     lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
     hipLaunchKernelGGL(k_cand_frame<false>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
@@ -608,8 +651,9 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
   if (nl > 0)
     hipLaunchKernelGGL(k_cand_frame<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
                        reinterpret_cast<const uint4*>(ld), cnt, off, cand);
-  hipLaunchKernelGGL(k_resolve<1>, dim3(1), dim3(1024), 0, ctx->stream, nl, nk, off, cand, K.octave, K.slot_state, lk,
-                     la, K.angle, res, claim, dassign, bins, nulls, dnm);
+  hipLaunchKernelGGL(k_resolve<1>, dim3(1), dim3(1024), resolve_lds_bytes(nl, nk), ctx->stream, nl, nk, off, cand, K.octave, K.slot_state, lk,
+                     la, K.angle, res, claim, dassign, bins, nulls, dnm,
+                     (int)(resolve_lds_bytes(nl, nk) > 0));
   LORB_CHECK_LAUNCH(ctx);
   LORB_HIP(ctx, hipMemcpyAsync(assign, dassign, sizeof(int) * nk, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, hipMemcpyAsync(nmatches, dnm, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
@@ -705,7 +749,7 @@ int lorb_track_local_map_dev(lorb_ctx* ctx, const lorb_frame_params* frame, cons
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 1, (size_t)np + 1, &off));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 2, (size_t)np + 1, &res));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 3, (size_t)nk + 1, &claim));
-  const unsigned g = lorb::ceil_div(std::max(np, 1), 256);
+  const unsigned g = lorb::ceil_div(std::max(np, 1), kCandWaves);
   const float* tx = d_track;
   if (np > 0) {
     lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
@@ -723,9 +767,10 @@ int lorb_track_local_map_dev(lorb_ctx* ctx, const lorb_frame_params* frame, cons
     hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, d_in_view, pts->is_bad, tx,
                        tx + np, tx + 2 * np, d_level, tx + 3 * np, reinterpret_cast<const uint4*>(pts->desc), cnt, off,
                        cand);
-  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), 0, ctx->stream, np, nk, off, cand, K.octave, K.slot_state,
+  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), resolve_lds_bytes(np, nk), ctx->stream, np, nk, off, cand, K.octave, K.slot_state,
                      pts->locked, (const float*)nullptr, (const float*)nullptr, res, claim, d_assign, (int*)nullptr,
-                     (int*)nullptr, d_nmatches);
+                     (int*)nullptr, d_nmatches,
+                     (int)(resolve_lds_bytes(np, nk) > 0));
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
 }

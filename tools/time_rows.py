@@ -16,8 +16,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import oracle as O  # noqa: E402
 from lorb_slam_amd import _abi as A, synth  # noqa: E402
-from lorb_slam_amd._abi import lib  # noqa: E402
-from lorb_slam_amd.runtime import Context  # noqa: E402
+
+from lorb_slam_amd.runtime import Context, lib  # noqa: E402
 import lorb_slam_amd.window  # noqa: E402,F401
 
 N = int(os.environ.get("ROWS_N", "200"))
