@@ -41,32 +41,49 @@ __device__ __forceinline__ int desc_dist(const uint4* a, const uint4* b) {
          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-// band [lo, hi] of right keypoint iR clipped to [0, nRows) (:155-160); lo > hi => empty
-__device__ __forceinline__ void band(const Keys& R, const float* sf, int n_levels, int iR, int nRows, int& lo,
-                                     int& hi) {
-  const int o = R.octave[iR];
-  if (o < 0 || o >= n_levels) { lo = 1; hi = 0; return; }
-  const float kpY = R.y[iR];
-  const float r = 2.0f * sf[o];
-  hi = (int)ceilf(kpY + r);
-  lo = (int)floorf(kpY - r);
+struct Scales { float sf[LORB_MAX_LEVELS]; };
+
+constexpr int kStBandKeys = 8192;  // right keypoints whose band is kept in LDS between the passes
+
+// band [lo, hi] of right keypoint (octave o, row y) clipped to [0, nRows) (:155-160); lo > hi => empty
+__device__ __forceinline__ int band_packed(int o, float kpY, const float* s_sf, int n_levels, int nRows) {
+  if (o < 0 || o >= n_levels) return 1;  // lo = 1, hi = 0
+  const float r = 2.0f * s_sf[o];
+  int hi = (int)ceilf(kpY + r), lo = (int)floorf(kpY - r);
   lo = lo < 0 ? 0 : lo;
   hi = hi > nRows - 1 ? nRows - 1 : hi;
+  if (lo > hi) return 1;
+  return lo | (hi << 16);
 }
-
-struct Scales { float sf[LORB_MAX_LEVELS]; };
 
 __global__ __launch_bounds__(1024) void k_st_rows(Keys R, Scales S, int n_levels, int nRows, int* __restrict__ row_off,
                                                   int* __restrict__ row_list) {
   __shared__ int cnt[kStMaxRows + 1];
+  __shared__ int s_band[kStBandKeys];
+  __shared__ float s_sf[LORB_MAX_LEVELS];
   __shared__ int wsum[16];
   const int t = threadIdx.x;
+  if (t < LORB_MAX_LEVELS) s_sf[t] = S.sf[t];
   for (int i = t; i <= nRows; i += 1024) cnt[i] = 0;
   __syncthreads();
-  for (int iR = t; iR < R.n; iR += 1024) {
-    int lo, hi;
-    band(R, S.sf, n_levels, iR, nRows, lo, hi);
-    for (int yi = lo; yi <= hi; yi++) atomicAdd(&cnt[yi], 1);
+  // pass 1: bands (four keypoints per thread per sweep, loads issued together) and row counts
+  for (int base = 0; base < R.n; base += 4096) {
+    int o[4];
+    float y[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int i = base + t + 1024 * k;
+      o[k] = i < R.n ? R.octave[i] : -1;
+      y[k] = i < R.n ? R.y[i] : 0.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int i = base + t + 1024 * k;
+      if (i >= R.n) continue;
+      const int bp = band_packed(o[k], y[k], s_sf, n_levels, nRows);
+      if (i < kStBandKeys) s_band[i] = bp;
+      for (int yi = bp & 0xffff; yi <= (bp >> 16); yi++) atomicAdd(&cnt[yi], 1);
+    }
   }
   __syncthreads();
   // exclusive scan of cnt[0..nRows) in place: each thread owns a contiguous chunk
@@ -79,10 +96,10 @@ __global__ __launch_bounds__(1024) void k_st_rows(Keys R, Scales S, int n_levels
   for (int i = b0; i < b1; i++) { const int c = cnt[i]; cnt[i] = run; row_off[i] = run; run += c; }
   if (t == 1023) row_off[nRows] = tot;
   __syncthreads();
+  // pass 2: fill (row lists are unordered, see the header)
   for (int iR = t; iR < R.n; iR += 1024) {
-    int lo, hi;
-    band(R, S.sf, n_levels, iR, nRows, lo, hi);
-    for (int yi = lo; yi <= hi; yi++) row_list[atomicAdd(&cnt[yi], 1)] = iR;
+    const int bp = iR < kStBandKeys ? s_band[iR] : band_packed(R.octave[iR], R.y[iR], s_sf, n_levels, nRows);
+    for (int yi = bp & 0xffff; yi <= (bp >> 16); yi++) row_list[atomicAdd(&cnt[yi], 1)] = iR;
   }
 }
 
