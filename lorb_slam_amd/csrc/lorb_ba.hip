@@ -1306,6 +1306,9 @@ struct BandSide {
 __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_bad;
+#ifdef LORB_CHOL_STAMPS
+  const unsigned long long st_entry = __builtin_amdgcn_s_memtime();
+#endif
   const int w = blockIdx.x;
   if (d.st[w].done) return;
   if (d.sharded && d.wfail[w] > 0.0) {
@@ -1327,18 +1330,48 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   double* xb = xt + 64 * 18;
   double* zX = xb + 64 * 18;  // 48
   {
+    // Staging is latency-bound (S was written by k_ba_schur on other XCDs): thread (off = t & 63,
+    // r0 = t >> 6) covers band column off of rows r0, r0+4, ...; kStageU rows per batch, all loads
+    // of a batch issued before any store.  (The bottom is a transposing gather: one cache line
+    // per lane.)
+    constexpr int kStageU = 20;
     const double* __restrict__ S = d.env + W.env_base;
-    for (int k = t; k < rt * B1; k += 256) {  // top: rows 0 .. m+47 as they are (m + 48 <= n)
-      const int i = k / B1, off = k - i * B1;
-      At[k] = i - (bw - off) >= 0 ? S[k] : 0.0;
-    }
-    for (int k = t; k < rb * B1; k += 256) {  // bottom reversed: (i', j' = i' + off - bw)
-      const int ip = k / B1, off = k - ip * B1;
-      const int jp = ip + off - bw;
-      const int row = n16 - 1 - jp, col = n16 - 1 - ip;  // original lower entry, row >= col
-      double v = 0.0;
-      if (jp >= 0) v = row >= n ? (row == col ? 1.0 : 0.0) : S[row * B1 + (col - row + bw)];
-      Ab[k] = v;
+    const int off = t & 63, r0 = t >> 6;
+    if (off < B1) {
+      for (int i0 = r0; i0 < rt; i0 += 4 * kStageU) {  // top: rows 0 .. m+47 as they are (m + 48 <= n)
+        double v[kStageU];
+#pragma unroll
+        for (int u = 0; u < kStageU; ++u) {
+          const int i = i0 + 4 * u;
+          const bool ok = i < rt && i - (bw - off) >= 0;
+          const double sv = S[ok ? i * B1 + off : 0];
+          v[u] = ok ? sv : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kStageU; ++u) {
+          const int i = i0 + 4 * u;
+          if (i < rt) At[i * B1 + off] = v[u];
+        }
+      }
+      // bottom reversed: entry (i', off) is the original lower entry (row, col) with
+      // row = n16-1-i'+bw-off, col = n16-1-i', i.e. S[row * B1 + off]; rows >= n: identity pad
+      for (int i0 = r0; i0 < rb; i0 += 4 * kStageU) {
+        double v[kStageU];
+#pragma unroll
+        for (int u = 0; u < kStageU; ++u) {
+          const int ip = i0 + 4 * u;
+          const int jp = ip + off - bw;
+          const int row = n16 - 1 - jp;
+          const bool ld = ip < rb && jp >= 0 && row < n;
+          const double sv = S[ld ? row * B1 + off : 0];
+          v[u] = ld ? sv : ((ip < rb && jp >= 0 && off == bw) ? 1.0 : 0.0);
+        }
+#pragma unroll
+        for (int u = 0; u < kStageU; ++u) {
+          const int ip = i0 + 4 * u;
+          if (ip < rb) Ab[ip * B1 + off] = v[u];
+        }
+      }
     }
     for (int k = t; k < rt; k += 256) zt[k] = d.rhs[W.row_base + k];
     for (int k = t; k < rb; k += 256) { const int row = n16 - 1 - k; zb[k] = row < n ? d.rhs[W.row_base + row] : 0.0; }
@@ -1353,6 +1386,7 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   bool bad = false;
 #ifdef LORB_CHOL_STAMPS
   const unsigned long long st0 = __builtin_amdgcn_s_memtime();
+  if (lane == 0 && wv == 1) d.dbg[8 * w + 5] = st0 - st_entry;  // staging
 #define C2_STAMP(k) do { if (lane == 0 && wv < 2) d.dbg[8 * w + (k) + 4 * wv] = __builtin_amdgcn_s_memtime() - st0; } while (0)
 #else
 #define C2_STAMP(k) do {} while (0)
@@ -1423,6 +1457,9 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
     }
     d.rot_cand[c] = lorb::rot_val(xn);
   }
+#ifdef LORB_CHOL_STAMPS
+  if (lane == 0 && wv == 1) d.dbg[8 * w + 6] = __builtin_amdgcn_s_memtime() - st0;  // to the end
+#endif
 }
 
 // K7: point-group back-substitution: b_p -= sum_e W_e^T y_c(e) (observation phase + ordered
