@@ -1139,15 +1139,22 @@ __global__ __launch_bounds__(256) void k_ba_chol_w(BaDev d) {
 // (3 panels).  Back-substitution: M, then T (wave 0) and B (wave 1) concurrently.  Rows
 // n .. n16-1 are an identity pad.
 struct BandSide {
-  double* A;     // band storage, rows x (bw + 1), row i holds cols i-bw .. i; the diagonal slot
-                 // holds 1 / L(i, i) (the only use of the diagonal is the back-substitution)
+  double* A;     // band storage of the whole matrix (row-major, rows x (bw + 1), row i holds cols
+                 // i-bw .. i); the diagonal slot holds 1 / L(i, i) (its only use is the
+                 // back-substitution).  Element (i, j) of this side's view is A[base + si*i + sj*j]:
+                 // the top side views it as is (si = bw, sj = 1, base = bw); the bottom side views
+                 // it reversed, (i', j') = (n16-1-j, n16-1-i) (si = -1, sj = -bw, base =
+                 // (n16-1)(bw+1) + bw), so both sides run the same panel code on one staging.
   double* z;     // rows: rhs -> forward substitution -> solution
   double* xch;   // 64 x 17 exchange (column 16 of each row: dummy store slot of that lane)
   int rows, bw, lane;
+  int base, si, sj;
+
+  __device__ __forceinline__ int idx(int i, int j) const { return base + si * i + sj * j; }
 
   __device__ __forceinline__ double get(int i, int j) const {  // branch-free; 0 outside band / rows
     const bool ok = j <= i && i - j <= bw && i < rows;
-    const double v = A[ok ? i * (bw + 1) + (j - i + bw) : 0];
+    const double v = A[ok ? idx(i, j) : base];
     return ok ? v : 0.0;
   }
   __device__ __forceinline__ void init(v4d (&T)[10], double& zr) const {
@@ -1165,8 +1172,8 @@ struct BandSide {
   // through LDS broadcast reads, off the chain.
   __device__ __forceinline__ void panels(v4d (&T)[10], double& zr, bool& bad, int kb0, int kend) const {
     const int ci = lane & 15, ck = lane >> 4;
-    const int B1 = bw + 1;
-    int tn_addr = (kb0 + 64 + ck) * B1 + (16 + ci - 64 - ck + bw) ;  // entering tile (J, r) adds 16 J - 4 r bw ... (below)
+    const int dstep = 16 * (si + sj);  // address step of one panel along the diagonal
+    int tn_addr = idx(kb0 + 64 + ck, kb0 + 16 + ci);  // entering tile (J, r) adds 4 r si + 16 J sj (below)
     unsigned tn_ok = 0;
 #pragma unroll
     for (int J = 0; J < 4; ++J)
@@ -1178,7 +1185,7 @@ struct BandSide {
     unsigned l_ok = 0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) l_ok |= (unsigned)(q <= lane && lane - q <= bw) << q;
-    int l_base = (kb0 + lane) * B1 + (bw - lane);  // slot of (kb0 + lane, kb0 + q) = l_base + q
+    int l_base = idx(kb0 + lane, kb0);  // slot of (kb0 + lane, kb0 + q) = l_base + q sj
     double* colbuf = xch;  // 16 x 64 during the factorization (xch is idle then)
     double* dummy = xch + lane * 17 + 16;
     for (int kb = kb0; kb < kend; kb += 16) {
@@ -1193,10 +1200,10 @@ struct BandSide {
         for (int r = 0; r < 4; ++r) {
           // (kb+64+ck+4r, kb+16+16J+ci): row offset 4r, column offset 16J relative to tn_addr
           const bool ok = (((unsigned)tok >> (4 * J + r)) & 1u) && kb + 64 + ck + 4 * r < rows;
-          const double v = A[ok ? tn_addr + 4 * r * B1 + 16 * J - 4 * r : 0];
+          const double v = A[ok ? tn_addr + 4 * r * si + 16 * J * sj : base];
           Tn[J][r] = ok ? v : 0.0;
         }
-      tn_addr += 16 * B1;
+      tn_addr += dstep;
       const double zin = kb + 16 + lane < rows ? z[kb + 16 + lane] : 0.0;
 #pragma unroll
       for (int I = 0; I < 4; ++I)
@@ -1231,10 +1238,10 @@ struct BandSide {
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
           const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
-          *(ok ? A + l_base + q : dummy) = q == lane ? yq : P[q];
+          *(ok ? A + l_base + q * sj : dummy) = q == lane ? yq : P[q];
           xch[lane * 17 + q] = P[q];
         }
-        l_base += 16 * B1;
+        l_base += dstep;
         if (lane < NB) z[kb + lane] = zr;
       }
       wave_sync_lds();
@@ -1271,7 +1278,7 @@ struct BandSide {
 #pragma unroll
       for (int k = 0; k < NB; ++k) {
         const bool ok = k > jc;
-        const double v = A[ok ? (c0 + k) * (bw + 1) + (j - (c0 + k) + bw) : 0];
+        const double v = A[ok ? idx(c0 + k, j) : base];
         lk[k] = ok ? v : 0.0;
       }
       const int iend = min(rows - 1, j + bw);
@@ -1280,7 +1287,7 @@ struct BandSide {
       for (int u = 0; u < 16; ++u) {
         const int i = c0 + 16 + g + 4 * u;
         const bool ok = i <= iend;
-        av[u] = A[ok ? i * (bw + 1) + (j - i + bw) : 0];
+        av[u] = A[ok ? idx(i, j) : base];
         zv[u] = z[ok ? i : 0];
         av[u] = ok ? av[u] : 0.0;
       }
@@ -1291,7 +1298,7 @@ struct BandSide {
       acc += __shfl_xor(acc, 16, 64);
       acc += __shfl_xor(acc, 32, 64);
       double zb = z[j] - acc;
-      const double iv = A[j * (bw + 1) + bw];  // 1 / L(j, j)
+      const double iv = A[idx(j, j)];  // 1 / L(j, j)
 #pragma unroll
       for (int k = NB - 1; k >= 0; --k) {
         const double yk = readlane_d(zb, k) * readlane_d(iv, k);
@@ -1322,54 +1329,32 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   const int nB = n16 - m - 48;
   const int rt = m + 48, rb = nB + 48;    // rows of the top / reversed-bottom bands
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  double* At = smem;
-  double* Ab = At + rt * B1;
-  double* zt = Ab + rb * B1;
+  double* Ab = smem;          // the whole band once, n16 rows (rows n .. n16-1: identity pad)
+  double* zt = Ab + n16 * B1;
   double* zb = zt + rt;
   double* xt = zb + rb;       // 64 x 18 per side (rows of 17); both together hold X (48 x 48)
   double* xb = xt + 64 * 18;
   double* zX = xb + 64 * 18;  // 48
   {
-    // Staging is latency-bound (S was written by k_ba_schur on other XCDs): thread (off = t & 63,
-    // r0 = t >> 6) covers band column off of rows r0, r0+4, ...; kStageU rows per batch, all loads
-    // of a batch issued before any store.  (The bottom is a transposing gather: one cache line
-    // per lane.)
+    // Row-major copy of S (coalesced: lane = band column), kStageU rows per batch with all loads
+    // of a batch issued before any store; left triangle of the first bw rows zeroed.
     constexpr int kStageU = 20;
     const double* __restrict__ S = d.env + W.env_base;
     const int off = t & 63, r0 = t >> 6;
     if (off < B1) {
-      for (int i0 = r0; i0 < rt; i0 += 4 * kStageU) {  // top: rows 0 .. m+47 as they are (m + 48 <= n)
+      for (int i0 = r0; i0 < n16; i0 += 4 * kStageU) {
         double v[kStageU];
 #pragma unroll
         for (int u = 0; u < kStageU; ++u) {
           const int i = i0 + 4 * u;
-          const bool ok = i < rt && i - (bw - off) >= 0;
+          const bool ok = i < n && i - (bw - off) >= 0;
           const double sv = S[ok ? i * B1 + off : 0];
-          v[u] = ok ? sv : 0.0;
+          v[u] = ok ? sv : ((i >= n && off == bw) ? 1.0 : 0.0);
         }
 #pragma unroll
         for (int u = 0; u < kStageU; ++u) {
           const int i = i0 + 4 * u;
-          if (i < rt) At[i * B1 + off] = v[u];
-        }
-      }
-      // bottom reversed: entry (i', off) is the original lower entry (row, col) with
-      // row = n16-1-i'+bw-off, col = n16-1-i', i.e. S[row * B1 + off]; rows >= n: identity pad
-      for (int i0 = r0; i0 < rb; i0 += 4 * kStageU) {
-        double v[kStageU];
-#pragma unroll
-        for (int u = 0; u < kStageU; ++u) {
-          const int ip = i0 + 4 * u;
-          const int jp = ip + off - bw;
-          const int row = n16 - 1 - jp;
-          const bool ld = ip < rb && jp >= 0 && row < n;
-          const double sv = S[ld ? row * B1 + off : 0];
-          v[u] = ld ? sv : ((ip < rb && jp >= 0 && off == bw) ? 1.0 : 0.0);
-        }
-#pragma unroll
-        for (int u = 0; u < kStageU; ++u) {
-          const int ip = i0 + 4 * u;
-          if (ip < rb) Ab[ip * B1 + off] = v[u];
+          if (i < n16) Ab[i * B1 + off] = v[u];
         }
       }
     }
@@ -1378,8 +1363,8 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
     if (t == 0) s_bad = 0;
   }
   __syncthreads();
-  const BandSide top{At, zt, xt, rt, bw, lane};
-  const BandSide bot{Ab, zb, xb, rb, bw, lane};
+  const BandSide top{Ab, zt, xt, rt, bw, lane, bw, bw, 1};
+  const BandSide bot{Ab, zb, xb, rb, bw, lane, (n16 - 1) * B1 + bw, -1, -bw};
   const BandSide& me = wv == 0 ? top : bot;
   v4d T[10];
   double zr = 0.0;
