@@ -1338,7 +1338,10 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   {
     // Row-major copy of S (coalesced: lane = band column), kStageU rows per batch with all loads
     // of a batch issued before any store; left triangle of the first bw rows zeroed.
-    constexpr int kStageU = 20;
+#ifndef LORB_STAGE_U
+#define LORB_STAGE_U 20
+#endif
+    constexpr int kStageU = LORB_STAGE_U;
     const double* __restrict__ S = d.env + W.env_base;
     const int off = t & 63, r0 = t >> 6;
     if (off < B1) {
