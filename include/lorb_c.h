@@ -290,6 +290,20 @@ int lorb_compute_stereo_matches_dev(lorb_ctx* ctx, const lorb_frame_params* fram
                                     const lorb_image_pyramid* d_left_pyr, const lorb_image_pyramid* d_right_pyr,
                                     float* d_u_right, float* d_depth);
 
+/* SURVEY §8f row 3 (descriptor stage of ORBextractor::operator(), src/ORBextractor.cpp:1087-1154):
+ * for every keypoint (level coordinates, i.e. before the `pt *= scale` of :1144-1149) the IC_Angle
+ * orientation on its raw pyramid level (computeOrientation, :79-107, :487-493; cv::fastAtan2) and
+ * the 32-byte rBRIEF descriptor on the level blurred by GaussianBlur(7x7, sigma 2,
+ * BORDER_REFLECT_101) (:1131-1132, :110-150).  pattern: the 512 test points as 1024 ints
+ * (x0, y0, x1, y1, ...), the reference's bit_pattern_31_ (:152).  Outputs: angle[n] (KeyPoint::angle,
+ * degrees) and desc (n x 32).  Defined for keypoints at least 19 px (EDGE_THRESHOLD, :76) inside
+ * their level, as the extractor produces them; the host entry point rejects others. */
+int lorb_orb_describe(lorb_ctx* ctx, const lorb_image_pyramid* pyr, int32_t n, const float* x, const float* y,
+                      const int32_t* level, const int32_t* pattern, float* angle, uint8_t* desc);
+int lorb_orb_describe_dev(lorb_ctx* ctx, const lorb_image_pyramid* d_pyr, int32_t n, const float* d_x,
+                          const float* d_y, const int32_t* d_level, const int32_t* d_pattern, float* d_angle,
+                          uint8_t* d_desc);
+
 /* ----------------------------------------------------------------------------------------
  * Bundle adjustment: Ceres-default Levenberg-Marquardt + DENSE_SCHUR restated
  * (src/bundle_adjust.cpp:158-202 and :207-330; solver defaults in SURVEY Appendix B).

@@ -1,0 +1,289 @@
+// lorb_orb.hip -- the descriptor stage of ORBextractor::operator() (src/ORBextractor.cpp:1087-1154),
+// SURVEY §8f row 3:
+//   k_orb_blur  GaussianBlur(level, 7x7, sigma 2, BORDER_REFLECT_101) of every pyramid level
+//               (:1131-1132), OpenCV 3.1's 8U fixed-point separable smoothing (integer taps =
+//               round(256 k), integer row and column passes, (s + 2^15) >> 16, saturate); one
+//               workgroup per 64 x 16 output tile, the 70 x 22 input tile and the row pass in LDS;
+//   k_orb_desc  one wavefront per keypoint: IC_Angle on the raw level (:79-107; lane = patch
+//               column, integer moments reduced across the wave) with cv::fastAtan2, then the
+//               rBRIEF test pairs on the blurred level (:110-150; lane = four pairs, nibbles
+//               merged by a lane shuffle).  The 256-pair pattern is the caller's (the reference's
+//               bit_pattern_31_), staged in LDS.
+// Integer sums make the blur and the moments order-independent, so results are bit-exact with
+// oracle/orb.c; the float expressions follow the reference's order (-ffp-contract=off).
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+#include "lorb_internal.h"
+
+namespace {
+
+constexpr int kHalfPatch = 15;
+constexpr int kTileW = 64, kTileH = 16;
+
+struct OrbPyr {
+  const uint8_t* data;
+  uint8_t* blur;  // same layout (offsets / steps) as data
+  int64_t offset[LORB_MAX_LEVELS];
+  int rows[LORB_MAX_LEVELS], cols[LORB_MAX_LEVELS], step[LORB_MAX_LEVELS];
+  int tile_off[LORB_MAX_LEVELS + 1];  // first tile of each level
+  int tiles_x[LORB_MAX_LEVELS];
+  int n_levels;
+  int k[7];                           // fixed-point Gaussian taps
+  int umax[kHalfPatch + 1];
+};
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+  return p;
+}
+
+__global__ __launch_bounds__(256) void k_orb_blur(OrbPyr P) {
+  __shared__ int in[kTileH + 6][kTileW + 6 + 1];
+  __shared__ int rowp[kTileH + 6][kTileW + 1];
+  const int b = blockIdx.x, t = threadIdx.x;
+  int l = 0;
+  while (l + 1 < P.n_levels && b >= P.tile_off[l + 1]) ++l;
+  const int tb = b - P.tile_off[l];
+  const int x0 = (tb % P.tiles_x[l]) * kTileW, y0 = (tb / P.tiles_x[l]) * kTileH;
+  const int rows = P.rows[l], cols = P.cols[l], step = P.step[l];
+  const uint8_t* src = P.data + P.offset[l];
+  for (int e = t; e < (kTileH + 6) * (kTileW + 6); e += 256) {
+    const int r = e / (kTileW + 6), c = e - r * (kTileW + 6);
+    const int yy = reflect101(y0 + r - 3, rows), xx = reflect101(x0 + c - 3, cols);
+    in[r][c] = src[(int64_t)yy * step + xx];
+  }
+  __syncthreads();
+  for (int e = t; e < (kTileH + 6) * kTileW; e += 256) {  // row pass (every staged row)
+    const int r = e / kTileW, c = e - r * kTileW;
+    int s = 0;
+#pragma unroll
+    for (int d = 0; d < 7; ++d) s += P.k[d] * in[r][c + d];
+    rowp[r][c] = s;
+  }
+  __syncthreads();
+  uint8_t* dst = P.blur + P.offset[l];
+  for (int e = t; e < kTileH * kTileW; e += 256) {  // column pass
+    const int r = e / kTileW, c = e - r * kTileW;
+    const int y = y0 + r, x = x0 + c;
+    if (y >= rows || x >= cols) continue;
+    int s = 0;
+#pragma unroll
+    for (int d = 0; d < 7; ++d) s += P.k[d] * rowp[r + d][c];
+    const int v = (s + (1 << 15)) >> 16;
+    dst[(int64_t)y * step + x] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+  }
+}
+
+// cv::fastAtan2 (OpenCV 3.1), degrees
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+  const float p1 = 0.9997878412794807f * (float)(180 / 3.1415926535897932384626433832795);
+  const float p3 = -0.3258083974640975f * (float)(180 / 3.1415926535897932384626433832795);
+  const float p5 = 0.1555786518463281f * (float)(180 / 3.1415926535897932384626433832795);
+  const float p7 = -0.04432655554792128f * (float)(180 / 3.1415926535897932384626433832795);
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + (float)DBL_EPSILON);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + (float)DBL_EPSILON);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+__device__ __forceinline__ int wave_isum(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+constexpr int kDescWaves = 4;
+
+__global__ __launch_bounds__(64 * kDescWaves) void k_orb_desc(OrbPyr P, int n, const float* __restrict__ kx,
+                                                              const float* __restrict__ ky,
+                                                              const int* __restrict__ klev,
+                                                              const int* __restrict__ pattern,
+                                                              float* __restrict__ angle_out,
+                                                              uint8_t* __restrict__ desc_out) {
+  __shared__ int s_pat[1024];
+  for (int e = threadIdx.x; e < 1024; e += 64 * kDescWaves) s_pat[e] = pattern[e];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * kDescWaves + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int l = klev[i];
+  if (l < 0 || l >= P.n_levels) return;  // validated on the host for the host entry point
+  const int step = P.step[l];
+  const int cx = __float2int_rn(kx[i]), cy = __float2int_rn(ky[i]);  // cvRound
+  // IC_Angle: lane u + 15 (u in [-15, 15]) sums column u over the disc, rows split in two halves
+  int m10 = 0, m01 = 0;
+  {
+    const uint8_t* center = P.data + P.offset[l] + (int64_t)cy * step + cx;
+    const int u = (lane & 31) - kHalfPatch;
+    const bool half = lane >= 32;  // rows v > 0 for the upper half-wave, v <= 0 for the lower
+    if ((lane & 31) < 2 * kHalfPatch + 1) {
+      for (int k = 0; k <= kHalfPatch; ++k) {
+        const int v = half ? k + 1 : -k;
+        if (v > kHalfPatch) break;
+        const int av = v < 0 ? -v : v;
+        if ((u < 0 ? -u : u) <= P.umax[av]) {
+          const int val = center[u + v * step];
+          m10 += u * val;
+          m01 += v * val;
+        }
+      }
+    }
+    m10 = wave_isum(m10);
+    m01 = wave_isum(m01);
+  }
+  const float ang = fast_atan2((float)m01, (float)m10);
+  // computeOrbDescriptor on the blurred level
+  const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+  const float angle = ang * factorPI;
+  const float a = (float)cos((double)angle), b = (float)sin((double)angle);
+  const uint8_t* center = P.blur + P.offset[l] + (int64_t)cy * step + cx;
+  int nib = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int* p0 = s_pat + 4 * (4 * lane + k);  // pair 4 lane + k = bit (4 lane + k) & 7 of byte lane / 2
+    const int t0 = center[__float2int_rn(p0[0] * b + p0[1] * a) * step + __float2int_rn(p0[0] * a - p0[1] * b)];
+    const int t1 = center[__float2int_rn(p0[2] * b + p0[3] * a) * step + __float2int_rn(p0[2] * a - p0[3] * b)];
+    nib |= (t0 < t1) << k;
+  }
+  const int hi = __shfl_down(nib, 1, 64);
+  if ((lane & 1) == 0) desc_out[32 * (size_t)i + (lane >> 1)] = (uint8_t)(nib | (hi << 4));
+  if (lane == 0) angle_out[i] = ang;
+}
+
+// cv::getGaussianKernel(7, 2, CV_32F) * 256, rounded (convertTo CV_32S, float arithmetic)
+void gauss_taps(int* k7) {
+  float cf[7];
+  double sum = 0;
+  const double sigmaX = 2.0, scale2X = -0.5 / (sigmaX * sigmaX);
+  for (int i = 0; i < 7; i++) {
+    const double x = i - (7 - 1) * 0.5;
+    cf[i] = (float)std::exp(scale2X * x * x);
+    sum += cf[i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < 7; i++) cf[i] = (float)(cf[i] * sum);
+  for (int i = 0; i < 7; i++) k7[i] = (int)std::nearbyint(cf[i] * 256.f);
+}
+
+// ORBextractor::ORBextractor, src/ORBextractor.cpp:469-483
+void orb_umax(int* umax) {
+  int v, v0;
+  const int vmax = (int)std::floor(kHalfPatch * std::sqrt(2.f) / 2 + 1);
+  const int vmin = (int)std::ceil(kHalfPatch * std::sqrt(2.f) / 2);
+  const double hp2 = kHalfPatch * kHalfPatch;
+  for (v = 0; v <= vmax; ++v) umax[v] = (int)std::nearbyint(std::sqrt(hp2 - v * v));
+  for (v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+    while (umax[v0] == umax[v0 + 1]) ++v0;
+    umax[v] = v0;
+    ++v0;
+  }
+}
+
+int64_t pyr_extent(const lorb_image_pyramid* p) {
+  int64_t e = 0;
+  for (int l = 0; l < p->n_levels; l++)
+    if (p->rows[l] > 0) e = std::max<int64_t>(e, p->offset[l] + (int64_t)(p->rows[l] - 1) * p->step[l] + p->cols[l]);
+  return e;
+}
+
+int check_orb(lorb_ctx* ctx, const lorb_image_pyramid* p, int n) {
+  if (!p || n < 0) return lorb::set_error(ctx, LORB_E_INVALID, "null pyramid or negative count");
+  if (p->n_levels < 1 || p->n_levels > LORB_MAX_LEVELS || !p->data)
+    return lorb::set_error(ctx, LORB_E_INVALID, "pyramid n_levels %d out of range (or no data)", p->n_levels);
+  for (int l = 0; l < p->n_levels; l++)
+    if (p->rows[l] < 1 || p->cols[l] < 1 || p->step[l] < p->cols[l] || p->offset[l] < 0)
+      return lorb::set_error(ctx, LORB_E_INVALID, "pyramid level %d: bad geometry", l);
+  return LORB_OK;
+}
+
+enum { S_ORB = 48 };  // shares the stereo family's slots (calls on one ctx are serialized)
+
+int enqueue_orb(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const uint8_t* d_data, int n, const float* d_x,
+                const float* d_y, const int* d_lev, const int* d_pat, float* d_ang, uint8_t* d_desc) {
+  OrbPyr P{};
+  P.data = d_data;
+  P.n_levels = pyr->n_levels;
+  int tiles = 0;
+  for (int l = 0; l < pyr->n_levels; l++) {
+    P.offset[l] = pyr->offset[l]; P.rows[l] = pyr->rows[l]; P.cols[l] = pyr->cols[l]; P.step[l] = pyr->step[l];
+    P.tile_off[l] = tiles;
+    P.tiles_x[l] = (pyr->cols[l] + kTileW - 1) / kTileW;
+    tiles += P.tiles_x[l] * ((pyr->rows[l] + kTileH - 1) / kTileH);
+  }
+  P.tile_off[pyr->n_levels] = tiles;
+  gauss_taps(P.k);
+  orb_umax(P.umax);
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 0, (size_t)pyr_extent(pyr), &P.blur));
+  hipLaunchKernelGGL(k_orb_blur, dim3(tiles), dim3(256), 0, ctx->stream, P);
+  if (n > 0)
+    hipLaunchKernelGGL(k_orb_desc, dim3(lorb::ceil_div(n, kDescWaves)), dim3(64 * kDescWaves), 0, ctx->stream, P, n,
+                       d_x, d_y, d_lev, d_pat, d_ang, d_desc);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lorb_orb_describe_dev(lorb_ctx* ctx, const lorb_image_pyramid* d_pyr, int32_t n, const float* d_x,
+                          const float* d_y, const int32_t* d_level, const int32_t* d_pattern, float* d_angle,
+                          uint8_t* d_desc) {
+  if (!ctx) return LORB_E_INVALID;
+  LORB_TRY(check_orb(ctx, d_pyr, n));
+  if (n > 0 && (!d_x || !d_y || !d_level || !d_pattern || !d_angle || !d_desc))
+    return lorb::set_error(ctx, LORB_E_INVALID, "null keypoint / pattern / output array");
+  return enqueue_orb(ctx, d_pyr, d_pyr->data, n, d_x, d_y, d_level, d_pattern, d_angle, d_desc);
+}
+
+int lorb_orb_describe(lorb_ctx* ctx, const lorb_image_pyramid* pyr, int32_t n, const float* x, const float* y,
+                      const int32_t* level, const int32_t* pattern, float* angle, uint8_t* desc) {
+  if (!ctx) return LORB_E_INVALID;
+  LORB_TRY(check_orb(ctx, pyr, n));
+  if (n > 0 && (!x || !y || !level || !pattern || !angle || !desc))
+    return lorb::set_error(ctx, LORB_E_INVALID, "null keypoint / pattern / output array");
+  // the defined domain: every patch and test pair inside the level (the extractor keeps keypoints
+  // EDGE_THRESHOLD = 19 pixels from each level border, src/ORBextractor.cpp:76, 912-915)
+  for (int i = 0; i < n; i++) {
+    const int l = level[i];
+    if (l < 0 || l >= pyr->n_levels)
+      return lorb::set_error(ctx, LORB_E_INVALID, "keypoint %d: level %d out of range", i, l);
+    const long cx = std::lrint(x[i]), cy = std::lrint(y[i]);
+    if (cx < 19 || cy < 19 || cx > pyr->cols[l] - 20 || cy > pyr->rows[l] - 20)
+      return lorb::set_error(ctx, LORB_E_INVALID, "keypoint %d (%g, %g) closer than 19 px to level %d border", i,
+                             (double)x[i], (double)y[i], l);
+  }
+  uint8_t* dd;
+  float *dx, *dy, *dang;
+  int *dl, *dp;
+  uint8_t* ddesc;
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 1, pyr->data, (size_t)pyr_extent(pyr), &dd));
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 2, x, (size_t)n, &dx));
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 3, y, (size_t)n, &dy));
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 4, level, (size_t)n, &dl));
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 5, pattern, (size_t)1024, &dp));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 6, (size_t)std::max(n, 1), &dang));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 7, (size_t)std::max(n, 1) * 32, &ddesc));
+  LORB_TRY(enqueue_orb(ctx, pyr, dd, n, dx, dy, dl, dp, dang, ddesc));
+  if (n > 0) {
+    LORB_HIP(ctx, hipMemcpyAsync(angle, dang, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(desc, ddesc, (size_t)32 * n, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+}  // extern "C"

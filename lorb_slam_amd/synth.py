@@ -388,3 +388,19 @@ def stereo_problem(seed=21, n_left=2000, n_distract=800, frac_true=0.75, width=W
     right = {k_: v[perm] for k_, v in right.items()}
     left = dict(x=x, y=y, octave=octv, desc=desc)
     return dict(fp=frame_params(width=width, height=height), left=left, right=right, pyr_l=pyr_l, pyr_r=pyr_r)
+
+
+def orb_problem(seed=31, n_kps=2000, width=W, height=H, border=19):
+    """ORBextractor descriptor-stage inputs: an 8-level textured pyramid, keypoints
+    in level coordinates at least `border` pixels inside their level (EDGE_THRESHOLD = 19), and a
+    random 256-pair test pattern with ORB's coordinate range [-13, 12]."""
+    rng = np.random.default_rng(seed)
+    sp = stereo_problem(seed=seed, n_left=1, n_distract=1, width=width, height=height)
+    pyr = sp["pyr_l"]
+    lev = rng.choice(N_LEVELS, size=n_kps, p=level_probs()).astype(np.int32)
+    rows = np.array([p.shape[0] for p in pyr])[lev]
+    cols = np.array([p.shape[1] for p in pyr])[lev]
+    x = (border + rng.uniform(0, 1, n_kps) * (cols - 2 * border - 1)).astype(np.float32)
+    y = (border + rng.uniform(0, 1, n_kps) * (rows - 2 * border - 1)).astype(np.float32)
+    pattern = rng.integers(-13, 13, size=1024).astype(np.int32)
+    return dict(pyr=pyr, x=x, y=y, level=lev, pattern=pattern)

@@ -137,6 +137,33 @@ def _compute_stereo_matches(self, fp, left, right, pyr_l, pyr_r, device_resident
     return out
 
 
+def _orb_describe(self, pyr, x, y, level, pattern, device_resident=False):
+    """ORBextractor descriptor stage -> (angle, desc).  device_resident=True stages the inputs in
+    device memory first and calls lorb_orb_describe_dev."""
+    buf, P = A.pack_pyramid(pyr)
+    x, y, level, pattern = A.f32(x), A.f32(y), A.i32(level), A.i32(pattern).reshape(-1)
+    n = len(x)
+    if not device_resident:
+        P.data = buf.ctypes.data
+        ang = np.empty(max(n, 1), np.float32)
+        desc = np.empty((max(n, 1), 32), np.uint8)
+        self.check(lib().lorb_orb_describe(self._p, C.byref(P), C.c_int32(n), A.ptr(x, C.c_float), A.ptr(y, C.c_float),
+                                           A.ptr(level, C.c_int32), A.ptr(pattern, C.c_int32), A.ptr(ang, C.c_float),
+                                           A.ptr(desc, C.c_uint8)), "lorb_orb_describe")
+        return ang[:n].copy(), desc[:n].copy()
+    keep = [self.to_device(a) for a in (buf, x, y, level, pattern)]
+    P.data = keep[0].ptr
+    ang, desc = self.empty(max(n, 1), np.float32), self.empty((max(n, 1), 32), np.uint8)
+    keep += [ang, desc]
+    self.check(lib().lorb_orb_describe_dev(self._p, C.byref(P), C.c_int32(n), keep[1].ptr, keep[2].ptr, keep[3].ptr,
+                                           keep[4].ptr, ang.ptr, desc.ptr), "lorb_orb_describe_dev")
+    out = ang.numpy()[:n], desc.numpy()[:n]
+    for a in keep:
+        a.free()
+    return out
+
+
+Context.orb_describe = _orb_describe
 Context.compute_stereo_matches = _compute_stereo_matches
 Context.track_local_map = _track_local_map
 Context.search_by_projection_frame = _search_by_projection_frame

@@ -105,6 +105,18 @@ int or_compute_stereo_matches(const lorb_frame_params* fp, const lorb_stereo_key
                               const lorb_image_pyramid* PL, const lorb_image_pyramid* PR, float* u_right,
                               float* depth);
 
+/* orb.c: the descriptor stage of ORBextractor::operator() (src/ORBextractor.cpp:79-150, 469-493,
+ * 1131-1132) with OpenCV 3.1's fastAtan2 / getGaussianKernel / fixed-point 8U smoothing restated */
+void or_orb_umax(int* umax);
+float or_fast_atan2(float y, float x);
+void or_orb_gauss_kernel(int32_t* k7);
+void or_orb_blur(const uint8_t* src, int rows, int cols, int sstep, uint8_t* dst, int dstep);
+float or_orb_ic_angle(const uint8_t* img, int step, float px, float py, const int* umax);
+void or_orb_descriptor(const uint8_t* img, int step, float px, float py, float angle_deg, const int32_t* pattern,
+                       uint8_t* desc);
+void or_orb_describe(const lorb_image_pyramid* P, int n, const float* x, const float* y, const int32_t* level,
+                     const int32_t* pattern, float* angle, uint8_t* desc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -266,3 +266,42 @@ def compute_stereo_matches(fp, left, right, pyr_l, pyr_r):
     npair = lib().or_compute_stereo_matches(C.byref(fps), C.byref(kl), C.byref(kr), C.byref(pl), C.byref(pr),
                                             A.ptr(ur, C.c_float), A.ptr(dp, C.c_float))
     return ur[:n].copy(), dp[:n].copy(), npair
+
+
+def orb_umax():
+    u = np.zeros(16, np.int32)
+    lib().or_orb_umax(A.ptr(u, C.c_int32))
+    return u
+
+
+def orb_gauss_kernel():
+    k = np.zeros(7, np.int32)
+    lib().or_orb_gauss_kernel(A.ptr(k, C.c_int32))
+    return k
+
+
+def fast_atan2(y, x):
+    lib().or_fast_atan2.restype = C.c_float
+    return np.float32(lib().or_fast_atan2(C.c_float(y), C.c_float(x)))
+
+
+def orb_blur(img):
+    img = A.u8(img)
+    out = np.empty_like(img)
+    lib().or_orb_blur(A.ptr(img, C.c_uint8), C.c_int(img.shape[0]), C.c_int(img.shape[1]), C.c_int(img.shape[1]),
+                      A.ptr(out, C.c_uint8), C.c_int(img.shape[1]))
+    return out
+
+
+def orb_describe(pyr, x, y, level, pattern):
+    """Descriptor stage of ORBextractor::operator() (src/ORBextractor.cpp:1087-1154): angle per keypoint
+    (IC_Angle on the raw level) and the 32-byte rBRIEF descriptor on the blurred level."""
+    buf, P = A.pack_pyramid(pyr)
+    P.data = buf.ctypes.data
+    x, y, level, pattern = A.f32(x), A.f32(y), A.i32(level), A.i32(pattern).reshape(-1)
+    n = len(x)
+    ang = np.zeros(max(n, 1), np.float32)
+    desc = np.zeros((max(n, 1), 32), np.uint8)
+    lib().or_orb_describe(C.byref(P), C.c_int(n), A.ptr(x, C.c_float), A.ptr(y, C.c_float), A.ptr(level, C.c_int32),
+                          A.ptr(pattern, C.c_int32), A.ptr(ang, C.c_float), A.ptr(desc, C.c_uint8))
+    return ang[:n].copy(), desc[:n].copy()

@@ -164,3 +164,73 @@ def compute_stereo_matches(fp, left, right, pyr_l, pyr_r):  # src/frame.cpp:125-
                 break
             ur[i] = -1; dp[i] = -1
     return ur, dp, len(pairs)
+
+
+def orb_blur(img):  # GaussianBlur 7x7 sigma 2 REFLECT_101, OpenCV 3.1 8U fixed point (via scipy)
+    from scipy.ndimage import correlate1d
+    cf = np.array([np.float32(math.exp(-0.125 * (i - 3) ** 2)) for i in range(7)], np.float32)
+    s = 1.0 / float(np.sum(cf.astype(np.float64)))
+    cf = np.array([np.float32(float(c) * s) for c in cf], np.float32)
+    k = np.rint(cf * np.float32(256)).astype(np.int64)
+    r = correlate1d(img.astype(np.int64), k, axis=1, mode="mirror")
+    c = correlate1d(r, k, axis=0, mode="mirror")
+    return np.clip((c + (1 << 15)) >> 16, 0, 255).astype(np.uint8)
+
+
+def fast_atan2(y, x):  # cv::fastAtan2 (OpenCV 3.1) in float32
+    k = f32(180 / math.pi)
+    p1, p3 = f32(f32(0.9997878412794807) * k), f32(f32(-0.3258083974640975) * k)
+    p5, p7 = f32(f32(0.1555786518463281) * k), f32(f32(-0.04432655554792128) * k)
+    x, y = f32(x), f32(y)
+    ax, ay = abs(x), abs(y)
+    eps = f32(np.finfo(np.float64).eps)
+    if ax >= ay:
+        c = f32(ay / f32(ax + eps)); c2 = f32(c * c)
+        a = f32(f32(f32(f32(f32(f32(f32(p7 * c2) + p5) * c2) + p3) * c2) + p1) * c)
+    else:
+        c = f32(ax / f32(ay + eps)); c2 = f32(c * c)
+        a = f32(f32(90) - f32(f32(f32(f32(f32(f32(f32(p7 * c2) + p5) * c2) + p3) * c2) + p1) * c))
+    if x < 0:
+        a = f32(f32(180) - a)
+    if y < 0:
+        a = f32(f32(360) - a)
+    return a
+
+
+def orb_describe(pyr, x, y, level, pattern):  # src/ORBextractor.cpp:79-150, 469-493, 1131-1132
+    umax = np.zeros(16, np.int64)
+    for v in range(0, 12):
+        umax[v] = int(np.rint(math.sqrt(225 - v * v)))
+    v0 = 0
+    for v in range(15, 10, -1):
+        while umax[v0] == umax[v0 + 1]:
+            v0 += 1
+        umax[v] = v0
+        v0 += 1
+    blurred = [orb_blur(p) for p in pyr]
+    pat = np.asarray(pattern, np.int64).reshape(512, 2)
+    ang = np.zeros(len(x), np.float32)
+    desc = np.zeros((len(x), 32), np.uint8)
+    for i in range(len(x)):
+        img = pyr[level[i]].astype(np.int64)
+        cx, cy = int(np.rint(f32(x[i]))), int(np.rint(f32(y[i])))
+        m10 = m01 = 0
+        for v in range(-15, 16):
+            d = umax[abs(v)]
+            row = img[cy + v, cx - d:cx + d + 1]
+            u = np.arange(-d, d + 1)
+            m10 += int((u * row).sum()); m01 += v * int(row.sum())
+        ang[i] = fast_atan2(f32(m01), f32(m10))
+        angle = f32(ang[i] * f32(math.pi / 180.0))
+        a, b = f32(math.cos(float(angle))), f32(math.sin(float(angle)))
+        bl = blurred[level[i]]
+        bits = []
+        for p in range(512):
+            px, py = f32(pat[p, 0]), f32(pat[p, 1])
+            r = int(np.rint(f32(f32(px * b) + f32(py * a))))
+            c = int(np.rint(f32(f32(px * a) - f32(py * b))))
+            bits.append(int(bl[cy + r, cx + c]))
+        t = np.array(bits).reshape(256, 2)
+        bv = (t[:, 0] < t[:, 1]).astype(np.uint8).reshape(32, 8)
+        desc[i] = (bv << np.arange(8, dtype=np.uint8)).sum(1).astype(np.uint8)
+    return ang, desc

@@ -154,3 +154,22 @@ def test_compute_stereo_matches_edges(ctx):
     ur, dp = ctx.compute_stereo_matches(fp, one, R, pl, prr)
     o = O.compute_stereo_matches(fp, one, R, pl, prr)
     assert np.array_equal(ur, o[0]) and np.array_equal(dp, o[1])
+
+
+@pytest.mark.parametrize("seed,n,dev", [(31, 2000, False), (32, 5000, True), (33, 1, False)])
+def test_orb_describe(ctx, seed, n, dev):
+    """ORB descriptor stage (IC_Angle + GaussianBlur + rBRIEF) bit-exact vs the oracle."""
+    pr = synth.orb_problem(seed=seed, n_kps=n)
+    ang, desc = ctx.orb_describe(pr["pyr"], pr["x"], pr["y"], pr["level"], pr["pattern"], device_resident=dev)
+    oang, odesc = O.orb_describe(pr["pyr"], pr["x"], pr["y"], pr["level"], pr["pattern"])
+    assert np.array_equal(ang, oang)
+    assert np.array_equal(desc, odesc)
+
+
+def test_orb_describe_edges(ctx):
+    pr = synth.orb_problem(seed=34, n_kps=10)
+    ang, desc = ctx.orb_describe(pr["pyr"], pr["x"][:0], pr["y"][:0], pr["level"][:0], pr["pattern"])
+    assert len(ang) == 0 and desc.shape == (0, 32)
+    x = pr["x"].copy(); x[3] = 5.0  # inside the 19-pixel border: rejected, not read out of bounds
+    with pytest.raises(Exception):
+        ctx.orb_describe(pr["pyr"], x, pr["y"], pr["level"], pr["pattern"])

@@ -69,3 +69,19 @@ def test_stereo_oracle_vs_pyref(seed):
     b = pyref.compute_stereo_matches(pr["fp"], pr["left"], pr["right"], pr["pyr_l"], pr["pyr_r"])
     assert a[2] == b[2] and a[2] > 100
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_orb_oracle_vs_pyref():
+    """ORB descriptor stage: C restatement == independent numpy/scipy restatement (blur via
+    scipy.ndimage mirror correlation, moments via numpy), bit for bit."""
+    pr = synth.orb_problem(seed=31, n_kps=120)
+    for lv in (0, 3, 7):
+        assert np.array_equal(O.orb_blur(pr["pyr"][lv]), pyref.orb_blur(pr["pyr"][lv]))
+    a = O.orb_describe(pr["pyr"], pr["x"], pr["y"], pr["level"], pr["pattern"])
+    b = pyref.orb_describe(pr["pyr"], pr["x"], pr["y"], pr["level"], pr["pattern"])
+    assert np.array_equal(a[0], b[0])
+    assert np.array_equal(a[1], b[1])
+    assert O.orb_gauss_kernel().tolist() == [18, 34, 49, 55, 49, 34, 18]
+    assert O.orb_umax().tolist() == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+    for yx in [(1.0, 1.0), (-3.0, 2.0), (0.0, -5.0), (7.5, -0.25), (0.0, 0.0)]:
+        assert O.fast_atan2(*yx) == pyref.fast_atan2(*yx)
