@@ -2,7 +2,8 @@
 the _dev entry points) and the single-thread oracle on the same inputs.
   lorb_compute_stereo_matches_dev  (row 2, one stereo frame: 2000 left / 2800 right keypoints, 752x480)
   lorb_track_local_map_dev         (row 1, 2000 keypoints x 3000 local map points)
-  lorb_compute_descriptor_dev      (row 4, 3000 points x 8 observations)"""
+  lorb_compute_descriptor_dev      (row 4, 3000 points x 8 observations)
+  lorb_orb_describe_dev            (row 3 descriptor stage, 2000 keypoints on a 752x480 8-level pyramid)"""
 import ctypes as C
 import json
 import os
@@ -98,4 +99,18 @@ us = timed(lambda: ctx.check(lib().lorb_compute_descriptor_dev(ctx.handle, C.c_i
                              "compute_descriptor"))
 out["compute_descriptor"] = dict(gpu_us=us, cpu_us=cpu(lambda: O.compute_descriptor(d_off, desc)), n_points=npd,
                                  obs_per_point=nobs)
+# row 3: ORB descriptor stage (blur of all 8 levels + orientation + rBRIEF)
+op = synth.orb_problem(seed=31, n_kps=2000)
+buf, P = A.pack_pyramid(op["pyr"])
+P.data = dev(buf, np.uint8)
+ox, oy, ol, opat = (dev(op[k], t) for k, t in (("x", np.float32), ("y", np.float32), ("level", np.int32),
+                                               ("pattern", np.int32)))
+oang, odesc = ctx.empty(2000, np.float32), ctx.empty((2000, 32), np.uint8)
+us = timed(lambda: ctx.check(lib().lorb_orb_describe_dev(ctx.handle, C.byref(P), C.c_int32(2000), ox, oy, ol, opat,
+                                                         oang.ptr, odesc.ptr), "orb_describe"))
+ra, rd = O.orb_describe(op["pyr"], op["x"], op["y"], op["level"], op["pattern"])
+assert np.array_equal(odesc.numpy(), rd) and np.array_equal(oang.numpy(), ra)
+out["orb_describe"] = dict(gpu_us=us, cpu_us=cpu(lambda: O.orb_describe(op["pyr"], op["x"], op["y"], op["level"],
+                                                                        op["pattern"])),
+                           n_kps=2000, pyramid="752x480, 8 levels x 1.2")
 print(json.dumps(out))
