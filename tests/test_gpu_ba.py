@@ -119,3 +119,29 @@ def test_local_ba_dense_covisibility(ctx, n_kf, n_pts):
     assert sg[0]["iterations"] == so[0]["iterations"]
     assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
     assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
+
+
+def test_local_ba_c4_full_size(ctx):
+    """BASELINE config 3 (the bench workload): 50 KF / 10k points / 77k obs (+5 fixed KFs), 10 LM its,
+    at full size against the oracle."""
+    w = synth.ba_window(seed=4, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400)
+    assert len(w["obs_point"]) == 77000
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    Pg, Xg, sg = ctx.ba_local([w], opt)
+    Po, Xo, so = O.ba_local([w], opt)
+    assert sg[0]["iterations"] == so[0]["iterations"] == 10
+    assert sg[0]["successful_steps"] == so[0]["successful_steps"]
+    assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
+    assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
+
+
+def test_local_ba_eight_c4_windows_independent(ctx):
+    """BASELINE config 4 shape on one GPU: 8 C4 windows in one plan.  Size-independent property:
+    batching never couples windows -- each window's result is bit-identical to its solo solve."""
+    wins = [synth.ba_window(seed=40 + i, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400) for i in range(8)]
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    Pb, Xb, sb = ctx.ba_local(wins, opt)
+    for i in (0, 5):
+        Ps, Xs, ss = ctx.ba_local([wins[i]], opt)
+        assert np.array_equal(Pb[i], Ps[0]) and np.array_equal(Xb[i], Xs[0])
+        assert sb[i]["final_cost"] == ss[0]["final_cost"]
