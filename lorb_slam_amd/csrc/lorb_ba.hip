@@ -622,12 +622,18 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// v_rsq_f64 is accurate to about 2^-22 relative; each Newton step squares the error.  Two steps
+// reach full double precision; LORB_RSQ_STEPS=1 stops at ~1e-14.
+#ifndef LORB_RSQ_STEPS
+#define LORB_RSQ_STEPS 2
+#endif
 __device__ __forceinline__ double rsqrt_refined(double a) {
   double y = __builtin_amdgcn_rsq(a);
-  double e = fma(-a * y, y, 1.0);
-  y = fma(0.5 * y, e, y);
-  e = fma(-a * y, y, 1.0);
-  y = fma(0.5 * y, e, y);
+#pragma unroll
+  for (int s = 0; s < LORB_RSQ_STEPS; ++s) {
+    const double e = fma(-a * y, y, 1.0);
+    y = fma(0.5 * y, e, y);
+  }
   return y;
 }
 
