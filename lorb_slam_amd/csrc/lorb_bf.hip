@@ -39,11 +39,14 @@ struct BfTile {
 
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t r;
-  asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  // not volatile: a pure value, so the scheduler may interleave independent pairs' chains
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
   return r;
 }
 
 // popcount-accumulate chain: one v_xor_b32 + one v_bcnt_u32_b32 per 32-bit word (16 VALU/pair)
+// (written as asm: from __builtin_popcount(x) + acc the compiler emits v_bcnt x, 0 plus v_add3
+// trees, 12% slower here)
 __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
   uint32_t r;
   asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
@@ -63,7 +66,7 @@ __device__ __forceinline__ uint32_t hamming256(const uint4& a0, const uint4& a1,
   return d;
 }
 
-// QPL = lane-side descriptors per thread (1 or 2): a block covers 256*QPL lane items; every
+// QPL = lane-side descriptors per thread (1, 2 or 4; LORB_BF_QPL): a block covers 256*QPL lane items; every
 // uniform descriptor loaded into SGPRs feeds QPL distance chains.
 template <bool TOP2, int QPL>
 __global__ __launch_bounds__(256) void k_bf_scan(const uint4* __restrict__ lane_desc,
@@ -89,10 +92,21 @@ __global__ __launch_bounds__(256) void k_bf_scan(const uint4* __restrict__ lane_
   const uint32_t kb = (uint32_t)tl.uni_local0;
   const int n = tl.uni_count;
   int j = 0;
+  // 4 train descriptors per step in SGPRs (s_load); the next step's are requested before this
+  // step's 19 x 4 x QPL VALU ops, so the scalar-cache / L2 latency hides behind them
+  uint4 bn[8];
+  if (n >= 4) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) bn[s] = u[s];
+  }
   for (; j + 4 <= n; j += 4) {
     uint4 b[8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) b[s] = u[2 * j + s];  // 4 descriptors -> SGPRs (s_load) up front
+    for (int s = 0; s < 8; ++s) b[s] = bn[s];
+    if (j + 8 <= n) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) bn[s] = u[2 * (j + 4) + s];
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
 #pragma unroll
@@ -393,7 +407,11 @@ int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, con
          const int32_t* u_off, uint32_t** k1_final, uint32_t** k2_final, const int32_t* u_base = nullptr) {
   std::vector<BfTile> tiles;
   int n_chunks = 1;
-  static const int qpl = [] { const char* e = getenv("LORB_BF_QPL"); return (e && atoi(e) == 1) ? 1 : 2; }();
+  static const int qpl = [] {
+    const char* e = getenv("LORB_BF_QPL");
+    const int v = e ? atoi(e) : 2;
+    return v == 1 || v == 4 ? v : 2;
+  }();
   LORB_TRY(build_tiles(ctx, np, l_off, u_off, 256 * qpl, tiles, &n_chunks, u_base));
   const int nl = l_off[np] - l_off[0];
   BfTile* d_tiles = nullptr;
@@ -405,6 +423,10 @@ int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, con
     lorb::KernelTimer kt(ctx, TOP2 ? LORB_K_BF_SCAN_TOP2 : LORB_K_BF_SCAN_TOP1);
     if (qpl == 2)
       hipLaunchKernelGGL((k_bf_scan<TOP2, 2>), dim3((unsigned)tiles.size()), dim3(256), 0, ctx->stream,
+                         reinterpret_cast<const uint4*>(d_lane), reinterpret_cast<const uint4*>(d_uni),
+                         d_tiles, k1, k2);
+    else if (qpl == 4)
+      hipLaunchKernelGGL((k_bf_scan<TOP2, 4>), dim3((unsigned)tiles.size()), dim3(256), 0, ctx->stream,
                          reinterpret_cast<const uint4*>(d_lane), reinterpret_cast<const uint4*>(d_uni),
                          d_tiles, k1, k2);
     else

@@ -19,6 +19,7 @@ tools/gpu_step.sh 300 $O/pmc_fetch.log rocprofv3 --pmc FETCH_SIZE -d $P/fetch -o
 tools/gpu_step.sh 300 $O/pmc_write.log rocprofv3 --pmc WRITE_SIZE -d $P/write -o ${TAG}_c4_write \
   --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $?
 python tools/pmc_traffic.py $P $O/${TAG}_traffic.json > $O/traffic.log 2>&1
+tools/gpu_step.sh 300 $O/bench_c2.log python bench.py --workload c2 --steps 20 --warmup 3 || exit $?
 tools/gpu_step.sh 300 $O/bench_shared.log python bench.py --workload shared --steps 5 --warmup 1 || exit $?
 tools/gpu_step.sh 300 $O/prof_shared.log rocprofv3 --kernel-trace --stats -d $P/stats_shared -o ${TAG}_shared \
   --output-format csv -- python3 $R/bench.py --workload shared --steps 5 --warmup 1 --no-cpu-baseline || exit $?
