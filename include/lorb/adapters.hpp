@@ -18,6 +18,7 @@
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../lorb_c.h"
@@ -348,6 +349,95 @@ void LocalPoseOptimization(lorb_ctx* ctx, FrameT* cur) {
     const float X[3] = {(float)pt[3 * i], (float)pt[3 * i + 1], (float)pt[3 * i + 2]};
     PT::set_pos(points[i], X);
   }
+}
+
+// ---- the callers either side of the path ---------------------------------
+
+// One camera's ORBextractor::mvImagePyramid packed into one buffer (levels are separate cv::Mat
+// ROIs in the reference; the C-ABI takes one buffer + per-level offsets).
+struct PyramidPack {
+  std::vector<uint8_t> buf;
+  lorb_image_pyramid view;
+};
+template <class FrameT>
+PyramidPack pack_pyramid(FrameT* F, int side /* 0 left, 1 right */) {
+  using FT = FrameTraits<FrameT>;
+  PyramidPack p;
+  std::memset(&p.view, 0, sizeof(p.view));
+  const int L = FT::num_levels(F);
+  p.view.n_levels = L;
+  std::vector<const uint8_t*> src(L);
+  std::vector<int> sstep(L);
+  size_t off = 0;
+  for (int l = 0; l < L; ++l) {
+    int rows, cols;
+    FT::pyramid_level(F, side, l, &src[l], &rows, &cols, &sstep[l]);
+    p.view.offset[l] = (int64_t)off; p.view.rows[l] = rows; p.view.cols[l] = cols; p.view.step[l] = cols;
+    off += (size_t)rows * cols;
+  }
+  p.buf.resize(off > 0 ? off : 1);
+  for (int l = 0; l < L; ++l)
+    for (int r = 0; r < p.view.rows[l]; ++r)
+      std::memcpy(&p.buf[p.view.offset[l] + (size_t)r * p.view.cols[l]], src[l] + (size_t)r * sstep[l], p.view.cols[l]);
+  p.view.data = p.buf.data();
+  return p;
+}
+
+// ---- Frame::ComputeStereoMatches, src/frame.cpp:125-333 (§8f row 2) ------------------------
+// Reads mvKeys / mvKeysRight (distorted, :178, :206), both descriptor matrices and both
+// pyramids; writes mvuRight / mvDepth (:127-128, :310-311, :329-330).
+template <class FrameT>
+void ComputeStereoMatches(lorb_ctx* ctx, FrameT* F) {
+  using FT = FrameTraits<FrameT>;
+  const size_t nl = FT::num_keypoints(F), nr = FT::num_right_keypoints(F);
+  std::vector<float> lx(nl + 1), ly(nl + 1), rx(nr + 1), ry(nr + 1);
+  std::vector<int32_t> lo(nl + 1), ro(nr + 1);
+  std::vector<uint8_t> ld(32 * nl + 32), rd(32 * nr + 32);
+  for (size_t i = 0; i < nl; ++i) {
+    FT::raw_keypoint(F, i, &lx[i], &ly[i], &lo[i]);
+    FT::descriptor(F, i, &ld[32 * i]);
+  }
+  for (size_t i = 0; i < nr; ++i) {
+    FT::right_keypoint(F, i, &rx[i], &ry[i], &ro[i]);
+    FT::right_descriptor(F, i, &rd[32 * i]);
+  }
+  const lorb_stereo_keys L{(int32_t)nl, lx.data(), ly.data(), lo.data(), ld.data()};
+  const lorb_stereo_keys R{(int32_t)nr, rx.data(), ry.data(), ro.data(), rd.data()};
+  const PyramidPack pl = pack_pyramid(F, 0), pr = pack_pyramid(F, 1);
+  const lorb_frame_params fp = frame_params(F);
+  std::vector<float> uR(nl + 1, -1.0f), depth(nl + 1, -1.0f);
+  check(ctx, lorb_compute_stereo_matches(ctx, &fp, &L, &R, &pl.view, &pr.view, uR.data(), depth.data()),
+        "lorb_compute_stereo_matches");
+  FT::set_stereo(F, uR.data(), depth.data(), nl);
+}
+
+// ---- MapPoint::ComputeDescriptor, src/map_point.cpp:69-129, batched (§8f row 4) -----------
+// Candidates: the observations in std::map<Frame*, size_t> order, bad frames skipped (:74-81).
+// A point with no candidate keeps its descriptor (the reference indexes an empty vector there).
+template <class PointT>
+void ComputeDescriptors(lorb_ctx* ctx, const std::vector<PointT*>& mps) {
+  using PT = PointTraits<PointT>;
+  using ObsMap = decltype(PT::observations(std::declval<PointT*>()));
+  using FrameT = std::remove_pointer_t<typename std::decay_t<ObsMap>::key_type>;
+  using FT = FrameTraits<FrameT>;
+  std::vector<int32_t> off(1, 0);
+  std::vector<uint8_t> desc;
+  for (PointT* p : mps) {
+    for (const auto& kv : PT::observations(p)) {
+      if (FT::is_bad(kv.first)) continue;
+      desc.resize(desc.size() + 32);
+      FT::descriptor(kv.first, kv.second, &desc[desc.size() - 32]);
+    }
+    off.push_back((int32_t)(desc.size() / 32));
+  }
+  const int32_t n = (int32_t)mps.size();
+  std::vector<int32_t> best(n + 1);
+  std::vector<uint8_t> out(32 * (size_t)n + 32);
+  if (desc.empty()) desc.resize(32);
+  check(ctx, lorb_compute_descriptor(ctx, n, off.data(), desc.data(), best.data(), out.data()),
+        "lorb_compute_descriptor");
+  for (int32_t i = 0; i < n; ++i)
+    if (best[i] >= 0) PT::set_descriptor(mps[i], &out[32 * (size_t)i]);
 }
 
 }  // namespace lorb

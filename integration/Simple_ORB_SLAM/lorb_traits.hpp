@@ -28,6 +28,30 @@ template <> struct FrameTraits<Simple_ORB_SLAM::Frame> {
   static bool has_right(F* f) { return f->mvuRight.size() == f->mnMapPoints; }     // frame.h:90
   static float u_right(F* f, size_t i) { return f->mvuRight[i]; }
   static point_type* map_point(F* f, size_t i) { return f->mvpMapPoints[i]; }    // frame.h:80
+  // SURVEY §8f row 2 (lorb::ComputeStereoMatches, called as the body of
+  // Frame::ComputeStereoMatches).  mDescriptorsRight and the extractors are private
+  // (frame.h:126-134): this binding needs `friend struct lorb::FrameTraits<Frame>;` in frame.h.
+  static void raw_keypoint(F* f, size_t i, float* x, float* y, int* o) {         // mvKeys (frame.h:94)
+    const cv::KeyPoint& k = f->mvKeys[i];
+    *x = k.pt.x; *y = k.pt.y; *o = k.octave;
+  }
+  static size_t num_right_keypoints(F* f) { return f->mvKeysRight.size(); }       // frame.h:94
+  static void right_keypoint(F* f, size_t i, float* x, float* y, int* o) {
+    const cv::KeyPoint& k = f->mvKeysRight[i];
+    *x = k.pt.x; *y = k.pt.y; *o = k.octave;
+  }
+  static void right_descriptor(F* f, size_t i, uint8_t* d) {                       // mDescriptorsRight (frame.h:132)
+    std::memcpy(d, f->mDescriptorsRight.ptr<uint8_t>((int)i), 32);
+  }
+  static int num_levels(F* f) { return (int)f->mpORBextractorLeft->mvImagePyramid.size(); }
+  static void pyramid_level(F* f, int side, int l, const uint8_t** d, int* rows, int* cols, int* step) {
+    const cv::Mat& m = (side ? f->mpORBextractorRight : f->mpORBextractorLeft)->mvImagePyramid[l];  // ORBextractor.h:85
+    *d = m.ptr<uint8_t>(); *rows = m.rows; *cols = m.cols; *step = (int)m.step;
+  }
+  static void set_stereo(F* f, const float* uR, const float* depth, size_t n) {   // mvuRight / mvDepth (frame.h:90-91)
+    f->mvuRight.assign(uR, uR + n);
+    f->mvDepth.assign(depth, depth + n);
+  }
   static void set_map_point(F* f, size_t i, point_type* p) { f->mvpMapPoints[i] = p; }
   static bool outlier(F* f, size_t i) { return f->mvbOutlier[i]; }                // frame.h:92
   static void params(F* f, lorb_frame_params* fp) {                                // frame.h:96-110
@@ -79,6 +103,12 @@ template <> struct PointTraits<Simple_ORB_SLAM::MapPoint> {
   static float found_ratio(P* p) { return p->GetFoundRatio(); }
   static void set_bad(P* p) { p->SetBadFlag(); }
   static size_t first_frame_id(P* p) { return p->mnFirstFId; }
+  // SURVEY §8f row 4 (lorb::ComputeDescriptors): mDescriptor is private (map_point.h:81), so
+  // batching needs `friend struct lorb::PointTraits<MapPoint>;` in map_point.h.
+  static void set_descriptor(P* p, const uint8_t* d) {
+    p->mDescriptor = cv::Mat(1, 32, CV_8U);
+    std::memcpy(p->mDescriptor.ptr<uint8_t>(), d, 32);
+  }
 };
 
 }  // namespace lorb

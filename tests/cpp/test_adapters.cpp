@@ -29,6 +29,12 @@ struct MiniPoint {
 struct MiniFrame {
   size_t id = 0;
   std::vector<float> x, y, angle, uR;
+  // stereo side: raw left keypoints = (x, y, octave); right keypoints + pyramids
+  std::vector<float> rx, ry, depth;
+  std::vector<int> roct;
+  std::vector<uint8_t> rdesc;
+  std::vector<std::vector<uint8_t>> pyr[2];
+  std::vector<int> prows, pcols;
   std::vector<int> octave;
   std::vector<uint8_t> desc;
   std::vector<MiniPoint*> mps;
@@ -68,6 +74,17 @@ template <> struct FrameTraits<MiniFrame> {
   static size_t id(MiniFrame* f) { return f->id; }
   static void update_connections(MiniFrame*) {}
   static void map_add_frame(MiniMap* m, MiniFrame* f) { m->frames.push_back(f); }
+  static void raw_keypoint(MiniFrame* f, size_t i, float* x, float* y, int* o) { *x = f->x[i]; *y = f->y[i]; *o = f->octave[i]; }
+  static size_t num_right_keypoints(MiniFrame* f) { return f->rx.size(); }
+  static void right_keypoint(MiniFrame* f, size_t i, float* x, float* y, int* o) { *x = f->rx[i]; *y = f->ry[i]; *o = f->roct[i]; }
+  static void right_descriptor(MiniFrame* f, size_t i, uint8_t* d) { memcpy(d, &f->rdesc[32 * i], 32); }
+  static int num_levels(MiniFrame* f) { return (int)f->prows.size(); }
+  static void pyramid_level(MiniFrame* f, int side, int l, const uint8_t** d, int* rows, int* cols, int* step) {
+    *d = f->pyr[side][l].data(); *rows = f->prows[l]; *cols = f->pcols[l]; *step = f->pcols[l];
+  }
+  static void set_stereo(MiniFrame* f, const float* uR, const float* depth, size_t n) {
+    f->uR.assign(uR, uR + n); f->depth.assign(depth, depth + n);
+  }
 };
 template <> struct PointTraits<MiniPoint> {
   static size_t num_obs(MiniPoint* p) { return p->nobs; }
@@ -84,6 +101,7 @@ template <> struct PointTraits<MiniPoint> {
     p->obs[f] = i; p->nobs++;
   }
   static float found_ratio(MiniPoint*) { return 1.0f; }
+  static void set_descriptor(MiniPoint* p, const uint8_t* d) { memcpy(p->desc, d, 32); }
   static void set_bad(MiniPoint* p) { p->bad = true; }
   static size_t first_frame_id(MiniPoint* p) { return p->first_id; }
 };
@@ -290,6 +308,87 @@ int main() {
     const size_t ng = lorb::SearchLocalPoints(ctx, cur, s);
     EXPECT((int)ng == no, "SearchLocalPoints gpu %zu oracle %d", ng, no);
     printf("SearchLocalPoints: %zu matches\n", ng);
+  }
+
+  // ---- Frame::ComputeStereoMatches (§8f row 2) ----------------------------------------------
+  {
+    MiniFrame* sf = make_frame(9, 1500, r0, t0);
+    const float disp = 24.37f;
+    float sc = 1.0f;
+    for (int l = 0; l < 8; l++, sc *= 1.2f) {  // textured level images, right = left shifted by disp/scale
+      const int rows = (int)lrintf(480 / sc), cols = (int)lrintf(752 / sc);
+      sf->prows.push_back(rows); sf->pcols.push_back(cols);
+      std::vector<uint8_t> L(rows * cols), R(rows * cols);
+      for (int y = 0; y < rows; y++)
+        for (int x = 0; x < cols; x++) {
+          const float fx = x * sc, fy = y * sc;
+          L[y * cols + x] = (uint8_t)(127 + 60 * sinf(fx * 0.31f + fy * 0.07f) + 50 * cosf(fy * 0.23f - fx * 0.11f) +
+                                      (float)(rnd() % 9) - 4.0f);
+          const float gx = fx + disp;
+          R[y * cols + x] = (uint8_t)(127 + 60 * sinf(gx * 0.31f + fy * 0.07f) + 50 * cosf(fy * 0.23f - gx * 0.11f) +
+                                      (float)(rnd() % 9) - 4.0f);
+        }
+      sf->pyr[0].push_back(L); sf->pyr[1].push_back(R);
+    }
+    for (size_t i = 0; i < sf->x.size(); i++) {  // keypoints away from the borders, a right twin for most
+      const float b = 24.0f * sf->fp.scale_factors[sf->octave[i]];
+      sf->x[i] = urand(b + 30, 752 - b); sf->y[i] = urand(b, 480 - b);
+      if (rnd() % 4) {
+        sf->rx.push_back(sf->x[i] - disp + urand(-0.4f, 0.4f)); sf->ry.push_back(sf->y[i] + urand(-0.5f, 0.5f));
+        sf->roct.push_back(sf->octave[i]);
+        for (int k = 0; k < 32; k++) sf->rdesc.push_back(sf->desc[32 * i + k] ^ (uint8_t)((rnd() % 16) == 0 ? 1 << (rnd() % 8) : 0));
+      }
+    }
+    lorb::ComputeStereoMatches(ctx, sf);
+    // oracle on the same inputs
+    const size_t nl = sf->x.size(), nr = sf->rx.size();
+    std::vector<int32_t> lo(sf->octave.begin(), sf->octave.end()), ro(sf->roct.begin(), sf->roct.end());
+    lorb_stereo_keys L{(int32_t)nl, sf->x.data(), sf->y.data(), lo.data(), sf->desc.data()};
+    lorb_stereo_keys R{(int32_t)nr, sf->rx.data(), sf->ry.data(), ro.data(), sf->rdesc.data()};
+    lorb::PyramidPack pl = lorb::pack_pyramid(sf, 0), pr = lorb::pack_pyramid(sf, 1);
+    std::vector<float> ouR(nl), odp(nl);
+    const int npair = or_compute_stereo_matches(&sf->fp, &L, &R, &pl.view, &pr.view, ouR.data(), odp.data());
+    int diff = 0, ndepth = 0;
+    for (size_t i = 0; i < nl; i++) {
+      diff += memcmp(&ouR[i], &sf->uR[i], 4) != 0 || memcmp(&odp[i], &sf->depth[i], 4) != 0;
+      ndepth += sf->depth[i] > 0;
+    }
+    EXPECT(diff == 0 && npair > 300, "ComputeStereoMatches: %d differing slots, %d pairs", diff, npair);
+    printf("ComputeStereoMatches: %d depths (%d pairs before the median cut), bit-exact\n", ndepth, npair);
+  }
+
+  // ---- MapPoint::ComputeDescriptor, batched (§8f row 4) ---------------------------------------
+  {
+    // more observers: three extra frames, each point seen in 0-3 of them at random slots
+    MiniFrame* ex[3];
+    for (int k = 0; k < 3; k++) ex[k] = make_frame(20 + k, 400, r0, t0);
+    ex[1]->bad = true;  // a bad observer is skipped (src/map_point.cpp:75-77)
+    for (MiniPoint* p : pts)
+      for (int k = 0; k < 3; k++)
+        if (rnd() % 2) p->obs[ex[k]] = rnd() % 400;
+    std::vector<MiniPoint*> mps;
+    std::vector<int32_t> off(1, 0);
+    std::vector<uint8_t> cand;
+    for (MiniPoint* p : pts) {
+      mps.push_back(p);
+      for (const auto& kv : p->obs)
+        if (!kv.first->bad) cand.insert(cand.end(), &kv.first->desc[32 * kv.second], &kv.first->desc[32 * kv.second] + 32);
+      off.push_back((int32_t)(cand.size() / 32));
+    }
+    std::vector<int32_t> best(mps.size() + 1);
+    if (cand.empty()) cand.resize(32);
+    or_compute_descriptor((int)mps.size(), off.data(), cand.data(), best.data());
+    std::vector<uint8_t> before(32 * mps.size());
+    for (size_t i = 0; i < mps.size(); i++) memcpy(&before[32 * i], mps[i]->desc, 32);
+    lorb::ComputeDescriptors(ctx, mps);
+    int diff = 0, changed = 0;
+    for (size_t i = 0; i < mps.size(); i++) {
+      const uint8_t* want = best[i] >= 0 ? &cand[32 * (size_t)(off[i] + best[i])] : &before[32 * i];
+      diff += memcmp(mps[i]->desc, want, 32) != 0;
+      changed += memcmp(mps[i]->desc, &before[32 * i], 32) != 0;
+    }
+    EXPECT(diff == 0, "ComputeDescriptors: %d points differ", diff);
+    printf("ComputeDescriptors: %zu points, %d descriptors changed, bit-exact\n", mps.size(), changed);
   }
 
   printf(g_fail ? "RESULT FAIL (%d)\n" : "RESULT PASS\n", g_fail);
