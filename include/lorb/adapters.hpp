@@ -440,4 +440,59 @@ void ComputeDescriptors(lorb_ctx* ctx, const std::vector<PointT*>& mps) {
     if (best[i] >= 0) PT::set_descriptor(mps[i], &out[32 * (size_t)i]);
 }
 
+// ---- VisualOdometry::EstimatePoseLocal's local-map loop, src/visual_odometry.cpp:173-201 ---
+// (§8f row 1).  For every local point neither seen in this frame yet (mnLastFrameSeen == mnId;
+// its mbTrackInView was cleared at :168) nor bad: Frame::IsInFrustum(pMP, 0.5) (src/frame.cpp:
+// 425-494) writes mbTrackInView and, in view, the tracking fields + IncreaseVisible (:190); then,
+// if any point is in view, SearchByProjection(F, localMPs, th) (:197-201).  Returns nMatches.
+template <class FrameT, class PointT>
+size_t TrackLocalMap(lorb_ctx* ctx, FrameT* F, const std::set<PointT*>& localMPs, float th = 1.0f,
+                     float viewing_cos_limit = 0.5f) {
+  using FT = FrameTraits<FrameT>;
+  using PT = PointTraits<PointT>;
+  const lorb_frame_params fp = frame_params(F);
+  float T[16];
+  FT::Tcw(F, T);
+  KeypointsSoA k = gather_keypoints(F);
+  std::vector<uint8_t> st = gather_slot_state(F);
+  const size_t n = localMPs.size();
+  std::vector<PointT*> mps;
+  mps.reserve(n);
+  std::vector<float> pos(3 * n + 3), nrm(3 * n + 3), maxd(n + 1), mind(n + 1);
+  std::vector<uint8_t> desc(32 * n + 32), locked(n + 1), bad(n + 1), inframe(n + 1);
+  for (PointT* p : localMPs) {  // std::set iteration order (:175)
+    const size_t i = mps.size();
+    mps.push_back(p);
+    PT::pos(p, &pos[3 * i]);
+    PT::normal(p, &nrm[3 * i]);
+    PT::distances(p, &maxd[i], &mind[i]);
+    PT::descriptor(p, &desc[32 * i]);
+    locked[i] = PT::num_obs(p) > 0 ? 1 : 0;
+    bad[i] = PT::is_bad(p) ? 1 : 0;
+    inframe[i] = PT::last_frame_seen(p) == FT::id(F) ? 1 : 0;
+  }
+  lorb_map_points_dev M;  // host arrays for the host entry point
+  M.n = (int32_t)n; M.pos = pos.data(); M.normal = nrm.data(); M.max_dist = maxd.data(); M.min_dist = mind.data();
+  M.desc = desc.data(); M.locked = locked.data(); M.is_bad = bad.data(); M.in_frame = inframe.data();
+  lorb_keypoints kv = k.view();
+  std::vector<uint8_t> iv(n + 1);
+  std::vector<float> tr(4 * n + 4);
+  std::vector<int32_t> lev(n + 1), assign(kv.n + 1);
+  int32_t nm = 0;
+  check(ctx, lorb_track_local_map(ctx, &fp, T, &kv, st.data(), &M, viewing_cos_limit, th, iv.data(), tr.data(),
+                                  lev.data(), assign.data(), &nm),
+        "lorb_track_local_map");
+  size_t nToMatch = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (inframe[i] || bad[i]) continue;
+    const float t4[4] = {tr[i], tr[n + i], tr[2 * n + i], tr[3 * n + i]};  // planes x, y, xr, viewcos
+    PT::set_tracking(mps[i], iv[i] != 0, t4, lev[i]);
+    if (iv[i]) { PT::increase_visible(mps[i]); ++nToMatch; }
+  }
+  if (nToMatch == 0) return 0;
+  for (int32_t j = 0; j < kv.n; ++j)
+    if (assign[j] >= 0) FT::set_map_point(F, j, mps[assign[j]]);
+  return (size_t)nm;
+}
+
 }  // namespace lorb

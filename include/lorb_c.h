@@ -248,6 +248,12 @@ int lorb_track_local_map_dev(lorb_ctx* ctx, const lorb_frame_params* frame, cons
                              const lorb_map_points_dev* pts, float viewing_cos_limit, float th,
                              uint8_t* d_in_view, float* d_track, int32_t* d_level,
                              int32_t* d_assign, int32_t* d_nmatches);
+/* host-pointer variant (synchronous): the same structs with host arrays; d_track -> track (4 x n) */
+int lorb_track_local_map(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],
+                         const lorb_keypoints* kps, const uint8_t* slot_state,
+                         const lorb_map_points_dev* pts, float viewing_cos_limit, float th,
+                         uint8_t* in_view, float* track, int32_t* level,
+                         int32_t* assign, int32_t* nmatches);
 
 /* (a20) Frame::UnprojectStereo, src/frame.cpp:335-356, batched over keypoints. */
 int lorb_unproject_stereo(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16],

@@ -103,6 +103,21 @@ template <> struct PointTraits<Simple_ORB_SLAM::MapPoint> {
   static float found_ratio(P* p) { return p->GetFoundRatio(); }
   static void set_bad(P* p) { p->SetBadFlag(); }
   static size_t first_frame_id(P* p) { return p->mnFirstFId; }
+  // SURVEY §8f row 1 (lorb::TrackLocalMap)
+  static void normal(P* p, float* n) {                                              // GetNormal (map_point.h:48)
+    const cv::Mat m = p->GetNormal();
+    n[0] = m.at<float>(0); n[1] = m.at<float>(1); n[2] = m.at<float>(2);
+  }
+  static void distances(P* p, float* mx, float* mn) { *mx = p->mfMaxDistance; *mn = p->mfMinDistance; }  // map_point.h:70
+  static size_t last_frame_seen(P* p) { return p->mnLastFrameSeen; }              // map_point.h:69
+  static void set_tracking(P* p, bool in_view, const float* t, int level) {       // IsInFrustum (frame.cpp:427, 484-490)
+    p->mbTrackInView = in_view;
+    if (in_view) {
+      p->mTrackProjX = t[0]; p->mTrackProjY = t[1]; p->mTrackProjXR = t[2]; p->mTrackViewCos = t[3];
+      p->mnTrackScaleLevel = level;
+    }
+  }
+  static void increase_visible(P* p) { p->IncreaseVisible(); }                     // map_point.cpp:167
   // SURVEY §8f row 4 (lorb::ComputeDescriptors): mDescriptor is private (map_point.h:81), so
   // batching needs `friend struct lorb::PointTraits<MapPoint>;` in map_point.h.
   static void set_descriptor(P* p, const uint8_t* d) {

@@ -19,7 +19,7 @@ struct lorb_ctx {
   std::string err;
   hipEvent_t ev[64] = {};
   // grow-only device scratch buffers, one per slot
-  static constexpr int kScratch = 64;
+  static constexpr int kScratch = 96;
   void* scratch[kScratch] = {};
   size_t scratch_sz[kScratch] = {};
   // per-kernel event timing

@@ -775,6 +775,57 @@ int lorb_track_local_map_dev(lorb_ctx* ctx, const lorb_frame_params* frame, cons
   return LORB_OK;
 }
 
+int lorb_track_local_map(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16], const lorb_keypoints* kps,
+                         const uint8_t* slot_state, const lorb_map_points_dev* pts, float viewing_cos_limit, float th,
+                         uint8_t* in_view, float* track, int32_t* level, int32_t* assign, int32_t* nmatches) {
+  if (!ctx || !frame || !Tcw || !kps || !pts || !nmatches) return LORB_E_INVALID;
+  const int nk = kps->n, np = pts->n;
+  if (nk < 0 || np < 0) return lorb::set_error(ctx, LORB_E_INVALID, "negative sizes");
+  if ((np > 0 && (!in_view || !track || !level || !pts->pos || !pts->normal || !pts->max_dist || !pts->min_dist ||
+                  !pts->desc || !pts->locked)) ||
+      (nk > 0 && (!assign || !kps->x || !kps->y || !kps->octave || !kps->angle || !kps->desc)))
+    return lorb::set_error(ctx, LORB_E_INVALID, "null array");
+  enum { S_TL = 64 };  // 64 .. 87: staging of this call
+  lorb_keypoints K{};
+  lorb_map_points_dev M{};
+  K.n = nk; M.n = np;
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 0, kps->x, (size_t)nk, const_cast<float**>(&K.x)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 1, kps->y, (size_t)nk, const_cast<float**>(&K.y)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 2, kps->octave, (size_t)nk, const_cast<int32_t**>(&K.octave)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 3, kps->angle, (size_t)nk, const_cast<float**>(&K.angle)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 4, kps->u_right, kps->u_right ? (size_t)nk : 0, const_cast<float**>(&K.u_right)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 5, kps->desc, (size_t)nk * 32, const_cast<uint8_t**>(&K.desc)));
+  uint8_t* dss;
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 6, slot_state, slot_state ? (size_t)nk : 0, &dss));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 7, pts->pos, (size_t)np * 3, const_cast<float**>(&M.pos)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 8, pts->normal, (size_t)np * 3, const_cast<float**>(&M.normal)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 9, pts->max_dist, (size_t)np, const_cast<float**>(&M.max_dist)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 10, pts->min_dist, (size_t)np, const_cast<float**>(&M.min_dist)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 11, pts->desc, (size_t)np * 32, const_cast<uint8_t**>(&M.desc)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 12, pts->locked, (size_t)np, const_cast<uint8_t**>(&M.locked)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 13, pts->is_bad, pts->is_bad ? (size_t)np : 0, const_cast<uint8_t**>(&M.is_bad)));
+  LORB_TRY(lorb::upload_t(ctx, S_TL + 14, pts->in_frame, pts->in_frame ? (size_t)np : 0,
+                          const_cast<uint8_t**>(&M.in_frame)));
+  uint8_t* div;
+  float* dtr;
+  int32_t *dlv, *das, *dnm;
+  LORB_TRY(lorb::scratch_t(ctx, S_TL + 15, (size_t)std::max(np, 1), &div));
+  LORB_TRY(lorb::scratch_t(ctx, S_TL + 16, (size_t)std::max(np, 1) * 4, &dtr));
+  LORB_TRY(lorb::scratch_t(ctx, S_TL + 17, (size_t)std::max(np, 1), &dlv));
+  LORB_TRY(lorb::scratch_t(ctx, S_TL + 18, (size_t)std::max(nk, 1), &das));
+  LORB_TRY(lorb::scratch_t(ctx, S_TL + 19, 1, &dnm));
+  LORB_TRY(lorb_track_local_map_dev(ctx, frame, Tcw, &K, dss, &M, viewing_cos_limit, th, div, dtr, dlv, das, dnm));
+  if (np > 0) {
+    LORB_HIP(ctx, hipMemcpyAsync(in_view, div, (size_t)np, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(track, dtr, sizeof(float) * 4 * np, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(level, dlv, sizeof(int32_t) * np, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  if (nk > 0) LORB_HIP(ctx, hipMemcpyAsync(assign, das, sizeof(int32_t) * nk, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(nmatches, dnm, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
 int lorb_unproject_stereo_dev(lorb_ctx* ctx, const lorb_frame_params* frame, const float Tcw[16], int32_t n,
                               const float* d_x, const float* d_y, const float* d_depth, float* d_out) {
   if (!ctx || !frame || !Tcw) return LORB_E_INVALID;

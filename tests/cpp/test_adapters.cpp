@@ -25,6 +25,10 @@ struct MiniPoint {
   int level = 0;
   std::map<MiniFrame*, size_t> obs;
   size_t first_id = 0;
+  float normal[3] = {0, 0, 1};
+  float maxd = 0, mind = 0;
+  size_t last_seen = 0;
+  int visible = 0;
 };
 struct MiniFrame {
   size_t id = 0;
@@ -102,6 +106,14 @@ template <> struct PointTraits<MiniPoint> {
   }
   static float found_ratio(MiniPoint*) { return 1.0f; }
   static void set_descriptor(MiniPoint* p, const uint8_t* d) { memcpy(p->desc, d, 32); }
+  static void normal(MiniPoint* p, float* n) { memcpy(n, p->normal, 12); }
+  static void distances(MiniPoint* p, float* mx, float* mn) { *mx = p->maxd; *mn = p->mind; }
+  static size_t last_frame_seen(MiniPoint* p) { return p->last_seen; }
+  static void set_tracking(MiniPoint* p, bool in_view, const float* t, int level) {
+    p->in_view = in_view;
+    if (in_view) { memcpy(p->proj, t, 16); p->level = level; }
+  }
+  static void increase_visible(MiniPoint* p) { p->visible++; }
   static void set_bad(MiniPoint* p) { p->bad = true; }
   static size_t first_frame_id(MiniPoint* p) { return p->first_id; }
 };
@@ -308,6 +320,83 @@ int main() {
     const size_t ng = lorb::SearchLocalPoints(ctx, cur, s);
     EXPECT((int)ng == no, "SearchLocalPoints gpu %zu oracle %d", ng, no);
     printf("SearchLocalPoints: %zu matches\n", ng);
+  }
+
+  // ---- EstimatePoseLocal's local-map loop (§8f row 1): frustum + SearchByProjection ----------
+  {
+    MiniFrame* tf = make_frame(30, 1200, r1, t1);
+    std::set<MiniPoint*> local;
+    float Ow[3];
+    {  // camera centre of tf: Ow = -R^T t
+      const float* T = tf->Tcw;
+      for (int c = 0; c < 3; c++) Ow[c] = -(T[c] * T[3] + T[4 + c] * T[7] + T[8 + c] * T[11]);
+    }
+    std::vector<MiniPoint*> own;
+    for (int i = 0; i < 1500; i++) {
+      MiniPoint* p = new MiniPoint();
+      own.push_back(p);
+      p->pos[0] = urand(-4, 4); p->pos[1] = urand(-3, 3); p->pos[2] = urand(1, 12);
+      float d[3], dn = 0;
+      for (int c = 0; c < 3; c++) { d[c] = p->pos[c] - Ow[c]; dn += d[c] * d[c]; }
+      dn = sqrtf(dn);
+      for (int c = 0; c < 3; c++) p->normal[c] = d[c] / dn;
+      p->maxd = dn * urand(1.0f, 1.19f); p->mind = p->maxd / 3.5832f;  // predicted level 0 or 1
+      for (int b = 0; b < 32; b++) p->desc[b] = (uint8_t)rnd();
+      p->nobs = rnd() % 3;
+      p->bad = rnd() % 50 == 0;
+      p->last_seen = rnd() % 20 == 0 ? tf->id : 0;
+      if (i < 900) {  // a keypoint near the projection with a close descriptor
+        float u, v;
+        project(tf->Tcw, p->pos, tf->fp, &u, &v);
+        if (u > 5 && u < 747 && v > 5 && v < 475) {
+          const size_t j = rnd() % tf->x.size();
+          tf->x[j] = u + urand(-0.5f, 0.5f); tf->y[j] = v + urand(-0.5f, 0.5f); tf->octave[j] = 0;
+          for (int b = 0; b < 32; b++) tf->desc[32 * j + b] = p->desc[b] ^ (uint8_t)(rnd() % 8 == 0);
+        }
+      }
+      local.insert(p);
+    }
+    // oracle chain on the same gathered inputs (std::set order), before the adapter mutates them
+    std::vector<MiniPoint*> mp(local.begin(), local.end());
+    const size_t n = mp.size();
+    std::vector<float> pos(3 * n), nrm(3 * n), mx(n), mn(n);
+    std::vector<uint8_t> dsc(32 * n), lk(n), bd(n);
+    for (size_t i = 0; i < n; i++) {
+      memcpy(&pos[3 * i], mp[i]->pos, 12); memcpy(&nrm[3 * i], mp[i]->normal, 12);
+      mx[i] = mp[i]->maxd; mn[i] = mp[i]->mind; memcpy(&dsc[32 * i], mp[i]->desc, 32);
+      lk[i] = mp[i]->nobs > 0; bd[i] = mp[i]->bad;
+    }
+    lorb_frustum_points FPn{(int32_t)n, pos.data(), nrm.data(), mx.data(), mn.data()};
+    std::vector<uint8_t> oiv(n);
+    std::vector<float> ox(n), oy(n), oxr(n), ocos(n);
+    std::vector<int32_t> olev(n);
+    or_is_in_frustum(&tf->fp, tf->Tcw, &FPn, 0.5f, oiv.data(), ox.data(), oy.data(), oxr.data(), olev.data(), ocos.data());
+    for (size_t i = 0; i < n; i++)
+      if (mp[i]->last_seen == tf->id || mp[i]->bad) oiv[i] = 0;
+    lorb::KeypointsSoA ks = lorb::gather_keypoints(tf);
+    std::vector<uint8_t> st = lorb::gather_slot_state(tf);
+    lorb_local_points LP{(int32_t)n, oiv.data(), bd.data(), lk.data(), ox.data(), oy.data(), oxr.data(), olev.data(),
+                         ocos.data(), dsc.data()};
+    lorb_keypoints kv = ks.view();
+    std::vector<int32_t> oas(kv.n + 1);
+    int32_t onm = 0;
+    or_search_by_projection_local(&tf->fp, &kv, st.data(), &LP, 1.0f, oas.data(), &onm);
+    const size_t ng = lorb::TrackLocalMap(ctx, tf, local, 1.0f);
+    int diff = 0, inview = 0;
+    for (size_t i = 0; i < n; i++) {
+      if (mp[i]->last_seen == tf->id || mp[i]->bad) continue;
+      diff += (mp[i]->in_view != (oiv[i] != 0));
+      if (oiv[i]) {
+        inview++;
+        diff += memcmp(&mp[i]->proj[0], &ox[i], 4) != 0 || memcmp(&mp[i]->proj[1], &oy[i], 4) != 0 ||
+                memcmp(&mp[i]->proj[2], &oxr[i], 4) != 0 || memcmp(&mp[i]->proj[3], &ocos[i], 4) != 0 ||
+                mp[i]->level != olev[i] || mp[i]->visible != 1;
+      }
+    }
+    for (int32_t j = 0; j < kv.n; j++)
+      if (oas[j] >= 0) diff += tf->mps[j] != mp[oas[j]];
+    EXPECT(diff == 0 && (int)ng == onm && onm > 100, "TrackLocalMap: %d diffs, gpu %zu oracle %d", diff, ng, onm);
+    printf("TrackLocalMap: %d points in view, %zu matches, bit-exact\n", inview, ng);
   }
 
   // ---- Frame::ComputeStereoMatches (§8f row 2) ----------------------------------------------
