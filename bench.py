@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 
 from lorb_slam_amd import _abi as A  # noqa: E402
 from lorb_slam_amd import synth  # noqa: E402
-from lorb_slam_amd.runtime import BAPlan, Context, lib  # noqa: E402
+from lorb_slam_amd.runtime import BAPlan, Context, device_count, lib  # noqa: E402
 
 CLOCK = 2.4e9
 INT32_VALU_PEAK = 256 * 4 * 32 * CLOCK      # lane-ops/s: 256 CU x 4 SIMD32 (MI355X_MICROARCH)
@@ -357,7 +357,9 @@ def main():
     args = ap.parse_args()
 
     D = Dist()
-    ctx = Context(D.local_rank)
+    # one rank per GPU; with fewer GPUs than ranks (a rehearsal on a 1-GPU box) ranks share them
+    ndev = device_count()
+    ctx = Context(D.local_rank % ndev if ndev > 0 else D.local_rank)
     if args.workload == "shared":
         wl = workload_shared(ctx, args, D.rank, D)
     else:
