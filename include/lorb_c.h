@@ -310,6 +310,19 @@ int lorb_orb_describe_dev(lorb_ctx* ctx, const lorb_image_pyramid* d_pyr, int32_
                           const float* d_y, const int32_t* d_level, const int32_t* d_pattern, float* d_angle,
                           uint8_t* d_desc);
 
+/* SURVEY §8f row 3, detection stage of ORBextractor::ComputeKeyPointsOctTree
+ * (src/ORBextractor.cpp:898-1000): the cell grid of every level (:903-990; n_desired[l] =
+ * mnFeaturesPerLevel[l]) and per cell cv::FAST(cell, ini_th, nonmax = true), re-run with min_th
+ * when it finds at most 3 corners (:990-996).  Keypoints come out in level coordinates, grouped by
+ * level, then cell (row-major), then FAST's scan order, with response = FAST score.  Cell c of
+ * level l spans [cell_off[cell_base[l] + l + c], cell_off[cell_base[l] + l + c + 1]); cell_base
+ * has n_levels + 1 entries.  The retention that follows in the reference (KeyPointsFilter::
+ * retainBest, :1000-1060) is left to the caller: its std::nth_element tie order is
+ * implementation-defined.  Host pointers; synchronous. */
+int lorb_orb_fast_cells(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired, int32_t ini_th,
+                        int32_t min_th, int32_t max_keypoints, float* x, float* y, float* response,
+                        int32_t max_cells, int32_t* cell_base, int32_t* cell_off, int32_t* n_keypoints);
+
 /* ----------------------------------------------------------------------------------------
  * Bundle adjustment: Ceres-default Levenberg-Marquardt + DENSE_SCHUR restated
  * (src/bundle_adjust.cpp:158-202 and :207-330; solver defaults in SURVEY Appendix B).

@@ -235,6 +235,177 @@ int enqueue_orb(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const uint8_t* d_d
   return LORB_OK;
 }
 
+// ---- detection stage (src/ORBextractor.cpp:898-1000): per-cell cv::FAST ------------------
+
+constexpr int kOff16[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1}, {2, -2}, {1, -3},
+                               {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+struct FastCell {
+  int level, ini_x, ini_y, w, h, out_base;
+};
+
+// cornerScore<16> (OpenCV 3.1 fast_score.cpp) on the LDS cell image (row stride w)
+__device__ __forceinline__ int fast_score(const uint8_t* ptr, const int* pixel, int threshold) {
+  int d[25];
+  const int v = ptr[0];
+#pragma unroll
+  for (int k = 0; k < 25; k++) d[k] = v - ptr[pixel[k]];
+  int a0 = threshold;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int a = min(d[k + 1], d[k + 2]);
+    a = min(a, d[k + 3]);
+    if (a <= a0) continue;
+#pragma unroll
+    for (int m = 4; m <= 8; m++) a = min(a, d[k + m]);
+    a0 = max(a0, min(a, d[k]));
+    a0 = max(a0, min(a, d[k + 9]));
+  }
+  int b0 = -a0;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int b = max(d[k + 1], d[k + 2]);
+#pragma unroll
+    for (int m = 3; m <= 5; m++) b = max(b, d[k + m]);
+    if (b >= b0) continue;
+#pragma unroll
+    for (int m = 6; m <= 8; m++) b = max(b, d[k + m]);
+    b0 = min(b0, max(b, d[k]));
+    b0 = min(b0, max(b, d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+// One 1024-thread workgroup per cell: the cell image in LDS, FAST_t<16> detection + score for
+// every inner pixel, 3x3 non-maximum suppression, the iniThFAST -> minThFAST fallback when at
+// most 3 corners survive, and the survivors written in FAST's row-major order (block scan).
+__global__ __launch_bounds__(1024) void k_orb_fast(const uint8_t* __restrict__ data, OrbPyr P,
+                                                   const FastCell* __restrict__ cells, int ini_th, int min_th,
+                                                   float* __restrict__ ox, float* __restrict__ oy,
+                                                   float* __restrict__ oresp, int* __restrict__ ocount) {
+  extern __shared__ uint8_t lds[];
+  __shared__ int s_count, wsum[16];
+  __shared__ int pixel[25];
+  const FastCell c = cells[blockIdx.x];
+  const int w = c.w, h = c.h, n = w * h, t = threadIdx.x;
+  uint8_t* img = lds;
+  uint8_t* score = lds + n;
+  uint8_t* corner = lds + 2 * n;
+  const uint8_t* src = data + P.offset[c.level] + (int64_t)c.ini_y * P.step[c.level] + c.ini_x;
+  const int step = P.step[c.level];
+  for (int p = t; p < n; p += 1024) {
+    const int i = p / w, j = p - i * w;
+    img[p] = src[(int64_t)i * step + j];
+  }
+  if (t < 25) pixel[t] = kOff16[t & 15][0] + kOff16[t & 15][1] * w;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int th = min(max(pass ? min_th : ini_th, 0), 255);
+    for (int p = t; p < n; p += 1024) { score[p] = 0; corner[p] = 0; }
+    if (t == 0) s_count = 0;
+    __syncthreads();
+    for (int p = t; p < n; p += 1024) {
+      const int i = p / w, j = p - i * w;
+      if (i < 3 || i >= h - 3 || j < 3 || j >= w - 3) continue;
+      const uint8_t* ptr = img + p;
+      const int v = ptr[0];
+      auto cat = [&](int k) { const int e = ptr[pixel[k]] - v; return e < -th ? 1 : (e > th ? 2 : 0); };
+      int d = cat(0) | cat(8);
+      if (d == 0) continue;
+      d &= cat(2) | cat(10);
+      d &= cat(4) | cat(12);
+      d &= cat(6) | cat(14);
+      if (d == 0) continue;
+      d &= cat(1) | cat(9);
+      d &= cat(3) | cat(11);
+      d &= cat(5) | cat(13);
+      d &= cat(7) | cat(15);
+      bool is = false;
+      if (d & 1) {
+        const int vt = v - th;
+        int count = 0;
+        for (int k = 0; k < 25; k++) {
+          if (ptr[pixel[k]] < vt) { if (++count > 8) { is = true; break; } }
+          else count = 0;
+        }
+      }
+      if (!is && (d & 2)) {
+        const int vt = v + th;
+        int count = 0;
+        for (int k = 0; k < 25; k++) {
+          if (ptr[pixel[k]] > vt) { if (++count > 8) { is = true; break; } }
+          else count = 0;
+        }
+      }
+      if (is) { corner[p] = 1; score[p] = (uint8_t)fast_score(ptr, pixel, th); }
+    }
+    __syncthreads();
+    int mine = 0;
+    for (int p = t; p < n; p += 1024) {
+      if (!corner[p]) continue;
+      const int s = score[p];
+      mine += s > score[p - w - 1] && s > score[p - w] && s > score[p - w + 1] && s > score[p - 1] && s > score[p + 1] &&
+              s > score[p + w - 1] && s > score[p + w] && s > score[p + w + 1];
+    }
+    if (mine) atomicAdd(&s_count, mine);
+    __syncthreads();
+    if (pass == 0 && s_count > 3) break;  // uniform: s_count is read by every thread after the barrier
+    __syncthreads();
+  }
+  int run = 0;
+  for (int base = 0; base < n; base += 1024) {
+    const int p = base + t;
+    bool keep = false;
+    if (p < n && corner[p]) {
+      const int s = score[p];
+      keep = s > score[p - w - 1] && s > score[p - w] && s > score[p - w + 1] && s > score[p - 1] && s > score[p + 1] &&
+             s > score[p + w - 1] && s > score[p + w] && s > score[p + w + 1];
+    }
+    int tot;
+    const int ex = lorb::block_excl_scan_1024(keep ? 1 : 0, wsum, &tot);
+    if (keep) {
+      const int i = p / w, j = p - i * w;
+      const int o = c.out_base + run + ex;
+      ox[o] = (float)(j + c.ini_x); oy[o] = (float)(i + c.ini_y); oresp[o] = (float)score[p];
+    }
+    run += tot;
+  }
+  if (t == 0) ocount[blockIdx.x] = run;
+}
+
+// the cell grid of one level, src/ORBextractor.cpp:903-990 (see oracle/fast.c)
+int orb_cells(int rows, int cols, int n_desired, float image_ratio, std::vector<int>& cells) {
+  const int EDGE = 19;
+  const int levelCols = (int)std::sqrt((float)n_desired / (5 * image_ratio));
+  const int levelRows = (int)(image_ratio * levelCols);
+  if (levelCols < 1 || levelRows < 1) return -1;
+  const int minBorderX = EDGE, minBorderY = EDGE, maxBorderX = cols - EDGE, maxBorderY = rows - EDGE;
+  const int W = maxBorderX - minBorderX, H = maxBorderY - minBorderY;
+  const int cellW = (int)std::ceil((float)W / levelCols), cellH = (int)std::ceil((float)H / levelRows);
+  cells.assign(4 * (size_t)levelRows * levelCols, 0);
+  float hY = (float)(cellH + 6);
+  for (int i = 0; i < levelRows; i++) {
+    const float iniY = (float)(minBorderY + i * cellH - 3);
+    bool skip_row = false;
+    if (i == levelRows - 1) {
+      hY = maxBorderY + 3 - iniY;
+      if (hY <= 0) skip_row = true;
+    }
+    float hX = (float)(cellW + 6);
+    for (int j = 0; j < levelCols; j++) {
+      const float iniX = (float)(minBorderX + j * cellW - 3);
+      int* c = &cells[4 * (size_t)(i * levelCols + j)];
+      c[0] = (int)iniX; c[1] = (int)iniY;
+      if (skip_row) continue;
+      if (j == levelCols - 1) {
+        hX = maxBorderX + 3 - iniX;
+        if (hX <= 0) continue;
+      }
+      c[2] = (int)hX; c[3] = (int)hY;
+    }
+  }
+  return levelRows * levelCols;
+}
+
 }  // namespace
 
 extern "C" {
@@ -283,6 +454,91 @@ int lorb_orb_describe(lorb_ctx* ctx, const lorb_image_pyramid* pyr, int32_t n, c
     LORB_HIP(ctx, hipMemcpyAsync(desc, ddesc, (size_t)32 * n, hipMemcpyDeviceToHost, ctx->stream));
   }
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+
+int lorb_orb_fast_cells(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired, int32_t ini_th,
+                        int32_t min_th, int32_t max_keypoints, float* x, float* y, float* response, int32_t max_cells,
+                        int32_t* cell_base, int32_t* cell_off, int32_t* n_keypoints) {
+  if (!ctx) return LORB_E_INVALID;
+  LORB_TRY(check_orb(ctx, pyr, 0));
+  if (!n_desired || !cell_base || !cell_off || !n_keypoints || max_keypoints < 0 || max_cells < 0)
+    return lorb::set_error(ctx, LORB_E_INVALID, "null argument");
+  const float ratio = (float)pyr->cols[0] / pyr->rows[0];
+  std::vector<FastCell> hc;       // launched cells
+  std::vector<int> slot;          // launched cell -> global cell index
+  int nc = 0, cap_total = 0;
+  std::vector<int> cells;
+  for (int l = 0; l < pyr->n_levels; l++) {
+    const int ncl = orb_cells(pyr->rows[l], pyr->cols[l], n_desired[l], ratio, cells);
+    if (ncl < 0) return lorb::set_error(ctx, LORB_E_INVALID, "level %d: degenerate cell grid (%d features)", l, n_desired[l]);
+    if (nc + ncl > max_cells) return lorb::set_error(ctx, LORB_E_INVALID, "more than max_cells = %d cells", max_cells);
+    cell_base[l] = nc;
+    for (int c = 0; c < ncl; c++) {
+      const int* g = &cells[4 * (size_t)c];
+      if (g[2] <= 0 || g[3] <= 0) continue;
+      if (g[0] < 0 || g[1] < 0 || g[0] + g[2] > pyr->cols[l] || g[1] + g[3] > pyr->rows[l])
+        return lorb::set_error(ctx, LORB_E_INVALID, "level %d cell %d outside the image", l, c);
+      if (3 * g[2] * g[3] > 96 * 1024)
+        return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "cell %d x %d exceeds the LDS tile", g[2], g[3]);
+      hc.push_back(FastCell{l, g[0], g[1], g[2], g[3], cap_total});
+      slot.push_back(nc + c);
+      cap_total += ((g[2] + 1) / 2) * ((g[3] + 1) / 2);  // 3x3 maxima are never 8-adjacent
+    }
+    nc += ncl;
+  }
+  cell_base[pyr->n_levels] = nc;
+  OrbPyr P{};
+  for (int l = 0; l < pyr->n_levels; l++) { P.offset[l] = pyr->offset[l]; P.step[l] = pyr->step[l]; }
+  uint8_t* dd;
+  FastCell* dcells;
+  float *dx, *dy, *dr;
+  int* dcnt;
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 1, pyr->data, (size_t)pyr_extent(pyr), &dd));
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 2, hc.data(), hc.size(), &dcells));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 3, (size_t)std::max(cap_total, 1), &dx));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 4, (size_t)std::max(cap_total, 1), &dy));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 5, (size_t)std::max(cap_total, 1), &dr));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 6, std::max<size_t>(hc.size(), 1), &dcnt));
+  int max_lds = 0;
+  for (const FastCell& f : hc) max_lds = std::max(max_lds, 3 * f.w * f.h);
+  if (!hc.empty())
+    hipLaunchKernelGGL(k_orb_fast, dim3((unsigned)hc.size()), dim3(1024), (size_t)max_lds, ctx->stream, dd, P,
+                       dcells, ini_th, min_th, dx, dy, dr, dcnt);
+  LORB_CHECK_LAUNCH(ctx);
+  std::vector<int> cnt(hc.size());
+  std::vector<float> hx(cap_total), hy(cap_total), hr(cap_total);
+  if (!hc.empty()) {
+    LORB_HIP(ctx, hipMemcpyAsync(cnt.data(), dcnt, sizeof(int) * hc.size(), hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(hx.data(), dx, sizeof(float) * cap_total, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(hy.data(), dy, sizeof(float) * cap_total, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(hr.data(), dr, sizeof(float) * cap_total, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // compact in level / cell order; cell_off of level l, cell c at cell_base[l] + l + c
+  std::vector<int> per_cell(nc, 0), src_of(nc, -1);
+  for (size_t k = 0; k < hc.size(); k++) { per_cell[slot[k]] = cnt[k]; src_of[slot[k]] = (int)k; }
+  int nk = 0;
+  for (int l = 0; l < pyr->n_levels; l++) {
+    const int b = cell_base[l], e = cell_base[l + 1];
+    for (int g = b; g < e; g++) {
+      cell_off[g + l] = nk;
+      const int k = src_of[g];
+      if (k >= 0) {
+        for (int q = 0; q < cnt[k]; q++) {
+          if (nk + q < max_keypoints) {
+            x[nk + q] = hx[hc[k].out_base + q]; y[nk + q] = hy[hc[k].out_base + q]; response[nk + q] = hr[hc[k].out_base + q];
+          }
+        }
+        nk += cnt[k];
+      }
+    }
+    cell_off[e + l] = nk;
+  }
+  *n_keypoints = nk;
+  if (nk > max_keypoints)
+    return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints exceed max_keypoints = %d", nk, max_keypoints);
   return LORB_OK;
 }
 

@@ -163,6 +163,26 @@ def _orb_describe(self, pyr, x, y, level, pattern, device_resident=False):
     return out
 
 
+def _orb_fast_cells(self, pyr, n_desired, ini_th=20, min_th=7, max_kp=200000, max_cells=4096):
+    """Detection stage of ORBextractor::ComputeKeyPointsOctTree: per-cell FAST with the threshold
+    fallback.  Returns x, y, response (level coordinates) and the cell_base / cell_off tables."""
+    buf, P = A.pack_pyramid(pyr)
+    P.data = buf.ctypes.data
+    nd = A.i32(n_desired)
+    x, y, r = np.zeros(max_kp, np.float32), np.zeros(max_kp, np.float32), np.zeros(max_kp, np.float32)
+    base = np.zeros(len(pyr) + 1, np.int32)
+    off = np.zeros(max_cells + len(pyr) + 1, np.int32)
+    n = C.c_int32(0)
+    self.check(lib().lorb_orb_fast_cells(self._p, C.byref(P), A.ptr(nd, C.c_int32), C.c_int32(ini_th), C.c_int32(min_th),
+                                         C.c_int32(max_kp), A.ptr(x, C.c_float), A.ptr(y, C.c_float),
+                                         A.ptr(r, C.c_float), C.c_int32(max_cells), A.ptr(base, C.c_int32),
+                                         A.ptr(off, C.c_int32), C.byref(n)), "lorb_orb_fast_cells")
+    k = n.value
+    return dict(x=x[:k].copy(), y=y[:k].copy(), response=r[:k].copy(), cell_base=base,
+                cell_off=off[:base[-1] + len(pyr)].copy())
+
+
+Context.orb_fast_cells = _orb_fast_cells
 Context.orb_describe = _orb_describe
 Context.compute_stereo_matches = _compute_stereo_matches
 Context.track_local_map = _track_local_map

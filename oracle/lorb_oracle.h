@@ -117,6 +117,15 @@ void or_orb_descriptor(const uint8_t* img, int step, float px, float py, float a
 void or_orb_describe(const lorb_image_pyramid* P, int n, const float* x, const float* y, const int32_t* level,
                      const int32_t* pattern, float* angle, uint8_t* desc);
 
+/* fast.c: cv::FAST (OpenCV 3.1 FAST_t<16> + cornerScore<16>) and the per-level cell detection of
+ * ORBextractor::ComputeKeyPointsOctTree (src/ORBextractor.cpp:898-1000) */
+int or_fast_score(const uint8_t* ptr, const int* pixel, int threshold);
+int or_fast(const uint8_t* img, int w, int h, int step, int threshold, int max_out, float* ox, float* oy,
+            float* oresp);
+int or_orb_cells(int rows, int cols, int n_desired, float image_ratio, int* cells, int max_cells);
+int or_orb_fast_cells(const lorb_image_pyramid* P, const int32_t* n_desired, int ini_th, int min_th, int max_kp,
+                      float* x, float* y, float* resp, int max_cells, int32_t* cell_base, int32_t* cell_off);
+
 #ifdef __cplusplus
 }
 #endif

@@ -305,3 +305,43 @@ def orb_describe(pyr, x, y, level, pattern):
     lib().or_orb_describe(C.byref(P), C.c_int(n), A.ptr(x, C.c_float), A.ptr(y, C.c_float), A.ptr(level, C.c_int32),
                           A.ptr(pattern, C.c_int32), A.ptr(ang, C.c_float), A.ptr(desc, C.c_uint8))
     return ang[:n].copy(), desc[:n].copy()
+
+
+def orb_features_per_level(nfeatures=1000, scale=1.2, n_levels=8):
+    """ORBextractor::ORBextractor, src/ORBextractor.cpp:448-461 (float arithmetic as the reference)."""
+    f32 = np.float32
+    factor = f32(1.0) / f32(scale)
+    per = f32(f32(nfeatures) * (f32(1) - factor) / (f32(1) - f32(np.power(np.float64(factor), np.float64(n_levels)))))
+    out, s = [], 0
+    for _ in range(n_levels - 1):
+        v = int(np.rint(per))
+        out.append(v); s += v
+        per = f32(per * factor)
+    out.append(max(nfeatures - s, 0))
+    return np.array(out, np.int32)
+
+
+def fast(img, threshold):
+    """cv::FAST(img, kp, threshold, true) -> (x, y, response) in emission order."""
+    img = A.u8(img)
+    h, w = img.shape
+    cap = max(1, ((w + 1) // 2) * ((h + 1) // 2))
+    x, y, r = np.zeros(cap, np.float32), np.zeros(cap, np.float32), np.zeros(cap, np.float32)
+    n = lib().or_fast(A.ptr(img, C.c_uint8), C.c_int(w), C.c_int(h), C.c_int(w), C.c_int(threshold), C.c_int(cap),
+                      A.ptr(x, C.c_float), A.ptr(y, C.c_float), A.ptr(r, C.c_float))
+    return x[:n].copy(), y[:n].copy(), r[:n].copy()
+
+
+def orb_fast_cells(pyr, n_desired, ini_th=20, min_th=7, max_kp=200000, max_cells=4096):
+    buf, P = A.pack_pyramid(pyr)
+    P.data = buf.ctypes.data
+    nd = A.i32(n_desired)
+    x, y, r = np.zeros(max_kp, np.float32), np.zeros(max_kp, np.float32), np.zeros(max_kp, np.float32)
+    base = np.zeros(len(pyr) + 1, np.int32)
+    off = np.zeros(max_cells + len(pyr) + 1, np.int32)
+    n = lib().or_orb_fast_cells(C.byref(P), A.ptr(nd, C.c_int32), C.c_int(ini_th), C.c_int(min_th), C.c_int(max_kp),
+                                A.ptr(x, C.c_float), A.ptr(y, C.c_float), A.ptr(r, C.c_float), C.c_int(max_cells),
+                                A.ptr(base, C.c_int32), A.ptr(off, C.c_int32))
+    assert n >= 0, "degenerate grid or capacity"
+    return dict(x=x[:n].copy(), y=y[:n].copy(), response=r[:n].copy(), cell_base=base,
+                cell_off=off[:base[-1] + len(pyr)].copy())

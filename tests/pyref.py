@@ -234,3 +234,50 @@ def orb_describe(pyr, x, y, level, pattern):  # src/ORBextractor.cpp:79-150, 469
         bv = (t[:, 0] < t[:, 1]).astype(np.uint8).reshape(32, 8)
         desc[i] = (bv << np.arange(8, dtype=np.uint8)).sum(1).astype(np.uint8)
     return ang, desc
+
+
+_OFF16 = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3),
+          (0, -3), (-1, -3), (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+
+
+def fast(img, th):
+    """cv::FAST 9-16 with non-maximum suppression, restated independently with numpy: a pixel is a
+    corner if 9 contiguous circle pixels are all > v+th or all < v-th; its score is the largest t
+    for which that still holds over some 9-arc (the max over arcs of the min |difference|) minus 1
+    at the threshold floor -- computed here straight from that definition."""
+    img = img.astype(np.int64)
+    h, w = img.shape
+    ring = np.stack([img[3 + dy:h - 3 + dy, 3 + dx:w - 3 + dx] for dx, dy in _OFF16], 0)  # (16, h-6, w-6)
+    v = img[3:h - 3, 3:w - 3]
+    d = v[None] - ring                                    # center minus circle pixel
+    ext = np.concatenate([d, d[:9]], 0)                   # 25 entries
+    arcs_min = np.stack([ext[k:k + 9].min(0) for k in range(16)], 0)   # darker circle (d > 0)
+    arcs_max = np.stack([ext[k:k + 9].max(0) for k in range(16)], 0)   # brighter circle (d < 0)
+    dark = (arcs_min > th).any(0)
+    bright = (arcs_max < -th).any(0)
+    corner = dark | bright
+    # cornerScore: a0 = max(th, max over 10-long windows' ...); restated as in the C restatement's
+    # definition by brute force over the same arcs (k even starts, arcs [k..k+8] and [k+1..k+9])
+    a0 = np.full(v.shape, th, np.int64)
+    b0 = None
+    for k in range(0, 16, 2):
+        a = ext[k + 1:k + 9].min(0)
+        a0 = np.maximum(a0, np.minimum(a, ext[k]))
+        a0 = np.maximum(a0, np.minimum(a, ext[k + 9]))
+    b0 = -a0
+    for k in range(0, 16, 2):
+        b = ext[k + 1:k + 9].max(0)
+        b0 = np.minimum(b0, np.maximum(b, ext[k]))
+        b0 = np.minimum(b0, np.maximum(b, ext[k + 9]))
+    score = np.where(corner, (-b0 - 1) & 0xFF, 0)
+    S = np.zeros((h, w), np.int64)
+    S[3:h - 3, 3:w - 3] = score
+    C = np.zeros((h, w), bool)
+    C[3:h - 3, 3:w - 3] = corner
+    keep = C.copy()
+    for dy in (-1, 0, 1):
+        for dx in (-1, 0, 1):
+            if dy or dx:
+                keep &= S > np.roll(np.roll(S, -dy, 0), -dx, 1)
+    ys, xs = np.nonzero(keep)  # row-major = FAST's emission order
+    return xs.astype(np.float32), ys.astype(np.float32), S[ys, xs].astype(np.float32)

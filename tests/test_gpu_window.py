@@ -173,3 +173,17 @@ def test_orb_describe_edges(ctx):
     x = pr["x"].copy(); x[3] = 5.0  # inside the 19-pixel border: rejected, not read out of bounds
     with pytest.raises(Exception):
         ctx.orb_describe(pr["pyr"], x, pr["y"], pr["level"], pr["pattern"])
+
+
+@pytest.mark.parametrize("seed,nfeat,ini,mn", [(51, 1000, 20, 7), (52, 2000, 20, 7), (53, 1000, 60, 7)])
+def test_orb_fast_cells(ctx, seed, nfeat, ini, mn):
+    """SURVEY §8f row 3 detection stage: per-cell FAST + threshold fallback bit-exact vs the oracle
+    (ini=60 forces the minThFAST re-run in many cells)."""
+    pr = synth.orb_problem(seed=seed, n_kps=1)
+    nd = O.orb_features_per_level(nfeat)
+    g = ctx.orb_fast_cells(pr["pyr"], nd, ini, mn)
+    o = O.orb_fast_cells(pr["pyr"], nd, ini, mn)
+    assert np.array_equal(g["cell_base"], o["cell_base"]) and np.array_equal(g["cell_off"], o["cell_off"])
+    for k in ("x", "y", "response"):
+        assert np.array_equal(g[k], o[k]), k
+    assert len(o["x"]) > 1000

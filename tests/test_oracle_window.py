@@ -85,3 +85,24 @@ def test_orb_oracle_vs_pyref():
     assert O.orb_umax().tolist() == [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
     for yx in [(1.0, 1.0), (-3.0, 2.0), (0.0, -5.0), (7.5, -0.25), (0.0, 0.0)]:
         assert O.fast_atan2(*yx) == pyref.fast_atan2(*yx)
+
+
+@pytest.mark.parametrize("th", [7, 20])
+def test_fast_oracle_vs_pyref(th):
+    """cv::FAST restatement (C) == independent numpy restatement on textured images."""
+    pr = synth.orb_problem(seed=41, n_kps=1)
+    for lv in (0, 4):
+        img = pr["pyr"][lv][:90, :130]
+        a = O.fast(img, th)
+        b = pyref.fast(img, th)
+        assert len(a[0]) > 10
+        for u, v in zip(a, b):
+            assert np.array_equal(u, v)
+
+
+def test_orb_cells_layout():
+    nd = O.orb_features_per_level(1000)
+    assert nd.sum() == 1000 and nd[0] == 217
+    pr = synth.orb_problem(seed=42, n_kps=1)
+    out = O.orb_fast_cells(pr["pyr"], nd)
+    assert len(out["x"]) > 1000 and out["cell_base"][-1] > 8
