@@ -323,6 +323,17 @@ int lorb_orb_fast_cells(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int3
                         int32_t min_th, int32_t max_keypoints, float* x, float* y, float* response,
                         int32_t max_cells, int32_t* cell_base, int32_t* cell_off, int32_t* n_keypoints);
 
+/* SURVEY §8f row 3, ORBextractor::ComputeKeyPointsOctTree without the orientation
+ * (src/ORBextractor.cpp:898-1067): lorb_orb_fast_cells, then the nToRetain distribution,
+ * KeyPointsFilter::retainBest + resize per cell (std::nth_element / std::partition, as OpenCV),
+ * cell offsets, octave and size (PATCH_SIZE * scale_factors[l]), and the level-wide retainBest.
+ * Per keypoint: x, y (level coordinates), octave, size, response; level_off[n_levels + 1].
+ * Then lorb_orb_describe gives the angle and the descriptor.  Host pointers; synchronous. */
+int lorb_orb_detect(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired,
+                    const float* scale_factors, int32_t ini_th, int32_t min_th, int32_t max_keypoints, float* x,
+                    float* y, int32_t* octave, float* size, float* response, int32_t* level_off,
+                    int32_t* n_keypoints);
+
 /* ----------------------------------------------------------------------------------------
  * Bundle adjustment: Ceres-default Levenberg-Marquardt + DENSE_SCHUR restated
  * (src/bundle_adjust.cpp:158-202 and :207-330; solver defaults in SURVEY Appendix B).

@@ -13,6 +13,7 @@
 // oracle/orb.c; the float expressions follow the reference's order (-ffp-contract=off).
 #include <algorithm>
 #include <cfloat>
+#include <vector>
 #include <cmath>
 
 #include "lorb_internal.h"
@@ -539,6 +540,114 @@ int lorb_orb_fast_cells(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int3
   *n_keypoints = nk;
   if (nk > max_keypoints)
     return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints exceed max_keypoints = %d", nk, max_keypoints);
+  return LORB_OK;
+}
+
+
+// Detection + retention (src/ORBextractor.cpp:898-1067).  The FAST cells run on the device
+// (lorb_orb_fast_cells); the retention is sequential bookkeeping over a few hundred keypoints per
+// cell and runs here on the host with the very std::nth_element / std::partition that
+// KeyPointsFilter::retainBest (OpenCV 3.1) calls, so equal responses are resolved exactly as in
+// the reference build.
+namespace {
+struct OrbKp {
+  float x, y, size, resp;
+  int octave;
+};
+void retain_best(std::vector<OrbKp>& k, int n_points) {  // KeyPointsFilter::retainBest
+  if (n_points >= 0 && k.size() > (size_t)n_points) {
+    if (n_points == 0) { k.clear(); return; }
+    std::nth_element(k.begin(), k.begin() + n_points, k.end(),
+                     [](const OrbKp& a, const OrbKp& b) { return a.resp > b.resp; });
+    const float amb = k[n_points - 1].resp;
+    auto e = std::partition(k.begin() + n_points, k.end(), [amb](const OrbKp& a) { return a.resp >= amb; });
+    k.resize(e - k.begin());
+  }
+}
+}  // namespace
+
+int lorb_orb_detect(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired,
+                    const float* scale_factors, int32_t ini_th, int32_t min_th, int32_t max_keypoints, float* x,
+                    float* y, int32_t* octave, float* size, float* response, int32_t* level_off,
+                    int32_t* n_keypoints) {
+  if (!ctx) return LORB_E_INVALID;
+  LORB_TRY(check_orb(ctx, pyr, 0));
+  if (!n_desired || !scale_factors || !level_off || !n_keypoints || max_keypoints < 0)
+    return lorb::set_error(ctx, LORB_E_INVALID, "null argument");
+  const int L = pyr->n_levels;
+  int max_cells = 0, cap = 0;
+  const float ratio = (float)pyr->cols[0] / pyr->rows[0];
+  std::vector<int> cells;
+  for (int l = 0; l < L; l++) {
+    const int ncl = orb_cells(pyr->rows[l], pyr->cols[l], n_desired[l], ratio, cells);
+    if (ncl < 0) return lorb::set_error(ctx, LORB_E_INVALID, "level %d: degenerate cell grid (%d features)", l, n_desired[l]);
+    max_cells += ncl;
+    for (int c = 0; c < ncl; c++) cap += ((cells[4 * c + 2] + 1) / 2) * ((cells[4 * c + 3] + 1) / 2);
+  }
+  std::vector<float> fx(cap + 1), fy(cap + 1), fr(cap + 1);
+  std::vector<int32_t> base(L + 1), coff(max_cells + L + 1);
+  int32_t nf = 0;
+  LORB_TRY(lorb_orb_fast_cells(ctx, pyr, n_desired, ini_th, min_th, cap, fx.data(), fy.data(), fr.data(), max_cells,
+                               base.data(), coff.data(), &nf));
+  int out = 0;
+  for (int l = 0; l < L; l++) {
+    level_off[l] = out;
+    const int nd = n_desired[l];
+    const int levelCols = (int)std::sqrt((float)nd / (5 * ratio));
+    const int levelRows = (int)(ratio * levelCols);
+    const int nCells = levelRows * levelCols;
+    orb_cells(pyr->rows[l], pyr->cols[l], nd, ratio, cells);
+    const int nfeaturesCell = (int)std::ceil((float)nd / nCells);
+    std::vector<int> nToRetain(nCells, 0), nTotal(nCells, 0);
+    std::vector<char> bNoMore(nCells, 0);
+    int nNoMore = 0, nToDistribute = 0;
+    const int32_t* co = coff.data() + base[l] + l;
+    for (int c = 0; c < nCells; c++) {  // :983-1003
+      if (cells[4 * c + 2] <= 0 || cells[4 * c + 3] <= 0) continue;
+      const int nKeys = co[c + 1] - co[c];
+      nTotal[c] = nKeys;
+      if (nKeys > nfeaturesCell) { nToRetain[c] = nfeaturesCell; bNoMore[c] = 0; }
+      else { nToRetain[c] = nKeys; nToDistribute += nfeaturesCell - nKeys; bNoMore[c] = 1; nNoMore++; }
+    }
+    while (nToDistribute > 0 && nNoMore < nCells) {  // :1010-1035
+      const int nNew = (int)(nfeaturesCell + std::ceil((float)nToDistribute / (nCells - nNoMore)));
+      nToDistribute = 0;
+      for (int c = 0; c < nCells; c++)
+        if (!bNoMore[c]) {
+          if (nTotal[c] > nNew) { nToRetain[c] = nNew; bNoMore[c] = 0; }
+          else { nToRetain[c] = nTotal[c]; nToDistribute += nNew - nTotal[c]; bNoMore[c] = 1; nNoMore++; }
+        }
+    }
+    const int scaledPatchSize = (int)(31 * scale_factors[l]);  // PATCH_SIZE * mvScaleFactor (:1040)
+    std::vector<OrbKp> level;
+    std::vector<OrbKp> cell;
+    for (int c = 0; c < nCells; c++) {  // :1043-1060
+      cell.clear();
+      for (int k = co[c]; k < co[c + 1]; k++)
+        cell.push_back(OrbKp{fx[k] - (float)cells[4 * c], fy[k] - (float)cells[4 * c + 1], 7.f, fr[k], 0});
+      retain_best(cell, nToRetain[c]);
+      if ((int)cell.size() > nToRetain[c]) cell.resize(nToRetain[c]);
+      for (OrbKp& kp : cell) {
+        kp.x += (float)cells[4 * c]; kp.y += (float)cells[4 * c + 1];
+        kp.octave = l; kp.size = (float)scaledPatchSize;
+        level.push_back(kp);
+      }
+    }
+    if ((int)level.size() > nd) {  // :1063-1067
+      retain_best(level, nd);
+      level.resize(nd);
+    }
+    for (const OrbKp& kp : level) {
+      if (out < max_keypoints) {
+        x[out] = kp.x; y[out] = kp.y; octave[out] = kp.octave; size[out] = kp.size; response[out] = kp.resp;
+      }
+      out++;
+    }
+  }
+  level_off[L] = out;
+  *n_keypoints = out;
+  if (out > max_keypoints)
+    return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints exceed max_keypoints = %d", out, max_keypoints);
   return LORB_OK;
 }
 

@@ -182,6 +182,25 @@ def _orb_fast_cells(self, pyr, n_desired, ini_th=20, min_th=7, max_kp=200000, ma
                 cell_off=off[:base[-1] + len(pyr)].copy())
 
 
+def _orb_detect(self, pyr, n_desired, scale_factors, ini_th=20, min_th=7, max_kp=100000):
+    """ComputeKeyPointsOctTree without orientation: FAST cells on the device, retention on the host."""
+    buf, P = A.pack_pyramid(pyr)
+    P.data = buf.ctypes.data
+    nd, sf = A.i32(n_desired), A.f32(scale_factors)
+    x, y, sz, r = (np.zeros(max_kp, np.float32) for _ in range(4))
+    o = np.zeros(max_kp, np.int32)
+    lo = np.zeros(len(pyr) + 1, np.int32)
+    n = C.c_int32(0)
+    self.check(lib().lorb_orb_detect(self._p, C.byref(P), A.ptr(nd, C.c_int32), A.ptr(sf, C.c_float), C.c_int32(ini_th),
+                                     C.c_int32(min_th), C.c_int32(max_kp), A.ptr(x, C.c_float), A.ptr(y, C.c_float),
+                                     A.ptr(o, C.c_int32), A.ptr(sz, C.c_float), A.ptr(r, C.c_float),
+                                     A.ptr(lo, C.c_int32), C.byref(n)), "lorb_orb_detect")
+    k = n.value
+    return dict(x=x[:k].copy(), y=y[:k].copy(), octave=o[:k].copy(), size=sz[:k].copy(), response=r[:k].copy(),
+                level_off=lo)
+
+
+Context.orb_detect = _orb_detect
 Context.orb_fast_cells = _orb_fast_cells
 Context.orb_describe = _orb_describe
 Context.compute_stereo_matches = _compute_stereo_matches

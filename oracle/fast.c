@@ -6,8 +6,9 @@
  * (9 contiguous of the 16-pixel circle of radius 3, threshold_tab prefilter) with cornerScore<16>
  * and 3x3 non-maximum suppression, restated from its published source (features2d/src/fast.cpp,
  * fast_score.cpp); OpenCV is absent here, so this is "parity unpinned" (tests/ cross-check it
- * against an independent numpy restatement).  Retention (KeyPointsFilter::retainBest,
- * :1000-1060) is not restated: its std::nth_element tie order is implementation-defined.
+ * against an independent numpy restatement).  The retention that follows (KeyPointsFilter::
+ * retainBest, :1000-1067) is restated at the end of this file together with the libstdc++
+ * algorithms it runs on.
  */
 #include <math.h>
 #include <stdint.h>
@@ -190,4 +191,214 @@ int or_orb_fast_cells(const lorb_image_pyramid* P, const int32_t* n_desired, int
   cell_base[P->n_levels] = nc;
   free(cells);
   return nk;
+}
+
+/* ---- retention (src/ORBextractor.cpp:984-1067) -------------------------------------------
+ * KeyPointsFilter::retainBest (OpenCV 3.1) is std::nth_element + std::partition; the order they
+ * leave equal responses in decides which keypoints the following resize() keeps, so libstdc++'s
+ * algorithms (bits/stl_algo.h, stl_heap.h: introselect with median-of-3 pivots, heap_select past
+ * the depth limit, insertion sort; the bidirectional partition) are restated here step for step. */
+typedef struct { float x, y, size, resp; int octave; } or_kp;
+
+static int kp_greater(const or_kp* a, const or_kp* b) { return a->resp > b->resp; }  /* KeypointResponseGreater */
+static void kp_swap(or_kp* a, or_kp* b) { or_kp t = *a; *a = *b; *b = t; }
+
+static void adjust_heap(or_kp* f, long hole, long len, or_kp value) {
+  const long top = hole;
+  long second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (kp_greater(&f[second], &f[second - 1])) second--;
+    f[hole] = f[second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    f[hole] = f[second - 1];
+    hole = second - 1;
+  }
+  /* __push_heap */
+  long parent = (hole - 1) / 2;
+  while (hole > top && kp_greater(&f[parent], &value)) {
+    f[hole] = f[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  f[hole] = value;
+}
+static void make_heap(or_kp* f, long len) {
+  if (len < 2) return;
+  long parent = (len - 2) / 2;
+  while (1) {
+    or_kp v = f[parent];
+    adjust_heap(f, parent, len, v);
+    if (parent == 0) return;
+    parent--;
+  }
+}
+static void heap_select(or_kp* f, long mid, long last) {
+  make_heap(f, mid);
+  for (long i = mid; i < last; ++i)
+    if (kp_greater(&f[i], &f[0])) {  /* __pop_heap(first, middle, i) */
+      or_kp v = f[i];
+      f[i] = f[0];
+      adjust_heap(f, 0, mid, v);
+    }
+}
+static void move_median_to_first(or_kp* f, long r, long a, long b, long c) {
+  if (kp_greater(&f[a], &f[b])) {
+    if (kp_greater(&f[b], &f[c])) kp_swap(&f[r], &f[b]);
+    else if (kp_greater(&f[a], &f[c])) kp_swap(&f[r], &f[c]);
+    else kp_swap(&f[r], &f[a]);
+  } else if (kp_greater(&f[a], &f[c])) kp_swap(&f[r], &f[a]);
+  else if (kp_greater(&f[b], &f[c])) kp_swap(&f[r], &f[c]);
+  else kp_swap(&f[r], &f[b]);
+}
+static long unguarded_partition(or_kp* f, long first, long last, long pivot) {
+  while (1) {
+    while (kp_greater(&f[first], &f[pivot])) ++first;
+    --last;
+    while (kp_greater(&f[pivot], &f[last])) --last;
+    if (!(first < last)) return first;
+    kp_swap(&f[first], &f[last]);
+    ++first;
+  }
+}
+static void insertion_sort(or_kp* f, long first, long last) {
+  if (first == last) return;
+  for (long i = first + 1; i != last; ++i) {
+    if (kp_greater(&f[i], &f[first])) {
+      or_kp v = f[i];
+      memmove(&f[first + 1], &f[first], sizeof(or_kp) * (size_t)(i - first));
+      f[first] = v;
+    } else {
+      or_kp v = f[i];
+      long l = i, nx = i - 1;
+      while (kp_greater(&v, &f[nx])) { f[l] = f[nx]; l = nx; --nx; }
+      f[l] = v;
+    }
+  }
+}
+static int lg(long n) { int k = 0; while (n > 1) { n >>= 1; k++; } return k; }
+static void nth_element(or_kp* f, long nth, long n) {
+  if (n == 0 || nth == n) return;
+  long first = 0, last = n;
+  int depth = 2 * lg(n);
+  while (last - first > 3) {
+    if (depth == 0) {
+      heap_select(f + first, nth + 1 - first, last - first);
+      kp_swap(&f[first], &f[nth]);
+      return;
+    }
+    --depth;
+    const long mid = first + (last - first) / 2;
+    move_median_to_first(f, first, first + 1, mid, last - 1);
+    const long cut = unguarded_partition(f, first + 1, last, first);
+    if (cut <= nth) first = cut; else last = cut;
+  }
+  insertion_sort(f, first, last);
+}
+/* std::partition (bidirectional) with pred = response >= value; returns the new end */
+static long partition_ge(or_kp* f, long first, long last, float value) {
+  while (1) {
+    while (1) {
+      if (first == last) return first;
+      if (f[first].resp >= value) ++first; else break;
+    }
+    --last;
+    while (1) {
+      if (first == last) return first;
+      if (!(f[last].resp >= value)) --last; else break;
+    }
+    kp_swap(&f[first], &f[last]);
+    ++first;
+  }
+}
+/* KeyPointsFilter::retainBest; returns the new size */
+static long retain_best(or_kp* f, long n, long n_points) {
+  if (n_points >= 0 && n > n_points) {
+    if (n_points == 0) return 0;
+    nth_element(f, n_points, n);
+    const float amb = f[n_points - 1].resp;
+    return partition_ge(f, n_points, n, amb);
+  }
+  return n;
+}
+
+/* Detection + retention of every level (src/ORBextractor.cpp:898-1067): FAST per cell (above),
+ * the nToRetain distribution, retainBest + resize per cell, cell offsets added, octave and size,
+ * and the level-wide retainBest when more than n_desired survive.  Outputs per keypoint x, y (level
+ * coordinates), octave, size, response; level_off[n_levels + 1].  Returns the count or -1. */
+int or_orb_detect(const lorb_image_pyramid* P, const int32_t* n_desired, const float* scale_factors, int ini_th,
+                  int min_th, int max_kp, float* ox, float* oy, int32_t* ooct, float* osize, float* oresp,
+                  int32_t* level_off) {
+  const int max_cells = 1 << 16;
+  int32_t* base = (int32_t*)malloc(sizeof(int32_t) * (P->n_levels + 1));
+  int32_t* coff = (int32_t*)malloc(sizeof(int32_t) * (max_cells + P->n_levels + 1));
+  const int cap = 1 << 22;
+  float* fx = (float*)malloc(sizeof(float) * cap);
+  float* fy = (float*)malloc(sizeof(float) * cap);
+  float* fr = (float*)malloc(sizeof(float) * cap);
+  int nk = or_orb_fast_cells(P, n_desired, ini_th, min_th, cap, fx, fy, fr, max_cells, base, coff);
+  int out = 0, ok = nk >= 0;
+  const float ratio = (float)P->cols[0] / P->rows[0];
+  int* cells = (int*)malloc(sizeof(int) * 4 * (size_t)max_cells);
+  for (int l = 0; ok && l < P->n_levels; l++) {
+    level_off[l] = out;
+    const int nd = n_desired[l];
+    const int levelCols = (int)sqrtf((float)nd / (5 * ratio));
+    const int levelRows = (int)(ratio * levelCols);
+    const int nCells = levelRows * levelCols;
+    or_orb_cells(P->rows[l], P->cols[l], nd, ratio, cells, max_cells);
+    const int nfeaturesCell = (int)ceilf((float)nd / nCells);
+    int* nToRetain = (int*)calloc((size_t)nCells, sizeof(int));
+    int* nTotal = (int*)calloc((size_t)nCells, sizeof(int));
+    char* bNoMore = (char*)calloc((size_t)nCells, 1);
+    int nNoMore = 0, nToDistribute = 0;
+    const int32_t* co = coff + base[l] + l;
+    for (int c = 0; c < nCells; c++) {
+      if (cells[4 * c + 2] <= 0 || cells[4 * c + 3] <= 0) continue;  /* skipped cell (:940, :960) */
+      const int nKeys = co[c + 1] - co[c];
+      nTotal[c] = nKeys;
+      if (nKeys > nfeaturesCell) { nToRetain[c] = nfeaturesCell; bNoMore[c] = 0; }
+      else { nToRetain[c] = nKeys; nToDistribute += nfeaturesCell - nKeys; bNoMore[c] = 1; nNoMore++; }
+    }
+    while (nToDistribute > 0 && nNoMore < nCells) {
+      const int nNew = (int)(nfeaturesCell + ceilf((float)nToDistribute / (nCells - nNoMore)));
+      nToDistribute = 0;
+      for (int c = 0; c < nCells; c++)
+        if (!bNoMore[c]) {
+          if (nTotal[c] > nNew) { nToRetain[c] = nNew; bNoMore[c] = 0; }
+          else { nToRetain[c] = nTotal[c]; nToDistribute += nNew - nTotal[c]; bNoMore[c] = 1; nNoMore++; }
+        }
+    }
+    const int scaledPatchSize = (int)(31 * scale_factors[l]);
+    or_kp* lv = (or_kp*)malloc(sizeof(or_kp) * (size_t)(co[nCells] - co[0] + 1));
+    long nl = 0;
+    for (int c = 0; c < nCells; c++) {
+      or_kp* cell = lv + nl;
+      long n = 0;
+      for (int k = co[c]; k < co[c + 1]; k++) {  /* FAST order, cell coordinates restored below */
+        cell[n].x = fx[k] - (float)cells[4 * c]; cell[n].y = fy[k] - (float)cells[4 * c + 1];
+        cell[n].resp = fr[k]; cell[n].size = 7.f; cell[n].octave = 0; n++;
+      }
+      n = retain_best(cell, n, nToRetain[c]);
+      if (n > nToRetain[c]) n = nToRetain[c];
+      for (long k = 0; k < n; k++) {
+        cell[k].x += (float)cells[4 * c]; cell[k].y += (float)cells[4 * c + 1];
+        cell[k].octave = l; cell[k].size = (float)scaledPatchSize;
+      }
+      nl += n;
+    }
+    if (nl > nd) { nl = retain_best(lv, nl, nd); nl = nd < nl ? nd : nl; }
+    for (long k = 0; k < nl && ok; k++) {
+      if (out >= max_kp) { ok = 0; break; }
+      ox[out] = lv[k].x; oy[out] = lv[k].y; ooct[out] = lv[k].octave; osize[out] = lv[k].size; oresp[out] = lv[k].resp;
+      out++;
+    }
+    free(lv); free(nToRetain); free(nTotal); free(bNoMore);
+  }
+  level_off[P->n_levels] = out;
+  free(cells); free(base); free(coff); free(fx); free(fy); free(fr);
+  return ok ? out : -1;
 }

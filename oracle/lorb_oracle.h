@@ -126,6 +126,10 @@ int or_orb_cells(int rows, int cols, int n_desired, float image_ratio, int* cell
 int or_orb_fast_cells(const lorb_image_pyramid* P, const int32_t* n_desired, int ini_th, int min_th, int max_kp,
                       float* x, float* y, float* resp, int max_cells, int32_t* cell_base, int32_t* cell_off);
 
+int or_orb_detect(const lorb_image_pyramid* P, const int32_t* n_desired, const float* scale_factors, int ini_th,
+                  int min_th, int max_kp, float* ox, float* oy, int32_t* ooct, float* osize, float* oresp,
+                  int32_t* level_off);
+
 #ifdef __cplusplus
 }
 #endif

@@ -345,3 +345,19 @@ def orb_fast_cells(pyr, n_desired, ini_th=20, min_th=7, max_kp=200000, max_cells
     assert n >= 0, "degenerate grid or capacity"
     return dict(x=x[:n].copy(), y=y[:n].copy(), response=r[:n].copy(), cell_base=base,
                 cell_off=off[:base[-1] + len(pyr)].copy())
+
+
+def orb_detect(pyr, n_desired, scale_factors, ini_th=20, min_th=7, max_kp=100000):
+    """ComputeKeyPointsOctTree without orientation (src/ORBextractor.cpp:898-1067)."""
+    buf, P = A.pack_pyramid(pyr)
+    P.data = buf.ctypes.data
+    nd, sf = A.i32(n_desired), A.f32(scale_factors)
+    x, y, sz, r = (np.zeros(max_kp, np.float32) for _ in range(4))
+    o = np.zeros(max_kp, np.int32)
+    lo = np.zeros(len(pyr) + 1, np.int32)
+    n = lib().or_orb_detect(C.byref(P), A.ptr(nd, C.c_int32), A.ptr(sf, C.c_float), C.c_int(ini_th), C.c_int(min_th),
+                            C.c_int(max_kp), A.ptr(x, C.c_float), A.ptr(y, C.c_float), A.ptr(o, C.c_int32),
+                            A.ptr(sz, C.c_float), A.ptr(r, C.c_float), A.ptr(lo, C.c_int32))
+    assert n >= 0
+    return dict(x=x[:n].copy(), y=y[:n].copy(), octave=o[:n].copy(), size=sz[:n].copy(), response=r[:n].copy(),
+                level_off=lo)

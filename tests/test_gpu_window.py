@@ -187,3 +187,15 @@ def test_orb_fast_cells(ctx, seed, nfeat, ini, mn):
     for k in ("x", "y", "response"):
         assert np.array_equal(g[k], o[k]), k
     assert len(o["x"]) > 1000
+
+
+@pytest.mark.parametrize("seed,nfeat", [(61, 1000), (62, 2000), (63, 500)])
+def test_orb_detect(ctx, seed, nfeat):
+    """SURVEY §8f row 3: FAST cells (device) + retention (host, std::nth_element as OpenCV) vs the
+    oracle's restatement of the same libstdc++ algorithms: keypoints, order and attributes equal."""
+    pr = synth.orb_problem(seed=seed, n_kps=1)
+    nd = O.orb_features_per_level(nfeat)
+    g = ctx.orb_detect(pr["pyr"], nd, synth.scale_factors())
+    o = O.orb_detect(pr["pyr"], nd, synth.scale_factors())
+    for k in ("x", "y", "octave", "size", "response", "level_off"):
+        assert np.array_equal(g[k], o[k]), k

@@ -106,3 +106,16 @@ def test_orb_cells_layout():
     pr = synth.orb_problem(seed=42, n_kps=1)
     out = O.orb_fast_cells(pr["pyr"], nd)
     assert len(out["x"]) > 1000 and out["cell_base"][-1] > 8
+
+
+def test_orb_detect_oracle():
+    """Retention: per level at most n_desired keypoints (exactly n_desired when FAST finds enough),
+    responses of kept keypoints dominate the dropped ones of their cell."""
+    pr = synth.orb_problem(seed=43, n_kps=1)
+    nd = O.orb_features_per_level(1000)
+    d = O.orb_detect(pr["pyr"], nd, synth.scale_factors())
+    lo = d["level_off"]
+    for l in range(8):
+        assert lo[l + 1] - lo[l] <= nd[l]
+        assert (d["octave"][lo[l]:lo[l + 1]] == l).all()
+    assert lo[-1] > 900
