@@ -323,6 +323,18 @@ int lorb_orb_fast_cells(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int3
                         int32_t min_th, int32_t max_keypoints, float* x, float* y, float* response,
                         int32_t max_cells, int32_t* cell_base, int32_t* cell_off, int32_t* n_keypoints);
 
+/* SURVEY §8f row 3, ORBextractor::ComputePyramid (src/ORBextractor.cpp:1157-1184): level 0 is
+ * the image, level l = cv::resize(level l-1, cvRound(size / scale_factors[l]), INTER_LINEAR)
+ * (OpenCV 3.1's 8U fixed-point resize incl. its SSE2 vertical pass, see oracle/orb.c).  Levels are
+ * packed row-major into `out` (out_bytes capacity); `layout` receives the lorb_image_pyramid view
+ * (data = out).  The reference's copyMakeBorder margins are never read downstream and are not
+ * produced.  _dev: device image and out (returns after the levels are written). */
+int lorb_orb_pyramid(lorb_ctx* ctx, const uint8_t* image, int32_t rows, int32_t cols, int32_t step, int32_t n_levels,
+                     const float* scale_factors, uint8_t* out, int64_t out_bytes, lorb_image_pyramid* layout);
+int lorb_orb_pyramid_dev(lorb_ctx* ctx, const uint8_t* d_image, int32_t rows, int32_t cols, int32_t step,
+                         int32_t n_levels, const float* scale_factors, uint8_t* d_out, int64_t out_bytes,
+                         lorb_image_pyramid* layout);
+
 /* SURVEY §8f row 3, ORBextractor::ComputeKeyPointsOctTree without the orientation
  * (src/ORBextractor.cpp:898-1067): lorb_orb_fast_cells, then the nToRetain distribution,
  * KeyPointsFilter::retainBest + resize per cell (std::nth_element / std::partition, as OpenCV),

@@ -407,6 +407,121 @@ int orb_cells(int rows, int cols, int n_desired, float image_ratio, std::vector<
   return levelRows * levelCols;
 }
 
+// ---- ComputePyramid (src/ORBextractor.cpp:1157-1184): OpenCV 3.1 8U INTER_LINEAR resize ----
+// Host: the tap tables exactly as imgwarp.cpp builds them (double -> float coordinates,
+// cvRound(c * 2048) as short).  Device: one thread per destination pixel, the two source rows'
+// integer horizontal taps, then the vertical combine -- SSE2 VResizeLinearVec_32s8u arithmetic for
+// columns < xs and the scalar FixedPtCast for the rest (oracle/orb.c states the formulas).
+__device__ __forceinline__ int sat16d(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+
+__global__ __launch_bounds__(256) void k_orb_resize(const uint8_t* __restrict__ src, int sh, int sw, int sstep,
+                                                    uint8_t* __restrict__ dst, int dh, int dw, int dstep,
+                                                    const int* __restrict__ xofs, const short2* __restrict__ ia,
+                                                    const int* __restrict__ yofs, const short2* __restrict__ ib,
+                                                    int xmax, int xs) {
+  const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (dx >= dw || dy >= dh) return;
+  const int sx = xofs[dx];
+  const short2 a = ia[dx];
+  int r[2];
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    int sy = yofs[dy] + k;
+    sy = sy < 0 ? 0 : (sy >= sh ? sh - 1 : sy);
+    const uint8_t* S = src + (int64_t)sy * sstep;
+    r[k] = dx < xmax ? S[sx] * a.x + S[sx + 1] * a.y : S[sx] * 2048;
+  }
+  const short2 b = ib[dy];
+  int v;
+  if (dx < xs) {
+    const int x0 = sat16d(r[0] >> 4), y0 = sat16d(r[1] >> 4);
+    const int m0 = (x0 * b.x) >> 16, m1 = (y0 * b.y) >> 16;
+    const int sum = sat16d(m0 + m1);
+    v = sat16d(sum + 2) >> 2;
+  } else {
+    v = (r[0] * b.x + r[1] * b.y + (1 << 21)) >> 22;
+  }
+  dst[(int64_t)dy * dstep + dx] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+}
+
+short sat16h(int v) { return (short)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v)); }
+
+void resize_tabs(int ssize, int dsize, std::vector<int>& ofs, std::vector<short2>& a, int* xmax_out, bool clamp) {
+  const double inv_scale = (double)dsize / ssize, scale = 1. / inv_scale;
+  int xmax = dsize;
+  ofs.resize(dsize); a.resize(dsize);
+  for (int dx = 0; dx < dsize; dx++) {
+    float f = (float)((dx + 0.5) * scale - 0.5);
+    int s = (int)std::floor(f);
+    f -= s;
+    if (clamp) {
+      if (s < 0) { f = 0; s = 0; }
+      if (s + 1 >= ssize) {
+        xmax = std::min(xmax, dx);
+        if (s >= ssize - 1) { f = 0; s = ssize - 1; }
+      }
+    }
+    ofs[dx] = s;
+    a[dx].x = sat16h((int)std::nearbyint((1.f - f) * 2048));
+    a[dx].y = sat16h((int)std::nearbyint(f * 2048));
+  }
+  if (xmax_out) *xmax_out = xmax;
+}
+
+int simd_cols(int width) {
+  int x = 0;
+  while (x <= width - 16) x += 16;
+  while (x < width - 4) x += 4;
+  return x;
+}
+
+int pyramid_layout(int rows, int cols, int n_levels, const float* sf, lorb_image_pyramid* P) {
+  std::memset(P, 0, sizeof(*P));
+  P->n_levels = n_levels;
+  int64_t off = 0;
+  for (int l = 0; l < n_levels; l++) {
+    const float inv = 1.0f / sf[l];
+    P->cols[l] = (int)std::nearbyint((float)cols * inv);
+    P->rows[l] = (int)std::nearbyint((float)rows * inv);
+    P->step[l] = P->cols[l];
+    P->offset[l] = off;
+    off += (int64_t)P->rows[l] * P->cols[l];
+  }
+  return (int)std::min<int64_t>(off, INT32_MAX);
+}
+
+int enqueue_pyramid(lorb_ctx* ctx, const uint8_t* d_img, int rows, int cols, int step, const lorb_image_pyramid& P,
+                    uint8_t* d_out) {
+  LORB_HIP(ctx, hipMemcpy2DAsync(d_out, P.cols[0], d_img, step, P.cols[0], P.rows[0], hipMemcpyDeviceToDevice,
+                                 ctx->stream));
+  // the tap tables stay alive until the stream has consumed them (synchronised below)
+  std::vector<std::vector<int>> keep_i(2 * P.n_levels);
+  std::vector<std::vector<short2>> keep_s(2 * P.n_levels);
+  for (int l = 1; l < P.n_levels; l++) {
+    std::vector<int>& xofs = keep_i[2 * l];
+    std::vector<int>& yofs = keep_i[2 * l + 1];
+    std::vector<short2>& ia = keep_s[2 * l];
+    std::vector<short2>& ib = keep_s[2 * l + 1];
+    int xmax;
+    resize_tabs(P.cols[l - 1], P.cols[l], xofs, ia, &xmax, true);
+    resize_tabs(P.rows[l - 1], P.rows[l], yofs, ib, nullptr, false);
+    int *dxo, *dyo;
+    short2 *dia, *dib;
+    LORB_TRY(lorb::upload_t(ctx, S_ORB + 8 + 4 * (l & 1), xofs.data(), xofs.size(), &dxo));
+    LORB_TRY(lorb::upload_t(ctx, S_ORB + 9 + 4 * (l & 1), ia.data(), ia.size(), &dia));
+    LORB_TRY(lorb::upload_t(ctx, S_ORB + 10 + 4 * (l & 1), yofs.data(), yofs.size(), &dyo));
+    LORB_TRY(lorb::upload_t(ctx, S_ORB + 11 + 4 * (l & 1), ib.data(), ib.size(), &dib));
+    const dim3 grid(lorb::ceil_div(P.cols[l], 64), lorb::ceil_div(P.rows[l], 4));
+    hipLaunchKernelGGL(k_orb_resize, grid, dim3(256), 0, ctx->stream, d_out + P.offset[l - 1], P.rows[l - 1],
+                       P.cols[l - 1], P.step[l - 1], d_out + P.offset[l], P.rows[l], P.cols[l], P.step[l], dxo, dia, dyo,
+                       dib, xmax, simd_cols(P.cols[l]));
+  }
+  LORB_CHECK_LAUNCH(ctx);
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -648,6 +763,47 @@ int lorb_orb_detect(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t*
   *n_keypoints = out;
   if (out > max_keypoints)
     return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints exceed max_keypoints = %d", out, max_keypoints);
+  return LORB_OK;
+}
+
+
+int lorb_orb_pyramid(lorb_ctx* ctx, const uint8_t* image, int32_t rows, int32_t cols, int32_t step, int32_t n_levels,
+                     const float* scale_factors, uint8_t* out, int64_t out_bytes, lorb_image_pyramid* layout) {
+  if (!ctx) return LORB_E_INVALID;
+  if (!image || !scale_factors || !out || !layout || rows < 1 || cols < 1 || step < cols || n_levels < 1 ||
+      n_levels > LORB_MAX_LEVELS)
+    return lorb::set_error(ctx, LORB_E_INVALID, "bad image / level arguments");
+  const int64_t need = pyramid_layout(rows, cols, n_levels, scale_factors, layout);
+  for (int l = 0; l < n_levels; l++)
+    if (layout->rows[l] < 2 || layout->cols[l] < 2)
+      return lorb::set_error(ctx, LORB_E_INVALID, "level %d smaller than 2 x 2", l);
+  if (out_bytes < need) return lorb::set_error(ctx, LORB_E_INVALID, "out holds %lld bytes, %lld needed",
+                                               (long long)out_bytes, (long long)need);
+  uint8_t *dimg, *dout;
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 16, image, (size_t)(rows - 1) * step + cols, &dimg));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 17, (size_t)need, &dout));
+  LORB_TRY(enqueue_pyramid(ctx, dimg, rows, cols, step, *layout, dout));
+  LORB_HIP(ctx, hipMemcpyAsync(out, dout, (size_t)need, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  layout->data = out;
+  return LORB_OK;
+}
+
+int lorb_orb_pyramid_dev(lorb_ctx* ctx, const uint8_t* d_image, int32_t rows, int32_t cols, int32_t step,
+                         int32_t n_levels, const float* scale_factors, uint8_t* d_out, int64_t out_bytes,
+                         lorb_image_pyramid* layout) {
+  if (!ctx) return LORB_E_INVALID;
+  if (!d_image || !scale_factors || !d_out || !layout || rows < 1 || cols < 1 || step < cols || n_levels < 1 ||
+      n_levels > LORB_MAX_LEVELS)
+    return lorb::set_error(ctx, LORB_E_INVALID, "bad image / level arguments");
+  const int64_t need = pyramid_layout(rows, cols, n_levels, scale_factors, layout);
+  for (int l = 0; l < n_levels; l++)
+    if (layout->rows[l] < 2 || layout->cols[l] < 2)
+      return lorb::set_error(ctx, LORB_E_INVALID, "level %d smaller than 2 x 2", l);
+  if (out_bytes < need) return lorb::set_error(ctx, LORB_E_INVALID, "out holds %lld bytes, %lld needed",
+                                               (long long)out_bytes, (long long)need);
+  LORB_TRY(enqueue_pyramid(ctx, d_image, rows, cols, step, *layout, d_out));
+  layout->data = d_out;
   return LORB_OK;
 }
 

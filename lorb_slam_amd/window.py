@@ -200,6 +200,22 @@ def _orb_detect(self, pyr, n_desired, scale_factors, ini_th=20, min_th=7, max_kp
                 level_off=lo)
 
 
+def _orb_pyramid(self, img, scale_factors):
+    """ORBextractor::ComputePyramid on the device -> list of level images."""
+    img = A.u8(img)
+    sf = A.f32(scale_factors)
+    total = int(sum(int(np.rint(np.float32(img.shape[0]) * (np.float32(1) / s))) *
+                    int(np.rint(np.float32(img.shape[1]) * (np.float32(1) / s))) for s in sf))
+    out = np.zeros(total + 16, np.uint8)
+    P = A.ImagePyramid()
+    self.check(lib().lorb_orb_pyramid(self._p, A.ptr(img, C.c_uint8), C.c_int32(img.shape[0]), C.c_int32(img.shape[1]),
+                                      C.c_int32(img.shape[1]), C.c_int32(len(sf)), A.ptr(sf, C.c_float),
+                                      A.ptr(out, C.c_uint8), C.c_int64(len(out)), C.byref(P)), "lorb_orb_pyramid")
+    return [out[P.offset[l]:P.offset[l] + P.rows[l] * P.cols[l]].reshape(P.rows[l], P.cols[l]).copy()
+            for l in range(len(sf))]
+
+
+Context.orb_pyramid = _orb_pyramid
 Context.orb_detect = _orb_detect
 Context.orb_fast_cells = _orb_fast_cells
 Context.orb_describe = _orb_describe

@@ -130,6 +130,12 @@ int or_orb_detect(const lorb_image_pyramid* P, const int32_t* n_desired, const f
                   int min_th, int max_kp, float* ox, float* oy, int32_t* ooct, float* osize, float* oresp,
                   int32_t* level_off);
 
+/* orb.c: ORBextractor::ComputePyramid with OpenCV 3.1's 8U INTER_LINEAR resize restated */
+int or_resize_simd_cols(int width);
+void or_resize_linear_8u(const uint8_t* src, int sh, int sw, int sstep, uint8_t* dst, int dh, int dw, int dstep);
+void or_orb_pyramid(const uint8_t* img, int rows, int cols, int step, int n_levels, const float* scale_factors,
+                    uint8_t* out, lorb_image_pyramid* P);
+
 #ifdef __cplusplus
 }
 #endif

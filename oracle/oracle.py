@@ -361,3 +361,25 @@ def orb_detect(pyr, n_desired, scale_factors, ini_th=20, min_th=7, max_kp=100000
     assert n >= 0
     return dict(x=x[:n].copy(), y=y[:n].copy(), octave=o[:n].copy(), size=sz[:n].copy(), response=r[:n].copy(),
                 level_off=lo)
+
+
+def orb_pyramid(img, scale_factors):
+    """ORBextractor::ComputePyramid (src/ORBextractor.cpp:1157-1184) -> list of level images."""
+    img = A.u8(img)
+    sf = A.f32(scale_factors)
+    n = len(sf)
+    total = int(sum(int(np.rint(np.float32(img.shape[0]) * (np.float32(1) / s))) *
+                    int(np.rint(np.float32(img.shape[1]) * (np.float32(1) / s))) for s in sf))
+    out = np.zeros(total + 16, np.uint8)
+    P = A.ImagePyramid()
+    lib().or_orb_pyramid(A.ptr(img, C.c_uint8), C.c_int(img.shape[0]), C.c_int(img.shape[1]), C.c_int(img.shape[1]),
+                         C.c_int(n), A.ptr(sf, C.c_float), A.ptr(out, C.c_uint8), C.byref(P))
+    return [out[P.offset[l]:P.offset[l] + P.rows[l] * P.cols[l]].reshape(P.rows[l], P.cols[l]).copy() for l in range(n)]
+
+
+def resize_linear(img, h, w):
+    img = A.u8(img)
+    out = np.zeros((h, w), np.uint8)
+    lib().or_resize_linear_8u(A.ptr(img, C.c_uint8), C.c_int(img.shape[0]), C.c_int(img.shape[1]),
+                              C.c_int(img.shape[1]), A.ptr(out, C.c_uint8), C.c_int(h), C.c_int(w), C.c_int(w))
+    return out

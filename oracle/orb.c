@@ -156,3 +156,114 @@ void or_orb_describe(const lorb_image_pyramid* P, int n, const float* x, const f
   }
   for (int l = 0; l < P->n_levels; l++) free(blurred[l]);
 }
+
+/* ---- ORBextractor::ComputePyramid (src/ORBextractor.cpp:1157-1184) ------------------------
+ * Level 0 is the image; level l is cv::resize(level l-1, Size(cvRound(cols * inv_l),
+ * cvRound(rows * inv_l)), INTER_LINEAR) with inv_l = 1.0f / scale_l.  OpenCV 3.1's 8U linear
+ * resize is restated from imgwarp.cpp: fixed-point taps (cvRound(c * 2048) as short), exact
+ * integer horizontal pass, and the vertical pass of VResizeLinearVec_32s8u (SSE2) for the first
+ * columns -- (S >> 4) as int16, _mm_mulhi_epi16 with the taps, saturating add, (+2) >> 2, packus --
+ * followed by the scalar FixedPtCast ((s + 2^21) >> 22) for the remaining ones.  The borders
+ * copyMakeBorder adds are never read downstream (keypoints keep EDGE_THRESHOLD) and are not
+ * produced.  IPP builds of OpenCV may resize differently; that cannot be checked here. */
+static int16_t sat16(int v) { return (int16_t)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v)); }
+static uint8_t satu8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+int or_resize_simd_cols(int width) {  /* columns [0, x) take the SSE2 path */
+  int x = 0;
+  while (x <= width - 16) x += 16;
+  while (x < width - 4) x += 4;
+  return x;
+}
+
+void or_resize_tabs(int ssize, int dsize, int* ofs, int16_t* a /* 2 per entry */, int* xmax_out) {
+  const double inv_scale = (double)dsize / ssize, scale = 1. / inv_scale;
+  int xmax = dsize;
+  for (int dx = 0; dx < dsize; dx++) {
+    float f = (float)((dx + 0.5) * scale - 0.5);
+    int s = (int)floorf(f);
+    f -= s;
+    if (s < 0) { f = 0; s = 0; }  /* sx < ksize2 - 1 = 0 */
+    if (s + 1 >= ssize) {
+      xmax = xmax < dx ? xmax : dx;
+      if (s >= ssize - 1) { f = 0; s = ssize - 1; }
+    }
+    ofs[dx] = s;
+    const float c0 = 1.f - f, c1 = f;
+    a[2 * dx] = sat16((int)lrintf(c0 * 2048));
+    a[2 * dx + 1] = sat16((int)lrintf(c1 * 2048));
+  }
+  if (xmax_out) *xmax_out = xmax;
+}
+
+void or_resize_linear_8u(const uint8_t* src, int sh, int sw, int sstep, uint8_t* dst, int dh, int dw, int dstep) {
+  int* xofs = (int*)malloc(sizeof(int) * dw);
+  int* yofs = (int*)malloc(sizeof(int) * dh);
+  int16_t* ia = (int16_t*)malloc(sizeof(int16_t) * 2 * dw);
+  int16_t* ib = (int16_t*)malloc(sizeof(int16_t) * 2 * dh);
+  int xmax;
+  or_resize_tabs(sw, dw, xofs, ia, &xmax);
+  /* rows: fy = (float)((dy+0.5)*scale_y - 0.5), sy = floor, no clamp of fy here (imgwarp.cpp) */
+  {
+    const double scale_y = 1. / ((double)dh / sh);
+    for (int dy = 0; dy < dh; dy++) {
+      float f = (float)((dy + 0.5) * scale_y - 0.5);
+      const int s = (int)floorf(f);
+      f -= s;
+      yofs[dy] = s;
+      ib[2 * dy] = sat16((int)lrintf((1.f - f) * 2048));
+      ib[2 * dy + 1] = sat16((int)lrintf(f * 2048));
+    }
+  }
+  const int xs = or_resize_simd_cols(dw);
+  int* r0 = (int*)malloc(sizeof(int) * dw);
+  int* r1 = (int*)malloc(sizeof(int) * dw);
+  for (int dy = 0; dy < dh; dy++) {
+    int* rr[2] = {r0, r1};
+    for (int k = 0; k < 2; k++) {
+      int sy = yofs[dy] + k;
+      sy = sy < 0 ? 0 : (sy >= sh ? sh - 1 : sy);  /* clip(sy0 - ksize2 + 1 + k, 0, height) */
+      const uint8_t* S = src + (size_t)sy * sstep;
+      for (int dx = 0; dx < dw; dx++) {
+        const int sx = xofs[dx];
+        rr[k][dx] = dx < xmax ? S[sx] * ia[2 * dx] + S[sx + 1] * ia[2 * dx + 1] : S[sx] * 2048;
+      }
+    }
+    const int b0 = ib[2 * dy], b1 = ib[2 * dy + 1];
+    uint8_t* D = dst + (size_t)dy * dstep;
+    for (int x = 0; x < dw; x++) {
+      if (x < xs) {
+        const int16_t x0 = sat16(r0[x] >> 4), y0 = sat16(r1[x] >> 4);
+        const int16_t m0 = (int16_t)(((int)x0 * b0) >> 16), m1 = (int16_t)(((int)y0 * b1) >> 16);
+        const int16_t s = sat16((int)m0 + (int)m1);
+        const int16_t t = (int16_t)(sat16((int)s + 2) >> 2);
+        D[x] = satu8(t);
+      } else {
+        D[x] = satu8((r0[x] * b0 + r1[x] * b1 + (1 << 21)) >> 22);
+      }
+    }
+  }
+  free(xofs); free(yofs); free(ia); free(ib); free(r0); free(r1);
+}
+
+/* the pyramid of one image: level l is rows_l x cols_l with cvRound((float)size * (1.0f / scale_l)),
+ * packed row-major in `out` at the offsets it returns in P (data = out) */
+void or_orb_pyramid(const uint8_t* img, int rows, int cols, int step, int n_levels, const float* scale_factors,
+                    uint8_t* out, lorb_image_pyramid* P) {
+  int64_t off = 0;
+  memset(P, 0, sizeof(*P));
+  P->n_levels = n_levels;
+  for (int l = 0; l < n_levels; l++) {
+    const float inv = 1.0f / scale_factors[l];
+    const int w = (int)lrintf((float)cols * inv), h = (int)lrintf((float)rows * inv);
+    P->offset[l] = off; P->rows[l] = h; P->cols[l] = w; P->step[l] = w;
+    uint8_t* D = out + off;
+    if (l == 0) {
+      for (int r = 0; r < h; r++) memcpy(D + (size_t)r * w, img + (size_t)r * step, (size_t)w);
+    } else {
+      or_resize_linear_8u(out + P->offset[l - 1], P->rows[l - 1], P->cols[l - 1], P->step[l - 1], D, h, w, w);
+    }
+    off += (int64_t)w * h;
+  }
+  P->data = out;
+}

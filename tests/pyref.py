@@ -281,3 +281,51 @@ def fast(img, th):
                 keep &= S > np.roll(np.roll(S, -dy, 0), -dx, 1)
     ys, xs = np.nonzero(keep)  # row-major = FAST's emission order
     return xs.astype(np.float32), ys.astype(np.float32), S[ys, xs].astype(np.float32)
+
+
+def resize_linear(img, h, w):  # OpenCV 3.1 8U INTER_LINEAR (imgwarp.cpp), numpy restatement
+    sh, sw = img.shape
+
+    def tabs(ss, ds, clamp):
+        scale = 1.0 / (ds / ss)
+        ofs, a0, a1, xmax = [], [], [], ds
+        for d in range(ds):
+            f = f32((d + 0.5) * scale - 0.5)
+            s = int(np.floor(f))
+            f = f32(f - f32(s))
+            if clamp:
+                if s < 0:
+                    f, s = f32(0), 0
+                if s + 1 >= ss:
+                    xmax = min(xmax, d)
+                    if s >= ss - 1:
+                        f, s = f32(0), ss - 1
+            ofs.append(s)
+            a0.append(int(np.clip(np.rint(f32(f32(1) - f) * f32(2048)), -32768, 32767)))
+            a1.append(int(np.clip(np.rint(f * f32(2048)), -32768, 32767)))
+        return np.array(ofs), np.array(a0, np.int64), np.array(a1, np.int64), xmax
+
+    xo, xa0, xa1, xmax = tabs(sw, w, True)
+    yo, yb0, yb1, _ = tabs(sh, h, False)
+    src = img.astype(np.int64)
+    xs = 0
+    while xs <= w - 16:
+        xs += 16
+    while xs < w - 4:
+        xs += 4
+    out = np.zeros((h, w), np.uint8)
+    cols = np.arange(w)
+    for dy in range(h):
+        rows = []
+        for k in (0, 1):
+            sy = min(max(yo[dy] + k, 0), sh - 1)
+            S = src[sy]
+            nxt = S[np.minimum(xo + 1, sw - 1)]
+            rows.append(np.where(cols < xmax, S[xo] * xa0 + nxt * xa1, S[xo] * 2048))
+        b0, b1 = yb0[dy], yb1[dy]
+        x0 = np.clip(rows[0] >> 4, -32768, 32767)
+        y0 = np.clip(rows[1] >> 4, -32768, 32767)
+        simd = np.clip(np.clip((x0 * b0 >> 16) + (y0 * b1 >> 16), -32768, 32767) + 2, -32768, 32767) >> 2
+        scal = (rows[0] * b0 + rows[1] * b1 + (1 << 21)) >> 22
+        out[dy] = np.clip(np.where(cols < xs, simd, scal), 0, 255).astype(np.uint8)
+    return out

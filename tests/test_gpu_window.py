@@ -199,3 +199,35 @@ def test_orb_detect(ctx, seed, nfeat):
     o = O.orb_detect(pr["pyr"], nd, synth.scale_factors())
     for k in ("x", "y", "octave", "size", "response", "level_off"):
         assert np.array_equal(g[k], o[k]), k
+
+
+@pytest.mark.parametrize("seed,shape", [(71, (480, 752)), (72, (333, 517))])
+def test_orb_pyramid(ctx, seed, shape):
+    """ComputePyramid (OpenCV 3.1 8U linear resize chain) bit-exact vs the oracle."""
+    rng = np.random.default_rng(seed)
+    img = synth.orb_problem(seed=seed, n_kps=1)["pyr"][0][:shape[0], :shape[1]]
+    img = np.clip(img.astype(np.int32) + rng.integers(-3, 4, img.shape), 0, 255).astype(np.uint8)
+    g = ctx.orb_pyramid(img, synth.scale_factors())
+    o = O.orb_pyramid(img, synth.scale_factors())
+    assert len(g) == len(o) == 8
+    for a, b in zip(g, o):
+        assert a.shape == b.shape and np.array_equal(a, b)
+
+
+def test_orb_extract_end_to_end(ctx):
+    """The whole ORBextractor::operator() on one image: pyramid -> FAST cells + retention ->
+    orientation + blur + rBRIEF, GPU path vs the oracle chain (keypoints, angles, descriptors)."""
+    img = synth.orb_problem(seed=73, n_kps=1)["pyr"][0]
+    sf = synth.scale_factors()
+    nd = O.orb_features_per_level(1000)
+    pattern = np.random.default_rng(9).integers(-13, 13, size=1024).astype(np.int32)
+    gp = ctx.orb_pyramid(img, sf)
+    gd = ctx.orb_detect(gp, nd, sf)
+    ga, gdesc = ctx.orb_describe(gp, gd["x"], gd["y"], gd["octave"], pattern)
+    op = O.orb_pyramid(img, sf)
+    od = O.orb_detect(op, nd, sf)
+    oa, odesc = O.orb_describe(op, od["x"], od["y"], od["octave"], pattern)
+    assert len(gd["x"]) > 900
+    for k in ("x", "y", "octave", "response"):
+        assert np.array_equal(gd[k], od[k]), k
+    assert np.array_equal(ga, oa) and np.array_equal(gdesc, odesc)

@@ -119,3 +119,19 @@ def test_orb_detect_oracle():
         assert lo[l + 1] - lo[l] <= nd[l]
         assert (d["octave"][lo[l]:lo[l + 1]] == l).all()
     assert lo[-1] > 900
+
+
+def test_resize_oracle_vs_pyref():
+    """OpenCV 3.1 8U linear resize: C restatement == numpy restatement; a constant stays constant;
+    a horizontal ramp resamples within 1 grey level of the exact linear interpolation."""
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, size=(97, 131), dtype=np.uint8)
+    for h, w in ((81, 109), (67, 91), (40, 56)):
+        assert np.array_equal(O.resize_linear(img, h, w), pyref.resize_linear(img, h, w))
+    assert (O.resize_linear(np.full((50, 70), 77, np.uint8), 42, 58) == 77).all()
+    ramp = np.tile(np.arange(200, dtype=np.float64), (20, 1)).astype(np.uint8)
+    out = O.resize_linear(ramp, 17, 167).astype(np.float64)
+    xs = (np.arange(167) + 0.5) * (200 / 167) - 0.5
+    assert np.abs(out[5] - np.clip(xs, 0, 199)).max() <= 1.0
+    pyr = O.orb_pyramid(img, synth.scale_factors())
+    assert [p.shape for p in pyr[:3]] == [(97, 131), (81, 109), (67, 91)]
