@@ -294,9 +294,17 @@ __global__ __launch_bounds__(1024) void k_orb_fast(const uint8_t* __restrict__ d
   uint8_t* corner = lds + 2 * n;
   const uint8_t* src = data + P.offset[c.level] + (int64_t)c.ini_y * P.step[c.level] + c.ini_x;
   const int step = P.step[c.level];
-  for (int p = t; p < n; p += 1024) {
-    const int i = p / w, j = p - i * w;
-    img[p] = src[(int64_t)i * step + j];
+  for (int p0 = t; p0 < n; p0 += 1024 * 8) {  // eight loads in flight per thread
+    uint8_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int p = p0 + 1024 * u;
+      const int i = p / w, j = p - i * w;
+      v[u] = p < n ? src[(int64_t)i * step + j] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (p0 + 1024 * u < n) img[p0 + 1024 * u] = v[u];
   }
   if (t < 25) pixel[t] = kOff16[t & 15][0] + kOff16[t & 15][1] * w;
   for (int pass = 0; pass < 2; ++pass) {

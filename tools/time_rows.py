@@ -113,4 +113,33 @@ assert np.array_equal(odesc.numpy(), rd) and np.array_equal(oang.numpy(), ra)
 out["orb_describe"] = dict(gpu_us=us, cpu_us=cpu(lambda: O.orb_describe(op["pyr"], op["x"], op["y"], op["level"],
                                                                         op["pattern"])),
                            n_kps=2000, pyramid="752x480, 8 levels x 1.2")
+# row 3: the whole extractor on one 752x480 image: pyramid + FAST cells + retention (host) + describe
+img = synth.orb_problem(seed=73, n_kps=1)["pyr"][0]
+sf = synth.scale_factors()
+nd = O.orb_features_per_level(1000)
+pat = np.random.default_rng(9).integers(-13, 13, size=1024).astype(np.int32)
+
+
+def extract_gpu():
+    p = ctx.orb_pyramid(img, sf)
+    d = ctx.orb_detect(p, nd, sf)
+    return ctx.orb_describe(p, d["x"], d["y"], d["octave"], pat)
+
+
+def extract_cpu():
+    p = O.orb_pyramid(img, sf)
+    d = O.orb_detect(p, nd, sf)
+    return O.orb_describe(p, d["x"], d["y"], d["octave"], pat)
+
+
+def wall(fn, reps):
+    fn()
+    t = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return (time.perf_counter() - t) * 1e6 / reps
+
+
+out["orb_extract"] = dict(gpu_us=wall(extract_gpu, 20), cpu_us=wall(extract_cpu, 3),
+                          note="host API calls incl. H2D/D2H per stage (not device-resident)")
 print(json.dumps(out))
