@@ -231,3 +231,20 @@ def test_orb_extract_end_to_end(ctx):
     for k in ("x", "y", "octave", "response"):
         assert np.array_equal(gd[k], od[k]), k
     assert np.array_equal(ga, oa) and np.array_equal(gdesc, odesc)
+
+
+def test_orb_and_stereo_argument_errors(ctx):
+    """The 8f-row entry points reject malformed inputs with an error instead of reading out of
+    bounds: degenerate cell grids, too-small pyramids, pyramids with fewer levels than the frame."""
+    from lorb_slam_amd.runtime import LorbError
+    pr = synth.orb_problem(seed=81, n_kps=4)
+    nd = O.orb_features_per_level(1000)
+    with pytest.raises(LorbError):  # a level asking for 1 feature has a 0-column cell grid
+        ctx.orb_fast_cells(pr["pyr"], np.array([1] * 8, np.int32))
+    with pytest.raises(LorbError):  # 1 x 1 levels
+        ctx.orb_pyramid(np.zeros((4, 4), np.uint8), synth.scale_factors())
+    sp = synth.stereo_problem(seed=82, n_left=50, n_distract=10)
+    with pytest.raises(LorbError):  # right pyramid with fewer levels than the frame
+        ctx.compute_stereo_matches(sp["fp"], sp["left"], sp["right"], sp["pyr_l"], sp["pyr_r"][:3])
+    with pytest.raises(LorbError):  # capacity too small is reported, not overrun
+        ctx.orb_detect(pr["pyr"], nd, synth.scale_factors(), max_kp=10)
