@@ -231,7 +231,8 @@ int lorb_is_in_frustum(lorb_ctx* ctx, const lorb_frame_params* frame, const floa
  * All pointers below are DEVICE pointers (a lorb_keypoints whose arrays live on the device);
  * frame / Tcw are host values.  Outputs: d_in_view (mbTrackInView), d_track (n x 4 as four
  * planes: mTrackProjX, mTrackProjY, mTrackProjXR, mTrackViewCos), d_level (mnTrackScaleLevel),
- * d_assign / d_nmatches as lorb_search_by_projection_local. */
+ * d_assign / d_nmatches as lorb_search_by_projection_local.  Asynchronous on the ctx stream while
+ * n_points * n_keypoints <= 8M; larger calls read the candidate count back once. */
 typedef struct lorb_map_points_dev {
   int32_t n;
   const float* pos;          /* GetPos(), n x 3 */

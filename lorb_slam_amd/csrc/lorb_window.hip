@@ -269,6 +269,21 @@ __global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ cnt, int 
   if (threadIdx.x == 0) off[n] = carry;
 }
 
+// Candidate list of a windowed match: a query has at most nk candidates, so `bound` = n_queries *
+// nk entries always suffice.  Up to kCandBound entries that bound is allocated and the call needs
+// no host round trip; past it the exact total (d_total, written by k_scan) is read back.
+int alloc_candidates(lorb_ctx* ctx, const int* d_total, size_t bound, int2** cand) {
+  constexpr size_t kCandBound = size_t(8) << 20;
+  size_t cap = bound;
+  if (cap > kCandBound) {
+    int total = 0;
+    LORB_HIP(ctx, hipMemcpyAsync(&total, d_total, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    cap = (size_t)total;
+  }
+  return lorb::scratch_t(ctx, S_W9, std::max<size_t>(cap, 1), cand);
+}
+
 // resolver state in LDS when claim + res fit (nk + np ints <= 120 KiB)
 inline size_t resolve_lds_bytes(int np, int nk) {
   const size_t b = sizeof(int) * ((size_t)np + (size_t)nk);
@@ -568,11 +583,8 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
                        reinterpret_cast<const uint4*>(pd), cnt, (const int*)nullptr, (int2*)nullptr);
   }
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, np, off);
-  int total = 0;
-  LORB_HIP(ctx, hipMemcpyAsync(&total, off + np, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   int2* cand;
-  LORB_TRY(lorb::scratch_t(ctx, S_W9, (size_t)std::max(total, 1), &cand));
+  LORB_TRY(alloc_candidates(ctx, off + np, (size_t)np * (size_t)nk, &cand));
   if (np > 0)
     hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
                        reinterpret_cast<const uint4*>(pd), cnt, off, cand);
@@ -643,11 +655,8 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
                        reinterpret_cast<const uint4*>(ld), cnt, (const int*)nullptr, (int2*)nullptr);
   }
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, nl, off);
-  int total = 0;
-  LORB_HIP(ctx, hipMemcpyAsync(&total, off + nl, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   int2* cand;
-  LORB_TRY(lorb::scratch_t(ctx, S_W9, (size_t)std::max(total, 1), &cand));
+  LORB_TRY(alloc_candidates(ctx, off + nl, (size_t)nl * (size_t)nk, &cand));
   if (nl > 0)
     hipLaunchKernelGGL(k_cand_frame<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
                        reinterpret_cast<const uint4*>(ld), cnt, off, cand);
@@ -758,11 +767,8 @@ int lorb_track_local_map_dev(lorb_ctx* ctx, const lorb_frame_params* frame, cons
                        (const int*)nullptr, (int2*)nullptr);
   }
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, np, off);
-  int total = 0;  // candidate-list size: the one device -> host word of the call
-  LORB_HIP(ctx, hipMemcpyAsync(&total, off + np, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   int2* cand;
-  LORB_TRY(lorb::scratch_t(ctx, S_W9, (size_t)std::max(total, 1), &cand));
+  LORB_TRY(alloc_candidates(ctx, off + np, (size_t)np * (size_t)nk, &cand));
   if (np > 0)
     hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, d_in_view, pts->is_bad, tx,
                        tx + np, tx + 2 * np, d_level, tx + 3 * np, reinterpret_cast<const uint4*>(pts->desc), cnt, off,
