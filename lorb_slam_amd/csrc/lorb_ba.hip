@@ -175,25 +175,26 @@ __device__ __forceinline__ int u21(int a, int b) {  // packed upper index of 6x6
   return a * 6 - (a * (a - 1)) / 2 + (b - a);
 }
 
-// K0: state init
-__global__ void k_ba_init(BaDev d, int W, LMOpt o) {
-  const int w = blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= W) return;
-  WinState s;
-  s.radius = o.init_radius; s.decrease_factor = 2.0; s.cost = 0.0; s.x_norm = 0.0; s.gmax = 0.0;
-  s.initial_cost = 0.0; s.iter = 0; s.n_success = 0; s.n_invalid = 0;
-  s.done = d.win[w].n_obs_all == 0 ? 1 : 0;
-  s.relin = 1; s.cur = 0; s.last_successful = 1; s.term = 0; s.chol_fail = 0; s.pad = 0;
-  d.st[w] = s;
-}
-
-// K0: per-camera rotation state of the linearisation point (transcendentals once per camera)
-__global__ __launch_bounds__(64) void k_ba_rot_lin(BaDev d, int ctot) {
-  const int c = blockIdx.x * 64 + threadIdx.x;
-  if (c >= ctot) return;
-  const WinState& S = d.st[d.cam_win[c]];
-  if (S.done || !S.relin) return;
-  d.rot_lin[c] = lorb::rot_jet(d.x_pose[S.cur] + 6 * c);
+// K0: start of a solve, one launch: window states, x[0] <- the initial values, and the
+// per-camera rotation states of that first linearisation point (transcendentals once per
+// camera; later ones come from k_ba_lm_end on acceptance).
+__global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n_pt, LMOpt o) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < W) {
+    WinState s;
+    s.radius = o.init_radius; s.decrease_factor = 2.0; s.cost = 0.0; s.x_norm = 0.0; s.gmax = 0.0;
+    s.initial_cost = 0.0; s.iter = 0; s.n_success = 0; s.n_invalid = 0;
+    s.done = d.win[i].n_obs_all == 0 ? 1 : 0;
+    s.relin = 1; s.cur = 0; s.last_successful = 1; s.term = 0; s.chol_fail = 0; s.pad = 0;
+    d.st[i] = s;
+  }
+  if (i < ctot) {
+    double x[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { x[k] = d.x_init_pose[6 * i + k]; d.x_pose[0][6 * i + k] = x[k]; }
+    d.rot_lin[i] = lorb::rot_jet(x);
+  }
+  for (int k = i; k < 3 * n_pt; k += gridDim.x * blockDim.x) d.x_pt[0][k] = d.x_init_pt[k];
 }
 
 // Point groups (PBlk): consecutive points of one window whose observations (contiguous, sorted
@@ -2190,12 +2191,12 @@ int enqueue_finalize(lorb_ba_plan* P, const LMOpt& o) {
 int plan_solve(lorb_ba_plan* P, const lorb_lm_options* opt) {
   lorb_ctx* ctx = P->ctx;
   LMOpt o = to_dev_opt(opt);
-  // restore the initial values into x[0] (x[1] is the candidate buffer)
-  if (P->Ctot) LORB_HIP(ctx, hipMemcpyAsync(P->dev.x_pose[0], P->dev.x_init_pose, sizeof(double) * 6 * P->Ctot, hipMemcpyDeviceToDevice, ctx->stream));
-  if (P->Ptot) LORB_HIP(ctx, hipMemcpyAsync(P->dev.x_pt[0], P->dev.x_init_pt, sizeof(double) * 3 * P->Ptot, hipMemcpyDeviceToDevice, ctx->stream));
-  hipLaunchKernelGGL(k_ba_init, dim3(lorb::ceil_div(P->W, 64)), dim3(64), 0, ctx->stream, P->dev, P->W, o);
-  // rotation states of the initial linearisation point (later ones: k_ba_lm_end on acceptance)
-  if (P->Ctot) hipLaunchKernelGGL(k_ba_rot_lin, dim3(lorb::ceil_div(P->Ctot, 64)), dim3(64), 0, ctx->stream, P->dev, P->Ctot);
+  // x[0] <- the initial values (x[1] is the candidate buffer), window states, rotation states
+  {
+    const int n = std::max(std::max(P->W, P->Ctot), std::min(3 * P->Ptot, 256 * 1024));
+    hipLaunchKernelGGL(k_ba_init, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, P->dev, P->W, P->Ctot,
+                       P->Ptot, o);
+  }
   LORB_CHECK_LAUNCH(ctx);
   // per-kernel events cannot live inside a graph, and neither can a host-transport exchange
   static const bool no_graph = [] { const char* e = getenv("LORB_NO_GRAPH"); return e && e[0] == '1'; }();

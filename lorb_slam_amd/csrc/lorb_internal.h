@@ -22,6 +22,10 @@ struct lorb_ctx {
   static constexpr int kScratch = 96;
   void* scratch[kScratch] = {};
   size_t scratch_sz[kScratch] = {};
+  // host copy of the bytes last uploaded into a slot (lorb::upload); an identical re-upload of
+  // per-call constants (problem offsets, scan tiles) is skipped.  Cleared whenever the slot is
+  // handed out as kernel-written scratch.
+  std::vector<unsigned char> up_mirror[kScratch];
   // per-kernel event timing
   bool ktime = false;
   std::vector<hipEvent_t> kev_pool;

@@ -13,10 +13,11 @@ int set_error(lorb_ctx* ctx, int code, const char* fmt, ...) {
   return code;
 }
 
-int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out) {
+static int scratch_alloc(lorb_ctx* ctx, int slot, size_t bytes, void** out) {
   if (slot < 0 || slot >= lorb_ctx::kScratch) return set_error(ctx, LORB_E_INVALID, "bad scratch slot %d", slot);
   if (bytes == 0) bytes = 16;
   if (ctx->scratch_sz[slot] < bytes) {
+    ctx->up_mirror[slot].clear();
     if (ctx->scratch[slot]) {
       LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
       LORB_HIP(ctx, hipFree(ctx->scratch[slot]));
@@ -31,9 +32,19 @@ int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out) {
   return LORB_OK;
 }
 
+int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out) {
+  LORB_TRY(scratch_alloc(ctx, slot, bytes, out));
+  ctx->up_mirror[slot].clear();  // kernels may write it: the uploaded bytes are no longer known
+  return LORB_OK;
+}
+
 int upload(lorb_ctx* ctx, int slot, const void* host, size_t bytes, void** dev) {
-  LORB_TRY(scratch(ctx, slot, bytes, dev));
-  if (bytes) LORB_HIP(ctx, hipMemcpyAsync(*dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+  LORB_TRY(scratch_alloc(ctx, slot, bytes, dev));
+  if (!bytes) return LORB_OK;
+  std::vector<unsigned char>& m = ctx->up_mirror[slot];
+  if (m.size() == bytes && std::memcmp(m.data(), host, bytes) == 0) return LORB_OK;  // already resident
+  LORB_HIP(ctx, hipMemcpyAsync(*dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
+  m.assign(static_cast<const unsigned char*>(host), static_cast<const unsigned char*>(host) + bytes);
   return LORB_OK;
 }
 
