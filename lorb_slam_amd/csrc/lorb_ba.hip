@@ -51,14 +51,34 @@ struct LMOpt {
   double ftol, gtol, ptol, init_radius, max_radius, min_radius, min_rel, min_diag, max_diag;
 };
 
+// Wave reductions, butterfly xor 32, 16, 8, 4, 2, 1.  The two cross-row steps go through
+// ds_bpermute; the four in-row steps are DPP moves (VALU, no LDS): row_ror:8 is xor 8 within a
+// 16-lane row, and once lanes i and i^8 agree row_ror:4 delivers the xor-4 partner's value;
+// quad_perm does xor 2 and xor 1.  Every step adds a lane and its partner (commutative), so all
+// lanes end with the same bits as the plain shuffle butterfly.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(u & 0xffffffffu), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += __shfl_xor(v, 32, 64);
+  v += __shfl_xor(v, 16, 64);
+  v += dpp_d<0x128>(v);  // row_ror:8
+  v += dpp_d<0x124>(v);  // row_ror:4
+  v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_d<0xB1>(v);   // quad_perm [1,0,3,2]
   return v;
 }
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  v = fmax(v, __shfl_xor(v, 32, 64));
+  v = fmax(v, __shfl_xor(v, 16, 64));
+  v = fmax(v, dpp_d<0x128>(v));
+  v = fmax(v, dpp_d<0x124>(v));
+  v = fmax(v, dpp_d<0x4E>(v));
+  v = fmax(v, dpp_d<0xB1>(v));
   return v;
 }
 template <int N>
