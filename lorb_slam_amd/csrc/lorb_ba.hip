@@ -51,11 +51,12 @@ struct LMOpt {
   double ftol, gtol, ptol, init_radius, max_radius, min_radius, min_rel, min_diag, max_diag;
 };
 
-// Wave reductions, butterfly xor 32, 16, 8, 4, 2, 1.  The two cross-row steps go through
-// ds_bpermute; the four in-row steps are DPP moves (VALU, no LDS): row_ror:8 is xor 8 within a
-// 16-lane row, and once lanes i and i^8 agree row_ror:4 delivers the xor-4 partner's value;
-// quad_perm does xor 2 and xor 1.  Every step adds a lane and its partner (commutative), so all
-// lanes end with the same bits as the plain shuffle butterfly.
+// Wave reductions, butterfly xor 32, 16, 8, 4, 2, 1, with no LDS traffic.  The cross-row steps
+// use gfx950's v_permlane32_swap / v_permlane16_swap on two copies of the value: afterwards lane i
+// holds {v_i, v_(i^32)} (resp. i^16) across the two copies.  The in-row steps are DPP moves:
+// row_ror:8 is xor 8 within a 16-lane row, and once lanes i and i^8 agree row_ror:4 delivers the
+// xor-4 partner's value; quad_perm does xor 2 and xor 1.  Every step combines a lane and its
+// partner with a commutative op, so all lanes end with the bits of the plain shuffle butterfly.
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
   const unsigned long long u = __double_as_longlong(v);
@@ -63,9 +64,22 @@ __device__ __forceinline__ double dpp_d(double v) {
   const int hi = __builtin_amdgcn_mov_dpp((int)(u >> 32), CTRL, 0xF, 0xF, false);
   return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
+// {v_i, v_partner} for partner i^32 (W32) or i^16
+template <bool W32>
+__device__ __forceinline__ void xrow_pair(double v, double& a, double& b) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = (unsigned)(u & 0xffffffffu), hi = (unsigned)(u >> 32);
+  const auto l = W32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                     : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = W32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                     : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  a = __longlong_as_double(((unsigned long long)h[0] << 32) | l[0]);
+  b = __longlong_as_double(((unsigned long long)h[1] << 32) | l[1]);
+}
 __device__ __forceinline__ double wave_sum(double v) {
-  v += __shfl_xor(v, 32, 64);
-  v += __shfl_xor(v, 16, 64);
+  double a, b;
+  xrow_pair<true>(v, a, b); v = a + b;
+  xrow_pair<false>(v, a, b); v = a + b;
   v += dpp_d<0x128>(v);  // row_ror:8
   v += dpp_d<0x124>(v);  // row_ror:4
   v += dpp_d<0x4E>(v);   // quad_perm [2,3,0,1]
@@ -73,8 +87,9 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 __device__ __forceinline__ double wave_max(double v) {
-  v = fmax(v, __shfl_xor(v, 32, 64));
-  v = fmax(v, __shfl_xor(v, 16, 64));
+  double a, b;
+  xrow_pair<true>(v, a, b); v = fmax(a, b);
+  xrow_pair<false>(v, a, b); v = fmax(a, b);
   v = fmax(v, dpp_d<0x128>(v));
   v = fmax(v, dpp_d<0x124>(v));
   v = fmax(v, dpp_d<0x4E>(v));
