@@ -1139,8 +1139,11 @@ __global__ __launch_bounds__(256) void k_ba_chol_w(BaDev d) {
 #pragma unroll
       for (int u = 0; u < 16; ++u) a4[u & 3] = fma(av[u], zv[u], a4[u & 3]);
       double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-      acc += __shfl_xor(acc, 16, 64);
-      acc += __shfl_xor(acc, 32, 64);
+      {  // butterfly xor 16, xor 32 (permlane swaps, no LDS)
+        double a, b;
+        xrow_pair<false>(acc, a, b); acc = a + b;
+        xrow_pair<true>(acc, a, b); acc = a + b;
+      }
       double zb = z[j] - acc;
       const double iv = invd[j];
 #pragma unroll
@@ -1337,8 +1340,11 @@ struct BandSide {
 #pragma unroll
       for (int u = 0; u < 16; ++u) a4[u & 3] = fma(av[u], zv[u], a4[u & 3]);
       double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-      acc += __shfl_xor(acc, 16, 64);
-      acc += __shfl_xor(acc, 32, 64);
+      {  // butterfly xor 16, xor 32 (permlane swaps, no LDS)
+        double a, b;
+        xrow_pair<false>(acc, a, b); acc = a + b;
+        xrow_pair<true>(acc, a, b); acc = a + b;
+      }
       double zb = z[j] - acc;
       const double iv = A[idx(j, j)];  // 1 / L(j, j)
 #pragma unroll
