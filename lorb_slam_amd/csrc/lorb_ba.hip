@@ -272,20 +272,23 @@ __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
   __shared__ double sh[kGB][9];
   __shared__ double red4[4];
   const PBlk g = d.pblk[blockIdx.x];
+  const int t = threadIdx.x;
+  // plan-structure loads of the first chunk go out together with the window state
+  const int of = g.o0 + min(t, max(g.no - 1, 0));
+  const int p_f = g.no > 0 ? d.obs_pt[of] : 0, c_f = g.no > 0 ? d.obs_cam[of] : -1;
+  int po0 = 0, po1 = 0;
+  if (t < g.cnt) { po0 = d.pt_obs_off[g.p0 + t]; po1 = d.pt_obs_off[g.p0 + t + 1]; }
   const WinState& S = d.st[g.win];
   if (S.done || !S.relin) return;
   const BaWin& W = d.win[g.win];
   const int cur = S.cur;
-  const int t = threadIdx.x;
   double cost = 0.0;
   double E[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-  int po0 = 0, po1 = 0;
-  if (t < g.cnt) { po0 = d.pt_obs_off[g.p0 + t]; po1 = d.pt_obs_off[g.p0 + t + 1]; }
   for (int c0 = 0; c0 < g.no; c0 += kGB) {
     if (c0 + t < g.no) {
       const int o = g.o0 + c0 + t;
-      const int p = d.obs_pt[o];
-      const int c = d.obs_cam[o];
+      const int p = c0 == 0 ? p_f : d.obs_pt[o];
+      const int c = c0 == 0 ? c_f : d.obs_cam[o];
       double X[3], pose[6];
 #pragma unroll
       for (int k = 0; k < 3; ++k) X[k] = d.x_pt[cur][3 * p + k];
@@ -361,6 +364,7 @@ __global__ __launch_bounds__(256) void k_ba_camera(BaDev d) {
   __shared__ double red[4][27];
   const int c = blockIdx.x;
   const int w = d.cam_win[c];
+  const int a0 = d.cam_obs_off[c], a1 = d.cam_obs_off[c + 1];  // issued with cam_win
   const WinState& S = d.st[w];
   if (S.done || !S.relin) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -369,7 +373,6 @@ __global__ __launch_bounds__(256) void k_ba_camera(BaDev d) {
   for (int k = 0; k < 21; ++k) U[k] = 0.0;
 #pragma unroll
   for (int k = 0; k < 6; ++k) V[k] = 0.0;
-  const int a0 = d.cam_obs_off[c], a1 = d.cam_obs_off[c + 1];
   for (int e = a0 + t; e < a1; e += 256) {
     double J[12];
 #pragma unroll
@@ -486,16 +489,24 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
 __global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
   __shared__ double sEi[kGB][6], sb[kGB][3], ssp[kGB][3];
   const PBlk g = d.pblk[blockIdx.x];
+  const int t = threadIdx.x;
+  // the point's terms go out together with the window state
+  const int pf = g.p0 + min(t, max(g.cnt - 1, 0));
+  double sp[3] = {0, 0, 0}, b[3] = {0, 0, 0}, Eu[6] = {0, 0, 0, 0, 0, 0};
+  if (g.cnt > 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * pf + k]; b[k] = d.etb[3 * pf + k]; }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Eu[k] = d.ete[6 * pf + k];
+  }
   const WinState& S = d.st[g.win];
   if (S.done) return;
-  const int t = threadIdx.x;
   if (t < g.cnt) {
     const int p = g.p0 + t;
     const double rad = S.radius;
-    double sp[3], E[6], b[3];
+    double E[6];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * p + k]; b[k] = d.etb[3 * p + k] * sp[k]; }
-    const double* Eu = d.ete + 6 * p;
+    for (int k = 0; k < 3; ++k) b[k] = b[k] * sp[k];
     E[0] = Eu[0] * sp[0] * sp[0]; E[1] = Eu[1] * sp[0] * sp[1]; E[2] = Eu[2] * sp[0] * sp[2];
     E[3] = Eu[3] * sp[1] * sp[1]; E[4] = Eu[4] * sp[1] * sp[2]; E[5] = Eu[5] * sp[2] * sp[2];
     E[0] += fmin(fmax(E[0], o.min_diag), o.max_diag) / rad;
@@ -1505,11 +1516,10 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
   __shared__ double sh[kGB][3], sst[kGB][3], sxn[kGB][3];
   __shared__ double red4[4];
   const PBlk g = d.pblk[blockIdx.x];
-  const WinState& S = d.st[g.win];
-  if (S.done || S.chol_fail) return;
-  const BaWin& W = d.win[g.win];
-  const int cur = S.cur;
   const int t = threadIdx.x;
+  // plan-structure loads of the first chunk and the point's terms go out with the window state
+  const int of = g.o0 + min(t, max(g.no - 1, 0));
+  const int c_f = g.no > 0 ? d.obs_cam[of] : -1, m_f = g.no > 0 ? d.obs_cm[of] : -1;
   double b[3] = {0, 0, 0};
   int po0 = 0, po1 = 0;
   if (t < g.cnt) {
@@ -1518,14 +1528,18 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) b[k] = d.etb[3 * p + k] * d.scale_pt[3 * p + k];
   }
+  const WinState& S = d.st[g.win];
+  if (S.done || S.chol_fail) return;
+  const BaWin& W = d.win[g.win];
+  const int cur = S.cur;
   for (int c0 = 0; c0 < g.no; c0 += kGB) {
     if (c0 + t < g.no) {
       const int e = g.o0 + c0 + t;
-      const int c = d.obs_cam[e];
+      const int c = c0 == 0 ? c_f : d.obs_cam[e];
       if (c >= 0) {
         // W^T y = Jps^T (Jcs y), W = Jcs^T Jps
         const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
-        const int m = d.obs_cm[e];
+        const int m = c0 == 0 ? m_f : d.obs_cm[e];
         double a0 = 0.0, a1 = 0.0;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
