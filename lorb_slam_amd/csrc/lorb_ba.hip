@@ -439,9 +439,9 @@ template <bool SH>
 __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
   const int w = blockIdx.x;
   const WinState* Sp = d.st + w;
-  if (Sp->done) return;
   WinState S = *Sp;
-  const BaWin W = d.win[w];
+  const BaWin W = d.win[w];  // issued with the state, before the done test
+  if (S.done) return;
   const int lane = threadIdx.x;
   if (SH && lane == 0) d.wfail_part[w] = 0.0;  // point-block failures of this iteration (K4)
   if (S.relin) {
@@ -1678,9 +1678,9 @@ template <bool SH>
 __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
   const int w = blockIdx.x;
   const WinState* Sp = d.st + w;
-  if (Sp->done) return;
   WinState S = *Sp;
-  const BaWin W = d.win[w];
+  const BaWin W = d.win[w];  // issued with the state, before the done test
+  if (S.done) return;
   const int lane = threadIdx.x;
   bool valid = !S.chol_fail;
   double mccs = 0.0, ncost = 0.0, sn2 = 0.0;
