@@ -1395,29 +1395,41 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   double* xb = xt + 64 * 18;
   double* zX = xb + 64 * 18;  // 48
   {
-    // Row-major copy of S (coalesced: lane = band column), kStageU rows per batch with all loads
-    // of a batch issued before any store; left triangle of the first bw rows zeroed.
+    // Flat copy of S (row-major n x B1, contiguous) in 16-byte chunks, kStageU chunks per thread
+    // per batch with all loads of a batch issued before any store.  Element k = (i, off) keeps
+    // S's value inside the matrix; the left triangle of the first bw rows is zeroed and rows
+    // n .. n16-1 are an identity pad.  (i, off) of a thread's chunks advance by a fixed step.
 #ifndef LORB_STAGE_U
-#define LORB_STAGE_U 20
+#define LORB_STAGE_U 14
 #endif
     constexpr int kStageU = LORB_STAGE_U;
-    const double* __restrict__ S = d.env + W.env_base;
-    const int off = t & 63, r0 = t >> 6;
-    if (off < B1) {
-      for (int i0 = r0; i0 < n16; i0 += 4 * kStageU) {
-        double v[kStageU];
+    const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
+    const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
+    const int di = (2 * 256) / B1, doff = (2 * 256) % B1;
+    int ci0 = (2 * t) / B1, co0 = (2 * t) % B1;  // (row, column) of this thread's first element
+    for (int j0 = t; j0 < nch; j0 += 256 * kStageU) {
+      double2 v[kStageU];
 #pragma unroll
-        for (int u = 0; u < kStageU; ++u) {
-          const int i = i0 + 4 * u;
-          const bool ok = i < n && i - (bw - off) >= 0;
-          const double sv = S[ok ? i * B1 + off : 0];
-          v[u] = ok ? sv : ((i >= n && off == bw) ? 1.0 : 0.0);
-        }
+      for (int u = 0; u < kStageU; ++u) {
+        const int j = j0 + 256 * u;
+        v[u] = S2[j < nsrc ? j : 0];
+      }
 #pragma unroll
-        for (int u = 0; u < kStageU; ++u) {
-          const int i = i0 + 4 * u;
-          if (i < n16) Ab[i * B1 + off] = v[u];
+      for (int u = 0; u < kStageU; ++u) {
+        const int j = j0 + 256 * u;
+        if (j < nch) {
+          int i = ci0, off = co0;
+          double e[2] = {v[u].x, v[u].y};
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const bool in = i < n && i - (bw - off) >= 0;
+            e[h] = in ? e[h] : ((i >= n && off == bw) ? 1.0 : 0.0);
+            if (++off == B1) { off = 0; ++i; }
+          }
+          reinterpret_cast<double2*>(Ab)[j] = double2{e[0], e[1]};
         }
+        ci0 += di; co0 += doff;
+        if (co0 >= B1) { co0 -= B1; ++ci0; }
       }
     }
     for (int k = t; k < rt; k += 256) zt[k] = d.rhs[W.row_base + k];
