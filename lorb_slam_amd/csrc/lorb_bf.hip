@@ -371,12 +371,25 @@ int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_of
     if (nu > 0) lane_tiles += (nl + lt - 1) / lt;
     max_u = std::max<int64_t>(max_u, nu);
   }
-  // enough workgroups to fill 256 CUs x ~8, but keep >= 128 uniform items per chunk
+  // Uniform-range chunks per lane tile.  With >= 256 lane tiles the chip is filled already: aim
+  // at ~8 workgroups per CU (latency hiding), >= 128 uniform items per chunk (measured best for
+  // C2).  With fewer tiles the scan is VALU-bound on a partly filled chip and workgroups sharing
+  // a CU share its SIMDs: a CU's time is (workgroups on it) x (uniform items per chunk), so pick
+  // the count minimising ceil(tiles x chunks / CUs) x ceil(max_u / chunks) (+ chunks: the merge
+  // reads one key per chunk), >= 32 uniform items per chunk, at most 64 chunks.
   int n_chunks = 1;
-  if (lane_tiles > 0) {
+  constexpr int64_t kCUs = 256;  // MI355X: 8 XCDs x 32 CUs
+  if (lane_tiles >= kCUs) {
     const int64_t want = (2048 + lane_tiles - 1) / lane_tiles;
     const int64_t cap = std::max<int64_t>(1, max_u / 128);
     n_chunks = (int)std::max<int64_t>(1, std::min<int64_t>(want, std::min<int64_t>(cap, 64)));
+  } else if (lane_tiles > 0) {
+    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(64, max_u / 32));
+    int64_t best = -1;
+    for (int64_t nc = 1; nc <= cap; ++nc) {
+      const int64_t cost = (lane_tiles * nc + kCUs - 1) / kCUs * ((max_u + nc - 1) / nc) + nc;
+      if (best < 0 || cost < best) { best = cost; n_chunks = (int)nc; }
+    }
   }
   tiles.clear();
   for (int p = 0; p < np; p++) {
