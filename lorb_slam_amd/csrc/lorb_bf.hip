@@ -141,8 +141,10 @@ template <bool TOP2>
 __global__ __launch_bounds__(256) void k_bf_merge(const uint32_t* __restrict__ k1p,
                                                   const uint32_t* __restrict__ k2p, int n,
                                                   int n_chunks, uint32_t* __restrict__ k1o,
-                                                  uint32_t* __restrict__ k2o) {
+                                                  uint32_t* __restrict__ k2o,
+                                                  unsigned long long* __restrict__ kinit, int n_init) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_init) kinit[i] = ~0ull;  // crossCheck query keys, folded in instead of a fill launch
   if (i >= n) return;
   uint32_t k1 = kSentinel, k2 = kSentinel;
   for (int c = 0; c < n_chunks; ++c) {
@@ -415,9 +417,13 @@ int build_tiles(lorb_ctx* ctx, int np, const int32_t* l_off, const int32_t* u_of
 }
 
 // scan + merge; final keys land in k1/k2 (n_lanes entries)
+// kinit (n_init entries) is set to all-ones by the merge when one runs (*kinit_done = true);
+// otherwise the caller initialises it.
 template <bool TOP2>
 int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, const uint8_t* d_uni,
-         const int32_t* u_off, uint32_t** k1_final, uint32_t** k2_final, const int32_t* u_base = nullptr) {
+         const int32_t* u_off, uint32_t** k1_final, uint32_t** k2_final, const int32_t* u_base = nullptr,
+         unsigned long long* kinit = nullptr, int n_init = 0, bool* kinit_done = nullptr) {
+  if (kinit_done) *kinit_done = false;
   std::vector<BfTile> tiles;
   int n_chunks = 1;
   static const int qpl = [] {
@@ -451,9 +457,11 @@ int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, con
   if (n_chunks > 1 && nl > 0) {
     LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT4, (size_t)nl, &m1));
     LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT5, (size_t)nl, &m2));
-    hipLaunchKernelGGL(k_bf_merge<TOP2>, dim3(lorb::ceil_div(nl, 256)), dim3(256), 0, ctx->stream,
-                       k1, k2, nl, n_chunks, m1, m2);
+    const int ni = kinit ? n_init : 0;
+    hipLaunchKernelGGL(k_bf_merge<TOP2>, dim3(lorb::ceil_div(std::max(nl, ni), 256)), dim3(256), 0, ctx->stream,
+                       k1, k2, nl, n_chunks, m1, m2, kinit, ni);
     LORB_CHECK_LAUNCH(ctx);
+    if (kinit_done) *kinit_done = ni > 0;
     *k1_final = m1;
     *k2_final = m2;
   } else {
@@ -533,13 +541,16 @@ int lorb_bf_match_dev(lorb_ctx* ctx, int32_t np, const uint8_t* d_q, const int32
   offs.insert(offs.end(), t_off, t_off + np + 1);
   LORB_TRY(lorb::upload_t(ctx, S_BF_OFF, offs.data(), offs.size(), &d_off));
   LORB_TRY(lorb::scratch_t(ctx, S_BF_QKEY, (size_t)std::max(nq, 1), &qkey));
-  if (nq > 0) LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, ctx->stream));
+  bool keyed = false;
   if (nt > 0 && nq > 0) {
     // reverse pass: lanes = trains, uniform = queries  -> nearest query per train
-    LORB_TRY(scan<false>(ctx, np, d_t, t_off, d_q, q_off, &k1, &k2));
+    LORB_TRY(scan<false>(ctx, np, d_t, t_off, d_q, q_off, &k1, &k2, nullptr, qkey, nq, &keyed));
+    if (!keyed) LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, ctx->stream));
     hipLaunchKernelGGL(k_cc_scatter, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, k1,
                        nt, d_off, d_off + np + 1, np, (const int32_t*)nullptr, qkey);
     LORB_CHECK_LAUNCH(ctx);
+  } else if (nq > 0) {
+    LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, ctx->stream));
   }
   hipLaunchKernelGGL(k_cc_finalize<0>, dim3(np), dim3(256), 0, ctx->stream, qkey, d_off,
                      d_off + np + 1, d_cc_train, d_cc_dist, d_match_train, d_n_matches, (double*)nullptr, np);
