@@ -409,6 +409,32 @@ __global__ __launch_bounds__(256) void k_ba_camera(BaDev d) {
   }
 }
 
+// Lane-strided partial sums over a window's point groups (b = lane, lane + 64, ... in that order,
+// the per-lane order of a plain loop) with the loads of kPU groups issued before any is added: the
+// partials come from the previous kernel (another XCD's L2), so a load-add loop pays one memory
+// round trip per step.  F0..F2 pick the fields; M1: field 1 is a max.
+template <int F0, int F1, int F2, bool M1>
+__device__ __forceinline__ void group_partials(const double* __restrict__ part, int base, int n, int lane,
+                                               double& a, double& b, double& c) {
+  constexpr int kPU = 8;
+  for (int b0 = lane; b0 < n; b0 += 64 * kPU) {
+    double v0[kPU], v1[kPU], v2[kPU];
+#pragma unroll
+    for (int u = 0; u < kPU; ++u) {
+      const int g = b0 + 64 * u;
+      const double* P = part + 8 * (base + (g < n ? g : 0));
+      v0[u] = P[F0]; v1[u] = P[F1]; v2[u] = P[F2];
+    }
+#pragma unroll
+    for (int u = 0; u < kPU; ++u)
+      if (b0 + 64 * u < n) {
+        a += v0[u];
+        b = M1 ? fmax(b, v1[u]) : b + v1[u];
+        c += v2[u];
+      }
+  }
+}
+
 // K2b (sharded plans): per-window reduction of the point-group partials of one phase into the
 // exchange buffers (PH 0: cost, point |x|^2 (sum) and point gradient max; PH 1: model cost
 // change, candidate cost, point |step|^2), fixed lane order + butterfly.
@@ -419,11 +445,8 @@ __global__ __launch_bounds__(64) void k_ba_win_reduce(BaDev d) {
   const BaWin& W = d.win[w];
   const int lane = threadIdx.x;
   double a = 0.0, b = 0.0, c = 0.0;
-  for (int g = lane; g < W.n_pblk; g += 64) {
-    const double* P = d.part + 8 * (W.pblk_base + g);
-    if (PH == 0) { a += P[0]; b += P[2]; c = fmax(c, P[1]); }
-    else { a += P[3]; b += P[4]; c += P[5]; }
-  }
+  if (PH == 0) group_partials<0, 1, 2, true>(d.part, W.pblk_base, W.n_pblk, lane, a, c, b);
+  else group_partials<3, 4, 5, false>(d.part, W.pblk_base, W.n_pblk, lane, a, b, c);
   a = wave_sum(a); b = wave_sum(b);
   c = PH == 0 ? wave_max(c) : wave_sum(c);
   if (lane == 0) {
@@ -447,12 +470,7 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
   if (S.relin) {
     // fixed lane assignment + fixed butterfly => deterministic
     double cost = 0.0, gm = 0.0, xn2 = 0.0;
-    if (!SH) {
-      for (int b = lane; b < W.n_pblk; b += 64) {
-        const double* P = d.part + 8 * (W.pblk_base + b);
-        cost += P[0]; gm = fmax(gm, P[1]); xn2 += P[2];
-      }
-    }
+    if (!SH) group_partials<0, 1, 2, true>(d.part, W.pblk_base, W.n_pblk, lane, cost, gm, xn2);
     const int cur = S.cur;
     for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64) {
       if (S.iter == 0) {
@@ -1697,12 +1715,7 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
   bool valid = !S.chol_fail;
   double mccs = 0.0, ncost = 0.0, sn2 = 0.0;
   if (valid) {
-    if (!SH) {
-      for (int b = lane; b < W.n_pblk; b += 64) {
-        const double* P = d.part + 8 * (W.pblk_base + b);
-        mccs += P[3]; ncost += P[4]; sn2 += P[5];
-      }
-    }
+    if (!SH) group_partials<3, 4, 5, false>(d.part, W.pblk_base, W.n_pblk, lane, mccs, ncost, sn2);
     const int cur = S.cur;
     for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64) {
       const bool active = d.cam_active[c];
