@@ -623,10 +623,16 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o, int n_bp) {
 #pragma unroll
   for (int k = 0; k < 36; ++k) acc[k] = 0.0;
   const int end = bp.off + bp.cnt;
-  for (int q = bp.off + t; q < end; q += 512) {
-    const int2 p0 = d.pairs[q];  // camera-major slots (obs in camera ch, obs in camera cl) of one point
+  // camera-major slots (obs in camera ch, obs in camera cl) of one point; the next step's pair
+  // indices are read while this step's tiles load (same pairs, same order)
+  int q = bp.off + t;
+  int2 p0n = make_int2(0, 0), p1n = make_int2(0, 0);
+  if (q < end) { p0n = d.pairs[q]; p1n = d.pairs[q + 256 < end ? q + 256 : q]; }
+  for (; q < end; q += 512) {
+    const int2 p0 = p0n, p1 = p1n;
     const bool two = q + 256 < end;
-    const int2 p1 = d.pairs[two ? q + 256 : q];
+    const int qn = q + 512;
+    if (qn < end) { p0n = d.pairs[qn]; p1n = d.pairs[qn + 256 < end ? qn + 256 : qn]; }
     schur_pair(d, p0, acc);
     if (two) schur_pair(d, p1, acc);
   }
