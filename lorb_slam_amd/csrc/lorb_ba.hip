@@ -517,6 +517,15 @@ __global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) Eu[k] = d.ete[6 * pf + k];
   }
+  // ... and so do the first chunk's observation terms (used after the point phase)
+  const int ef = g.o0 + min(t, max(g.no - 1, 0));
+  int m_f = -1, pt_f = 0;
+  double Jp_f[6] = {0, 0, 0, 0, 0, 0};
+  if (g.no > 0) {
+    m_f = d.obs_cm[ef]; pt_f = d.obs_pt[ef];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Jp_f[k] = d.obs_Jp[6 * ef + k];
+  }
   const WinState& S = d.st[g.win];
   if (S.done) return;
   if (t < g.cnt) {
@@ -545,14 +554,15 @@ __global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
   __syncthreads();
   for (int c0 = t; c0 < g.no; c0 += kGB) {
     const int e = g.o0 + c0;
-    const int m = d.obs_cm[e];
+    const bool first = c0 == t;
+    const int m = first ? m_f : d.obs_cm[e];
     if (m < 0) continue;
-    const int lp = d.obs_pt[e] - g.p0;
+    const int lp = (first ? pt_f : d.obs_pt[e]) - g.p0;
     const double* Ei = sEi[lp];
     const double* b = sb[lp];
     double Jps[6], Q[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) Jps[k] = d.obs_Jp[6 * e + k] * ssp[lp][k % 3];
+    for (int k = 0; k < 6; ++k) Jps[k] = (first ? Jp_f[k] : d.obs_Jp[6 * e + k]) * ssp[lp][k % 3];
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
