@@ -242,27 +242,22 @@ __global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n
 // deterministic point-group reductions (fixed butterfly per wave, fixed wave order) over the
 // kGB / 64 waves of a point-group workgroup
 constexpr int kGW = kGB / 64;
-__device__ __forceinline__ double block_sum256(double v, double* red4) {
-  v = wave_sum(v);
-  if (kGW == 1) return v;
+static_assert(kGW >= 1 && kGW <= 4, "point groups of 64..256 observations (red3 holds 4 waves)");
+// three block reductions behind one LDS exchange (M1: the second is a max): per-wave butterfly,
+// then the waves' values in wave order
+template <bool M1>
+__device__ __forceinline__ void block_red3(double& a, double& b, double& c, double (*red)[4]) {
+  a = wave_sum(a); b = M1 ? wave_max(b) : wave_sum(b); c = wave_sum(c);
+  if (kGW == 1) return;
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    red[0][w] = a; red[1][w] = b; red[2][w] = c;
+  }
   __syncthreads();
-  double s = red4[0];
+  a = red[0][0]; b = red[1][0]; c = red[2][0];
 #pragma unroll
-  for (int k = 1; k < kGW; ++k) s += red4[k];
-  return s;
-}
-__device__ __forceinline__ double block_max256(double v, double* red4) {
-  v = wave_max(v);
-  if (kGW == 1) return v;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double s = red4[0];
-#pragma unroll
-  for (int k = 1; k < kGW; ++k) s = fmax(s, red4[k]);
-  return s;
+  for (int k = 1; k < kGW; ++k) { a += red[0][k]; b = M1 ? fmax(b, red[1][k]) : b + red[1][k]; c += red[2][k]; }
 }
 
 // K1: linearisation of a point group (windows that (re)linearise this iteration): per
@@ -270,7 +265,7 @@ __device__ __forceinline__ double block_max256(double v, double* red4) {
 // (iteration 0), gradient-max / point-norm / cost partials.
 __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
   __shared__ double sh[kGB][9];
-  __shared__ double red4[4];
+  __shared__ double red3[3][4];
   const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x;
   // plan-structure loads of the first chunk go out together with the window state
@@ -353,9 +348,7 @@ __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
       }
     }
   }
-  cost = block_sum256(cost, red4);
-  gm = block_max256(gm, red4);
-  xn2 = block_sum256(xn2, red4);
+  block_red3<true>(cost, gm, xn2, red3);
   if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[0] = cost; P[1] = gm; P[2] = xn2; }
 }
 
@@ -1560,7 +1553,7 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
 // per observation (observation phase).
 __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
   __shared__ double sh[kGB][3], sst[kGB][3], sxn[kGB][3];
-  __shared__ double red4[4];
+  __shared__ double red3[3][4];
   const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x;
   // plan-structure loads of the first chunk and the point's terms go out with the window state
@@ -1666,9 +1659,7 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
     mcc += m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0);
     ncost += 0.5 * (rn[0] * rn[0] + rn[1] * rn[1]);
   }
-  mcc = block_sum256(mcc, red4);
-  ncost = block_sum256(ncost, red4);
-  sn2 = block_sum256(sn2, red4);
+  block_red3<false>(mcc, ncost, sn2, red3);
   if (t == 0) {
     double* P = d.part + 8 * blockIdx.x;
     P[3] = mcc; P[4] = ncost; P[5] = sn2;
