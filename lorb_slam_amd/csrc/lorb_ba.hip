@@ -1721,6 +1721,7 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
   const int lane = threadIdx.x;
   bool valid = !S.chol_fail;
   double mccs = 0.0, ncost = 0.0, sn2 = 0.0;
+  double xc[6] = {0, 0, 0, 0, 0, 0};  // candidate pose of camera pose_base + lane (kept for its jet)
   if (valid) {
     if (!SH) group_partials<3, 4, 5, false>(d.part, W.pblk_base, W.n_pblk, lane, mccs, ncost, sn2);
     const int cur = S.cur;
@@ -1730,6 +1731,7 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
         const double x = d.x_pose[cur][6 * c + k];
         const double xn = d.x_pose[cur ^ 1][6 * c + k];  // written by k_ba_chol
         if (active) sn2 += (x - xn) * (x - xn);
+        if (c == W.pose_base + lane) xc[k] = xn;
       }
     }
     mccs = wave_sum(mccs); ncost = wave_sum(ncost); sn2 = wave_sum(sn2);
@@ -1739,9 +1741,12 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
   if (lane == 0) s_accept = lm_decide(d, o, w, S, valid, mccs, ncost, sn2);
   __syncthreads();
   // accepted: the candidate is the new linearisation point -> its rotation states for k_ba_lin
-  if (s_accept)
-    for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64)
+  // (an accepted step is a valid one, so the first 64 candidates are already in registers)
+  if (s_accept) {
+    if (lane < W.n_poses) d.rot_lin[W.pose_base + lane] = lorb::rot_jet(xc);
+    for (int c = W.pose_base + lane + 64; c < W.pose_base + W.n_poses; c += 64)
       d.rot_lin[c] = lorb::rot_jet(d.x_pose[S.cur ^ 1] + 6 * c);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
