@@ -1,7 +1,14 @@
 #!/usr/bin/env python3
 """bench.py -- LORB_SLAM matcher + local-BA hot path on MI355X (one process per GPU).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2] [--windows W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|shared|rehearse]
+
+Launch.  The driver starts N>1 ranks itself (`torch.distributed.run ... bench.py --gpus N`).  When
+`--gpus N > 1` is given without WORLD_SIZE in the environment, this script starts the N ranks
+itself (a `torch.distributed.run` child process, before anything here touches a GPU) and exits
+with its code.  A rank refuses to run (exit 2) when WORLD_SIZE != --gpus or when fewer devices
+than ranks are visible: ranks never share a GPU silently.  `n_gpus` in the JSON line is the rank
+count of the RCCL communicator the ranks build (ncclCommCount), not an argument echo.
 
 Default workload (c4, BASELINE config "full local_mapping step -- match + triangulate + BA on a
 50-KF / 10k-point sliding window"): per GPU and per step, for each of `--windows` independent
@@ -11,19 +18,20 @@ windows (default 1, i.e. C4 at N=1 and C5 -- one window per GPU -- at N=8):
   2. stereo unprojection of the new keyframe's keypoints (Frame::UnprojectStereo),
   3. 10 Levenberg-Marquardt iterations of BA::LocalPoseOptimization on the window
      (50 optimised KFs + 5 fixed, 10,000 points, 77,000 observations), tolerances 0.
-The window's observation structure (CSR, Schur block-pair lists) is built once per window
-outside the timed region (reported as plan_build_ms).  `value` = LM iterations/s over all GPUs;
-`matches_per_sec` = keyframe descriptors resolved per second in the same steps.
+`value` = LM iterations/s over all GPUs.  The same run also times the BASELINE C2 matcher
+config (batched 2000x2000 top-2 + ratio test) and reports it as the `c2` sub-record, so both
+halves of the metric ("ORB matches/sec + local-BA iterations/sec") come from one driver run.
 
 Inputs are synthetic (lorb_slam_amd.synth, seeded per rank) and resident in HBM before the
-timed region.  Multi-GPU: launched by torch.distributed.run; each rank owns its own windows
-(weak scaling, no data-path collective); torch.distributed (gloo, CPU) only provides the barrier
-and the max-over-ranks of the timing.
+timed region.  torch.distributed (gloo, CPU) provides the barrier, the max-over-ranks of the
+timing and the RCCL unique id; the data-path collectives (shared workload) are RCCL.
 """
 import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,10 +39,6 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-from lorb_slam_amd import _abi as A  # noqa: E402
-from lorb_slam_amd import synth  # noqa: E402
-from lorb_slam_amd.runtime import BAPlan, Context, device_count, lib  # noqa: E402
 
 CLOCK = 2.4e9
 INT32_VALU_PEAK = 256 * 4 * 32 * CLOCK      # lane-ops/s: 256 CU x 4 SIMD32 (MI355X_MICROARCH)
@@ -46,8 +50,31 @@ OPS_PER_PAIR = 16                            # 8 x v_xor_b32 + 8 x v_bcnt_u32_b3
 K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_2s"}
 # rocprofv3 short names (tools/pmc_traffic.py) of the same kernels, for the PMC traffic lookup
 K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_2s"}
-TRAFFIC = os.path.join(ROOT, "profiles", "r01", "traffic.json")
+# committed PMC summaries, newest first; each is keyed by workload (tools/pmc_traffic.py)
+TRAFFIC = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r02", "r01")]
 METRIC = "ORB matches/sec + local-BA iterations/sec (50 KF, 10k pts) at 1/2/4/8 MI355X"
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """Start n ranks as a torch.distributed.run child (no GPU has been touched in this process)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def refuse(msg):
+    print(f"bench.py: refusing to run: {msg}", file=sys.stderr, flush=True)
+    sys.exit(2)
 
 
 class Dist:
@@ -87,7 +114,55 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+def host_cpu():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return model, avail
+
+
+def cpu_threads():
+    """host threads for the nproc leg: the cores this process may use, capped at the GPU box's
+    per-GPU CPU share (OMP_NUM_THREADS is 16 there)"""
+    _, avail = host_cpu()
+    cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(avail, cap, 16))
+
+
+def run_parallel(fn, threads, budget_s):
+    """fn() repeatedly on `threads` Python threads (the oracle's C calls release the GIL) for
+    about budget_s; returns (completed calls, elapsed s)."""
+    import threading
+    stop = time.perf_counter() + budget_s
+    counts = [0] * threads
+
+    def worker(i):
+        while True:
+            fn()
+            counts[i] += 1
+            if time.perf_counter() >= stop:
+                break
+    t0 = time.perf_counter()
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return sum(counts), time.perf_counter() - t0
+
+
 def kernel_times(ctx, ids):
+    from lorb_slam_amd.runtime import lib
     L = lib()
     out = {}
     for k in ids:
@@ -99,6 +174,9 @@ def kernel_times(ctx, ids):
 
 # ------------------------------------------------------------------------------------------
 def workload_c4(ctx, args, rank):
+    from lorb_slam_amd import _abi as A
+    from lorb_slam_amd import synth
+    from lorb_slam_amd.runtime import BAPlan, lib
     W = args.windows
     steps = [synth.local_mapping_step(seed=4 + 1009 * rank + 17 * i) for i in range(W)]
     wins = [s["window"] for s in steps]
@@ -140,78 +218,69 @@ def workload_c4(ctx, args, rank):
         return {"n_matches": [int(v) for v in n], "ba_final_cost": [s["final_cost"] for s in summ],
                 "ba_iterations": [s["iterations"] for s in summ]}
 
-    # algorithmic work per step: matcher pairs, BA FP64 flops per LM iteration
-    pairs = float(W) * nq * nt
     n_obs = sum(len(w["obs_point"]) for w in wins)
     n_pts = sum(len(w["point_init"]) for w in wins)
     F = len(wins[0]["pose_init"])
-    kp = np.bincount(wins[0]["obs_point"][wins[0]["obs_frame"] >= 0])
-    pt_flops = float(np.sum(60 + 108 * kp + 108 * kp * (kp + 1)))
-    it_flops = W * (420.0 * n_obs / W + pt_flops + (6 * F) ** 3 / 3 + 4 * (6 * F) ** 2)
-    # per-launch algorithmic work of each BA kernel (all windows of the step); DESIGN.md §Roofline
-    pair_cnt = 0
-    for w in wins:
-        m = w["obs_frame"] >= 0
-        k = np.bincount(w["obs_point"][m], minlength=len(w["point_init"]))
-        pair_cnt += int(np.sum(k * (k + 1) // 2))
     opt_obs = sum(int((w["obs_frame"] >= 0).sum()) for w in wins)
     bw = 6 * 8 - 1
     kspec = {
-        # Schur block accumulation: 216 flop per (obs_h, obs_l) pair; compulsory bytes = the W and Y
-        # tiles (2 x 18 doubles per optimised observation) read once + S written once
+        # Schur block accumulation: compulsory bytes = the W and Y tiles (2 x 18 doubles per
+        # optimised observation) read once + the S band written once
         2: ("hbm", opt_obs * 36 * 8.0 + W * (6 * F) * (bw + 1) * 8.0, "GB/s"),
         # linearisation: residual + 2x3 + 2x6 Jacobian per observation: reads pose/point/uv, writes 20 doubles
         3: ("hbm", n_obs * (20 * 8.0 + 16 + 8) + 0.0, "GB/s"),
         # banded Cholesky + 2 triangular solves: n*bw^2 + 4*n*bw flops
         4: ("fp64", W * ((6 * F) * bw * bw + 4.0 * (6 * F) * bw), "TFLOP/s"),
     }
-    return dict(step=step, check=check, ba_iters=10.0 * W, matches=float(W * nq), pairs=pairs,
-                it_flops=it_flops, plan_ms=plan_ms, cleanup=plan.close, kspec=kspec,
+    return dict(step=step, check=check, ba_iters=10.0 * W, matches=float(W * nq), pairs=float(W) * nq * nt,
+                plan_ms=plan_ms, cleanup=plan.close, kspec=kspec, traffic_key="c4",
                 config={"workload": "c4_local_mapping_step", "windows_per_gpu": W, "kf": F, "fixed_kf": 5,
                         "points": n_pts // W, "observations": n_obs // W, "lm_iterations": 10,
                         "new_kf_keypoints": nq, "match": f"{nq}x{nt} bf crossCheck"},
-                cpu=lambda: cpu_baseline_c4(steps[0]))
+                cpu=lambda: cpu_baseline_c4(steps[0], args.cpu_budget))
 
 
-def cpu_baseline_c4(st, budget_s=12.0):
-    """Oracle (C restatement of the reference path, TEST INFRASTRUCTURE) timed on host cores:
-    the same step on a bounded sample (1 window: match + unproject + 10 LM iterations)."""
+def cpu_baseline_c4(st, budget_s):
+    """Oracle (C restatement of the reference path, TEST INFRASTRUCTURE) timed on host cores on a
+    bounded sample of the same step (1 window: match + unproject + 10 LM iterations): at 1 thread
+    (Ceres' default num_threads=1) and at the host's thread count (independent windows in flight)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
+    from lorb_slam_amd import _abi as A
+    from lorb_slam_amd import synth
     fp = synth.frame_params()
     opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
-    n, t_match, t_ba = 0, 0.0, 0.0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or n == 0:
-        a = time.perf_counter()
+
+    def one():
         O.bf_match(st["kf_desc"], st["mp_desc"])
         O.unproject_stereo(fp, st["kf_Tcw"], st["kf_x"], st["kf_y"], st["kf_depth"])
-        b = time.perf_counter()
         O.ba_local([st["window"]], opt)
-        c = time.perf_counter()
-        t_match += b - a; t_ba += c - b; n += 1
-    dt = time.perf_counter() - t0
-    return {"value": 10.0 * n / dt, "unit": "BA iterations/s", "cores": 1, "kind": "port",
-            "matches_per_sec": 2000.0 * n / dt, "stage_s": {"match+unproject": t_match / n, "ba_10_its": t_ba / n},
-            "sample": f"{n} x C4 local-mapping step (1 window), oracle C restatement gcc -O2, 1 thread "
-                      f"(Ceres default num_threads=1), {dt:.1f}s"}
+    n1, d1 = run_parallel(one, 1, budget_s)
+    nt = cpu_threads()
+    nn, dn = run_parallel(one, nt, budget_s) if nt > 1 else (n1, d1)
+    model, avail = host_cpu()
+    return {"value": 10.0 * n1 / d1, "unit": "BA iterations/s", "cores": 1, "kind": "port",
+            "matches_per_sec": 2000.0 * n1 / d1,
+            "sample": f"{n1} x C4 local-mapping step (1 window: 2000x10000 crossCheck + unproject + 10 LM its), "
+                      f"oracle C restatement gcc -O2, 1 thread (Ceres default num_threads=1), {d1:.1f}s",
+            "nproc": {"value": 10.0 * nn / dn, "cores": nt, "matches_per_sec": 2000.0 * nn / dn,
+                      "sample": f"{nn} steps on {nt} threads (independent windows), {dn:.1f}s"},
+            "host_cpu": model, "host_cpus_available": avail}
 
 
-def workload_shared(ctx, args, rank, D):
+def workload_shared(ctx, args, rank, D, comm):
     """BASELINE C5 shared-window variant: ONE 50-KF window with 80,000 points
     (~600,000 observations) point-partitioned over the N ranks, 10 LM iterations per step with
     the three RCCL all-reduces per iteration; plus the new keyframe's 2,000 descriptors matched
     (crossCheck) against the window's 80,000 map-point descriptors with the query rows split over
     the ranks.  Strong scaling: total work is fixed as N grows."""
-    from lorb_slam_amd import shard
-    from lorb_slam_amd.runtime import Comm, unique_id
+    from lorb_slam_amd import _abi as A
+    from lorb_slam_amd import shard, synth
+    from lorb_slam_amd.runtime import BAPlan, lib
     world = D.world
     win = synth.ba_window(seed=11, n_kf=50, n_pts=args.shared_points, n_fixed=5, fixed_obs_per_kf=400)
     sh = shard.shard_window(win, rank, world)
-    uid = unique_id() if rank == 0 else None
-    uid = D.broadcast_bytes(uid)
-    comm = Comm.rccl(ctx, world, rank, uid)
     t0 = time.perf_counter()
     plan = BAPlan(ctx, [sh], comm=comm)
     plan_ms = (time.perf_counter() - t0) * 1e3
@@ -242,14 +311,7 @@ def workload_shared(ctx, args, rank, D):
         return {"n_matches": int(nm.numpy()[0]), "ba_final_cost": summ[0]["final_cost"],
                 "ba_iterations": summ[0]["iterations"]}
 
-    def cleanup():
-        plan.close()
-        comm.close()
-
     n_obs = len(win["obs_point"])
-    kp = np.bincount(sh["obs_point"][sh["obs_frame"] >= 0])
-    pt_flops = float(np.sum(60 + 108 * kp + 108 * kp * (kp + 1)))
-    pair_cnt = float(np.sum(kp * (kp + 1) // 2))
     opt_obs = int((sh["obs_frame"] >= 0).sum())
     bw = 6 * 8 - 1
     kspec = {
@@ -257,10 +319,10 @@ def workload_shared(ctx, args, rank, D):
         3: ("hbm", len(sh["obs_point"]) * (20 * 8.0 + 16 + 8), "GB/s"),
         4: ("fp64", (6 * 50) * bw * bw + 4.0 * (6 * 50) * bw, "TFLOP/s"),
     }
-    del pair_cnt, pt_flops
     # whole-job units: the shared window's iterations / matches are counted once (rank 0 only)
     return dict(step=step, check=check, ba_iters=10.0 if rank == 0 else 0.0, matches=float(nq) if rank == 0 else 0.0,
-                pairs=float(b - a) * nt, it_flops=0.0, plan_ms=plan_ms, cleanup=cleanup, kspec=kspec,
+                pairs=float(b - a) * nt, plan_ms=plan_ms, cleanup=plan.close, kspec=kspec,
+                traffic_key=f"shared_w{world}",
                 config={"workload": "c5_shared_window", "kf": 50, "fixed_kf": 5, "points": len(win["point_init"]),
                         "observations": n_obs, "lm_iterations": 10, "new_kf_keypoints": nq,
                         "match": f"{nq}x{nt} bf crossCheck, query rows sharded", "points_this_rank": len(sh["point_init"])},
@@ -269,12 +331,17 @@ def workload_shared(ctx, args, rank, D):
 
 def workload_c2(ctx, args, rank):
     """BASELINE config 1: brute-force Hamming 2000x2000 random 256-bit + ratio test, batched
-    over `pairs` independent frame pairs per GPU."""
+    over `pairs` independent frame pairs per GPU (each pair is a full 2000x2000 problem; the
+    inputs cycle through `unique` generated pairs to keep input generation short)."""
+    from lorb_slam_amd import _abi as A
+    from lorb_slam_amd import synth
+    from lorb_slam_amd.runtime import lib
     B = args.pairs
-    qs, ts, ls = [], [], []
-    for p in range(B):
-        q, t, lev = synth.bf_problem(seed=1000 * rank + p, nq=2000, nt=2000, n_planted=1000, random_levels=True)
-        qs.append(q); ts.append(t); ls.append(lev)
+    U = min(B, 64)
+    gen = [synth.bf_problem(seed=1000 * rank + p, nq=2000, nt=2000, n_planted=1000, random_levels=True) for p in range(U)]
+    qs = [gen[p % U][0] for p in range(B)]
+    ts = [gen[p % U][1] for p in range(B)]
+    ls = [gen[p % U][2] for p in range(B)]
     q_off = np.arange(B + 1, dtype=np.int32) * 2000
     t_off = np.arange(B + 1, dtype=np.int32) * 2000
     dq, dt, dl = ctx.to_device(np.concatenate(qs)), ctx.to_device(np.concatenate(ts)), ctx.to_device(np.concatenate(ls))
@@ -291,32 +358,66 @@ def workload_c2(ctx, args, rank):
     def cpu():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
-        threads = max(1, min(16, os.cpu_count() or 1))
-        n, t0 = 0, time.perf_counter()
-        while time.perf_counter() - t0 < 10.0 or n == 0:
-            O.bf_top2(qs[0], ts[0], ls[0], threads=threads)
-            n += 1
-        d = time.perf_counter() - t0
-        return {"value": n * 2000 / d, "unit": "matches/s", "cores": threads, "kind": "port",
-                "sample": f"{n} x (2000x2000 bf top-2 + ratio test), oracle C -O2, {threads} threads, {d:.1f}s"}
+        budget = max(2.0, args.cpu_budget / 2)
+        n1, d1 = run_parallel(lambda: O.bf_top2(qs[0], ts[0], ls[0]), 1, budget)
+        nt = cpu_threads()
+        nn, dn = run_parallel(lambda: O.bf_top2(qs[0], ts[0], ls[0]), nt, budget) if nt > 1 else (n1, d1)
+        model, avail = host_cpu()
+        return {"value": n1 * 2000 / d1, "unit": "matches/s", "cores": 1, "kind": "port",
+                "sample": f"{n1} x (2000x2000 bf top-2 + ratio test), oracle C -O2, 1 thread, {d1:.1f}s",
+                "nproc": {"value": nn * 2000 / dn, "cores": nt,
+                          "sample": f"{nn} problems on {nt} threads, {dn:.1f}s"},
+                "host_cpu": model, "host_cpus_available": avail}
+
+    def cleanup():
+        for a in (dq, dt, dl, acc, *outs):
+            a.free()
 
     return dict(step=step, check=lambda: {"accepted": int(acc.numpy().sum())}, ba_iters=0.0, matches=float(nq),
-                pairs=float(nq) * 2000, it_flops=0.0, plan_ms=0.0, cleanup=lambda: None, kspec={},
-                config={"workload": "c2_bf_top2_ratio", "pairs_per_gpu": B, "nq": 2000, "nt": 2000}, cpu=cpu)
+                pairs=float(nq) * 2000, plan_ms=0.0, cleanup=cleanup, kspec={}, traffic_key="c2",
+                config={"workload": "c2_bf_top2_ratio", "pairs_per_gpu": B, "unique_pairs": U, "nq": 2000, "nt": 2000},
+                cpu=cpu)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes (FETCH_SIZE and
-    WRITE_SIZE collected in separate runs, gfx950 FETCH_SIZE x2 correction; tools/pmc_traffic.py).
-    PMC counters cannot be read live from inside the timed process, so this is the profiled
-    value of the same command; null when no summary is committed."""
-    try:
-        with open(TRAFFIC) as f:
-            tab = json.load(f)
-    except (OSError, ValueError):
-        return None
-    ent = tab.get("kernels", {}).get(kernel)
-    return None if ent is None else ent.get("hbm_bytes_per_launch")
+class _NullCtx:
+    def sync(self):
+        pass
+
+    def close(self):
+        pass
+
+
+def workload_rehearse(ctx, args, rank):
+    """Launcher / gloo rehearsal without a GPU: a fixed CPU busy-step per rank.  Exercises the
+    rank spawn, barrier, max-over-ranks timing and the single JSON line; its value measures
+    nothing about the hot path (the line says so)."""
+    a = np.random.default_rng(rank).standard_normal((128, 128))
+
+    def step():
+        for _ in range(4):
+            a @ a
+    return dict(step=step, check=lambda: {}, ba_iters=1.0, matches=0.0, pairs=0.0, plan_ms=0.0,
+                cleanup=lambda: None, kspec={}, traffic_key=None,
+                config={"workload": "rehearsal_cpu_no_gpu"}, cpu=None)
+
+
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` in `workload` from the committed rocprofv3 PMC passes
+    (FETCH_SIZE and WRITE_SIZE collected in separate runs, gfx950 FETCH_SIZE x2 correction;
+    tools/pmc_traffic.py).  PMC counters cannot be read live from inside the timed process, so
+    this is the profiled value of the same command; null when no summary for this workload
+    and kernel is committed."""
+    for path in TRAFFIC:
+        try:
+            with open(path) as f:
+                tab = json.load(f)
+        except (OSError, ValueError):
+            continue
+        wls = tab.get("workloads") or {"c4": tab}  # r01 files hold the c4 workload only
+        ent = wls.get(workload, {}).get("kernels", {}).get(kernel)
+        if ent is not None and ent.get("hbm_bytes_per_launch") is not None:
+            return {"hbm_bytes_per_launch": ent["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
+    return None
 
 
 def roofline_entry(kt, wl, steps):
@@ -338,10 +439,60 @@ def roofline_entry(kt, wl, steps):
     achieved = amount / avg_s
     scale = 1e9 if unit == "GB/s" else 1e12
     name = K_NAMES.get(k, str(k))
+    tr = pmc_traffic(wl["traffic_key"], K_PROF.get(k, name)) if wl.get("traffic_key") else None
     return {"bound": bound, "achieved": achieved / scale, "peak": peak / scale, "unit": unit,
-            "frac": achieved / peak, "traffic": pmc_traffic(K_PROF.get(k, name)), "kernel": name,
+            "frac": achieved / peak, "traffic": tr["hbm_bytes_per_launch"] if tr else None,
+            "traffic_source": tr["source"] if tr else None, "kernel": name,
             "algorithmic_per_launch": amount, "avg_kernel_us": avg_s * 1e6, "launches_per_step": per_step,
             "all_kernels_ms_per_step": {K_NAMES.get(kk, str(kk)): v[0] / steps for kk, v in kt.items()}}
+
+
+def timed(ctx, D, wl, steps, warmup):
+    """W untimed steps, then exactly K steps bracketed by barrier + device sync; max over ranks."""
+    for _ in range(warmup):
+        wl["step"]()
+    ctx.sync()
+    D.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        wl["step"]()
+    ctx.sync()
+    t1 = time.perf_counter()
+    D.barrier()
+    return D.reduce(t1 - t0, "MAX")
+
+
+def profile_pass(ctx, wl, steps):
+    """the same steps again with per-kernel HIP events on the context stream (BA runs eagerly
+    instead of as a graph); returns {kernel id: (total ms, launches)} and the step count"""
+    from lorb_slam_amd.runtime import lib
+    L = lib()
+    kernel_times(ctx, range(8))
+    L.lorb_kernel_timing_enable(ctx.handle, 1)
+    n = max(3, min(steps, 10))
+    for _ in range(n):
+        wl["step"]()
+    ctx.sync()
+    kt = {k: v for k, v in kernel_times(ctx, range(8)).items() if v[1] > 0}
+    L.lorb_kernel_timing_enable(ctx.handle, 0)
+    return kt, n
+
+
+def sub_c2(ctx, D, args):
+    """BASELINE C2 (2000x2000 top-2 + ratio test, `--pairs` pairs per GPU) inside the default run."""
+    wl = workload_c2(ctx, args, D.rank)
+    steps = max(5, args.steps)
+    elapsed = timed(ctx, D, wl, steps, max(2, args.warmup))
+    kt, pn = profile_pass(ctx, wl, steps)
+    total = D.reduce(wl["matches"] * steps, "SUM")
+    chk = wl["check"]()
+    cpu = wl["cpu"]() if (D.rank == 0 and not args.no_cpu_baseline and D.world == 1) else None
+    wl["cleanup"]()
+    return {"workload": wl["config"]["workload"], "config": wl["config"], "value": total / elapsed,
+            "unit": "matches/s", "pairs_per_sec": total * 2000 / elapsed, "steps": steps,
+            "ms_per_step": elapsed / steps * 1e3, "roofline": roofline_entry(kt, wl, pn),
+            "cpu_baseline": cpu, "check": chk}
 
 
 def main():
@@ -349,64 +500,75 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c2", "shared"])
+    ap.add_argument("--workload", default="c4", choices=["c4", "c2", "shared", "rehearse"])
     ap.add_argument("--shared-points", type=int, default=80000)
     ap.add_argument("--windows", type=int, default=1)
     ap.add_argument("--pairs", type=int, default=256)
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 sub-record of the default run")
     args = ap.parse_args()
 
-    D = Dist()
-    # one rank per GPU; with fewer GPUs than ranks (a rehearsal on a 1-GPU box) ranks share them
-    ndev = device_count()
-    ctx = Context(D.local_rank % ndev if ndev > 0 else D.local_rank)
-    if args.workload == "shared":
-        wl = workload_shared(ctx, args, D.rank, D)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        refuse(f"WORLD_SIZE={world} but --gpus {args.gpus}")
+    rehearse = args.workload == "rehearse"
+
+    if rehearse:
+        ctx = _NullCtx()
     else:
-        wl = (workload_c4 if args.workload == "c4" else workload_c2)(ctx, args, D.rank)
-    for _ in range(args.warmup):
-        wl["step"]()
-    ctx.sync()
-    D.barrier()
-    ctx.sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        wl["step"]()
-    ctx.sync()
-    t1 = time.perf_counter()
-    D.barrier()
-    elapsed = D.reduce(t1 - t0, "MAX")
+        from lorb_slam_amd.runtime import Context, device_count
+        ndev = device_count()
+        if ndev < world:
+            refuse(f"{world} ranks but only {ndev} visible GPU(s); ranks never share a GPU")
+    D = Dist()
+    comm = None
+    n_gpus = D.world
+    if not rehearse:
+        ctx = Context(D.local_rank)
+        if D.world > 1 or args.workload == "shared":
+            from lorb_slam_amd.runtime import Comm, unique_id
+            uid = D.broadcast_bytes(unique_id() if D.rank == 0 else None)
+            comm = Comm.rccl(ctx, D.world, D.rank, uid)
+            n_gpus = comm.size()[0]
+    if args.workload == "shared":
+        wl = workload_shared(ctx, args, D.rank, D, comm)
+    else:
+        wl = {"c4": workload_c4, "c2": workload_c2, "rehearse": workload_rehearse}[args.workload](ctx, args, D.rank)
+
+    elapsed = timed(ctx, D, wl, args.steps, args.warmup)
     check = wl["check"]()
-    # profile pass (same steps, per-kernel HIP events; BA runs eagerly instead of as a graph)
-    L = lib()
-    kernel_times(ctx, range(8))
-    L.lorb_kernel_timing_enable(ctx.handle, 1)
-    prof_steps = max(3, min(args.steps, 10))
-    for _ in range(prof_steps):
-        wl["step"]()
-    ctx.sync()
-    kt = {k: v for k, v in kernel_times(ctx, range(8)).items() if v[1] > 0}
-    L.lorb_kernel_timing_enable(ctx.handle, 0)
+    kt, pn = ({}, 1) if rehearse else profile_pass(ctx, wl, args.steps)
     total_iters = D.reduce(wl["ba_iters"] * args.steps, "SUM")
     total_matches = D.reduce(wl["matches"] * args.steps, "SUM")
     cpu = wl["cpu"]() if (D.rank == 0 and not args.no_cpu_baseline and D.world == 1 and wl["cpu"]) else None
+    c2 = sub_c2(ctx, D, args) if (args.workload == "c4" and not args.no_c2) else None
     if D.rank == 0:
         if args.workload in ("c4", "shared"):
             value, unit = total_iters / elapsed, "BA iterations/s"
-        else:
+        elif args.workload == "c2":
             value, unit = total_matches / elapsed, "matches/s"
-        rf = roofline_entry(kt, wl, prof_steps)
+        else:
+            value, unit = total_iters / elapsed, "rehearsal steps/s"
+        par = (f"point-partitioned window over {D.world} ranks (RCCL)" if args.workload == "shared"
+               else f"independent windows x{D.world}")
         out = {
-            "metric": METRIC, "value": value, "unit": unit, "n_gpus": D.world, "steps": args.steps,
+            "metric": METRIC, "value": value, "unit": unit, "n_gpus": n_gpus, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": wl.get("scaling", "weak"), "vs_baseline": None, "dtype": "f64+u8", "data": "synthetic",
-            "config": dict(wl["config"], parallelism=(f"point-partitioned window over {D.world} ranks (RCCL)"
-                                                      if args.workload == "shared" else f"independent windows x{D.world}")),
+            "scaling": wl.get("scaling", "weak"), "vs_baseline": None, "dtype": "f64+u8",
+            "data": "synthetic (lorb_slam_amd.synth, seeded per rank)",
+            "config": dict(wl["config"], parallelism=par),
             "matches_per_sec": total_matches / elapsed, "plan_build_ms": wl["plan_ms"],
-            "roofline": rf, "cpu_baseline": cpu, "check": check,
+            "roofline": roofline_entry(kt, wl, pn), "cpu_baseline": cpu, "c2": c2, "check": check,
         }
-        print(json.dumps(out))
+        if rehearse:
+            out["rehearsal"] = "no GPU: launcher + gloo path only; value is not a hot-path measurement"
+        print(json.dumps(out), flush=True)
     wl["cleanup"]()
+    if comm is not None:
+        comm.close()
     ctx.close()
     D.close()
 

@@ -464,6 +464,8 @@ int lorb_comm_init_rccl(lorb_ctx* ctx, int32_t nranks, int32_t rank, const void*
 int lorb_comm_init_host(lorb_ctx* ctx, int32_t nranks, int32_t rank, lorb_host_allreduce_fn fn,
                         void* user, lorb_comm** out);
 int lorb_comm_destroy(lorb_comm* comm);
+/* ranks in the communicator (ncclCommCount / ncclCommUserRank for RCCL); rank may be NULL */
+int lorb_comm_size(lorb_comm* comm, int32_t* nranks, int32_t* rank);
 /* all-reduce of device doubles on the ctx stream (send == recv allowed) */
 int lorb_comm_allreduce_f64(lorb_comm* comm, const double* d_send, double* d_recv, int64_t count,
                             int32_t op);

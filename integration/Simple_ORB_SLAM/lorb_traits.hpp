@@ -30,7 +30,10 @@ template <> struct FrameTraits<Simple_ORB_SLAM::Frame> {
   static point_type* map_point(F* f, size_t i) { return f->mvpMapPoints[i]; }    // frame.h:80
   // SURVEY §8f row 2 (lorb::ComputeStereoMatches, called as the body of
   // Frame::ComputeStereoMatches).  mDescriptorsRight and the extractors are private
-  // (frame.h:126-134): this binding needs `friend struct lorb::FrameTraits<Frame>;` in frame.h.
+  // (frame.h:126-134): these accessors need `friend struct lorb::FrameTraits<Frame>;` in frame.h
+  // and are compiled only with -DLORB_REFERENCE_FRIENDS.  The three drop-in
+  // files never call them, so the default build needs the reference headers unchanged.
+#ifdef LORB_REFERENCE_FRIENDS
   static void raw_keypoint(F* f, size_t i, float* x, float* y, int* o) {         // mvKeys (frame.h:94)
     const cv::KeyPoint& k = f->mvKeys[i];
     *x = k.pt.x; *y = k.pt.y; *o = k.octave;
@@ -48,6 +51,7 @@ template <> struct FrameTraits<Simple_ORB_SLAM::Frame> {
     const cv::Mat& m = (side ? f->mpORBextractorRight : f->mpORBextractorLeft)->mvImagePyramid[l];  // ORBextractor.h:85
     *d = m.ptr<uint8_t>(); *rows = m.rows; *cols = m.cols; *step = (int)m.step;
   }
+#endif  // LORB_REFERENCE_FRIENDS
   static void set_stereo(F* f, const float* uR, const float* depth, size_t n) {   // mvuRight / mvDepth (frame.h:90-91)
     f->mvuRight.assign(uR, uR + n);
     f->mvDepth.assign(depth, depth + n);
@@ -57,8 +61,8 @@ template <> struct FrameTraits<Simple_ORB_SLAM::Frame> {
   static void params(F* f, lorb_frame_params* fp) {                                // frame.h:96-110
     fp->fx = f->fx; fp->fy = f->fy; fp->cx = f->cx; fp->cy = f->cy; fp->bf = f->mbf; fp->b = f->mb;
     fp->min_x = f->mnMinX; fp->max_x = f->mnMaxX; fp->min_y = f->mnMinY; fp->max_y = f->mnMaxY;
-    fp->grid_w_inv = static_cast<float>(FRAME_GRID_COLS) / (f->mnMaxX - f->mnMinX);   // frame.cpp:83
-    fp->grid_h_inv = static_cast<float>(FRAME_GRID_ROWS) / (f->mnMaxY - f->mnMinY);
+    fp->grid_w_inv = static_cast<float>(Simple_ORB_SLAM::FRAME_GRID_COLS) / (f->mnMaxX - f->mnMinX);   // frame.cpp:83
+    fp->grid_h_inv = static_cast<float>(Simple_ORB_SLAM::FRAME_GRID_ROWS) / (f->mnMaxY - f->mnMinY);
     fp->n_levels = f->mnScaleLevels; fp->log_scale_factor = f->mfLogScaleFactor;
     for (int i = 0; i < f->mnScaleLevels && i < LORB_MAX_LEVELS; ++i) fp->scale_factors[i] = f->mvScaleFactors[i];
   }
@@ -119,11 +123,14 @@ template <> struct PointTraits<Simple_ORB_SLAM::MapPoint> {
   }
   static void increase_visible(P* p) { p->IncreaseVisible(); }                     // map_point.cpp:167
   // SURVEY §8f row 4 (lorb::ComputeDescriptors): mDescriptor is private (map_point.h:81), so
-  // batching needs `friend struct lorb::PointTraits<MapPoint>;` in map_point.h.
+  // batching needs `friend struct lorb::PointTraits<MapPoint>;` in map_point.h
+  // (-DLORB_REFERENCE_FRIENDS, as above).
+#ifdef LORB_REFERENCE_FRIENDS
   static void set_descriptor(P* p, const uint8_t* d) {
     p->mDescriptor = cv::Mat(1, 32, CV_8U);
     std::memcpy(p->mDescriptor.ptr<uint8_t>(), d, 32);
   }
+#endif  // LORB_REFERENCE_FRIENDS
 };
 
 }  // namespace lorb

@@ -2349,7 +2349,7 @@ int plan_read(lorb_ba_plan* P, double* const* pose_out, double* const* point_out
       lorb_ba_summary s{};
       s.iterations = st[w].iter; s.successful_steps = st[w].n_success; s.termination = st[w].term;
       s.initial_cost = st[w].initial_cost; s.final_cost = st[w].cost;
-      if (bw.n_obs == 0) { s.iterations = 0; s.termination = LORB_TERM_FUNCTION_TOL; }
+      if (bw.n_obs_all == 0) { s.iterations = 0; s.termination = LORB_TERM_FUNCTION_TOL; }
       sums[w] = s;
     }
   }

@@ -98,6 +98,22 @@ int lorb_comm_destroy(lorb_comm* c) {
   return LORB_OK;
 }
 
+int lorb_comm_size(lorb_comm* c, int32_t* nranks, int32_t* rank) {
+  if (!c || !nranks) return LORB_E_INVALID;
+  if (c->rccl) {
+    int n = 0, r = 0;
+    ncclResult_t e = ncclCommCount(static_cast<ncclComm_t>(c->nccl), &n);
+    if (e == ncclSuccess) e = ncclCommUserRank(static_cast<ncclComm_t>(c->nccl), &r);
+    if (e != ncclSuccess) return lorb::set_error(c->ctx, LORB_E_COMM, "ncclCommCount: %s", ncclGetErrorString(e));
+    *nranks = n;
+    if (rank) *rank = r;
+  } else {
+    *nranks = c->nranks;
+    if (rank) *rank = c->rank;
+  }
+  return LORB_OK;
+}
+
 int lorb_comm_allreduce_f64(lorb_comm* c, const double* d_send, double* d_recv, int64_t count, int32_t op) {
   if (!c || count < 0 || (count > 0 && (!d_send || !d_recv))) return LORB_E_INVALID;
   return lorb::comm_allreduce(c, d_send, d_recv, (size_t)count, op);

@@ -283,6 +283,12 @@ class Comm:
     def handle(self):
         return self._p
 
+    def size(self):
+        """(nranks, rank) as the communicator itself reports them (ncclCommCount for RCCL)."""
+        n, r = C.c_int32(0), C.c_int32(0)
+        self.ctx.check(lib().lorb_comm_size(self._p, C.byref(n), C.byref(r)), "lorb_comm_size")
+        return n.value, r.value
+
     def close(self):
         if self._p:
             lib().lorb_comm_destroy(self._p)
