@@ -91,7 +91,7 @@ class LocalMapping {
   void RequestFinish() { mbFinish.store(true); }
   void set_full_step(bool on) { mbFullStep = on; }
   void set_device(int d) { mDevice = d; }
-  size_t processed() const { return mnProcessed; }
+  size_t processed() const { return mnProcessed.load(); }
   FrameT* current() const { return mpCurrFrame; }
 
  protected:
@@ -105,7 +105,7 @@ class LocalMapping {
   std::atomic<bool> mbFinish{false};
   bool mbFullStep = false;
   int mDevice = 0;
-  size_t mnProcessed = 0;
+  std::atomic<size_t> mnProcessed{0};  // read by other threads (processed())
 };
 
 }  // namespace lorb
