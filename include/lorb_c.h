@@ -311,18 +311,16 @@ int lorb_orb_describe_dev(lorb_ctx* ctx, const lorb_image_pyramid* d_pyr, int32_
                           const float* d_y, const int32_t* d_level, const int32_t* d_pattern, float* d_angle,
                           uint8_t* d_desc);
 
-/* SURVEY §8f row 3, detection stage of ORBextractor::ComputeKeyPointsOctTree
- * (src/ORBextractor.cpp:898-1000): the cell grid of every level (:903-990; n_desired[l] =
- * mnFeaturesPerLevel[l]) and per cell cv::FAST(cell, ini_th, nonmax = true), re-run with min_th
- * when it finds at most 3 corners (:990-996).  Keypoints come out in level coordinates, grouped by
- * level, then cell (row-major), then FAST's scan order, with response = FAST score.  Cell c of
- * level l spans [cell_off[cell_base[l] + l + c], cell_off[cell_base[l] + l + c + 1]); cell_base
- * has n_levels + 1 entries.  The retention that follows in the reference (KeyPointsFilter::
- * retainBest, :1000-1060) is left to the caller: its std::nth_element tie order is
- * implementation-defined.  Host pointers; synchronous. */
-int lorb_orb_fast_cells(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired, int32_t ini_th,
-                        int32_t min_th, int32_t max_keypoints, float* x, float* y, float* response,
-                        int32_t max_cells, int32_t* cell_base, int32_t* cell_off, int32_t* n_keypoints);
+/* SURVEY §8f row 3, FAST stage of ORBextractor::ComputeKeyPointsOctTree (src/ORBextractor.cpp:
+ * 803-872): per level the grid of 30-pixel cells with a 6-pixel overlap inside the
+ * EDGE_THRESHOLD - 3 = 16-pixel border, and per cell cv::FAST(cell, ini_th, nonmax = true), re-run
+ * with min_th when the cell found NO corner (:855-859).  Keypoints come out in level coordinates,
+ * grouped by level, then cell (row-major), then FAST's scan order -- the order of vToDistributeKeys
+ * -- with response = FAST score.  Cell c of level l spans [cell_off[cell_base[l] + l + c],
+ * cell_off[cell_base[l] + l + c + 1]); cell_base has n_levels + 1 entries.  Host pointers; sync. */
+int lorb_orb_fast_cells(lorb_ctx* ctx, const lorb_image_pyramid* pyr, int32_t ini_th, int32_t min_th,
+                        int32_t max_keypoints, float* x, float* y, float* response, int32_t max_cells,
+                        int32_t* cell_base, int32_t* cell_off, int32_t* n_keypoints);
 
 /* SURVEY §8f row 3, ORBextractor::ComputePyramid (src/ORBextractor.cpp:1157-1184): level 0 is
  * the image, level l = cv::resize(level l-1, cvRound(size / scale_factors[l]), INTER_LINEAR)
@@ -337,15 +335,41 @@ int lorb_orb_pyramid_dev(lorb_ctx* ctx, const uint8_t* d_image, int32_t rows, in
                          lorb_image_pyramid* layout);
 
 /* SURVEY §8f row 3, ORBextractor::ComputeKeyPointsOctTree without the orientation
- * (src/ORBextractor.cpp:898-1067): lorb_orb_fast_cells, then the nToRetain distribution,
- * KeyPointsFilter::retainBest + resize per cell (std::nth_element / std::partition, as OpenCV),
- * cell offsets, octave and size (PATCH_SIZE * scale_factors[l]), and the level-wide retainBest.
- * Per keypoint: x, y (level coordinates), octave, size, response; level_off[n_levels + 1].
- * Then lorb_orb_describe gives the angle and the descriptor.  Host pointers; synchronous. */
+ * (src/ORBextractor.cpp:799-892): lorb_orb_fast_cells, then DistributeOctTree per level
+ * (:554-797; N = n_desired[l] = mnFeaturesPerLevel[l]) -- the quadtree that keeps the strongest
+ * keypoint of every node -- then the border offset, octave and size (PATCH_SIZE * scale_factors[l]
+ * truncated to int, :881).  Per keypoint: x, y (level coordinates), octave, size, response, in the
+ * reference's order (level, then the final std::list order of the quadtree nodes);
+ * level_off[n_levels + 1].  Nodes holding equal key counts are ranked by creation order where the
+ * reference compares std::list node addresses (:717).  Host pointers; synchronous. */
 int lorb_orb_detect(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired,
                     const float* scale_factors, int32_t ini_th, int32_t min_th, int32_t max_keypoints, float* x,
                     float* y, int32_t* octave, float* size, float* response, int32_t* level_off,
                     int32_t* n_keypoints);
+
+/* SURVEY §8f row 3, the whole ORBextractor::operator()(image, mask, keypoints, descriptors)
+ * (src/ORBextractor.cpp:1087-1151): ComputePyramid, ComputeKeyPointsOctTree (+ IC_Angle
+ * orientation), GaussianBlur + rBRIEF per level with the caller's 256-pair pattern
+ * (bit_pattern_31_, :152), and the coordinates of level > 0 keypoints scaled to level 0 (:1141-1147).
+ * Outputs in the reference's keypoint order: x, y, octave, size, angle (degrees), response and the
+ * 32-byte descriptors; level_off[n_levels + 1]; *n_keypoints.  max_keypoints must be at least
+ * lorb_orb_extract_capacity()'s bound for the _dev variant.  Host pointers; synchronous. */
+int lorb_orb_extract(lorb_ctx* ctx, const uint8_t* image, int32_t rows, int32_t cols, int32_t step, int32_t n_levels,
+                     const float* scale_factors, const int32_t* n_desired, int32_t ini_th, int32_t min_th,
+                     const int32_t* pattern, int32_t max_keypoints, float* x, float* y, int32_t* octave, float* size,
+                     float* angle, float* response, uint8_t* desc, int32_t* level_off, int32_t* n_keypoints);
+/* device variant: image, pattern (1024 ints), the pyramid buffer (pyramid_bytes) and every output
+ * are device arrays, d_level_off (n_levels + 1) and d_n (1) too.  Returns once the pyramid is
+ * built (its resize tables are host-staged); detection and description run asynchronously on the
+ * ctx stream.  *d_n = -1 when a quadtree exceeded its node capacity. */
+int lorb_orb_extract_dev(lorb_ctx* ctx, const uint8_t* d_image, int32_t rows, int32_t cols, int32_t step,
+                         int32_t n_levels, const float* scale_factors, const int32_t* n_desired, int32_t ini_th,
+                         int32_t min_th, const int32_t* d_pattern, int32_t max_keypoints, uint8_t* d_pyramid,
+                         int64_t pyramid_bytes, float* d_x, float* d_y, int32_t* d_octave, float* d_size,
+                         float* d_angle, float* d_response, uint8_t* d_desc, int32_t* d_level_off, int32_t* d_n);
+/* output capacity (keypoints) and pyramid bytes lorb_orb_extract_dev needs for an image size */
+int lorb_orb_extract_capacity(int32_t rows, int32_t cols, int32_t n_levels, const float* scale_factors,
+                              const int32_t* n_desired, int32_t* max_keypoints, int64_t* pyramid_bytes);
 
 /* ----------------------------------------------------------------------------------------
  * Bundle adjustment: Ceres-default Levenberg-Marquardt + DENSE_SCHUR restated

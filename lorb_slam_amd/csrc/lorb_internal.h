@@ -19,7 +19,7 @@ struct lorb_ctx {
   std::string err;
   hipEvent_t ev[64] = {};
   // grow-only device scratch buffers, one per slot
-  static constexpr int kScratch = 96;
+  static constexpr int kScratch = 128;
   void* scratch[kScratch] = {};
   size_t scratch_sz[kScratch] = {};
   // host copy of the bytes last uploaded into a slot (lorb::upload); an identical re-upload of
@@ -126,6 +126,89 @@ __device__ __forceinline__ int block_excl_scan_1024(int v, int* wsum, int* total
   __syncthreads();
   *total = tot;
   return pre + incl - v;
+}
+
+// The same for any workgroup size NT (a multiple of 64); wsum: __shared__ int[NT / 64].
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const int s = wsum[w];
+    pre += w < wv ? s : 0;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + incl - v;
+}
+
+// Exclusive max-scan (identity `lo`) across an NT-thread workgroup; wmax: __shared__ int[NT / 64].
+template <int NT>
+__device__ __forceinline__ int block_excl_max(int v, int lo, int* wmax) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl = max(incl, u);
+  }
+  int ex = __shfl_up(incl, 1, 64);
+  if (lane == 0) ex = lo;
+  if (lane == 63) wmax[wv] = incl;
+  __syncthreads();
+  int pre = lo;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) pre = w < wv ? max(pre, wmax[w]) : pre;
+  __syncthreads();
+  return max(pre, ex);
+}
+
+// Four counters (plain POD: HIP's int4 member proxies are avoided in arithmetic-heavy code).
+struct I4 {
+  int v[4];
+};
+
+// Exclusive scan of four counters at once across an NT-thread workgroup; wsum: __shared__ I4[NT / 64].
+template <int NT>
+__device__ __forceinline__ I4 block_excl_scan4(const I4& v, I4* wsum, I4* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  I4 incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int u = __shfl_up(incl.v[q], o, 64);
+      if (lane >= o) incl.v[q] += u;
+    }
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  I4 pre = {{0, 0, 0, 0}}, tot = {{0, 0, 0, 0}};
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const I4 s = wsum[w];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pre.v[q] += w < wv ? s.v[q] : 0;
+      tot.v[q] += s.v[q];
+    }
+  }
+  __syncthreads();
+  *total = tot;
+  I4 r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r.v[q] = pre.v[q] + incl.v[q] - v.v[q];
+  return r;
 }
 
 }  // namespace lorb

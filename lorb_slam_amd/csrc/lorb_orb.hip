@@ -17,6 +17,7 @@
 #include <cmath>
 
 #include "lorb_internal.h"
+#include "lorb_sincosf.h"
 
 namespace {
 
@@ -108,7 +109,8 @@ __device__ __forceinline__ int wave_isum(int v) {
 
 constexpr int kDescWaves = 4;
 
-__global__ __launch_bounds__(64 * kDescWaves) void k_orb_desc(OrbPyr P, int n, const float* __restrict__ kx,
+__global__ __launch_bounds__(64 * kDescWaves) void k_orb_desc(OrbPyr P, int n, const int* __restrict__ d_n,
+                                                              const float* __restrict__ kx,
                                                               const float* __restrict__ ky,
                                                               const int* __restrict__ klev,
                                                               const int* __restrict__ pattern,
@@ -119,6 +121,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orb_desc(OrbPyr P, int n, c
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * kDescWaves + (threadIdx.x >> 6);
+  if (d_n) n = min(n, *d_n);  // device-side count (extraction pipeline); < 0 = failed upstream
   if (i >= n) return;
   const int l = klev[i];
   if (l < 0 || l >= P.n_levels) return;  // validated on the host for the host entry point
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(64 * kDescWaves) void k_orb_desc(OrbPyr P, int n, c
   // computeOrbDescriptor on the blurred level
   const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
   const float angle = ang * factorPI;
-  const float a = (float)cos((double)angle), b = (float)sin((double)angle);
+  const float a = lorb_cosf(angle), b = lorb_sinf(angle);  // std::cos(float) = libm cosf (:115)
   const uint8_t* center = P.blur + P.offset[l] + (int64_t)cy * step + cx;
   int nib = 0;
 #pragma unroll
@@ -212,7 +215,7 @@ int check_orb(lorb_ctx* ctx, const lorb_image_pyramid* p, int n) {
 
 enum { S_ORB = 48 };  // shares the stereo family's slots (calls on one ctx are serialized)
 
-int enqueue_orb(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const uint8_t* d_data, int n, const float* d_x,
+int enqueue_orb(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const uint8_t* d_data, int n, const int* d_n, const float* d_x,
                 const float* d_y, const int* d_lev, const int* d_pat, float* d_ang, uint8_t* d_desc) {
   OrbPyr P{};
   P.data = d_data;
@@ -230,189 +233,10 @@ int enqueue_orb(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const uint8_t* d_d
   LORB_TRY(lorb::scratch_t(ctx, S_ORB + 0, (size_t)pyr_extent(pyr), &P.blur));
   hipLaunchKernelGGL(k_orb_blur, dim3(tiles), dim3(256), 0, ctx->stream, P);
   if (n > 0)
-    hipLaunchKernelGGL(k_orb_desc, dim3(lorb::ceil_div(n, kDescWaves)), dim3(64 * kDescWaves), 0, ctx->stream, P, n,
+    hipLaunchKernelGGL(k_orb_desc, dim3(lorb::ceil_div(n, kDescWaves)), dim3(64 * kDescWaves), 0, ctx->stream, P, n, d_n,
                        d_x, d_y, d_lev, d_pat, d_ang, d_desc);
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
-}
-
-// ---- detection stage (src/ORBextractor.cpp:898-1000): per-cell cv::FAST ------------------
-
-constexpr int kOff16[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1}, {2, -2}, {1, -3},
-                               {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
-
-struct FastCell {
-  int level, ini_x, ini_y, w, h, out_base;
-};
-
-// cornerScore<16> (OpenCV 3.1 fast_score.cpp) on the LDS cell image (row stride w)
-__device__ __forceinline__ int fast_score(const uint8_t* ptr, const int* pixel, int threshold) {
-  int d[25];
-  const int v = ptr[0];
-#pragma unroll
-  for (int k = 0; k < 25; k++) d[k] = v - ptr[pixel[k]];
-  int a0 = threshold;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    int a = min(d[k + 1], d[k + 2]);
-    a = min(a, d[k + 3]);
-    if (a <= a0) continue;
-#pragma unroll
-    for (int m = 4; m <= 8; m++) a = min(a, d[k + m]);
-    a0 = max(a0, min(a, d[k]));
-    a0 = max(a0, min(a, d[k + 9]));
-  }
-  int b0 = -a0;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    int b = max(d[k + 1], d[k + 2]);
-#pragma unroll
-    for (int m = 3; m <= 5; m++) b = max(b, d[k + m]);
-    if (b >= b0) continue;
-#pragma unroll
-    for (int m = 6; m <= 8; m++) b = max(b, d[k + m]);
-    b0 = min(b0, max(b, d[k]));
-    b0 = min(b0, max(b, d[k + 9]));
-  }
-  return -b0 - 1;
-}
-
-// One 1024-thread workgroup per cell: the cell image in LDS, FAST_t<16> detection + score for
-// every inner pixel, 3x3 non-maximum suppression, the iniThFAST -> minThFAST fallback when at
-// most 3 corners survive, and the survivors written in FAST's row-major order (block scan).
-__global__ __launch_bounds__(1024) void k_orb_fast(const uint8_t* __restrict__ data, OrbPyr P,
-                                                   const FastCell* __restrict__ cells, int ini_th, int min_th,
-                                                   float* __restrict__ ox, float* __restrict__ oy,
-                                                   float* __restrict__ oresp, int* __restrict__ ocount) {
-  extern __shared__ uint8_t lds[];
-  __shared__ int s_count, wsum[16];
-  __shared__ int pixel[25];
-  const FastCell c = cells[blockIdx.x];
-  const int w = c.w, h = c.h, n = w * h, t = threadIdx.x;
-  uint8_t* img = lds;
-  uint8_t* score = lds + n;
-  uint8_t* corner = lds + 2 * n;
-  const uint8_t* src = data + P.offset[c.level] + (int64_t)c.ini_y * P.step[c.level] + c.ini_x;
-  const int step = P.step[c.level];
-  for (int p0 = t; p0 < n; p0 += 1024 * 8) {  // eight loads in flight per thread
-    uint8_t v[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int p = p0 + 1024 * u;
-      const int i = p / w, j = p - i * w;
-      v[u] = p < n ? src[(int64_t)i * step + j] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; u++)
-      if (p0 + 1024 * u < n) img[p0 + 1024 * u] = v[u];
-  }
-  if (t < 25) pixel[t] = kOff16[t & 15][0] + kOff16[t & 15][1] * w;
-  for (int pass = 0; pass < 2; ++pass) {
-    const int th = min(max(pass ? min_th : ini_th, 0), 255);
-    for (int p = t; p < n; p += 1024) { score[p] = 0; corner[p] = 0; }
-    if (t == 0) s_count = 0;
-    __syncthreads();
-    for (int p = t; p < n; p += 1024) {
-      const int i = p / w, j = p - i * w;
-      if (i < 3 || i >= h - 3 || j < 3 || j >= w - 3) continue;
-      const uint8_t* ptr = img + p;
-      const int v = ptr[0];
-      auto cat = [&](int k) { const int e = ptr[pixel[k]] - v; return e < -th ? 1 : (e > th ? 2 : 0); };
-      int d = cat(0) | cat(8);
-      if (d == 0) continue;
-      d &= cat(2) | cat(10);
-      d &= cat(4) | cat(12);
-      d &= cat(6) | cat(14);
-      if (d == 0) continue;
-      d &= cat(1) | cat(9);
-      d &= cat(3) | cat(11);
-      d &= cat(5) | cat(13);
-      d &= cat(7) | cat(15);
-      bool is = false;
-      if (d & 1) {
-        const int vt = v - th;
-        int count = 0;
-        for (int k = 0; k < 25; k++) {
-          if (ptr[pixel[k]] < vt) { if (++count > 8) { is = true; break; } }
-          else count = 0;
-        }
-      }
-      if (!is && (d & 2)) {
-        const int vt = v + th;
-        int count = 0;
-        for (int k = 0; k < 25; k++) {
-          if (ptr[pixel[k]] > vt) { if (++count > 8) { is = true; break; } }
-          else count = 0;
-        }
-      }
-      if (is) { corner[p] = 1; score[p] = (uint8_t)fast_score(ptr, pixel, th); }
-    }
-    __syncthreads();
-    int mine = 0;
-    for (int p = t; p < n; p += 1024) {
-      if (!corner[p]) continue;
-      const int s = score[p];
-      mine += s > score[p - w - 1] && s > score[p - w] && s > score[p - w + 1] && s > score[p - 1] && s > score[p + 1] &&
-              s > score[p + w - 1] && s > score[p + w] && s > score[p + w + 1];
-    }
-    if (mine) atomicAdd(&s_count, mine);
-    __syncthreads();
-    if (pass == 0 && s_count > 3) break;  // uniform: s_count is read by every thread after the barrier
-    __syncthreads();
-  }
-  int run = 0;
-  for (int base = 0; base < n; base += 1024) {
-    const int p = base + t;
-    bool keep = false;
-    if (p < n && corner[p]) {
-      const int s = score[p];
-      keep = s > score[p - w - 1] && s > score[p - w] && s > score[p - w + 1] && s > score[p - 1] && s > score[p + 1] &&
-             s > score[p + w - 1] && s > score[p + w] && s > score[p + w + 1];
-    }
-    int tot;
-    const int ex = lorb::block_excl_scan_1024(keep ? 1 : 0, wsum, &tot);
-    if (keep) {
-      const int i = p / w, j = p - i * w;
-      const int o = c.out_base + run + ex;
-      ox[o] = (float)(j + c.ini_x); oy[o] = (float)(i + c.ini_y); oresp[o] = (float)score[p];
-    }
-    run += tot;
-  }
-  if (t == 0) ocount[blockIdx.x] = run;
-}
-
-// the cell grid of one level, src/ORBextractor.cpp:903-990 (see oracle/fast.c)
-int orb_cells(int rows, int cols, int n_desired, float image_ratio, std::vector<int>& cells) {
-  const int EDGE = 19;
-  const int levelCols = (int)std::sqrt((float)n_desired / (5 * image_ratio));
-  const int levelRows = (int)(image_ratio * levelCols);
-  if (levelCols < 1 || levelRows < 1) return -1;
-  const int minBorderX = EDGE, minBorderY = EDGE, maxBorderX = cols - EDGE, maxBorderY = rows - EDGE;
-  const int W = maxBorderX - minBorderX, H = maxBorderY - minBorderY;
-  const int cellW = (int)std::ceil((float)W / levelCols), cellH = (int)std::ceil((float)H / levelRows);
-  cells.assign(4 * (size_t)levelRows * levelCols, 0);
-  float hY = (float)(cellH + 6);
-  for (int i = 0; i < levelRows; i++) {
-    const float iniY = (float)(minBorderY + i * cellH - 3);
-    bool skip_row = false;
-    if (i == levelRows - 1) {
-      hY = maxBorderY + 3 - iniY;
-      if (hY <= 0) skip_row = true;
-    }
-    float hX = (float)(cellW + 6);
-    for (int j = 0; j < levelCols; j++) {
-      const float iniX = (float)(minBorderX + j * cellW - 3);
-      int* c = &cells[4 * (size_t)(i * levelCols + j)];
-      c[0] = (int)iniX; c[1] = (int)iniY;
-      if (skip_row) continue;
-      if (j == levelCols - 1) {
-        hX = maxBorderX + 3 - iniX;
-        if (hX <= 0) continue;
-      }
-      c[2] = (int)hX; c[3] = (int)hY;
-    }
-  }
-  return levelRows * levelCols;
 }
 
 // ---- ComputePyramid (src/ORBextractor.cpp:1157-1184): OpenCV 3.1 8U INTER_LINEAR resize ----
@@ -530,6 +354,683 @@ int enqueue_pyramid(lorb_ctx* ctx, const uint8_t* d_img, int rows, int cols, int
   return LORB_OK;
 }
 
+// ---- keypoint stage: ComputeKeyPointsOctTree (src/ORBextractor.cpp:799-897) --------------
+// Per level, 30-pixel cells with a 6-pixel overlap inside the EDGE_THRESHOLD-3 border (:803-847);
+// per cell cv::FAST(iniThFAST, nonmax) re-run with minThFAST only when the cell found nothing
+// (:849-859); then DistributeOctTree (:554-797).  Keypoints travel relative to the level's
+// (minBorderX, minBorderY) = (16, 16), as vToDistributeKeys does.
+
+constexpr int kOff16[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1}, {2, -2}, {1, -3},
+                               {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+constexpr int kBorder = 19 - 3;       // EDGE_THRESHOLD - 3 (:808)
+constexpr int kCellMax = 66;          // cells are < 60 + 6 pixels on a side (wCell = ceil(w / floor(w / 30)))
+constexpr int kFastThreads = 256;
+
+struct FastCell {
+  int level, ini_x, ini_y, w, h, out_base, rel_x, rel_y;  // rel = (j wCell, i hCell), :865-866
+};
+
+// cornerScore<16> (OpenCV 3.1 fast_score.cpp) on the LDS cell image (row stride w)
+__device__ __forceinline__ int fast_score(const uint8_t* ptr, const int* pixel, int threshold) {
+  int d[25];
+  const int v = ptr[0];
+#pragma unroll
+  for (int k = 0; k < 25; k++) d[k] = v - ptr[pixel[k]];
+  int a0 = threshold;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int a = min(d[k + 1], d[k + 2]);
+    a = min(a, d[k + 3]);
+    if (a <= a0) continue;
+#pragma unroll
+    for (int m = 4; m <= 8; m++) a = min(a, d[k + m]);
+    a0 = max(a0, min(a, d[k]));
+    a0 = max(a0, min(a, d[k + 9]));
+  }
+  int b0 = -a0;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int b = max(d[k + 1], d[k + 2]);
+#pragma unroll
+    for (int m = 3; m <= 5; m++) b = max(b, d[k + m]);
+    if (b >= b0) continue;
+#pragma unroll
+    for (int m = 6; m <= 8; m++) b = max(b, d[k + m]);
+    b0 = min(b0, max(b, d[k]));
+    b0 = min(b0, max(b, d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+// One 256-thread workgroup per cell: the cell image in LDS, FAST_t<16> detection + score of every
+// inner pixel, 3x3 non-maximum suppression, the minThFAST re-run when no corner survives, and the
+// survivors written in FAST's row-major order (block scan) relative to the level border.
+__global__ __launch_bounds__(kFastThreads) void k_orb_fast(const uint8_t* __restrict__ data, OrbPyr P,
+                                                           const FastCell* __restrict__ cells, int ini_th, int min_th,
+                                                           float* __restrict__ ox, float* __restrict__ oy,
+                                                           float* __restrict__ oresp, int* __restrict__ ocount) {
+  __shared__ uint8_t img[kCellMax * kCellMax], score[kCellMax * kCellMax], corner[kCellMax * kCellMax];
+  __shared__ int s_count, wsum[kFastThreads / 64];
+  __shared__ int pixel[25];
+  const FastCell c = cells[blockIdx.x];
+  const int w = c.w, h = c.h, n = w * h, t = threadIdx.x;
+  const uint8_t* src = data + P.offset[c.level] + (int64_t)c.ini_y * P.step[c.level] + c.ini_x;
+  const int step = P.step[c.level];
+  for (int p0 = t; p0 < n; p0 += kFastThreads * 8) {  // eight loads in flight per thread
+    uint8_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int p = p0 + kFastThreads * u;
+      const int i = p / w, j = p - i * w;
+      v[u] = p < n ? src[(int64_t)i * step + j] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++)
+      if (p0 + kFastThreads * u < n) img[p0 + kFastThreads * u] = v[u];
+  }
+  if (t < 25) pixel[t] = kOff16[t & 15][0] + kOff16[t & 15][1] * w;
+  for (int pass = 0; pass < 2; ++pass) {
+    const int th = min(max(pass ? min_th : ini_th, 0), 255);
+    for (int p = t; p < n; p += kFastThreads) { score[p] = 0; corner[p] = 0; }
+    if (t == 0) s_count = 0;
+    __syncthreads();
+    for (int p = t; p < n; p += kFastThreads) {
+      const int i = p / w, j = p - i * w;
+      if (i < 3 || i >= h - 3 || j < 3 || j >= w - 3) continue;
+      const uint8_t* ptr = img + p;
+      const int v = ptr[0];
+      auto cat = [&](int k) { const int e = ptr[pixel[k]] - v; return e < -th ? 1 : (e > th ? 2 : 0); };
+      int d = cat(0) | cat(8);
+      if (d == 0) continue;
+      d &= cat(2) | cat(10);
+      d &= cat(4) | cat(12);
+      d &= cat(6) | cat(14);
+      if (d == 0) continue;
+      d &= cat(1) | cat(9);
+      d &= cat(3) | cat(11);
+      d &= cat(5) | cat(13);
+      d &= cat(7) | cat(15);
+      bool is = false;
+      if (d & 1) {
+        const int vt = v - th;
+        int count = 0;
+        for (int k = 0; k < 25; k++) {
+          if (ptr[pixel[k]] < vt) { if (++count > 8) { is = true; break; } }
+          else count = 0;
+        }
+      }
+      if (!is && (d & 2)) {
+        const int vt = v + th;
+        int count = 0;
+        for (int k = 0; k < 25; k++) {
+          if (ptr[pixel[k]] > vt) { if (++count > 8) { is = true; break; } }
+          else count = 0;
+        }
+      }
+      if (is) { corner[p] = 1; score[p] = (uint8_t)fast_score(ptr, pixel, th); }
+    }
+    __syncthreads();
+    int mine = 0;
+    for (int p = t; p < n; p += kFastThreads) {
+      if (!corner[p]) continue;
+      const int s = score[p];
+      mine += s > score[p - w - 1] && s > score[p - w] && s > score[p - w + 1] && s > score[p - 1] && s > score[p + 1] &&
+              s > score[p + w - 1] && s > score[p + w] && s > score[p + w + 1];
+    }
+    if (mine) atomicAdd(&s_count, mine);
+    __syncthreads();
+    if (pass == 0 && s_count > 0) break;  // uniform: s_count is read by every thread after the barrier
+    __syncthreads();
+  }
+  int run = 0;
+  for (int base = 0; base < n; base += kFastThreads) {
+    const int p = base + t;
+    bool keep = false;
+    if (p < n && corner[p]) {
+      const int s = score[p];
+      keep = s > score[p - w - 1] && s > score[p - w] && s > score[p - w + 1] && s > score[p - 1] && s > score[p + 1] &&
+             s > score[p + w - 1] && s > score[p + w] && s > score[p + w + 1];
+    }
+    int tot;
+    const int ex = lorb::block_excl_scan<kFastThreads>(keep ? 1 : 0, wsum, &tot);
+    if (keep) {
+      const int i = p / w, j = p - i * w;
+      const int o = c.out_base + run + ex;
+      ox[o] = (float)(j + c.rel_x); oy[o] = (float)(i + c.rel_y); oresp[o] = (float)score[p];
+    }
+    run += tot;
+  }
+  if (t == 0) ocount[blockIdx.x] = run;
+}
+
+// the cell grid of one level, src/ORBextractor.cpp:803-847 (see oracle/fast.c)
+int orb_cells(int rows, int cols, std::vector<int>& cells, int* ncols, int* nrows) {
+  const float W = 30;
+  const int minBorderX = kBorder, minBorderY = kBorder, maxBorderX = cols - kBorder, maxBorderY = rows - kBorder;
+  const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
+  const int nCols = (int)(width / W), nRows = (int)(height / W);
+  if (nCols < 1 || nRows < 1) return -1;
+  const int wCell = (int)std::ceil(width / (float)nCols), hCell = (int)std::ceil(height / (float)nRows);
+  cells.assign(6 * (size_t)nRows * nCols, 0);
+  for (int i = 0; i < nRows; i++) {
+    const float iniY = (float)(minBorderY + i * hCell);
+    float maxY = iniY + (float)hCell + 6;
+    const bool skip_row = iniY >= (float)(maxBorderY - 3);
+    if (maxY > (float)maxBorderY) maxY = (float)maxBorderY;
+    for (int j = 0; j < nCols; j++) {
+      const float iniX = (float)(minBorderX + j * wCell);
+      float maxX = iniX + (float)wCell + 6;
+      int* c = &cells[6 * (size_t)(i * nCols + j)];
+      c[0] = (int)iniX; c[1] = (int)iniY; c[4] = j * wCell; c[5] = i * hCell;
+      if (skip_row || iniX >= (float)(maxBorderX - 6)) continue;
+      if (maxX > (float)maxBorderX) maxX = (float)maxBorderX;
+      c[2] = (int)maxX - (int)iniX; c[3] = (int)maxY - (int)iniY;
+    }
+  }
+  *ncols = nCols; *nrows = nRows;
+  return nRows * nCols;
+}
+
+// ---- DistributeOctTree (src/ORBextractor.cpp:496-797) on the device ----------------------
+// One 1024-thread workgroup per level.  The reference's std::list<ExtractorNode> is kept as an
+// array of nodes in LIST ORDER (front first); every key is owned by exactly one live node, and each
+// node owns a contiguous segment of the level's key permutation `perm`, in the order of its vKeys.
+// A division pass (main loop :632-698, or one iteration of the focused loop :709-770):
+//   * owner of each permutation position = a max-scan over the positions where segments start;
+//   * child class (n1..n4 of DivideNode, :527-541) of every key of a dividing node; four
+//     exclusive scans of the one-hot classes give each key's rank among its siblings, i.e. a
+//     stable in-place 4-way partition of the parent's segment (the children's vKeys orders);
+//   * the new list: push_front of the non-empty children of the dividing nodes in processing
+//     order (the last processed parent's children first, each group n4 n3 n2 n1), then the
+//     surviving nodes in their old order -- two scans over the nodes;
+//   * the focused loop processes vPrevSizeAndPointerToNode in descending (size, creation) order
+//     (pointer-order model, oracle/fast.c) and stops after the division that reaches N nodes: a
+//     scan of (children - 1) in processing order finds that division.
+// The strongest key of each final node (strict >, first in vKeys order, :778-794) is the output.
+struct OctNode {
+  int x0, y0, x1, y1;  // UL = (x0, y0), BR = (x1, y1)
+  int beg, end;        // segment of perm
+  int cre;             // creation order (pointer-order model)
+  int pend;            // in vSizeAndPointerToNode (a child with > 1 key created by the last pass)
+};
+
+struct OctLevel {
+  int N, n_ini, node_cap, key_cap;
+  int key_base, node_base, cell_begin, cell_end;
+  int wd, ht;          // maxX - minX, maxY - minY
+  float hx;            // (maxX - minX) / nIni
+  float size;          // PATCH_SIZE * mvScaleFactor[l] truncated to int (:881)
+  float scale;         // mvScaleFactor[l]
+};
+
+struct OctArgs {
+  OctLevel lv[LORB_MAX_LEVELS];
+  int n_levels;
+  const FastCell* cells;
+  const int* cell_cnt;
+  const float *fx, *fy, *fr;         // FAST output (cell slots)
+  float *kx, *ky, *kr;               // compact keys per level (key_base)
+  int *perm, *perm2, *cls, *own, *hd;
+  lorb::I4* ex;                      // key_cap + 1 per level: key_base + l
+  OctNode *na, *nb;                  // two node buffers (node_base)
+  int *act, *rank, *ech, *tmp, *surv;
+  lorb::I4* cnt;
+  int* out_key;                      // kept key per final node (node_base)
+  int* out_cnt;                      // nodes per level, -1: failure (capacity / iteration cap)
+  int* trace;                        // diagnostics (nullable): per level 8 ints per pass, 64 passes
+};
+
+constexpr int kOctThreads = 1024;
+constexpr int kOctMaxPasses = 1 << 14;
+constexpr int kOctKeyChunk = 2048;
+
+__device__ __forceinline__ int oct_class(float x, float y, const OctNode& nd) {
+  const int mx = nd.x0 + (int)ceilf((float)(nd.x1 - nd.x0) / 2);  // DivideNode halfX / halfY (:498-499)
+  const int my = nd.y0 + (int)ceilf((float)(nd.y1 - nd.y0) / 2);
+  if (x < (float)mx) return y < (float)my ? 0 : 2;
+  return y < (float)my ? 1 : 3;
+}
+
+__device__ __forceinline__ OctNode oct_child(const OctNode& p, int c, int beg, int n, int cre) {
+  const int mx = p.x0 + (int)ceilf((float)(p.x1 - p.x0) / 2);
+  const int my = p.y0 + (int)ceilf((float)(p.y1 - p.y0) / 2);
+  OctNode r;
+  r.x0 = (c & 1) ? mx : p.x0;
+  r.x1 = (c & 1) ? p.x1 : mx;
+  r.y0 = (c & 2) ? my : p.y0;
+  r.y1 = (c & 2) ? p.y1 : my;
+  r.beg = beg; r.end = beg + n; r.cre = cre; r.pend = n > 1;
+  return r;
+}
+
+// in-place exclusive scan of a[0, n) by the whole workgroup (chunked); returns the total
+__device__ int oct_scan(int* a, int n, int* wsum) {
+  const int t = threadIdx.x, per = (n + kOctThreads - 1) / kOctThreads;
+  const int b = min(n, t * per), e = min(n, b + per);
+  int s = 0;
+  for (int i = b; i < e; i++) s += a[i];
+  int tot;
+  int pre = lorb::block_excl_scan<kOctThreads>(s, wsum, &tot);
+  for (int i = b; i < e; i++) { const int v = a[i]; a[i] = pre; pre += v; }
+  __syncthreads();
+  return tot;
+}
+
+__global__ __launch_bounds__(kOctThreads) void k_orb_octree(OctArgs A) {
+  __shared__ int wsum[kOctThreads / 64];
+  __shared__ lorb::I4 wsum4[kOctThreads / 64];
+  __shared__ int s_L, s_mode, s_state, s_cm, s_E;
+  __shared__ long long s_key[kOctKeyChunk];
+  const int l = blockIdx.x, t = threadIdx.x;
+  const OctLevel V = A.lv[l];
+  float* kx = A.kx + V.key_base;
+  float* ky = A.ky + V.key_base;
+  float* kr = A.kr + V.key_base;
+  int* perm = A.perm + V.key_base;
+  int* perm2 = A.perm2 + V.key_base;
+  int* cls = A.cls + V.key_base;
+  int* own = A.own + V.key_base;
+  int* hd = A.hd + V.key_base;
+  lorb::I4* ex = A.ex + V.key_base + l;
+  OctNode* cur = A.na + V.node_base;
+  OctNode* nxt = A.nb + V.node_base;
+  int* act = A.act + V.node_base;
+  int* rank = A.rank + V.node_base;
+  int* ech = A.ech + V.node_base;
+  int* tmp = A.tmp + V.node_base;
+  int* surv = A.surv + V.node_base;
+  lorb::I4* cnt = A.cnt + V.node_base;
+
+  // 1. vToDistributeKeys: the level's cells in row-major order, FAST order inside (:827-872)
+  int n = 0;
+  for (int base = V.cell_begin; base < V.cell_end; base += kOctThreads) {
+    const int c = base + t;
+    const int v = c < V.cell_end ? A.cell_cnt[c] : 0;
+    int tot;
+    const int e0 = lorb::block_excl_scan<kOctThreads>(v, wsum, &tot);
+    if (c < V.cell_end && n + e0 + v <= V.key_cap) {
+      const int ob = A.cells[c].out_base;
+      for (int q = 0; q < v; q++) {
+        kx[n + e0 + q] = A.fx[ob + q]; ky[n + e0 + q] = A.fy[ob + q]; kr[n + e0 + q] = A.fr[ob + q];
+      }
+    }
+    n += tot;
+  }
+  __syncthreads();  // the keys written above are read by other threads below
+  if (n > V.key_cap) { if (t == 0) A.out_cnt[l] = -1; return; }
+  if (n == 0) { if (t == 0) A.out_cnt[l] = 0; return; }
+  const int per = (n + kOctThreads - 1) / kOctThreads;
+  const int pb = min(n, t * per), pe = min(n, pb + per);
+
+  // 2. initial nodes (:575-609): keys bucketed by x / hX, stable; empty nodes erased
+  {
+    lorb::I4 loc = {{0, 0, 0, 0}};
+    for (int p = pb; p < pe; p++) {
+      const int b = min((int)(kx[p] / V.hx), V.n_ini - 1);
+      cls[p] = b;
+      loc.v[b] += 1;
+    }
+    lorb::I4 tot;
+    lorb::I4 run = lorb::block_excl_scan4<kOctThreads>(loc, wsum4, &tot);
+    int start[4] = {0, tot.v[0], tot.v[0] + tot.v[1], tot.v[0] + tot.v[1] + tot.v[2]};
+    for (int p = pb; p < pe; p++) {
+      const int b = cls[p];
+      perm[start[b] + run.v[b]++] = p;
+    }
+    if (t == 0) {
+      int L = 0, beg = 0;
+      for (int b = 0; b < V.n_ini; b++) {
+        const int k = tot.v[b];
+        if (k > 0) {
+          OctNode nd;
+          nd.x0 = (int)(V.hx * (float)b); nd.x1 = (int)(V.hx * (float)(b + 1)); nd.y0 = 0; nd.y1 = V.ht;
+          nd.beg = beg; nd.end = beg + k; nd.cre = b; nd.pend = 0;
+          cur[L++] = nd;
+        }
+        beg += k;
+      }
+      s_L = L; s_mode = 0; s_state = 0;
+    }
+    __syncthreads();
+  }
+
+  // 3. division passes (:619-772)
+  for (int pass = 0;; pass++) {
+    const int L = s_L, mode = s_mode;  // mode 0: main loop pass, 1: focused-loop iteration
+    if (s_state != 0) break;
+    if (pass >= kOctMaxPasses) { if (t == 0) A.out_cnt[l] = -1; return; }
+    // A. dividing candidates; segment heads
+    for (int i = t; i < L; i += kOctThreads) {
+      const OctNode nd = cur[i];
+      act[i] = mode == 0 ? (nd.end - nd.beg >= 2) : nd.pend;
+    }
+    for (int p = pb; p < pe; p++) hd[p] = -1;
+    __syncthreads();
+    for (int i = t; i < L; i += kOctThreads) hd[cur[i].beg] = i;
+    __syncthreads();
+    // B. owner of every position (last segment head at or before it), child class, class scans
+    {
+      int m = -1;
+      for (int p = pb; p < pe; p++) m = hd[p] >= 0 ? p : m;
+      int run = lorb::block_excl_max<kOctThreads>(m, -1, wsum);
+      lorb::I4 loc = {{0, 0, 0, 0}};
+      for (int p = pb; p < pe; p++) {
+        run = hd[p] >= 0 ? p : run;
+        const int o = hd[run];
+        own[p] = o;
+        int c = -1;
+        if (act[o]) {
+          const int k = perm[p];
+          c = oct_class(kx[k], ky[k], cur[o]);
+          loc.v[c] += 1;
+        }
+        cls[p] = c;
+      }
+      lorb::I4 tot;
+      lorb::I4 r4 = lorb::block_excl_scan4<kOctThreads>(loc, wsum4, &tot);
+      for (int p = pb; p < pe; p++) {
+        ex[p] = r4;
+        const int c = cls[p];
+        if (c >= 0) r4.v[c] += 1;
+      }
+      if (t == kOctThreads - 1) ex[n] = tot;
+    }
+    __syncthreads();
+    // C. children per dividing node; processing order
+    for (int i = t; i < L; i += kOctThreads) {
+      if (!act[i]) { ech[i] = 0; continue; }
+      const OctNode nd = cur[i];
+      const lorb::I4 a = ex[nd.beg], b = ex[nd.end];
+      lorb::I4 k;
+      int e = 0;
+      for (int q = 0; q < 4; q++) { k.v[q] = b.v[q] - a.v[q]; e += k.v[q] > 0; }
+      cnt[i] = k;
+      ech[i] = e;
+    }
+    if (mode == 0) {
+      for (int i = t; i < L; i += kOctThreads) tmp[i] = act[i];
+      __syncthreads();
+      oct_scan(tmp, L, wsum);
+      for (int i = t; i < L; i += kOctThreads) rank[i] = tmp[i];
+    } else {  // descending (size, creation): sort(vPrev...) then j from the back (:717-718)
+      // pending nodes as (size << 32 | creation) keys, staged in LDS chunk by chunk
+      for (int i = t; i < L; i += kOctThreads) rank[i] = 0;
+      for (int c0 = 0; c0 < L; c0 += kOctKeyChunk) {
+        const int cn = min(kOctKeyChunk, L - c0);
+        __syncthreads();
+        for (int j = t; j < cn; j += kOctThreads) {
+          const OctNode nd = cur[c0 + j];
+          s_key[j] = act[c0 + j] ? ((long long)(nd.end - nd.beg) << 32) | (unsigned)nd.cre : -1ll;
+        }
+        __syncthreads();
+        for (int i = t; i < L; i += kOctThreads) {
+          if (!act[i]) continue;
+          const long long ki = ((long long)(cur[i].end - cur[i].beg) << 32) | (unsigned)cur[i].cre;
+          int r = 0;
+          for (int j = 0; j < cn; j++) r += s_key[j] > ki;
+          rank[i] += r;
+        }
+      }
+    }
+    __syncthreads();
+    // D. children counts in processing order; the focused loop's break (:763-764)
+    for (int i = t; i < L; i += kOctThreads) if (act[i]) tmp[rank[i]] = ech[i];
+    __syncthreads();
+    int n_act = 0;
+    {
+      int s = 0;
+      for (int i = t; i < L; i += kOctThreads) s += act[i];
+      int tot;
+      (void)lorb::block_excl_scan<kOctThreads>(s, wsum, &tot);
+      n_act = tot;
+    }
+    // inclusive prefix of children in processing order -> surv (as scratch), then the break
+    for (int r = t; r < n_act; r += kOctThreads) surv[r] = tmp[r];
+    __syncthreads();
+    (void)oct_scan(surv, n_act, wsum);  // surv[r] = exclusive prefix in processing order
+    if (t == 0) s_cm = n_act;
+    __syncthreads();
+    if (mode == 1) {
+      for (int r = t; r < n_act; r += kOctThreads) {
+        const int live = L + (surv[r] + tmp[r]) - (r + 1);  // after processing r
+        if (live >= V.N) atomicMin(&s_cm, r + 1);
+      }
+    }
+    __syncthreads();
+    if (t == 0) s_E = s_cm > 0 ? surv[s_cm - 1] + tmp[s_cm - 1] : 0;
+    __syncthreads();
+    const int cm = s_cm, E = s_E;
+    // E. survivors (not divided this pass) keep their order after the new children
+    for (int i = t; i < L; i += kOctThreads) {
+      const bool div = act[i] && rank[i] < cm;
+      act[i] = div;
+      tmp[i] = div ? 0 : 1;
+    }
+    __syncthreads();
+    const int n_surv = oct_scan(tmp, L, wsum);  // tmp[i] = survivor rank
+    const int newL = E + n_surv;
+    if (newL > V.node_cap) { if (t == 0) A.out_cnt[l] = -1; return; }
+    // F. new permutation (stable partition of the divided segments) and the new node list
+    for (int p = pb; p < pe; p++) {
+      const int o = own[p];
+      if (act[o]) {
+        const OctNode nd = cur[o];
+        const int c = cls[p];
+        const lorb::I4 k = cnt[o];
+        int off = 0;
+        for (int q = 0; q < c; q++) off += k.v[q];
+        perm2[nd.beg + off + (ex[p].v[c] - ex[nd.beg].v[c])] = perm[p];
+      } else {
+        perm2[p] = perm[p];
+      }
+    }
+    int n_pend = 0;
+    for (int i = t; i < L; i += kOctThreads) {
+      const OctNode nd = cur[i];
+      if (!act[i]) {
+        OctNode s = nd;
+        s.pend = 0;
+        nxt[E + tmp[i]] = s;
+        continue;
+      }
+      const int r = rank[i];
+      const int incl = surv[r] + ech[i];
+      int slot = E - incl;  // children of the last processed parent come first
+      const lorb::I4 k = cnt[i];
+      int beg = nd.beg + k.v[0] + k.v[1] + k.v[2] + k.v[3];
+      for (int c = 3; c >= 0; c--) {  // push_front n1, n2, n3, n4 -> the list reads n4 n3 n2 n1
+        const int kc = k.v[c];
+        beg -= kc;
+        if (kc == 0) continue;
+        nxt[slot++] = oct_child(nd, c, beg, kc, 4 * r + c);
+        n_pend += kc > 1;
+      }
+    }
+    {
+      int tot;
+      (void)lorb::block_excl_scan<kOctThreads>(n_pend, wsum, &tot);
+      n_pend = tot;
+    }
+    __syncthreads();
+    // G. termination (:703-707, :767-768)
+    if (t == 0) {
+      if (A.trace && pass < 64) {
+        int* tr = A.trace + (l * 64 + pass) * 72;
+        tr[0] = L; tr[1] = mode; tr[2] = n_act; tr[3] = cm; tr[4] = E; tr[5] = n_surv; tr[6] = newL; tr[7] = n_pend;
+        for (int q = 0; q < 16 && q < newL; q++) {
+          tr[8 + 4 * q] = nxt[q].beg; tr[9 + 4 * q] = nxt[q].end; tr[10 + 4 * q] = nxt[q].x0; tr[11 + 4 * q] = nxt[q].y0;
+        }
+      }
+      int state = 0, m = mode;
+      if (newL >= V.N || newL == L) state = 1;
+      else if (mode == 0 && newL + 3 * n_pend > V.N) m = 1;
+      s_state = state; s_mode = m; s_L = newL;
+    }
+    {
+      int* sw = perm; perm = perm2; perm2 = sw;
+      OctNode* nw = cur; cur = nxt; nxt = nw;
+    }
+    __syncthreads();
+  }
+  // 4. the strongest key of each node (:776-794)
+  const int L = s_L;
+  for (int i = t; i < L; i += kOctThreads) {
+    const OctNode nd = cur[i];
+    int best = perm[nd.beg];
+    float m = kr[best];
+    for (int q = nd.beg + 1; q < nd.end; q++) {
+      const int k = perm[q];
+      if (kr[k] > m) { best = k; m = kr[k]; }
+    }
+    A.out_key[V.node_base + i] = best;
+  }
+  if (t == 0) A.out_cnt[l] = L;
+}
+
+// Gathers the per-level results in level order: level coordinates, octave, size, response and the
+// level-0 (scaled) coordinates (:881-891, :1141-1147); level_off[n_levels + 1] and *n_total (-1
+// when a level failed).
+__global__ __launch_bounds__(256) void k_orb_gather(OctArgs A, int cap, float* __restrict__ lx, float* __restrict__ ly,
+                                                    float* __restrict__ sx, float* __restrict__ sy,
+                                                    int* __restrict__ oct, float* __restrict__ size,
+                                                    float* __restrict__ resp, int* __restrict__ level_off,
+                                                    int* __restrict__ n_total) {
+  __shared__ int off[LORB_MAX_LEVELS + 1];
+  __shared__ int bad;
+  if (threadIdx.x == 0) {
+    int s = 0, b = 0;
+    for (int l = 0; l < A.n_levels; l++) {
+      off[l] = s;
+      const int c = A.out_cnt[l];
+      b |= c < 0;
+      s += c < 0 ? 0 : c;
+    }
+    off[A.n_levels] = s;
+    bad = b || s > cap;
+    if (blockIdx.x == 0) {
+      for (int l = 0; l <= A.n_levels; l++) level_off[l] = off[l];
+      *n_total = bad ? -1 : s;
+    }
+  }
+  __syncthreads();
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (bad || i >= off[A.n_levels]) return;
+  int l = 0;
+  while (l + 1 < A.n_levels && i >= off[l + 1]) ++l;
+  const OctLevel& V = A.lv[l];
+  const int k = A.out_key[V.node_base + i - off[l]];
+  const float x = A.kx[V.key_base + k] + (float)kBorder, y = A.ky[V.key_base + k] + (float)kBorder;
+  lx[i] = x; ly[i] = y;
+  sx[i] = l != 0 ? x * V.scale : x;
+  sy[i] = l != 0 ? y * V.scale : y;
+  oct[i] = l; size[i] = V.size; resp[i] = A.kr[V.key_base + k];
+}
+
+// Host plan of the keypoint stage: cells, capacities and the octree arguments (device pointers are
+// filled by orb_alloc).
+struct OrbPlan {
+  std::vector<FastCell> cells;
+  int fast_cap = 0, key_total = 0, node_total = 0, out_cap = 0;
+  OctArgs A{};
+};
+
+int orb_plan(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired, const float* sf, OrbPlan* P) {
+  P->cells.clear();
+  P->fast_cap = P->key_total = P->node_total = P->out_cap = 0;
+  std::memset(&P->A, 0, sizeof(P->A));
+  P->A.n_levels = pyr->n_levels;
+  std::vector<int> cells;
+  for (int l = 0; l < pyr->n_levels; l++) {
+    int nc, nr;
+    const int ncl = orb_cells(pyr->rows[l], pyr->cols[l], cells, &nc, &nr);
+    if (ncl < 0) return lorb::set_error(ctx, LORB_E_INVALID, "level %d (%d x %d) too small for one 30-pixel cell", l,
+                                        pyr->rows[l], pyr->cols[l]);
+    OctLevel& V = P->A.lv[l];
+    V.cell_begin = (int)P->cells.size();
+    int kcap = 0;
+    for (int c = 0; c < ncl; c++) {
+      const int* g = &cells[6 * (size_t)c];
+      if (g[2] <= 0 || g[3] <= 0) continue;
+      if (g[2] > kCellMax || g[3] > kCellMax)
+        return lorb::set_error(ctx, LORB_E_INVALID, "level %d cell %d x %d exceeds the LDS tile", l, g[2], g[3]);
+      const int cap = ((g[2] + 1) / 2) * ((g[3] + 1) / 2);  // 3x3 maxima are never 8-adjacent
+      P->cells.push_back(FastCell{l, g[0], g[1], g[2], g[3], P->fast_cap, g[4], g[5]});
+      P->fast_cap += cap;
+      kcap += cap;
+    }
+    V.cell_end = (int)P->cells.size();
+    const int minX = kBorder, maxX = pyr->cols[l] - kBorder, minY = kBorder, maxY = pyr->rows[l] - kBorder;
+    V.wd = maxX - minX; V.ht = maxY - minY;
+    V.n_ini = (int)std::round((float)(maxX - minX) / (float)(maxY - minY));  // :559
+    if (V.n_ini < 1 || V.n_ini > 4)
+      return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "level %d: %d initial quadtree nodes (1..4 supported)", l, V.n_ini);
+    V.hx = (float)(maxX - minX) / (float)V.n_ini;
+    V.N = std::max(0, (int)n_desired[l]);
+    V.node_cap = 4 * std::max(V.N, 4) + 16;
+    V.key_cap = std::max(kcap, 1);
+    V.key_base = P->key_total;
+    V.node_base = P->node_total;
+    V.size = (float)(int)(31 * sf[l]);
+    V.scale = sf[l];
+    P->key_total += V.key_cap;
+    P->node_total += V.node_cap;
+  }
+  P->out_cap = P->node_total;
+  return LORB_OK;
+}
+
+// allocates the scratch of a plan (slots S_ORB + 20 ..) and fills the device pointers of P->A
+int orb_alloc(lorb_ctx* ctx, OrbPlan* P, FastCell** d_cells, int** d_cnt) {
+  OctArgs& A = P->A;
+  const size_t K = (size_t)std::max(P->key_total, 1), NN = (size_t)std::max(P->node_total, 1);
+  const size_t F = (size_t)std::max(P->fast_cap, 1);
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 20, P->cells.data(), P->cells.size(), d_cells));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 21, std::max<size_t>(P->cells.size(), 1), d_cnt));
+  float *fx, *fy, *fr, *kx, *ky, *kr;
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 22, F, &fx));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 23, F, &fy));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 24, F, &fr));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 25, K, &kx));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 26, K, &ky));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 27, K, &kr));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 28, K, &A.perm));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 29, K, &A.perm2));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 30, K, &A.cls));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 31, K, &A.own));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 32, K, &A.hd));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 33, K + LORB_MAX_LEVELS, &A.ex));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 34, NN, &A.na));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 35, NN, &A.nb));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 36, NN, &A.act));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 37, NN, &A.rank));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 38, NN, &A.ech));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 39, NN, &A.tmp));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 40, NN, &A.surv));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 41, NN, &A.cnt));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 42, NN, &A.out_key));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 43, (size_t)LORB_MAX_LEVELS, &A.out_cnt));
+  A.cells = *d_cells; A.cell_cnt = *d_cnt;
+  A.fx = fx; A.fy = fy; A.fr = fr; A.kx = kx; A.ky = ky; A.kr = kr;
+  return LORB_OK;
+}
+
+// FAST cells + DistributeOctTree of every level, enqueued on the ctx stream (device pyramid)
+int enqueue_keypoints(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const uint8_t* d_data, OrbPlan* P, int ini_th,
+                      int min_th) {
+  FastCell* dcells;
+  int* dcnt;
+  LORB_TRY(orb_alloc(ctx, P, &dcells, &dcnt));
+  OrbPyr Q{};
+  for (int l = 0; l < pyr->n_levels; l++) { Q.offset[l] = pyr->offset[l]; Q.step[l] = pyr->step[l]; }
+  if (!P->cells.empty())
+    hipLaunchKernelGGL(k_orb_fast, dim3((unsigned)P->cells.size()), dim3(kFastThreads), 0, ctx->stream, d_data, Q,
+                       dcells, ini_th, min_th, const_cast<float*>(P->A.fx), const_cast<float*>(P->A.fy),
+                       const_cast<float*>(P->A.fr), dcnt);
+  hipLaunchKernelGGL(k_orb_octree, dim3(pyr->n_levels), dim3(kOctThreads), 0, ctx->stream, P->A);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -541,7 +1042,7 @@ int lorb_orb_describe_dev(lorb_ctx* ctx, const lorb_image_pyramid* d_pyr, int32_
   LORB_TRY(check_orb(ctx, d_pyr, n));
   if (n > 0 && (!d_x || !d_y || !d_level || !d_pattern || !d_angle || !d_desc))
     return lorb::set_error(ctx, LORB_E_INVALID, "null keypoint / pattern / output array");
-  return enqueue_orb(ctx, d_pyr, d_pyr->data, n, d_x, d_y, d_level, d_pattern, d_angle, d_desc);
+  return enqueue_orb(ctx, d_pyr, d_pyr->data, n, nullptr, d_x, d_y, d_level, d_pattern, d_angle, d_desc);
 }
 
 int lorb_orb_describe(lorb_ctx* ctx, const lorb_image_pyramid* pyr, int32_t n, const float* x, const float* y,
@@ -572,205 +1073,12 @@ int lorb_orb_describe(lorb_ctx* ctx, const lorb_image_pyramid* pyr, int32_t n, c
   LORB_TRY(lorb::upload_t(ctx, S_ORB + 5, pattern, (size_t)1024, &dp));
   LORB_TRY(lorb::scratch_t(ctx, S_ORB + 6, (size_t)std::max(n, 1), &dang));
   LORB_TRY(lorb::scratch_t(ctx, S_ORB + 7, (size_t)std::max(n, 1) * 32, &ddesc));
-  LORB_TRY(enqueue_orb(ctx, pyr, dd, n, dx, dy, dl, dp, dang, ddesc));
+  LORB_TRY(enqueue_orb(ctx, pyr, dd, n, nullptr, dx, dy, dl, dp, dang, ddesc));
   if (n > 0) {
     LORB_HIP(ctx, hipMemcpyAsync(angle, dang, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
     LORB_HIP(ctx, hipMemcpyAsync(desc, ddesc, (size_t)32 * n, hipMemcpyDeviceToHost, ctx->stream));
   }
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  return LORB_OK;
-}
-
-
-int lorb_orb_fast_cells(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired, int32_t ini_th,
-                        int32_t min_th, int32_t max_keypoints, float* x, float* y, float* response, int32_t max_cells,
-                        int32_t* cell_base, int32_t* cell_off, int32_t* n_keypoints) {
-  if (!ctx) return LORB_E_INVALID;
-  LORB_TRY(check_orb(ctx, pyr, 0));
-  if (!n_desired || !cell_base || !cell_off || !n_keypoints || max_keypoints < 0 || max_cells < 0)
-    return lorb::set_error(ctx, LORB_E_INVALID, "null argument");
-  const float ratio = (float)pyr->cols[0] / pyr->rows[0];
-  std::vector<FastCell> hc;       // launched cells
-  std::vector<int> slot;          // launched cell -> global cell index
-  int nc = 0, cap_total = 0;
-  std::vector<int> cells;
-  for (int l = 0; l < pyr->n_levels; l++) {
-    const int ncl = orb_cells(pyr->rows[l], pyr->cols[l], n_desired[l], ratio, cells);
-    if (ncl < 0) return lorb::set_error(ctx, LORB_E_INVALID, "level %d: degenerate cell grid (%d features)", l, n_desired[l]);
-    if (nc + ncl > max_cells) return lorb::set_error(ctx, LORB_E_INVALID, "more than max_cells = %d cells", max_cells);
-    cell_base[l] = nc;
-    for (int c = 0; c < ncl; c++) {
-      const int* g = &cells[4 * (size_t)c];
-      if (g[2] <= 0 || g[3] <= 0) continue;
-      if (g[0] < 0 || g[1] < 0 || g[0] + g[2] > pyr->cols[l] || g[1] + g[3] > pyr->rows[l])
-        return lorb::set_error(ctx, LORB_E_INVALID, "level %d cell %d outside the image", l, c);
-      if (3 * g[2] * g[3] > 96 * 1024)
-        return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "cell %d x %d exceeds the LDS tile", g[2], g[3]);
-      hc.push_back(FastCell{l, g[0], g[1], g[2], g[3], cap_total});
-      slot.push_back(nc + c);
-      cap_total += ((g[2] + 1) / 2) * ((g[3] + 1) / 2);  // 3x3 maxima are never 8-adjacent
-    }
-    nc += ncl;
-  }
-  cell_base[pyr->n_levels] = nc;
-  OrbPyr P{};
-  for (int l = 0; l < pyr->n_levels; l++) { P.offset[l] = pyr->offset[l]; P.step[l] = pyr->step[l]; }
-  uint8_t* dd;
-  FastCell* dcells;
-  float *dx, *dy, *dr;
-  int* dcnt;
-  LORB_TRY(lorb::upload_t(ctx, S_ORB + 1, pyr->data, (size_t)pyr_extent(pyr), &dd));
-  LORB_TRY(lorb::upload_t(ctx, S_ORB + 2, hc.data(), hc.size(), &dcells));
-  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 3, (size_t)std::max(cap_total, 1), &dx));
-  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 4, (size_t)std::max(cap_total, 1), &dy));
-  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 5, (size_t)std::max(cap_total, 1), &dr));
-  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 6, std::max<size_t>(hc.size(), 1), &dcnt));
-  int max_lds = 0;
-  for (const FastCell& f : hc) max_lds = std::max(max_lds, 3 * f.w * f.h);
-  if (!hc.empty())
-    hipLaunchKernelGGL(k_orb_fast, dim3((unsigned)hc.size()), dim3(1024), (size_t)max_lds, ctx->stream, dd, P,
-                       dcells, ini_th, min_th, dx, dy, dr, dcnt);
-  LORB_CHECK_LAUNCH(ctx);
-  std::vector<int> cnt(hc.size());
-  std::vector<float> hx(cap_total), hy(cap_total), hr(cap_total);
-  if (!hc.empty()) {
-    LORB_HIP(ctx, hipMemcpyAsync(cnt.data(), dcnt, sizeof(int) * hc.size(), hipMemcpyDeviceToHost, ctx->stream));
-    LORB_HIP(ctx, hipMemcpyAsync(hx.data(), dx, sizeof(float) * cap_total, hipMemcpyDeviceToHost, ctx->stream));
-    LORB_HIP(ctx, hipMemcpyAsync(hy.data(), dy, sizeof(float) * cap_total, hipMemcpyDeviceToHost, ctx->stream));
-    LORB_HIP(ctx, hipMemcpyAsync(hr.data(), dr, sizeof(float) * cap_total, hipMemcpyDeviceToHost, ctx->stream));
-  }
-  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  // compact in level / cell order; cell_off of level l, cell c at cell_base[l] + l + c
-  std::vector<int> per_cell(nc, 0), src_of(nc, -1);
-  for (size_t k = 0; k < hc.size(); k++) { per_cell[slot[k]] = cnt[k]; src_of[slot[k]] = (int)k; }
-  int nk = 0;
-  for (int l = 0; l < pyr->n_levels; l++) {
-    const int b = cell_base[l], e = cell_base[l + 1];
-    for (int g = b; g < e; g++) {
-      cell_off[g + l] = nk;
-      const int k = src_of[g];
-      if (k >= 0) {
-        for (int q = 0; q < cnt[k]; q++) {
-          if (nk + q < max_keypoints) {
-            x[nk + q] = hx[hc[k].out_base + q]; y[nk + q] = hy[hc[k].out_base + q]; response[nk + q] = hr[hc[k].out_base + q];
-          }
-        }
-        nk += cnt[k];
-      }
-    }
-    cell_off[e + l] = nk;
-  }
-  *n_keypoints = nk;
-  if (nk > max_keypoints)
-    return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints exceed max_keypoints = %d", nk, max_keypoints);
-  return LORB_OK;
-}
-
-
-// Detection + retention (src/ORBextractor.cpp:898-1067).  The FAST cells run on the device
-// (lorb_orb_fast_cells); the retention is sequential bookkeeping over a few hundred keypoints per
-// cell and runs here on the host with the very std::nth_element / std::partition that
-// KeyPointsFilter::retainBest (OpenCV 3.1) calls, so equal responses are resolved exactly as in
-// the reference build.
-namespace {
-struct OrbKp {
-  float x, y, size, resp;
-  int octave;
-};
-void retain_best(std::vector<OrbKp>& k, int n_points) {  // KeyPointsFilter::retainBest
-  if (n_points >= 0 && k.size() > (size_t)n_points) {
-    if (n_points == 0) { k.clear(); return; }
-    std::nth_element(k.begin(), k.begin() + n_points, k.end(),
-                     [](const OrbKp& a, const OrbKp& b) { return a.resp > b.resp; });
-    const float amb = k[n_points - 1].resp;
-    auto e = std::partition(k.begin() + n_points, k.end(), [amb](const OrbKp& a) { return a.resp >= amb; });
-    k.resize(e - k.begin());
-  }
-}
-}  // namespace
-
-int lorb_orb_detect(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired,
-                    const float* scale_factors, int32_t ini_th, int32_t min_th, int32_t max_keypoints, float* x,
-                    float* y, int32_t* octave, float* size, float* response, int32_t* level_off,
-                    int32_t* n_keypoints) {
-  if (!ctx) return LORB_E_INVALID;
-  LORB_TRY(check_orb(ctx, pyr, 0));
-  if (!n_desired || !scale_factors || !level_off || !n_keypoints || max_keypoints < 0)
-    return lorb::set_error(ctx, LORB_E_INVALID, "null argument");
-  const int L = pyr->n_levels;
-  int max_cells = 0, cap = 0;
-  const float ratio = (float)pyr->cols[0] / pyr->rows[0];
-  std::vector<int> cells;
-  for (int l = 0; l < L; l++) {
-    const int ncl = orb_cells(pyr->rows[l], pyr->cols[l], n_desired[l], ratio, cells);
-    if (ncl < 0) return lorb::set_error(ctx, LORB_E_INVALID, "level %d: degenerate cell grid (%d features)", l, n_desired[l]);
-    max_cells += ncl;
-    for (int c = 0; c < ncl; c++) cap += ((cells[4 * c + 2] + 1) / 2) * ((cells[4 * c + 3] + 1) / 2);
-  }
-  std::vector<float> fx(cap + 1), fy(cap + 1), fr(cap + 1);
-  std::vector<int32_t> base(L + 1), coff(max_cells + L + 1);
-  int32_t nf = 0;
-  LORB_TRY(lorb_orb_fast_cells(ctx, pyr, n_desired, ini_th, min_th, cap, fx.data(), fy.data(), fr.data(), max_cells,
-                               base.data(), coff.data(), &nf));
-  int out = 0;
-  for (int l = 0; l < L; l++) {
-    level_off[l] = out;
-    const int nd = n_desired[l];
-    const int levelCols = (int)std::sqrt((float)nd / (5 * ratio));
-    const int levelRows = (int)(ratio * levelCols);
-    const int nCells = levelRows * levelCols;
-    orb_cells(pyr->rows[l], pyr->cols[l], nd, ratio, cells);
-    const int nfeaturesCell = (int)std::ceil((float)nd / nCells);
-    std::vector<int> nToRetain(nCells, 0), nTotal(nCells, 0);
-    std::vector<char> bNoMore(nCells, 0);
-    int nNoMore = 0, nToDistribute = 0;
-    const int32_t* co = coff.data() + base[l] + l;
-    for (int c = 0; c < nCells; c++) {  // :983-1003
-      if (cells[4 * c + 2] <= 0 || cells[4 * c + 3] <= 0) continue;
-      const int nKeys = co[c + 1] - co[c];
-      nTotal[c] = nKeys;
-      if (nKeys > nfeaturesCell) { nToRetain[c] = nfeaturesCell; bNoMore[c] = 0; }
-      else { nToRetain[c] = nKeys; nToDistribute += nfeaturesCell - nKeys; bNoMore[c] = 1; nNoMore++; }
-    }
-    while (nToDistribute > 0 && nNoMore < nCells) {  // :1010-1035
-      const int nNew = (int)(nfeaturesCell + std::ceil((float)nToDistribute / (nCells - nNoMore)));
-      nToDistribute = 0;
-      for (int c = 0; c < nCells; c++)
-        if (!bNoMore[c]) {
-          if (nTotal[c] > nNew) { nToRetain[c] = nNew; bNoMore[c] = 0; }
-          else { nToRetain[c] = nTotal[c]; nToDistribute += nNew - nTotal[c]; bNoMore[c] = 1; nNoMore++; }
-        }
-    }
-    const int scaledPatchSize = (int)(31 * scale_factors[l]);  // PATCH_SIZE * mvScaleFactor (:1040)
-    std::vector<OrbKp> level;
-    std::vector<OrbKp> cell;
-    for (int c = 0; c < nCells; c++) {  // :1043-1060
-      cell.clear();
-      for (int k = co[c]; k < co[c + 1]; k++)
-        cell.push_back(OrbKp{fx[k] - (float)cells[4 * c], fy[k] - (float)cells[4 * c + 1], 7.f, fr[k], 0});
-      retain_best(cell, nToRetain[c]);
-      if ((int)cell.size() > nToRetain[c]) cell.resize(nToRetain[c]);
-      for (OrbKp& kp : cell) {
-        kp.x += (float)cells[4 * c]; kp.y += (float)cells[4 * c + 1];
-        kp.octave = l; kp.size = (float)scaledPatchSize;
-        level.push_back(kp);
-      }
-    }
-    if ((int)level.size() > nd) {  // :1063-1067
-      retain_best(level, nd);
-      level.resize(nd);
-    }
-    for (const OrbKp& kp : level) {
-      if (out < max_keypoints) {
-        x[out] = kp.x; y[out] = kp.y; octave[out] = kp.octave; size[out] = kp.size; response[out] = kp.resp;
-      }
-      out++;
-    }
-  }
-  level_off[L] = out;
-  *n_keypoints = out;
-  if (out > max_keypoints)
-    return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints exceed max_keypoints = %d", out, max_keypoints);
   return LORB_OK;
 }
 
@@ -812,6 +1120,258 @@ int lorb_orb_pyramid_dev(lorb_ctx* ctx, const uint8_t* d_image, int32_t rows, in
                                                (long long)out_bytes, (long long)need);
   LORB_TRY(enqueue_pyramid(ctx, d_image, rows, cols, step, *layout, d_out));
   layout->data = d_out;
+  return LORB_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// dummy n_desired for the FAST-only entry point (DistributeOctTree is not run)
+int plan_fast_only(lorb_ctx* ctx, const lorb_image_pyramid* pyr, OrbPlan* P) {
+  std::vector<int32_t> nd(pyr->n_levels, 1);
+  std::vector<float> sf(pyr->n_levels, 1.0f);
+  return orb_plan(ctx, pyr, nd.data(), sf.data(), P);
+}
+
+}  // namespace
+
+extern "C" {
+
+int lorb_orb_fast_cells(lorb_ctx* ctx, const lorb_image_pyramid* pyr, int32_t ini_th, int32_t min_th,
+                        int32_t max_keypoints, float* x, float* y, float* response, int32_t max_cells,
+                        int32_t* cell_base, int32_t* cell_off, int32_t* n_keypoints) {
+  if (!ctx) return LORB_E_INVALID;
+  LORB_TRY(check_orb(ctx, pyr, 0));
+  if (!cell_base || !cell_off || !n_keypoints || max_keypoints < 0 || max_cells < 0 || (max_keypoints > 0 && (!x || !y || !response)))
+    return lorb::set_error(ctx, LORB_E_INVALID, "null argument");
+  OrbPlan P;
+  LORB_TRY(plan_fast_only(ctx, pyr, &P));
+  FastCell* dcells;
+  int* dcnt;
+  uint8_t* dd;
+  LORB_TRY(orb_alloc(ctx, &P, &dcells, &dcnt));
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 1, pyr->data, (size_t)pyr_extent(pyr), &dd));
+  OrbPyr Q{};
+  for (int l = 0; l < pyr->n_levels; l++) { Q.offset[l] = pyr->offset[l]; Q.step[l] = pyr->step[l]; }
+  if (!P.cells.empty())
+    hipLaunchKernelGGL(k_orb_fast, dim3((unsigned)P.cells.size()), dim3(kFastThreads), 0, ctx->stream, dd, Q, dcells,
+                       ini_th, min_th, const_cast<float*>(P.A.fx), const_cast<float*>(P.A.fy),
+                       const_cast<float*>(P.A.fr), dcnt);
+  LORB_CHECK_LAUNCH(ctx);
+  const size_t nc = P.cells.size(), F = (size_t)std::max(P.fast_cap, 1);
+  std::vector<int> cnt(std::max<size_t>(nc, 1));
+  std::vector<float> hx(F), hy(F), hr(F);
+  if (nc) {
+    LORB_HIP(ctx, hipMemcpyAsync(cnt.data(), dcnt, sizeof(int) * nc, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(hx.data(), P.A.fx, sizeof(float) * F, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(hy.data(), P.A.fy, sizeof(float) * F, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(hr.data(), P.A.fr, sizeof(float) * F, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // the whole grid of every level (skipped cells hold no keypoint), level coordinates
+  int nk = 0, ng = 0;
+  size_t k = 0;
+  std::vector<int> cells;
+  for (int l = 0; l < pyr->n_levels; l++) {
+    int ncol, nrow;
+    const int ncl = orb_cells(pyr->rows[l], pyr->cols[l], cells, &ncol, &nrow);
+    if (ng + ncl > max_cells) return lorb::set_error(ctx, LORB_E_INVALID, "more than max_cells = %d cells", max_cells);
+    cell_base[l] = ng;
+    for (int c = 0; c < ncl; c++) {
+      cell_off[ng + c + l] = nk;
+      const int* g = &cells[6 * (size_t)c];
+      if (g[2] <= 0 || g[3] <= 0) continue;
+      const FastCell& fc = P.cells[k];
+      for (int q = 0; q < cnt[k]; q++, nk++)
+        if (nk < max_keypoints) {
+          x[nk] = hx[fc.out_base + q] + (float)kBorder; y[nk] = hy[fc.out_base + q] + (float)kBorder;
+          response[nk] = hr[fc.out_base + q];
+        }
+      k++;
+    }
+    ng += ncl;
+    cell_off[ng + l] = nk;
+  }
+  cell_base[pyr->n_levels] = ng;
+  *n_keypoints = nk;
+  if (nk > max_keypoints)
+    return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints exceed max_keypoints = %d", nk, max_keypoints);
+  return LORB_OK;
+}
+
+int lorb_orb_detect(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired,
+                    const float* scale_factors, int32_t ini_th, int32_t min_th, int32_t max_keypoints, float* x,
+                    float* y, int32_t* octave, float* size, float* response, int32_t* level_off,
+                    int32_t* n_keypoints) {
+  if (!ctx) return LORB_E_INVALID;
+  LORB_TRY(check_orb(ctx, pyr, 0));
+  if (!n_desired || !scale_factors || !level_off || !n_keypoints || max_keypoints < 0)
+    return lorb::set_error(ctx, LORB_E_INVALID, "null argument");
+  OrbPlan P;
+  LORB_TRY(orb_plan(ctx, pyr, n_desired, scale_factors, &P));
+  uint8_t* dd;
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 1, pyr->data, (size_t)pyr_extent(pyr), &dd));
+  LORB_TRY(enqueue_keypoints(ctx, pyr, dd, &P, ini_th, min_th));
+  const size_t cap = (size_t)std::max(P.out_cap, 1);
+  float *lx, *ly, *sx, *sy, *sz, *rs;
+  int *oc, *lo, *nt;
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 44, cap, &lx));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 45, cap, &ly));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 46, cap, &sx));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 47, cap, &sy));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 6, cap, &sz));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 7, cap, &rs));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 3, cap, &oc));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 4, (size_t)LORB_MAX_LEVELS + 1, &lo));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 5, (size_t)1, &nt));
+  hipLaunchKernelGGL(k_orb_gather, dim3(lorb::ceil_div(cap, 256)), dim3(256), 0, ctx->stream, P.A, (int)cap, lx, ly, sx,
+                     sy, oc, sz, rs, lo, nt);
+  LORB_CHECK_LAUNCH(ctx);
+  int n = 0;
+  LORB_HIP(ctx, hipMemcpyAsync(&n, nt, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(level_off, lo, sizeof(int) * (pyr->n_levels + 1), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (n < 0) return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "DistributeOctTree exceeded its node capacity");
+  *n_keypoints = n;
+  if (n > max_keypoints)
+    return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints exceed max_keypoints = %d", n, max_keypoints);
+  if (n > 0) {
+    LORB_HIP(ctx, hipMemcpyAsync(x, lx, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(y, ly, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(octave, oc, sizeof(int) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(size, sz, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(response, rs, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+// diagnostics: lorb_orb_detect with the per-pass trace of the device quadtree (8 ints per pass:
+// L, mode, dividing nodes, divided, new children, survivors, new L, pending children; 64 passes
+// per level; trace holds n_levels * 512 ints)
+int lorb_orb_debug_octree(lorb_ctx* ctx, const lorb_image_pyramid* pyr, const int32_t* n_desired,
+                          const float* scale_factors, int32_t ini_th, int32_t min_th, int32_t* trace) {
+  if (!ctx || !trace) return LORB_E_INVALID;
+  LORB_TRY(check_orb(ctx, pyr, 0));
+  OrbPlan P;
+  LORB_TRY(orb_plan(ctx, pyr, n_desired, scale_factors, &P));
+  uint8_t* dd;
+  int* dtr;
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 1, pyr->data, (size_t)pyr_extent(pyr), &dd));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 50, (size_t)pyr->n_levels * (64 * 72 + 16384), &dtr));
+  LORB_HIP(ctx, hipMemsetAsync(dtr, 0, sizeof(int) * pyr->n_levels * (64 * 72 + 16384), ctx->stream));
+  P.A.trace = dtr;
+  LORB_TRY(enqueue_keypoints(ctx, pyr, dd, &P, ini_th, min_th));
+  LORB_HIP(ctx, hipMemcpyAsync(trace, dtr, sizeof(int) * pyr->n_levels * (64 * 72 + 16384), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_orb_extract_capacity(int32_t rows, int32_t cols, int32_t n_levels, const float* scale_factors,
+                              const int32_t* n_desired, int32_t* max_keypoints, int64_t* pyramid_bytes) {
+  if (!scale_factors || !n_desired || !max_keypoints || rows < 1 || cols < 1 || n_levels < 1 || n_levels > LORB_MAX_LEVELS)
+    return LORB_E_INVALID;
+  lorb_image_pyramid L;
+  const int64_t need = pyramid_layout(rows, cols, n_levels, scale_factors, &L);
+  int cap = 0;
+  for (int l = 0; l < n_levels; l++) cap += 4 * std::max(std::max(0, (int)n_desired[l]), 4) + 16;
+  *max_keypoints = cap;
+  if (pyramid_bytes) *pyramid_bytes = need;
+  return LORB_OK;
+}
+
+// ORBextractor::operator() (src/ORBextractor.cpp:1087-1151) on the device.  d_image, d_pattern and
+// every output are device arrays; d_n (1 int) and d_level_off (n_levels + 1 ints) too.  The call
+// returns once the pyramid is built (its resize tables are host-staged); the rest runs async.
+int lorb_orb_extract_dev(lorb_ctx* ctx, const uint8_t* d_image, int32_t rows, int32_t cols, int32_t step,
+                         int32_t n_levels, const float* scale_factors, const int32_t* n_desired, int32_t ini_th,
+                         int32_t min_th, const int32_t* d_pattern, int32_t max_keypoints, uint8_t* d_pyramid,
+                         int64_t pyramid_bytes, float* d_x, float* d_y, int32_t* d_octave, float* d_size,
+                         float* d_angle, float* d_response, uint8_t* d_desc, int32_t* d_level_off, int32_t* d_n) {
+  if (!ctx) return LORB_E_INVALID;
+  if (!d_image || !scale_factors || !n_desired || !d_pattern || !d_pyramid || !d_x || !d_y || !d_octave || !d_size ||
+      !d_angle || !d_response || !d_desc || !d_level_off || !d_n || rows < 1 || cols < 1 || step < cols ||
+      n_levels < 1 || n_levels > LORB_MAX_LEVELS)
+    return lorb::set_error(ctx, LORB_E_INVALID, "bad image / level / output arguments");
+  lorb_image_pyramid pyr;
+  const int64_t need = pyramid_layout(rows, cols, n_levels, scale_factors, &pyr);
+  if (pyramid_bytes < need)
+    return lorb::set_error(ctx, LORB_E_INVALID, "pyramid buffer holds %lld bytes, %lld needed", (long long)pyramid_bytes,
+                           (long long)need);
+  OrbPlan P;
+  LORB_TRY(orb_plan(ctx, &pyr, n_desired, scale_factors, &P));
+  if (max_keypoints < P.out_cap)
+    return lorb::set_error(ctx, LORB_E_INVALID, "max_keypoints %d below the extractor's bound %d (lorb_orb_extract_capacity)",
+                           max_keypoints, P.out_cap);
+  FastCell* dcells;
+  int* dcnt;
+  LORB_TRY(orb_alloc(ctx, &P, &dcells, &dcnt));  // uploads the cells; the pyramid's sync covers them
+  LORB_TRY(enqueue_pyramid(ctx, d_image, rows, cols, step, pyr, d_pyramid));
+  pyr.data = d_pyramid;
+  OrbPyr Q{};
+  for (int l = 0; l < n_levels; l++) { Q.offset[l] = pyr.offset[l]; Q.step[l] = pyr.step[l]; }
+  if (!P.cells.empty())
+    hipLaunchKernelGGL(k_orb_fast, dim3((unsigned)P.cells.size()), dim3(kFastThreads), 0, ctx->stream, d_pyramid, Q,
+                       dcells, ini_th, min_th, const_cast<float*>(P.A.fx), const_cast<float*>(P.A.fy),
+                       const_cast<float*>(P.A.fr), dcnt);
+  hipLaunchKernelGGL(k_orb_octree, dim3(n_levels), dim3(kOctThreads), 0, ctx->stream, P.A);
+  const size_t cap = (size_t)P.out_cap;
+  float *lx, *ly;
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 44, cap, &lx));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 45, cap, &ly));
+  hipLaunchKernelGGL(k_orb_gather, dim3(lorb::ceil_div(cap, 256)), dim3(256), 0, ctx->stream, P.A, (int)cap, lx, ly, d_x,
+                     d_y, d_octave, d_size, d_response, d_level_off, d_n);
+  LORB_CHECK_LAUNCH(ctx);
+  return enqueue_orb(ctx, &pyr, d_pyramid, (int)cap, d_n, lx, ly, d_octave, d_pattern, d_angle, d_desc);
+}
+
+int lorb_orb_extract(lorb_ctx* ctx, const uint8_t* image, int32_t rows, int32_t cols, int32_t step, int32_t n_levels,
+                     const float* scale_factors, const int32_t* n_desired, int32_t ini_th, int32_t min_th,
+                     const int32_t* pattern, int32_t max_keypoints, float* x, float* y, int32_t* octave, float* size,
+                     float* angle, float* response, uint8_t* desc, int32_t* level_off, int32_t* n_keypoints) {
+  if (!ctx) return LORB_E_INVALID;
+  if (!image || !scale_factors || !n_desired || !pattern || !level_off || !n_keypoints || rows < 1 || cols < 1 ||
+      step < cols || n_levels < 1 || n_levels > LORB_MAX_LEVELS || max_keypoints < 0)
+    return lorb::set_error(ctx, LORB_E_INVALID, "bad image / level arguments");
+  int32_t cap = 0;
+  int64_t pb = 0;
+  LORB_TRY(lorb_orb_extract_capacity(rows, cols, n_levels, scale_factors, n_desired, &cap, &pb));
+  uint8_t *dimg, *dpyr, *ddesc;
+  int32_t *dpat, *doct, *dlo, *dn;
+  float *dx, *dy, *dsz, *dang, *drs;
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 16, image, (size_t)(rows - 1) * step + cols, &dimg));
+  LORB_TRY(lorb::upload_t(ctx, S_ORB + 19, pattern, (size_t)1024, &dpat));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 17, (size_t)pb, &dpyr));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 48, (size_t)cap, &dx));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 49, (size_t)cap, &dy));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 2, (size_t)cap, &doct));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 6, (size_t)cap, &dsz));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 7, (size_t)cap, &dang));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 3, (size_t)cap, &drs));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 18, (size_t)cap * 32, &ddesc));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 4, (size_t)LORB_MAX_LEVELS + 1, &dlo));
+  LORB_TRY(lorb::scratch_t(ctx, S_ORB + 5, (size_t)1, &dn));
+  LORB_TRY(lorb_orb_extract_dev(ctx, dimg, rows, cols, step, n_levels, scale_factors, n_desired, ini_th, min_th, dpat, cap,
+                                dpyr, pb, dx, dy, doct, dsz, dang, drs, ddesc, dlo, dn));
+  int n = 0;
+  LORB_HIP(ctx, hipMemcpyAsync(&n, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipMemcpyAsync(level_off, dlo, sizeof(int) * (n_levels + 1), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (n < 0) return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "DistributeOctTree exceeded its node capacity");
+  *n_keypoints = n;
+  if (n > max_keypoints)
+    return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints exceed max_keypoints = %d", n, max_keypoints);
+  if (n > 0) {
+    LORB_HIP(ctx, hipMemcpyAsync(x, dx, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(y, dy, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(octave, doct, sizeof(int) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(size, dsz, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(angle, dang, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(response, drs, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipMemcpyAsync(desc, ddesc, (size_t)32 * n, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return LORB_OK;
 }
 

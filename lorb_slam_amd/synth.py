@@ -404,3 +404,28 @@ def orb_problem(seed=31, n_kps=2000, width=W, height=H, border=19):
     y = (border + rng.uniform(0, 1, n_kps) * (rows - 2 * border - 1)).astype(np.float32)
     pattern = rng.integers(-13, 13, size=1024).astype(np.int32)
     return dict(pyr=pyr, x=x, y=y, level=lev, pattern=pattern)
+
+
+def orb_scene(seed=91, rows=H, cols=W, n_shapes=120, noise=3):
+    """A camera-like test image for the whole ORB extractor: a smooth background
+    gradient, random rectangles and discs of random grey levels (corners and edges of every
+    orientation), a few noise-textured patches (dense FAST responses, many equal scores), and
+    small pixel noise.  uint8, rows x cols."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:rows, 0:cols].astype(np.float64)
+    img = 90 + 40 * np.sin(xx / 97.0) + 30 * np.cos(yy / 71.0)
+    for _ in range(n_shapes):
+        v = rng.uniform(0, 255)
+        if rng.uniform() < 0.6:
+            x0, y0 = rng.uniform(-40, cols), rng.uniform(-40, rows)
+            w, h = rng.uniform(8, 120), rng.uniform(8, 90)
+            m = (xx >= x0) & (xx < x0 + w) & (yy >= y0) & (yy < y0 + h)
+        else:
+            cx, cy, r = rng.uniform(0, cols), rng.uniform(0, rows), rng.uniform(5, 50)
+            m = (xx - cx) ** 2 + (yy - cy) ** 2 < r * r
+        img[m] = v
+    for _ in range(6):
+        x0, y0 = int(rng.uniform(0, cols - 80)), int(rng.uniform(0, rows - 60))
+        img[y0:y0 + 60, x0:x0 + 80] += rng.normal(0, 25, (60, 80))
+    img += rng.integers(-noise, noise + 1, img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)

@@ -163,17 +163,17 @@ def _orb_describe(self, pyr, x, y, level, pattern, device_resident=False):
     return out
 
 
-def _orb_fast_cells(self, pyr, n_desired, ini_th=20, min_th=7, max_kp=200000, max_cells=4096):
-    """Detection stage of ORBextractor::ComputeKeyPointsOctTree: per-cell FAST with the threshold
-    fallback.  Returns x, y, response (level coordinates) and the cell_base / cell_off tables."""
+def _orb_fast_cells(self, pyr, ini_th=20, min_th=7, max_kp=200000, max_cells=4096):
+    """FAST stage of ORBextractor::ComputeKeyPointsOctTree (src/ORBextractor.cpp:803-872): per-cell
+    FAST with the empty-cell fallback.  Returns x, y, response (level coordinates) and the
+    cell_base / cell_off tables."""
     buf, P = A.pack_pyramid(pyr)
     P.data = buf.ctypes.data
-    nd = A.i32(n_desired)
     x, y, r = np.zeros(max_kp, np.float32), np.zeros(max_kp, np.float32), np.zeros(max_kp, np.float32)
     base = np.zeros(len(pyr) + 1, np.int32)
     off = np.zeros(max_cells + len(pyr) + 1, np.int32)
     n = C.c_int32(0)
-    self.check(lib().lorb_orb_fast_cells(self._p, C.byref(P), A.ptr(nd, C.c_int32), C.c_int32(ini_th), C.c_int32(min_th),
+    self.check(lib().lorb_orb_fast_cells(self._p, C.byref(P), C.c_int32(ini_th), C.c_int32(min_th),
                                          C.c_int32(max_kp), A.ptr(x, C.c_float), A.ptr(y, C.c_float),
                                          A.ptr(r, C.c_float), C.c_int32(max_cells), A.ptr(base, C.c_int32),
                                          A.ptr(off, C.c_int32), C.byref(n)), "lorb_orb_fast_cells")
@@ -183,7 +183,8 @@ def _orb_fast_cells(self, pyr, n_desired, ini_th=20, min_th=7, max_kp=200000, ma
 
 
 def _orb_detect(self, pyr, n_desired, scale_factors, ini_th=20, min_th=7, max_kp=100000):
-    """ComputeKeyPointsOctTree without orientation: FAST cells on the device, retention on the host."""
+    """ComputeKeyPointsOctTree without orientation (src/ORBextractor.cpp:799-892): FAST cells and
+    DistributeOctTree on the device."""
     buf, P = A.pack_pyramid(pyr)
     P.data = buf.ctypes.data
     nd, sf = A.i32(n_desired), A.f32(scale_factors)
@@ -198,6 +199,26 @@ def _orb_detect(self, pyr, n_desired, scale_factors, ini_th=20, min_th=7, max_kp
     k = n.value
     return dict(x=x[:k].copy(), y=y[:k].copy(), octave=o[:k].copy(), size=sz[:k].copy(), response=r[:k].copy(),
                 level_off=lo)
+
+
+def _orb_extract(self, img, n_desired, scale_factors, pattern, ini_th=20, min_th=7, max_kp=100000):
+    """The whole ORBextractor::operator() (src/ORBextractor.cpp:1087-1151) on the device."""
+    img = A.u8(img)
+    nd, sf, pat = A.i32(n_desired), A.f32(scale_factors), A.i32(pattern).reshape(-1)
+    x, y, sz, ang, r = (np.zeros(max_kp, np.float32) for _ in range(5))
+    o = np.zeros(max_kp, np.int32)
+    desc = np.zeros((max_kp, 32), np.uint8)
+    lo = np.zeros(len(sf) + 1, np.int32)
+    n = C.c_int32(0)
+    self.check(lib().lorb_orb_extract(self._p, A.ptr(img, C.c_uint8), C.c_int32(img.shape[0]), C.c_int32(img.shape[1]),
+                                      C.c_int32(img.shape[1]), C.c_int32(len(sf)), A.ptr(sf, C.c_float),
+                                      A.ptr(nd, C.c_int32), C.c_int32(ini_th), C.c_int32(min_th), A.ptr(pat, C.c_int32),
+                                      C.c_int32(max_kp), A.ptr(x, C.c_float), A.ptr(y, C.c_float), A.ptr(o, C.c_int32),
+                                      A.ptr(sz, C.c_float), A.ptr(ang, C.c_float), A.ptr(r, C.c_float),
+                                      A.ptr(desc, C.c_uint8), A.ptr(lo, C.c_int32), C.byref(n)), "lorb_orb_extract")
+    k = n.value
+    return dict(x=x[:k].copy(), y=y[:k].copy(), octave=o[:k].copy(), size=sz[:k].copy(), angle=ang[:k].copy(),
+                response=r[:k].copy(), desc=desc[:k].copy(), level_off=lo)
 
 
 def _orb_pyramid(self, img, scale_factors):
@@ -216,6 +237,7 @@ def _orb_pyramid(self, img, scale_factors):
 
 
 Context.orb_pyramid = _orb_pyramid
+Context.orb_extract = _orb_extract
 Context.orb_detect = _orb_detect
 Context.orb_fast_cells = _orb_fast_cells
 Context.orb_describe = _orb_describe

@@ -1,14 +1,22 @@
 /*
- * fast.c -- TEST INFRASTRUCTURE ONLY (see lorb_oracle.h).  CPU restatement of the detection stage
- * of ORBextractor::ComputeKeyPointsOctTree (src/ORBextractor.cpp:898-1000), SURVEY §8f row 3:
- * the per-level cell grid (:903-990) and, per cell, cv::FAST(cell, iniThFAST, true) re-run with
- * minThFAST when it finds at most 3 corners (:990-996).  cv::FAST is OpenCV 3.1's FAST_t<16>
- * (9 contiguous of the 16-pixel circle of radius 3, threshold_tab prefilter) with cornerScore<16>
- * and 3x3 non-maximum suppression, restated from its published source (features2d/src/fast.cpp,
- * fast_score.cpp); OpenCV is absent here, so this is "parity unpinned" (tests/ cross-check it
- * against an independent numpy restatement).  The retention that follows (KeyPointsFilter::
- * retainBest, :1000-1067) is restated at the end of this file together with the libstdc++
- * algorithms it runs on.
+ * fast.c -- TEST INFRASTRUCTURE ONLY (see lorb_oracle.h).  CPU restatement of the keypoint stage
+ * of ORBextractor::operator() (src/ORBextractor.cpp:1087-1103), SURVEY §8f row 3:
+ * ComputeKeyPointsOctTree (:799-897) -- per level, 30-pixel cells with a 6-pixel overlap inside
+ * the EDGE_THRESHOLD-3 border, cv::FAST(cell, iniThFAST, true) re-run with minThFAST only when a
+ * cell finds NO corner (:849-859) -- and DistributeOctTree (:554-797), the quadtree that keeps the
+ * strongest keypoint of each node.  (The reference also holds ComputeKeyPointsOld, :899-1076; it is
+ * dead code -- operator() calls ComputeKeyPointsOctTree, the Old call is commented out at :1103 --
+ * and is not restated.)  cv::FAST is OpenCV 3.1's FAST_t<16> (9 contiguous of the 16-pixel circle
+ * of radius 3, threshold_tab prefilter) with cornerScore<16> and 3x3 non-maximum suppression,
+ * restated from its published source (features2d/src/fast.cpp, fast_score.cpp); OpenCV is absent
+ * here, so FAST is cross-checked against an independent numpy restatement in tests/.
+ *
+ * Pointer-order model.  DistributeOctTree sorts vector<pair<int, ExtractorNode*>> (:717), so nodes
+ * with equal key counts are ordered by the ADDRESS of their std::list element, which depends on the
+ * allocator.  This restatement (and the device kernel) orders them by creation order (the n-th
+ * node pushed into lNodes compares below every later one), i.e. the address order of a heap that
+ * hands out increasing addresses; it is the same kind of convention as the std::set<MapPoint*>
+ * iteration order the adapters take from the caller.
  */
 #include <math.h>
 #include <stdint.h>
@@ -25,7 +33,6 @@ static void make_offsets(int* pixel, int step) {
   for (int k = 0; k < 16; k++) pixel[k] = kOff16[k][0] + kOff16[k][1] * step;
   for (int k = 16; k < 25; k++) pixel[k] = pixel[k - 16];
 }
-
 /* cornerScore<16> */
 int or_fast_score(const uint8_t* ptr, const int* pixel, int threshold) {
   const int K = 8, N = K * 3 + 1;
@@ -122,55 +129,50 @@ int or_fast(const uint8_t* img, int w, int h, int step, int threshold, int max_o
   return n;
 }
 
-/* The cell grid of one level, src/ORBextractor.cpp:903-990.  cells[4 c + 0..3] = iniX, iniY, hX,
- * hY of cell c = i * levelCols + j (hX = hY = 0: the reference skips it).  Returns the number of
- * cells (levelRows * levelCols), or -1 when the grid is degenerate (levelCols or levelRows < 1:
- * the reference divides by zero). */
-int or_orb_cells(int rows, int cols, int n_desired, float image_ratio, int* cells, int max_cells) {
-  const int EDGE = 19;
-  const int levelCols = (int)sqrtf((float)n_desired / (5 * image_ratio));
-  const int levelRows = (int)(image_ratio * levelCols);
-  if (levelCols < 1 || levelRows < 1) return -1;
-  const int minBorderX = EDGE, minBorderY = EDGE, maxBorderX = cols - EDGE, maxBorderY = rows - EDGE;
-  const int W = maxBorderX - minBorderX, H = maxBorderY - minBorderY;
-  const int cellW = (int)ceilf((float)W / levelCols), cellH = (int)ceilf((float)H / levelRows);
-  const int nCells = levelRows * levelCols;
-  if (nCells > max_cells) return -1;
-  float hY = (float)(cellH + 6);
-  for (int i = 0; i < levelRows; i++) {
-    const float iniY = (float)(minBorderY + i * cellH - 3);
-    int skip_row = 0;
-    if (i == levelRows - 1) {
-      hY = maxBorderY + 3 - iniY;
-      if (hY <= 0) skip_row = 1;
-    }
-    float hX = (float)(cellW + 6);
-    for (int j = 0; j < levelCols; j++) {
-      const float iniX = (float)(minBorderX + j * cellW - 3);
-      int* c = cells + 4 * (i * levelCols + j);
+
+/* The cell grid of one level, src/ORBextractor.cpp:803-847.  cells[4 c + 0..3] = iniX, iniY, width,
+ * height of cell c = i * nCols + j in level pixels (width = height = 0: the reference skips it,
+ * :833-834, :843-844).  *ncols / *nrows = the grid; returns nRows * nCols, or -1 when the level is
+ * too small for one 30-pixel cell (the reference divides by zero there). */
+int or_orb_cells(int rows, int cols, int* cells, int max_cells, int* ncols, int* nrows) {
+  const float W = 30;
+  const int minBorderX = 19 - 3, minBorderY = minBorderX;  /* EDGE_THRESHOLD - 3 */
+  const int maxBorderX = cols - 19 + 3, maxBorderY = rows - 19 + 3;
+  const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
+  const int nCols = (int)(width / W), nRows = (int)(height / W);
+  if (nCols < 1 || nRows < 1 || nCols * nRows > max_cells) return -1;
+  const int wCell = (int)ceilf(width / (float)nCols), hCell = (int)ceilf(height / (float)nRows);
+  for (int i = 0; i < nRows; i++) {
+    const float iniY = (float)(minBorderY + i * hCell);
+    float maxY = iniY + (float)hCell + 6;
+    const int skip_row = iniY >= (float)(maxBorderY - 3);
+    if (maxY > (float)maxBorderY) maxY = (float)maxBorderY;
+    for (int j = 0; j < nCols; j++) {
+      const float iniX = (float)(minBorderX + j * wCell);
+      float maxX = iniX + (float)wCell + 6;
+      int* c = cells + 4 * (i * nCols + j);
       c[0] = (int)iniX; c[1] = (int)iniY; c[2] = 0; c[3] = 0;
-      if (skip_row) continue;
-      if (j == levelCols - 1) {
-        hX = maxBorderX + 3 - iniX;
-        if (hX <= 0) continue;
-      }
-      c[2] = (int)hX; c[3] = (int)hY;
+      if (skip_row || iniX >= (float)(maxBorderX - 6)) continue;
+      if (maxX > (float)maxBorderX) maxX = (float)maxBorderX;
+      c[2] = (int)maxX - (int)iniX; c[3] = (int)maxY - (int)iniY;  /* rowRange / colRange */
     }
   }
-  return nCells;
+  if (ncols) *ncols = nCols;
+  if (nrows) *nrows = nRows;
+  return nRows * nCols;
 }
 
-/* Detection over every cell of every level: FAST(ini_th), re-run with min_th when <= 3 corners.
+/* FAST over every cell of every level: FAST(ini_th), re-run with min_th when the cell found none.
  * Keypoints in level coordinates (cell offset added), grouped by level then cell (row-major),
- * FAST's order within a cell.  cell_off[] gets, per level, levelRows*levelCols + 1 offsets
- * (concatenated over levels; level l starts at cell_base[l]).  Returns the keypoint count or -1. */
-int or_orb_fast_cells(const lorb_image_pyramid* P, const int32_t* n_desired, int ini_th, int min_th, int max_kp,
-                      float* x, float* y, float* resp, int max_cells, int32_t* cell_base, int32_t* cell_off) {
-  const float ratio = (float)P->cols[0] / P->rows[0];
+ * FAST's order within a cell -- the order of vToDistributeKeys.  cell_off[] gets, per level,
+ * nRows*nCols + 1 offsets (concatenated over levels; level l starts at cell_base[l] + l).
+ * Returns the keypoint count, or -1 (degenerate level, capacity). */
+int or_orb_fast_cells(const lorb_image_pyramid* P, int ini_th, int min_th, int max_kp, float* x, float* y,
+                      float* resp, int max_cells, int32_t* cell_base, int32_t* cell_off) {
   int nk = 0, nc = 0;
-  int* cells = (int*)malloc(sizeof(int) * 4 * (size_t)max_cells);
+  int* cells = (int*)malloc(sizeof(int) * 4 * (size_t)(max_cells > 0 ? max_cells : 1));
   for (int l = 0; l < P->n_levels; l++) {
-    const int ncl = or_orb_cells(P->rows[l], P->cols[l], n_desired[l], ratio, cells, max_cells - nc);
+    const int ncl = or_orb_cells(P->rows[l], P->cols[l], cells, max_cells - nc, NULL, NULL);
     if (ncl < 0) { free(cells); return -1; }
     cell_base[l] = nc;
     for (int c = 0; c < ncl; c++) {
@@ -180,7 +182,7 @@ int or_orb_fast_cells(const lorb_image_pyramid* P, const int32_t* n_desired, int
       const uint8_t* img = P->data + P->offset[l] + (int64_t)g[1] * P->step[l] + g[0];
       const int cap = max_kp - nk;
       int n = or_fast(img, g[2], g[3], P->step[l], ini_th, cap, x + nk, y + nk, resp + nk);
-      if (n <= 3) n = or_fast(img, g[2], g[3], P->step[l], min_th, cap, x + nk, y + nk, resp + nk);
+      if (n == 0) n = or_fast(img, g[2], g[3], P->step[l], min_th, cap, x + nk, y + nk, resp + nk);
       if (n > cap) { free(cells); return -1; }
       for (int k = 0; k < n; k++) { x[nk + k] += (float)g[0]; y[nk + k] += (float)g[1]; }
       nk += n;
@@ -193,142 +195,176 @@ int or_orb_fast_cells(const lorb_image_pyramid* P, const int32_t* n_desired, int
   return nk;
 }
 
-/* ---- retention (src/ORBextractor.cpp:984-1067) -------------------------------------------
- * KeyPointsFilter::retainBest (OpenCV 3.1) is std::nth_element + std::partition; the order they
- * leave equal responses in decides which keypoints the following resize() keeps, so libstdc++'s
- * algorithms (bits/stl_algo.h, stl_heap.h: introselect with median-of-3 pivots, heap_select past
- * the depth limit, insertion sort; the bidirectional partition) are restated here step for step. */
-typedef struct { float x, y, size, resp; int octave; } or_kp;
+/* ---- DistributeOctTree, src/ORBextractor.cpp:496-797 ---------------------------------------
+ * The list lNodes is a doubly linked list of node records; vKeys holds key indices in the order
+ * the reference's vectors hold the keypoints.  UL / UR / BL / BR are always an axis-aligned box, so
+ * a node keeps (x0, y0) = UL and (x1, y1) = BR. */
+typedef struct oct_node {
+  int x0, y0, x1, y1;
+  int* keys;
+  int n;
+  int no_more;            /* bNoMore */
+  long creation;          /* pointer-order model, see the file header */
+  struct oct_node *prev, *next;
+} oct_node;
 
-static int kp_greater(const or_kp* a, const or_kp* b) { return a->resp > b->resp; }  /* KeypointResponseGreater */
-static void kp_swap(or_kp* a, or_kp* b) { or_kp t = *a; *a = *b; *b = t; }
+typedef struct {
+  oct_node *head, *tail;
+  long size, created;
+} oct_list;
 
-static void adjust_heap(or_kp* f, long hole, long len, or_kp value) {
-  const long top = hole;
-  long second = hole;
-  while (second < (len - 1) / 2) {
-    second = 2 * (second + 1);
-    if (kp_greater(&f[second], &f[second - 1])) second--;
-    f[hole] = f[second];
-    hole = second;
-  }
-  if ((len & 1) == 0 && second == (len - 2) / 2) {
-    second = 2 * (second + 1);
-    f[hole] = f[second - 1];
-    hole = second - 1;
-  }
-  /* __push_heap */
-  long parent = (hole - 1) / 2;
-  while (hole > top && kp_greater(&f[parent], &value)) {
-    f[hole] = f[parent];
-    hole = parent;
-    parent = (hole - 1) / 2;
-  }
-  f[hole] = value;
-}
-static void make_heap(or_kp* f, long len) {
-  if (len < 2) return;
-  long parent = (len - 2) / 2;
-  while (1) {
-    or_kp v = f[parent];
-    adjust_heap(f, parent, len, v);
-    if (parent == 0) return;
-    parent--;
-  }
-}
-static void heap_select(or_kp* f, long mid, long last) {
-  make_heap(f, mid);
-  for (long i = mid; i < last; ++i)
-    if (kp_greater(&f[i], &f[0])) {  /* __pop_heap(first, middle, i) */
-      or_kp v = f[i];
-      f[i] = f[0];
-      adjust_heap(f, 0, mid, v);
-    }
-}
-static void move_median_to_first(or_kp* f, long r, long a, long b, long c) {
-  if (kp_greater(&f[a], &f[b])) {
-    if (kp_greater(&f[b], &f[c])) kp_swap(&f[r], &f[b]);
-    else if (kp_greater(&f[a], &f[c])) kp_swap(&f[r], &f[c]);
-    else kp_swap(&f[r], &f[a]);
-  } else if (kp_greater(&f[a], &f[c])) kp_swap(&f[r], &f[a]);
-  else if (kp_greater(&f[b], &f[c])) kp_swap(&f[r], &f[c]);
-  else kp_swap(&f[r], &f[b]);
-}
-static long unguarded_partition(or_kp* f, long first, long last, long pivot) {
-  while (1) {
-    while (kp_greater(&f[first], &f[pivot])) ++first;
-    --last;
-    while (kp_greater(&f[pivot], &f[last])) --last;
-    if (!(first < last)) return first;
-    kp_swap(&f[first], &f[last]);
-    ++first;
-  }
-}
-static void insertion_sort(or_kp* f, long first, long last) {
-  if (first == last) return;
-  for (long i = first + 1; i != last; ++i) {
-    if (kp_greater(&f[i], &f[first])) {
-      or_kp v = f[i];
-      memmove(&f[first + 1], &f[first], sizeof(or_kp) * (size_t)(i - first));
-      f[first] = v;
-    } else {
-      or_kp v = f[i];
-      long l = i, nx = i - 1;
-      while (kp_greater(&v, &f[nx])) { f[l] = f[nx]; l = nx; --nx; }
-      f[l] = v;
-    }
-  }
-}
-static int lg(long n) { int k = 0; while (n > 1) { n >>= 1; k++; } return k; }
-static void nth_element(or_kp* f, long nth, long n) {
-  if (n == 0 || nth == n) return;
-  long first = 0, last = n;
-  int depth = 2 * lg(n);
-  while (last - first > 3) {
-    if (depth == 0) {
-      heap_select(f + first, nth + 1 - first, last - first);
-      kp_swap(&f[first], &f[nth]);
-      return;
-    }
-    --depth;
-    const long mid = first + (last - first) / 2;
-    move_median_to_first(f, first, first + 1, mid, last - 1);
-    const long cut = unguarded_partition(f, first + 1, last, first);
-    if (cut <= nth) first = cut; else last = cut;
-  }
-  insertion_sort(f, first, last);
-}
-/* std::partition (bidirectional) with pred = response >= value; returns the new end */
-static long partition_ge(or_kp* f, long first, long last, float value) {
-  while (1) {
-    while (1) {
-      if (first == last) return first;
-      if (f[first].resp >= value) ++first; else break;
-    }
-    --last;
-    while (1) {
-      if (first == last) return first;
-      if (!(f[last].resp >= value)) --last; else break;
-    }
-    kp_swap(&f[first], &f[last]);
-    ++first;
-  }
-}
-/* KeyPointsFilter::retainBest; returns the new size */
-static long retain_best(or_kp* f, long n, long n_points) {
-  if (n_points >= 0 && n > n_points) {
-    if (n_points == 0) return 0;
-    nth_element(f, n_points, n);
-    const float amb = f[n_points - 1].resp;
-    return partition_ge(f, n_points, n, amb);
-  }
+static oct_node* oct_new(oct_list* L, int x0, int y0, int x1, int y1, int cap) {
+  oct_node* n = (oct_node*)calloc(1, sizeof(oct_node));
+  n->x0 = x0; n->y0 = y0; n->x1 = x1; n->y1 = y1;
+  n->keys = (int*)malloc(sizeof(int) * (size_t)(cap > 0 ? cap : 1));
+  n->creation = L->created++;
   return n;
 }
+static void oct_push_back(oct_list* L, oct_node* n) {
+  n->prev = L->tail; n->next = NULL;
+  if (L->tail) L->tail->next = n; else L->head = n;
+  L->tail = n; L->size++;
+}
+static void oct_push_front(oct_list* L, oct_node* n) {
+  n->next = L->head; n->prev = NULL;
+  if (L->head) L->head->prev = n; else L->tail = n;
+  L->head = n; L->size++;
+}
+static oct_node* oct_erase(oct_list* L, oct_node* n) {  /* returns the next element */
+  oct_node* nx = n->next;
+  if (n->prev) n->prev->next = n->next; else L->head = n->next;
+  if (n->next) n->next->prev = n->prev; else L->tail = n->prev;
+  L->size--;
+  free(n->keys);
+  free(n);
+  return nx;
+}
 
-/* Detection + retention of every level (src/ORBextractor.cpp:898-1067): FAST per cell (above),
- * the nToRetain distribution, retainBest + resize per cell, cell offsets added, octave and size,
- * and the level-wide retainBest when more than n_desired survive.  Outputs per keypoint x, y (level
- * coordinates), octave, size, response; level_off[n_levels + 1].  Returns the count or -1. */
+/* ExtractorNode::DivideNode (:496-552): the four children n1..n4 (returned in c[0..3], never
+ * NULL), each key of the parent appended to the child whose box holds it, in parent order. */
+static void oct_divide(oct_list* L, const oct_node* p, const float* kx, const float* ky, oct_node* c[4]) {
+  const int halfX = (int)ceilf((float)(p->x1 - p->x0) / 2);
+  const int halfY = (int)ceilf((float)(p->y1 - p->y0) / 2);
+  const int mx = p->x0 + halfX, my = p->y0 + halfY;
+  c[0] = oct_new(L, p->x0, p->y0, mx, my, p->n);
+  c[1] = oct_new(L, mx, p->y0, p->x1, my, p->n);
+  c[2] = oct_new(L, p->x0, my, mx, p->y1, p->n);
+  c[3] = oct_new(L, mx, my, p->x1, p->y1, p->n);
+  for (int i = 0; i < p->n; i++) {
+    const int k = p->keys[i];
+    oct_node* d;
+    if (kx[k] < (float)mx) d = ky[k] < (float)my ? c[0] : c[2];
+    else d = ky[k] < (float)my ? c[1] : c[3];
+    d->keys[d->n++] = k;
+  }
+  for (int q = 0; q < 4; q++) c[q]->no_more = c[q]->n == 1;
+}
+
+typedef struct { int size; long creation; oct_node* node; } oct_pair;
+static int oct_pair_cmp(const void* a, const void* b) {  /* std::pair operator<, pointers as creation */
+  const oct_pair* p = (const oct_pair*)a;
+  const oct_pair* q = (const oct_pair*)b;
+  if (p->size != q->size) return p->size < q->size ? -1 : 1;
+  return (p->creation > q->creation) - (p->creation < q->creation);
+}
+
+/* push the non-empty children to the front (n1 first, so the list reads n4 n3 n2 n1 ...), record
+ * the ones holding more than one key in (pairs, *np); returns how many were recorded */
+static int oct_push_children(oct_list* L, oct_node* c[4], oct_pair* pairs, long* np) {
+  int rec = 0;
+  for (int q = 0; q < 4; q++) {
+    if (c[q]->n > 0) {
+      oct_push_front(L, c[q]);
+      if (c[q]->n > 1) {
+        pairs[(*np)++] = (oct_pair){c[q]->n, c[q]->creation, c[q]};
+        rec++;
+      }
+    } else {
+      free(c[q]->keys);
+      free(c[q]);
+    }
+  }
+  return rec;
+}
+
+/* kx, ky: key coordinates relative to (minX, minY); resp: responses; n keys in vToDistributeKeys
+ * order.  Writes the kept key indices in lNodes order to out (capacity >= n) and returns their
+ * count, or -1 when the level is degenerate (nIni < 1). */
+int or_distribute_octree(const float* kx, const float* ky, const float* resp, int n, int minX, int maxX, int minY,
+                         int maxY, int N, int32_t* out) {
+  const int nIni = (int)roundf((float)(maxX - minX) / (float)(maxY - minY));
+  if (nIni < 1) return -1;
+  const float hX = (float)(maxX - minX) / (float)nIni;
+  oct_list L = {NULL, NULL, 0, 0};
+  oct_node** ini = (oct_node**)malloc(sizeof(oct_node*) * (size_t)nIni);
+  for (int i = 0; i < nIni; i++) {  /* :575-586 */
+    const int ulx = (int)(hX * (float)i), urx = (int)(hX * (float)(i + 1));
+    ini[i] = oct_new(&L, ulx, 0, urx, maxY - minY, n);
+    oct_push_back(&L, ini[i]);
+  }
+  for (int i = 0; i < n; i++) {  /* :590-594 */
+    oct_node* d = ini[(size_t)(kx[i] / hX)];
+    d->keys[d->n++] = i;
+  }
+  free(ini);
+  for (oct_node* it = L.head; it;) {  /* :596-609 */
+    if (it->n == 1) { it->no_more = 1; it = it->next; }
+    else if (it->n == 0) it = oct_erase(&L, it);
+    else it = it->next;
+  }
+  long cap_pairs = 4 * (long)(n + 4), npairs = 0, nprev = 0;
+  oct_pair* pairs = (oct_pair*)malloc(sizeof(oct_pair) * (size_t)cap_pairs);
+  oct_pair* prevp = (oct_pair*)malloc(sizeof(oct_pair) * (size_t)cap_pairs);
+  int finish = 0;
+  while (!finish) {  /* :619-772 */
+    long prevSize = L.size;
+    int nToExpand = 0;
+    npairs = 0;
+    for (oct_node* it = L.head; it;) {
+      if (it->no_more) { it = it->next; continue; }
+      oct_node* c[4];
+      oct_divide(&L, it, kx, ky, c);
+      nToExpand += oct_push_children(&L, c, pairs, &npairs);
+      it = oct_erase(&L, it);
+    }
+    if (L.size >= N || L.size == prevSize) {
+      finish = 1;
+    } else if (L.size + nToExpand * 3 > N) {
+      while (!finish) {  /* :709-770 */
+        prevSize = L.size;
+        memcpy(prevp, pairs, sizeof(oct_pair) * (size_t)npairs);
+        nprev = npairs;
+        npairs = 0;
+        qsort(prevp, (size_t)nprev, sizeof(oct_pair), oct_pair_cmp);
+        for (long j = nprev - 1; j >= 0; j--) {
+          oct_node* c[4];
+          oct_divide(&L, prevp[j].node, kx, ky, c);
+          oct_push_children(&L, c, pairs, &npairs);
+          oct_erase(&L, prevp[j].node);
+          if (L.size >= N) break;
+        }
+        if (L.size >= N || L.size == prevSize) finish = 1;
+      }
+    }
+  }
+  int m = 0;
+  for (oct_node* it = L.head; it; it = it->next) {  /* :776-794 */
+    int best = it->keys[0];
+    float maxResponse = resp[best];
+    for (int k = 1; k < it->n; k++)
+      if (resp[it->keys[k]] > maxResponse) { best = it->keys[k]; maxResponse = resp[best]; }
+    out[m++] = best;
+  }
+  while (L.head) oct_erase(&L, L.head);
+  free(pairs);
+  free(prevp);
+  return m;
+}
+
+/* ComputeKeyPointsOctTree without the orientation (:799-892): FAST cells, DistributeOctTree per
+ * level with mnFeaturesPerLevel[l] = n_desired[l], then the border offset, octave and size
+ * (PATCH_SIZE * mvScaleFactor[l], truncated to int, :881).  Per keypoint x, y (level coordinates),
+ * octave, size, response; level_off[n_levels + 1].  Returns the count or -1. */
 int or_orb_detect(const lorb_image_pyramid* P, const int32_t* n_desired, const float* scale_factors, int ini_th,
                   int min_th, int max_kp, float* ox, float* oy, int32_t* ooct, float* osize, float* oresp,
                   int32_t* level_off) {
@@ -339,66 +375,27 @@ int or_orb_detect(const lorb_image_pyramid* P, const int32_t* n_desired, const f
   float* fx = (float*)malloc(sizeof(float) * cap);
   float* fy = (float*)malloc(sizeof(float) * cap);
   float* fr = (float*)malloc(sizeof(float) * cap);
-  int nk = or_orb_fast_cells(P, n_desired, ini_th, min_th, cap, fx, fy, fr, max_cells, base, coff);
+  int32_t* kept = (int32_t*)malloc(sizeof(int32_t) * cap);
+  const int nk = or_orb_fast_cells(P, ini_th, min_th, cap, fx, fy, fr, max_cells, base, coff);
   int out = 0, ok = nk >= 0;
-  const float ratio = (float)P->cols[0] / P->rows[0];
-  int* cells = (int*)malloc(sizeof(int) * 4 * (size_t)max_cells);
   for (int l = 0; ok && l < P->n_levels; l++) {
     level_off[l] = out;
-    const int nd = n_desired[l];
-    const int levelCols = (int)sqrtf((float)nd / (5 * ratio));
-    const int levelRows = (int)(ratio * levelCols);
-    const int nCells = levelRows * levelCols;
-    or_orb_cells(P->rows[l], P->cols[l], nd, ratio, cells, max_cells);
-    const int nfeaturesCell = (int)ceilf((float)nd / nCells);
-    int* nToRetain = (int*)calloc((size_t)nCells, sizeof(int));
-    int* nTotal = (int*)calloc((size_t)nCells, sizeof(int));
-    char* bNoMore = (char*)calloc((size_t)nCells, 1);
-    int nNoMore = 0, nToDistribute = 0;
-    const int32_t* co = coff + base[l] + l;
-    for (int c = 0; c < nCells; c++) {
-      if (cells[4 * c + 2] <= 0 || cells[4 * c + 3] <= 0) continue;  /* skipped cell (:940, :960) */
-      const int nKeys = co[c + 1] - co[c];
-      nTotal[c] = nKeys;
-      if (nKeys > nfeaturesCell) { nToRetain[c] = nfeaturesCell; bNoMore[c] = 0; }
-      else { nToRetain[c] = nKeys; nToDistribute += nfeaturesCell - nKeys; bNoMore[c] = 1; nNoMore++; }
-    }
-    while (nToDistribute > 0 && nNoMore < nCells) {
-      const int nNew = (int)(nfeaturesCell + ceilf((float)nToDistribute / (nCells - nNoMore)));
-      nToDistribute = 0;
-      for (int c = 0; c < nCells; c++)
-        if (!bNoMore[c]) {
-          if (nTotal[c] > nNew) { nToRetain[c] = nNew; bNoMore[c] = 0; }
-          else { nToRetain[c] = nTotal[c]; nToDistribute += nNew - nTotal[c]; bNoMore[c] = 1; nNoMore++; }
-        }
-    }
+    const int minBorderX = 16, minBorderY = 16, maxBorderX = P->cols[l] - 16, maxBorderY = P->rows[l] - 16;
+    const int k0 = coff[base[l] + l], k1 = coff[base[l + 1] + l];
+    for (int k = k0; k < k1; k++) { fx[k] -= (float)minBorderX; fy[k] -= (float)minBorderY; }
+    const int m = or_distribute_octree(fx + k0, fy + k0, fr + k0, k1 - k0, minBorderX, maxBorderX, minBorderY,
+                                       maxBorderY, n_desired[l], kept);
+    if (m < 0) { ok = 0; break; }
     const int scaledPatchSize = (int)(31 * scale_factors[l]);
-    or_kp* lv = (or_kp*)malloc(sizeof(or_kp) * (size_t)(co[nCells] - co[0] + 1));
-    long nl = 0;
-    for (int c = 0; c < nCells; c++) {
-      or_kp* cell = lv + nl;
-      long n = 0;
-      for (int k = co[c]; k < co[c + 1]; k++) {  /* FAST order, cell coordinates restored below */
-        cell[n].x = fx[k] - (float)cells[4 * c]; cell[n].y = fy[k] - (float)cells[4 * c + 1];
-        cell[n].resp = fr[k]; cell[n].size = 7.f; cell[n].octave = 0; n++;
-      }
-      n = retain_best(cell, n, nToRetain[c]);
-      if (n > nToRetain[c]) n = nToRetain[c];
-      for (long k = 0; k < n; k++) {
-        cell[k].x += (float)cells[4 * c]; cell[k].y += (float)cells[4 * c + 1];
-        cell[k].octave = l; cell[k].size = (float)scaledPatchSize;
-      }
-      nl += n;
-    }
-    if (nl > nd) { nl = retain_best(lv, nl, nd); nl = nd < nl ? nd : nl; }
-    for (long k = 0; k < nl && ok; k++) {
+    for (int q = 0; q < m; q++) {
       if (out >= max_kp) { ok = 0; break; }
-      ox[out] = lv[k].x; oy[out] = lv[k].y; ooct[out] = lv[k].octave; osize[out] = lv[k].size; oresp[out] = lv[k].resp;
+      const int k = k0 + kept[q];
+      ox[out] = fx[k] + (float)minBorderX; oy[out] = fy[k] + (float)minBorderY;
+      ooct[out] = l; osize[out] = (float)scaledPatchSize; oresp[out] = fr[k];
       out++;
     }
-    free(lv); free(nToRetain); free(nTotal); free(bNoMore);
   }
   level_off[P->n_levels] = out;
-  free(cells); free(base); free(coff); free(fx); free(fy); free(fr);
+  free(base); free(coff); free(fx); free(fy); free(fr); free(kept);
   return ok ? out : -1;
 }

@@ -117,18 +117,24 @@ void or_orb_descriptor(const uint8_t* img, int step, float px, float py, float a
 void or_orb_describe(const lorb_image_pyramid* P, int n, const float* x, const float* y, const int32_t* level,
                      const int32_t* pattern, float* angle, uint8_t* desc);
 
-/* fast.c: cv::FAST (OpenCV 3.1 FAST_t<16> + cornerScore<16>) and the per-level cell detection of
- * ORBextractor::ComputeKeyPointsOctTree (src/ORBextractor.cpp:898-1000) */
+/* fast.c: cv::FAST (OpenCV 3.1 FAST_t<16> + cornerScore<16>) and ORBextractor::
+ * ComputeKeyPointsOctTree + DistributeOctTree (src/ORBextractor.cpp:554-897) */
 int or_fast_score(const uint8_t* ptr, const int* pixel, int threshold);
 int or_fast(const uint8_t* img, int w, int h, int step, int threshold, int max_out, float* ox, float* oy,
             float* oresp);
-int or_orb_cells(int rows, int cols, int n_desired, float image_ratio, int* cells, int max_cells);
-int or_orb_fast_cells(const lorb_image_pyramid* P, const int32_t* n_desired, int ini_th, int min_th, int max_kp,
-                      float* x, float* y, float* resp, int max_cells, int32_t* cell_base, int32_t* cell_off);
-
+int or_orb_cells(int rows, int cols, int* cells, int max_cells, int* ncols, int* nrows);
+int or_orb_fast_cells(const lorb_image_pyramid* P, int ini_th, int min_th, int max_kp, float* x, float* y,
+                      float* resp, int max_cells, int32_t* cell_base, int32_t* cell_off);
+int or_distribute_octree(const float* kx, const float* ky, const float* resp, int n, int minX, int maxX, int minY,
+                         int maxY, int N, int32_t* out);
 int or_orb_detect(const lorb_image_pyramid* P, const int32_t* n_desired, const float* scale_factors, int ini_th,
                   int min_th, int max_kp, float* ox, float* oy, int32_t* ooct, float* osize, float* oresp,
                   int32_t* level_off);
+/* orb.c: the whole ORBextractor::operator() (src/ORBextractor.cpp:1087-1151) */
+int or_orb_extract(const uint8_t* img, int rows, int cols, int step, int n_levels, const float* scale_factors,
+                   const int32_t* n_desired, int ini_th, int min_th, const int32_t* pattern, int max_kp, float* ox,
+                   float* oy, int32_t* ooct, float* osize, float* oangle, float* oresp, uint8_t* odesc,
+                   int32_t* level_off);
 
 /* orb.c: ORBextractor::ComputePyramid with OpenCV 3.1's 8U INTER_LINEAR resize restated */
 int or_resize_simd_cols(int width);

@@ -332,14 +332,25 @@ def fast(img, threshold):
     return x[:n].copy(), y[:n].copy(), r[:n].copy()
 
 
-def orb_fast_cells(pyr, n_desired, ini_th=20, min_th=7, max_kp=200000, max_cells=4096):
+def orb_cells(rows, cols, max_cells=4096):
+    """The cell grid of one level (src/ORBextractor.cpp:803-847): (cells[n, 4] = iniX, iniY, w, h;
+    w = h = 0 for skipped cells), nCols, nRows."""
+    cells = np.zeros((max_cells, 4), np.int32)
+    nc, nr = C.c_int(0), C.c_int(0)
+    n = lib().or_orb_cells(C.c_int(rows), C.c_int(cols), A.ptr(cells, C.c_int32), C.c_int(max_cells), C.byref(nc),
+                           C.byref(nr))
+    assert n >= 0, "degenerate level"
+    return cells[:n].copy(), nc.value, nr.value
+
+
+def orb_fast_cells(pyr, ini_th=20, min_th=7, max_kp=200000, max_cells=4096):
+    """FAST over the OctTree cells of every level (src/ORBextractor.cpp:803-872)."""
     buf, P = A.pack_pyramid(pyr)
     P.data = buf.ctypes.data
-    nd = A.i32(n_desired)
     x, y, r = np.zeros(max_kp, np.float32), np.zeros(max_kp, np.float32), np.zeros(max_kp, np.float32)
     base = np.zeros(len(pyr) + 1, np.int32)
     off = np.zeros(max_cells + len(pyr) + 1, np.int32)
-    n = lib().or_orb_fast_cells(C.byref(P), A.ptr(nd, C.c_int32), C.c_int(ini_th), C.c_int(min_th), C.c_int(max_kp),
+    n = lib().or_orb_fast_cells(C.byref(P), C.c_int(ini_th), C.c_int(min_th), C.c_int(max_kp),
                                 A.ptr(x, C.c_float), A.ptr(y, C.c_float), A.ptr(r, C.c_float), C.c_int(max_cells),
                                 A.ptr(base, C.c_int32), A.ptr(off, C.c_int32))
     assert n >= 0, "degenerate grid or capacity"
@@ -347,8 +358,20 @@ def orb_fast_cells(pyr, n_desired, ini_th=20, min_th=7, max_kp=200000, max_cells
                 cell_off=off[:base[-1] + len(pyr)].copy())
 
 
+def distribute_octree(kx, ky, resp, minX, maxX, minY, maxY, N):
+    """DistributeOctTree (src/ORBextractor.cpp:554-797): indices of the kept keys in list order.
+    kx, ky relative to (minX, minY)."""
+    kx, ky, resp = A.f32(kx), A.f32(ky), A.f32(resp)
+    out = np.zeros(max(len(kx), 1), np.int32)
+    m = lib().or_distribute_octree(A.ptr(kx, C.c_float), A.ptr(ky, C.c_float), A.ptr(resp, C.c_float),
+                                   C.c_int(len(kx)), C.c_int(minX), C.c_int(maxX), C.c_int(minY), C.c_int(maxY),
+                                   C.c_int(N), A.ptr(out, C.c_int32))
+    assert m >= 0
+    return out[:m].copy()
+
+
 def orb_detect(pyr, n_desired, scale_factors, ini_th=20, min_th=7, max_kp=100000):
-    """ComputeKeyPointsOctTree without orientation (src/ORBextractor.cpp:898-1067)."""
+    """ComputeKeyPointsOctTree without orientation (src/ORBextractor.cpp:799-892)."""
     buf, P = A.pack_pyramid(pyr)
     P.data = buf.ctypes.data
     nd, sf = A.i32(n_desired), A.f32(scale_factors)
@@ -361,6 +384,24 @@ def orb_detect(pyr, n_desired, scale_factors, ini_th=20, min_th=7, max_kp=100000
     assert n >= 0
     return dict(x=x[:n].copy(), y=y[:n].copy(), octave=o[:n].copy(), size=sz[:n].copy(), response=r[:n].copy(),
                 level_off=lo)
+
+
+def orb_extract(img, n_desired, scale_factors, pattern, ini_th=20, min_th=7, max_kp=100000):
+    """The whole ORBextractor::operator() (src/ORBextractor.cpp:1087-1151) on one image."""
+    img = A.u8(img)
+    nd, sf, pat = A.i32(n_desired), A.f32(scale_factors), A.i32(pattern).reshape(-1)
+    x, y, sz, ang, r = (np.zeros(max_kp, np.float32) for _ in range(5))
+    o = np.zeros(max_kp, np.int32)
+    desc = np.zeros((max_kp, 32), np.uint8)
+    lo = np.zeros(len(sf) + 1, np.int32)
+    n = lib().or_orb_extract(A.ptr(img, C.c_uint8), C.c_int(img.shape[0]), C.c_int(img.shape[1]), C.c_int(img.shape[1]),
+                             C.c_int(len(sf)), A.ptr(sf, C.c_float), A.ptr(nd, C.c_int32), C.c_int(ini_th),
+                             C.c_int(min_th), A.ptr(pat, C.c_int32), C.c_int(max_kp), A.ptr(x, C.c_float),
+                             A.ptr(y, C.c_float), A.ptr(o, C.c_int32), A.ptr(sz, C.c_float), A.ptr(ang, C.c_float),
+                             A.ptr(r, C.c_float), A.ptr(desc, C.c_uint8), A.ptr(lo, C.c_int32))
+    assert n >= 0
+    return dict(x=x[:n].copy(), y=y[:n].copy(), octave=o[:n].copy(), size=sz[:n].copy(), angle=ang[:n].copy(),
+                response=r[:n].copy(), desc=desc[:n].copy(), level_off=lo)
 
 
 def orb_pyramid(img, scale_factors):

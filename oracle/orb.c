@@ -124,7 +124,9 @@ void or_orb_descriptor(const uint8_t* img, int step, float px, float py, float a
                        uint8_t* desc) {
   const float factorPI = (float)(OR_CV_PI / 180.f);
   const float angle = angle_deg * factorPI;
-  const float a = (float)cos(angle), b = (float)sin(angle);
+  /* `cos(angle)` with a float argument under `using namespace std` (:69) is std::cos(float), i.e.
+   * libm's cosf / sinf -- not the double cos rounded to float (they differ on ~0.1 % of angles) */
+  const float a = cosf(angle), b = sinf(angle);
   const uint8_t* center = img + (ptrdiff_t)lrintf(py) * step + lrintf(px);
   for (int i = 0; i < 32; ++i) {
     int val = 0;
@@ -266,4 +268,34 @@ void or_orb_pyramid(const uint8_t* img, int rows, int cols, int step, int n_leve
     off += (int64_t)w * h;
   }
   P->data = out;
+}
+
+/* ORBextractor::operator() (src/ORBextractor.cpp:1087-1151) on one image: ComputePyramid,
+ * ComputeKeyPointsOctTree (keypoints + IC_Angle orientation, :895-896), then per level the Gaussian
+ * blur and the descriptors, and the keypoint coordinates scaled to level 0 (pt *= mvScaleFactor[l]
+ * for l != 0, :1141-1147).  Outputs in the reference's order (level, then DistributeOctTree's list
+ * order): x, y, octave, size, angle, response, desc (32 bytes each); level_off[n_levels + 1].
+ * Returns the keypoint count or -1. */
+int or_orb_extract(const uint8_t* img, int rows, int cols, int step, int n_levels, const float* scale_factors,
+                   const int32_t* n_desired, int ini_th, int min_th, const int32_t* pattern, int max_kp, float* ox,
+                   float* oy, int32_t* ooct, float* osize, float* oangle, float* oresp, uint8_t* odesc,
+                   int32_t* level_off) {
+  size_t total = 0;
+  for (int l = 0; l < n_levels; l++) {
+    const float inv = 1.0f / scale_factors[l];
+    total += (size_t)lrintf((float)rows * inv) * (size_t)lrintf((float)cols * inv);
+  }
+  uint8_t* pyr = (uint8_t*)malloc(total + 16);
+  lorb_image_pyramid P;
+  memset(&P, 0, sizeof(P));
+  or_orb_pyramid(img, rows, cols, step, n_levels, scale_factors, pyr, &P);
+  P.data = pyr;
+  const int n = or_orb_detect(&P, n_desired, scale_factors, ini_th, min_th, max_kp, ox, oy, ooct, osize, oresp,
+                              level_off);
+  if (n < 0) { free(pyr); return -1; }
+  or_orb_describe(&P, n, ox, oy, ooct, pattern, oangle, odesc);
+  for (int i = 0; i < n; i++)
+    if (ooct[i] != 0) { ox[i] = ox[i] * scale_factors[ooct[i]]; oy[i] = oy[i] * scale_factors[ooct[i]]; }
+  free(pyr);
+  return n;
 }

@@ -1,6 +1,8 @@
 """Independent pure-Python restatement (small cases only) of the windowed matchers, used to pin
 the C oracle.  float32 arithmetic is reproduced with numpy float32 scalars; reference
 file:line cited per function."""
+import ctypes
+import ctypes.util
 import math
 
 import numpy as np
@@ -197,6 +199,19 @@ def fast_atan2(y, x):  # cv::fastAtan2 (OpenCV 3.1) in float32
     return a
 
 
+_LIBM = ctypes.CDLL(ctypes.util.find_library("m"))
+_LIBM.cosf.restype = _LIBM.sinf.restype = ctypes.c_float
+_LIBM.cosf.argtypes = _LIBM.sinf.argtypes = [ctypes.c_float]
+
+
+def _cosf(v):
+    return f32(_LIBM.cosf(float(f32(v))))
+
+
+def _sinf(v):
+    return f32(_LIBM.sinf(float(f32(v))))
+
+
 def orb_describe(pyr, x, y, level, pattern):  # src/ORBextractor.cpp:79-150, 469-493, 1131-1132
     umax = np.zeros(16, np.int64)
     for v in range(0, 12):
@@ -222,7 +237,7 @@ def orb_describe(pyr, x, y, level, pattern):  # src/ORBextractor.cpp:79-150, 469
             m10 += int((u * row).sum()); m01 += v * int(row.sum())
         ang[i] = fast_atan2(f32(m01), f32(m10))
         angle = f32(ang[i] * f32(math.pi / 180.0))
-        a, b = f32(math.cos(float(angle))), f32(math.sin(float(angle)))
+        a, b = _cosf(angle), _sinf(angle)  # std::cos(float) under `using namespace std` = libm cosf
         bl = blurred[level[i]]
         bits = []
         for p in range(512):
@@ -329,3 +344,100 @@ def resize_linear(img, h, w):  # OpenCV 3.1 8U INTER_LINEAR (imgwarp.cpp), numpy
         scal = (rows[0] * b0 + rows[1] * b1 + (1 << 21)) >> 22
         out[dy] = np.clip(np.where(cols < xs, simd, scal), 0, 255).astype(np.uint8)
     return out
+
+
+def orb_cells(rows, cols):
+    """ComputeKeyPointsOctTree's cell grid (src/ORBextractor.cpp:803-847): list of
+    (iniX, iniY, w, h) per cell, row-major, w = h = 0 for skipped cells."""
+    W = f32(30)
+    minb = 16
+    maxbx, maxby = cols - 16, rows - 16
+    width, height = f32(maxbx - minb), f32(maxby - minb)
+    ncols, nrows = int(width / W), int(height / W)
+    wcell, hcell = int(math.ceil(f32(width / f32(ncols)))), int(math.ceil(f32(height / f32(nrows))))
+    cells = []
+    for i in range(nrows):
+        iy = minb + i * hcell
+        my = min(iy + hcell + 6, maxby)
+        for j in range(ncols):
+            ix = minb + j * wcell
+            mx = min(ix + wcell + 6, maxbx)
+            if iy >= maxby - 3 or ix >= maxbx - 6:
+                cells.append((ix, iy, 0, 0))
+            else:
+                cells.append((ix, iy, mx - ix, my - iy))
+    return cells
+
+
+def distribute_octree(kx, ky, resp, minX, maxX, minY, maxY, N):
+    """DistributeOctTree (src/ORBextractor.cpp:554-797) restated with a Python list standing in for
+    std::list<ExtractorNode> (push_front = insert at 0).  Nodes are [x0, y0, x1, y1, keys, creation];
+    equal-size nodes sort by creation order (the pointer-order model of oracle/fast.c)."""
+    kx = np.asarray(kx, np.float32); ky = np.asarray(ky, np.float32); resp = np.asarray(resp, np.float32)
+    created = [0]
+
+    def node(x0, y0, x1, y1):
+        created[0] += 1
+        return [x0, y0, x1, y1, [], created[0]]
+
+    def divide(p):
+        hx = int(math.ceil(f32(f32(p[2] - p[0]) / f32(2))))
+        hy = int(math.ceil(f32(f32(p[3] - p[1]) / f32(2))))
+        mx, my = p[0] + hx, p[1] + hy
+        c = [node(p[0], p[1], mx, my), node(mx, p[1], p[2], my), node(p[0], my, mx, p[3]), node(mx, my, p[2], p[3])]
+        for k in p[4]:
+            q = (0 if ky[k] < my else 2) if kx[k] < mx else (1 if ky[k] < my else 3)
+            c[q][4].append(k)
+        return c
+
+    n_ini = int(math.floor(float(f32(maxX - minX) / f32(maxY - minY)) + 0.5))  # std::round(float)
+    hX = f32(f32(maxX - minX) / f32(n_ini))
+    nodes = [node(int(f32(hX * f32(i))), 0, int(f32(hX * f32(i + 1))), maxY - minY) for i in range(n_ini)]
+    for k in range(len(kx)):
+        nodes[int(f32(kx[k] / hX))][4].append(k)
+    nodes = [n for n in nodes if n[4]]
+    finish = False
+    pairs = []
+    while not finish:
+        prev = len(nodes)
+        pairs = []
+        n_expand = 0
+        i = 0
+        while i < len(nodes):
+            n = nodes[i]
+            if len(n[4]) == 1:
+                i += 1
+                continue
+            kids = [c for c in divide(n) if c[4]]
+            for c in kids:                      # push_front n1..n4
+                nodes.insert(0, c)
+                if len(c[4]) > 1:
+                    n_expand += 1
+                    pairs.append(c)
+            i += len(kids)
+            del nodes[i]                        # erase the divided node
+        if len(nodes) >= N or len(nodes) == prev:
+            finish = True
+        elif len(nodes) + 3 * n_expand > N:
+            while not finish:
+                prev = len(nodes)
+                todo = sorted(pairs, key=lambda c: (len(c[4]), c[5]))
+                pairs = []
+                for p in reversed(todo):
+                    for c in [c for c in divide(p) if c[4]]:
+                        nodes.insert(0, c)
+                        if len(c[4]) > 1:
+                            pairs.append(c)
+                    nodes.remove(p)
+                    if len(nodes) >= N:
+                        break
+                if len(nodes) >= N or len(nodes) == prev:
+                    finish = True
+    out = []
+    for n in nodes:
+        best = n[4][0]
+        for k in n[4][1:]:
+            if resp[k] > resp[best]:
+                best = k
+        out.append(best)
+    return np.array(out, np.int32)

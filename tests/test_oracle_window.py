@@ -101,24 +101,66 @@ def test_fast_oracle_vs_pyref(th):
 
 
 def test_orb_cells_layout():
+    """ComputeKeyPointsOctTree's grid (src/ORBextractor.cpp:803-847): C restatement == Python one;
+    752 x 480 level 0 has 24 x 14 cells of 30 x 32 pixels (+6 overlap)."""
     nd = O.orb_features_per_level(1000)
     assert nd.sum() == 1000 and nd[0] == 217
+    for shape in ((480, 752), (400, 667), (134, 210), (97, 131)):
+        c, nc, nr = O.orb_cells(*shape)
+        assert [tuple(x) for x in c] == pyref.orb_cells(*shape), shape
+    c, nc, nr = O.orb_cells(480, 752)
+    assert (nc, nr) == (24, 14) and tuple(c[0]) == (16, 16, 36, 38)
     pr = synth.orb_problem(seed=42, n_kps=1)
-    out = O.orb_fast_cells(pr["pyr"], nd)
+    out = O.orb_fast_cells(pr["pyr"])
     assert len(out["x"]) > 1000 and out["cell_base"][-1] > 8
 
 
+@pytest.mark.parametrize("seed,kind", [(43, "noise"), (91, "scene"), (92, "scene")])
+def test_distribute_octree_oracle_vs_pyref(seed, kind):
+    """DistributeOctTree (src/ORBextractor.cpp:554-797): the C restatement (linked list) equals the
+    Python one (list insert(0, ...)) on every level, at several N (incl. N above the key count and
+    the focused loop's break)."""
+    pyr = (synth.orb_problem(seed=seed, n_kps=1)["pyr"] if kind == "noise"
+           else O.orb_pyramid(synth.orb_scene(seed=seed), synth.scale_factors()))
+    f = O.orb_fast_cells(pyr)
+    for l, p in enumerate(pyr):
+        b0, b1 = f["cell_off"][f["cell_base"][l] + l], f["cell_off"][f["cell_base"][l + 1] + l]
+        kx, ky, kr = f["x"][b0:b1] - 16, f["y"][b0:b1] - 16, f["response"][b0:b1]
+        for N in (1, 37, 217, 5000):
+            a = O.distribute_octree(kx, ky, kr, 16, p.shape[1] - 16, 16, p.shape[0] - 16, N)
+            b = pyref.distribute_octree(kx, ky, kr, 16, p.shape[1] - 16, 16, p.shape[0] - 16, N)
+            assert np.array_equal(a, b), (l, N)
+            assert len(a) >= min(N, 1) and len(set(a.tolist())) == len(a)
+
+
+def test_distribute_octree_edges():
+    """Empty input, one key, duplicate keys at one position (overlapping cells) and keys on the
+    split lines."""
+    e = np.zeros(0, np.float32)
+    assert len(O.distribute_octree(e, e, e, 16, 736, 16, 464, 100)) == 0
+    one = np.array([5.0], np.float32)
+    assert O.distribute_octree(one, one, one, 16, 736, 16, 464, 100).tolist() == [0]
+    x = np.array([100, 100, 100, 360, 360, 360, 359, 0], np.float32)
+    y = np.array([50, 50, 50, 224, 224, 223, 224, 0], np.float32)
+    r = np.array([3, 9, 9, 1, 2, 2, 5, 4], np.float32)
+    for N in (1, 2, 4, 8, 100):
+        a = O.distribute_octree(x, y, r, 16, 736, 16, 464, N)
+        assert np.array_equal(a, pyref.distribute_octree(x, y, r, 16, 736, 16, 464, N)), N
+
+
 def test_orb_detect_oracle():
-    """Retention: per level at most n_desired keypoints (exactly n_desired when FAST finds enough),
-    responses of kept keypoints dominate the dropped ones of their cell."""
+    """ComputeKeyPointsOctTree: per level about n_desired keypoints (the quadtree may overshoot by
+    up to 3), all at the level's octave and inside its 16-pixel border."""
     pr = synth.orb_problem(seed=43, n_kps=1)
     nd = O.orb_features_per_level(1000)
     d = O.orb_detect(pr["pyr"], nd, synth.scale_factors())
     lo = d["level_off"]
     for l in range(8):
-        assert lo[l + 1] - lo[l] <= nd[l]
+        assert nd[l] <= lo[l + 1] - lo[l] <= nd[l] + 3
         assert (d["octave"][lo[l]:lo[l + 1]] == l).all()
-    assert lo[-1] > 900
+        h, w = pr["pyr"][l].shape
+        assert (d["x"][lo[l]:lo[l + 1]] >= 19).all() and (d["x"][lo[l]:lo[l + 1]] <= w - 20).all()
+    assert lo[-1] >= 1000
 
 
 def test_resize_oracle_vs_pyref():

@@ -102,9 +102,72 @@ def ba():
     print("ba:", out["local"]["iterations"], out["local"]["final_cost"], out["pose_only"]["iterations"])
 
 
+REF = os.environ.get("LORB_REFERENCE", "/root/reference")
+
+
+def orb_pattern():
+    """bit_pattern_31_ (src/ORBextractor.cpp:152-410, the 256 ORB test pairs the reference's
+    ORBextractor passes to computeOrbDescriptor), read from the reference tree as data."""
+    import re
+    src = open(os.path.join(REF, "src", "ORBextractor.cpp")).read()
+    body = src[src.index("bit_pattern_31_[256*4]"):]
+    body = body[body.index("{") + 1:body.index("};")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    vals = np.array([int(v) for v in body.replace("\n", " ").split(",") if v.strip()], np.int32)
+    assert vals.shape == (1024,) and vals.min() >= -13 and vals.max() <= 12
+    return vals
+
+
+def orb():
+    """The whole ORBextractor::operator() on a 752 x 480 scene at 1000 and 2000 features, with the
+    reference's own bit_pattern_31_.  The oracle's keypoints are checked at generation time against
+    the independent Python restatement (tests/pyref.py: cells, numpy FAST, list-based
+    DistributeOctTree) and its descriptors against pyref.orb_describe (libm cosf)."""
+    pattern = orb_pattern()
+    img = synth.orb_scene(seed=91)
+    sf = synth.scale_factors()
+    out = {"pattern": pattern, "image": img}
+    for nfeat in (1000, 2000):
+        nd = O.orb_features_per_level(nfeat)
+        e = O.orb_extract(img, nd, sf, pattern)
+        pyr = O.orb_pyramid(img, sf)
+        lo = e["level_off"]
+        for l in range(8):
+            kx, ky, kr = [], [], []
+            for (ix, iy, w, h), (rx, ry) in zip(pyref.orb_cells(*pyr[l].shape), pyref_cell_offsets(*pyr[l].shape)):
+                if w <= 0:
+                    continue
+                cell = pyr[l][iy:iy + h, ix:ix + w]
+                fx, fy, fr = pyref.fast(cell, 20)
+                if len(fx) == 0:
+                    fx, fy, fr = pyref.fast(cell, 7)
+                kx += list(fx + rx); ky += list(fy + ry); kr += list(fr)
+            keep = pyref.distribute_octree(kx, ky, kr, 16, pyr[l].shape[1] - 16, 16, pyr[l].shape[0] - 16, nd[l])
+            s = sf[l] if l else np.float32(1)
+            gx = (np.asarray(kx, np.float32)[keep] + np.float32(16)) * s if l else np.asarray(kx, np.float32)[keep] + 16
+            assert np.array_equal(e["x"][lo[l]:lo[l + 1]], np.asarray(gx, np.float32)), (nfeat, l)
+        d = O.orb_detect(pyr, nd, sf)
+        ang, desc = pyref.orb_describe(pyr, d["x"], d["y"], d["octave"], pattern)
+        assert np.array_equal(ang, e["angle"]) and np.array_equal(desc, e["desc"]), nfeat
+        out[f"n{nfeat}"] = dict(n_desired=nd, **{k: v for k, v in e.items()})
+    golden_io.save(os.path.join(OUT, "orb.npz"), out)
+    print("orb:", {k: len(v["x"]) for k, v in out.items() if k.startswith("n")})
+
+
+def pyref_cell_offsets(rows, cols):
+    """(j wCell, i hCell) of every cell: the offset ComputeKeyPointsOctTree adds to the FAST
+    coordinates (src/ORBextractor.cpp:865-866)."""
+    import math
+    width, height = np.float32(cols - 32), np.float32(rows - 32)
+    nc, nr = int(width / np.float32(30)), int(height / np.float32(30))
+    wc, hc = int(math.ceil(np.float32(width / np.float32(nc)))), int(math.ceil(np.float32(height / np.float32(nr))))
+    return [(j * wc, i * hc) for i in range(nr) for j in range(nc)]
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     O.build()
     hamming()
     windows()
     ba()
+    orb()
