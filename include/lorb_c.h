@@ -456,6 +456,12 @@ int lorb_ba_plan_solve(lorb_ba_plan* plan, const lorb_lm_options* opt);
 int lorb_ba_plan_read(lorb_ba_plan* plan, double* const* pose_out, double* const* point_out,
                       lorb_ba_summary* summaries);
 int lorb_ba_plan_destroy(lorb_ba_plan* plan);
+/* plan structure, first n of: [0] S half band (max over windows, scalar rows), [1] Cholesky kernel of
+ * the last solve (0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s, -1 none yet), [2] (camera, camera)
+ * blocks, [3] point groups, [4] observations, [5] points, [6] cameras, [7] 1 if some window's
+ * cameras were reordered (reverse Cuthill-McKee on the covisibility graph; outputs keep the
+ * caller's order) */
+int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n);
 /* diagnostics: Cholesky phase stamps of window 0 (non-zero only in LORB_CHOL_STAMPS builds) */
 int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8);
 

@@ -1955,6 +1955,9 @@ struct lorb_ba_plan {
   LMOpt graph_opt{};
   bool has_graph = false;
   lorb_comm* comm = nullptr;  // sharded plan (not owned)
+  // per window: camera relabelling (input pose index -> plan camera index; RCM order, §8 item 4)
+  std::vector<std::vector<int>> cam_map;
+  int chol_kind = -1;         // last launched Cholesky: 0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s
   ~lorb_ba_plan() {
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
@@ -1980,7 +1983,101 @@ int dupload(lorb_ba_plan* P, const std::vector<T>& v, T** out) {
   return LORB_OK;
 }
 
-int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win, lorb_ba_plan* P) {
+// Camera-level half band of S for a labelling (pos[c] = new index of camera c): max over cameras of
+// pos(c) - min(pos(n)) over the cameras n it shares a point with (itself included).
+int camera_band(int C, const std::vector<char>& adj, const std::vector<int>& pos) {
+  int b = 0;
+  for (int c = 0; c < C; ++c) {
+    int lo = pos[c];
+    for (int n = 0; n < C; ++n)
+      if (adj[(size_t)c * C + n]) lo = std::min(lo, pos[n]);
+    b = std::max(b, pos[c] - lo);
+  }
+  return b;
+}
+
+// Reverse Cuthill-McKee over the window's camera covisibility graph (adj: C x C, symmetric).  The
+// reference orders a LocalPoseOptimization window as [current] + GetCovisibleFrames() sorted by
+// ascending covisibility weight (src/bundle_adjust.cpp:210-220, src/frame.cpp:754-774), which
+// scatters the non-zero blocks of S over the whole matrix; RCM restores a narrow band, so the
+// banded Cholesky applies.  Deterministic: BFS from the lowest-degree unvisited camera (lowest
+// index on ties), neighbours in (degree, index) order, then reversed.  Returns old -> new; the
+// identity when RCM does not narrow the band.
+std::vector<int> camera_order(int C, const std::vector<char>& adj) {
+  std::vector<int> id(C), deg(C, 0);
+  for (int c = 0; c < C; ++c) {
+    id[c] = c;
+    for (int n = 0; n < C; ++n) deg[c] += (n != c) && adj[(size_t)c * C + n];
+  }
+  static const bool off = [] { const char* e = getenv("LORB_NO_RCM"); return e && e[0] == '1'; }();
+  if (off || C < 3) return id;
+  std::vector<int> order;
+  std::vector<char> seen(C, 0);
+  order.reserve(C);
+  while ((int)order.size() < C) {
+    int s = -1;
+    for (int c = 0; c < C; ++c)
+      if (!seen[c] && (s < 0 || deg[c] < deg[s])) s = c;
+    size_t head = order.size();
+    order.push_back(s);
+    seen[s] = 1;
+    while (head < order.size()) {
+      const int u = order[head++];
+      std::vector<int> nb;
+      for (int n = 0; n < C; ++n)
+        if (n != u && adj[(size_t)u * C + n] && !seen[n]) nb.push_back(n);
+      std::sort(nb.begin(), nb.end(), [&](int a, int b) { return deg[a] != deg[b] ? deg[a] < deg[b] : a < b; });
+      for (int n : nb) { seen[n] = 1; order.push_back(n); }
+    }
+  }
+  std::reverse(order.begin(), order.end());
+  std::vector<int> pos(C);
+  for (int i = 0; i < C; ++i) pos[order[i]] = i;
+  return camera_band(C, adj, pos) < camera_band(C, adj, id) ? pos : id;
+}
+
+int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan* P) {
+  // camera relabelling per window (RCM), applied to copies of the pose / observation arrays; the
+  // covisibility graph of a sharded window is all-reduced so every rank picks the same order
+  P->cam_map.assign(nw, {});
+  std::vector<lorb_ba_window> wins(win_in, win_in + nw);
+  std::vector<std::vector<int>> frame_buf(nw);
+  std::vector<std::vector<float>> pose_buf(nw);
+  for (int w = 0; w < nw; ++w) {
+    const lorb_ba_window& in = win_in[w];
+    const int C = std::max(in.n_poses, 0);
+    std::vector<char> adj((size_t)C * C, 0);
+    {
+      std::vector<std::vector<int>> pf(std::max(in.n_points, 0));
+      for (int k = 0; k < in.n_obs; ++k) {
+        const int p = in.obs_point[k], f = in.obs_frame[k];
+        if (p < 0 || p >= in.n_points || f < 0 || f >= C) continue;  // rejected by the main pass
+        pf[p].push_back(f);
+      }
+      for (auto& v : pf)
+        for (int a : v)
+          for (int b : v) adj[(size_t)a * C + b] = 1;
+      if (P->comm && C > 0) {
+        std::vector<double> h(adj.begin(), adj.end());
+        LORB_TRY(lorb::comm_allreduce_host(P->comm, h.data(), h.size(), LORB_OP_MAX));
+        for (size_t i = 0; i < h.size(); ++i) adj[i] = h[i] > 0.0;
+      }
+    }
+    std::vector<int> map = camera_order(C, adj);
+    bool ident = true;
+    for (int c = 0; c < C; ++c) ident &= map[c] == c;
+    P->cam_map[w] = map;
+    if (ident) continue;
+    frame_buf[w].assign(in.obs_frame, in.obs_frame + std::max(in.n_obs, 0));
+    for (int& f : frame_buf[w])
+      if (f >= 0 && f < C) f = map[f];
+    pose_buf[w].resize(6 * (size_t)C);
+    for (int c = 0; c < C; ++c)
+      for (int q = 0; q < 6; ++q) pose_buf[w][6 * (size_t)map[c] + q] = in.pose_init[6 * (size_t)c + q];
+    wins[w].obs_frame = frame_buf[w].data();
+    wins[w].pose_init = pose_buf[w].data();
+  }
+  const lorb_ba_window* win = wins.data();
   P->ctx = ctx;
   P->W = nw;
   lorb_comm* comm = P->comm;
@@ -2262,6 +2359,7 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   const bool chol_w = !force_old && P->max_bw <= 48 && sizeof(double) * (size_t)P->max_env_w <= (size_t)kLdsBudget;
   static const bool no_2s = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'w'; }();
   const bool chol_2s = chol_w && !no_2s && P->min_n16 >= 128;
+  P->chol_kind = !P->Ctot ? -1 : chol_2s ? 2 : chol_w ? 1 : 0;
   if (P->Ctot && chol_2s) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
     hipLaunchKernelGGL(k_ba_chol_2s, dim3(P->W), dim3(256), sizeof(double) * (size_t)P->max_env_w, s, d);
@@ -2336,13 +2434,16 @@ int plan_read(lorb_ba_plan* P, double* const* pose_out, double* const* point_out
               lorb_ba_summary* sums) {
   lorb_ctx* ctx = P->ctx;
   std::vector<WinState> st(P->W);
+  std::vector<std::vector<double>> hp(P->W);  // poses in plan camera order
   LORB_HIP(ctx, hipMemcpyAsync(st.data(), P->d_state, sizeof(WinState) * P->W, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   for (int w = 0; w < P->W; ++w) {
     const BaWin& bw = P->hwin[w];
     const int cur = st[w].cur;
-    if (pose_out && pose_out[w] && bw.n_poses)
-      LORB_HIP(ctx, hipMemcpyAsync(pose_out[w], P->dev.x_pose[cur] + 6 * bw.pose_base, sizeof(double) * 6 * bw.n_poses, hipMemcpyDeviceToHost, ctx->stream));
+    if (pose_out && pose_out[w] && bw.n_poses) {
+      hp[w].resize(6 * (size_t)bw.n_poses);
+      LORB_HIP(ctx, hipMemcpyAsync(hp[w].data(), P->dev.x_pose[cur] + 6 * bw.pose_base, sizeof(double) * 6 * bw.n_poses, hipMemcpyDeviceToHost, ctx->stream));
+    }
     if (point_out && point_out[w] && bw.n_points)
       LORB_HIP(ctx, hipMemcpyAsync(point_out[w], P->dev.x_pt[cur] + 3 * bw.point_base, sizeof(double) * 3 * bw.n_points, hipMemcpyDeviceToHost, ctx->stream));
     if (sums) {
@@ -2354,6 +2455,13 @@ int plan_read(lorb_ba_plan* P, double* const* pose_out, double* const* point_out
     }
   }
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  for (int w = 0; w < P->W; ++w) {  // back to the caller's pose order
+    if (hp[w].empty()) continue;
+    const std::vector<int>& map = P->cam_map[w];
+    for (int c = 0; c < P->hwin[w].n_poses; ++c)
+      for (int q = 0; q < 6; ++q)
+        pose_out[w][6 * (size_t)c + q] = hp[w][6 * (size_t)(map.empty() ? c : map[c]) + q];
+  }
   return LORB_OK;
 }
 
@@ -2405,6 +2513,18 @@ int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8) {
   if (!plan || !out8) return LORB_E_INVALID;
   LORB_HIP(plan->ctx, hipMemcpyAsync(out8, plan->dev.dbg, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, plan->ctx->stream));
   LORB_HIP(plan->ctx, hipStreamSynchronize(plan->ctx->stream));
+  return LORB_OK;
+}
+
+int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n) {
+  if (!plan || !info || n < 0) return LORB_E_INVALID;
+  int bw = 0;
+  for (const BaWin& w : plan->hwin) bw = std::max(bw, w.bw);
+  int reordered = 0;
+  for (const auto& m : plan->cam_map)
+    for (size_t c = 0; c < m.size(); ++c) reordered |= m[c] != (int)c;
+  const int32_t v[8] = {bw, plan->chol_kind, plan->n_bp, plan->n_pblk, plan->K, plan->Ptot, plan->Ctot, reordered};
+  for (int i = 0; i < n && i < 8; ++i) info[i] = v[i];
   return LORB_OK;
 }
 

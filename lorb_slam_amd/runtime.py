@@ -327,6 +327,13 @@ class BAPlan:
         self.ctx.check(lib().lorb_ba_plan_read(self._p, pp, qp, summ), "lorb_ba_plan_read")
         return poses, pts, [summ[i].as_dict() for i in range(len(wins))]
 
+    def info(self):
+        """lorb_ba_plan_info: structure of the plan and the Cholesky kernel of the last solve."""
+        v = (C.c_int32 * 8)()
+        self.ctx.check(lib().lorb_ba_plan_info(self._p, v, C.c_int32(8)), "lorb_ba_plan_info")
+        keys = ("band", "cholesky", "blocks", "point_groups", "observations", "points", "cameras", "reordered")
+        return dict(zip(keys, [int(x) for x in v]))
+
     def close(self):
         if self._p:
             lib().lorb_ba_plan_destroy(self._p)

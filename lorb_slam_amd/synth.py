@@ -136,6 +136,29 @@ def ba_window(seed=3, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400, obs_
                 true_poses=true_poses, true_points=pts)
 
 
+def reference_window_order(win, curr=None):
+    """The window as BA::LocalPoseOptimization assembles it (src/bundle_adjust.cpp:210-220): the
+    current keyframe first, then GetCovisibleFrames() -- the connected keyframes sorted by ASCENDING
+    covisibility weight (shared map points; src/frame.cpp:754-774, 851), ties by keyframe index.
+    Returns (window with its poses / observation frames relabelled, order) where order[i] is the
+    original pose index of window pose i."""
+    n = len(win["pose_init"])
+    curr = n - 1 if curr is None else curr
+    opt = win["obs_frame"] >= 0
+    pts_of = [set(win["obs_point"][opt & (win["obs_frame"] == f)].tolist()) for f in range(n)]
+    weight = [len(pts_of[curr] & pts_of[f]) for f in range(n)]
+    others = sorted((f for f in range(n) if f != curr), key=lambda f: (weight[f], f))
+    order = np.array([curr] + others, np.int64)
+    pos = np.empty(n, np.int64)
+    pos[order] = np.arange(n)
+    out = dict(win)
+    out["pose_init"] = win["pose_init"][order].copy()
+    out["obs_frame"] = np.where(opt, pos[np.maximum(win["obs_frame"], 0)], win["obs_frame"]).astype(np.int32)
+    if "true_poses" in win:
+        out["true_poses"] = win["true_poses"][order].copy()
+    return out, order
+
+
 def pose_only_batch(seed=1, n_frames=1, n_res=200, fx=FX, fy=FY, cx=CX, cy=CY, quirk=True, noise_px=0.5):
     """BA::ProjectPoseOptimization problems (SURVEY C1): n_res matched map points per frame,
     observation = reprojection + N(0, noise_px).  quirk=True passes fy_eff = fx (PoseCost uses fx
