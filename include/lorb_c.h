@@ -456,6 +456,33 @@ int lorb_ba_plan_solve(lorb_ba_plan* plan, const lorb_lm_options* opt);
 int lorb_ba_plan_read(lorb_ba_plan* plan, double* const* pose_out, double* const* point_out,
                       lorb_ba_summary* summaries);
 int lorb_ba_plan_destroy(lorb_ba_plan* plan);
+/* Device-resident plan of ONE window whose arrays already live in HBM (the LocalMapping step
+ * appends the new keyframe's observations on the device).  Sizes that change from call to call are
+ * device ints; the capacities bound them.  Observation slots k < *d_n_obs with
+ * d_obs_frame[k] < -n_fixed are unused (skipped) -- how a keyframe leaves the window without a
+ * compaction.  Observations of one point come out in slot order, as lorb_ba_window's do.  A point
+ * may be observed at most once per camera (the reference keys observations by Frame*,
+ * include/map_point.h:83).  create: capacity allocations + the first build; update: rebuild from
+ * the arrays' current contents (one small readback of counts and the camera covisibility, then
+ * sorting, point groups and Schur pair lists on the device).  solve / read / info / destroy as
+ * lorb_ba_plan_*; result_dev writes the solution as float in the caller's pose order (device
+ * pointers, either may be NULL; async). */
+typedef struct lorb_ba_window_dev {
+  int32_t n_poses, n_fixed;          /* host values */
+  int32_t max_points, max_obs;       /* capacities of the arrays below */
+  const int32_t* d_n_points;         /* device: points in use (<= max_points) */
+  const int32_t* d_n_obs;            /* device: observation slots in use (<= max_obs) */
+  float fx, fy, cx, cy;
+  const float* d_pose_init;          /* n_poses x 6 (mRvec | mTvec) */
+  const float* d_fixed_pose;         /* n_fixed x 6 */
+  const float* d_point_init;         /* max_points x 3 */
+  const int32_t* d_obs_point;        /* max_obs */
+  const int32_t* d_obs_frame;        /* max_obs: >= 0 optimised pose, -1-j fixed pose j, < -n_fixed unused */
+  const float* d_obs_uv;             /* max_obs x 2 */
+} lorb_ba_window_dev;
+int lorb_ba_plan_create_dev(lorb_ctx* ctx, const lorb_ba_window_dev* win, lorb_ba_plan** out);
+int lorb_ba_plan_update_dev(lorb_ba_plan* plan, const lorb_ba_window_dev* win);
+int lorb_ba_plan_result_dev(lorb_ba_plan* plan, float* d_pose_out, float* d_point_out);
 /* plan structure, first n of: [0] S half band (max over windows, scalar rows), [1] Cholesky kernel of
  * the last solve (0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s, -1 none yet), [2] (camera, camera)
  * blocks, [3] point groups, [4] observations, [5] points, [6] cameras, [7] 1 if some window's

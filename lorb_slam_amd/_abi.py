@@ -245,6 +245,15 @@ def make_pose_batch(pb, keep):
     return s
 
 
+class BAWindowDev(C.Structure):
+    """lorb_ba_window_dev: one window whose arrays live in device memory (device pointers)."""
+    _fields_ = [("n_poses", C.c_int32), ("n_fixed", C.c_int32), ("max_points", C.c_int32), ("max_obs", C.c_int32),
+                ("d_n_points", C.c_void_p), ("d_n_obs", C.c_void_p),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("d_pose_init", C.c_void_p), ("d_fixed_pose", C.c_void_p), ("d_point_init", C.c_void_p),
+                ("d_obs_point", C.c_void_p), ("d_obs_frame", C.c_void_p), ("d_obs_uv", C.c_void_p)]
+
+
 def make_windows(wins, keep):
     arr = (BAWindow * max(1, len(wins)))()
     for i, w in enumerate(wins):

@@ -16,6 +16,8 @@
 #include "lorb_ba_math.h"
 #include "lorb_internal.h"
 
+#include <hipcub/hipcub.hpp>
+
 #include <algorithm>
 #include <cmath>
 #include <map>
@@ -1941,6 +1943,23 @@ LMOpt to_dev_opt(const lorb_lm_options* o) {
 }  // namespace
 
 // ------------------------------------------------------------------------------------------
+// device plan construction state (lorb_ba_plan_create_dev; see "Device-resident plan construction")
+struct lorb_ba_devbuild {
+  int K_cap = 0, P_cap = 0, C = 0, F = 0;
+  int* key_in = nullptr; int* key_out = nullptr; int* val_in = nullptr; int* val_out = nullptr;
+  int* ckey = nullptr; int* ckey_out = nullptr; int* cval = nullptr;
+  int* pt_cnt = nullptr;      // P_cap + 1
+  int* hdr = nullptr;         // [0] valid obs, [1] max obs per point, [2] error flags, [3] points
+  int* cov = nullptr;         // C * C
+  int* cam_cnt = nullptr;     // C
+  int* perm = nullptr;        // C: input camera -> plan camera
+  int* gstart = nullptr;      // group starts
+  void* tmp = nullptr; size_t tmp_bytes = 0;
+  int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0, gs_cap = 0;
+  std::vector<int> h_hdr, h_cov, h_cam;
+  int* pinned = nullptr; size_t pinned_n = 0;
+};
+
 struct lorb_ba_plan {
   lorb_ctx* ctx = nullptr;
   int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_bp = 0, n_pairs = 0;
@@ -1958,7 +1977,12 @@ struct lorb_ba_plan {
   // per window: camera relabelling (input pose index -> plan camera index; RCM order, §8 item 4)
   std::vector<std::vector<int>> cam_map;
   int chol_kind = -1;         // last launched Cholesky: 0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s
+  lorb_ba_devbuild* devb = nullptr;  // device-built plan (lorb_ba_plan_create_dev)
   ~lorb_ba_plan() {
+    if (devb) {
+      if (devb->pinned) (void)hipHostFree(devb->pinned);
+      delete devb;
+    }
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
     for (void* p : allocs) (void)hipFree(p);
@@ -2467,6 +2491,401 @@ int plan_read(lorb_ba_plan* P, double* const* pose_out, double* const* point_out
 
 }  // namespace
 
+// ==========================================================================================
+// Device-resident plan construction: the plan of ONE window built from
+// observation arrays that already live in HBM (the LocalMapping step appends the new keyframe's
+// matches on the device).  The host keeps only the camera-level decisions: one small readback
+// (observation / point counts, per-camera counts and the C x C covisibility counts) per build, then
+// the camera order (RCM), the (camera, camera) block list, band and kernel choice.  Everything
+// per observation, per point and per pair is built by kernels:
+//   k_db_keys    validity + point keys of the observation slots, per-point counts
+//   radix sort   observations by point (stable: the caller's order within a point)
+//   k_db_cov     per point: camera-pair covisibility counts, per-camera counts, duplicate check
+//   k_db_gather  point-sorted structure arrays, camera keys (RCM labels)
+//   radix sort   optimised observations by camera (stable) -> camera-major slots
+//   k_db_groups  point groups of <= kGB observations (weights k + 1, fixed-size bins)
+//   k_db_pairs   per block pair: the points both cameras observe (sorted-list intersection)
+//   k_db_init    initial values (float -> double, camera relabelling)
+// ==========================================================================================
+
+namespace {
+
+
+
+__global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int K_cap, int P_cap, int C, int F,
+                                                 int* __restrict__ key, int* __restrict__ val,
+                                                 int* __restrict__ pt_cnt, int* __restrict__ hdr) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K_cap) return;
+  const int n_obs = *w.d_n_obs, n_pt = *w.d_n_points;
+  int p = P_cap;
+  if (k < n_obs) {
+    const int q = w.d_obs_point[k], f = w.d_obs_frame[k];
+    if (f >= -F && f < C) {
+      if (q < 0 || q >= n_pt) atomicOr(&hdr[2], 1);
+      else { p = q; atomicAdd(&pt_cnt[q], 1); atomicAdd(&hdr[0], 1); }
+    } else if (f >= C) {
+      atomicOr(&hdr[2], 2);
+    }
+  }
+  key[k] = p;
+  val[k] = k;
+  if (k == 0) hdr[3] = n_pt;
+}
+
+// one thread per point: covisibility of its optimised cameras (ordered pairs, both directions),
+// per-camera counts, largest observation count, a camera seen twice by one point (error 4)
+__global__ __launch_bounds__(256) void k_db_cov(lorb_ba_window_dev w, int C, const int* __restrict__ pt_off,
+                                                const int* __restrict__ val, int* __restrict__ cov,
+                                                int* __restrict__ cam_cnt, int* __restrict__ hdr) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= *w.d_n_points) return;
+  const int a0 = pt_off[p], a1 = pt_off[p + 1];
+  atomicMax(&hdr[1], a1 - a0);
+  for (int a = a0; a < a1; ++a) {
+    const int fa = w.d_obs_frame[val[a]];
+    if (fa < 0) continue;
+    atomicAdd(&cam_cnt[fa], 1);
+    for (int b = a0; b < a1; ++b) {
+      const int fb = w.d_obs_frame[val[b]];
+      if (fb < 0) continue;
+      if (b != a && fb == fa) atomicOr(&hdr[2], 4);
+      if (b != a) atomicAdd(&cov[fa * C + fb], 1);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d, int K, int C,
+                                                   const int* __restrict__ key, const int* __restrict__ val,
+                                                   const int* __restrict__ perm, int* __restrict__ ckey,
+                                                   int* __restrict__ cval) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= K) return;
+  const int k = val[e], f = w.d_obs_frame[k];
+  const int c = f >= 0 ? perm[f] : -1;
+  const_cast<int*>(d.obs_pt)[e] = key[e];
+  const_cast<int*>(d.obs_cam)[e] = c;
+  const_cast<int*>(d.obs_fix)[e] = f >= 0 ? -1 : -1 - f;
+  const_cast<double2*>(d.obs_uv)[e] = make_double2(w.d_obs_uv[2 * k], w.d_obs_uv[2 * k + 1]);
+  const_cast<int*>(d.obs_cm)[e] = -1;
+  ckey[e] = c >= 0 ? c : C;
+  cval[e] = e;
+}
+
+__global__ __launch_bounds__(256) void k_db_obscm(BaDev d, int n_opt) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < n_opt) const_cast<int*>(d.obs_cm)[d.cam_obs[j]] = j;
+}
+
+// point groups: point p (weight k_p + 1, exclusive weight prefix off[p] + p) goes to group
+// (off[p] + p) / S with S = kGB - max_weight + 1, so a group holds <= kGB observations and points
+__global__ __launch_bounds__(256) void k_db_group_starts(const int* __restrict__ pt_off, int P, int S,
+                                                         int* __restrict__ gstart) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  const int g = (pt_off[p] + p) / S;
+  if (p == 0 || (pt_off[p - 1] + p - 1) / S != g) gstart[g] = p;
+}
+
+__global__ __launch_bounds__(64) void k_db_groups(BaDev d, const int* __restrict__ pt_off, int P, int G,
+                                                  int* __restrict__ gstart) {
+  if (threadIdx.x != 0) return;
+  int nxt = P;
+  for (int g = G - 1; g >= 0; --g) {  // empty bins start where the next non-empty one does
+    const int s = gstart[g] < 0 ? nxt : gstart[g];
+    PBlk b;
+    b.win = 0; b.p0 = s; b.cnt = nxt - s; b.o0 = pt_off[s]; b.no = pt_off[nxt] - pt_off[s];
+    const_cast<PBlk*>(d.pblk)[g] = b;
+    nxt = s;
+  }
+}
+
+// one workgroup per (camera, camera) block: its pair list in point order
+__global__ __launch_bounds__(256) void k_db_pairs(BaDev d) {
+  __shared__ int wsum[4];
+  const BlockPair B = d.bp[blockIdx.x];
+  const int h0 = d.cam_obs_off[B.ch], h1 = d.cam_obs_off[B.ch + 1];
+  const int l0 = d.cam_obs_off[B.cl], l1 = d.cam_obs_off[B.cl + 1];
+  int2* out = const_cast<int2*>(d.pairs) + B.off;
+  int run = 0;
+  for (int base = h0; base < h1; base += 256) {
+    const int i = base + threadIdx.x;
+    int j = -1;
+    if (i < h1) {
+      if (B.ch == B.cl) {
+        j = i;
+      } else {
+        const int p = d.obs_pt[d.cam_obs[i]];
+        int lo = l0, hi = l1;
+        while (lo < hi) {
+          const int m = (lo + hi) >> 1;
+          if (d.obs_pt[d.cam_obs[m]] < p) lo = m + 1; else hi = m;
+        }
+        if (lo < l1 && d.obs_pt[d.cam_obs[lo]] == p) j = lo;
+      }
+    }
+    int tot;
+    const int ex = lorb::block_excl_scan<256>(j >= 0 ? 1 : 0, wsum, &tot);
+    if (j >= 0 && run + ex < B.cnt) out[run + ex] = make_int2(i, j);
+    run += tot;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_db_init(lorb_ba_window_dev w, BaDev d, int C, int F, int P,
+                                                 const int* __restrict__ perm, const int* __restrict__ cam_cnt) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < 6 * C) {
+    const int c = i / 6, q = i - 6 * c;
+    d.x_init_pose[6 * perm[c] + q] = (double)w.d_pose_init[i];
+    if (q == 0) const_cast<int*>(d.cam_active)[perm[c]] = cam_cnt[c] > 0;
+    if (q == 0) const_cast<int*>(d.cam_win)[c] = 0;
+  }
+  if (i < 6 * F) const_cast<double*>(d.fixed_pose)[i] = (double)w.d_fixed_pose[i];
+  for (int k = i; k < 3 * P; k += gridDim.x * 256) d.x_init_pt[k] = (double)w.d_point_init[k];
+}
+
+// plan camera order -> caller order, as float (Frame::SetPose / MapPoint::SetWorldPos write-back)
+__global__ __launch_bounds__(256) void k_db_result(BaDev d, int C, int P, const int* __restrict__ perm,
+                                                   float* __restrict__ pose_out, float* __restrict__ pt_out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int cur = d.st[0].cur;
+  if (pose_out && i < 6 * C) {
+    const int c = i / 6, q = i - 6 * c;
+    pose_out[i] = (float)d.x_pose[cur][6 * perm[c] + q];
+  }
+  if (pt_out)
+    for (int k = i; k < 3 * P; k += gridDim.x * 256) pt_out[k] = (float)d.x_pt[cur][k];
+}
+
+int bits_for(int v) {
+  int b = 1;
+  while ((1 << b) <= v) ++b;
+  return b;
+}
+
+}  // namespace
+
+namespace {
+
+template <typename T>
+int grow(lorb_ba_plan* P, T** ptr, int* cap, size_t need) {
+  if (*ptr && (size_t)*cap >= need) return LORB_OK;
+  if (*ptr) {
+    LORB_HIP(P->ctx, hipStreamSynchronize(P->ctx->stream));
+    LORB_HIP(P->ctx, hipFree(*ptr));
+    auto it = std::find(P->allocs.begin(), P->allocs.end(), (void*)*ptr);
+    if (it != P->allocs.end()) P->allocs.erase(it);
+  }
+  const size_t n = std::max<size_t>(need + need / 4, 16);
+  LORB_TRY(dalloc(P, n, ptr));
+  *cap = (int)n;
+  P->has_graph = false;  // kernel arguments changed
+  return LORB_OK;
+}
+
+// capacity allocations (once per plan)
+int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
+  lorb_ba_devbuild& b = *P->devb;
+  b.K_cap = w->max_obs; b.P_cap = w->max_points; b.C = w->n_poses; b.F = w->n_fixed;
+  const size_t K = (size_t)std::max(b.K_cap, 1), Pn = (size_t)std::max(b.P_cap, 1), C = (size_t)std::max(b.C, 1);
+  BaDev& d = P->dev;
+  LORB_TRY(dalloc(P, K, &b.key_in)); LORB_TRY(dalloc(P, K, &b.key_out));
+  LORB_TRY(dalloc(P, K, &b.val_in)); LORB_TRY(dalloc(P, K, &b.val_out));
+  LORB_TRY(dalloc(P, K, &b.ckey)); LORB_TRY(dalloc(P, K, &b.ckey_out)); LORB_TRY(dalloc(P, K, &b.cval));
+  LORB_TRY(dalloc(P, Pn + 1, &b.pt_cnt)); LORB_TRY(dalloc(P, (size_t)8, &b.hdr));
+  LORB_TRY(dalloc(P, C * C, &b.cov)); LORB_TRY(dalloc(P, C, &b.cam_cnt)); LORB_TRY(dalloc(P, C, &b.perm));
+  int *a_pt, *a_cam, *a_fix, *a_cm, *a_co, *a_camobs, *a_win, *a_act, *a_ptoff;
+  double2* a_uv;
+  double* a_fixp;
+  LORB_TRY(dalloc(P, K, &a_pt)); LORB_TRY(dalloc(P, K, &a_cam)); LORB_TRY(dalloc(P, K, &a_fix));
+  LORB_TRY(dalloc(P, K, &a_uv)); LORB_TRY(dalloc(P, K, &a_cm)); LORB_TRY(dalloc(P, K, &a_camobs));
+  LORB_TRY(dalloc(P, C + 1, &a_co)); LORB_TRY(dalloc(P, C, &a_win)); LORB_TRY(dalloc(P, C, &a_act));
+  LORB_TRY(dalloc(P, Pn + 1, &a_ptoff)); LORB_TRY(dalloc(P, (size_t)std::max(b.F, 1) * 6, &a_fixp));
+  d.obs_pt = a_pt; d.obs_cam = a_cam; d.obs_fix = a_fix; d.obs_uv = a_uv; d.obs_cm = a_cm; d.cam_obs = a_camobs;
+  d.cam_obs_off = a_co; d.cam_win = a_win; d.cam_active = a_act; d.pt_obs_off = a_ptoff; d.fixed_pose = a_fixp;
+  LORB_TRY(dalloc(P, C * 6, &d.x_init_pose)); LORB_TRY(dalloc(P, Pn * 3, &d.x_init_pt));
+  LORB_TRY(dalloc(P, C * 6, &d.x_pose[0])); LORB_TRY(dalloc(P, C * 6, &d.x_pose[1]));
+  LORB_TRY(dalloc(P, Pn * 3, &d.x_pt[0])); LORB_TRY(dalloc(P, Pn * 3, &d.x_pt[1]));
+  LORB_TRY(dalloc(P, C * 6, &d.scale_pose)); LORB_TRY(dalloc(P, Pn * 3, &d.scale_pt));
+  LORB_TRY(dalloc(P, Pn * 6, &d.ete)); LORB_TRY(dalloc(P, Pn * 3, &d.etb)); LORB_TRY(dalloc(P, Pn * 6, &d.pinv));
+  const size_t n = 6 * C, lin_n = C * 27 + 2, solve_n = n * n + n + 1;
+  double *lin, *mx, *sol, *stp;
+  LORB_TRY(dalloc(P, lin_n, &lin)); LORB_TRY(dalloc(P, (size_t)1, &mx));
+  LORB_TRY(dalloc(P, solve_n, &sol)); LORB_TRY(dalloc(P, (size_t)3, &stp));
+  d.U = lin; d.V = lin + C * 21; d.wlin = lin + C * 27; d.wmax = mx;
+  d.U_part = d.U; d.V_part = d.V; d.wlin_part = d.wlin; d.wmax_part = d.wmax;
+  d.env = sol; d.env_part = sol;  // rhs / wfail are placed after the band at each build
+  d.wstep = stp; d.wstep_part = stp;
+  d.sharded = 0; d.rank0 = 1;
+  LORB_TRY(dalloc(P, C, &d.cam_gmax));
+  LORB_TRY(dalloc(P, K * 2, &d.obs_r)); LORB_TRY(dalloc(P, K * 6, &d.obs_Jp)); LORB_TRY(dalloc(P, K * 12, &d.obs_Jc));
+  LORB_TRY(dalloc(P, K * 2, &d.cam_r));
+  LORB_TRY(dalloc(P, C, &d.rot_lin)); LORB_TRY(dalloc(P, C, &d.rot_cand));
+  LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
+  LORB_TRY(dalloc(P, n, &d.ycam));
+  LORB_TRY(dalloc(P, (size_t)8, &d.dbg));
+  LORB_TRY(dalloc(P, (size_t)1, &P->d_state)); d.st = P->d_state;
+  BaWin* dwin;
+  LORB_TRY(dalloc(P, (size_t)1, &dwin)); d.win = dwin;
+  size_t t1 = 0, t2 = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, t1, b.key_in, b.key_out, b.val_in, b.val_out, (int)K, 0, 31,
+                                         ctx->stream) != hipSuccess ||
+      hipcub::DeviceScan::ExclusiveSum(nullptr, t2, b.pt_cnt, a_ptoff, (int)Pn + 1, ctx->stream) != hipSuccess)
+    return lorb::set_error(ctx, LORB_E_DEVICE, "hipcub temp-storage query failed");
+  b.tmp_bytes = std::max(t1, t2);
+  LORB_HIP(ctx, hipMalloc(&b.tmp, b.tmp_bytes));
+  P->allocs.push_back(b.tmp);
+  P->W = 1;
+  P->hwin.assign(1, BaWin{});
+  return LORB_OK;
+}
+
+int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
+  lorb_ba_devbuild& b = *P->devb;
+  if (w->n_poses != b.C || w->n_fixed != b.F || w->max_obs > b.K_cap || w->max_points > b.P_cap)
+    return lorb::set_error(ctx, LORB_E_INVALID, "window shape differs from the plan's (cameras %d/%d, fixed %d/%d)",
+                           w->n_poses, b.C, w->n_fixed, b.F);
+  hipStream_t s = ctx->stream;
+  BaDev& d = P->dev;
+  const int C = b.C, F = b.F, Kc = w->max_obs;
+  // 1. observation keys, per-point counts; sort by point (stable); point offsets
+  LORB_HIP(ctx, hipMemsetAsync(b.pt_cnt, 0, sizeof(int) * ((size_t)b.P_cap + 1), s));
+  LORB_HIP(ctx, hipMemsetAsync(b.hdr, 0, sizeof(int) * 8, s));
+  LORB_HIP(ctx, hipMemsetAsync(b.cov, 0, sizeof(int) * (size_t)std::max(C * C, 1), s));
+  LORB_HIP(ctx, hipMemsetAsync(b.cam_cnt, 0, sizeof(int) * (size_t)std::max(C, 1), s));
+  if (Kc > 0) {
+    hipLaunchKernelGGL(k_db_keys, dim3(lorb::ceil_div(Kc, 256)), dim3(256), 0, s, *w, Kc, b.P_cap, C, F, b.key_in,
+                       b.val_in, b.pt_cnt, b.hdr);
+    size_t tb = b.tmp_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(b.tmp, tb, b.key_in, b.key_out, b.val_in, b.val_out, Kc, 0,
+                                           bits_for(b.P_cap), s) != hipSuccess)
+      return lorb::set_error(ctx, LORB_E_DEVICE, "radix sort (points) failed");
+  }
+  {
+    size_t tb = b.tmp_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(b.tmp, tb, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1, s) != hipSuccess)
+      return lorb::set_error(ctx, LORB_E_DEVICE, "scan (point offsets) failed");
+  }
+  hipLaunchKernelGGL(k_db_cov, dim3(lorb::ceil_div(std::max(b.P_cap, 1), 256)), dim3(256), 0, s, *w, C, d.pt_obs_off,
+                     b.val_out, b.cov, b.cam_cnt, b.hdr);
+  LORB_CHECK_LAUNCH(ctx);
+  // 2. the one readback: counts and the covisibility structure
+  const size_t nrb = 8 + (size_t)C + (size_t)C * C;
+  if (b.pinned_n < nrb) {
+    if (b.pinned) (void)hipHostFree(b.pinned);
+    LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&b.pinned), sizeof(int) * nrb));
+    b.pinned_n = nrb;
+  }
+  LORB_HIP(ctx, hipMemcpyAsync(b.pinned, b.hdr, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
+  if (C > 0) {
+    LORB_HIP(ctx, hipMemcpyAsync(b.pinned + 8, b.cam_cnt, sizeof(int) * C, hipMemcpyDeviceToHost, s));
+    LORB_HIP(ctx, hipMemcpyAsync(b.pinned + 8 + C, b.cov, sizeof(int) * C * C, hipMemcpyDeviceToHost, s));
+  }
+  LORB_HIP(ctx, hipStreamSynchronize(s));
+  const int* H = b.pinned;
+  const int K = H[0], maxk = H[1], err = H[2], Pn = H[3];
+  if (err & 1) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a point index outside [0, n_points)");
+  if (err & 2) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a frame index >= n_poses");
+  if (err & 4) return lorb::set_error(ctx, LORB_E_INVALID, "a point observed twice by one camera");
+  if (Pn < 0 || Pn > b.P_cap) return lorb::set_error(ctx, LORB_E_INVALID, "n_points %d outside [0, %d]", Pn, b.P_cap);
+  const int* cam_cnt = H + 8;
+  const int* cov = H + 8 + C;
+  // 3. host: camera order, blocks, band, groups
+  std::vector<char> adj((size_t)C * C, 0);
+  for (int i = 0; i < C; ++i)
+    for (int j = 0; j < C; ++j) adj[(size_t)i * C + j] = (i == j && cam_cnt[i] > 0) || cov[(size_t)i * C + j] > 0;
+  const std::vector<int> map = camera_order(C, adj);
+  std::vector<int> inv(C);
+  for (int c = 0; c < C; ++c) inv[map[c]] = c;
+  P->cam_map.assign(1, map);
+  std::vector<int> cam_off(C + 1, 0);
+  for (int c = 0; c < C; ++c) cam_off[c + 1] = cam_off[c] + cam_cnt[inv[c]];
+  std::vector<BlockPair> bps;
+  std::vector<int> fc(C);
+  int n_pairs = 0;
+  for (int ch = 0; ch < C; ++ch) {  // std::map order of the host builder: (ch, cl) ascending
+    fc[ch] = ch;
+    for (int cl = 0; cl <= ch; ++cl) {
+      const int cnt = ch == cl ? cam_cnt[inv[ch]] : cov[(size_t)inv[ch] * C + inv[cl]];
+      if (ch != cl && cnt == 0) continue;
+      if (ch != cl) fc[ch] = std::min(fc[ch], cl);
+      bps.push_back(BlockPair{0, ch, cl, n_pairs, cnt});
+      n_pairs += cnt;
+    }
+  }
+  const int n = 6 * C;
+  int bwid = 0;
+  for (int c = 0; c < C; ++c) bwid = std::max(bwid, 6 * c + 5 - 6 * fc[c]);
+  if (n == 0) bwid = 0;
+  const int S = kGB - (maxk + 1) + 1;
+  if (S < 1) return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "a point with %d observations (device plans hold <= %d)", maxk, kGB - 1);
+  const int G = Pn > 0 ? (K + Pn - 1) / S + 1 : 0;
+  BaWin bw{};
+  bw.pose_base = 0; bw.n_poses = C; bw.point_base = 0; bw.n_points = Pn; bw.pblk_base = 0; bw.n_pblk = G;
+  bw.env_base = 0; bw.env_size = n * (bwid + 1); bw.n = n; bw.row_base = 0; bw.bw = bwid;
+  bw.obs_base = 0; bw.n_obs = K; bw.n_obs_all = K;
+  bw.fx = w->fx; bw.fy = w->fy; bw.cx = w->cx; bw.cy = w->cy;
+  P->hwin[0] = bw;
+  P->Ctot = C; P->Ptot = Pn; P->K = K; P->NF = F; P->n_pblk = G; P->n_bp = (int)bps.size(); P->n_pairs = n_pairs;
+  P->env_total = bw.env_size; P->n_total = n;
+  P->max_env = bw.env_size + 2 * n; P->max_bw = bwid;
+  {
+    const int n16 = (n + 15) & ~15;
+    P->max_env_w = std::max(n16 * (bwid + 1) + 2 * n16 + 64 * 18, (n16 + 48) * (bwid + 2) + 2 * 64 * 18 + 48);
+    P->min_n16 = n16 > 0 ? n16 : (1 << 30);
+  }
+  // grow-only structure buffers
+  PBlk* pb = const_cast<PBlk*>(d.pblk);
+  BlockPair* bpp = const_cast<BlockPair*>(d.bp);
+  int2* pr = const_cast<int2*>(d.pairs);
+  LORB_TRY(grow(P, &pb, &b.pblk_cap, (size_t)std::max(G, 1)));
+  LORB_TRY(grow(P, &b.gstart, &b.gs_cap, (size_t)std::max(G, 1)));
+  LORB_TRY(grow(P, &bpp, &b.bp_cap, std::max<size_t>(bps.size(), 1)));
+  LORB_TRY(grow(P, &pr, &b.pairs_cap, (size_t)std::max(n_pairs, 1)));
+  d.pblk = pb; d.bp = bpp; d.pairs = pr;
+  {
+    double* pt = d.part;
+    LORB_TRY(grow(P, &pt, &b.part_cap, (size_t)std::max(G, 1) * 8));
+    d.part = pt;
+  }
+  d.rhs = d.env + P->env_total; d.wfail = d.rhs + n;
+  d.rhs_part = d.rhs; d.wfail_part = d.wfail;
+  // uploads (pinned staging, stream-ordered)
+  std::vector<int> hperm(map.begin(), map.end());
+  LORB_HIP(ctx, hipMemcpyAsync(b.perm, hperm.data(), sizeof(int) * C, hipMemcpyHostToDevice, s));
+  LORB_HIP(ctx, hipMemcpyAsync(const_cast<int*>(d.cam_obs_off), cam_off.data(), sizeof(int) * (C + 1), hipMemcpyHostToDevice, s));
+  if (!bps.empty())
+    LORB_HIP(ctx, hipMemcpyAsync(bpp, bps.data(), sizeof(BlockPair) * bps.size(), hipMemcpyHostToDevice, s));
+  LORB_HIP(ctx, hipMemcpyAsync(const_cast<BaWin*>(d.win), &P->hwin[0], sizeof(BaWin), hipMemcpyHostToDevice, s));
+  // 4. structure kernels
+  if (K > 0) {
+    hipLaunchKernelGGL(k_db_gather, dim3(lorb::ceil_div(K, 256)), dim3(256), 0, s, *w, d, K, C, b.key_out, b.val_out,
+                       b.perm, b.ckey, b.cval);
+    size_t tb = b.tmp_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(b.tmp, tb, b.ckey, b.ckey_out, b.cval, const_cast<int*>(d.cam_obs), K, 0,
+                                           bits_for(C), s) != hipSuccess)
+      return lorb::set_error(ctx, LORB_E_DEVICE, "radix sort (cameras) failed");
+    if (cam_off[C] > 0) hipLaunchKernelGGL(k_db_obscm, dim3(lorb::ceil_div(cam_off[C], 256)), dim3(256), 0, s, d, cam_off[C]);
+  }
+  if (G > 0) {
+    LORB_HIP(ctx, hipMemsetAsync(b.gstart, 0xff, sizeof(int) * G, s));
+    hipLaunchKernelGGL(k_db_group_starts, dim3(lorb::ceil_div(Pn, 256)), dim3(256), 0, s, d.pt_obs_off, Pn, S, b.gstart);
+    hipLaunchKernelGGL(k_db_groups, dim3(1), dim3(64), 0, s, d, d.pt_obs_off, Pn, G, b.gstart);
+  }
+  if (!bps.empty()) hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), 0, s, d);
+  {
+    const int m = std::max(std::max(6 * C, 6 * F), std::min(3 * Pn, 256 * 1024));
+    if (m > 0)
+      hipLaunchKernelGGL(k_db_init, dim3(lorb::ceil_div(m, 256)), dim3(256), 0, s, *w, d, C, F, Pn, b.perm, b.cam_cnt);
+  }
+  if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
+  LORB_CHECK_LAUNCH(ctx);
+  P->has_graph = false;  // block / group counts changed: the LM graph is captured again
+  return LORB_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int lorb_ba_plan_create(lorb_ctx* ctx, int32_t n_windows, const lorb_ba_window* windows,
@@ -2492,6 +2911,42 @@ int lorb_ba_plan_create_sharded(lorb_ctx* ctx, lorb_comm* comm, int32_t n_window
   int rc = build_plan(ctx, n_windows, shards, P);
   if (rc != LORB_OK) { delete P; return rc; }
   *out = P;
+  return LORB_OK;
+}
+
+int lorb_ba_plan_create_dev(lorb_ctx* ctx, const lorb_ba_window_dev* win, lorb_ba_plan** out) {
+  if (!ctx || !win || !out || win->n_poses < 0 || win->n_fixed < 0 || win->max_points < 0 || win->max_obs < 0 ||
+      !win->d_n_points || !win->d_n_obs || (win->n_poses > 0 && !win->d_pose_init) ||
+      (win->n_fixed > 0 && !win->d_fixed_pose) || (win->max_points > 0 && !win->d_point_init) ||
+      (win->max_obs > 0 && (!win->d_obs_point || !win->d_obs_frame || !win->d_obs_uv)))
+    return LORB_E_INVALID;
+  *out = nullptr;
+  lorb_ba_plan* P = new (std::nothrow) lorb_ba_plan();
+  if (!P) return LORB_E_NOMEM;
+  P->ctx = ctx;
+  P->devb = new (std::nothrow) lorb_ba_devbuild();
+  int rc = P->devb ? dev_alloc(ctx, win, P) : LORB_E_NOMEM;
+  if (rc == LORB_OK) rc = dev_build(ctx, win, P);
+  if (rc != LORB_OK) { delete P; return rc; }
+  *out = P;
+  return LORB_OK;
+}
+
+int lorb_ba_plan_update_dev(lorb_ba_plan* plan, const lorb_ba_window_dev* win) {
+  if (!plan || !win) return LORB_E_INVALID;
+  if (!plan->devb) return lorb::set_error(plan->ctx, LORB_E_INVALID, "not a device-built plan");
+  return dev_build(plan->ctx, win, plan);
+}
+
+int lorb_ba_plan_result_dev(lorb_ba_plan* plan, float* d_pose_out, float* d_point_out) {
+  if (!plan) return LORB_E_INVALID;
+  if (!plan->devb) return lorb::set_error(plan->ctx, LORB_E_INVALID, "not a device-built plan");
+  const int C = plan->Ctot, Pn = plan->Ptot;
+  const int m = std::max(6 * C, std::min(3 * Pn, 256 * 1024));
+  if (m > 0)
+    hipLaunchKernelGGL(k_db_result, dim3(lorb::ceil_div(m, 256)), dim3(256), 0, plan->ctx->stream, plan->dev, C, Pn,
+                       plan->devb->perm, d_pose_out, d_point_out);
+  LORB_CHECK_LAUNCH(plan->ctx);
   return LORB_OK;
 }
 

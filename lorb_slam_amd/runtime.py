@@ -346,6 +346,49 @@ class BAPlan:
             pass
 
 
+class BAPlanDev(BAPlan):
+    """Device-built plan (lorb_ba_plan_create_dev / _update_dev) of one window held in device
+    memory: `arrays` is a dict of DeviceArrays (n_points, n_obs: 1 int each; pose_init, fixed_pose,
+    point_init, obs_point, obs_frame, obs_uv), `intr` = (fx, fy, cx, cy)."""
+
+    def __init__(self, ctx, arrays, n_poses, n_fixed, intr):  # noqa: D107 -- BAPlan's fields, another constructor
+        self.ctx, self.comm, self._keep = ctx, None, A.KeepAlive()
+        self._p = C.c_void_p()
+        self.n_poses, self.n_fixed = n_poses, n_fixed
+        self.win = self._window(arrays, intr)
+        ctx.check(lib().lorb_ba_plan_create_dev(ctx.handle, C.byref(self.win), C.byref(self._p)), "lorb_ba_plan_create_dev")
+
+    def _window(self, a, intr):
+        self.arrays = a
+        w = A.BAWindowDev()
+        w.n_poses, w.n_fixed = self.n_poses, self.n_fixed
+        w.max_points, w.max_obs = a["point_init"].shape[0], a["obs_point"].shape[0]
+        w.d_n_points, w.d_n_obs = a["n_points"].ptr, a["n_obs"].ptr
+        w.fx, w.fy, w.cx, w.cy = (float(v) for v in intr)
+        for k in ("pose_init", "fixed_pose", "point_init", "obs_point", "obs_frame", "obs_uv"):
+            setattr(w, "d_" + k, a[k].ptr)
+        return w
+
+    def update(self, arrays=None, intr=None):
+        if arrays is not None:
+            self.win = self._window(arrays, intr if intr is not None else (self.win.fx, self.win.fy, self.win.cx, self.win.cy))
+        self.ctx.check(lib().lorb_ba_plan_update_dev(self._p, C.byref(self.win)), "lorb_ba_plan_update_dev")
+
+    def read(self):
+        info = self.info()
+        poses = np.zeros((self.n_poses, 6)); pts = np.zeros((max(info["points"], 1), 3))
+        pp = (A.f64p * 1)(A.ptr(poses, C.c_double))
+        qp = (A.f64p * 1)(A.ptr(pts, C.c_double))
+        summ = (A.BASummary * 1)()
+        self.ctx.check(lib().lorb_ba_plan_read(self._p, pp, qp, summ), "lorb_ba_plan_read")
+        return [poses], [pts[:info["points"]]], [summ[0].as_dict()]
+
+    def result_dev(self, d_pose, d_points):
+        self.ctx.check(lib().lorb_ba_plan_result_dev(self._p, d_pose.ptr if d_pose is not None else None,
+                                                     d_points.ptr if d_points is not None else None),
+                       "lorb_ba_plan_result_dev")
+
+
 Context.ba_pose_only = _ba_pose_only
 Context.ba_local = _ba_local
 

@@ -185,3 +185,92 @@ def test_local_ba_eight_c4_windows_independent(ctx):
         Ps, Xs, ss = ctx.ba_local([wins[i]], opt)
         assert np.array_equal(Pb[i], Ps[0]) and np.array_equal(Xb[i], Xs[0])
         assert sb[i]["final_cost"] == ss[0]["final_cost"]
+
+
+def _dev_window(ctx, w, extra_pts=37, extra_obs=500, shuffle_seed=None, holes=0):
+    """Upload window w into device arrays with spare capacity, optionally with the observations in
+    a shuffled slot order and `holes` unused slots (frame < -n_fixed) spread among them."""
+    rng = np.random.default_rng(shuffle_seed or 0)
+    K = len(w["obs_point"])
+    op, of, uv = w["obs_point"].copy(), w["obs_frame"].copy(), w["obs_uv"].copy()
+    order = rng.permutation(K) if shuffle_seed is not None else np.arange(K)
+    op, of, uv = op[order], of[order], uv[order]
+    if holes:
+        at = np.sort(rng.choice(K + holes, size=holes, replace=False))
+        keep = np.setdiff1d(np.arange(K + holes), at)
+        op2 = np.zeros(K + holes, np.int32); of2 = np.full(K + holes, -10 ** 6, np.int32); uv2 = np.zeros((K + holes, 2), np.float32)
+        op2[keep], of2[keep], uv2[keep] = op, of, uv
+        op2[at] = rng.integers(0, 10 ** 6, holes)  # garbage point ids in unused slots are ignored
+        op, of, uv = op2, of2, uv2
+    Kc, P = len(op) + extra_obs, len(w["point_init"])
+    pad = lambda a, n, fill=0: np.concatenate([a, np.full((n - len(a),) + a.shape[1:], fill, a.dtype)])
+    arrays = dict(n_points=ctx.to_device(np.array([P], np.int32)), n_obs=ctx.to_device(np.array([len(op)], np.int32)),
+                  pose_init=ctx.to_device(w["pose_init"].astype(np.float32)),
+                  fixed_pose=ctx.to_device(w["fixed_pose"].astype(np.float32).reshape(-1, 6)),
+                  point_init=ctx.to_device(pad(w["point_init"].astype(np.float32), P + extra_pts)),
+                  obs_point=ctx.to_device(pad(op.astype(np.int32), Kc)), obs_frame=ctx.to_device(pad(of.astype(np.int32), Kc)),
+                  obs_uv=ctx.to_device(pad(uv.astype(np.float32), Kc)))
+    return arrays, order
+
+
+@pytest.mark.parametrize("case", ["c3_sorted", "c3_shuffled_holes", "c4_reference_order", "small_ragged"])
+def test_device_built_plan(ctx, case):
+    """the plan built on the device from HBM-resident observation arrays (point
+    sort, covisibility, camera order, groups, Schur pair lists) solves to the oracle's solution
+    within 1e-5; unused slots and slot order do not matter beyond round-off."""
+    from lorb_slam_amd.runtime import BAPlanDev
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    if case.startswith("c3"):
+        w = synth.ba_window(seed=3, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400)
+    elif case == "c4_reference_order":
+        w, _ = synth.reference_window_order(synth.ba_window(seed=4, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400))
+    else:
+        w = synth.ba_window(seed=12, n_kf=7, n_pts=500, n_fixed=2, fixed_obs_per_kf=50)
+    arrays, order = _dev_window(ctx, w, shuffle_seed=5 if "shuffled" in case else None, holes=700 if "holes" in case else 0)
+    plan = BAPlanDev(ctx, arrays, len(w["pose_init"]), len(w["fixed_pose"]), w["intr"])
+    plan.solve(opt)
+    Pg, Xg, sg = plan.read()
+    info = plan.info()
+    # the oracle on the same observations in the same per-point order (stable sort by point)
+    srt = np.argsort(w["obs_point"][order], kind="stable")
+    wo = dict(w, obs_point=w["obs_point"][order][srt], obs_frame=w["obs_frame"][order][srt], obs_uv=w["obs_uv"][order][srt])
+    Po, Xo, so = O.ba_local([wo], opt)
+    plan.close()
+    for a in arrays.values():
+        a.free()
+    assert info["observations"] == len(w["obs_point"]) and info["points"] == len(w["point_init"])
+    if case != "small_ragged":
+        assert info["band"] == 47 and info["cholesky"] == 2, info
+    lm_match(sg[0], so[0])
+    assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
+    assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
+
+
+def test_device_built_plan_update_and_result(ctx):
+    """The same plan object rebuilt for a changed window (more observations, a keyframe's slots
+    marked unused) equals a fresh host plan; result_dev writes float poses in the caller's order."""
+    from lorb_slam_amd.runtime import BAPlanDev
+    opt = A.LMOptions.default(max_num_iterations=6)
+    w = synth.ba_window(seed=31, n_kf=10, n_pts=1200, n_fixed=2, fixed_obs_per_kf=100)
+    arrays, _ = _dev_window(ctx, w, extra_obs=3000)
+    plan = BAPlanDev(ctx, arrays, 10, 2, w["intr"])
+    plan.solve(opt)
+    # drop keyframe 0's observations (slots unused) and rebuild in place
+    of = w["obs_frame"].copy()
+    of[of == 0] = -10 ** 6
+    K = len(of)
+    buf = np.full(arrays["obs_frame"].shape[0], 0, np.int32); buf[:K] = of
+    arrays["obs_frame"].free(); arrays["obs_frame"] = ctx.to_device(buf)
+    plan.update(arrays)
+    plan.solve(opt)
+    Pg, Xg, sg = plan.read()
+    w2 = dict(w, obs_point=w["obs_point"][of > -10], obs_frame=of[of > -10], obs_uv=w["obs_uv"][of > -10])
+    Ph, Xh, sh = ctx.ba_local([w2], opt)
+    assert close(Pg[0], Ph[0]) and close(Xg[0], Xh[0])
+    dp = ctx.empty((10, 6), np.float32)
+    plan.result_dev(dp, None)
+    assert np.array_equal(dp.numpy(), Pg[0].astype(np.float32))
+    plan.close()
+    dp.free()
+    for a in arrays.values():
+        a.free()
