@@ -452,3 +452,97 @@ def orb_scene(seed=91, rows=H, cols=W, n_shapes=120, noise=3):
         img[y0:y0 + 60, x0:x0 + 80] += rng.normal(0, 25, (60, 80))
     img += rng.integers(-noise, noise + 1, img.shape)
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def mapping_sequence(seed=4, n_kf=50, n_fixed=5, n_new=189, obs_lens=(7, 8), steps=8, n_kps=2000,
+                     max_flips=20, noise_px=0.5, pert=(2e-3, 2e-2, 5e-2), fx=FX, fy=FY, cx=CX, cy=CY):
+    """A stationary keyframe stream for the LocalMapping full step (VERDICT r01
+    item 3).  Keyframe t: camera centre (0.1 t, 0, 0), yaw 0.01 t.  Keyframe t creates n_new map
+    points, each seen by the contiguous keyframe range [t, t + L), L in obs_lens -- so a 50-KF window
+    holds ~10k points and ~77k observations at every step.
+
+    Returns dict(init=..., steps=[...]):
+      init: the window before the first step -- optimised keyframes [0, n_kf), fixed [-n_fixed, 0):
+            pose_init (perturbed) / fixed_pose (float rvec|tvec), points (perturbed positions), their
+            descriptors, and every observation (point, keyframe id, uv) of a point seen by an
+            optimised keyframe, point-major;
+      steps[i]: keyframe n_kf + i: its tracked pose (perturbed truth; rvec|tvec and Tcw as float),
+            n_kps keypoints (x, y, 32-byte descriptors, stereo depth) -- re-observations of the
+            map's points (descriptor of the point with U{0..max_flips} flipped bits, depth -1), the
+            keyframe's new points (depth > 0: to be unprojected) and random distractors (depth -1).
+    A point's descriptor is the one of the keypoint that created it (random for initial points)."""
+    rng = np.random.default_rng(seed)
+
+    def pose_of(t):
+        aa = np.array([0.0, 0.01 * t, 0.0])
+        R = rodrigues(aa)
+        return aa, -R @ np.array([0.1 * t, 0.0, 0.0])
+
+    lmax = max(obs_lens)
+    first = -n_fixed - lmax + 1
+    last = n_kf + steps
+    # points: creation keyframe, length, true position in front of the creating camera's view
+    created, length, X = [], [], []
+    for t in range(first, last):
+        aa, tt = pose_of(t)
+        R = rodrigues(aa)
+        C = -R.T @ tt
+        for _ in range(n_new):
+            L = obs_lens[len(created) % len(obs_lens)]
+            # a point visible from keyframes t .. t+L-1: ahead of the cameras, inside the image
+            z = rng.uniform(4, 20)
+            u = rng.uniform(40, W - 40); v = rng.uniform(40, H - 40)
+            pc = np.array([(u - cx) / fx * z, (v - cy) / fy * z, z])
+            X.append(R.T @ (pc - tt))
+            created.append(t); length.append(L)
+    created = np.array(created); length = np.array(length); X = np.array(X)
+    n_all = len(X)
+    desc = random_desc(rng, n_all)
+
+    def project(t, idx):
+        aa, tt = pose_of(t)
+        Xc = X[idx] @ rodrigues(aa).T + tt
+        return np.stack([fx * Xc[:, 0] / Xc[:, 2] + cx, fy * Xc[:, 1] / Xc[:, 2] + cy], 1), Xc[:, 2]
+
+    def perturbed_pose(t):
+        aa, tt = pose_of(t)
+        return np.concatenate([aa + rng.normal(0, pert[0], 3), tt + rng.normal(0, pert[1], 3)]).astype(np.float32)
+
+    # initial window: points seen by an optimised keyframe in [0, n_kf)
+    vis0 = np.nonzero((created + length > 0) & (created < n_kf))[0]
+    obs_p, obs_k, obs_uv = [], [], []
+    for t in range(-n_fixed, n_kf):  # keyframe by keyframe, then point-major
+        j = np.nonzero((created[vis0] <= t) & (created[vis0] + length[vis0] > t))[0]
+        uv, _ = project(t, vis0[j])
+        obs_p.append(j); obs_k.append(np.full(len(j), t)); obs_uv.append(uv + rng.normal(0, noise_px, uv.shape))
+    obs_p, obs_k, obs_uv = np.concatenate(obs_p), np.concatenate(obs_k), np.concatenate(obs_uv)
+    o = np.lexsort((obs_k, obs_p))
+    obs_p, obs_k, obs_uv = obs_p[o], obs_k[o], obs_uv[o]
+    init = dict(n_kf=n_kf, n_fixed=n_fixed, intr=(np.float32(fx), np.float32(fy), np.float32(cx), np.float32(cy)),
+                pose_init=np.array([perturbed_pose(t) for t in range(n_kf)], np.float32),
+                fixed_pose=np.array([np.concatenate(pose_of(-1 - j)) for j in range(n_fixed)], np.float32),
+                point_init=(X[vis0] + rng.normal(0, pert[2], (len(vis0), 3))).astype(np.float32),
+                point_desc=desc[vis0].copy(), point_truth=vis0.copy(),
+                obs_point=np.array(obs_p, np.int32), obs_kf=np.array(obs_k, np.int32),
+                obs_uv=np.array(obs_uv, np.float32))
+    out = []
+    for i in range(steps):
+        t = n_kf + i
+        reob = np.nonzero((created < t) & (created + length > t))[0]
+        new = np.nonzero(created == t)[0]
+        uv_r, _ = project(t, reob)
+        uv_n, z_n = project(t, new)
+        n_d = max(0, n_kps - len(reob) - len(new))
+        x = np.concatenate([uv_r[:, 0], uv_n[:, 0], rng.uniform(0, W, n_d)]) + np.concatenate(
+            [rng.normal(0, noise_px, len(reob) + len(new)), np.zeros(n_d)])
+        y = np.concatenate([uv_r[:, 1], uv_n[:, 1], rng.uniform(0, H, n_d)]) + np.concatenate(
+            [rng.normal(0, noise_px, len(reob) + len(new)), np.zeros(n_d)])
+        kdesc = np.concatenate([flip_bits(rng, desc[reob], max_flips), random_desc(rng, len(new) + n_d)])
+        desc[new] = kdesc[len(reob):len(reob) + len(new)]  # a new point takes its keypoint's descriptor
+        depth = np.concatenate([np.full(len(reob), -1.0), z_n + rng.normal(0, 0.02, len(new)), np.full(n_d, -1.0)])
+        perm = rng.permutation(len(x))  # keypoints in no particular order
+        pv = perturbed_pose(t)
+        out.append(dict(kf=t, pose=pv, Tcw=Tcw_from(pv[:3].astype(np.float64), pv[3:].astype(np.float64)),
+                        x=x[perm].astype(np.float32), y=y[perm].astype(np.float32), desc=kdesc[perm].copy(),
+                        depth=depth[perm].astype(np.float32), n_reobs=len(reob), n_new=len(new)))
+    return dict(init=init, steps=out)
