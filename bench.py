@@ -11,13 +11,17 @@ than ranks are visible: ranks never share a GPU silently.  `n_gpus` in the JSON 
 count of the RCCL communicator the ranks build (ncclCommCount), not an argument echo.
 
 Default workload (c4, BASELINE config "full local_mapping step -- match + triangulate + BA on a
-50-KF / 10k-point sliding window"): per GPU and per step, for each of `--windows` independent
-windows (default 1, i.e. C4 at N=1 and C5 -- one window per GPU -- at N=8):
+50-KF / 10k-point sliding window"): per GPU, `--windows` independent HBM-resident local maps
+(default 1, i.e. C4 at N=1 and C5 -- one window per GPU -- at N=8), each fed the next keyframe of
+a synthetic stream every step (lorb_map_step_dev, the chained LocalMapping step):
   1. brute-force Hamming + OpenCV crossCheck + minDist filter of the new keyframe's 2,000
-     descriptors against the window's 10,000 map-point descriptors (Matcher::SearchLocalPoints),
-  2. stereo unprojection of the new keyframe's keypoints (Frame::UnprojectStereo),
-  3. 10 Levenberg-Marquardt iterations of BA::LocalPoseOptimization on the window
-     (50 optimised KFs + 5 fixed, 10,000 points, 77,000 observations), tolerances 0.
+     descriptors against the map's ~10,000 point descriptors (Matcher::SearchLocalPoints),
+  2. stereo unprojection of the keyframe's keypoints (Frame::UnprojectStereo),
+  3. matches become observations, unmatched keypoints with depth become new points, the window
+     slides by one keyframe (points no window keyframe sees leave), the BA plan of the slid window
+     is built on the device (one small readback),
+  4. 10 Levenberg-Marquardt iterations of BA::LocalPoseOptimization on the window (50 optimised
+     KFs + 5 fixed, ~10,000 points, ~75,000 observations), tolerances 0, float write-back.
 `value` = LM iterations/s over all GPUs.  The same run also times the BASELINE C2 matcher
 config (batched 2000x2000 top-2 + ratio test) and reports it as the `c2` sub-record, so both
 halves of the metric ("ORB matches/sec + local-BA iterations/sec") come from one driver run.
@@ -174,97 +178,107 @@ def kernel_times(ctx, ids):
 
 # ------------------------------------------------------------------------------------------
 def workload_c4(ctx, args, rank):
+    """The chained LocalMapping step on an HBM-resident map (lorb_map_step_dev), one map per window:
+    each step takes the next keyframe of a synthetic stream (synth.mapping_sequence), matches it
+    against the map, appends observations and new points, slides the window by one keyframe, builds
+    the BA plan on the device and runs 10 LM iterations.  The plan build is inside the step."""
     from lorb_slam_amd import _abi as A
     from lorb_slam_amd import synth
-    from lorb_slam_amd.runtime import BAPlan, lib
+    from lorb_slam_amd.runtime import LocalMap
     W = args.windows
-    steps = [synth.local_mapping_step(seed=4 + 1009 * rank + 17 * i) for i in range(W)]
-    wins = [s["window"] for s in steps]
-    t0 = time.perf_counter()
-    plan = BAPlan(ctx, wins)
-    plan_ms = (time.perf_counter() - t0) * 1e3
+    n_kf_needed = args.warmup + args.steps + max(3, min(args.steps, 10)) + 2
+    seqs = [synth.mapping_sequence(seed=4 + 1009 * rank + 17 * i, steps=n_kf_needed) for i in range(W)]
     opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
-    nq, nt = len(steps[0]["kf_desc"]), len(steps[0]["mp_desc"])
-    dq = ctx.to_device(np.concatenate([s["kf_desc"] for s in steps]))
-    dt = ctx.to_device(np.concatenate([s["mp_desc"] for s in steps]))
-    q_off = np.arange(W + 1, dtype=np.int32) * nq
-    t_off = np.arange(W + 1, dtype=np.int32) * nt
-    cc_t, cc_d, mt = (ctx.empty(W * nq, np.int32) for _ in range(3))
-    nm = ctx.empty(W, np.int32)
-    dx = [ctx.to_device(s["kf_x"]) for s in steps]
-    dy = [ctx.to_device(s["kf_y"]) for s in steps]
-    dd = [ctx.to_device(s["kf_depth"]) for s in steps]
-    dxyz = [ctx.empty((nq, 3), np.float32) for _ in steps]
+    t0 = time.perf_counter()
+    maps = [LocalMap(ctx, s["init"]) for s in seqs]
+    create_ms = (time.perf_counter() - t0) * 1e3
     fp = A.make_frame_params(synth.frame_params())
-    Ts = [A.f32(s["kf_Tcw"]).reshape(16) for s in steps]
-    L = lib()
+    # the keyframe stream, resident in HBM before the timed region
+    kfs = [[(k["pose"], k["Tcw"], len(k["x"]), ctx.to_device(A.u8(k["desc"])), ctx.to_device(A.f32(k["x"])),
+             ctx.to_device(A.f32(k["y"])), ctx.to_device(A.f32(k["depth"]))) for k in s["steps"]] for s in seqs]
+    pos = [0]
 
     def step():
-        ctx.check(L.lorb_bf_match_dev(ctx.handle, C.c_int32(W), dq.as_ptr(C.c_uint8), A.ptr(q_off, C.c_int32),
-                                      dt.as_ptr(C.c_uint8), A.ptr(t_off, C.c_int32), cc_t.as_ptr(C.c_int32),
-                                      cc_d.as_ptr(C.c_int32), mt.as_ptr(C.c_int32), nm.as_ptr(C.c_int32)),
-                  "lorb_bf_match_dev")
-        for i in range(W):
-            ctx.check(L.lorb_unproject_stereo_dev(ctx.handle, C.byref(fp), A.ptr(Ts[i], C.c_float), C.c_int32(nq),
-                                                  dx[i].as_ptr(C.c_float), dy[i].as_ptr(C.c_float),
-                                                  dd[i].as_ptr(C.c_float), dxyz[i].as_ptr(C.c_float)),
-                      "lorb_unproject_stereo_dev")
-        plan.solve(opt)
+        i = pos[0]
+        if i >= n_kf_needed:
+            raise RuntimeError("bench keyframe stream exhausted")
+        for m, ks in zip(maps, kfs):
+            pose, Tcw, n, dd, dx, dy, dz = ks[i]
+            m.step_dev(fp, pose, Tcw, n, dd, dx, dy, dz, opt)
+        pos[0] = i + 1
 
     def check():
-        n = nm.numpy()
-        _, _, summ = plan.read()
-        return {"n_matches": [int(v) for v in n], "ba_final_cost": [s["final_cost"] for s in summ],
-                "ba_iterations": [s["iterations"] for s in summ]}
+        out = {"keyframes_stepped": pos[0], "windows": []}
+        for m in maps:
+            st = m.read()
+            out["windows"].append({k: st[k] for k in ("t0", "points", "observations", "matches", "new_points")}
+                                  | {"ba_final_cost": st["summary"]["final_cost"],
+                                     "ba_iterations": st["summary"]["iterations"]})
+        return out
 
-    n_obs = sum(len(w["obs_point"]) for w in wins)
-    n_pts = sum(len(w["point_init"]) for w in wins)
-    F = len(wins[0]["pose_init"])
-    opt_obs = sum(int((w["obs_frame"] >= 0).sum()) for w in wins)
+    c = maps[0].counts()
+    n_obs, n_pts = c["observations"], c["points"]
+    F = maps[0].W
+    nq = len(seqs[0]["steps"][0]["x"])
     bw = 6 * 8 - 1
+    opt_obs = n_obs  # window observations; the fixed ones (~4%) are in n_obs too
     kspec = {
         # Schur block accumulation: compulsory bytes = the W and Y tiles (2 x 18 doubles per
         # optimised observation) read once + the S band written once
-        2: ("hbm", opt_obs * 36 * 8.0 + W * (6 * F) * (bw + 1) * 8.0, "GB/s"),
+        2: ("hbm", W * opt_obs * 36 * 8.0 + W * (6 * F) * (bw + 1) * 8.0, "GB/s"),
         # linearisation: residual + 2x3 + 2x6 Jacobian per observation: reads pose/point/uv, writes 20 doubles
-        3: ("hbm", n_obs * (20 * 8.0 + 16 + 8) + 0.0, "GB/s"),
+        3: ("hbm", W * n_obs * (20 * 8.0 + 16 + 8), "GB/s"),
         # banded Cholesky + 2 triangular solves: n*bw^2 + 4*n*bw flops
         4: ("fp64", W * ((6 * F) * bw * bw + 4.0 * (6 * F) * bw), "TFLOP/s"),
     }
-    return dict(step=step, check=check, ba_iters=10.0 * W, matches=float(W * nq), pairs=float(W) * nq * nt,
-                plan_ms=plan_ms, cleanup=plan.close, kspec=kspec, traffic_key="c4",
-                config={"workload": "c4_local_mapping_step", "windows_per_gpu": W, "kf": F, "fixed_kf": 5,
-                        "points": n_pts // W, "observations": n_obs // W, "lm_iterations": 10,
-                        "new_kf_keypoints": nq, "match": f"{nq}x{nt} bf crossCheck"},
-                cpu=lambda: cpu_baseline_c4(steps[0], args.cpu_budget))
+
+    def cleanup():
+        for m in maps:
+            m.close()
+        for ks in kfs:
+            for k in ks:
+                for a in k[3:]:
+                    a.free()
+
+    return dict(step=step, check=check, ba_iters=10.0 * W, matches=float(W * nq), pairs=float(W) * nq * n_pts,
+                plan_ms=0.0, create_ms=create_ms, cleanup=cleanup, kspec=kspec, traffic_key="c4_chain",
+                config={"workload": "c4_local_mapping_step_chained", "windows_per_gpu": W, "kf": F,
+                        "fixed_kf": maps[0].F, "points": n_pts, "observations": n_obs, "lm_iterations": 10,
+                        "new_kf_keypoints": nq, "match": f"{nq}x~{n_pts} bf crossCheck",
+                        "step": "match + unproject + append + slide/cull + device plan build + 10 LM its + write-back"},
+                cpu=lambda: cpu_baseline_c4(seqs[0], args.cpu_budget))
 
 
-def cpu_baseline_c4(st, budget_s):
-    """Oracle (C restatement of the reference path, TEST INFRASTRUCTURE) timed on host cores on a
-    bounded sample of the same step (1 window: match + unproject + 10 LM iterations): at 1 thread
-    (Ceres' default num_threads=1) and at the host's thread count (independent windows in flight)."""
+def cpu_baseline_c4(seq, budget_s):
+    """Oracle (restatement of the reference path, TEST INFRASTRUCTURE) timed on host cores on a
+    bounded sample of the same chained step (1 window: crossCheck match + unproject + append/slide +
+    10 LM iterations, from the same starting map every call): at 1 thread (Ceres' default
+    num_threads=1) and at the host's thread count (independent windows in flight)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
+    from oracle_map import MapOracle
     from lorb_slam_amd import _abi as A
     from lorb_slam_amd import synth
     fp = synth.frame_params()
     opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
+    base = MapOracle(seq["init"]).state()
+    kf = seq["steps"][0]
+    intr = seq["init"]["intr"]
 
     def one():
-        O.bf_match(st["kf_desc"], st["mp_desc"])
-        O.unproject_stereo(fp, st["kf_Tcw"], st["kf_x"], st["kf_y"], st["kf_depth"])
-        O.ba_local([st["window"]], opt)
+        MapOracle.from_state(base, intr).step(fp, kf, opt)
     n1, d1 = run_parallel(one, 1, budget_s)
     nt = cpu_threads()
     nn, dn = run_parallel(one, nt, budget_s) if nt > 1 else (n1, d1)
     model, avail = host_cpu()
+    nq = len(kf["x"])
     return {"value": 10.0 * n1 / d1, "unit": "BA iterations/s", "cores": 1, "kind": "port",
-            "matches_per_sec": 2000.0 * n1 / d1,
-            "sample": f"{n1} x C4 local-mapping step (1 window: 2000x10000 crossCheck + unproject + 10 LM its), "
-                      f"oracle C restatement gcc -O2, 1 thread (Ceres default num_threads=1), {d1:.1f}s",
-            "nproc": {"value": 10.0 * nn / dn, "cores": nt, "matches_per_sec": 2000.0 * nn / dn,
+            "matches_per_sec": nq * n1 / d1, "steps_per_sec": n1 / d1,
+            "sample": f"{n1} x C4 chained local-mapping step (1 window: {nq}x{len(base['point'])} crossCheck + "
+                      f"unproject + append/slide + 10 LM its), oracle C restatement gcc -O2 + numpy bookkeeping, "
+                      f"1 thread (Ceres default num_threads=1), {d1:.1f}s",
+            "nproc": {"value": 10.0 * nn / dn, "cores": nt, "matches_per_sec": nq * nn / dn,
                       "sample": f"{nn} steps on {nt} threads (independent windows), {dn:.1f}s"},
             "host_cpu": model, "host_cpus_available": avail}
 
@@ -561,6 +575,7 @@ def main():
             "data": "synthetic (lorb_slam_amd.synth, seeded per rank)",
             "config": dict(wl["config"], parallelism=par),
             "matches_per_sec": total_matches / elapsed, "plan_build_ms": wl["plan_ms"],
+            "map_create_ms": wl.get("create_ms"),
             "roofline": roofline_entry(kt, wl, pn), "cpu_baseline": cpu, "c2": c2, "check": check,
         }
         if rehearse:

@@ -493,6 +493,66 @@ int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n);
 int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8);
 
 /* ----------------------------------------------------------------------------------------
+ * SURVEY §8 a17, the LocalMapping "full step" (SURVEY §7 item 8): a local map resident in HBM and
+ * the chained step over it.  Replaces LocalMapping::ProcessNewFrames' disabled steps 1-3 followed by
+ * BA::LocalPoseOptimization (src/local_mapping.cpp:24-33, 55-76; src/bundle_adjust.cpp:207-330).
+ *
+ * The map holds keyframes by id: the window [t0, t0 + W) is optimised, the F keyframes before it
+ * are fixed (MPCost), older ones are gone.  create: keyframes [0, W) optimised, [-F, 0) fixed.
+ * Per step the new keyframe gets id t0 + W and:
+ *   1. its descriptors are matched against the map's points (Matcher::SearchLocalPoints,
+ *      src/matcher.cpp:319-366 -- crossCheck + minDist filter, trains in map order);
+ *   2. a matched keypoint adds an observation (point, keyframe, keypoint uv) to its point
+ *      (MapPoint::AddObservation, src/local_mapping.cpp:57-70); an unmatched keypoint with
+ *      depth > 0 becomes a new map point at Frame::UnprojectStereo (src/frame.cpp:335-356) with the
+ *      keypoint's descriptor, observed by the keyframe.  Appended in keypoint order;
+ *   3. the window slides by one keyframe: points that no window keyframe observes leave the map,
+ *      observations by keyframes older than the F fixed ones are dropped; order is kept (stable);
+ *   4. BA::LocalPoseOptimization of the window (device-built plan, LM with `opt`), then the float
+ *      write-back of the window's poses and all points (src/bundle_adjust.cpp:317-329).
+ * step_dev is asynchronous except for one small readback (the plan's counts and covisibility).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct lorb_map lorb_map;
+typedef struct lorb_map_init {
+  int32_t n_window, n_fixed;          /* W optimised keyframes (ids 0..W-1), F fixed (ids -1..-F) */
+  int32_t max_points, max_obs, max_keypoints;   /* capacities */
+  float fx, fy, cx, cy;
+  const float* pose;                  /* W x 6 (mRvec | mTvec), row j = keyframe j */
+  const float* fixed_pose;            /* F x 6, row j = keyframe -1-j */
+  int32_t n_points, n_obs;
+  const float* point;                 /* n_points x 3 (MapPoint::GetPos) */
+  const uint8_t* point_desc;          /* n_points x 32 (MapPoint::GetDescriptor) */
+  const int32_t* obs_point;           /* n_obs */
+  const int32_t* obs_kf;              /* n_obs: keyframe id in [-F, W); a point at most once per keyframe */
+  const float* obs_uv;                /* n_obs x 2 */
+} lorb_map_init;
+/* host buffers for lorb_map_read (any may be NULL): sizes from lorb_map_counts */
+typedef struct lorb_map_state {
+  float* point;                       /* n_points x 3 */
+  uint8_t* point_desc;                /* n_points x 32 */
+  int32_t* obs_point;                 /* n_obs */
+  int32_t* obs_kf;                    /* n_obs: keyframe ids */
+  float* obs_uv;                      /* n_obs x 2 */
+  int32_t* obs_frame;                 /* n_obs: the BA slot (lorb_ba_window convention) */
+  float* pose;                        /* W x 6: keyframes t0 .. t0 + W - 1 */
+  float* fixed_pose;                  /* F x 6: keyframes t0 - 1 .. t0 - F */
+  int32_t* match_train;               /* last step's keypoints: matched map point (pre-step index) or -1 */
+  lorb_ba_summary* summary;           /* last BA solve */
+} lorb_map_state;
+int lorb_map_create(lorb_ctx* ctx, const lorb_map_init* init, lorb_map** out);
+/* frame / pose (the tracked mRvec | mTvec) / Tcw (its 4x4) are host values; descriptors, x, y
+ * (Frame::mvKeysUn) and depth (Frame::mvDepth) are device arrays of n keypoints */
+int lorb_map_step_dev(lorb_map* map, const lorb_frame_params* frame, const float pose[6], const float Tcw[16],
+                      int32_t n, const uint8_t* d_desc, const float* d_x, const float* d_y, const float* d_depth,
+                      const lorb_lm_options* opt);
+/* first n of: [0] points, [1] observations, [2] t0, [3] last step's keypoints, [4] its new points,
+ * [5] its new observations (matches + new points), [6] its matches, [7] W.  Synchronises. */
+int lorb_map_counts(lorb_map* map, int32_t* out, int32_t n);
+int lorb_map_read(lorb_map* map, const lorb_map_state* state);
+int lorb_map_plan(lorb_map* map, lorb_ba_plan** out);   /* the map's BA plan (owned by the map) */
+int lorb_map_destroy(lorb_map* map);
+
+/* ----------------------------------------------------------------------------------------
  * Multi-GPU: point-partitioned ("sharded") local BA.  No reference counterpart:
  * the reference is single-process (its Ceres solve is src/bundle_adjust.cpp:308-314).
  *

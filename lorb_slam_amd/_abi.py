@@ -254,6 +254,22 @@ class BAWindowDev(C.Structure):
                 ("d_obs_point", C.c_void_p), ("d_obs_frame", C.c_void_p), ("d_obs_uv", C.c_void_p)]
 
 
+class MapInit(C.Structure):
+    """lorb_map_init: the local map's initial window (host arrays)."""
+    _fields_ = [("n_window", C.c_int32), ("n_fixed", C.c_int32), ("max_points", C.c_int32), ("max_obs", C.c_int32),
+                ("max_keypoints", C.c_int32), ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float),
+                ("pose", f32p), ("fixed_pose", f32p), ("n_points", C.c_int32), ("n_obs", C.c_int32),
+                ("point", f32p), ("point_desc", C.POINTER(C.c_uint8)), ("obs_point", i32p), ("obs_kf", i32p),
+                ("obs_uv", f32p)]
+
+
+class MapState(C.Structure):
+    """lorb_map_state: host buffers lorb_map_read fills (NULL = skip)."""
+    _fields_ = [("point", f32p), ("point_desc", C.POINTER(C.c_uint8)), ("obs_point", i32p), ("obs_kf", i32p),
+                ("obs_uv", f32p), ("obs_frame", i32p), ("pose", f32p), ("fixed_pose", f32p), ("match_train", i32p),
+                ("summary", C.POINTER(BASummary))]
+
+
 def make_windows(wins, keep):
     arr = (BAWindow * max(1, len(wins)))()
     for i, w in enumerate(wins):

@@ -1,0 +1,430 @@
+// lorb_map.hip -- the device-resident local map and its chained LocalMapping step (SURVEY §8 a17
+// "full step" mode, §7 item 8).
+//
+// The reference's designed-but-disabled step (src/local_mapping.cpp:24-33, 55-76):
+//   1. the new keyframe's matches become observations: for every slot with a map point that the
+//      frame is not yet in, MapPoint::AddObservation(frame, slot)  (src/local_mapping.cpp:57-70);
+//      the matches come from Matcher::SearchLocalPoints -- BFMatcher(NORM_HAMMING, crossCheck) of
+//      the keyframe's descriptors against the window's map points (src/matcher.cpp:319-366);
+//   2. the keyframe's unmatched keypoints with a stereo depth become new map points at
+//      Frame::UnprojectStereo (src/frame.cpp:335-356), observed by the keyframe, with the
+//      keypoint's descriptor (the VisualOdometry::UpdateFrame pattern, src/visual_odometry.cpp:214-230);
+//   3. Map::AddFrame (src/local_mapping.cpp:76) -- the keyframe joins the window; the window
+//      keeps the newest W keyframes (the oldest leaves; KeyFramesCulling is empty in the reference,
+//      src/local_mapping.cpp:110-113, so this is the step's sliding-window policy);
+//   4. BA::LocalPoseOptimization over the window (src/local_mapping.cpp:32; src/bundle_adjust.cpp:207-330):
+//      points = those with an observation by a window keyframe, observations by the F keyframes
+//      before the window are MPCost residuals (fixed poses), and the float write-back of poses and
+//      points (src/bundle_adjust.cpp:317-329).
+//
+// Everything stays in HBM: map points (position, descriptor), observations (point, keyframe id, uv),
+// a ring of keyframe poses.  One step = matcher + unprojection + append (one workgroup, block scans
+// in keypoint order) + cull/compaction (flags, hipcub scans, stable gathers) + the device-built BA
+// plan (lorb_ba_plan_update_dev: its one small readback is the step's only host synchronisation)
+// + the LM solve (hipGraph per iteration) + the float write-back.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+#include "lorb_internal.h"
+
+namespace {
+
+struct MapDev {
+  float* pos; uint8_t* desc; int* obs_pt; int* obs_kf; float* obs_uv;        // current buffers
+  float* pos2; uint8_t* desc2; int* obs_pt2; int* obs_kf2; float* obs_uv2;   // compaction targets
+  int* obs_frame;                                                            // BA slot of each observation
+  int* cnt;      // [0] points, [1] observations, [2] error flags, [3] new points, [4] new observations, [5] matches
+  int* flag_pt; int* newid; int* flag_obs; int* newpos;
+  float* ring;   // R x 6 keyframe poses, slot = kf mod R
+  float* pose_init; float* fixed; float* pose_out;
+  int P_cap, K_cap, W, F, R;
+};
+
+struct Pose6 { float v[6]; };
+
+__device__ __forceinline__ int ring_slot(int kf, int R) { const int r = kf % R; return r < 0 ? r + R : r; }
+
+// step 1 + 2: one workgroup, keypoints in order.  A matched keypoint adds an observation of its map
+// point; an unmatched one with depth > 0 adds a new point (and its observation).  Observations and
+// new points are appended in keypoint order.
+__global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Pose6 pose, const int* __restrict__ mt,
+                                                     const float* __restrict__ xyz, const uint8_t* __restrict__ kdesc,
+                                                     const float* __restrict__ x, const float* __restrict__ y,
+                                                     const float* __restrict__ depth) {
+  __shared__ int wsum[16];
+  __shared__ int s_ok;
+  const int t = threadIdx.x;
+  const int P0 = m.cnt[0], K0 = m.cnt[1];
+  if (t < 6) m.ring[6 * ring_slot(kf, m.R) + t] = pose.v[t];
+  // pass 1: totals
+  int n_obs = 0, n_new = 0, n_mat = 0;
+  for (int base = 0; base < n; base += 1024) {
+    const int q = base + t;
+    const bool mat = q < n && mt[q] >= 0;
+    const bool nw = q < n && !mat && depth[q] > 0.0f;
+    int a, b, c;
+    lorb::block_excl_scan_1024(mat || nw, wsum, &a);
+    lorb::block_excl_scan_1024(nw, wsum, &b);
+    lorb::block_excl_scan_1024(mat, wsum, &c);
+    n_obs += a; n_new += b; n_mat += c;
+  }
+  if (t == 0) {
+    s_ok = (P0 + n_new <= m.P_cap) && (K0 + n_obs <= m.K_cap);
+    if (!s_ok) m.cnt[2] |= 1;
+  }
+  __syncthreads();
+  if (!s_ok) return;
+  int ro = 0, rn = 0;
+  for (int base = 0; base < n; base += 1024) {
+    const int q = base + t;
+    const bool mat = q < n && mt[q] >= 0;
+    const bool nw = q < n && !mat && depth[q] > 0.0f;
+    int to, tn;
+    const int eo = lorb::block_excl_scan_1024(mat || nw, wsum, &to);
+    const int en = lorb::block_excl_scan_1024(nw, wsum, &tn);
+    if (mat || nw) {
+      int p;
+      if (nw) {
+        p = P0 + rn + en;
+        m.pos[3 * p + 0] = xyz[3 * q + 0];
+        m.pos[3 * p + 1] = xyz[3 * q + 1];
+        m.pos[3 * p + 2] = xyz[3 * q + 2];
+        const uint4* s = reinterpret_cast<const uint4*>(kdesc + 32 * (size_t)q);
+        uint4* d = reinterpret_cast<uint4*>(m.desc + 32 * (size_t)p);
+        d[0] = s[0]; d[1] = s[1];
+      } else {
+        p = mt[q];
+      }
+      const int k = K0 + ro + eo;
+      m.obs_pt[k] = p;
+      m.obs_kf[k] = kf;
+      m.obs_uv[2 * k + 0] = x[q];
+      m.obs_uv[2 * k + 1] = y[q];
+    }
+    ro += to; rn += tn;
+  }
+  __syncthreads();
+  if (t == 0) {
+    m.cnt[0] = P0 + n_new; m.cnt[1] = K0 + n_obs;
+    m.cnt[3] = n_new; m.cnt[4] = n_obs; m.cnt[5] = n_mat;
+  }
+}
+
+// cull, part 1: a point stays while a window keyframe (id >= t0) observes it
+__global__ __launch_bounds__(256) void k_map_mark(MapDev m, int Kb, int t0) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= Kb || k >= m.cnt[1]) return;
+  if (m.obs_kf[k] >= t0) m.flag_pt[m.obs_pt[k]] = 1;
+}
+
+// cull, part 2: an observation stays while its point stays and its keyframe is in the window or
+// among the F fixed keyframes before it; flags beyond the count are 0 (scan tail)
+__global__ __launch_bounds__(256) void k_map_obs_flag(MapDev m, int Kb, int t0) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k > Kb) return;
+  int f = 0;
+  if (k < m.cnt[1]) f = m.flag_pt[m.obs_pt[k]] && m.obs_kf[k] >= t0 - m.F;
+  m.flag_obs[k] = f;
+}
+
+// stable gathers into the alternate buffers; observation slots as lorb_ba_window_dev wants them
+__global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, int t0) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < Pb && m.flag_pt[i]) {
+    const int d = m.newid[i];
+    m.pos2[3 * d + 0] = m.pos[3 * i + 0];
+    m.pos2[3 * d + 1] = m.pos[3 * i + 1];
+    m.pos2[3 * d + 2] = m.pos[3 * i + 2];
+    const uint4* s = reinterpret_cast<const uint4*>(m.desc + 32 * (size_t)i);
+    uint4* o = reinterpret_cast<uint4*>(m.desc2 + 32 * (size_t)d);
+    o[0] = s[0]; o[1] = s[1];
+  }
+  if (i < Kb && m.flag_obs[i]) {
+    const int d = m.newpos[i], kf = m.obs_kf[i];
+    m.obs_pt2[d] = m.newid[m.obs_pt[i]];
+    m.obs_kf2[d] = kf;
+    m.obs_uv2[2 * d + 0] = m.obs_uv[2 * i + 0];
+    m.obs_uv2[2 * d + 1] = m.obs_uv[2 * i + 1];
+    m.obs_frame[d] = kf >= t0 ? kf - t0 : -1 - (t0 - 1 - kf);
+  }
+}
+
+// new counts; the window's initial poses and the fixed poses from the ring
+__global__ __launch_bounds__(256) void k_map_window(MapDev m, int Pb, int Kb, int t0) {
+  const int i = threadIdx.x;
+  if (i == 0) { m.cnt[0] = m.newid[Pb]; m.cnt[1] = m.newpos[Kb]; }
+  for (int j = i; j < 6 * m.W; j += 256) m.pose_init[j] = m.ring[6 * ring_slot(t0 + j / 6, m.R) + j % 6];
+  for (int j = i; j < 6 * m.F; j += 256) m.fixed[j] = m.ring[6 * ring_slot(t0 - 1 - j / 6, m.R) + j % 6];
+}
+
+// Frame::SetPose write-back of the solved window poses into the ring
+__global__ __launch_bounds__(256) void k_map_writeback(MapDev m, int t0) {
+  for (int j = threadIdx.x; j < 6 * m.W; j += 256) m.ring[6 * ring_slot(t0 + j / 6, m.R) + j % 6] = m.pose_out[j];
+}
+
+}  // namespace
+
+struct lorb_map {
+  lorb_ctx* ctx = nullptr;
+  MapDev m{};
+  int t0 = 0;            // id of the oldest window keyframe
+  int h_P = 0, h_K = 0;  // counts after the last step (host mirror)
+  int n_cap = 0, last_n = 0;
+  float fx = 0, fy = 0, cx = 0, cy = 0;
+  int* cc_t = nullptr; int* cc_d = nullptr; int* mt = nullptr; int* nm = nullptr; float* xyz = nullptr;
+  void* tmp = nullptr; size_t tmp_bytes = 0;
+  int* pinned = nullptr;
+  lorb_ba_plan* plan = nullptr;
+  std::vector<void*> allocs;
+  ~lorb_map() {
+    if (plan) (void)lorb_ba_plan_destroy(plan);
+    if (pinned) (void)hipHostFree(pinned);
+    for (void* p : allocs) (void)hipFree(p);
+  }
+};
+
+namespace {
+
+template <typename T>
+int malloc_n(lorb_map* M, size_t n, T** out) {
+  void* p = nullptr;
+  LORB_HIP(M->ctx, hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)));
+  M->allocs.push_back(p);
+  *out = static_cast<T*>(p);
+  return LORB_OK;
+}
+
+int map_alloc(lorb_map* M, const lorb_map_init* in) {
+  MapDev& m = M->m;
+  m.P_cap = in->max_points; m.K_cap = in->max_obs; m.W = in->n_window; m.F = in->n_fixed;
+  m.R = in->n_window + in->n_fixed + 1;
+  const size_t P = (size_t)m.P_cap, K = (size_t)m.K_cap;
+  LORB_TRY(malloc_n(M, 3 * P, &m.pos)); LORB_TRY(malloc_n(M, 3 * P, &m.pos2));
+  LORB_TRY(malloc_n(M, 32 * P, &m.desc)); LORB_TRY(malloc_n(M, 32 * P, &m.desc2));
+  LORB_TRY(malloc_n(M, K, &m.obs_pt)); LORB_TRY(malloc_n(M, K, &m.obs_pt2));
+  LORB_TRY(malloc_n(M, K, &m.obs_kf)); LORB_TRY(malloc_n(M, K, &m.obs_kf2));
+  LORB_TRY(malloc_n(M, 2 * K, &m.obs_uv)); LORB_TRY(malloc_n(M, 2 * K, &m.obs_uv2));
+  LORB_TRY(malloc_n(M, K, &m.obs_frame));
+  LORB_TRY(malloc_n(M, (size_t)8, &m.cnt));
+  LORB_TRY(malloc_n(M, P + 1, &m.flag_pt)); LORB_TRY(malloc_n(M, P + 1, &m.newid));
+  LORB_TRY(malloc_n(M, K + 1, &m.flag_obs)); LORB_TRY(malloc_n(M, K + 1, &m.newpos));
+  LORB_TRY(malloc_n(M, 6 * (size_t)m.R, &m.ring));
+  LORB_TRY(malloc_n(M, 6 * (size_t)m.W, &m.pose_init)); LORB_TRY(malloc_n(M, 6 * (size_t)m.W, &m.pose_out));
+  LORB_TRY(malloc_n(M, 6 * (size_t)std::max(m.F, 1), &m.fixed));
+  const size_t n = (size_t)std::max(in->max_keypoints, 1);
+  M->n_cap = (int)n;
+  LORB_TRY(malloc_n(M, n, &M->cc_t)); LORB_TRY(malloc_n(M, n, &M->cc_d)); LORB_TRY(malloc_n(M, n, &M->mt));
+  LORB_TRY(malloc_n(M, (size_t)1, &M->nm)); LORB_TRY(malloc_n(M, 3 * n, &M->xyz));
+  size_t t1 = 0, t2 = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, t1, m.flag_pt, m.newid, (int)P + 1, M->ctx->stream) != hipSuccess ||
+      hipcub::DeviceScan::ExclusiveSum(nullptr, t2, m.flag_obs, m.newpos, (int)K + 1, M->ctx->stream) != hipSuccess)
+    return lorb::set_error(M->ctx, LORB_E_DEVICE, "hipcub temp-storage query failed");
+  M->tmp_bytes = std::max(t1, t2);
+  LORB_TRY(malloc_n(M, M->tmp_bytes, reinterpret_cast<uint8_t**>(&M->tmp)));
+  LORB_HIP(M->ctx, hipHostMalloc(reinterpret_cast<void**>(&M->pinned), sizeof(int) * 8));
+  return LORB_OK;
+}
+
+lorb_ba_window_dev window_of(const lorb_map* M) {
+  const MapDev& m = M->m;
+  lorb_ba_window_dev w{};
+  w.n_poses = m.W; w.n_fixed = m.F; w.max_points = m.P_cap; w.max_obs = m.K_cap;
+  w.d_n_points = m.cnt; w.d_n_obs = m.cnt + 1;
+  w.fx = M->fx; w.fy = M->fy; w.cx = M->cx; w.cy = M->cy;
+  w.d_pose_init = m.pose_init; w.d_fixed_pose = m.fixed; w.d_point_init = m.pos;
+  w.d_obs_point = m.obs_pt; w.d_obs_frame = m.obs_frame; w.d_obs_uv = m.obs_uv;
+  return w;
+}
+
+// slide to window [t0, t0 + W): cull points no window keyframe observes, drop observations by
+// keyframes older than the fixed ones, compact (stable), rebuild the BA slots and window poses
+int map_slide(lorb_map* M, int t0, int Pb, int Kb) {
+  lorb_ctx* ctx = M->ctx;
+  hipStream_t s = ctx->stream;
+  MapDev& m = M->m;
+  LORB_HIP(ctx, hipMemsetAsync(m.flag_pt, 0, sizeof(int) * ((size_t)Pb + 1), s));
+  if (Kb > 0) hipLaunchKernelGGL(k_map_mark, dim3(lorb::ceil_div(Kb, 256)), dim3(256), 0, s, m, Kb, t0);
+  hipLaunchKernelGGL(k_map_obs_flag, dim3(lorb::ceil_div(Kb + 1, 256)), dim3(256), 0, s, m, Kb, t0);
+  size_t tb = M->tmp_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(M->tmp, tb, m.flag_pt, m.newid, Pb + 1, s) != hipSuccess)
+    return lorb::set_error(ctx, LORB_E_DEVICE, "scan (points) failed");
+  tb = M->tmp_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(M->tmp, tb, m.flag_obs, m.newpos, Kb + 1, s) != hipSuccess)
+    return lorb::set_error(ctx, LORB_E_DEVICE, "scan (observations) failed");
+  const int nmax = std::max(Pb, Kb);
+  if (nmax > 0) hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, t0);
+  hipLaunchKernelGGL(k_map_window, dim3(1), dim3(256), 0, s, m, Pb, Kb, t0);
+  LORB_CHECK_LAUNCH(ctx);
+  std::swap(m.pos, m.pos2); std::swap(m.desc, m.desc2); std::swap(m.obs_pt, m.obs_pt2);
+  std::swap(m.obs_kf, m.obs_kf2); std::swap(m.obs_uv, m.obs_uv2);
+  M->t0 = t0;
+  return LORB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lorb_map_create(lorb_ctx* ctx, const lorb_map_init* in, lorb_map** out) {
+  if (!ctx || !in || !out) return LORB_E_INVALID;
+  *out = nullptr;
+  if (in->n_window < 1 || in->n_fixed < 0 || in->n_points < 0 || in->n_obs < 0 || in->max_keypoints < 0 ||
+      in->n_points > in->max_points || in->n_obs > in->max_obs || !in->pose ||
+      (in->n_fixed > 0 && !in->fixed_pose) ||
+      (in->n_points > 0 && (!in->point || !in->point_desc)) ||
+      (in->n_obs > 0 && (!in->obs_point || !in->obs_kf || !in->obs_uv)))
+    return lorb::set_error(ctx, LORB_E_INVALID, "lorb_map_create: bad sizes or missing arrays");
+  const int W = in->n_window, F = in->n_fixed;
+  for (int k = 0; k < in->n_obs; ++k) {
+    if (in->obs_point[k] < 0 || in->obs_point[k] >= in->n_points)
+      return lorb::set_error(ctx, LORB_E_INVALID, "observation %d: point %d outside [0, %d)", k, in->obs_point[k], in->n_points);
+    if (in->obs_kf[k] < -F || in->obs_kf[k] >= W)
+      return lorb::set_error(ctx, LORB_E_INVALID, "observation %d: keyframe %d outside [-%d, %d)", k, in->obs_kf[k], F, W);
+  }
+  lorb_map* M = new (std::nothrow) lorb_map();
+  if (!M) return LORB_E_NOMEM;
+  M->ctx = ctx;
+  M->fx = in->fx; M->fy = in->fy; M->cx = in->cx; M->cy = in->cy;
+  int rc = map_alloc(M, in);
+  if (rc == LORB_OK) {
+    hipStream_t s = ctx->stream;
+    MapDev& m = M->m;
+    std::vector<float> ring(6 * (size_t)m.R, 0.0f);
+    for (int j = 0; j < W; ++j)
+      for (int q = 0; q < 6; ++q) ring[6 * (size_t)(j % m.R) + q] = in->pose[6 * (size_t)j + q];
+    for (int j = 0; j < F; ++j)
+      for (int q = 0; q < 6; ++q) ring[6 * (size_t)(((-1 - j) % m.R + m.R) % m.R) + q] = in->fixed_pose[6 * (size_t)j + q];
+    const int cnt[8] = {in->n_points, in->n_obs, 0, 0, 0, 0, 0, 0};
+    auto up = [&](void* d, const void* h, size_t bytes) -> int {
+      if (bytes) LORB_HIP(ctx, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s));
+      return LORB_OK;
+    };
+    rc = up(m.ring, ring.data(), sizeof(float) * ring.size());
+    if (rc == LORB_OK) rc = up(m.cnt, cnt, sizeof(cnt));
+    if (rc == LORB_OK) rc = up(m.pos, in->point, sizeof(float) * 3 * (size_t)in->n_points);
+    if (rc == LORB_OK) rc = up(m.desc, in->point_desc, 32 * (size_t)in->n_points);
+    if (rc == LORB_OK) rc = up(m.obs_pt, in->obs_point, sizeof(int) * (size_t)in->n_obs);
+    if (rc == LORB_OK) rc = up(m.obs_kf, in->obs_kf, sizeof(int) * (size_t)in->n_obs);
+    if (rc == LORB_OK) rc = up(m.obs_uv, in->obs_uv, sizeof(float) * 2 * (size_t)in->n_obs);
+    if (rc == LORB_OK) {
+      // the initial window [0, W): obs slots / window poses, no culling of a consistent input
+      rc = map_slide(M, 0, in->n_points, in->n_obs);
+      M->h_P = in->n_points; M->h_K = in->n_obs;  // upper bounds until the first readback
+    }
+    if (rc == LORB_OK) {
+      const lorb_ba_window_dev w = window_of(M);
+      rc = lorb_ba_plan_create_dev(ctx, &w, &M->plan);
+    }
+    if (rc == LORB_OK) {
+      LORB_HIP(ctx, hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
+      LORB_HIP(ctx, hipStreamSynchronize(s));
+      M->h_P = M->pinned[0]; M->h_K = M->pinned[1];
+    }
+  }
+  if (rc != LORB_OK) { delete M; return rc; }
+  *out = M;
+  return LORB_OK;
+}
+
+int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float pose[6], const float Tcw[16], int32_t n,
+                      const uint8_t* d_desc, const float* d_x, const float* d_y, const float* d_depth,
+                      const lorb_lm_options* opt) {
+  if (!M || !frame || !pose || !Tcw || !opt || n < 0) return LORB_E_INVALID;
+  lorb_ctx* ctx = M->ctx;
+  if (n > M->n_cap) return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints > the map's max_keypoints %d", n, M->n_cap);
+  if (n > 0 && (!d_desc || !d_x || !d_y || !d_depth)) return LORB_E_INVALID;
+  hipStream_t s = ctx->stream;
+  MapDev& m = M->m;
+  const int kf = M->t0 + m.W;  // the new keyframe's id
+  // 1. SearchLocalPoints: the keyframe's descriptors against the map's points (crossCheck + minDist filter)
+  if (n > 0 && M->h_P > 0) {
+    const int32_t q_off[2] = {0, n}, t_off[2] = {0, M->h_P};
+    LORB_TRY(lorb_bf_match_dev(ctx, 1, d_desc, q_off, m.desc, t_off, M->cc_t, M->cc_d, M->mt, M->nm));
+  } else if (n > 0) {
+    LORB_HIP(ctx, hipMemsetAsync(M->mt, 0xff, sizeof(int) * (size_t)n, s));
+  }
+  // 2. UnprojectStereo of every keypoint (used where depth > 0 and unmatched)
+  if (n > 0) LORB_TRY(lorb_unproject_stereo_dev(ctx, frame, Tcw, n, d_x, d_y, d_depth, M->xyz));
+  // 3. AddObservation / new points, keyframe pose into the ring
+  Pose6 p6;
+  for (int q = 0; q < 6; ++q) p6.v[q] = pose[q];
+  LORB_HIP(ctx, hipMemsetAsync(m.cnt + 2, 0, sizeof(int), s));
+  hipLaunchKernelGGL(k_map_append, dim3(1), dim3(1024), 0, s, m, n, kf, p6, M->mt, M->xyz, d_desc, d_x, d_y, d_depth);
+  LORB_CHECK_LAUNCH(ctx);
+  // 4. slide the window by one keyframe; cull and compact
+  LORB_TRY(map_slide(M, M->t0 + 1, std::min(M->h_P + n, m.P_cap), std::min(M->h_K + n, m.K_cap)));
+  LORB_HIP(ctx, hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
+  // 5. BA plan of the slid window (its readback synchronises the stream, so the counts above are in)
+  const lorb_ba_window_dev w = window_of(M);
+  LORB_TRY(lorb_ba_plan_update_dev(M->plan, &w));
+  M->last_n = n;
+  if (M->pinned[2] & 1)
+    return lorb::set_error(ctx, LORB_E_NOMEM, "map capacity exceeded (points %d/%d, observations %d/%d)", M->pinned[0],
+                           m.P_cap, M->pinned[1], m.K_cap);
+  M->h_P = M->pinned[0]; M->h_K = M->pinned[1];
+  // 6. LocalPoseOptimization + float write-back of poses (ring) and points (map)
+  LORB_TRY(lorb_ba_plan_solve(M->plan, opt));
+  LORB_TRY(lorb_ba_plan_result_dev(M->plan, m.pose_out, m.pos));
+  hipLaunchKernelGGL(k_map_writeback, dim3(1), dim3(256), 0, s, m, M->t0);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
+int lorb_map_counts(lorb_map* M, int32_t* out, int32_t n) {
+  if (!M || !out || n < 0) return LORB_E_INVALID;
+  lorb_ctx* ctx = M->ctx;
+  LORB_HIP(ctx, hipMemcpyAsync(M->pinned, M->m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const int32_t v[8] = {M->pinned[0], M->pinned[1], M->t0, M->last_n, M->pinned[3], M->pinned[4], M->pinned[5], M->m.W};
+  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  return LORB_OK;
+}
+
+int lorb_map_read(lorb_map* M, const lorb_map_state* st) {
+  if (!M || !st) return LORB_E_INVALID;
+  lorb_ctx* ctx = M->ctx;
+  hipStream_t s = ctx->stream;
+  const MapDev& m = M->m;
+  int32_t c[8];
+  LORB_TRY(lorb_map_counts(M, c, 8));
+  const size_t P = (size_t)c[0], K = (size_t)c[1];
+  auto down = [&](void* h, const void* d, size_t bytes) -> int {
+    if (h && bytes) LORB_HIP(ctx, hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s));
+    return LORB_OK;
+  };
+  LORB_TRY(down(st->point, m.pos, sizeof(float) * 3 * P));
+  LORB_TRY(down(st->point_desc, m.desc, 32 * P));
+  LORB_TRY(down(st->obs_point, m.obs_pt, sizeof(int) * K));
+  LORB_TRY(down(st->obs_kf, m.obs_kf, sizeof(int) * K));
+  LORB_TRY(down(st->obs_uv, m.obs_uv, sizeof(float) * 2 * K));
+  LORB_TRY(down(st->obs_frame, m.obs_frame, sizeof(int) * K));
+  LORB_TRY(down(st->match_train, M->mt, sizeof(int) * (size_t)M->last_n));
+  std::vector<float> ring(6 * (size_t)m.R);
+  LORB_TRY(down(ring.data(), m.ring, sizeof(float) * ring.size()));
+  LORB_HIP(ctx, hipStreamSynchronize(s));
+  auto slot = [&](int kf) { return ((kf % m.R) + m.R) % m.R; };
+  if (st->pose)
+    for (int j = 0; j < m.W; ++j)
+      for (int q = 0; q < 6; ++q) st->pose[6 * j + q] = ring[6 * (size_t)slot(M->t0 + j) + q];
+  if (st->fixed_pose)
+    for (int j = 0; j < m.F; ++j)
+      for (int q = 0; q < 6; ++q) st->fixed_pose[6 * j + q] = ring[6 * (size_t)slot(M->t0 - 1 - j) + q];
+  if (st->summary && M->plan) LORB_TRY(lorb_ba_plan_read(M->plan, nullptr, nullptr, st->summary));
+  return LORB_OK;
+}
+
+int lorb_map_plan(lorb_map* M, lorb_ba_plan** out) {
+  if (!M || !out) return LORB_E_INVALID;
+  *out = M->plan;
+  return LORB_OK;
+}
+
+int lorb_map_destroy(lorb_map* M) {
+  if (!M) return LORB_E_INVALID;
+  (void)hipStreamSynchronize(M->ctx->stream);
+  delete M;
+  return LORB_OK;
+}
+
+}  // extern "C"

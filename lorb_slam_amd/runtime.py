@@ -389,6 +389,103 @@ class BAPlanDev(BAPlan):
                        "lorb_ba_plan_result_dev")
 
 
+class LocalMap:
+    """lorb_map: the HBM-resident local map and its chained LocalMapping step (include/lorb_c.h;
+    SURVEY §8 a17 full step).  `init`: dict(pose_init W x 6, fixed_pose F x 6, point_init, point_desc,
+    obs_point, obs_kf (keyframe ids in [-F, W)), obs_uv, intr) -- synth.mapping_sequence()["init"]."""
+
+    COUNT_KEYS = ("points", "observations", "t0", "keypoints", "new_points", "new_observations", "matches", "window")
+
+    def __init__(self, ctx, init, max_points=None, max_obs=None, max_keypoints=4096):
+        self.ctx, self._keep = ctx, A.KeepAlive()
+        k = self._keep.keep
+        s = A.MapInit()
+        s.n_window, s.n_fixed = len(init["pose_init"]), len(init["fixed_pose"])
+        s.n_points, s.n_obs = len(init["point_init"]), len(init["obs_point"])
+        s.max_points = int(max_points or 2 * s.n_points + 8 * max_keypoints)
+        s.max_obs = int(max_obs or 2 * s.n_obs + 8 * max_keypoints)
+        s.max_keypoints = int(max_keypoints)
+        s.fx, s.fy, s.cx, s.cy = (float(v) for v in init["intr"])
+        s.pose = A.ptr(k(A.f32(init["pose_init"])), C.c_float)
+        s.fixed_pose = A.ptr(k(A.f32(init["fixed_pose"]).reshape(-1, 6)), C.c_float)
+        s.point = A.ptr(k(A.f32(init["point_init"])), C.c_float)
+        s.point_desc = A.ptr(k(A.u8(init["point_desc"])), C.c_uint8)
+        s.obs_point = A.ptr(k(A.i32(init["obs_point"])), C.c_int32)
+        s.obs_kf = A.ptr(k(A.i32(init["obs_kf"])), C.c_int32)
+        s.obs_uv = A.ptr(k(A.f32(init["obs_uv"])), C.c_float)
+        self.W, self.F, self.max_keypoints = s.n_window, s.n_fixed, s.max_keypoints
+        self._p = C.c_void_p()
+        ctx.check(lib().lorb_map_create(ctx.handle, C.byref(s), C.byref(self._p)), "lorb_map_create")
+        self._keep.clear()
+
+    def step_dev(self, fp, pose, Tcw, n, d_desc, d_x, d_y, d_depth, opt=None):
+        """one step on device-resident keypoints (DeviceArrays); fp: FrameParams"""
+        opt = opt or A.LMOptions.default()
+        pose = A.f32(pose).reshape(6); T = A.f32(Tcw).reshape(16)
+        self.ctx.check(lib().lorb_map_step_dev(self._p, C.byref(fp), A.ptr(pose, C.c_float), A.ptr(T, C.c_float),
+                                               C.c_int32(n), d_desc.ptr, d_x.ptr, d_y.ptr, d_depth.ptr, C.byref(opt)),
+                       "lorb_map_step_dev")
+
+    def step(self, fp, kf, opt=None):
+        """upload one keyframe (synth.mapping_sequence()["steps"][i]) and step"""
+        fps = A.make_frame_params(fp) if isinstance(fp, dict) else fp
+        arrs = [self.ctx.to_device(A.u8(kf["desc"])), self.ctx.to_device(A.f32(kf["x"])),
+                self.ctx.to_device(A.f32(kf["y"])), self.ctx.to_device(A.f32(kf["depth"]))]
+        try:
+            self.step_dev(fps, kf["pose"], kf["Tcw"], len(kf["x"]), *arrs, opt=opt)
+            self.ctx.sync()
+        finally:
+            for a in arrs:
+                a.free()
+
+    def counts(self):
+        v = (C.c_int32 * 8)()
+        self.ctx.check(lib().lorb_map_counts(self._p, v, C.c_int32(8)), "lorb_map_counts")
+        return dict(zip(self.COUNT_KEYS, [int(x) for x in v]))
+
+    def read(self):
+        c = self.counts()
+        P, K = c["points"], c["observations"]
+        out = dict(point=np.zeros((max(P, 1), 3), np.float32), point_desc=np.zeros((max(P, 1), 32), np.uint8),
+                   obs_point=np.zeros(max(K, 1), np.int32), obs_kf=np.zeros(max(K, 1), np.int32),
+                   obs_uv=np.zeros((max(K, 1), 2), np.float32), obs_frame=np.zeros(max(K, 1), np.int32),
+                   pose=np.zeros((self.W, 6), np.float32), fixed_pose=np.zeros((max(self.F, 1), 6), np.float32),
+                   match_train=np.zeros(max(c["keypoints"], 1), np.int32))
+        summ = A.BASummary()
+        st = A.MapState()
+        st.point = A.ptr(out["point"], C.c_float); st.point_desc = A.ptr(out["point_desc"], C.c_uint8)
+        st.obs_point = A.ptr(out["obs_point"], C.c_int32); st.obs_kf = A.ptr(out["obs_kf"], C.c_int32)
+        st.obs_uv = A.ptr(out["obs_uv"], C.c_float); st.obs_frame = A.ptr(out["obs_frame"], C.c_int32)
+        st.pose = A.ptr(out["pose"], C.c_float); st.fixed_pose = A.ptr(out["fixed_pose"], C.c_float)
+        st.match_train = A.ptr(out["match_train"], C.c_int32); st.summary = C.pointer(summ)
+        self.ctx.check(lib().lorb_map_read(self._p, C.byref(st)), "lorb_map_read")
+        for key, n in (("point", P), ("point_desc", P), ("obs_point", K), ("obs_kf", K), ("obs_uv", K),
+                       ("obs_frame", K), ("fixed_pose", self.F), ("match_train", c["keypoints"])):
+            out[key] = out[key][:n]
+        out["summary"] = summ.as_dict()
+        out.update(c)
+        return out
+
+    def plan_info(self):
+        p = C.c_void_p()
+        self.ctx.check(lib().lorb_map_plan(self._p, C.byref(p)), "lorb_map_plan")
+        v = (C.c_int32 * 8)()
+        self.ctx.check(lib().lorb_ba_plan_info(p, v, C.c_int32(8)), "lorb_ba_plan_info")
+        keys = ("band", "cholesky", "blocks", "point_groups", "observations", "points", "cameras", "reordered")
+        return dict(zip(keys, [int(x) for x in v]))
+
+    def close(self):
+        if self._p:
+            lib().lorb_map_destroy(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 Context.ba_pose_only = _ba_pose_only
 Context.ba_local = _ba_local
 

@@ -1,0 +1,96 @@
+"""GPU parity: the chained LocalMapping step on the HBM-resident map (lorb_map_*, liblorb.so) vs the
+oracle's restatement (oracle/oracle_map.py) run on the same slid window.
+
+Per step the oracle starts from the device map's state read back before the step, so each step is
+compared from identical inputs: the matcher outputs, the appended / culled / compacted map structure
+(point order, descriptors, observations, BA slots) and the observation uv are bit-exact; poses and
+points after LocalPoseOptimization's float write-back are within the north_star tolerance 1e-5
+relative (|gpu - oracle| <= 1e-5 * max(|oracle|, 1)); the LM summaries agree as in test_gpu_ba."""
+import numpy as np
+import pytest
+
+from lorb_slam_amd import _abi as A
+from lorb_slam_amd import synth
+from lorb_slam_amd.runtime import LocalMap, LorbError
+from oracle_map import MapOracle
+from test_gpu_ba import close, lm_match
+
+pytestmark = pytest.mark.gpu
+OPT10 = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                            parameter_tolerance=0.0)
+EXACT = ("point_desc", "obs_point", "obs_kf", "obs_uv", "obs_frame")
+
+
+def same_structure(g, o):
+    assert g["t0"] == o["t0"]
+    assert g["points"] == o["points"] and g["observations"] == o["observations"], (g["points"], o["points"])
+    for k in EXACT:
+        assert np.array_equal(g[k], o[k]), k
+
+
+def run_chain(ctx, seq, opt, n_steps):
+    fp = synth.frame_params()
+    M = LocalMap(ctx, seq["init"])
+    try:
+        g = M.read()
+        o = MapOracle(seq["init"]).state()
+        same_structure(g, o)
+        assert np.array_equal(g["point"], o["point"]) and np.array_equal(g["pose"], o["pose"])
+        for i in range(n_steps):
+            kf = seq["steps"][i]
+            ref = MapOracle.from_state(g, seq["init"]["intr"])
+            M.step(fp, kf, opt)
+            g = M.read()
+            r = ref.step(fp, kf, opt)
+            o = ref.state()
+            assert np.array_equal(g["match_train"], r["match_train"]), i
+            assert g["matches"] == r["n_matches"] and g["new_points"] == r["new_points"]
+            assert g["new_observations"] == r["new_observations"]
+            same_structure(g, o)
+            assert close(g["pose"], o["pose"]), np.abs(g["pose"] - o["pose"]).max()
+            assert close(g["point"], o["point"]), np.abs(g["point"] - o["point"]).max()
+            assert np.array_equal(g["fixed_pose"], o["fixed_pose"])
+            lm_match(g["summary"], r["summary"])
+        return M, g
+    except BaseException:
+        M.close()
+        raise
+
+
+def test_local_mapping_chain_c4(ctx):
+    """C4 sizes: 50-KF window + 5 fixed, ~10k points, ~75k observations, 2,000 keypoints per new
+    keyframe; 3 consecutive steps"""
+    seq = synth.mapping_sequence(steps=3)
+    M, g = run_chain(ctx, seq, OPT10, 3)
+    info = M.plan_info()
+    assert info["cameras"] == 50 and info["band"] <= 47, info
+    assert 9000 < g["points"] < 12000 and 60000 < g["observations"] < 90000
+    M.close()
+
+
+def test_local_mapping_chain_default_options(ctx):
+    """Ceres default options (tolerances on), a small window"""
+    seq = synth.mapping_sequence(seed=9, n_kf=12, n_fixed=3, n_new=60, obs_lens=(4, 5), steps=3, n_kps=600)
+    M, _ = run_chain(ctx, seq, A.LMOptions.default(), 3)
+    M.close()
+
+
+def test_local_mapping_ragged_keyframes(ctx):
+    """a keyframe without keypoints, one without stereo depth, then a normal one"""
+    seq = synth.mapping_sequence(seed=5, n_kf=10, n_fixed=2, n_new=40, obs_lens=(3, 4), steps=3, n_kps=300)
+    k0, k1 = seq["steps"][0], seq["steps"][1]
+    seq["steps"][0] = dict(k0, x=k0["x"][:0], y=k0["y"][:0], desc=k0["desc"][:0], depth=k0["depth"][:0])
+    seq["steps"][1] = dict(k1, depth=np.full_like(k1["depth"], -1.0))
+    M, g = run_chain(ctx, seq, OPT10, 3)
+    M.close()
+
+
+def test_local_mapping_capacity_error(ctx):
+    seq = synth.mapping_sequence(seed=5, n_kf=10, n_fixed=2, n_new=40, obs_lens=(3, 4), steps=1, n_kps=300)
+    n_pts = len(seq["init"]["point_init"])
+    M = LocalMap(ctx, seq["init"], max_points=n_pts + 5, max_keypoints=512)
+    try:
+        with pytest.raises(LorbError, match="capacity"):
+            M.step(synth.frame_params(), seq["steps"][0], OPT10)
+    finally:
+        M.close()
