@@ -205,6 +205,9 @@ struct BaDev {
   double* part;              // n_pblk * 8 partials
   unsigned long long* dbg;   // diagnostic stamps (LORB_CHOL_STAMPS builds only)
   WinState* st;
+  // [0] point groups, [1] block pairs in use.  Launch grids may be larger (device-built plans
+  // launch at capacity so that the captured LM graph survives a rebuild); the extra workgroups exit.
+  const int* live;
 };
 
 __device__ __forceinline__ int u21(int a, int b) {  // packed upper index of 6x6 sym
@@ -268,6 +271,7 @@ __device__ __forceinline__ void block_red3(double& a, double& b, double& c, doub
 __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
   __shared__ double sh[kGB][9];
   __shared__ double red3[3][4];
+  if ((int)blockIdx.x >= d.live[0]) return;
   const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x;
   // plan-structure loads of the first chunk go out together with the window state
@@ -501,6 +505,7 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
 // observation Jps (scaled Jp), Q = Jps E^-1 and g = Q b (observation phase).
 __global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
   __shared__ double sEi[kGB][6], sb[kGB][3], ssp[kGB][3];
+  if ((int)blockIdx.x >= d.live[0]) return;
   const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x;
   // the point's terms go out together with the window state
@@ -611,11 +616,13 @@ __device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc
 // 36 doubles read); the camera Jacobi scales are applied once per block.  Block pairs are sorted
 // by camera and remapped so that each XCD (blockIdx % 8 group) takes a contiguous run: the tiles
 // of a camera are re-read from that XCD's L2 instead of from the fabric.
-__global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o, int n_bp) {
+__global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
   __shared__ double red[4][37];
+  const int n_bp = d.live[1];
+  if ((int)blockIdx.x >= n_bp) return;
   int bid;
   {
-    const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = blockIdx.x % 8;
+    const int nwg = n_bp, q = nwg / 8, r = nwg % 8, x = blockIdx.x % 8;
     bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
   }
   if (bid >= n_bp) return;
@@ -1556,6 +1563,7 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
 __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
   __shared__ double sh[kGB][3], sst[kGB][3], sxn[kGB][3];
   __shared__ double red3[3][4];
+  if ((int)blockIdx.x >= d.live[0]) return;
   const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x;
   // plan-structure loads of the first chunk and the point's terms go out with the window state
@@ -1958,6 +1966,9 @@ struct lorb_ba_devbuild {
   int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0, gs_cap = 0;
   std::vector<int> h_hdr, h_cov, h_cam;
   int* pinned = nullptr; size_t pinned_n = 0;
+  // per-build structure uploaded in one copy: [BaWin | live (2) | perm (C) | cam_obs_off (C+1) | bp (up_bp_cap)]
+  unsigned char* up_dev = nullptr; unsigned char* up_host = nullptr; int up_bp_cap = 0;
+  size_t off_live = 0, off_perm = 0, off_camoff = 0, off_bp = 0, up_bytes = 0;
 };
 
 struct lorb_ba_plan {
@@ -1973,6 +1984,15 @@ struct lorb_ba_plan {
   hipGraphExec_t gexec = nullptr;
   LMOpt graph_opt{};
   bool has_graph = false;
+  // launch shape of the captured solve: a rebuild that keeps it (device-built plans launch the
+  // point-group / block-pair kernels at capacity) replays the graph without a new capture
+  struct GraphKey {
+    int kind = -1, lds = 0, memset_env = 0, env_total = 0, grid_pblk = 0, grid_bp = 0, pt_launch = 0;
+    bool operator==(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) == 0; }
+  } gkey;
+  int grid_pblk = 0, grid_bp = 0;  // launch grids of the point-group and block-pair kernels
+  int pt_launch = 0;               // points k_ba_init copies (Ptot, or the capacity)
+  int* live = nullptr;             // device [n_pblk, n_bp] (BaDev::live)
   lorb_comm* comm = nullptr;  // sharded plan (not owned)
   // per window: camera relabelling (input pose index -> plan camera index; RCM order, §8 item 4)
   std::vector<std::vector<int>> cam_map;
@@ -1981,6 +2001,7 @@ struct lorb_ba_plan {
   ~lorb_ba_plan() {
     if (devb) {
       if (devb->pinned) (void)hipHostFree(devb->pinned);
+      if (devb->up_host) (void)hipHostFree(devb->up_host);
       delete devb;
     }
     if (gexec) (void)hipGraphExecDestroy(gexec);
@@ -2273,11 +2294,13 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   }
   P->n_pblk = (int)pblk.size(); P->n_bp = (int)bps.size(); P->n_pairs = (int)pairs.size();
   P->env_total = env_base; P->n_total = row_base;
+  P->grid_pblk = P->n_pblk; P->grid_bp = P->n_bp; P->pt_launch = P->Ptot;
   BaDev& d = P->dev;
   BaWin* dwin; PBlk* dpb; BlockPair* dbp; int2* dpairs; double2* duv;
   int *a1, *a2, *a3, *a4, *a5, *a6;
   double* dfix;
   LORB_TRY(dupload(P, P->hwin, &dwin)); d.win = dwin;
+  LORB_TRY(dupload(P, std::vector<int>{P->n_pblk, P->n_bp}, &P->live)); d.live = P->live;
   LORB_TRY(dupload(P, pblk, &dpb)); d.pblk = dpb;
   int* dopt;
   LORB_TRY(dupload(P, obs_pt, &dopt)); d.obs_pt = dopt;
@@ -2341,13 +2364,33 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
 
 constexpr int kLdsBudget = 160 * 1024 - 2048;
 
+// Cholesky kernel for the plan's band: 2 k_ba_chol_2s, 1 k_ba_chol_w, 0 k_ba_chol, -1 none
+int chol_kind_of(const lorb_ba_plan* P) {
+  static const bool force_old = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'o'; }();
+  static const bool no_2s = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'w'; }();
+  if (!P->Ctot) return -1;
+  const bool chol_w = !force_old && P->max_bw <= 48 && sizeof(double) * (size_t)P->max_env_w <= (size_t)kLdsBudget;
+  const bool chol_2s = chol_w && !no_2s && P->min_n16 >= 128;
+  return chol_2s ? 2 : chol_w ? 1 : 0;
+}
+
+lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
+  lorb_ba_plan::GraphKey k;
+  k.kind = chol_kind_of(P);
+  k.lds = k.kind >= 1 ? P->max_env_w : P->max_env + 1000000 * P->max_bw;
+  k.memset_env = sizeof(double) * (size_t)P->max_env > (size_t)kLdsBudget;
+  k.env_total = k.memset_env ? P->env_total : 0;
+  k.grid_pblk = P->grid_pblk; k.grid_bp = P->grid_bp; k.pt_launch = P->pt_launch;
+  return k;
+}
+
 // one LM iteration (K1..K8) on the ctx stream
 int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = P->ctx->stream;
   const BaDev& d = P->dev;
-  if (P->n_pblk) {
+  if (P->grid_pblk) {
     lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-    hipLaunchKernelGGL(k_ba_lin, dim3(P->n_pblk), dim3(kGB), 0, s, d);
+    hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
   }
   if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(256), 0, s, d);
   if (P->comm) {  // exchange 1: camera blocks + cost / |x|^2 (sum), gradient max (max)
@@ -2367,23 +2410,21 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = ctx->stream;
   const BaDev& d = P->dev;
   LORB_TRY(enqueue_linearize(P, o));
-  if (P->n_pblk) hipLaunchKernelGGL(k_ba_point_prep, dim3(P->n_pblk), dim3(kGB), 0, s, d, o);
+  if (P->grid_pblk) hipLaunchKernelGGL(k_ba_point_prep, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
   // The LDS Cholesky never writes env, and k_ba_schur rewrites every stored entry of every
   // block each iteration, so the band's structural zeros (set at plan creation) persist; the
   // in-place global variant needs them restored.
   const bool chol_in_lds = sizeof(double) * (size_t)P->max_env <= (size_t)kLdsBudget;
   if (P->env_total && !chol_in_lds && !P->comm) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
-  if (P->n_bp) {
+  if (P->grid_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
-    hipLaunchKernelGGL(k_ba_schur, dim3(P->n_bp), dim3(256), 0, s, d, o, P->n_bp);
+    hipLaunchKernelGGL(k_ba_schur, dim3(P->grid_bp), dim3(256), 0, s, d, o);
   }
   if (P->comm)  // exchange 2: reduced camera system, rhs, point-block failure flags
     LORB_TRY(lorb::comm_allreduce(P->comm, d.env_part, d.env, (size_t)P->env_total + P->n_total + P->W, LORB_OP_SUM));
-  static const bool force_old = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'o'; }();
-  const bool chol_w = !force_old && P->max_bw <= 48 && sizeof(double) * (size_t)P->max_env_w <= (size_t)kLdsBudget;
-  static const bool no_2s = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'w'; }();
-  const bool chol_2s = chol_w && !no_2s && P->min_n16 >= 128;
-  P->chol_kind = !P->Ctot ? -1 : chol_2s ? 2 : chol_w ? 1 : 0;
+  const int kind = chol_kind_of(P);
+  const bool chol_2s = kind == 2, chol_w = kind == 1 || kind == 2;
+  P->chol_kind = kind;
   if (P->Ctot && chol_2s) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
     hipLaunchKernelGGL(k_ba_chol_2s, dim3(P->W), dim3(256), sizeof(double) * (size_t)P->max_env_w, s, d);
@@ -2401,7 +2442,7 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
     else { if (rpl == 1) LORB_CHOL(false, 1); else if (rpl == 2) LORB_CHOL(false, 2); else if (rpl == 4) LORB_CHOL(false, 4); else LORB_CHOL(false, 8); }
 #undef LORB_CHOL
   }
-  if (P->n_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->n_pblk), dim3(kGB), 0, s, d);
+  if (P->grid_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
   if (P->comm) {  // exchange 3: model cost change, candidate cost, point |step|^2
     hipLaunchKernelGGL(k_ba_win_reduce<1>, dim3(P->W), dim3(64), 0, s, d);
     LORB_TRY(lorb::comm_allreduce(P->comm, d.wstep_part, d.wstep, 3 * (size_t)P->W, LORB_OP_SUM));
@@ -2419,24 +2460,32 @@ int enqueue_finalize(lorb_ba_plan* P, const LMOpt& o) {
   return LORB_OK;
 }
 
+// the whole solve: x <- initial values, max_iter LM iterations, the final linearisation
+int enqueue_solve(lorb_ba_plan* P, const LMOpt& o) {
+  lorb_ctx* ctx = P->ctx;
+  {
+    const int n = std::max(std::max(P->W, P->Ctot), std::min(3 * P->pt_launch, 256 * 1024));
+    hipLaunchKernelGGL(k_ba_init, dim3(lorb::ceil_div(std::max(n, 1), 256)), dim3(256), 0, ctx->stream, P->dev, P->W,
+                       P->Ctot, P->pt_launch, o);
+  }
+  LORB_CHECK_LAUNCH(ctx);
+  for (int it = 0; it < o.max_iter; ++it) LORB_TRY(enqueue_iteration(P, o));
+  return enqueue_finalize(P, o);
+}
+
 int plan_solve(lorb_ba_plan* P, const lorb_lm_options* opt) {
   lorb_ctx* ctx = P->ctx;
   LMOpt o = to_dev_opt(opt);
-  // x[0] <- the initial values (x[1] is the candidate buffer), window states, rotation states
-  {
-    const int n = std::max(std::max(P->W, P->Ctot), std::min(3 * P->Ptot, 256 * 1024));
-    hipLaunchKernelGGL(k_ba_init, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, P->dev, P->W, P->Ctot,
-                       P->Ptot, o);
-  }
-  LORB_CHECK_LAUNCH(ctx);
   // per-kernel events cannot live inside a graph, and neither can a host-transport exchange
   static const bool no_graph = [] { const char* e = getenv("LORB_NO_GRAPH"); return e && e[0] == '1'; }();
   const bool timing = ctx->ktime || no_graph || (P->comm && !P->comm->rccl);
-  if (!timing && (!P->has_graph || memcmp(&P->graph_opt, &o, sizeof(LMOpt)) != 0)) {
+  if (timing) return enqueue_solve(P, o);
+  const lorb_ba_plan::GraphKey key = graph_key(P);
+  if (!P->has_graph || !(key == P->gkey) || memcmp(&P->graph_opt, &o, sizeof(LMOpt)) != 0) {
     if (P->gexec) { (void)hipGraphExecDestroy(P->gexec); P->gexec = nullptr; }
     if (P->graph) { (void)hipGraphDestroy(P->graph); P->graph = nullptr; }
     LORB_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-    int rc = enqueue_iteration(P, o);
+    int rc = enqueue_solve(P, o);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(ctx->stream, &g);
     if (rc != LORB_OK) return rc;
@@ -2444,13 +2493,10 @@ int plan_solve(lorb_ba_plan* P, const lorb_lm_options* opt) {
     P->graph = g;
     LORB_HIP(ctx, hipGraphInstantiate(&P->gexec, P->graph, nullptr, nullptr, 0));
     P->graph_opt = o;
+    P->gkey = key;
     P->has_graph = true;
   }
-  for (int it = 0; it < o.max_iter; ++it) {
-    if (timing) LORB_TRY(enqueue_iteration(P, o));
-    else LORB_HIP(ctx, hipGraphLaunch(P->gexec, ctx->stream));
-  }
-  LORB_TRY(enqueue_finalize(P, o));
+  LORB_HIP(ctx, hipGraphLaunch(P->gexec, ctx->stream));
   return LORB_OK;
 }
 
@@ -2534,24 +2580,56 @@ __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int K_cap
 }
 
 // one thread per point: covisibility of its optimised cameras (ordered pairs, both directions),
-// per-camera counts, largest observation count, a camera seen twice by one point (error 4)
-__global__ __launch_bounds__(256) void k_db_cov(lorb_ba_window_dev w, int C, const int* __restrict__ pt_off,
-                                                const int* __restrict__ val, int* __restrict__ cov,
-                                                int* __restrict__ cam_cnt, int* __restrict__ hdr) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= *w.d_n_points) return;
-  const int a0 = pt_off[p], a1 = pt_off[p + 1];
-  atomicMax(&hdr[1], a1 - a0);
-  for (int a = a0; a < a1; ++a) {
-    const int fa = w.d_obs_frame[val[a]];
-    if (fa < 0) continue;
-    atomicAdd(&cam_cnt[fa], 1);
-    for (int b = a0; b < a1; ++b) {
-      const int fb = w.d_obs_frame[val[b]];
-      if (fb < 0) continue;
-      if (b != a && fb == fa) atomicOr(&hdr[2], 4);
-      if (b != a) atomicAdd(&cov[fa * C + fb], 1);
+// per-camera counts, largest observation count, a camera seen twice by one point (error 4).  The
+// counts build in an LDS copy per workgroup (a few workgroups stride over the points) and are
+// flushed with one global atomic per non-zero entry -- the camera pairs are few and hot, so
+// per-observation global atomics would serialise on them.  LDS=false: C too large for LDS.
+constexpr int kCovWG = 16;
+template <bool LDS>
+__global__ __launch_bounds__(1024) void k_db_cov(lorb_ba_window_dev w, int C, const int* __restrict__ pt_off,
+                                                 const int* __restrict__ val, int* __restrict__ cov,
+                                                 int* __restrict__ cam_cnt, int* __restrict__ hdr) {
+  extern __shared__ int s_cov[];  // C * C covisibility, then C camera counts
+  int* lc = LDS ? s_cov : cov;
+  int* lcc = LDS ? s_cov + C * C : cam_cnt;
+  if (LDS) {
+    for (int i = threadIdx.x; i < C * C + C; i += 1024) s_cov[i] = 0;
+    __syncthreads();
+  }
+  const int n_pt = *w.d_n_points;
+  int mx = 0, err = 0;
+  for (int p = blockIdx.x * 1024 + threadIdx.x; p < n_pt; p += gridDim.x * 1024) {
+    const int a0 = pt_off[p], a1 = pt_off[p + 1];
+    mx = max(mx, a1 - a0);
+    for (int a = a0; a < a1; ++a) {
+      const int fa = w.d_obs_frame[val[a]];
+      if (fa < 0) continue;
+      atomicAdd(&lcc[fa], 1);
+      for (int b = a0; b < a1; ++b) {
+        if (b == a) continue;
+        const int fb = w.d_obs_frame[val[b]];
+        if (fb < 0) continue;
+        err |= fb == fa;
+        atomicAdd(&lc[fa * C + fb], 1);
+      }
     }
+  }
+  // workgroup max / error flag, then one global atomic each
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = max(mx, __shfl_xor(mx, o, 64));
+    err |= __shfl_xor(err, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (mx) atomicMax(&hdr[1], mx);
+    if (err) atomicOr(&hdr[2], 4);
+  }
+  if (LDS) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < C * C; i += 1024)
+      if (s_cov[i]) atomicAdd(&cov[i], s_cov[i]);
+    for (int i = threadIdx.x; i < C; i += 1024)
+      if (s_cov[C * C + i]) atomicAdd(&cam_cnt[i], s_cov[C * C + i]);
   }
 }
 
@@ -2587,17 +2665,21 @@ __global__ __launch_bounds__(256) void k_db_group_starts(const int* __restrict__
   if (p == 0 || (pt_off[p - 1] + p - 1) / S != g) gstart[g] = p;
 }
 
-__global__ __launch_bounds__(64) void k_db_groups(BaDev d, const int* __restrict__ pt_off, int P, int G,
-                                                  int* __restrict__ gstart) {
-  if (threadIdx.x != 0) return;
-  int nxt = P;
-  for (int g = G - 1; g >= 0; --g) {  // empty bins start where the next non-empty one does
-    const int s = gstart[g] < 0 ? nxt : gstart[g];
-    PBlk b;
-    b.win = 0; b.p0 = s; b.cnt = nxt - s; b.o0 = pt_off[s]; b.no = pt_off[nxt] - pt_off[s];
-    const_cast<PBlk*>(d.pblk)[g] = b;
-    nxt = s;
-  }
+// group g = points [start(g), start(g + 1)); an empty bin starts where the next non-empty one does
+// (bins are at least as wide as any point's weight, so only trailing bins can be empty and the
+// forward search is short)
+__global__ __launch_bounds__(256) void k_db_groups(BaDev d, const int* __restrict__ pt_off, int P, int G,
+                                                   const int* __restrict__ gstart) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= G) return;
+  int s = P, e = P;
+  for (int h = g; h < G; ++h)
+    if (gstart[h] >= 0) { s = gstart[h]; break; }
+  for (int h = g + 1; h < G; ++h)
+    if (gstart[h] >= 0) { e = gstart[h]; break; }
+  PBlk b;
+  b.win = 0; b.p0 = s; b.cnt = e - s; b.o0 = pt_off[s]; b.no = pt_off[e] - pt_off[s];
+  const_cast<PBlk*>(d.pblk)[g] = b;
 }
 
 // one workgroup per (camera, camera) block: its pair list in point order
@@ -2693,16 +2775,16 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(dalloc(P, K, &b.val_in)); LORB_TRY(dalloc(P, K, &b.val_out));
   LORB_TRY(dalloc(P, K, &b.ckey)); LORB_TRY(dalloc(P, K, &b.ckey_out)); LORB_TRY(dalloc(P, K, &b.cval));
   LORB_TRY(dalloc(P, Pn + 1, &b.pt_cnt)); LORB_TRY(dalloc(P, (size_t)8, &b.hdr));
-  LORB_TRY(dalloc(P, C * C, &b.cov)); LORB_TRY(dalloc(P, C, &b.cam_cnt)); LORB_TRY(dalloc(P, C, &b.perm));
-  int *a_pt, *a_cam, *a_fix, *a_cm, *a_co, *a_camobs, *a_win, *a_act, *a_ptoff;
+  LORB_TRY(dalloc(P, C * C, &b.cov)); LORB_TRY(dalloc(P, C, &b.cam_cnt));
+  int *a_pt, *a_cam, *a_fix, *a_cm, *a_camobs, *a_win, *a_act, *a_ptoff;
   double2* a_uv;
   double* a_fixp;
   LORB_TRY(dalloc(P, K, &a_pt)); LORB_TRY(dalloc(P, K, &a_cam)); LORB_TRY(dalloc(P, K, &a_fix));
   LORB_TRY(dalloc(P, K, &a_uv)); LORB_TRY(dalloc(P, K, &a_cm)); LORB_TRY(dalloc(P, K, &a_camobs));
-  LORB_TRY(dalloc(P, C + 1, &a_co)); LORB_TRY(dalloc(P, C, &a_win)); LORB_TRY(dalloc(P, C, &a_act));
+  LORB_TRY(dalloc(P, C, &a_win)); LORB_TRY(dalloc(P, C, &a_act));
   LORB_TRY(dalloc(P, Pn + 1, &a_ptoff)); LORB_TRY(dalloc(P, (size_t)std::max(b.F, 1) * 6, &a_fixp));
   d.obs_pt = a_pt; d.obs_cam = a_cam; d.obs_fix = a_fix; d.obs_uv = a_uv; d.obs_cm = a_cm; d.cam_obs = a_camobs;
-  d.cam_obs_off = a_co; d.cam_win = a_win; d.cam_active = a_act; d.pt_obs_off = a_ptoff; d.fixed_pose = a_fixp;
+  d.cam_win = a_win; d.cam_active = a_act; d.pt_obs_off = a_ptoff; d.fixed_pose = a_fixp;
   LORB_TRY(dalloc(P, C * 6, &d.x_init_pose)); LORB_TRY(dalloc(P, Pn * 3, &d.x_init_pt));
   LORB_TRY(dalloc(P, C * 6, &d.x_pose[0])); LORB_TRY(dalloc(P, C * 6, &d.x_pose[1]));
   LORB_TRY(dalloc(P, Pn * 3, &d.x_pt[0])); LORB_TRY(dalloc(P, Pn * 3, &d.x_pt[1]));
@@ -2714,7 +2796,10 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(dalloc(P, solve_n, &sol)); LORB_TRY(dalloc(P, (size_t)3, &stp));
   d.U = lin; d.V = lin + C * 21; d.wlin = lin + C * 27; d.wmax = mx;
   d.U_part = d.U; d.V_part = d.V; d.wlin_part = d.wlin; d.wmax_part = d.wmax;
-  d.env = sol; d.env_part = sol;  // rhs / wfail are placed after the band at each build
+  // rhs / wfail at a fixed place after the largest band (n x n), so the captured solve survives a
+  // rebuild that changes the band
+  d.env = sol; d.env_part = sol;
+  d.rhs = sol + n * n; d.wfail = d.rhs + n; d.rhs_part = d.rhs; d.wfail_part = d.wfail;
   d.wstep = stp; d.wstep_part = stp;
   d.sharded = 0; d.rank0 = 1;
   LORB_TRY(dalloc(P, C, &d.cam_gmax));
@@ -2725,8 +2810,6 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(dalloc(P, n, &d.ycam));
   LORB_TRY(dalloc(P, (size_t)8, &d.dbg));
   LORB_TRY(dalloc(P, (size_t)1, &P->d_state)); d.st = P->d_state;
-  BaWin* dwin;
-  LORB_TRY(dalloc(P, (size_t)1, &dwin)); d.win = dwin;
   size_t t1 = 0, t2 = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, t1, b.key_in, b.key_out, b.val_in, b.val_out, (int)K, 0, 31,
                                          ctx->stream) != hipSuccess ||
@@ -2737,6 +2820,42 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   P->allocs.push_back(b.tmp);
   P->W = 1;
   P->hwin.assign(1, BaWin{});
+  P->pt_launch = b.P_cap;
+  return LORB_OK;
+}
+
+// (re)allocate the upload block for bp_need block pairs; repoints BaDev at it
+int up_alloc(lorb_ba_plan* P, int bp_need) {
+  lorb_ba_devbuild& b = *P->devb;
+  if (b.up_dev && b.up_bp_cap >= bp_need) return LORB_OK;
+  lorb_ctx* ctx = P->ctx;
+  const int cap = std::max(bp_need + bp_need / 4, 16);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t C = (size_t)std::max(b.C, 1);
+  b.off_live = al(sizeof(BaWin));
+  b.off_perm = b.off_live + 256;
+  b.off_camoff = b.off_perm + al(4 * C);
+  b.off_bp = b.off_camoff + al(4 * (C + 1));
+  b.up_bytes = b.off_bp + sizeof(BlockPair) * (size_t)cap;
+  if (b.up_dev) {
+    LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    LORB_HIP(ctx, hipFree(b.up_dev));
+    auto it = std::find(P->allocs.begin(), P->allocs.end(), (void*)b.up_dev);
+    if (it != P->allocs.end()) P->allocs.erase(it);
+    (void)hipHostFree(b.up_host);
+    b.up_host = nullptr;
+  }
+  LORB_TRY(dalloc(P, b.up_bytes, &b.up_dev));
+  LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&b.up_host), b.up_bytes));
+  b.up_bp_cap = cap;
+  BaDev& d = P->dev;
+  d.win = reinterpret_cast<const BaWin*>(b.up_dev);
+  d.live = reinterpret_cast<const int*>(b.up_dev + b.off_live);
+  b.perm = reinterpret_cast<int*>(b.up_dev + b.off_perm);
+  d.cam_obs_off = reinterpret_cast<const int*>(b.up_dev + b.off_camoff);
+  d.bp = reinterpret_cast<const BlockPair*>(b.up_dev + b.off_bp);
+  P->grid_bp = cap;
+  P->has_graph = false;
   return LORB_OK;
 }
 
@@ -2766,8 +2885,15 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     if (hipcub::DeviceScan::ExclusiveSum(b.tmp, tb, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1, s) != hipSuccess)
       return lorb::set_error(ctx, LORB_E_DEVICE, "scan (point offsets) failed");
   }
-  hipLaunchKernelGGL(k_db_cov, dim3(lorb::ceil_div(std::max(b.P_cap, 1), 256)), dim3(256), 0, s, *w, C, d.pt_obs_off,
-                     b.val_out, b.cov, b.cam_cnt, b.hdr);
+  {
+    const size_t lds = sizeof(int) * ((size_t)C * C + C);
+    if (lds <= 64 * 1024)
+      hipLaunchKernelGGL(k_db_cov<true>, dim3(kCovWG), dim3(1024), lds, s, *w, C, d.pt_obs_off, b.val_out, b.cov,
+                         b.cam_cnt, b.hdr);
+    else
+      hipLaunchKernelGGL(k_db_cov<false>, dim3(lorb::ceil_div(std::max(b.P_cap, 1), 1024)), dim3(1024), 0, s, *w, C,
+                         d.pt_obs_off, b.val_out, b.cov, b.cam_cnt, b.hdr);
+  }
   LORB_CHECK_LAUNCH(ctx);
   // 2. the one readback: counts and the covisibility structure
   const size_t nrb = 8 + (size_t)C + (size_t)C * C;
@@ -2830,33 +2956,43 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   P->env_total = bw.env_size; P->n_total = n;
   P->max_env = bw.env_size + 2 * n; P->max_bw = bwid;
   {
+    // the Cholesky's LDS is sized for a band of 48 (the widest k_ba_chol_w / _2s take) when that
+    // fits, so that a narrower band after a rebuild keeps the captured solve
     const int n16 = (n + 15) & ~15;
-    P->max_env_w = std::max(n16 * (bwid + 1) + 2 * n16 + 64 * 18, (n16 + 48) * (bwid + 2) + 2 * 64 * 18 + 48);
+    auto env_w = [&](int bwv) {
+      return std::max(n16 * (bwv + 1) + 2 * n16 + 64 * 18, (n16 + 48) * (bwv + 2) + 2 * 64 * 18 + 48);
+    };
+    P->max_env_w = env_w(bwid);
+    if (bwid <= 48 && sizeof(double) * (size_t)env_w(48) <= (size_t)kLdsBudget) P->max_env_w = env_w(48);
     P->min_n16 = n16 > 0 ? n16 : (1 << 30);
   }
-  // grow-only structure buffers
+  // grow-only structure buffers; the point-group kernels launch at capacity
   PBlk* pb = const_cast<PBlk*>(d.pblk);
-  BlockPair* bpp = const_cast<BlockPair*>(d.bp);
   int2* pr = const_cast<int2*>(d.pairs);
   LORB_TRY(grow(P, &pb, &b.pblk_cap, (size_t)std::max(G, 1)));
   LORB_TRY(grow(P, &b.gstart, &b.gs_cap, (size_t)std::max(G, 1)));
-  LORB_TRY(grow(P, &bpp, &b.bp_cap, std::max<size_t>(bps.size(), 1)));
   LORB_TRY(grow(P, &pr, &b.pairs_cap, (size_t)std::max(n_pairs, 1)));
-  d.pblk = pb; d.bp = bpp; d.pairs = pr;
+  d.pblk = pb; d.pairs = pr;
   {
     double* pt = d.part;
-    LORB_TRY(grow(P, &pt, &b.part_cap, (size_t)std::max(G, 1) * 8));
+    LORB_TRY(grow(P, &pt, &b.part_cap, (size_t)b.pblk_cap * 8));
     d.part = pt;
   }
-  d.rhs = d.env + P->env_total; d.wfail = d.rhs + n;
-  d.rhs_part = d.rhs; d.wfail_part = d.wfail;
-  // uploads (pinned staging, stream-ordered)
-  std::vector<int> hperm(map.begin(), map.end());
-  LORB_HIP(ctx, hipMemcpyAsync(b.perm, hperm.data(), sizeof(int) * C, hipMemcpyHostToDevice, s));
-  LORB_HIP(ctx, hipMemcpyAsync(const_cast<int*>(d.cam_obs_off), cam_off.data(), sizeof(int) * (C + 1), hipMemcpyHostToDevice, s));
-  if (!bps.empty())
-    LORB_HIP(ctx, hipMemcpyAsync(bpp, bps.data(), sizeof(BlockPair) * bps.size(), hipMemcpyHostToDevice, s));
-  LORB_HIP(ctx, hipMemcpyAsync(const_cast<BaWin*>(d.win), &P->hwin[0], sizeof(BaWin), hipMemcpyHostToDevice, s));
+  P->grid_pblk = b.pblk_cap;
+  LORB_TRY(up_alloc(P, (int)bps.size()));
+  // one upload (pinned staging, stream-ordered; the next build writes the staging only after its
+  // own readback synchronised the stream)
+  {
+    unsigned char* h = b.up_host;
+    memcpy(h, &P->hwin[0], sizeof(BaWin));
+    const int live[2] = {G, (int)bps.size()};
+    memcpy(h + b.off_live, live, sizeof(live));
+    memcpy(h + b.off_perm, map.data(), sizeof(int) * C);
+    memcpy(h + b.off_camoff, cam_off.data(), sizeof(int) * (C + 1));
+    if (!bps.empty()) memcpy(h + b.off_bp, bps.data(), sizeof(BlockPair) * bps.size());
+    const size_t bytes = b.off_bp + sizeof(BlockPair) * bps.size();
+    LORB_HIP(ctx, hipMemcpyAsync(b.up_dev, h, bytes, hipMemcpyHostToDevice, s));
+  }
   // 4. structure kernels
   if (K > 0) {
     hipLaunchKernelGGL(k_db_gather, dim3(lorb::ceil_div(K, 256)), dim3(256), 0, s, *w, d, K, C, b.key_out, b.val_out,
@@ -2870,7 +3006,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   if (G > 0) {
     LORB_HIP(ctx, hipMemsetAsync(b.gstart, 0xff, sizeof(int) * G, s));
     hipLaunchKernelGGL(k_db_group_starts, dim3(lorb::ceil_div(Pn, 256)), dim3(256), 0, s, d.pt_obs_off, Pn, S, b.gstart);
-    hipLaunchKernelGGL(k_db_groups, dim3(1), dim3(64), 0, s, d, d.pt_obs_off, Pn, G, b.gstart);
+    hipLaunchKernelGGL(k_db_groups, dim3(lorb::ceil_div(G, 256)), dim3(256), 0, s, d, d.pt_obs_off, Pn, G, b.gstart);
   }
   if (!bps.empty()) hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), 0, s, d);
   {
@@ -2880,7 +3016,6 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   }
   if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   LORB_CHECK_LAUNCH(ctx);
-  P->has_graph = false;  // block / group counts changed: the LM graph is captured again
   return LORB_OK;
 }
 

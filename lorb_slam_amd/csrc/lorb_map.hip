@@ -25,6 +25,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 
 #include "lorb_internal.h"
 
@@ -172,12 +174,20 @@ struct lorb_map {
   int h_P = 0, h_K = 0;  // counts after the last step (host mirror)
   int n_cap = 0, last_n = 0;
   float fx = 0, fy = 0, cx = 0, cy = 0;
+  // LORB_MAP_PROFILE=1: host wall time per phase with a stream sync after each (diagnostics only)
+  bool prof = false;
+  double prof_ms[8] = {};
+  int prof_n = 0;
   int* cc_t = nullptr; int* cc_d = nullptr; int* mt = nullptr; int* nm = nullptr; float* xyz = nullptr;
   void* tmp = nullptr; size_t tmp_bytes = 0;
   int* pinned = nullptr;
   lorb_ba_plan* plan = nullptr;
   std::vector<void*> allocs;
   ~lorb_map() {
+    if (prof && prof_n)
+      fprintf(stderr, "lorb_map profile over %d steps (ms/step): match %.3f unproject %.3f append %.3f slide %.3f "
+              "plan %.3f solve %.3f writeback %.3f\n", prof_n, prof_ms[0] / prof_n, prof_ms[1] / prof_n,
+              prof_ms[2] / prof_n, prof_ms[3] / prof_n, prof_ms[4] / prof_n, prof_ms[5] / prof_n, prof_ms[6] / prof_n);
     if (plan) (void)lorb_ba_plan_destroy(plan);
     if (pinned) (void)hipHostFree(pinned);
     for (void* p : allocs) (void)hipFree(p);
@@ -285,6 +295,10 @@ int lorb_map_create(lorb_ctx* ctx, const lorb_map_init* in, lorb_map** out) {
   lorb_map* M = new (std::nothrow) lorb_map();
   if (!M) return LORB_E_NOMEM;
   M->ctx = ctx;
+  {
+    const char* e = getenv("LORB_MAP_PROFILE");
+    M->prof = e && e[0] == '1';
+  }
   M->fx = in->fx; M->fy = in->fy; M->cx = in->cx; M->cy = in->cy;
   int rc = map_alloc(M, in);
   if (rc == LORB_OK) {
@@ -337,6 +351,16 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   hipStream_t s = ctx->stream;
   MapDev& m = M->m;
   const int kf = M->t0 + m.W;  // the new keyframe's id
+  auto clk = std::chrono::steady_clock::now();
+  auto mark = [&](int i) -> int {
+    if (!M->prof) return LORB_OK;
+    LORB_HIP(ctx, hipStreamSynchronize(s));
+    const auto now = std::chrono::steady_clock::now();
+    M->prof_ms[i] += std::chrono::duration<double, std::milli>(now - clk).count();
+    clk = now;
+    return LORB_OK;
+  };
+  LORB_TRY(mark(7));
   // 1. SearchLocalPoints: the keyframe's descriptors against the map's points (crossCheck + minDist filter)
   if (n > 0 && M->h_P > 0) {
     const int32_t q_off[2] = {0, n}, t_off[2] = {0, M->h_P};
@@ -344,20 +368,25 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   } else if (n > 0) {
     LORB_HIP(ctx, hipMemsetAsync(M->mt, 0xff, sizeof(int) * (size_t)n, s));
   }
+  LORB_TRY(mark(0));
   // 2. UnprojectStereo of every keypoint (used where depth > 0 and unmatched)
   if (n > 0) LORB_TRY(lorb_unproject_stereo_dev(ctx, frame, Tcw, n, d_x, d_y, d_depth, M->xyz));
+  LORB_TRY(mark(1));
   // 3. AddObservation / new points, keyframe pose into the ring
   Pose6 p6;
   for (int q = 0; q < 6; ++q) p6.v[q] = pose[q];
   LORB_HIP(ctx, hipMemsetAsync(m.cnt + 2, 0, sizeof(int), s));
   hipLaunchKernelGGL(k_map_append, dim3(1), dim3(1024), 0, s, m, n, kf, p6, M->mt, M->xyz, d_desc, d_x, d_y, d_depth);
   LORB_CHECK_LAUNCH(ctx);
+  LORB_TRY(mark(2));
   // 4. slide the window by one keyframe; cull and compact
   LORB_TRY(map_slide(M, M->t0 + 1, std::min(M->h_P + n, m.P_cap), std::min(M->h_K + n, m.K_cap)));
+  LORB_TRY(mark(3));
   LORB_HIP(ctx, hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
   // 5. BA plan of the slid window (its readback synchronises the stream, so the counts above are in)
   const lorb_ba_window_dev w = window_of(M);
   LORB_TRY(lorb_ba_plan_update_dev(M->plan, &w));
+  LORB_TRY(mark(4));
   M->last_n = n;
   if (M->pinned[2] & 1)
     return lorb::set_error(ctx, LORB_E_NOMEM, "map capacity exceeded (points %d/%d, observations %d/%d)", M->pinned[0],
@@ -365,9 +394,12 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   M->h_P = M->pinned[0]; M->h_K = M->pinned[1];
   // 6. LocalPoseOptimization + float write-back of poses (ring) and points (map)
   LORB_TRY(lorb_ba_plan_solve(M->plan, opt));
+  LORB_TRY(mark(5));
   LORB_TRY(lorb_ba_plan_result_dev(M->plan, m.pose_out, m.pos));
   hipLaunchKernelGGL(k_map_writeback, dim3(1), dim3(256), 0, s, m, M->t0);
   LORB_CHECK_LAUNCH(ctx);
+  LORB_TRY(mark(6));
+  if (M->prof) M->prof_n++;
   return LORB_OK;
 }
 
