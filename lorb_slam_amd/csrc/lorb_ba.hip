@@ -1230,6 +1230,13 @@ __global__ __launch_bounds__(256) void k_ba_chol_w(BaDev d) {
 // S_MM - L_MT L_MT^T and S_MM - L_MB L_MB^T; wave 0 combines them (minus S_MM) and factors M
 // (3 panels).  Back-substitution: M, then T (wave 0) and B (wave 1) concurrently.  Rows
 // n .. n16-1 are an identity pad.
+// Progressive staging (k_ba_chol_2s): bit b of the workgroup's mask = rows [16 b, 16 b + 16) of the
+// band are in LDS.  Waves 2 / 3 publish with release, the factoring waves wait with acquire.
+__device__ __forceinline__ void wait_bit(unsigned long long* mask, int b) {
+  while (!((__hip_atomic_load(mask, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> b) & 1ull))
+    __builtin_amdgcn_s_sleep(1);
+}
+
 struct BandSide {
   double* A;     // band storage of the whole matrix (row-major, rows x (bw + 1), row i holds cols
                  // i-bw .. i); the diagonal slot holds 1 / L(i, i) (its only use is the
@@ -1241,6 +1248,9 @@ struct BandSide {
   double* xch;   // 64 x 17 exchange (column 16 of each row: dummy store slot of that lane)
   int rows, bw, lane;
   int base, si, sj;
+  unsigned long long* mask = nullptr;  // progressive staging (null: the whole band is staged)
+  int* pdone = nullptr;                // panels whose L is in the band (release-counted)
+  int nbk = 0, dir = 0;                // row blocks; +1 top view, -1 reversed bottom view
 
   __device__ __forceinline__ int idx(int i, int j) const { return base + si * i + sj * j; }
 
@@ -1285,17 +1295,6 @@ struct BandSide {
       // unrolled panel is hoisted out of the loop as an SGPR mask and the masks spill.
       int lane = this->lane, lok = (int)l_ok, tok = (int)tn_ok;
       asm volatile("" : "+v"(lane), "+v"(lok), "+v"(tok));
-      v4d Tn[4];
-#pragma unroll
-      for (int J = 0; J < 4; ++J)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          // (kb+64+ck+4r, kb+16+16J+ci): row offset 4r, column offset 16J relative to tn_addr
-          const bool ok = (((unsigned)tok >> (4 * J + r)) & 1u) && kb + 64 + ck + 4 * r < rows;
-          const double v = A[ok ? tn_addr + 4 * r * si + 16 * J * sj : base];
-          Tn[J][r] = ok ? v : 0.0;
-        }
-      tn_addr += dstep;
       const double zin = kb + 16 + lane < rows ? z[kb + 16 + lane] : 0.0;
 #pragma unroll
       for (int I = 0; I < 4; ++I)
@@ -1336,7 +1335,25 @@ struct BandSide {
         l_base += dstep;
         if (lane < NB) z[kb + lane] = zr;
       }
+      if (pdone && lane == 0) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       wave_sync_lds();
+      // the tile row entering at the end of this panel (view rows kb+64 .. kb+79): untouched S,
+      // read here so that a progressively staged band has the panel's factorization to arrive
+      if (mask) {
+        const int b = dir > 0 ? kb / 16 + 4 : nbk - 5 - kb / 16;
+        if (b >= 0 && b < nbk) wait_bit(mask, b);
+      }
+      v4d Tn[4];
+#pragma unroll
+      for (int J = 0; J < 4; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // (kb+64+ck+4r, kb+16+16J+ci): row offset 4r, column offset 16J relative to tn_addr
+          const bool ok = (((unsigned)tok >> (4 * J + r)) & 1u) && kb + 64 + ck + 4 * r < rows;
+          const double v = A[ok ? tn_addr + 4 * r * si + 16 * J * sj : base];
+          Tn[J][r] = ok ? v : 0.0;
+        }
+      tn_addr += dstep;
       double opA[4][4];
 #pragma unroll
       for (int I = 1; I < 4; ++I)
@@ -1360,8 +1377,35 @@ struct BandSide {
       for (int J = 0; J < 4; ++J) T[tri4(3, J)] = Tn[J];
     }
   }
+  // The 16 x 16 diagonal block of L at view rows c0 .. c0+15 replaced in place by its inverse X
+  // (lower triangular; the diagonal slot already holds 1 / L(i, i) = X(i, i)).  Column j = lane
+  // (lanes 0..15): X(i, j) = -X(i, i) sum_{k=j}^{i-1} L(i, k) X(k, j).  Only the back-substitution
+  // reads the block afterwards.
+  __device__ __forceinline__ void linv(int c0) const {
+    if (lane >= 16) return;
+    const int j = lane;
+    // column sweep: acc[i] collects sum_k L(i, k) X(k, j) as the X(k, j) become final; the
+    // L(i, k) loads do not depend on the chain
+    double acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const double dk = A[idx(c0 + k, c0 + k)];
+      const double xk = k == j ? dk : (k > j ? -dk * acc[k] : 0.0);
+      if (k > j && k - j <= bw) A[idx(c0 + k, c0 + j)] = xk;
+#pragma unroll
+      for (int i = k + 1; i < 16; ++i) {
+        const bool ok = i - k <= bw;
+        const double l = A[ok ? idx(c0 + i, c0 + k) : base];
+        acc[i] = fma(ok ? l : 0.0, xk, acc[i]);
+      }
+    }
+  }
   // L^T y = z for the 16-row blocks c0 = c_hi, c_hi-16, ..., c_lo; rows below a block are
-  // gathered up to rows-1
+  // gathered up to rows-1.  INV: the blocks' diagonal holds X = L_bb^-1 (linv), so
+  // y_b = X^T (z_b - gathered) is a 16 x 16 product instead of a 16-step chain.
+  template <bool INV>
   __device__ __forceinline__ void backsub(int c_hi, int c_lo) const {
     const int jc = lane & 15, g = lane >> 4;
     for (int c0 = c_hi; c0 >= c_lo; c0 -= 16) {
@@ -1393,17 +1437,107 @@ struct BandSide {
         xrow_pair<true>(acc, a, b); acc = a + b;
       }
       double zb = z[j] - acc;
-      const double iv = A[idx(j, j)];  // 1 / L(j, j)
+      if (INV) {
+        double xv[4];
 #pragma unroll
-      for (int k = NB - 1; k >= 0; --k) {
-        const double yk = readlane_d(zb, k) * readlane_d(iv, k);
-        zb = jc == k ? yk : fma(-lk[k], yk, zb);
+        for (int u = 0; u < 4; ++u) {  // X(c0 + k, j), k = g + 4u >= jc
+          const int k = g + 4 * u;
+          const bool ok = k >= jc && k - jc <= bw;
+          const double v = A[ok ? idx(c0 + k, j) : base];
+          xv[u] = ok ? v : 0.0;
+        }
+        if (g == 0) z[j] = zb;
+        wave_sync_lds();
+        double part = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) part = fma(xv[u], z[c0 + g + 4 * u], part);
+        double a, b;
+        xrow_pair<false>(part, a, b); part = a + b;
+        xrow_pair<true>(part, a, b); part = a + b;
+        wave_sync_lds();
+        if (g == 0) z[j] = part;
+      } else {
+        const double iv = A[idx(j, j)];  // 1 / L(j, j)
+#pragma unroll
+        for (int k = NB - 1; k >= 0; --k) {
+          const double yk = readlane_d(zb, k) * readlane_d(iv, k);
+          zb = jc == k ? yk : fma(-lk[k], yk, zb);
+        }
+        if (g == 0) z[j] = zb;
       }
-      if (g == 0) z[j] = zb;
       wave_sync_lds();
     }
   }
 };
+
+// Flat copy of band chunks [j0, j1) (16-byte chunks of the row-major n x (bw + 1) band) by nthr
+// threads, U chunks per thread per batch with all loads of a batch issued before any store.
+// Element (i, off) keeps S's value inside the matrix; the left triangle of the first bw rows is
+// zeroed and rows n .. n16-1 are an identity pad.
+template <int U>
+__device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, double* Ab, int a0, int a1, int b0, int b1,
+                                            int tid, int nthr, int n, int bw, int nsrc);
+template <int U>
+__device__ __forceinline__ void stage_band(const double2* __restrict__ S2, double* Ab, int j0, int j1, int tid,
+                                           int nthr, int n, int bw, int nsrc) {
+  const int B1 = bw + 1;
+  for (int jb = j0 + tid; jb < j1; jb += nthr * U) {
+    double2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = jb + nthr * u;
+      v[u] = S2[(j < j1 && j < nsrc) ? j : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = jb + nthr * u;
+      if (j < j1) {
+        int i = (2 * j) / B1, off = (2 * j) % B1;
+        double e[2] = {v[u].x, v[u].y};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const bool in = i < n && i - (bw - off) >= 0;
+          e[h] = in ? e[h] : ((i >= n && off == bw) ? 1.0 : 0.0);
+          if (++off == B1) { off = 0; ++i; }
+        }
+        reinterpret_cast<double2*>(Ab)[j] = double2{e[0], e[1]};
+      }
+    }
+  }
+}
+
+
+// the same over two chunk ranges [a0, a1) and [b0, b1), all loads of a batch before any store
+template <int U>
+__device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, double* Ab, int a0, int a1, int b0, int b1,
+                                            int tid, int nthr, int n, int bw, int nsrc) {
+  const int B1 = bw + 1, la = a1 - a0, tot = la + (b1 - b0);
+  for (int vb = tid; vb < tot; vb += nthr * U) {
+    double2 v[U];
+    int jj[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int vv = vb + nthr * u;
+      jj[u] = vv < la ? a0 + vv : b0 + (vv - la);
+      v[u] = S2[(vv < tot && jj[u] < nsrc) ? jj[u] : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = jj[u];
+      if (vb + nthr * u < tot) {
+        int i = (2 * j) / B1, off = (2 * j) % B1;
+        double e[2] = {v[u].x, v[u].y};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const bool in = i < n && i - (bw - off) >= 0;
+          e[h] = in ? e[h] : ((i >= n && off == bw) ? 1.0 : 0.0);
+          if (++off == B1) { off = 0; ++i; }
+        }
+        reinterpret_cast<double2*>(Ab)[j] = double2{e[0], e[1]};
+      }
+    }
+  }
+}
 
 __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1412,13 +1546,19 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   const unsigned long long st_entry = __builtin_amdgcn_s_memtime();
 #endif
   const int w = blockIdx.x;
-  if (d.st[w].done) return;
-  if (d.sharded && d.wfail[w] > 0.0) {
+  // window, state and failure flag requested together (one round trip before the band copy)
+  const BaWin W = d.win[w];
+  const int done = d.st[w].done;
+  const double wfail = d.sharded ? d.wfail[w] : 0.0;
+  if (done) return;
+  if (wfail > 0.0) {
     if (threadIdx.x == 0) d.st[w].chol_fail = 1;
     return;
   }
-  const BaWin W = d.win[w];
   const int n = W.n, bw = W.bw, B1 = bw + 1;
+#ifdef LORB_STAGE_DIAG
+  if (threadIdx.x == 64) d.dbg[8 * w + 4] = __builtin_amdgcn_s_memtime() - st_entry;
+#endif
   const int n16 = (n + 15) & ~15;
   const int m = 16 * ((n16 - 48) / 32);  // T = [0, m), M = [m, m+48), B = [m+48, n16)
   const int nB = n16 - m - 48;
@@ -1430,51 +1570,60 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   double* xt = zb + rb;       // 64 x 18 per side (rows of 17); both together hold X (48 x 48)
   double* xb = xt + 64 * 18;
   double* zX = xb + 64 * 18;  // 48
-  {
-    // Flat copy of S (row-major n x B1, contiguous) in 16-byte chunks, kStageU chunks per thread
-    // per batch with all loads of a batch issued before any store.  Element k = (i, off) keeps
-    // S's value inside the matrix; the left triangle of the first bw rows is zeroed and rows
-    // n .. n16-1 are an identity pad.  (i, off) of a thread's chunks advance by a fixed step.
-#ifndef LORB_STAGE_U
-#define LORB_STAGE_U 14
+  // Staging.  The rows each side's first panel reads (view rows 0 .. 79 of both sides) are copied
+  // by all four waves; the rest of the band by waves 2 / 3 while waves 0 / 1 factor, in the order
+  // the panels need it (a block mask in LDS).  Waves 2 / 3 then invert the diagonal 16 x 16 blocks
+  // of L as the panels finish, for the back-substitution.
+  __shared__ unsigned long long s_mask;
+  __shared__ int s_pdone[2];
+  const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
+  const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
+  const int nbk = n16 / 16, ib = 4;
+#ifndef LORB_CHOL_PROG
+#define LORB_CHOL_PROG 1
 #endif
-    constexpr int kStageU = LORB_STAGE_U;
-    const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
-    const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
-    const int di = (2 * 256) / B1, doff = (2 * 256) % B1;
-    int ci0 = (2 * t) / B1, co0 = (2 * t) % B1;  // (row, column) of this thread's first element
-    for (int j0 = t; j0 < nch; j0 += 256 * kStageU) {
-      double2 v[kStageU];
+  const bool prog = LORB_CHOL_PROG && nbk <= 64 && nbk > 2 * ib;
+  const int cpb = 8 * B1;  // chunks per 16-row block
+  // rhs loads issued before the band copy (one round trip for both)
+  double rz[2];
 #pragma unroll
-      for (int u = 0; u < kStageU; ++u) {
-        const int j = j0 + 256 * u;
-        v[u] = S2[j < nsrc ? j : 0];
-      }
+  for (int u = 0; u < 2; ++u) {
+    const int k = t + 256 * u;
+    const int row = k < rt ? k : n16 - 1 - (k - rt);
+    rz[u] = (k < rt + rb && row < n) ? d.rhs[W.row_base + row] : 0.0;
+  }
+  if (prog) {  // both sides' first ib blocks in one batch
+    stage_band2<13>(S2, Ab, 0, ib * cpb, (nbk - ib) * cpb, nch, t, 256, n, bw, nsrc);
+  } else {
+    stage_band<14>(S2, Ab, 0, nch, t, 256, n, bw, nsrc);
+  }
+#ifdef LORB_STAGE_DIAG
+  if (threadIdx.x == 64) d.dbg[8 * w + 6] = __builtin_amdgcn_s_memtime() - st_entry;
+#endif
 #pragma unroll
-      for (int u = 0; u < kStageU; ++u) {
-        const int j = j0 + 256 * u;
-        if (j < nch) {
-          int i = ci0, off = co0;
-          double e[2] = {v[u].x, v[u].y};
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const bool in = i < n && i - (bw - off) >= 0;
-            e[h] = in ? e[h] : ((i >= n && off == bw) ? 1.0 : 0.0);
-            if (++off == B1) { off = 0; ++i; }
-          }
-          reinterpret_cast<double2*>(Ab)[j] = double2{e[0], e[1]};
-        }
-        ci0 += di; co0 += doff;
-        if (co0 >= B1) { co0 -= B1; ++ci0; }
-      }
-    }
-    for (int k = t; k < rt; k += 256) zt[k] = d.rhs[W.row_base + k];
-    for (int k = t; k < rb; k += 256) { const int row = n16 - 1 - k; zb[k] = row < n ? d.rhs[W.row_base + row] : 0.0; }
-    if (t == 0) s_bad = 0;
+  for (int u = 0; u < 2; ++u) {
+    const int k = t + 256 * u;
+    if (k < rt) zt[k] = rz[u];
+    else if (k < rt + rb) zb[k - rt] = rz[u];
+  }
+  for (int k = t + 512; k < rt + rb; k += 256) {  // (n16 > 416 only)
+    const int row = k < rt ? k : n16 - 1 - (k - rt);
+    const double v = row < n ? d.rhs[W.row_base + row] : 0.0;
+    if (k < rt) zt[k] = v; else zb[k - rt] = v;
+  }
+  if (t == 0) {
+    s_bad = 0;
+    s_pdone[0] = 0; s_pdone[1] = 0;
+    unsigned long long msk = 0;
+    for (int b = 0; b < nbk; ++b) msk |= (unsigned long long)(!prog || b < ib || b >= nbk - ib) << (b & 63);
+    s_mask = msk;
   }
   __syncthreads();
-  const BandSide top{Ab, zt, xt, rt, bw, lane, bw, bw, 1};
-  const BandSide bot{Ab, zb, xb, rb, bw, lane, (n16 - 1) * B1 + bw, -1, -bw};
+  BandSide top{Ab, zt, xt, rt, bw, lane, bw, bw, 1};
+  BandSide bot{Ab, zb, xb, rb, bw, lane, (n16 - 1) * B1 + bw, -1, -bw};
+  top.pdone = &s_pdone[0]; bot.pdone = &s_pdone[1];
+  top.nbk = bot.nbk = nbk; top.dir = 1; bot.dir = -1;
+  if (prog) { top.mask = &s_mask; bot.mask = &s_mask; }
   const BandSide& me = wv == 0 ? top : bot;
   v4d T[10];
   double zr = 0.0;
@@ -1482,10 +1631,31 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
 #ifdef LORB_CHOL_STAMPS
   const unsigned long long st0 = __builtin_amdgcn_s_memtime();
   if (lane == 0 && wv == 1) d.dbg[8 * w + 5] = st0 - st_entry;  // staging
+#ifdef LORB_STAGE_DIAG
+#define C2_STAMP(k) do { if (lane == 0 && wv == 0) d.dbg[8 * w + (k)] = __builtin_amdgcn_s_memtime() - st0; } while (0)
+#else
 #define C2_STAMP(k) do { if (lane == 0 && wv < 2) d.dbg[8 * w + (k) + 4 * wv] = __builtin_amdgcn_s_memtime() - st0; } while (0)
+#endif
 #else
 #define C2_STAMP(k) do {} while (0)
 #endif
+  if (wv >= 2) {
+    if (prog) {  // remaining blocks [ib, nbk - ib): wave 2 from the top, wave 3 from the bottom
+      const int lo = ib, hi = nbk - ib, mid = (lo + hi) / 2;
+      for (int k = 0; k < (wv == 2 ? mid - lo : hi - mid); ++k) {
+        const int b = wv == 2 ? lo + k : hi - 1 - k;
+        stage_band<7>(S2, Ab, b * cpb, min((b + 1) * cpb, nch), lane, 64, n, bw, nsrc);
+        if (lane == 0) __hip_atomic_fetch_or(&s_mask, 1ull << b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    const BandSide& side = wv == 2 ? top : bot;
+    int* pd = &s_pdone[wv - 2];
+    const int nblk = (wv == 2 ? m : nB) / 16;
+    for (int p = 0; p + 1 < nblk; ++p) {  // the last block after the panels' barrier
+      while (__hip_atomic_load(pd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= p) __builtin_amdgcn_s_sleep(1);
+      side.linv(16 * p);
+    }
+  }
   if (wv < 2) { me.init(T, zr); me.panels(T, zr, bad, 0, wv == 0 ? m : nB); }
   C2_STAMP(0);
   __syncthreads();
@@ -1504,6 +1674,10 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
     if (bad) s_bad = 1;
   }
   __syncthreads();
+  if (wv >= 2) {  // last diagonal block of each side, behind the M panels
+    const int nblk = (wv == 2 ? m : nB) / 16;
+    if (nblk > 0) (wv == 2 ? top : bot).linv(16 * (nblk - 1));
+  }
   if (wv == 0) {
     // S_M = (S_MM - L_MT L_MT^T) + (S_MM - L_MB L_MB^T) - S_MM ; rows >= m+48 leave the window
 #pragma unroll
@@ -1519,7 +1693,9 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
     for (int J = 0; J < 4; ++J) T[tri4(3, J)] = v4d{0.0, 0.0, 0.0, 0.0};
     zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
     C2_STAMP(1);
-    top.panels(T, zr, bad, m, m + 48);
+    BandSide topM = top;
+    topM.mask = nullptr; topM.pdone = nullptr;
+    topM.panels(T, zr, bad, m, m + 48);
     if (bad) s_bad = 1;
     C2_STAMP(2);
   }
@@ -1529,12 +1705,12 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
     return;
   }
   if (wv == 0) {
-    top.backsub(m + 32, m);                      // y_M
+    top.backsub<false>(m + 32, m);               // y_M
     if (lane < 48) zb[nB + 47 - lane] = zt[m + lane];  // into the reversed bottom rows
   }
   __syncthreads();
-  if (wv == 0) top.backsub(m - 16, 0);           // y_T
-  else if (wv == 1) bot.backsub(nB - 16, 0);     // y_B (reversed)
+  if (wv == 0) top.backsub<true>(m - 16, 0);     // y_T
+  else if (wv == 1) bot.backsub<true>(nB - 16, 0);  // y_B (reversed)
   C2_STAMP(3);
   __syncthreads();
 #undef C2_STAMP
@@ -1553,7 +1729,9 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
     d.rot_cand[c] = lorb::rot_val(xn);
   }
 #ifdef LORB_CHOL_STAMPS
+#ifndef LORB_STAGE_DIAG
   if (lane == 0 && wv == 1) d.dbg[8 * w + 6] = __builtin_amdgcn_s_memtime() - st0;  // to the end
+#endif
 #endif
 }
 

@@ -3,7 +3,7 @@
 cd "$(dirname "$0")/../lorb_slam_amd/csrc" || exit 1
 mkdir -p _build_st
 for f in *.hip; do
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -DLORB_CHOL_STAMPS -c "$f" -o "_build_st/${f%.hip}.o" &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -DLORB_CHOL_STAMPS $EXTRA -c "$f" -o "_build_st/${f%.hip}.o" &
 done
 wait
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared -o ../liblorb_stamps.so _build_st/*.o \
