@@ -1,7 +1,10 @@
 """Reduce rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE, collected in SEPARATE runs) to HBM
 bytes per launch per kernel, and the --stats kernel summary to average durations.
 
-    python tools/pmc_traffic.py PROF_DIR OUT_JSON
+    python tools/pmc_traffic.py PROF_DIR OUT_JSON [--workload KEY]
+
+With --workload the summary is merged into OUT_JSON under "workloads": {KEY: ...} (the layout
+bench.py reads), so one file holds every profiled workload.
 
 PROF_DIR holds the rocprofv3 CSV outputs (searched recursively): *counter_collection.csv from
 the FETCH_SIZE and WRITE_SIZE passes and *kernel_stats.csv from the --kernel-trace --stats pass.
@@ -23,7 +26,7 @@ def short_name(name):
     return m.group(1) if m else name
 
 
-def main(prof_dir, out):
+def main(prof_dir, out, workload=None):
     per = {}
     for path in glob.glob(os.path.join(prof_dir, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
@@ -59,11 +62,27 @@ def main(prof_dir, out):
             e["calls"] = stats[k]["calls"]
             e["avg_us"] = stats[k]["total_ns"] / stats[k]["calls"] / 1e3
         kernels[k] = e
+    summary = {"source": prof_dir, "fetch_correction": 2.0, "kernels": kernels}
+    if workload:
+        try:
+            with open(out) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            doc = {}
+        doc.setdefault("workloads", {})[workload] = summary
+    else:
+        doc = summary
     with open(out, "w") as f:
-        json.dump({"source": prof_dir, "fetch_correction": 2.0, "kernels": kernels}, f, indent=1, sort_keys=True)
+        json.dump(doc, f, indent=1, sort_keys=True)
     for k, e in kernels.items():
         print(k, e)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    args = sys.argv[1:]
+    wl = None
+    if "--workload" in args:
+        i = args.index("--workload")
+        wl = args[i + 1]
+        del args[i:i + 2]
+    main(args[0], args[1], wl)
