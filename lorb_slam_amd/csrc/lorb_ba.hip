@@ -16,7 +16,6 @@
 #include "lorb_ba_math.h"
 #include "lorb_internal.h"
 
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -2131,16 +2130,20 @@ LMOpt to_dev_opt(const lorb_lm_options* o) {
 // ------------------------------------------------------------------------------------------
 // device plan construction state (lorb_ba_plan_create_dev; see "Device-resident plan construction")
 struct lorb_ba_devbuild {
-  int K_cap = 0, P_cap = 0, C = 0, F = 0;
-  int* key_in = nullptr; int* key_out = nullptr; int* val_in = nullptr; int* val_out = nullptr;
-  int* ckey = nullptr; int* ckey_out = nullptr; int* cval = nullptr;
+  int K_cap = 0, P_cap = 0, C = 0, F = 0, Wd = 0;
+  int* key_out = nullptr; int* val_out = nullptr;  // point-sorted: point, observation slot
+  // build scratch, cleared by one memset per build: pt_cnt (P_cap + 1) | hdr (8) | cov (C * C) |
+  // cam_cnt (C) | bits (C * Wd u64, camera x point)
+  int* scr = nullptr; size_t scr_bytes = 0;
   int* pt_cnt = nullptr;      // P_cap + 1
   int* hdr = nullptr;         // [0] valid obs, [1] max obs per point, [2] error flags, [3] points
   int* cov = nullptr;         // C * C
   int* cam_cnt = nullptr;     // C
+  unsigned long long* bits = nullptr;
+  int* hist = nullptr; int* hoff = nullptr; int hist_cap = 0;  // camera-major block histograms
+  int* cam_pt = nullptr;      // K_cap: point of each camera-major slot
   int* perm = nullptr;        // C: input camera -> plan camera
   int* gstart = nullptr;      // group starts
-  void* tmp = nullptr; size_t tmp_bytes = 0;
   int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0, gs_cap = 0;
   std::vector<int> h_hdr, h_cov, h_cam;
   int* pinned = nullptr; size_t pinned_n = 0;
@@ -2722,13 +2725,18 @@ int plan_read(lorb_ba_plan* P, double* const* pose_out, double* const* point_out
 // (observation / point counts, per-camera counts and the C x C covisibility counts) per build, then
 // the camera order (RCM), the (camera, camera) block list, band and kernel choice.  Everything
 // per observation, per point and per pair is built by kernels:
-//   k_db_keys    validity + point keys of the observation slots, per-point counts
-//   radix sort   observations by point (stable: the caller's order within a point)
-//   k_db_cov     per point: camera-pair covisibility counts, per-camera counts, duplicate check
-//   k_db_gather  point-sorted structure arrays, camera keys (RCM labels)
-//   radix sort   optimised observations by camera (stable) -> camera-major slots
+//   k_db_keys    validity of the observation slots, per-point counts, camera x point bitsets
+//                (a camera seen twice by one point is the bit already set)
+//   k_db_scan1   point offsets (one workgroup: exclusive scan, total, largest count)
+//   k_db_scatter counting sort by point: slot order within a point restored by k_db_segsort
+//                (stable: the caller's order within a point, as a stable radix sort gives it)
+//   k_db_cov     covisibility counts of camera pairs = popcount(bits_a & bits_b), per-camera counts
+//   k_db_gather  point-sorted structure arrays, per-block camera histograms (RCM labels)
+//   k_db_scan1   camera-major block offsets
+//   k_db_place   counting sort of the optimised observations by camera (stable), camera slots
 //   k_db_groups  point groups of <= kGB observations (weights k + 1, fixed-size bins)
-//   k_db_pairs   per block pair: the points both cameras observe (sorted-list intersection)
+//   k_db_pairs   per block pair: the points both cameras observe (binary search of the lower
+//                camera's point list staged in LDS)
 //   k_db_init    initial values (float -> double, camera relabelling)
 // ==========================================================================================
 
@@ -2736,101 +2744,157 @@ namespace {
 
 
 
-__global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int K_cap, int P_cap, int C, int F,
-                                                 int* __restrict__ key, int* __restrict__ val,
-                                                 int* __restrict__ pt_cnt, int* __restrict__ hdr) {
+// Build-time scratch of the device plan (one allocation, one clear per build):
+//   pt_cnt[P_cap + 1] | hdr[8] | cov[C * C] | cam_cnt[C] | bits[C * Wd] (u64 words)
+// hdr: [0] valid observations, [1] largest count per point, [2] error flags, [3] points.
+__global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, int F, int Wd,
+                                                 int* __restrict__ pt_cnt, int* __restrict__ hdr,
+                                                 unsigned long long* __restrict__ bits) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= K_cap) return;
   const int n_obs = *w.d_n_obs, n_pt = *w.d_n_points;
-  int p = P_cap;
-  if (k < n_obs) {
-    const int q = w.d_obs_point[k], f = w.d_obs_frame[k];
-    if (f >= -F && f < C) {
-      if (q < 0 || q >= n_pt) atomicOr(&hdr[2], 1);
-      else { p = q; atomicAdd(&pt_cnt[q], 1); atomicAdd(&hdr[0], 1); }
-    } else if (f >= C) {
-      atomicOr(&hdr[2], 2);
-    }
-  }
-  key[k] = p;
-  val[k] = k;
   if (k == 0) hdr[3] = n_pt;
-}
-
-// one thread per point: covisibility of its optimised cameras (ordered pairs, both directions),
-// per-camera counts, largest observation count, a camera seen twice by one point (error 4).  The
-// counts build in an LDS copy per workgroup (a few workgroups stride over the points) and are
-// flushed with one global atomic per non-zero entry -- the camera pairs are few and hot, so
-// per-observation global atomics would serialise on them.  LDS=false: C too large for LDS.
-constexpr int kCovWG = 16;
-template <bool LDS>
-__global__ __launch_bounds__(1024) void k_db_cov(lorb_ba_window_dev w, int C, const int* __restrict__ pt_off,
-                                                 const int* __restrict__ val, int* __restrict__ cov,
-                                                 int* __restrict__ cam_cnt, int* __restrict__ hdr) {
-  extern __shared__ int s_cov[];  // C * C covisibility, then C camera counts
-  int* lc = LDS ? s_cov : cov;
-  int* lcc = LDS ? s_cov + C * C : cam_cnt;
-  if (LDS) {
-    for (int i = threadIdx.x; i < C * C + C; i += 1024) s_cov[i] = 0;
-    __syncthreads();
-  }
-  const int n_pt = *w.d_n_points;
-  int mx = 0, err = 0;
-  for (int p = blockIdx.x * 1024 + threadIdx.x; p < n_pt; p += gridDim.x * 1024) {
-    const int a0 = pt_off[p], a1 = pt_off[p + 1];
-    mx = max(mx, a1 - a0);
-    for (int a = a0; a < a1; ++a) {
-      const int fa = w.d_obs_frame[val[a]];
-      if (fa < 0) continue;
-      atomicAdd(&lcc[fa], 1);
-      for (int b = a0; b < a1; ++b) {
-        if (b == a) continue;
-        const int fb = w.d_obs_frame[val[b]];
-        if (fb < 0) continue;
-        err |= fb == fa;
-        atomicAdd(&lc[fa * C + fb], 1);
+  if (k >= n_obs) return;
+  const int q = w.d_obs_point[k], f = w.d_obs_frame[k];
+  if (f >= -F && f < C) {
+    if (q < 0 || q >= n_pt) {
+      atomicOr(&hdr[2], 1);
+    } else {
+      atomicAdd(&pt_cnt[q], 1);
+      if (f >= 0) {
+        const unsigned long long m = 1ull << (q & 63);
+        if (atomicOr(&bits[(size_t)f * Wd + (q >> 6)], m) & m) atomicOr(&hdr[2], 4);
       }
     }
+  } else if (f >= C) {
+    atomicOr(&hdr[2], 2);
   }
-  // workgroup max / error flag, then one global atomic each
+}
+
+// One workgroup: out[0 .. n) = exclusive prefix sums of in[0 .. n).  hdr (optional): hdr[0] =
+// total, hdr[1] = max(in).
+__global__ __launch_bounds__(1024) void k_db_scan1(const int* __restrict__ in, int* __restrict__ out, int n,
+                                                   int* __restrict__ hdr) {
+  __shared__ int wsum[16];
+  int mx;
+  const int tot = lorb::wg_excl_scan(in, out, n, wsum, &mx);
+  if (hdr) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mx = max(mx, __shfl_xor(mx, o, 64));
-    err |= __shfl_xor(err, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (mx) atomicMax(&hdr[1], mx);
-    if (err) atomicOr(&hdr[2], 4);
-  }
-  if (LDS) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < C * C; i += 1024)
-      if (s_cov[i]) atomicAdd(&cov[i], s_cov[i]);
-    for (int i = threadIdx.x; i < C; i += 1024)
-      if (s_cov[C * C + i]) atomicAdd(&cam_cnt[i], s_cov[C * C + i]);
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(&hdr[1], mx);
+    if (threadIdx.x == 0) hdr[0] = tot;
   }
 }
 
-__global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d, int K, int C,
+// counting sort by point: slot k goes to the end of its point's free range (the counts run down
+// to zero, which leaves pt_cnt cleared); k_db_segsort restores the slot order within a point
+__global__ __launch_bounds__(256) void k_db_scatter(lorb_ba_window_dev w, int C, int F,
+                                                    const int* __restrict__ pt_off, int* __restrict__ pt_cnt,
+                                                    int* __restrict__ val) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  const int n_obs = *w.d_n_obs, n_pt = *w.d_n_points;
+  if (k >= n_obs) return;
+  const int q = w.d_obs_point[k], f = w.d_obs_frame[k];
+  if (f < -F || f >= C || q < 0 || q >= n_pt) return;
+  val[pt_off[q] + atomicSub(&pt_cnt[q], 1) - 1] = k;
+}
+
+// one thread per point: its slots ascending.  Points have a few observations (up to kGB - 1):
+// up to 16 sort in registers (odd-even transposition network), longer ones by insertion in place.
+__global__ __launch_bounds__(256) void k_db_segsort(lorb_ba_window_dev w, const int* __restrict__ pt_off,
+                                                    int* __restrict__ val, int* __restrict__ key) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= *w.d_n_points) return;
+  const int a0 = pt_off[p], a1 = pt_off[p + 1], m = a1 - a0;
+  if (m <= 16) {
+    int v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = i < m ? val[a0 + i] : 0x7fffffff;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+#pragma unroll
+      for (int i = r & 1; i + 1 < 16; i += 2) {
+        const int lo = min(v[i], v[i + 1]), hi = max(v[i], v[i + 1]);
+        v[i] = lo; v[i + 1] = hi;
+      }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (i < m) { val[a0 + i] = v[i]; key[a0 + i] = p; }
+  } else {
+    for (int i = a0 + 1; i < a1; ++i) {
+      const int x = val[i];
+      int j = i - 1;
+      while (j >= a0 && val[j] > x) { val[j + 1] = val[j]; --j; }
+      val[j + 1] = x;
+    }
+    for (int i = a0; i < a1; ++i) key[i] = p;
+  }
+}
+
+// one wavefront per camera pair (a <= b): covisibility = popcount of the AND of their point bitsets
+__global__ __launch_bounds__(256) void k_db_cov(int C, int Wd, const unsigned long long* __restrict__ bits,
+                                                int* __restrict__ cov, int* __restrict__ cam_cnt) {
+  const int pr = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (pr >= C * (C + 1) / 2) return;
+  int a = 0, r = pr;  // pr -> (a, b), a <= b, row a holds C - a pairs
+  while (r >= C - a) { r -= C - a; ++a; }
+  const int b = a + r;
+  const unsigned long long* x = bits + (size_t)a * Wd;
+  const unsigned long long* y = bits + (size_t)b * Wd;
+  int c = 0;
+  for (int i = lane; i < Wd; i += 64) c += __popcll(x[i] & y[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane == 0) {
+    if (a == b) {
+      cam_cnt[a] = c;
+      cov[a * C + a] = 0;
+    } else {
+      cov[a * C + b] = c;
+      cov[b * C + a] = c;
+    }
+  }
+}
+
+// point-sorted structure arrays; per 256-observation block the plan-camera histogram (camera-major
+// hist[c * NB + block], fixed-camera observations not counted)
+__global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d, int K, int C, int NB,
                                                    const int* __restrict__ key, const int* __restrict__ val,
-                                                   const int* __restrict__ perm, int* __restrict__ ckey,
-                                                   int* __restrict__ cval) {
+                                                   const int* __restrict__ perm, int* __restrict__ hist) {
+  extern __shared__ int s_h[];  // C
+  for (int i = threadIdx.x; i < C; i += 256) s_h[i] = 0;
+  __syncthreads();
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= K) return;
-  const int k = val[e], f = w.d_obs_frame[k];
-  const int c = f >= 0 ? perm[f] : -1;
-  const_cast<int*>(d.obs_pt)[e] = key[e];
-  const_cast<int*>(d.obs_cam)[e] = c;
-  const_cast<int*>(d.obs_fix)[e] = f >= 0 ? -1 : -1 - f;
-  const_cast<double2*>(d.obs_uv)[e] = make_double2(w.d_obs_uv[2 * k], w.d_obs_uv[2 * k + 1]);
-  const_cast<int*>(d.obs_cm)[e] = -1;
-  ckey[e] = c >= 0 ? c : C;
-  cval[e] = e;
+  if (e < K) {
+    const int k = val[e], f = w.d_obs_frame[k];
+    const int c = f >= 0 ? perm[f] : -1;
+    const_cast<int*>(d.obs_pt)[e] = key[e];
+    const_cast<int*>(d.obs_cam)[e] = c;
+    const_cast<int*>(d.obs_fix)[e] = f >= 0 ? -1 : -1 - f;
+    const_cast<double2*>(d.obs_uv)[e] = make_double2(w.d_obs_uv[2 * k], w.d_obs_uv[2 * k + 1]);
+    const_cast<int*>(d.obs_cm)[e] = -1;
+    if (c >= 0) atomicAdd(&s_h[c], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += 256) hist[(size_t)i * NB + blockIdx.x] = s_h[i];
 }
 
-__global__ __launch_bounds__(256) void k_db_obscm(BaDev d, int n_opt) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j < n_opt) const_cast<int*>(d.obs_cm)[d.cam_obs[j]] = j;
+// counting sort of the optimised observations by plan camera, stable: slot = camera-major block
+// offset + rank among the block's earlier observations of the same camera.  Writes the camera-major
+// list, its point ids and each observation's camera slot.
+__global__ __launch_bounds__(256) void k_db_place(BaDev d, int K, int NB, const int* __restrict__ hoff,
+                                                  int* __restrict__ cam_pt) {
+  __shared__ int s_c[256];
+  const int e = blockIdx.x * 256 + threadIdx.x, t = threadIdx.x;
+  const int c = e < K ? d.obs_cam[e] : -1;
+  s_c[t] = c;
+  __syncthreads();
+  if (c < 0) return;
+  int rank = 0;
+  for (int u = 0; u < t; ++u) rank += s_c[u] == c;
+  const int j = hoff[(size_t)c * NB + blockIdx.x] + rank;
+  const_cast<int*>(d.cam_obs)[j] = e;
+  const_cast<int*>(d.obs_cm)[e] = j;
+  cam_pt[j] = d.obs_pt[e];
 }
 
 // point groups: point p (weight k_p + 1, exclusive weight prefix off[p] + p) goes to group
@@ -2860,28 +2924,38 @@ __global__ __launch_bounds__(256) void k_db_groups(BaDev d, const int* __restric
   const_cast<PBlk*>(d.pblk)[g] = b;
 }
 
-// one workgroup per (camera, camera) block: its pair list in point order
-__global__ __launch_bounds__(256) void k_db_pairs(BaDev d) {
+// one workgroup per (camera, camera) block: its pair list in point order.  The lower camera's
+// point ids (ascending) are staged in LDS for the binary searches when they fit.
+constexpr int kPairsLds = 8192;
+__global__ __launch_bounds__(256) void k_db_pairs(BaDev d, const int* __restrict__ cam_pt) {
   __shared__ int wsum[4];
+  __shared__ int s_pt[kPairsLds];
   const BlockPair B = d.bp[blockIdx.x];
   const int h0 = d.cam_obs_off[B.ch], h1 = d.cam_obs_off[B.ch + 1];
   const int l0 = d.cam_obs_off[B.cl], l1 = d.cam_obs_off[B.cl + 1];
+  const int nl = l1 - l0;
+  const bool diag = B.ch == B.cl, lds = nl <= kPairsLds;
+  if (!diag && lds) {
+    for (int i = threadIdx.x; i < nl; i += 256) s_pt[i] = cam_pt[l0 + i];
+    __syncthreads();
+  }
+  const int* lp = lds ? s_pt : cam_pt + l0;
   int2* out = const_cast<int2*>(d.pairs) + B.off;
   int run = 0;
   for (int base = h0; base < h1; base += 256) {
     const int i = base + threadIdx.x;
     int j = -1;
     if (i < h1) {
-      if (B.ch == B.cl) {
+      if (diag) {
         j = i;
       } else {
-        const int p = d.obs_pt[d.cam_obs[i]];
-        int lo = l0, hi = l1;
+        const int p = cam_pt[i];
+        int lo = 0, hi = nl;
         while (lo < hi) {
           const int m = (lo + hi) >> 1;
-          if (d.obs_pt[d.cam_obs[m]] < p) lo = m + 1; else hi = m;
+          if (lp[m] < p) lo = m + 1; else hi = m;
         }
-        if (lo < l1 && d.obs_pt[d.cam_obs[lo]] == p) j = lo;
+        if (lo < nl && lp[lo] == p) j = l0 + lo;
       }
     }
     int tot;
@@ -2917,11 +2991,6 @@ __global__ __launch_bounds__(256) void k_db_result(BaDev d, int C, int P, const 
     for (int k = i; k < 3 * P; k += gridDim.x * 256) pt_out[k] = (float)d.x_pt[cur][k];
 }
 
-int bits_for(int v) {
-  int b = 1;
-  while ((1 << b) <= v) ++b;
-  return b;
-}
 
 }  // namespace
 
@@ -2947,13 +3016,19 @@ int grow(lorb_ba_plan* P, T** ptr, int* cap, size_t need) {
 int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   lorb_ba_devbuild& b = *P->devb;
   b.K_cap = w->max_obs; b.P_cap = w->max_points; b.C = w->n_poses; b.F = w->n_fixed;
+  b.Wd = (std::max(b.P_cap, 1) + 63) / 64;
   const size_t K = (size_t)std::max(b.K_cap, 1), Pn = (size_t)std::max(b.P_cap, 1), C = (size_t)std::max(b.C, 1);
   BaDev& d = P->dev;
-  LORB_TRY(dalloc(P, K, &b.key_in)); LORB_TRY(dalloc(P, K, &b.key_out));
-  LORB_TRY(dalloc(P, K, &b.val_in)); LORB_TRY(dalloc(P, K, &b.val_out));
-  LORB_TRY(dalloc(P, K, &b.ckey)); LORB_TRY(dalloc(P, K, &b.ckey_out)); LORB_TRY(dalloc(P, K, &b.cval));
-  LORB_TRY(dalloc(P, Pn + 1, &b.pt_cnt)); LORB_TRY(dalloc(P, (size_t)8, &b.hdr));
-  LORB_TRY(dalloc(P, C * C, &b.cov)); LORB_TRY(dalloc(P, C, &b.cam_cnt));
+  LORB_TRY(dalloc(P, K, &b.key_out)); LORB_TRY(dalloc(P, K, &b.val_out)); LORB_TRY(dalloc(P, K, &b.cam_pt));
+  {
+    const size_t ints = ((Pn + 1 + 8 + C * C + C) + 1) & ~(size_t)1;  // the u64 bitsets 8-byte aligned
+    b.scr_bytes = sizeof(int) * ints + sizeof(unsigned long long) * C * (size_t)b.Wd;
+    unsigned char* m;
+    LORB_TRY(dalloc(P, b.scr_bytes, &m));
+    b.scr = reinterpret_cast<int*>(m);
+    b.pt_cnt = b.scr; b.hdr = b.pt_cnt + Pn + 1; b.cov = b.hdr + 8; b.cam_cnt = b.cov + C * C;
+    b.bits = reinterpret_cast<unsigned long long*>(b.scr + ints);
+  }
   int *a_pt, *a_cam, *a_fix, *a_cm, *a_camobs, *a_win, *a_act, *a_ptoff;
   double2* a_uv;
   double* a_fixp;
@@ -2988,14 +3063,6 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(dalloc(P, n, &d.ycam));
   LORB_TRY(dalloc(P, (size_t)8, &d.dbg));
   LORB_TRY(dalloc(P, (size_t)1, &P->d_state)); d.st = P->d_state;
-  size_t t1 = 0, t2 = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, t1, b.key_in, b.key_out, b.val_in, b.val_out, (int)K, 0, 31,
-                                         ctx->stream) != hipSuccess ||
-      hipcub::DeviceScan::ExclusiveSum(nullptr, t2, b.pt_cnt, a_ptoff, (int)Pn + 1, ctx->stream) != hipSuccess)
-    return lorb::set_error(ctx, LORB_E_DEVICE, "hipcub temp-storage query failed");
-  b.tmp_bytes = std::max(t1, t2);
-  LORB_HIP(ctx, hipMalloc(&b.tmp, b.tmp_bytes));
-  P->allocs.push_back(b.tmp);
   P->W = 1;
   P->hwin.assign(1, BaWin{});
   P->pt_launch = b.P_cap;
@@ -3045,33 +3112,20 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   hipStream_t s = ctx->stream;
   BaDev& d = P->dev;
   const int C = b.C, F = b.F, Kc = w->max_obs;
-  // 1. observation keys, per-point counts; sort by point (stable); point offsets
-  LORB_HIP(ctx, hipMemsetAsync(b.pt_cnt, 0, sizeof(int) * ((size_t)b.P_cap + 1), s));
-  LORB_HIP(ctx, hipMemsetAsync(b.hdr, 0, sizeof(int) * 8, s));
-  LORB_HIP(ctx, hipMemsetAsync(b.cov, 0, sizeof(int) * (size_t)std::max(C * C, 1), s));
-  LORB_HIP(ctx, hipMemsetAsync(b.cam_cnt, 0, sizeof(int) * (size_t)std::max(C, 1), s));
+  // 1. per-point counts and camera x point bitsets; point offsets; counting sort by point
+  //    (stable); covisibility counts from the bitsets
+  LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
+  const int nb_obs = lorb::ceil_div(std::max(Kc, 1), 256), nb_pt = lorb::ceil_div(std::max(b.P_cap, 1), 256);
+  hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);
+  hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1,
+                     b.hdr);
   if (Kc > 0) {
-    hipLaunchKernelGGL(k_db_keys, dim3(lorb::ceil_div(Kc, 256)), dim3(256), 0, s, *w, Kc, b.P_cap, C, F, b.key_in,
-                       b.val_in, b.pt_cnt, b.hdr);
-    size_t tb = b.tmp_bytes;
-    if (hipcub::DeviceRadixSort::SortPairs(b.tmp, tb, b.key_in, b.key_out, b.val_in, b.val_out, Kc, 0,
-                                           bits_for(b.P_cap), s) != hipSuccess)
-      return lorb::set_error(ctx, LORB_E_DEVICE, "radix sort (points) failed");
+    hipLaunchKernelGGL(k_db_scatter, dim3(nb_obs), dim3(256), 0, s, *w, C, F, d.pt_obs_off, b.pt_cnt, b.val_out);
+    hipLaunchKernelGGL(k_db_segsort, dim3(nb_pt), dim3(256), 0, s, *w, d.pt_obs_off, b.val_out, b.key_out);
   }
-  {
-    size_t tb = b.tmp_bytes;
-    if (hipcub::DeviceScan::ExclusiveSum(b.tmp, tb, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1, s) != hipSuccess)
-      return lorb::set_error(ctx, LORB_E_DEVICE, "scan (point offsets) failed");
-  }
-  {
-    const size_t lds = sizeof(int) * ((size_t)C * C + C);
-    if (lds <= 64 * 1024)
-      hipLaunchKernelGGL(k_db_cov<true>, dim3(kCovWG), dim3(1024), lds, s, *w, C, d.pt_obs_off, b.val_out, b.cov,
-                         b.cam_cnt, b.hdr);
-    else
-      hipLaunchKernelGGL(k_db_cov<false>, dim3(lorb::ceil_div(std::max(b.P_cap, 1), 1024)), dim3(1024), 0, s, *w, C,
-                         d.pt_obs_off, b.val_out, b.cov, b.cam_cnt, b.hdr);
-  }
+  if (C > 0)
+    hipLaunchKernelGGL(k_db_cov, dim3(lorb::ceil_div(C * (C + 1) / 2, 4)), dim3(256), 0, s, C, b.Wd, b.bits, b.cov,
+                       b.cam_cnt);
   LORB_CHECK_LAUNCH(ctx);
   // 2. the one readback: counts and the covisibility structure
   const size_t nrb = 8 + (size_t)C + (size_t)C * C;
@@ -3173,20 +3227,23 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   }
   // 4. structure kernels
   if (K > 0) {
-    hipLaunchKernelGGL(k_db_gather, dim3(lorb::ceil_div(K, 256)), dim3(256), 0, s, *w, d, K, C, b.key_out, b.val_out,
-                       b.perm, b.ckey, b.cval);
-    size_t tb = b.tmp_bytes;
-    if (hipcub::DeviceRadixSort::SortPairs(b.tmp, tb, b.ckey, b.ckey_out, b.cval, const_cast<int*>(d.cam_obs), K, 0,
-                                           bits_for(C), s) != hipSuccess)
-      return lorb::set_error(ctx, LORB_E_DEVICE, "radix sort (cameras) failed");
-    if (cam_off[C] > 0) hipLaunchKernelGGL(k_db_obscm, dim3(lorb::ceil_div(cam_off[C], 256)), dim3(256), 0, s, d, cam_off[C]);
+    const int NB = lorb::ceil_div(K, 256);
+    if ((size_t)NB * C > (size_t)b.hist_cap) {
+      LORB_TRY(grow(P, &b.hist, &b.hist_cap, (size_t)NB * C));
+      int cap2 = 0;
+      LORB_TRY(grow(P, &b.hoff, &cap2, (size_t)b.hist_cap));
+    }
+    hipLaunchKernelGGL(k_db_gather, dim3(NB), dim3(256), sizeof(int) * C, s, *w, d, K, C, NB, b.key_out, b.val_out,
+                       b.perm, b.hist);
+    hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.hist, b.hoff, NB * C, nullptr);
+    hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), 0, s, d, K, NB, b.hoff, b.cam_pt);
   }
   if (G > 0) {
     LORB_HIP(ctx, hipMemsetAsync(b.gstart, 0xff, sizeof(int) * G, s));
     hipLaunchKernelGGL(k_db_group_starts, dim3(lorb::ceil_div(Pn, 256)), dim3(256), 0, s, d.pt_obs_off, Pn, S, b.gstart);
     hipLaunchKernelGGL(k_db_groups, dim3(lorb::ceil_div(G, 256)), dim3(256), 0, s, d, d.pt_obs_off, Pn, G, b.gstart);
   }
-  if (!bps.empty()) hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), 0, s, d);
+  if (!bps.empty()) hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), 0, s, d, b.cam_pt);
   {
     const int m = std::max(std::max(6 * C, 6 * F), std::min(3 * Pn, 256 * 1024));
     if (m > 0)

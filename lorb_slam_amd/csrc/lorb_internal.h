@@ -152,6 +152,36 @@ __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* total) {
   return pre + incl - v;
 }
 
+// Exclusive prefix sums of in[0 .. n) into out[0 .. n) by ONE 1024-thread workgroup: tiles of
+// 1024 x 8 consecutive values with a running carry (a small array needs one launch, not the two or
+// three of a device-wide scan).  Returns the total; *mx (optional) gets this thread's max of in.
+__device__ __forceinline__ int wg_excl_scan(const int* __restrict__ in, int* __restrict__ out, int n, int* wsum,
+                                            int* mx = nullptr) {
+  const int t = threadIdx.x;
+  int carry = 0, m = 0;
+  for (int base = 0; base < n; base += 8192) {
+    int v[8], loc = 0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + 8 * t + u;
+      v[u] = i < n ? in[i] : 0;
+      m = max(m, v[u]);
+      loc += v[u];
+    }
+    int tot;
+    int run = carry + block_excl_scan_1024(loc, wsum, &tot);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + 8 * t + u;
+      if (i < n) out[i] = run;
+      run += v[u];
+    }
+    carry += tot;
+  }
+  if (mx) *mx = m;
+  return carry;
+}
+
 // Exclusive max-scan (identity `lo`) across an NT-thread workgroup; wmax: __shared__ int[NT / 64].
 template <int NT>
 __device__ __forceinline__ int block_excl_max(int v, int lo, int* wmax) {

@@ -19,11 +19,9 @@
 //
 // Everything stays in HBM: map points (position, descriptor), observations (point, keyframe id, uv),
 // a ring of keyframe poses.  One step = matcher + unprojection + append (one workgroup, block scans
-// in keypoint order) + cull/compaction (flags, hipcub scans, stable gathers) + the device-built BA
+// in keypoint order) + cull/compaction (flags, one-launch scans, stable gathers) + the device-built BA
 // plan (lorb_ba_plan_update_dev: its one small readback is the step's only host synchronisation)
 // + the LM solve (hipGraph per iteration) + the float write-back.
-#include <hipcub/hipcub.hpp>
-
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -152,6 +150,13 @@ __global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, i
   }
 }
 
+// the two compaction scans in one launch: workgroup 0 the point flags, workgroup 1 the observation flags
+__global__ __launch_bounds__(1024) void k_map_scans(MapDev m, int Pb, int Kb) {
+  __shared__ int wsum[16];
+  if (blockIdx.x == 0) lorb::wg_excl_scan(m.flag_pt, m.newid, Pb + 1, wsum);
+  else lorb::wg_excl_scan(m.flag_obs, m.newpos, Kb + 1, wsum);
+}
+
 // new counts; the window's initial poses and the fixed poses from the ring
 __global__ __launch_bounds__(256) void k_map_window(MapDev m, int Pb, int Kb, int t0) {
   const int i = threadIdx.x;
@@ -179,7 +184,6 @@ struct lorb_map {
   double prof_ms[8] = {};
   int prof_n = 0;
   int* cc_t = nullptr; int* cc_d = nullptr; int* mt = nullptr; int* nm = nullptr; float* xyz = nullptr;
-  void* tmp = nullptr; size_t tmp_bytes = 0;
   int* pinned = nullptr;
   lorb_ba_plan* plan = nullptr;
   std::vector<void*> allocs;
@@ -226,12 +230,6 @@ int map_alloc(lorb_map* M, const lorb_map_init* in) {
   M->n_cap = (int)n;
   LORB_TRY(malloc_n(M, n, &M->cc_t)); LORB_TRY(malloc_n(M, n, &M->cc_d)); LORB_TRY(malloc_n(M, n, &M->mt));
   LORB_TRY(malloc_n(M, (size_t)1, &M->nm)); LORB_TRY(malloc_n(M, 3 * n, &M->xyz));
-  size_t t1 = 0, t2 = 0;
-  if (hipcub::DeviceScan::ExclusiveSum(nullptr, t1, m.flag_pt, m.newid, (int)P + 1, M->ctx->stream) != hipSuccess ||
-      hipcub::DeviceScan::ExclusiveSum(nullptr, t2, m.flag_obs, m.newpos, (int)K + 1, M->ctx->stream) != hipSuccess)
-    return lorb::set_error(M->ctx, LORB_E_DEVICE, "hipcub temp-storage query failed");
-  M->tmp_bytes = std::max(t1, t2);
-  LORB_TRY(malloc_n(M, M->tmp_bytes, reinterpret_cast<uint8_t**>(&M->tmp)));
   LORB_HIP(M->ctx, hipHostMalloc(reinterpret_cast<void**>(&M->pinned), sizeof(int) * 8));
   return LORB_OK;
 }
@@ -256,12 +254,7 @@ int map_slide(lorb_map* M, int t0, int Pb, int Kb) {
   LORB_HIP(ctx, hipMemsetAsync(m.flag_pt, 0, sizeof(int) * ((size_t)Pb + 1), s));
   if (Kb > 0) hipLaunchKernelGGL(k_map_mark, dim3(lorb::ceil_div(Kb, 256)), dim3(256), 0, s, m, Kb, t0);
   hipLaunchKernelGGL(k_map_obs_flag, dim3(lorb::ceil_div(Kb + 1, 256)), dim3(256), 0, s, m, Kb, t0);
-  size_t tb = M->tmp_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(M->tmp, tb, m.flag_pt, m.newid, Pb + 1, s) != hipSuccess)
-    return lorb::set_error(ctx, LORB_E_DEVICE, "scan (points) failed");
-  tb = M->tmp_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(M->tmp, tb, m.flag_obs, m.newpos, Kb + 1, s) != hipSuccess)
-    return lorb::set_error(ctx, LORB_E_DEVICE, "scan (observations) failed");
+  hipLaunchKernelGGL(k_map_scans, dim3(2), dim3(1024), 0, s, m, Pb, Kb);
   const int nmax = std::max(Pb, Kb);
   if (nmax > 0) hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, t0);
   hipLaunchKernelGGL(k_map_window, dim3(1), dim3(256), 0, s, m, Pb, Kb, t0);
