@@ -1235,6 +1235,13 @@ __device__ __forceinline__ void wait_bit(unsigned long long* mask, int b) {
   while (!((__hip_atomic_load(mask, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >> b) & 1ull))
     __builtin_amdgcn_s_sleep(1);
 }
+// SLEEP: the waiting wave backs off between polls so that it does not compete for LDS with the
+// chain it waits on; the chain wave's own wait is short and spins
+template <bool SLEEP>
+__device__ __forceinline__ void wait_ge(int* c, int v) {
+  while (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v)
+    if (SLEEP) __builtin_amdgcn_s_sleep(1);
+}
 
 struct BandSide {
   double* A;     // band storage of the whole matrix (row-major, rows x (bw + 1), row i holds cols
@@ -1248,8 +1255,9 @@ struct BandSide {
   int rows, bw, lane;
   int base, si, sj;
   unsigned long long* mask = nullptr;  // progressive staging (null: the whole band is staged)
-  int* pdone = nullptr;                // panels whose L is in the band (release-counted)
+  int* pdone = nullptr;                // panels whose L is in the band (release-counted, for linv)
   int nbk = 0, dir = 0;                // row blocks; +1 top view, -1 reversed bottom view
+  unsigned long long* phases = nullptr;  // LORB_CHOL_PHASES diagnostics: chain wait / factor / store cycles
 
   __device__ __forceinline__ int idx(int i, int j) const { return base + si * i + sj * j; }
 
@@ -1258,52 +1266,55 @@ struct BandSide {
     const double v = A[ok ? idx(i, j) : base];
     return ok ? v : 0.0;
   }
-  __device__ __forceinline__ void init(v4d (&T)[10], double& zr) const {
+  __device__ __forceinline__ void init_tiles(v4d (&T)[10]) const {  // column 0 is the chain wave's
 #pragma unroll
-    for (int I = 0; I < 4; ++I)
+    for (int I = 1; I < 4; ++I)
 #pragma unroll
-      for (int J = 0; J <= I; ++J)
+      for (int J = 1; J <= I; ++J)
 #pragma unroll
         for (int r = 0; r < 4; ++r) T[tri4(I, J)][r] = get(16 * I + (lane >> 4) + 4 * r, 16 * J + (lane & 15));
+  }
+  __device__ __forceinline__ void init_panel(double (&P)[NB], double& zr) const {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) P[q] = get(lane, q);
     zr = lane < rows ? z[lane] : 0.0;
   }
-  // panels kb = kb0, kb0+16, ... < kend.  Per-lane addresses are linear in kb; band validity is
-  // static per lane and element, only the row limit varies.  The pivot and next-column
-  // multipliers use v_readlane (the dependency chain); the other multipliers of a column go
-  // through LDS broadcast reads, off the chain.
-  __device__ __forceinline__ void panels(v4d (&T)[10], double& zr, bool& bad, int kb0, int kend) const {
-    const int ci = lane & 15, ck = lane >> 4;
+  // Lookahead split of the panel loop over two wavefronts of one side.  The CHAIN wave factors
+  // panels kb = kb0, kb0+16, ... < kend (lane = panel row): v_readlane pivots, rsqrt-refined, the
+  // forward substitution fused; it writes L to the band and to xch and posts *lrd.  The UPDATE
+  // wave holds the 64 x 64 trailing window as ten 16 x 16 MFMA accumulator tiles: on each posted
+  // panel it first applies the rank-16 update to the next panel's column (tiles (1..3, 1)), hands
+  // that column to the chain wave through pb (lane = row) and posts *prd, and only then updates
+  // the rest of the window and slides it by 16 -- off the chain's critical path.
+  //   chain(): P = the first panel when `pre` (else it comes from pb); pwant counts the pb posts
+  //   consumed so far (continues across phases).
+  __device__ __forceinline__ void chain(double (&P)[NB], double& zr, bool& bad, int kb0, int kend, bool pre,
+                                        int* lrd, int* prd, int& pwant, const double* pb) const {
     const int dstep = 16 * (si + sj);  // address step of one panel along the diagonal
-    int tn_addr = idx(kb0 + 64 + ck, kb0 + 16 + ci);  // entering tile (J, r) adds 4 r si + 16 J sj (below)
-    unsigned tn_ok = 0;
-#pragma unroll
-    for (int J = 0; J < 4; ++J)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 64 + ck + 4 * r, j = 16 + 16 * J + ci;
-        tn_ok |= (unsigned)(j <= i && i - j <= bw) << (4 * J + r);
-      }
     unsigned l_ok = 0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) l_ok |= (unsigned)(q <= lane && lane - q <= bw) << q;
     int l_base = idx(kb0 + lane, kb0);  // slot of (kb0 + lane, kb0 + q) = l_base + q sj
     double* colbuf = xch;  // 16 x 64 during the factorization (xch is idle then)
     double* dummy = xch + lane * 17 + 16;
+#ifdef LORB_CHOL_PHASES
+    unsigned long long ph_w = 0, ph_c = 0, ph_s = 0, tq = __builtin_amdgcn_s_memtime();
+#define CH_PH(v) do { const unsigned long long q_ = __builtin_amdgcn_s_memtime(); v += q_ - tq; tq = q_; } while (0)
+#else
+#define CH_PH(v) do {} while (0)
+#endif
     for (int kb = kb0; kb < kend; kb += 16) {
       // Opaque per-iteration copies of the lane constants: otherwise every lane comparison of the
       // unrolled panel is hoisted out of the loop as an SGPR mask and the masks spill.
-      int lane = this->lane, lok = (int)l_ok, tok = (int)tn_ok;
-      asm volatile("" : "+v"(lane), "+v"(lok), "+v"(tok));
+      int lane = this->lane, lok = (int)l_ok;
+      asm volatile("" : "+v"(lane), "+v"(lok));
+      if (!(pre && kb == kb0)) {
+        wait_ge<false>(prd, ++pwant);
+#pragma unroll
+        for (int q = 0; q < NB; ++q) P[q] = pb[lane * 17 + q];  // lanes < q: upper garbage, never used
+      }
+      CH_PH(ph_w);
       const double zin = kb + 16 + lane < rows ? z[kb + 16 + lane] : 0.0;
-#pragma unroll
-      for (int I = 0; I < 4; ++I)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) xch[(16 * I + ck + 4 * r) * 17 + ci] = T[tri4(I, 0)][r];
-      wave_sync_lds();
-      double P[NB];
-#pragma unroll
-      for (int q = 0; q < NB; ++q) P[q] = xch[lane * 17 + q];  // lanes < q: upper garbage, never used
-      wave_sync_lds();
       double yq = 0.0;
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
@@ -1322,22 +1333,50 @@ struct BandSide {
           for (int q2 = q + 2; q2 < NB; ++q2) P[q2] = fma(-P[q], colbuf[q * 64 + q2], P[q2]);
         }
       }
+      CH_PH(ph_c);
       wave_sync_lds();  // colbuf reads done before xch is rewritten
-      {
-        const bool rowvalid = kb + lane < rows;
+      const bool rowvalid = kb + lane < rows;
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-          const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
-          *(ok ? A + l_base + q * sj : dummy) = q == lane ? yq : P[q];
-          xch[lane * 17 + q] = P[q];
-        }
-        l_base += dstep;
-        if (lane < NB) z[kb + lane] = zr;
+      for (int q = 0; q < NB; ++q) {
+        const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
+        *(ok ? A + l_base + q * sj : dummy) = q == lane ? yq : P[q];
+        xch[lane * 17 + q] = P[q];
       }
-      if (pdone && lane == 0) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      wave_sync_lds();
+      l_base += dstep;
+      if (lane < NB) z[kb + lane] = zr;
+      if (lane == 0) {  // the release orders the whole wave's stores above
+        if (pdone) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(lrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      const double zs = __shfl_down(zr, 16, 64);
+      zr = lane < 48 ? zs : zin;
+      CH_PH(ph_s);
+    }
+#ifdef LORB_CHOL_PHASES
+    if (phases && this->lane == 0) { phases[0] += ph_w; phases[1] += ph_c; phases[2] += ph_s; }
+#endif
+#undef CH_PH
+  }
+  //   update(): T = the window at kb0 (column 0 unused); on return the window at kend (all ten
+  //   tiles).  lwant counts the L posts consumed so far.
+  __device__ __forceinline__ void update(v4d (&T)[10], int kb0, int kend, int* lrd, int* prd, int& lwant,
+                                         double* pb) const {
+    const int ci = lane & 15, ck = lane >> 4;
+    const int dstep = 16 * (si + sj);
+    int tn_addr = idx(kb0 + 64 + ck, kb0 + 16 + ci);  // entering tile (J, r) adds 4 r si + 16 J sj (below)
+    unsigned tn_ok = 0;
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 64 + ck + 4 * r, j = 16 + 16 * J + ci;
+        tn_ok |= (unsigned)(j <= i && i - j <= bw) << (4 * J + r);
+      }
+    for (int kb = kb0; kb < kend; kb += 16) {
+      int tok = (int)tn_ok;
+      asm volatile("" : "+v"(tok));
       // the tile row entering at the end of this panel (view rows kb+64 .. kb+79): untouched S,
-      // read here so that a progressively staged band has the panel's factorization to arrive
+      // loaded while the chain wave factors the panel
       if (mask) {
         const int b = dir > 0 ? kb / 16 + 4 : nbk - 5 - kb / 16;
         if (b >= 0 && b < nbk) wait_bit(mask, b);
@@ -1353,22 +1392,35 @@ struct BandSide {
           Tn[J][r] = ok ? v : 0.0;
         }
       tn_addr += dstep;
+      wait_ge<true>(lrd, ++lwant);
       double opA[4][4];
 #pragma unroll
       for (int I = 1; I < 4; ++I)
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) opA[I][kk] = xch[(16 * I + ci) * 17 + 4 * kk + ck];
-      // k-step outer: the six tiles' accumulation chains interleave, so consecutive MFMAs are
-      // independent and the matrix pipe stays full
+      // the next panel's column first, then hand it over
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-        for (int J = 1; J < 4; ++J)
+        for (int I = 1; I < 4; ++I)
+          T[tri4(I, 1)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[1][kk], T[tri4(I, 1)], 0, 0, 0);
+      if (kb + 16 < kend) {
+#pragma unroll
+        for (int I = 1; I < 4; ++I)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pb[(16 * (I - 1) + ck + 4 * r) * 17 + ci] = T[tri4(I, 1)][r];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pb[(48 + ck + 4 * r) * 17 + ci] = Tn[0][r];
+        if (lane == 0) __hip_atomic_fetch_add(prd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      // k-step outer: the three tiles' accumulation chains interleave
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int J = 2; J < 4; ++J)
 #pragma unroll
           for (int I = J; I < 4; ++I)
             T[tri4(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[J][kk], T[tri4(I, J)], 0, 0, 0);
-      const double zs = __shfl_down(zr, 16, 64);
-      zr = lane < 48 ? zs : zin;
       T[tri4(0, 0)] = T[tri4(1, 1)];
       T[tri4(1, 0)] = T[tri4(2, 1)]; T[tri4(1, 1)] = T[tri4(2, 2)];
       T[tri4(2, 0)] = T[tri4(3, 1)]; T[tri4(2, 1)] = T[tri4(3, 2)]; T[tri4(2, 2)] = T[tri4(3, 3)];
@@ -1538,7 +1590,16 @@ __device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, doub
   }
 }
 
-__global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
+constexpr int kChol2sThreads = 512;
+// LDS words of k_ba_chol_2s: band (n16 rows), both sides' rhs (n16 + 48), two 64 x 18 exchanges
+// (together the 48 x 48 combine), zX (48), two 64 x 17 panel hand-off buffers
+__host__ __device__ constexpr int chol2s_words(int n16, int bw) {
+  return n16 * (bw + 1) + (n16 + 48) + 2 * 64 * 18 + 48 + 2 * 64 * 17;
+}
+
+// Waves: 0 / 1 chain (top / bottom side), 2 / 3 their update waves, 4 / 5 the inverses of L's
+// diagonal blocks (for the back-substitution), 6 / 7 the progressive staging of the band.
+__global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_bad;
 #ifdef LORB_CHOL_STAMPS
@@ -1554,10 +1615,8 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
     if (threadIdx.x == 0) d.st[w].chol_fail = 1;
     return;
   }
+  constexpr int NT = kChol2sThreads;
   const int n = W.n, bw = W.bw, B1 = bw + 1;
-#ifdef LORB_STAGE_DIAG
-  if (threadIdx.x == 64) d.dbg[8 * w + 4] = __builtin_amdgcn_s_memtime() - st_entry;
-#endif
   const int n16 = (n + 15) & ~15;
   const int m = 16 * ((n16 - 48) / 32);  // T = [0, m), M = [m, m+48), B = [m+48, n16)
   const int nB = n16 - m - 48;
@@ -1569,12 +1628,15 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   double* xt = zb + rb;       // 64 x 18 per side (rows of 17); both together hold X (48 x 48)
   double* xb = xt + 64 * 18;
   double* zX = xb + 64 * 18;  // 48
+  double* pbt = zX + 48;      // 64 x 17 panel hand-off, top / bottom
+  double* pbb = pbt + 64 * 17;
   // Staging.  The rows each side's first panel reads (view rows 0 .. 79 of both sides) are copied
-  // by all four waves; the rest of the band by waves 2 / 3 while waves 0 / 1 factor, in the order
-  // the panels need it (a block mask in LDS).  Waves 2 / 3 then invert the diagonal 16 x 16 blocks
+  // by all waves; the rest of the band by waves 6 / 7 while the chains run, in the order the
+  // update waves need it (a block mask in LDS).  Waves 4 / 5 invert the diagonal 16 x 16 blocks
   // of L as the panels finish, for the back-substitution.
   __shared__ unsigned long long s_mask;
   __shared__ int s_pdone[2];
+  __shared__ int s_lrd[2], s_prd[2];  // per side: L panels posted (chain), panel columns posted (update)
   const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
   const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
   const int nbk = n16 / 16, ib = 4;
@@ -1584,28 +1646,19 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   const bool prog = LORB_CHOL_PROG && nbk <= 64 && nbk > 2 * ib;
   const int cpb = 8 * B1;  // chunks per 16-row block
   // rhs loads issued before the band copy (one round trip for both)
-  double rz[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int k = t + 256 * u;
-    const int row = k < rt ? k : n16 - 1 - (k - rt);
-    rz[u] = (k < rt + rb && row < n) ? d.rhs[W.row_base + row] : 0.0;
+  double rz;
+  {
+    const int row = t < rt ? t : n16 - 1 - (t - rt);
+    rz = (t < rt + rb && row < n) ? d.rhs[W.row_base + row] : 0.0;
   }
   if (prog) {  // both sides' first ib blocks in one batch
-    stage_band2<13>(S2, Ab, 0, ib * cpb, (nbk - ib) * cpb, nch, t, 256, n, bw, nsrc);
+    stage_band2<7>(S2, Ab, 0, ib * cpb, (nbk - ib) * cpb, nch, t, NT, n, bw, nsrc);
   } else {
-    stage_band<14>(S2, Ab, 0, nch, t, 256, n, bw, nsrc);
+    stage_band<14>(S2, Ab, 0, nch, t, NT, n, bw, nsrc);
   }
-#ifdef LORB_STAGE_DIAG
-  if (threadIdx.x == 64) d.dbg[8 * w + 6] = __builtin_amdgcn_s_memtime() - st_entry;
-#endif
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int k = t + 256 * u;
-    if (k < rt) zt[k] = rz[u];
-    else if (k < rt + rb) zb[k - rt] = rz[u];
-  }
-  for (int k = t + 512; k < rt + rb; k += 256) {  // (n16 > 416 only)
+  if (t < rt) zt[t] = rz;
+  else if (t < rt + rb) zb[t - rt] = rz;
+  for (int k = t + NT; k < rt + rb; k += NT) {  // (n16 > 464 only)
     const int row = k < rt ? k : n16 - 1 - (k - rt);
     const double v = row < n ? d.rhs[W.row_base + row] : 0.0;
     if (k < rt) zt[k] = v; else zb[k - rt] = v;
@@ -1613,6 +1666,7 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   if (t == 0) {
     s_bad = 0;
     s_pdone[0] = 0; s_pdone[1] = 0;
+    s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
     unsigned long long msk = 0;
     for (int b = 0; b < nbk; ++b) msk |= (unsigned long long)(!prog || b < ib || b >= nbk - ib) << (b & 63);
     s_mask = msk;
@@ -1623,43 +1677,55 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   top.pdone = &s_pdone[0]; bot.pdone = &s_pdone[1];
   top.nbk = bot.nbk = nbk; top.dir = 1; bot.dir = -1;
   if (prog) { top.mask = &s_mask; bot.mask = &s_mask; }
-  const BandSide& me = wv == 0 ? top : bot;
-  v4d T[10];
-  double zr = 0.0;
+  const int side = wv & 1;                 // 0 top, 1 bottom (waves 0..5)
+  const BandSide& me = side == 0 ? top : bot;
+  double* pb = side == 0 ? pbt : pbb;
+  int* lrd = &s_lrd[side];
+  int* prd = &s_prd[side];
+  int lwant = 0, pwant = 0;
   bool bad = false;
-#ifdef LORB_CHOL_STAMPS
+  double zr = 0.0;
+  double P[NB];
+  v4d T[10];
+  // LORB_CHOL_STAMPS: dbg[0..5] = waves 0..5 done with the T / B phase, [6] wave 0 done with M,
+  // [7] wave 0 done with the back-substitution (cycles from the end of the initial staging)
+#if defined(LORB_CHOL_STAMPS) && !defined(LORB_CHOL_PHASES)
   const unsigned long long st0 = __builtin_amdgcn_s_memtime();
-  if (lane == 0 && wv == 1) d.dbg[8 * w + 5] = st0 - st_entry;  // staging
-#ifdef LORB_STAGE_DIAG
-#define C2_STAMP(k) do { if (lane == 0 && wv == 0) d.dbg[8 * w + (k)] = __builtin_amdgcn_s_memtime() - st0; } while (0)
-#else
-#define C2_STAMP(k) do { if (lane == 0 && wv < 2) d.dbg[8 * w + (k) + 4 * wv] = __builtin_amdgcn_s_memtime() - st0; } while (0)
-#endif
+#define C2_STAMP(k) do { if (lane == 0) d.dbg[8 * w + (k)] = __builtin_amdgcn_s_memtime() - st0; } while (0)
 #else
 #define C2_STAMP(k) do {} while (0)
 #endif
-  if (wv >= 2) {
-    if (prog) {  // remaining blocks [ib, nbk - ib): wave 2 from the top, wave 3 from the bottom
+  if (wv >= 6) {
+    if (prog) {  // remaining blocks [ib, nbk - ib): wave 6 from the top, wave 7 from the bottom
       const int lo = ib, hi = nbk - ib, mid = (lo + hi) / 2;
-      for (int k = 0; k < (wv == 2 ? mid - lo : hi - mid); ++k) {
-        const int b = wv == 2 ? lo + k : hi - 1 - k;
+      for (int k = 0; k < (wv == 6 ? mid - lo : hi - mid); ++k) {
+        const int b = wv == 6 ? lo + k : hi - 1 - k;
         stage_band<7>(S2, Ab, b * cpb, min((b + 1) * cpb, nch), lane, 64, n, bw, nsrc);
         if (lane == 0) __hip_atomic_fetch_or(&s_mask, 1ull << b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
-    const BandSide& side = wv == 2 ? top : bot;
-    int* pd = &s_pdone[wv - 2];
-    const int nblk = (wv == 2 ? m : nB) / 16;
+  } else if (wv >= 4) {
+    int* pd = &s_pdone[side];
+    const int nblk = (side == 0 ? m : nB) / 16;
     for (int p = 0; p + 1 < nblk; ++p) {  // the last block after the panels' barrier
       while (__hip_atomic_load(pd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= p) __builtin_amdgcn_s_sleep(1);
-      side.linv(16 * p);
+      me.linv(16 * p);
     }
+  } else if (wv < 2) {
+    me.init_panel(P, zr);
+#ifdef LORB_CHOL_PHASES
+    unsigned long long* phv = d.dbg + 8 * w;  // wave 0, T phase: [0] wait [1] factor [2] store
+    if (wv == 0) { if (lane == 0) { phv[0] = phv[1] = phv[2] = 0; } const_cast<BandSide&>(me).phases = phv; }
+#endif
+    me.chain(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, pwant, pb);
+  } else if (wv < 4) {
+    me.init_tiles(T);
+    me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb);
   }
-  if (wv < 2) { me.init(T, zr); me.panels(T, zr, bad, 0, wv == 0 ? m : nB); }
-  C2_STAMP(0);
+  if (wv < 6) C2_STAMP(wv);
   __syncthreads();
   double* X = xt;  // 48 x 48 in the two exchanges (idle now), original M orientation
-  if (wv == 1) {
+  if (wv == 3) {   // the bottom side's window on M, reversed back
 #pragma unroll
     for (int I = 0; I < 3; ++I)
 #pragma unroll
@@ -1669,15 +1735,17 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
           const int rho = 16 * I + (lane >> 4) + 4 * r, kap = 16 * J + (lane & 15);
           if (kap <= rho) X[(47 - kap) * 48 + (47 - rho)] = T[tri4(I, J)][r];
         }
+  }
+  if (wv == 1) {
     if (lane < 48) zX[47 - lane] = zr;
     if (bad) s_bad = 1;
   }
   __syncthreads();
-  if (wv >= 2) {  // last diagonal block of each side, behind the M panels
-    const int nblk = (wv == 2 ? m : nB) / 16;
-    if (nblk > 0) (wv == 2 ? top : bot).linv(16 * (nblk - 1));
+  if (wv == 4 || wv == 5) {  // last diagonal block of each side, behind the M panels
+    const int nblk = (side == 0 ? m : nB) / 16;
+    if (nblk > 0) me.linv(16 * (nblk - 1));
   }
-  if (wv == 0) {
+  if (wv == 2) {
     // S_M = (S_MM - L_MT L_MT^T) + (S_MM - L_MB L_MB^T) - S_MM ; rows >= m+48 leave the window
 #pragma unroll
     for (int I = 0; I < 3; ++I)
@@ -1690,13 +1758,24 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
         }
 #pragma unroll
     for (int J = 0; J < 4; ++J) T[tri4(3, J)] = v4d{0.0, 0.0, 0.0, 0.0};
-    zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
-    C2_STAMP(1);
+    {  // M's first panel column to the chain wave
+      const int ci = lane & 15, ck = lane >> 4;
+#pragma unroll
+      for (int I = 0; I < 4; ++I)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pbt[(16 * I + ck + 4 * r) * 17 + ci] = T[tri4(I, 0)][r];
+      if (lane == 0) __hip_atomic_fetch_add(&s_prd[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     BandSide topM = top;
     topM.mask = nullptr; topM.pdone = nullptr;
-    topM.panels(T, zr, bad, m, m + 48);
+    topM.update(T, m, m + 48, &s_lrd[0], &s_prd[0], lwant, pbt);
+  } else if (wv == 0) {
+    zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
+    BandSide topM = top;
+    topM.mask = nullptr; topM.pdone = nullptr;
+    topM.chain(P, zr, bad, m, m + 48, false, &s_lrd[0], &s_prd[0], pwant, pbt);
     if (bad) s_bad = 1;
-    C2_STAMP(2);
+    C2_STAMP(6);
   }
   __syncthreads();
   if (s_bad) {
@@ -1710,12 +1789,12 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
   __syncthreads();
   if (wv == 0) top.backsub<true>(m - 16, 0);     // y_T
   else if (wv == 1) bot.backsub<true>(nB - 16, 0);  // y_B (reversed)
-  C2_STAMP(3);
+  if (wv == 0) C2_STAMP(7);
   __syncthreads();
 #undef C2_STAMP
-  for (int k = t; k < n; k += 256) d.ycam[W.row_base + k] = k < rt ? zt[k] : zb[n16 - 1 - k];
+  for (int k = t; k < n; k += NT) d.ycam[W.row_base + k] = k < rt ? zt[k] : zb[n16 - 1 - k];
   const int cur = d.st[w].cur;
-  for (int ci2 = t; ci2 < W.n_poses; ci2 += 256) {
+  for (int ci2 = t; ci2 < W.n_poses; ci2 += NT) {
     const int c = W.pose_base + ci2;
     double xn[6];
 #pragma unroll
@@ -1727,11 +1806,6 @@ __global__ __launch_bounds__(256) void k_ba_chol_2s(BaDev d) {
     }
     d.rot_cand[c] = lorb::rot_val(xn);
   }
-#ifdef LORB_CHOL_STAMPS
-#ifndef LORB_STAGE_DIAG
-  if (lane == 0 && wv == 1) d.dbg[8 * w + 6] = __builtin_amdgcn_s_memtime() - st0;  // to the end
-#endif
-#endif
 }
 
 // K7: point-group back-substitution: b_p -= sum_e W_e^T y_c(e) (observation phase + ordered
@@ -2435,8 +2509,9 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
       const int n16 = (n + 15) & ~15;
       // one-sided K6w: band + z + invd + exchange; two-sided K6t: (n16 + 48) band rows, z, invd,
       // two exchanges, zX -- the larger of the two
-      P->max_env_w = std::max(P->max_env_w, std::max(n16 * (bwid + 1) + 2 * n16 + 64 * 18,
-                                                      (n16 + 48) * (bwid + 2) + 2 * 64 * 18 + 48));
+      P->max_env_w = std::max(P->max_env_w, std::max(std::max(n16 * (bwid + 1) + 2 * n16 + 64 * 18,
+                                                                (n16 + 48) * (bwid + 2) + 2 * 64 * 18 + 48),
+                                                       chol2s_words(n16, bwid)));
       if (n16 > 0) P->min_n16 = std::min(P->min_n16, n16);
     }
     env_base += bw.env_size; row_base += n;
@@ -2608,7 +2683,7 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   P->chol_kind = kind;
   if (P->Ctot && chol_2s) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
-    hipLaunchKernelGGL(k_ba_chol_2s, dim3(P->W), dim3(256), sizeof(double) * (size_t)P->max_env_w, s, d);
+    hipLaunchKernelGGL(k_ba_chol_2s, dim3(P->W), dim3(kChol2sThreads), sizeof(double) * (size_t)P->max_env_w, s, d);
   } else if (P->Ctot && chol_w) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
     hipLaunchKernelGGL(k_ba_chol_w, dim3(P->W), dim3(256), sizeof(double) * (size_t)P->max_env_w, s, d);
@@ -3192,7 +3267,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     // fits, so that a narrower band after a rebuild keeps the captured solve
     const int n16 = (n + 15) & ~15;
     auto env_w = [&](int bwv) {
-      return std::max(n16 * (bwv + 1) + 2 * n16 + 64 * 18, (n16 + 48) * (bwv + 2) + 2 * 64 * 18 + 48);
+      return std::max(std::max(n16 * (bwv + 1) + 2 * n16 + 64 * 18, (n16 + 48) * (bwv + 2) + 2 * 64 * 18 + 48),
+                      chol2s_words(n16, bwv));
     };
     P->max_env_w = env_w(bwid);
     if (bwid <= 48 && sizeof(double) * (size_t)env_w(48) <= (size_t)kLdsBudget) P->max_env_w = env_w(48);
