@@ -1257,6 +1257,7 @@ struct BandSide {
   unsigned long long* mask = nullptr;  // progressive staging (null: the whole band is staged)
   int* pdone = nullptr;                // panels whose L is in the band (release-counted, for linv)
   int nbk = 0, dir = 0;                // row blocks; +1 top view, -1 reversed bottom view
+  int zslot = 0;                       // A[zslot] == 0.0 (out-of-band reads of the back-substitution)
   unsigned long long* phases = nullptr;  // LORB_CHOL_PHASES diagnostics: chain wait / factor / store cycles
 
   __device__ __forceinline__ int idx(int i, int j) const { return base + si * i + sj * j; }
@@ -1453,32 +1454,95 @@ struct BandSide {
       }
     }
   }
-  // L^T y = z for the 16-row blocks c0 = c_hi, c_hi-16, ..., c_lo; rows below a block are
-  // gathered up to rows-1.  INV: the blocks' diagonal holds X = L_bb^-1 (linv), so
-  // y_b = X^T (z_b - gathered) is a 16 x 16 product instead of a 16-step chain.
+  // Back-substitution L^T y = z, push style: the 64 rows c0-48 .. c0+15 of the current block c0
+  // live in registers (row r in lane r & 63, so sliding the window needs no shuffle).  A block
+  // solves its 16 x 16 triangle -- as a v_readlane chain (c0 >= c_inv) or as one product with the
+  // inverted diagonal block X from linv (c0 < c_inv) -- writes y to z, pushes y into the rows above
+  // it within the band, and its lanes load the rows that enter the window above.
+  __device__ __forceinline__ int bs_row(int c0) const { return c0 - 48 + ((lane - (c0 - 48)) & 63); }
+  // window of block c_hi; `known` rows c_hi+16 .. c_hi+15+known already hold final y in z and are
+  // pushed into it first
+  __device__ __forceinline__ double bs_init(int c_hi, int known) const {
+    const int row = bs_row(c_hi);
+    double zw = row >= 0 ? z[row] : 0.0;
+    for (int i0 = 0; i0 < known; i0 += 16) {
+      double l[16], y[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int ri = c_hi + 16 + i0 + k;
+        const bool ok = i0 + k < known && row >= 0 && ri - row <= bw;
+        l[k] = A[ok ? idx(ri, row) : base];
+        l[k] = ok ? l[k] : 0.0;
+        y[k] = z[i0 + k < known ? ri : 0];
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) zw = fma(-l[k], y[k], zw);
+    }
+    return zw;
+  }
+  struct BsWin {
+    double zw;         // the window
+    double zin = 0.0;  // rows that entered above (loaded by the last block's lanes), merged late
+    bool pend = false;
+  };
+  // blocks c_from, c_from - 16, ..., c_to; INV: multiply by the inverted diagonal block, else a
+  // v_readlane chain through the triangle.  The rows entering above are merged only before the
+  // next block's pushes, so their loads are off the chain.  Addresses are per-lane linear in the
+  // block index; the lane constants are kept opaque (VGPRs) so the unrolled block does not
+  // hoist dozens of uniform values into SGPRs.
   template <bool INV>
-  __device__ __forceinline__ void backsub(int c_hi, int c_lo) const {
-    const int jc = lane & 15, g = lane >> 4;
-    for (int c0 = c_hi; c0 >= c_lo; c0 -= 16) {
-      const int j = c0 + jc;
-      double lk[NB];
+  __device__ __forceinline__ void bs_run(BsWin& S, int c_from, int c_to) const {
+    for (int c0 = c_from; c0 >= c_to; c0 -= 16) {
+      int row = bs_row(c0);
+      const int j = row - c0, b0 = c0 & 63;
+      const bool blk = j >= 0;
+      // L(c0 + k, row) at aL + si k, valid for 1 <= c0 - row + k <= bw (and row >= 0; INV: not a
+      // block lane); X(c0 + k, c0 + j) at aX + si k, valid for k >= j.  Invalid entries read the
+      // zero word, so a load needs one compare and one address select.
+      int aL = base + si * c0 + sj * row;
+      int aX = base + si * c0 + sj * (c0 + j);
+      int eL = c0 - row - 1 + ((row < 0 || (INV && blk)) ? (1 << 20) : 0);
+      int eX = blk ? -j : (1 << 20);
+      asm volatile("" : "+v"(aL), "+v"(aX), "+v"(eL), "+v"(eX), "+v"(row));
+      double Lp[16], xv[16];
 #pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        const bool ok = k > jc;
-        const double v = A[ok ? idx(c0 + k, j) : base];
-        lk[k] = ok ? v : 0.0;
-      }
-      const int iend = min(rows - 1, j + bw);
-      double av[16], zv[16];
+      for (int k = 0; k < 16; ++k) Lp[k] = A[(unsigned)(eL + k) < (unsigned)bw ? aL + si * k : zslot];
+      double zw = S.zw;
+      if (!INV) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = c0 + 16 + g + 4 * u;
-        const bool ok = i <= iend;
-        av[u] = A[ok ? idx(i, j) : base];
-        zv[u] = z[ok ? i : 0];
-        av[u] = ok ? av[u] : 0.0;
+        for (int k = 0; k < 16; ++k) xv[k] = A[base + si * (c0 + k) + sj * (c0 + k)];  // 1 / L(i, i)
+        zw = S.pend ? S.zin : zw;
+#pragma unroll
+        for (int k = 15; k >= 0; --k) {
+          const double yk = readlane_d(zw, (b0 + k) & 63) * xv[k];
+          zw = (j == k) ? yk : fma(-Lp[k], yk, zw);
+        }
+        if (blk) z[row] = zw;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) xv[k] = A[(unsigned)(eX + k) < 16u ? aX + si * k : zslot];
+        // z_b and then y_b go through z in LDS (broadcast reads)
+        if (blk) z[row] = zw;
+        wave_sync_lds();
+        double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) a4[k & 3] = fma(xv[k], z[c0 + k], a4[k & 3]);
+        const double y = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        wave_sync_lds();
+        if (blk) z[row] = y;
+        wave_sync_lds();
+        zw = S.pend ? S.zin : zw;
+        double p4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) p4[k & 3] = fma(Lp[k], z[c0 + k], p4[k & 3]);
+        zw = blk ? y : zw - ((p4[0] + p4[1]) + (p4[2] + p4[3]));
       }
-      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+      if (blk) S.zin = row - 64 >= 0 ? z[row - 64] : 0.0;  // the row entering above
+      S.pend = blk;
+      S.zw = zw;
+    }
+  }
+};
 #pragma unroll
       for (int u = 0; u < 16; ++u) a4[u & 3] = fma(av[u], zv[u], a4[u & 3]);
       double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
@@ -1592,9 +1656,9 @@ __device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, doub
 
 constexpr int kChol2sThreads = 512;
 // LDS words of k_ba_chol_2s: band (n16 rows), both sides' rhs (n16 + 48), two 64 x 18 exchanges
-// (together the 48 x 48 combine), zX (48), two 64 x 17 panel hand-off buffers
+// (together the 48 x 48 combine), zX (48), two 64 x 17 panel hand-off buffers, a zero word
 __host__ __device__ constexpr int chol2s_words(int n16, int bw) {
-  return n16 * (bw + 1) + (n16 + 48) + 2 * 64 * 18 + 48 + 2 * 64 * 17;
+  return n16 * (bw + 1) + (n16 + 48) + 2 * 64 * 18 + 48 + 2 * 64 * 17 + 2;
 }
 
 // Waves: 0 / 1 chain (top / bottom side), 2 / 3 their update waves, 4 / 5 the inverses of L's
@@ -1630,6 +1694,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   double* zX = xb + 64 * 18;  // 48
   double* pbt = zX + 48;      // 64 x 17 panel hand-off, top / bottom
   double* pbb = pbt + 64 * 17;
+  double* zero = pbb + 64 * 17;  // one 0.0
   // Staging.  The rows each side's first panel reads (view rows 0 .. 79 of both sides) are copied
   // by all waves; the rest of the band by waves 6 / 7 while the chains run, in the order the
   // update waves need it (a block mask in LDS).  Waves 4 / 5 invert the diagonal 16 x 16 blocks
@@ -1637,6 +1702,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   __shared__ unsigned long long s_mask;
   __shared__ int s_pdone[2];
   __shared__ int s_lrd[2], s_prd[2];  // per side: L panels posted (chain), panel columns posted (update)
+  __shared__ int s_hand[3];           // T / B -> M hand-over (below)
   const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
   const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
   const int nbk = n16 / 16, ib = 4;
@@ -1664,9 +1730,11 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     if (k < rt) zt[k] = v; else zb[k - rt] = v;
   }
   if (t == 0) {
+    *zero = 0.0;
     s_bad = 0;
     s_pdone[0] = 0; s_pdone[1] = 0;
     s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
+    s_hand[0] = 0; s_hand[1] = 0; s_hand[2] = 0;
     unsigned long long msk = 0;
     for (int b = 0; b < nbk; ++b) msk |= (unsigned long long)(!prog || b < ib || b >= nbk - ib) << (b & 63);
     s_mask = msk;
@@ -1675,6 +1743,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   BandSide top{Ab, zt, xt, rt, bw, lane, bw, bw, 1};
   BandSide bot{Ab, zb, xb, rb, bw, lane, (n16 - 1) * B1 + bw, -1, -bw};
   top.pdone = &s_pdone[0]; bot.pdone = &s_pdone[1];
+  top.zslot = (int)(zero - Ab); bot.zslot = top.zslot;
   top.nbk = bot.nbk = nbk; top.dir = 1; bot.dir = -1;
   if (prog) { top.mask = &s_mask; bot.mask = &s_mask; }
   const int side = wv & 1;                 // 0 top, 1 bottom (waves 0..5)
@@ -1707,7 +1776,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   } else if (wv >= 4) {
     int* pd = &s_pdone[side];
     const int nblk = (side == 0 ? m : nB) / 16;
-    for (int p = 0; p + 1 < nblk; ++p) {  // the last block after the panels' barrier
+    for (int p = 0; p < nblk; ++p) {
       while (__hip_atomic_load(pd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= p) __builtin_amdgcn_s_sleep(1);
       me.linv(16 * p);
     }
@@ -1723,9 +1792,12 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb);
   }
   if (wv < 6) C2_STAMP(wv);
-  __syncthreads();
+  // Hand-over to the M phase by flags, not barriers (the diagonal-block inverses of waves 4 / 5
+  // may still be running): wave 2 posts that it has read its last L from xt, wave 3 then writes
+  // the bottom side's window on M into X = xt (+ xb) and posts it, wave 1 posts zX.
   double* X = xt;  // 48 x 48 in the two exchanges (idle now), original M orientation
   if (wv == 3) {   // the bottom side's window on M, reversed back
+    wait_ge<true>(&s_hand[0], 1);
 #pragma unroll
     for (int I = 0; I < 3; ++I)
 #pragma unroll
@@ -1735,16 +1807,18 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
           const int rho = 16 * I + (lane >> 4) + 4 * r, kap = 16 * J + (lane & 15);
           if (kap <= rho) X[(47 - kap) * 48 + (47 - rho)] = T[tri4(I, J)][r];
         }
+    if (lane == 0) __hip_atomic_fetch_add(&s_hand[1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   if (wv == 1) {
     if (lane < 48) zX[47 - lane] = zr;
     if (bad) s_bad = 1;
+    if (lane == 0) __hip_atomic_fetch_add(&s_hand[2], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  __syncthreads();
-  if (wv == 4 || wv == 5) {  // last diagonal block of each side, behind the M panels
-    const int nblk = (side == 0 ? m : nB) / 16;
-    if (nblk > 0) me.linv(16 * (nblk - 1));
+  if (wv == 2) {
+    if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    wait_ge<true>(&s_hand[1], 1);
   }
+  if (wv == 0) wait_ge<true>(&s_hand[2], 1);
   if (wv == 2) {
     // S_M = (S_MM - L_MT L_MT^T) + (S_MM - L_MB L_MB^T) - S_MM ; rows >= m+48 leave the window
 #pragma unroll
@@ -1782,13 +1856,28 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     if (t == 0) d.st[w].chol_fail = 1;
     return;
   }
+#ifdef LORB_CHOL_PHASES
+#define BS_PH(k) do { if (lane == 0) d.dbg[8 * w + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define BS_PH(k) do {} while (0)
+#endif
   if (wv == 0) {
-    top.backsub<false>(m + 32, m);               // y_M
+    BS_PH(3);
+    BandSide::BsWin S{top.bs_init(m + 32, 0)};
+    top.bs_run<false>(S, m + 32, m);                   // y_M (chained triangles)
+    BS_PH(4);
     if (lane < 48) zb[nB + 47 - lane] = zt[m + lane];  // into the reversed bottom rows
+    if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    top.bs_run<true>(S, m - 16, 0);                   // y_T (inverted diagonal blocks)
+    BS_PH(5);
+  } else if (wv == 1) {
+    wait_ge<false>(&s_hand[0], 2);
+    BS_PH(6);
+    BandSide::BsWin S{bot.bs_init(nB - 16, 48)};
+    bot.bs_run<true>(S, nB - 16, 0);                // y_B (reversed)
+    BS_PH(7);
   }
-  __syncthreads();
-  if (wv == 0) top.backsub<true>(m - 16, 0);     // y_T
-  else if (wv == 1) bot.backsub<true>(nB - 16, 0);  // y_B (reversed)
+#undef BS_PH
   if (wv == 0) C2_STAMP(7);
   __syncthreads();
 #undef C2_STAMP
