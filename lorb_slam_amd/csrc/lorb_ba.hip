@@ -1543,47 +1543,6 @@ struct BandSide {
     }
   }
 };
-#pragma unroll
-      for (int u = 0; u < 16; ++u) a4[u & 3] = fma(av[u], zv[u], a4[u & 3]);
-      double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-      {  // butterfly xor 16, xor 32 (permlane swaps, no LDS)
-        double a, b;
-        xrow_pair<false>(acc, a, b); acc = a + b;
-        xrow_pair<true>(acc, a, b); acc = a + b;
-      }
-      double zb = z[j] - acc;
-      if (INV) {
-        double xv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {  // X(c0 + k, j), k = g + 4u >= jc
-          const int k = g + 4 * u;
-          const bool ok = k >= jc && k - jc <= bw;
-          const double v = A[ok ? idx(c0 + k, j) : base];
-          xv[u] = ok ? v : 0.0;
-        }
-        if (g == 0) z[j] = zb;
-        wave_sync_lds();
-        double part = 0.0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) part = fma(xv[u], z[c0 + g + 4 * u], part);
-        double a, b;
-        xrow_pair<false>(part, a, b); part = a + b;
-        xrow_pair<true>(part, a, b); part = a + b;
-        wave_sync_lds();
-        if (g == 0) z[j] = part;
-      } else {
-        const double iv = A[idx(j, j)];  // 1 / L(j, j)
-#pragma unroll
-        for (int k = NB - 1; k >= 0; --k) {
-          const double yk = readlane_d(zb, k) * readlane_d(iv, k);
-          zb = jc == k ? yk : fma(-lk[k], yk, zb);
-        }
-        if (g == 0) z[j] = zb;
-      }
-      wave_sync_lds();
-    }
-  }
-};
 
 // Flat copy of band chunks [j0, j1) (16-byte chunks of the row-major n x (bw + 1) band) by nthr
 // threads, U chunks per thread per batch with all loads of a batch issued before any store.
