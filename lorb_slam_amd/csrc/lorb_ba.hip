@@ -1880,6 +1880,9 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
   if (S.done || S.chol_fail) return;
   const BaWin& W = d.win[g.win];
   const int cur = S.cur;
+  // Jcs y of this thread's first-chunk observation, kept for the model cost change below (the
+  // camera part of J step is -Jcs y): Jc is read once
+  double ya0 = 0.0, ya1 = 0.0;
   for (int c0 = 0; c0 < g.no; c0 += kGB) {
     if (c0 + t < g.no) {
       const int e = g.o0 + c0 + t;
@@ -1895,6 +1898,7 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
           a0 += d.obs_Jc[12 * m + i] * ys;
           a1 += d.obs_Jc[12 * m + 6 + i] * ys;
         }
+        if (c0 == 0) { ya0 = a0; ya1 = a1; }
 #pragma unroll
         for (int j = 0; j < 3; ++j) sh[t][j] = d.obs_Jps[6 * m + j] * a0 + d.obs_Jps[6 * m + 3 + j] * a1;
       } else {
@@ -1948,13 +1952,21 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
     const double2 uv = d.obs_uv[e];
     double rn[2];
     if (c >= 0) {
-      const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
-      const int m = d.obs_cm[e];
+      if (c0 == t) {
+        m0 -= ya0;
+        m1 -= ya1;
+      } else {  // observations beyond the first chunk (points with > kGB observations)
+        const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
+        const int m = d.obs_cm[e];
+        double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const double s = -y[k] * d.scale_pose[6 * c + k];
-        m0 += d.obs_Jc[12 * m + k] * s;
-        m1 += d.obs_Jc[12 * m + 6 + k] * s;
+        for (int k = 0; k < 6; ++k) {
+          const double ys = y[k] * d.scale_pose[6 * c + k];
+          a0 += d.obs_Jc[12 * m + k] * ys;
+          a1 += d.obs_Jc[12 * m + 6 + k] * ys;
+        }
+        m0 -= a0;
+        m1 -= a1;
       }
       // candidate camera (end of k_ba_chol): x_pose[cur ^ 1] with its rotation state
       residual_s(d.rot_cand[c], d.x_pose[cur ^ 1] + 6 * c + 3, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
@@ -2893,13 +2905,15 @@ __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, in
   }
 }
 
-// One workgroup: out[0 .. n) = exclusive prefix sums of in[0 .. n).  hdr (optional): hdr[0] =
-// total, hdr[1] = max(in).
+// One workgroup: out[0 .. n) = exclusive prefix sums of in[0 .. n) (n_dev: n = *n_dev + 1, the
+// live points and one past them).  hdr (optional): hdr[0] = total, hdr[1] = max(in).
 __global__ __launch_bounds__(1024) void k_db_scan1(const int* __restrict__ in, int* __restrict__ out, int n,
-                                                   int* __restrict__ hdr) {
+                                                   const int* __restrict__ n_dev, int* __restrict__ hdr) {
   __shared__ int wsum[16];
-  int mx;
-  const int tot = lorb::wg_excl_scan(in, out, n, wsum, &mx);
+  __shared__ int s_tile[lorb::kScanTileLds];
+  if (n_dev) n = min(n, *n_dev + 1);
+  int mx = 0;
+  const int tot = lorb::wg_excl_scan(in, out, n, s_tile, wsum, &mx);
   if (hdr) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
@@ -3241,7 +3255,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   const int nb_obs = lorb::ceil_div(std::max(Kc, 1), 256), nb_pt = lorb::ceil_div(std::max(b.P_cap, 1), 256);
   hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);
   hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1,
-                     b.hdr);
+                     w->d_n_points, b.hdr);
   if (Kc > 0) {
     hipLaunchKernelGGL(k_db_scatter, dim3(nb_obs), dim3(256), 0, s, *w, C, F, d.pt_obs_off, b.pt_cnt, b.val_out);
     hipLaunchKernelGGL(k_db_segsort, dim3(nb_pt), dim3(256), 0, s, *w, d.pt_obs_off, b.val_out, b.key_out);
@@ -3359,7 +3373,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     }
     hipLaunchKernelGGL(k_db_gather, dim3(NB), dim3(256), sizeof(int) * C, s, *w, d, K, C, NB, b.key_out, b.val_out,
                        b.perm, b.hist);
-    hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.hist, b.hoff, NB * C, nullptr);
+    hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.hist, b.hoff, NB * C, nullptr, nullptr);
     hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), 0, s, d, K, NB, b.hoff, b.cam_pt);
   }
   if (G > 0) {

@@ -152,33 +152,68 @@ __device__ __forceinline__ int block_excl_scan(int v, int* wsum, int* total) {
   return pre + incl - v;
 }
 
-// Exclusive prefix sums of in[0 .. n) into out[0 .. n) by ONE 1024-thread workgroup: tiles of
-// 1024 x 8 consecutive values with a running carry (a small array needs one launch, not the two or
-// three of a device-wide scan).  Returns the total; *mx (optional) gets this thread's max of in.
-__device__ __forceinline__ int wg_excl_scan(const int* __restrict__ in, int* __restrict__ out, int n, int* wsum,
-                                            int* mx = nullptr) {
+// Exclusive prefix sums of one tile in[0 .. n), n <= kScanTile, into out by ONE 1024-thread
+// workgroup, plus `carry`: coalesced 16-byte loads into LDS (one pad word per 16 so that each
+// thread's 16 consecutive values are conflict-free), a 16-value serial scan per thread, the
+// workgroup scan of the thread sums, coalesced stores.  s_tile: __shared__ int[kScanTileLds].
+// Returns the tile sum; *mx (optional) gets this thread's max of its values.
+constexpr int kScanTile = 16384, kScanTileLds = kScanTile + kScanTile / 16;
+__device__ __forceinline__ int wg_scan_tile(const int* __restrict__ in, int* __restrict__ out, int n, int carry,
+                                            int* s_tile, int* wsum, int* mx = nullptr) {
   const int t = threadIdx.x;
-  int carry = 0, m = 0;
-  for (int base = 0; base < n; base += 8192) {
-    int v[8], loc = 0;
+  auto pad = [](int i) { return i + (i >> 4); };
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = base + 8 * t + u;
-      v[u] = i < n ? in[i] : 0;
-      m = max(m, v[u]);
-      loc += v[u];
+  for (int u = 0; u < 4; ++u) {
+    const int i = 4 * (t + 1024 * u);
+    int4 v = make_int4(0, 0, 0, 0);
+    if (i + 3 < n && ((reinterpret_cast<size_t>(in) & 15) == 0)) {
+      v = *reinterpret_cast<const int4*>(in + i);
+    } else {
+      v.x = i < n ? in[i] : 0; v.y = i + 1 < n ? in[i + 1] : 0;
+      v.z = i + 2 < n ? in[i + 2] : 0; v.w = i + 3 < n ? in[i + 3] : 0;
     }
-    int tot;
-    int run = carry + block_excl_scan_1024(loc, wsum, &tot);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = base + 8 * t + u;
-      if (i < n) out[i] = run;
-      run += v[u];
-    }
-    carry += tot;
+    s_tile[pad(i)] = v.x; s_tile[pad(i + 1)] = v.y; s_tile[pad(i + 2)] = v.z; s_tile[pad(i + 3)] = v.w;
   }
-  if (mx) *mx = m;
+  __syncthreads();
+  int v[16], loc = 0, m = 0;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    v[u] = s_tile[17 * t + u];
+    m = max(m, v[u]);
+    loc += v[u];
+  }
+  int tot;
+  int run = carry + block_excl_scan_1024(loc, wsum, &tot);
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    s_tile[17 * t + u] = run;
+    run += v[u];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = 4 * (t + 1024 * u);
+    const int4 r = make_int4(s_tile[pad(i)], s_tile[pad(i + 1)], s_tile[pad(i + 2)], s_tile[pad(i + 3)]);
+    if (i + 3 < n && ((reinterpret_cast<size_t>(out) & 15) == 0)) {
+      *reinterpret_cast<int4*>(out + i) = r;
+    } else {
+      if (i < n) out[i] = r.x;
+      if (i + 1 < n) out[i + 1] = r.y;
+      if (i + 2 < n) out[i + 2] = r.z;
+      if (i + 3 < n) out[i + 3] = r.w;
+    }
+  }
+  __syncthreads();  // s_tile is reused by the next tile
+  if (mx) *mx = max(*mx, m);
+  return tot;
+}
+
+// The same over any n, tile after tile (one workgroup).  Returns the total.
+__device__ __forceinline__ int wg_excl_scan(const int* __restrict__ in, int* __restrict__ out, int n, int* s_tile,
+                                            int* wsum, int* mx = nullptr) {
+  int carry = 0;
+  for (int base = 0; base < n; base += kScanTile)
+    carry += wg_scan_tile(in + base, out + base, min(n - base, kScanTile), carry, s_tile, wsum, mx);
   return carry;
 }
 

@@ -35,7 +35,8 @@ struct MapDev {
   float* pos2; uint8_t* desc2; int* obs_pt2; int* obs_kf2; float* obs_uv2;   // compaction targets
   int* obs_frame;                                                            // BA slot of each observation
   int* cnt;      // [0] points, [1] observations, [2] error flags, [3] new points, [4] new observations, [5] matches
-  int* flag_pt; int* newid; int* flag_obs; int* newpos;
+  int* flag_pt; int* newid; int* flag_obs; int* newpos;  // newid / newpos: scans within kScanTile tiles
+  int* tile_tot;  // tile sums of the two scans: [0, ntP) points, then observations
   float* ring;   // R x 6 keyframe poses, slot = kf mod R
   float* pose_init; float* fixed; float* pose_out;
   int P_cap, K_cap, W, F, R;
@@ -128,11 +129,25 @@ __global__ __launch_bounds__(256) void k_map_obs_flag(MapDev m, int Kb, int t0) 
   m.flag_obs[k] = f;
 }
 
+// the flag scans are tile-local (one workgroup per tile, all tiles of both arrays in one launch);
+// a consumer adds the sums of the tiles before its own (few: kScanTile = 16 k entries each)
+__device__ __forceinline__ int tile_base(const int* tot, int tile) {
+  int s = 0;
+  for (int k = 0; k < tile; ++k) s += tot[k];
+  return s;
+}
+__device__ __forceinline__ int new_id(const MapDev& m, int i) {
+  return m.newid[i] + tile_base(m.tile_tot, i / lorb::kScanTile);
+}
+__device__ __forceinline__ int new_pos(const MapDev& m, int ntP, int i) {
+  return m.newpos[i] + tile_base(m.tile_tot + ntP, i / lorb::kScanTile);
+}
+
 // stable gathers into the alternate buffers; observation slots as lorb_ba_window_dev wants them
-__global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, int t0) {
+__global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, int t0, int ntP) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < Pb && m.flag_pt[i]) {
-    const int d = m.newid[i];
+    const int d = new_id(m, i);
     m.pos2[3 * d + 0] = m.pos[3 * i + 0];
     m.pos2[3 * d + 1] = m.pos[3 * i + 1];
     m.pos2[3 * d + 2] = m.pos[3 * i + 2];
@@ -141,8 +156,8 @@ __global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, i
     o[0] = s[0]; o[1] = s[1];
   }
   if (i < Kb && m.flag_obs[i]) {
-    const int d = m.newpos[i], kf = m.obs_kf[i];
-    m.obs_pt2[d] = m.newid[m.obs_pt[i]];
+    const int d = new_pos(m, ntP, i), kf = m.obs_kf[i];
+    m.obs_pt2[d] = new_id(m, m.obs_pt[i]);
     m.obs_kf2[d] = kf;
     m.obs_uv2[2 * d + 0] = m.obs_uv[2 * i + 0];
     m.obs_uv2[2 * d + 1] = m.obs_uv[2 * i + 1];
@@ -150,17 +165,24 @@ __global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, i
   }
 }
 
-// the two compaction scans in one launch: workgroup 0 the point flags, workgroup 1 the observation flags
-__global__ __launch_bounds__(1024) void k_map_scans(MapDev m, int Pb, int Kb) {
+// the two compaction scans, tile-local: workgroups [0, ntP) the point flags, the rest the
+// observation flags
+__global__ __launch_bounds__(1024) void k_map_scans(MapDev m, int Pb, int Kb, int ntP) {
   __shared__ int wsum[16];
-  if (blockIdx.x == 0) lorb::wg_excl_scan(m.flag_pt, m.newid, Pb + 1, wsum);
-  else lorb::wg_excl_scan(m.flag_obs, m.newpos, Kb + 1, wsum);
+  __shared__ int s_tile[lorb::kScanTileLds];
+  const bool pt = (int)blockIdx.x < ntP;
+  const int tile = pt ? blockIdx.x : blockIdx.x - ntP;
+  const int n = pt ? Pb + 1 : Kb + 1, base = tile * lorb::kScanTile;
+  const int* in = pt ? m.flag_pt : m.flag_obs;
+  int* out = pt ? m.newid : m.newpos;
+  const int tot = lorb::wg_scan_tile(in + base, out + base, min(n - base, lorb::kScanTile), 0, s_tile, wsum);
+  if (threadIdx.x == 0) m.tile_tot[blockIdx.x] = tot;
 }
 
 // new counts; the window's initial poses and the fixed poses from the ring
-__global__ __launch_bounds__(256) void k_map_window(MapDev m, int Pb, int Kb, int t0) {
+__global__ __launch_bounds__(256) void k_map_window(MapDev m, int Pb, int Kb, int t0, int ntP) {
   const int i = threadIdx.x;
-  if (i == 0) { m.cnt[0] = m.newid[Pb]; m.cnt[1] = m.newpos[Kb]; }
+  if (i == 0) { m.cnt[0] = new_id(m, Pb); m.cnt[1] = new_pos(m, ntP, Kb); }
   for (int j = i; j < 6 * m.W; j += 256) m.pose_init[j] = m.ring[6 * ring_slot(t0 + j / 6, m.R) + j % 6];
   for (int j = i; j < 6 * m.F; j += 256) m.fixed[j] = m.ring[6 * ring_slot(t0 - 1 - j / 6, m.R) + j % 6];
 }
@@ -223,6 +245,7 @@ int map_alloc(lorb_map* M, const lorb_map_init* in) {
   LORB_TRY(malloc_n(M, (size_t)8, &m.cnt));
   LORB_TRY(malloc_n(M, P + 1, &m.flag_pt)); LORB_TRY(malloc_n(M, P + 1, &m.newid));
   LORB_TRY(malloc_n(M, K + 1, &m.flag_obs)); LORB_TRY(malloc_n(M, K + 1, &m.newpos));
+  LORB_TRY(malloc_n(M, (P + 1 + K + 1) / lorb::kScanTile + 2, &m.tile_tot));
   LORB_TRY(malloc_n(M, 6 * (size_t)m.R, &m.ring));
   LORB_TRY(malloc_n(M, 6 * (size_t)m.W, &m.pose_init)); LORB_TRY(malloc_n(M, 6 * (size_t)m.W, &m.pose_out));
   LORB_TRY(malloc_n(M, 6 * (size_t)std::max(m.F, 1), &m.fixed));
@@ -254,10 +277,11 @@ int map_slide(lorb_map* M, int t0, int Pb, int Kb) {
   LORB_HIP(ctx, hipMemsetAsync(m.flag_pt, 0, sizeof(int) * ((size_t)Pb + 1), s));
   if (Kb > 0) hipLaunchKernelGGL(k_map_mark, dim3(lorb::ceil_div(Kb, 256)), dim3(256), 0, s, m, Kb, t0);
   hipLaunchKernelGGL(k_map_obs_flag, dim3(lorb::ceil_div(Kb + 1, 256)), dim3(256), 0, s, m, Kb, t0);
-  hipLaunchKernelGGL(k_map_scans, dim3(2), dim3(1024), 0, s, m, Pb, Kb);
+  const int ntP = lorb::ceil_div(Pb + 1, lorb::kScanTile), ntK = lorb::ceil_div(Kb + 1, lorb::kScanTile);
+  hipLaunchKernelGGL(k_map_scans, dim3(ntP + ntK), dim3(1024), 0, s, m, Pb, Kb, ntP);
   const int nmax = std::max(Pb, Kb);
-  if (nmax > 0) hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, t0);
-  hipLaunchKernelGGL(k_map_window, dim3(1), dim3(256), 0, s, m, Pb, Kb, t0);
+  if (nmax > 0) hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, t0, ntP);
+  hipLaunchKernelGGL(k_map_window, dim3(1), dim3(256), 0, s, m, Pb, Kb, t0, ntP);
   LORB_CHECK_LAUNCH(ctx);
   std::swap(m.pos, m.pos2); std::swap(m.desc, m.desc2); std::swap(m.obs_pt, m.obs_pt2);
   std::swap(m.obs_kf, m.obs_kf2); std::swap(m.obs_uv, m.obs_uv2);
