@@ -9,6 +9,7 @@
 The host layer calls the C-ABI; here it is linked against tests/cpp/abi_loopback.c, a test double
 that forwards to the oracle (no GPU in this container; GPU sanitizers are unavailable on the pool).
 """
+import fcntl
 import os
 import subprocess
 
@@ -17,7 +18,12 @@ CPP = os.path.join(ROOT, "tests", "cpp")
 
 
 def _build():
-    subprocess.run(["make", "-s", "-j8", "-C", CPP, "sanitize"], check=True, capture_output=True, timeout=600)
+    # one make at a time: under pytest-xdist the three tests would otherwise build the same
+    # targets concurrently and read half-written binaries
+    os.makedirs(os.path.join(CPP, "_build"), exist_ok=True)
+    with open(os.path.join(CPP, "_build", ".sanitize.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-j8", "-C", CPP, "sanitize"], check=True, capture_output=True, timeout=600)
 
 
 def _run(binary, **env):
