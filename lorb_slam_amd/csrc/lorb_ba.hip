@@ -226,6 +226,7 @@ __global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n
     s.done = d.win[i].n_obs_all == 0 ? 1 : 0;
     s.relin = 1; s.cur = 0; s.last_successful = 1; s.term = 0; s.chol_fail = 0; s.pad = 0;
     d.st[i] = s;
+    if (d.sharded) d.wfail_part[i] = 0.0;  // point-block failures (set by k_ba_lin, cleared by k_ba_lm_end)
   }
   if (i < ctot) {
     double x[6];
@@ -264,11 +265,58 @@ __device__ __forceinline__ void block_red3(double& a, double& b, double& c, doub
   for (int k = 1; k < kGW; ++k) { a += red[0][k]; b = M1 ? fmax(b, red[1][k]) : b + red[1][k]; c += red[2][k]; }
 }
 
+// Point-block prep shared by k_ba_lin (iterations that relinearise) and k_ba_point_prep (the
+// iterations after a rejected step, where only the radius changed): the point's scaled
+// E^T E + D^2 inverted, and per optimised observation Jps (scaled Jp), Q = Jps E^-1, g = Q b.
+// Returns false when the 3x3 block is not invertible (Ei = 0).
+__device__ __forceinline__ bool prep_point(const double (&Eu)[6], const double (&bu)[3], const double (&sp)[3],
+                                           double rad, const LMOpt& o, double (&Ei)[6], double (&b)[3]) {
+  double E[6];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) b[k] = bu[k] * sp[k];
+  E[0] = Eu[0] * sp[0] * sp[0]; E[1] = Eu[1] * sp[0] * sp[1]; E[2] = Eu[2] * sp[0] * sp[2];
+  E[3] = Eu[3] * sp[1] * sp[1]; E[4] = Eu[4] * sp[1] * sp[2]; E[5] = Eu[5] * sp[2] * sp[2];
+  E[0] += fmin(fmax(E[0], o.min_diag), o.max_diag) / rad;
+  E[3] += fmin(fmax(E[3], o.min_diag), o.max_diag) / rad;
+  E[5] += fmin(fmax(E[5], o.min_diag), o.max_diag) / rad;
+  if (!inv3(E, Ei)) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Ei[k] = 0.0;
+    return false;
+  }
+  return true;
+}
+__device__ __forceinline__ void prep_fail(const BaDev& d, int win) {
+  // benign race: every writer stores the same value; sharded plans reduce the flag (K5).  The
+  // flag is cleared by k_ba_lm_end (and k_ba_init), not by k_ba_lm_begin: k_ba_lin sets it
+  // before k_ba_lm_begin runs.
+  if (d.sharded) d.wfail_part[win] = 1.0;
+  else d.st[win].chol_fail = 1;
+}
+__device__ __forceinline__ void prep_obs(const BaDev& d, int m, const double (&Jp)[6], const double* Ei,
+                                         const double* b, const double* sp) {
+  double Jps[6], Q[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) Jps[k] = Jp[k] * sp[k % 3];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      Q[3 * r + j] = Jps[3 * r] * s3(Ei, 0, j) + Jps[3 * r + 1] * s3(Ei, 1, j) + Jps[3 * r + 2] * s3(Ei, 2, j);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { d.obs_Jps[6 * m + k] = Jps[k]; d.obs_Q[6 * m + k] = Q[k]; }
+  d.obs_g[2 * m] = Q[0] * b[0] + Q[1] * b[1] + Q[2] * b[2];
+  d.obs_g[2 * m + 1] = Q[3] * b[0] + Q[4] * b[1] + Q[5] * b[2];
+}
+
 // K1: linearisation of a point group (windows that (re)linearise this iteration): per
 // observation residual + Jacobians, per point E^T E / E^T r (unscaled), Jacobi scale
-// (iteration 0), gradient-max / point-norm / cost partials.
-__global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
-  __shared__ double sh[kGB][9];
+// (iteration 0), gradient-max / point-norm / cost partials, and the point-block prep of this
+// iteration (prep_point / prep_obs at the current radius: the radius only changes in
+// k_ba_lm_end), so the observations' Jp and the point's E, b never make an HBM round trip.
+__global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d, LMOpt o) {
+  __shared__ double sh[kGB][9];   // observation terms; then the points' Ei (6) and b (3)
+  __shared__ double ssp[kGB][3];
   __shared__ double red3[3][4];
   if ((int)blockIdx.x >= d.live[0]) return;
   const PBlk g = d.pblk[blockIdx.x];
@@ -282,13 +330,17 @@ __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
   if (S.done || !S.relin) return;
   const BaWin& W = d.win[g.win];
   const int cur = S.cur;
+  const double rad = S.radius;
   double cost = 0.0;
   double E[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+  double Jp_f[6] = {0, 0, 0, 0, 0, 0};  // the first chunk's Jp (this thread's observation)
+  int m_f = -1;
   for (int c0 = 0; c0 < g.no; c0 += kGB) {
     if (c0 + t < g.no) {
       const int o = g.o0 + c0 + t;
       const int p = c0 == 0 ? p_f : d.obs_pt[o];
       const int c = c0 == 0 ? c_f : d.obs_cam[o];
+      if (c0 == 0) m_f = d.obs_cm[o];
       double X[3], pose[6];
 #pragma unroll
       for (int k = 0; k < 3; ++k) X[k] = d.x_pt[cur][3 * p + k];
@@ -306,8 +358,12 @@ __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
       d.obs_r[2 * o] = r[0]; d.obs_r[2 * o + 1] = r[1];
 #pragma unroll
       for (int k = 0; k < 6; ++k) d.obs_Jp[6 * o + k] = Jp[k];
+      if (c0 == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) Jp_f[k] = Jp[k];
+      }
       if (c >= 0) {
-        const int m = d.obs_cm[o];
+        const int m = c0 == 0 ? m_f : d.obs_cm[o];
 #pragma unroll
         for (int k = 0; k < 12; ++k) d.obs_Jc[12 * m + k] = Jc[k];
         d.cam_r[2 * m] = r[0]; d.cam_r[2 * m + 1] = r[1];
@@ -339,10 +395,16 @@ __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
     for (int k = 0; k < 6; ++k) d.ete[6 * p + k] = E[k];
 #pragma unroll
     for (int k = 0; k < 3; ++k) d.etb[3 * p + k] = b[k];
+    double sp[3];
     if (S.iter == 0) {
-      d.scale_pt[3 * p] = 1.0 / (1.0 + sqrt(E[0]));
-      d.scale_pt[3 * p + 1] = 1.0 / (1.0 + sqrt(E[3]));
-      d.scale_pt[3 * p + 2] = 1.0 / (1.0 + sqrt(E[5]));
+      sp[0] = 1.0 / (1.0 + sqrt(E[0]));
+      sp[1] = 1.0 / (1.0 + sqrt(E[3]));
+      sp[2] = 1.0 / (1.0 + sqrt(E[5]));
+#pragma unroll
+      for (int k = 0; k < 3; ++k) d.scale_pt[3 * p + k] = sp[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) sp[k] = d.scale_pt[3 * p + k];
     }
     if (po1 > po0) {
 #pragma unroll
@@ -352,6 +414,26 @@ __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d) {
         xn2 += X * X;
       }
     }
+    // point-block prep (point phase)
+    double Ei[6], bs[3];
+    if (!prep_point(E, b, sp, rad, o, Ei, bs)) prep_fail(d, g.win);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { d.pinv[6 * p + k] = Ei[k]; sh[t][k] = Ei[k]; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sh[t][6 + k] = bs[k]; ssp[t][k] = sp[k]; }
+  }
+  __syncthreads();
+  // point-block prep (observation phase): the first chunk's Jp from registers
+  for (int c0 = t; c0 < g.no; c0 += kGB) {
+    const int e = g.o0 + c0;
+    const bool first = c0 == t;
+    const int m = first ? m_f : d.obs_cm[e];
+    if (m < 0) continue;
+    const int lp = (first ? p_f : d.obs_pt[e]) - g.p0;
+    double Jp[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Jp[k] = first ? Jp_f[k] : d.obs_Jp[6 * e + k];
+    prep_obs(d, m, Jp, sh[lp], sh[lp] + 6, ssp[lp]);
   }
   block_red3<true>(cost, gm, xn2, red3);
   if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[0] = cost; P[1] = gm; P[2] = xn2; }
@@ -464,7 +546,6 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
   const BaWin W = d.win[w];  // issued with the state, before the done test
   if (S.done) return;
   const int lane = threadIdx.x;
-  if (SH && lane == 0) d.wfail_part[w] = 0.0;  // point-block failures of this iteration (K4)
   if (S.relin) {
     // fixed lane assignment + fixed butterfly => deterministic
     double cost = 0.0, gm = 0.0, xn2 = 0.0;
@@ -495,13 +576,15 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
     if (S.iter >= o.max_iter) { S.done = 1; S.term = LORB_TERM_NO_CONVERGENCE; }
     else if (S.last_successful && S.gmax <= o.gtol) { S.done = 1; S.term = LORB_TERM_GRADIENT_TOL; }
     else if (S.radius <= o.min_radius) { S.done = 1; S.term = LORB_TERM_MIN_RADIUS; }
-    else { S.iter++; S.chol_fail = 0; }
+    else S.iter++;
     d.st[w] = S;
   }
 }
 
-// K4: point-group Schur prep: scaled E^T E + D^2 -> inverse (point phase), then per optimised
-// observation Jps (scaled Jp), Q = Jps E^-1 and g = Q b (observation phase).
+// K4: point-group Schur prep after a rejected step (only the radius changed since k_ba_lin's
+// prep): scaled E^T E + D^2 -> inverse (point phase), then per optimised observation Jps, Q =
+// Jps E^-1 and g = Q b (observation phase).  Iterations that relinearised (last_successful, set
+// by k_ba_lm_begin) were prepared by k_ba_lin.
 __global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
   __shared__ double sEi[kGB][6], sb[kGB][3], ssp[kGB][3];
   if ((int)blockIdx.x >= d.live[0]) return;
@@ -526,29 +609,15 @@ __global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
     for (int k = 0; k < 6; ++k) Jp_f[k] = d.obs_Jp[6 * ef + k];
   }
   const WinState& S = d.st[g.win];
-  if (S.done) return;
+  if (S.done || S.last_successful) return;
   if (t < g.cnt) {
     const int p = g.p0 + t;
-    const double rad = S.radius;
-    double E[6];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) b[k] = b[k] * sp[k];
-    E[0] = Eu[0] * sp[0] * sp[0]; E[1] = Eu[1] * sp[0] * sp[1]; E[2] = Eu[2] * sp[0] * sp[2];
-    E[3] = Eu[3] * sp[1] * sp[1]; E[4] = Eu[4] * sp[1] * sp[2]; E[5] = Eu[5] * sp[2] * sp[2];
-    E[0] += fmin(fmax(E[0], o.min_diag), o.max_diag) / rad;
-    E[3] += fmin(fmax(E[3], o.min_diag), o.max_diag) / rad;
-    E[5] += fmin(fmax(E[5], o.min_diag), o.max_diag) / rad;
-    double Ei[6];
-    if (!inv3(E, Ei)) {
-      // benign race: every writer stores the same value; sharded plans reduce the flag (K5)
-      if (d.sharded) d.wfail_part[g.win] = 1.0;
-      else d.st[g.win].chol_fail = 1;
-      for (int k = 0; k < 6; ++k) Ei[k] = 0.0;
-    }
+    double Ei[6], bs[3];
+    if (!prep_point(Eu, b, sp, S.radius, o, Ei, bs)) prep_fail(d, g.win);
 #pragma unroll
     for (int k = 0; k < 6; ++k) { d.pinv[6 * p + k] = Ei[k]; sEi[t][k] = Ei[k]; }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { sb[t][k] = b[k]; ssp[t][k] = sp[k]; }
+    for (int k = 0; k < 3; ++k) { sb[t][k] = bs[k]; ssp[t][k] = sp[k]; }
   }
   __syncthreads();
   for (int c0 = t; c0 < g.no; c0 += kGB) {
@@ -557,20 +626,10 @@ __global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
     const int m = first ? m_f : d.obs_cm[e];
     if (m < 0) continue;
     const int lp = (first ? pt_f : d.obs_pt[e]) - g.p0;
-    const double* Ei = sEi[lp];
-    const double* b = sb[lp];
-    double Jps[6], Q[6];
+    double Jp[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) Jps[k] = (first ? Jp_f[k] : d.obs_Jp[6 * e + k]) * ssp[lp][k % 3];
-#pragma unroll
-    for (int r = 0; r < 2; ++r)
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        Q[3 * r + j] = Jps[3 * r] * s3(Ei, 0, j) + Jps[3 * r + 1] * s3(Ei, 1, j) + Jps[3 * r + 2] * s3(Ei, 2, j);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { d.obs_Jps[6 * m + k] = Jps[k]; d.obs_Q[6 * m + k] = Q[k]; }
-    d.obs_g[2 * m] = Q[0] * b[0] + Q[1] * b[1] + Q[2] * b[2];
-    d.obs_g[2 * m + 1] = Q[3] * b[0] + Q[4] * b[1] + Q[5] * b[2];
+    for (int k = 0; k < 6; ++k) Jp[k] = first ? Jp_f[k] : d.obs_Jp[6 * e + k];
+    prep_obs(d, m, Jp, sEi[lp], sb[lp], ssp[lp]);
   }
 }
 
@@ -1705,7 +1764,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   top.zslot = (int)(zero - Ab); bot.zslot = top.zslot;
   top.nbk = bot.nbk = nbk; top.dir = 1; bot.dir = -1;
   if (prog) { top.mask = &s_mask; bot.mask = &s_mask; }
-  const int side = wv & 1;                 // 0 top, 1 bottom (waves 0..5)
+  const int side = wv & 1;                 // 0 top, 1 bottom
   const BandSide& me = side == 0 ? top : bot;
   double* pb = side == 0 ? pbt : pbb;
   int* lrd = &s_lrd[side];
@@ -1726,8 +1785,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   if (wv >= 6) {
     if (prog) {  // remaining blocks [ib, nbk - ib): wave 6 from the top, wave 7 from the bottom
       const int lo = ib, hi = nbk - ib, mid = (lo + hi) / 2;
-      for (int k = 0; k < (wv == 6 ? mid - lo : hi - mid); ++k) {
-        const int b = wv == 6 ? lo + k : hi - 1 - k;
+      for (int k = 0; k < (side == 0 ? mid - lo : hi - mid); ++k) {
+        const int b = side == 0 ? lo + k : hi - 1 - k;
         stage_band<7>(S2, Ab, b * cpb, min((b + 1) * cpb, nch), lane, 64, n, bw, nsrc);
         if (lane == 0) __hip_atomic_fetch_or(&s_mask, 1ull << b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -1791,6 +1850,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
         }
 #pragma unroll
     for (int J = 0; J < 4; ++J) T[tri4(3, J)] = v4d{0.0, 0.0, 0.0, 0.0};
+    BandSide topM = top;
+    topM.mask = nullptr; topM.pdone = nullptr;
     {  // M's first panel column to the chain wave
       const int ci = lane & 15, ck = lane >> 4;
 #pragma unroll
@@ -1799,8 +1860,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
         for (int r = 0; r < 4; ++r) pbt[(16 * I + ck + 4 * r) * 17 + ci] = T[tri4(I, 0)][r];
       if (lane == 0) __hip_atomic_fetch_add(&s_prd[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    BandSide topM = top;
-    topM.mask = nullptr; topM.pdone = nullptr;
     topM.update(T, m, m + 48, &s_lrd[0], &s_prd[0], lwant, pbt);
   } else if (wv == 0) {
     zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
@@ -2059,6 +2118,10 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
     if (SH) { mccs += d.wstep[3 * w]; ncost += d.wstep[3 * w + 1]; sn2 += d.wstep[3 * w + 2]; }
   }
   __shared__ int s_accept;
+  // point-block / Cholesky failures are per iteration: cleared here for the next one (k_ba_lin
+  // sets them before k_ba_lm_begin runs)
+  S.chol_fail = 0;
+  if (SH && lane == 0) d.wfail_part[w] = 0.0;
   if (lane == 0) s_accept = lm_decide(d, o, w, S, valid, mccs, ncost, sn2);
   __syncthreads();
   // accepted: the candidate is the new linearisation point -> its rotation states for k_ba_lin
@@ -2706,7 +2769,7 @@ int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   const BaDev& d = P->dev;
   if (P->grid_pblk) {
     lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-    hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
+    hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
   }
   if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(256), 0, s, d);
   if (P->comm) {  // exchange 1: camera blocks + cost / |x|^2 (sum), gradient max (max)
