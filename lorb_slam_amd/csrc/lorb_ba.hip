@@ -1302,6 +1302,20 @@ __device__ __forceinline__ void wait_ge(int* c, int v) {
     if (SLEEP) __builtin_amdgcn_s_sleep(1);
 }
 
+// LORB_CHOL_EARLY: 0 = the chain posts a panel after storing L to the band and to xch (row
+// layout); 1 = xch first, post, then the band; 2 = the update wave reads the panel's L columns
+// from the chain's own column buffer, posted right after the factorization, the band stores
+// overlap the update (C4: 58.0 -> 53.8 us); 3 = 2 + tile (3, 1) of the next column computed by
+// the chain wave (measured slower, 55.7 us)
+#ifndef LORB_CHOL_EARLY
+#define LORB_CHOL_EARLY 2
+#endif
+#ifndef LORB_CHOL_G4
+#define LORB_CHOL_G4 0
+#endif
+// column stride of the chain's L columns in xch (padded against bank conflicts when the update
+// wave reads them in MFMA operand layout)
+constexpr int kCS = LORB_CHOL_EARLY >= 2 ? 65 : 64;
 struct BandSide {
   double* A;     // band storage of the whole matrix (row-major, rows x (bw + 1), row i holds cols
                  // i-bw .. i); the diagonal slot holds 1 / L(i, i) (its only use is the
@@ -1318,6 +1332,16 @@ struct BandSide {
   int nbk = 0, dir = 0;                // row blocks; +1 top view, -1 reversed bottom view
   int zslot = 0;                       // A[zslot] == 0.0 (out-of-band reads of the back-substitution)
   unsigned long long* phases = nullptr;  // LORB_CHOL_PHASES diagnostics: chain wait / factor / store cycles
+  int* hrd = nullptr;                    // LORB_CHOL_EARLY >= 3: hand-overs consumed by the chain
+  int* ppr = nullptr;                    //   and pre-update tiles (3, 1) posted by the update wave
+  unsigned long long* trace = nullptr;   // LORB_CHOL_TRACE diagnostics: per-panel event times
+  int tslot = 0;                         // (slot of this wave's next panel; cycles since t0)
+  unsigned long long t0 = 0;
+  __device__ __forceinline__ void tr(int k) const {
+#ifdef LORB_CHOL_TRACE
+    if (trace && lane == 0) trace[tslot + k] = __builtin_amdgcn_s_memtime() - t0;
+#endif
+  }
 
   __device__ __forceinline__ int idx(int i, int j) const { return base + si * i + sj * j; }
 
@@ -1348,15 +1372,21 @@ struct BandSide {
   // the rest of the window and slides it by 16 -- off the chain's critical path.
   //   chain(): P = the first panel when `pre` (else it comes from pb); pwant counts the pb posts
   //   consumed so far (continues across phases).
+  //   LORB_CHOL_EARLY >= 3 splits the next-column update: the update wave computes tiles (1, 1)
+  //   and (2, 1), the chain wave tile (3, 1) from a pre-update copy the update wave posted early
+  //   (ppwant counts those), so the 12 MFMAs of the hand-over run on two SIMDs.
   __device__ __forceinline__ void chain(double (&P)[NB], double& zr, bool& bad, int kb0, int kend, bool pre,
-                                        int* lrd, int* prd, int& pwant, const double* pb) const {
+                                        int* lrd, int* prd, int& pwant, double* pb, int& ppwant) const {
     const int dstep = 16 * (si + sj);  // address step of one panel along the diagonal
     unsigned l_ok = 0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) l_ok |= (unsigned)(q <= lane && lane - q <= bw) << q;
     int l_base = idx(kb0 + lane, kb0);  // slot of (kb0 + lane, kb0 + q) = l_base + q sj
-    double* colbuf = xch;  // 16 x 64 during the factorization (xch is idle then)
-    double* dummy = xch + lane * 17 + 16;
+    // L column q of the panel at colbuf[q * kCS + row] during the factorization (xch is idle
+    // then); with LORB_CHOL_EARLY >= 2 it is also what the update wave reads
+    double* colbuf = xch;
+    // dummy target of the masked band stores: outside colbuf when the update wave reads colbuf
+    double* dummy = LORB_CHOL_EARLY >= 2 ? xch + 16 * kCS + lane : xch + lane * 17 + 16;
 #ifdef LORB_CHOL_PHASES
     unsigned long long ph_w = 0, ph_c = 0, ph_s = 0, tq = __builtin_amdgcn_s_memtime();
 #define CH_PH(v) do { const unsigned long long q_ = __builtin_amdgcn_s_memtime(); v += q_ - tq; tq = q_; } while (0)
@@ -1372,10 +1402,43 @@ struct BandSide {
         wait_ge<false>(prd, ++pwant);
 #pragma unroll
         for (int q = 0; q < NB; ++q) P[q] = pb[lane * 17 + q];  // lanes < q: upper garbage, never used
+        // pb consumed (the release orders the reads above before the post)
+        if (LORB_CHOL_EARLY >= 3 && lane == 0) __hip_atomic_fetch_add(hrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       CH_PH(ph_w);
+      tr(0);
       const double zin = kb + 16 + lane < rows ? z[kb + 16 + lane] : 0.0;
       double yq = 0.0;
+#if LORB_CHOL_G4
+      // columns in groups of four: inside a group the multipliers come by v_readlane (no LDS
+      // wait on the pivot chain), then one rank-4 update of the panel's later columns with
+      // multipliers broadcast from colbuf.  Every P[q2] receives the same FMAs in the same
+      // (column) order as the column-by-column loop, so the bits are the same.
+#pragma unroll
+      for (int g0 = 0; g0 < NB; g0 += 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = g0 + j;
+          const double akk = readlane_d(P[q], q);
+          bad |= !(akk > 0.0);
+          const double y = rsqrt_refined(akk);
+          P[q] *= y;
+          yq = lane == q ? y : yq;
+          const double zk = readlane_d(zr, q) * y;
+          zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
+          colbuf[q * kCS + lane] = P[q];
+#pragma unroll
+          for (int i = j + 1; i < 4; ++i) {
+            const double l = readlane_d(P[q], g0 + i);
+            P[g0 + i] = fma(-P[q], l, P[g0 + i]);
+          }
+        }
+#pragma unroll
+        for (int q2 = g0 + 4; q2 < NB; ++q2)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) P[q2] = fma(-P[g0 + j], colbuf[(g0 + j) * kCS + q2], P[q2]);
+      }
+#else
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
         const double akk = readlane_d(P[q], q);
@@ -1386,16 +1449,73 @@ struct BandSide {
         const double zk = readlane_d(zr, q) * y;
         zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
         if (q + 1 < NB) {
-          colbuf[q * 64 + lane] = P[q];
+          colbuf[q * kCS + lane] = P[q];
           const double l1 = readlane_d(P[q], q + 1);
           P[q + 1] = fma(-P[q], l1, P[q + 1]);
 #pragma unroll
-          for (int q2 = q + 2; q2 < NB; ++q2) P[q2] = fma(-P[q], colbuf[q * 64 + q2], P[q2]);
+          for (int q2 = q + 2; q2 < NB; ++q2) P[q2] = fma(-P[q], colbuf[q * kCS + q2], P[q2]);
+        } else if (LORB_CHOL_EARLY >= 2) {
+          colbuf[q * kCS + lane] = P[q];
         }
       }
+#endif
       CH_PH(ph_c);
-      wave_sync_lds();  // colbuf reads done before xch is rewritten
+      tr(1);
       const bool rowvalid = kb + lane < rows;
+#if LORB_CHOL_EARLY >= 2
+      // the update wave reads L from colbuf: post it now, then store L to the band (for the
+      // diagonal-block inverses and the back-substitution) while the update runs
+      if (lane == 0) __hip_atomic_fetch_add(lrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if LORB_CHOL_EARLY >= 3
+      // tile (3, 1) of the next panel column: pre-update copy from pb, this panel's L from colbuf
+      const bool nxt = kb + 16 < kend;
+      v4d C31 = {0.0, 0.0, 0.0, 0.0};
+      double o1[4], o3[4];
+      const int ci = lane & 15, ck = lane >> 4;
+      if (nxt) {
+        wait_ge<false>(ppr, ++ppwant);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C31[r] = pb[(32 + ck + 4 * r) * 17 + ci];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          o1[kk] = colbuf[(4 * kk + ck) * kCS + 16 + ci];
+          o3[kk] = colbuf[(4 * kk + ck) * kCS + 48 + ci];
+        }
+      }
+#endif
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
+        *(ok ? A + l_base + q * sj : dummy) = q == lane ? yq : P[q];
+      }
+      l_base += dstep;
+      if (lane < NB) z[kb + lane] = zr;
+      if (lane == 0 && pdone) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if LORB_CHOL_EARLY >= 3
+      if (nxt) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) C31 = __builtin_amdgcn_mfma_f64_16x16x4f64(-o3[kk], o1[kk], C31, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pb[(32 + ck + 4 * r) * 17 + ci] = C31[r];
+      }
+#endif
+#elif LORB_CHOL_EARLY
+      wave_sync_lds();  // colbuf reads done before xch is rewritten
+      // the update wave needs only xch: post it first, then store L to the band (for the
+      // diagonal-block inverses and the back-substitution) while the update runs
+#pragma unroll
+      for (int q = 0; q < NB; ++q) xch[lane * 17 + q] = P[q];
+      if (lane == 0) __hip_atomic_fetch_add(lrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
+        *(ok ? A + l_base + q * sj : dummy) = q == lane ? yq : P[q];
+      }
+      l_base += dstep;
+      if (lane < NB) z[kb + lane] = zr;
+      if (lane == 0 && pdone) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+      wave_sync_lds();  // colbuf reads done before xch is rewritten
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
         const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
@@ -1408,9 +1528,12 @@ struct BandSide {
         if (pdone) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(lrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+#endif
       const double zs = __shfl_down(zr, 16, 64);
       zr = lane < 48 ? zs : zin;
       CH_PH(ph_s);
+      tr(2);
+      const_cast<BandSide*>(this)->tslot += 3;
     }
 #ifdef LORB_CHOL_PHASES
     if (phases && this->lane == 0) { phases[0] += ph_w; phases[1] += ph_c; phases[2] += ph_s; }
@@ -1420,7 +1543,7 @@ struct BandSide {
   //   update(): T = the window at kb0 (column 0 unused); on return the window at kend (all ten
   //   tiles).  lwant counts the L posts consumed so far.
   __device__ __forceinline__ void update(v4d (&T)[10], int kb0, int kend, int* lrd, int* prd, int& lwant,
-                                         double* pb) const {
+                                         double* pb, int& hgive) const {
     const int ci = lane & 15, ck = lane >> 4;
     const int dstep = 16 * (si + sj);
     int tn_addr = idx(kb0 + 64 + ck, kb0 + 16 + ci);  // entering tile (J, r) adds 4 r si + 16 J sj (below)
@@ -1452,27 +1575,51 @@ struct BandSide {
           Tn[J][r] = ok ? v : 0.0;
         }
       tn_addr += dstep;
+      const bool nxt = kb + 16 < kend;
+#if LORB_CHOL_EARLY >= 3
+      if (nxt) {  // the pre-update tile (3, 1) and the entering rows, before this panel's L
+        wait_ge<true>(hrd, hgive);  // the chain has read the previous hand-over
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pb[(32 + ck + 4 * r) * 17 + ci] = T[tri4(3, 1)][r];
+          pb[(48 + ck + 4 * r) * 17 + ci] = Tn[0][r];
+        }
+        ++hgive;
+        if (lane == 0) __hip_atomic_fetch_add(ppr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+#endif
+      tr(0);
       wait_ge<true>(lrd, ++lwant);
+      tr(1);
       double opA[4][4];
 #pragma unroll
       for (int I = 1; I < 4; ++I)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) opA[I][kk] = xch[(16 * I + ci) * 17 + 4 * kk + ck];
-      // the next panel's column first, then hand it over
+        for (int kk = 0; kk < 4; ++kk)
+          opA[I][kk] = LORB_CHOL_EARLY >= 2 ? xch[(4 * kk + ck) * kCS + 16 * I + ci] : xch[(16 * I + ci) * 17 + 4 * kk + ck];
+      // the next panel's column first, then hand it over (EARLY >= 3: tile (3, 1) is the chain's)
+      constexpr int IH = LORB_CHOL_EARLY >= 3 ? 3 : 4;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-        for (int I = 1; I < 4; ++I)
+        for (int I = 1; I < IH; ++I)
           T[tri4(I, 1)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[1][kk], T[tri4(I, 1)], 0, 0, 0);
-      if (kb + 16 < kend) {
+      if (nxt) {
 #pragma unroll
-        for (int I = 1; I < 4; ++I)
+        for (int I = 1; I < IH; ++I)
 #pragma unroll
           for (int r = 0; r < 4; ++r) pb[(16 * (I - 1) + ck + 4 * r) * 17 + ci] = T[tri4(I, 1)][r];
+        if (LORB_CHOL_EARLY < 3) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pb[(48 + ck + 4 * r) * 17 + ci] = Tn[0][r];
+          for (int r = 0; r < 4; ++r) pb[(48 + ck + 4 * r) * 17 + ci] = Tn[0][r];
+        }
         if (lane == 0) __hip_atomic_fetch_add(prd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else if (LORB_CHOL_EARLY >= 3) {  // last panel of the phase: the window keeps column 1 whole
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          T[tri4(3, 1)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[3][kk], opA[1][kk], T[tri4(3, 1)], 0, 0, 0);
       }
+      tr(2);
       // k-step outer: the three tiles' accumulation chains interleave
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
@@ -1486,6 +1633,8 @@ struct BandSide {
       T[tri4(2, 0)] = T[tri4(3, 1)]; T[tri4(2, 1)] = T[tri4(3, 2)]; T[tri4(2, 2)] = T[tri4(3, 3)];
 #pragma unroll
       for (int J = 0; J < 4; ++J) T[tri4(3, J)] = Tn[J];
+      tr(3);
+      const_cast<BandSide*>(this)->tslot += 4;
     }
   }
   // The 16 x 16 diagonal block of L at view rows c0 .. c0+15 replaced in place by its inverse X
@@ -1721,12 +1870,14 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   __shared__ int s_pdone[2];
   __shared__ int s_lrd[2], s_prd[2];  // per side: L panels posted (chain), panel columns posted (update)
   __shared__ int s_hand[3];           // T / B -> M hand-over (below)
+  __shared__ int s_hrd[2], s_ppr[2];  // per side: hand-overs consumed, pre-update tiles posted (EARLY >= 3)
   const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
   const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
   const int nbk = n16 / 16, ib = 4;
 #ifndef LORB_CHOL_PROG
 #define LORB_CHOL_PROG 1
 #endif
+
   const bool prog = LORB_CHOL_PROG && nbk <= 64 && nbk > 2 * ib;
   const int cpb = 8 * B1;  // chunks per 16-row block
   // rhs loads issued before the band copy (one round trip for both)
@@ -1753,6 +1904,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     s_pdone[0] = 0; s_pdone[1] = 0;
     s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
     s_hand[0] = 0; s_hand[1] = 0; s_hand[2] = 0;
+    s_hrd[0] = 0; s_hrd[1] = 0; s_ppr[0] = 0; s_ppr[1] = 0;
     unsigned long long msk = 0;
     for (int b = 0; b < nbk; ++b) msk |= (unsigned long long)(!prog || b < ib || b >= nbk - ib) << (b & 63);
     s_mask = msk;
@@ -1761,15 +1913,27 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   BandSide top{Ab, zt, xt, rt, bw, lane, bw, bw, 1};
   BandSide bot{Ab, zb, xb, rb, bw, lane, (n16 - 1) * B1 + bw, -1, -bw};
   top.pdone = &s_pdone[0]; bot.pdone = &s_pdone[1];
+  top.hrd = &s_hrd[0]; bot.hrd = &s_hrd[1]; top.ppr = &s_ppr[0]; bot.ppr = &s_ppr[1];
   top.zslot = (int)(zero - Ab); bot.zslot = top.zslot;
   top.nbk = bot.nbk = nbk; top.dir = 1; bot.dir = -1;
   if (prog) { top.mask = &s_mask; bot.mask = &s_mask; }
+#ifdef LORB_CHOL_TRACE
+  // dbg[256 w + ...]: chain top 0.. (3 per panel), update top 64.. (4 per panel), chain bottom
+  // 128.., update bottom 160.., single events 200..
+  const unsigned long long tr0 = __builtin_amdgcn_s_memtime();
+  unsigned long long* trb = d.dbg + 256 * w;
+  top.trace = trb; bot.trace = trb; top.t0 = tr0; bot.t0 = tr0;
+  top.tslot = wv == 0 ? 0 : 64; bot.tslot = wv == 1 ? 128 : 160;
+#define TR1(k) do { if (lane == 0) trb[200 + (k)] = __builtin_amdgcn_s_memtime() - tr0; } while (0)
+#else
+#define TR1(k) do {} while (0)
+#endif
   const int side = wv & 1;                 // 0 top, 1 bottom
   const BandSide& me = side == 0 ? top : bot;
   double* pb = side == 0 ? pbt : pbb;
   int* lrd = &s_lrd[side];
   int* prd = &s_prd[side];
-  int lwant = 0, pwant = 0;
+  int lwant = 0, pwant = 0, ppwant = 0, hgive = 0;
   bool bad = false;
   double zr = 0.0;
   double P[NB];
@@ -1791,6 +1955,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
         if (lane == 0) __hip_atomic_fetch_or(&s_mask, 1ull << b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
+    TR1(8 + side);
   } else if (wv >= 4) {
     int* pd = &s_pdone[side];
     const int nblk = (side == 0 ? m : nB) / 16;
@@ -1798,16 +1963,17 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
       while (__hip_atomic_load(pd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= p) __builtin_amdgcn_s_sleep(1);
       me.linv(16 * p);
     }
+    TR1(10 + side);
   } else if (wv < 2) {
     me.init_panel(P, zr);
 #ifdef LORB_CHOL_PHASES
     unsigned long long* phv = d.dbg + 8 * w;  // wave 0, T phase: [0] wait [1] factor [2] store
     if (wv == 0) { if (lane == 0) { phv[0] = phv[1] = phv[2] = 0; } const_cast<BandSide&>(me).phases = phv; }
 #endif
-    me.chain(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, pwant, pb);
+    me.chain(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, pwant, pb, ppwant);
   } else if (wv < 4) {
     me.init_tiles(T);
-    me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb);
+    me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb, hgive);
   }
   if (wv < 6) C2_STAMP(wv);
   // Hand-over to the M phase by flags, not barriers (the diagonal-block inverses of waves 4 / 5
@@ -1826,6 +1992,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
           if (kap <= rho) X[(47 - kap) * 48 + (47 - rho)] = T[tri4(I, J)][r];
         }
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    TR1(2);
   }
   if (wv == 1) {
     if (lane < 48) zX[47 - lane] = zr;
@@ -1833,8 +2000,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[2], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   if (wv == 2) {
+    TR1(0);
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     wait_ge<true>(&s_hand[1], 1);
+    TR1(1);
   }
   if (wv == 0) wait_ge<true>(&s_hand[2], 1);
   if (wv == 2) {
@@ -1854,18 +2023,21 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     topM.mask = nullptr; topM.pdone = nullptr;
     {  // M's first panel column to the chain wave
       const int ci = lane & 15, ck = lane >> 4;
+      if (LORB_CHOL_EARLY >= 3) { wait_ge<true>(&s_hrd[0], hgive); ++hgive; }
 #pragma unroll
       for (int I = 0; I < 4; ++I)
 #pragma unroll
         for (int r = 0; r < 4; ++r) pbt[(16 * I + ck + 4 * r) * 17 + ci] = T[tri4(I, 0)][r];
       if (lane == 0) __hip_atomic_fetch_add(&s_prd[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    topM.update(T, m, m + 48, &s_lrd[0], &s_prd[0], lwant, pbt);
+    topM.update(T, m, m + 48, &s_lrd[0], &s_prd[0], lwant, pbt, hgive);
   } else if (wv == 0) {
     zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
     BandSide topM = top;
     topM.mask = nullptr; topM.pdone = nullptr;
-    topM.chain(P, zr, bad, m, m + 48, false, &s_lrd[0], &s_prd[0], pwant, pbt);
+    TR1(3);
+    topM.chain(P, zr, bad, m, m + 48, false, &s_lrd[0], &s_prd[0], pwant, pbt, ppwant);
+    TR1(4);
     if (bad) s_bad = 1;
     C2_STAMP(6);
   }
@@ -1882,23 +2054,29 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   if (wv == 0) {
     BS_PH(3);
     BandSide::BsWin S{top.bs_init(m + 32, 0)};
+    TR1(5);
     top.bs_run<false>(S, m + 32, m);                   // y_M (chained triangles)
     BS_PH(4);
+    TR1(6);
     if (lane < 48) zb[nB + 47 - lane] = zt[m + lane];  // into the reversed bottom rows
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     top.bs_run<true>(S, m - 16, 0);                   // y_T (inverted diagonal blocks)
     BS_PH(5);
+    TR1(7);
   } else if (wv == 1) {
     wait_ge<false>(&s_hand[0], 2);
     BS_PH(6);
     BandSide::BsWin S{bot.bs_init(nB - 16, 48)};
     bot.bs_run<true>(S, nB - 16, 0);                // y_B (reversed)
     BS_PH(7);
+    TR1(12);
   }
 #undef BS_PH
   if (wv == 0) C2_STAMP(7);
   __syncthreads();
+  TR1(13);
 #undef C2_STAMP
+#undef TR1
   for (int k = t; k < n; k += NT) d.ycam[W.row_base + k] = k < rt ? zt[k] : zb[n16 - 1 - k];
   const int cur = d.st[w].cur;
   for (int ci2 = t; ci2 < W.n_poses; ci2 += NT) {
@@ -2734,7 +2912,11 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
   if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, ctx->stream));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
+#ifdef LORB_CHOL_TRACE
+  LORB_TRY(dalloc(P, (size_t)nw * 256, &d.dbg));
+#else
   LORB_TRY(dalloc(P, (size_t)nw * 8, &d.dbg));
+#endif
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
   if (!obs_cam.empty()) { /* keep obs arrays alive via allocs */ }
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -3261,7 +3443,11 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(dalloc(P, C, &d.rot_lin)); LORB_TRY(dalloc(P, C, &d.rot_cand));
   LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
   LORB_TRY(dalloc(P, n, &d.ycam));
+#ifdef LORB_CHOL_TRACE
+  LORB_TRY(dalloc(P, (size_t)256, &d.dbg));
+#else
   LORB_TRY(dalloc(P, (size_t)8, &d.dbg));
+#endif
   LORB_TRY(dalloc(P, (size_t)1, &P->d_state)); d.st = P->d_state;
   P->W = 1;
   P->hwin.assign(1, BaWin{});
@@ -3537,7 +3723,12 @@ int lorb_ba_plan_read(lorb_ba_plan* plan, double* const* pose_out, double* const
 // diagnostic: copy the Cholesky phase stamps of window 0 (LORB_CHOL_STAMPS builds)
 int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8) {
   if (!plan || !out8) return LORB_E_INVALID;
-  LORB_HIP(plan->ctx, hipMemcpyAsync(out8, plan->dev.dbg, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, plan->ctx->stream));
+#ifdef LORB_CHOL_TRACE
+  const size_t nst = 256;  // trace builds: the caller passes 256 entries
+#else
+  const size_t nst = 8;
+#endif
+  LORB_HIP(plan->ctx, hipMemcpyAsync(out8, plan->dev.dbg, nst * sizeof(unsigned long long), hipMemcpyDeviceToHost, plan->ctx->stream));
   LORB_HIP(plan->ctx, hipStreamSynchronize(plan->ctx->stream));
   return LORB_OK;
 }

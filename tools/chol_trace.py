@@ -1,0 +1,32 @@
+"""Diagnostic: per-panel event timeline of k_ba_chol_2s on the C4 window (cycles, s_memtime).
+Needs LORB_LIB_PATH=liblorb_trace.so (tools/build_variant.sh trace -DLORB_CHOL_TRACE)."""
+import sys, os, ctypes as C
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from lorb_slam_amd import synth, _abi as A
+from lorb_slam_amd.runtime import Context, BAPlan, lib
+ctx = Context(0)
+opt = A.LMOptions.default(max_num_iterations=1, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+plan = BAPlan(ctx, [synth.ba_window(seed=4, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400)])
+for _ in range(4):
+    plan.solve(opt)
+ctx.sync()
+out = (C.c_ulonglong * 256)()
+lib().lorb_ba_plan_debug_stamps(plan._p, out)
+v = list(out)
+def chain(base, n):
+    return [(v[base + 3 * p], v[base + 3 * p + 1], v[base + 3 * p + 2]) for p in range(n)]
+def upd(base, n):
+    return [tuple(v[base + 4 * p + k] for k in range(4)) for p in range(n)]
+print("top chain  (ready, factored, posted):")
+for p, e in enumerate(chain(0, 11)): print("  ", p, e, "factor", e[1] - e[0], "store", e[2] - e[1])
+print("top update (Tn loaded, L got, handed, done):")
+for p, e in enumerate(upd(64, 11)): print("  ", p, e)
+print("bottom chain:")
+for p, e in enumerate(chain(128, 8)): print("  ", p, e, "factor", e[1] - e[0], "store", e[2] - e[1])
+print("bottom update:")
+for p, e in enumerate(upd(160, 8)): print("  ", p, e)
+names = ["w2 T done", "w2 got X", "w3 X written", "w0 M start", "w0 M done", "w0 bs start", "w0 bs M done",
+         "w0 bs T done", "stage top done", "stage bot done", "linv top done", "linv bot done", "w1 bs B done", "end"]
+for k, nm in enumerate(names): print(f"{nm:16s} {v[200 + k]}")
+plan.close()
