@@ -645,12 +645,20 @@ __device__ __forceinline__ double& band(double* A, int bw, int i, int j) {
 // the camera Jacobi scales are applied once per block.  Block pairs are sorted by camera and
 // remapped so that each XCD (blockIdx % 8 group) takes a contiguous run: the tiles of a camera
 // are re-read from that XCD's L2 instead of from the fabric.
-__device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc)[36]) {
-  double Qh[6], Jl[6], Ch[12], Cl[12];
+// DIAG (a diagonal block: pr.x == pr.y, pairs in camera-slot order): the camera's rhs term
+// Jc^T g of the same observation is accumulated from the tiles already loaded
+template <bool DIAG>
+__device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc)[36], double (&r6)[6]) {
+  double Qh[6], Jl[6], Ch[12], Cl[12], g0 = 0.0, g1 = 0.0;
 #pragma unroll
   for (int k = 0; k < 6; ++k) { Qh[k] = d.obs_Q[6 * pr.x + k]; Jl[k] = d.obs_Jps[6 * pr.y + k]; }
 #pragma unroll
-  for (int k = 0; k < 12; ++k) { Ch[k] = d.obs_Jc[12 * pr.x + k]; Cl[k] = d.obs_Jc[12 * pr.y + k]; }
+  for (int k = 0; k < 12; ++k) { Ch[k] = d.obs_Jc[12 * pr.x + k]; Cl[k] = DIAG ? Ch[k] : d.obs_Jc[12 * pr.y + k]; }
+  if (DIAG) {
+    g0 = d.obs_g[2 * pr.x]; g1 = d.obs_g[2 * pr.x + 1];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) r6[k] += Ch[k] * g0 + Ch[6 + k] * g1;
+  }
   double M[4], N[12];
 #pragma unroll
   for (int r = 0; r < 2; ++r)
@@ -695,27 +703,26 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
   const int end = bp.off + bp.cnt;
   // camera-major slots (obs in camera ch, obs in camera cl) of one point; the next step's pair
   // indices are read while this step's tiles load (same pairs, same order)
-  int q = bp.off + t;
-  int2 p0n = make_int2(0, 0), p1n = make_int2(0, 0);
-  if (q < end) { p0n = d.pairs[q]; p1n = d.pairs[q + 256 < end ? q + 256 : q]; }
-  for (; q < end; q += 512) {
-    const int2 p0 = p0n, p1 = p1n;
-    const bool two = q + 256 < end;
-    const int qn = q + 512;
-    if (qn < end) { p0n = d.pairs[qn]; p1n = d.pairs[qn + 256 < end ? qn + 256 : qn]; }
-    schur_pair(d, p0, acc);
-    if (two) schur_pair(d, p1, acc);
-  }
   const bool diag = bp.ch == bp.cl;
   double r6[6] = {0, 0, 0, 0, 0, 0};
-  if (diag) {
-    const int a0 = d.cam_obs_off[bp.ch], a1 = d.cam_obs_off[bp.ch + 1];
-    for (int e = a0 + t; e < a1; e += 256) {
-      const double g0 = d.obs_g[2 * e], g1 = d.obs_g[2 * e + 1];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) r6[k] += d.obs_Jc[12 * e + k] * g0 + d.obs_Jc[12 * e + 6 + k] * g1;
+  // A diagonal block's pairs are (e, e) for the camera's slots e in order (both plan builders),
+  // so thread t meets the observations a0 + t, a0 + t + 256, ... of the rhs sum in its order.
+  auto run = [&](auto diag_c) {
+    constexpr bool DG = decltype(diag_c)::value;
+    int q = bp.off + t;
+    int2 p0n = make_int2(0, 0), p1n = make_int2(0, 0);
+    if (q < end) { p0n = d.pairs[q]; p1n = d.pairs[q + 256 < end ? q + 256 : q]; }
+    for (; q < end; q += 512) {
+      const int2 p0 = p0n, p1 = p1n;
+      const bool two = q + 256 < end;
+      const int qn = q + 512;
+      if (qn < end) { p0n = d.pairs[qn]; p1n = d.pairs[qn + 256 < end ? qn + 256 : qn]; }
+      schur_pair<DG>(d, p0, acc, r6);
+      if (two) schur_pair<DG>(d, p1, acc, r6);
     }
-  }
+  };
+  if (diag) run(std::true_type{});
+  else run(std::false_type{});
 #pragma unroll
   for (int k = 0; k < 36; ++k) {
     const double v = wave_sum(acc[k]);
@@ -1313,6 +1320,19 @@ __device__ __forceinline__ void wait_ge(int* c, int v) {
 #ifndef LORB_CHOL_G4
 #define LORB_CHOL_G4 0
 #endif
+// LORB_CHOL_SP: 2 = software-pipelined panel columns (the previous column's updates issued
+// inside the pivot chain behind a scheduling barrier; factor 4.7k -> 3.9k cycles per panel)
+#ifndef LORB_CHOL_SP
+#define LORB_CHOL_SP 2
+#endif
+#ifndef LORB_CHOL_LINV6
+#define LORB_CHOL_LINV6 0
+#endif
+// LORB_CHOL_LINV4: 1 = diagonal-block inverses on all 64 lanes (10k -> 5k cycles per block;
+// with SP they were the back-substitution's critical path)
+#ifndef LORB_CHOL_LINV4
+#define LORB_CHOL_LINV4 1
+#endif
 // column stride of the chain's L columns in xch (padded against bank conflicts when the update
 // wave reads them in MFMA operand layout)
 constexpr int kCS = LORB_CHOL_EARLY >= 2 ? 65 : 64;
@@ -1409,7 +1429,45 @@ struct BandSide {
       tr(0);
       const double zin = kb + 16 + lane < rows ? z[kb + 16 + lane] : 0.0;
       double yq = 0.0;
-#if LORB_CHOL_G4
+#if LORB_CHOL_SP
+      // software-pipelined columns: column q-1's updates of the later columns (multipliers loaded
+      // from colbuf at the end of iteration q-1) are issued inside column q's pivot chain, which
+      // no longer waits on LDS.  Every P[q2] still receives its FMAs in column order (same bits).
+      double mp[NB];
+#pragma unroll
+      for (int q2 = 0; q2 < NB; ++q2) mp[q2] = 0.0;
+      double akk = readlane_d(P[0], 0);
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        bad |= !(akk > 0.0);
+        double y = __builtin_amdgcn_rsq(akk);
+        {
+          const double e = fma(-akk * y, y, 1.0);
+          y = fma(0.5 * y, e, y);
+        }
+        if (LORB_CHOL_SP >= 2) __builtin_amdgcn_sched_barrier(0);
+        if (q >= 1) {
+#pragma unroll
+          for (int q2 = q + 1; q2 < NB; ++q2) P[q2] = fma(-P[q - 1], mp[q2], P[q2]);
+        }
+        {
+          const double e = fma(-akk * y, y, 1.0);
+          y = fma(0.5 * y, e, y);
+        }
+        P[q] *= y;  // lane q: akk * y = L(k, k)
+        yq = lane == q ? y : yq;
+        const double zk = readlane_d(zr, q) * y;
+        zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
+        colbuf[q * kCS + lane] = P[q];
+        if (q + 1 < NB) {
+          const double l1 = readlane_d(P[q], q + 1);
+          P[q + 1] = fma(-P[q], l1, P[q + 1]);
+          akk = readlane_d(P[q + 1], q + 1);
+#pragma unroll
+          for (int q2 = q + 2; q2 < NB; ++q2) mp[q2] = colbuf[q * kCS + q2];
+        }
+      }
+#elif LORB_CHOL_G4
       // columns in groups of four: inside a group the multipliers come by v_readlane (no LDS
       // wait on the pivot chain), then one rank-4 update of the panel's later columns with
       // multipliers broadcast from colbuf.  Every P[q2] receives the same FMAs in the same
@@ -1641,6 +1699,47 @@ struct BandSide {
   // (lower triangular; the diagonal slot already holds 1 / L(i, i) = X(i, i)).  Column j = lane
   // (lanes 0..15): X(i, j) = -X(i, i) sum_{k=j}^{i-1} L(i, k) X(k, j).  Only the back-substitution
   // reads the block afterwards.
+#if LORB_CHOL_LINV4
+  // All 64 lanes: lane = 4 j + r holds column j's rows i = 4 m + r (acc[m]).  Step k: the lane
+  // of row k (r = k & 3) forms X(k, j) and stores it, a quad broadcast hands it to the column's
+  // four lanes, each adds L(i, k) X(k, j) to its rows.  The L loads (about 30 per lane) are all
+  // issued before the sweep.  Per row the FMAs run in k order as in the 16-lane sweep (same bits).
+  template <int K>
+  __device__ __forceinline__ void linv_step(int c0, int j, int r, double (&acc)[4], const double (&dv)[4],
+                                            const double (&lv)[16][4]) const {
+    constexpr int rk = K & 3, mk = K >> 2;
+    const double xo = K == j ? dv[mk] : (K > j ? -dv[mk] * acc[mk] : 0.0);
+    if (r == rk && K > j && K - j <= bw) A[idx(c0 + K, c0 + j)] = xo;
+    const double xk = dpp_d<rk * 0x55>(xo);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      if (4 * m + 3 > K) acc[m] = fma(lv[K][m], xk, acc[m]);  // lv == 0 where 4 m + r <= K
+  }
+  template <int K>
+  __device__ __forceinline__ void linv_sweep(int c0, int j, int r, double (&acc)[4], const double (&dv)[4],
+                                             const double (&lv)[16][4]) const {
+    linv_step<K>(c0, j, r, acc, dv, lv);
+    if constexpr (K + 1 < 16) linv_sweep<K + 1>(c0, j, r, acc, dv, lv);
+  }
+  __device__ __forceinline__ void linv(int c0) const {
+    const int j = lane >> 2, r = lane & 3;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0}, dv[4], lv[16][4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) dv[m] = A[idx(c0 + 4 * m + r, c0 + 4 * m + r)];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        if (4 * m + 3 > k) {
+          const int i = 4 * m + r;
+          lv[k][m] = A[(i > k && i - k <= bw) ? idx(c0 + i, c0 + k) : zslot];
+        } else {
+          lv[k][m] = 0.0;
+        }
+      }
+    linv_sweep<0>(c0, j, r, acc, dv, lv);
+  }
+#else
   __device__ __forceinline__ void linv(int c0) const {
     if (lane >= 16) return;
     const int j = lane;
@@ -1662,6 +1761,7 @@ struct BandSide {
       }
     }
   }
+#endif
   // Back-substitution L^T y = z, push style: the 64 rows c0-48 .. c0+15 of the current block c0
   // live in registers (row r in lane r & 63, so sliding the window needs no shuffle).  A block
   // solves its 16 x 16 triangle -- as a v_readlane chain (c0 >= c_inv) or as one product with the
@@ -1918,10 +2018,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   top.nbk = bot.nbk = nbk; top.dir = 1; bot.dir = -1;
   if (prog) { top.mask = &s_mask; bot.mask = &s_mask; }
 #ifdef LORB_CHOL_TRACE
-  // dbg[256 w + ...]: chain top 0.. (3 per panel), update top 64.. (4 per panel), chain bottom
-  // 128.., update bottom 160.., single events 200..
+  // dbg[512 w + ...]: chain top 0.. (3 per panel), update top 64.. (4 per panel), chain bottom
+  // 128.., update bottom 160.., single events 200.., diagonal-block inverses 256..
   const unsigned long long tr0 = __builtin_amdgcn_s_memtime();
-  unsigned long long* trb = d.dbg + 256 * w;
+  unsigned long long* trb = d.dbg + 512 * w;
   top.trace = trb; bot.trace = trb; top.t0 = tr0; bot.t0 = tr0;
   top.tslot = wv == 0 ? 0 : 64; bot.tslot = wv == 1 ? 128 : 160;
 #define TR1(k) do { if (lane == 0) trb[200 + (k)] = __builtin_amdgcn_s_memtime() - tr0; } while (0)
@@ -1956,12 +2056,17 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
       }
     }
     TR1(8 + side);
-  } else if (wv >= 4) {
+  }
+  // diagonal-block inverses: waves 4 / 5 share SIMDs with the chain waves; LORB_CHOL_LINV6 moves
+  // them to waves 6 / 7 after their staging (SIMDs of the MFMA-paced update waves)
+  if (LORB_CHOL_LINV6 ? wv >= 6 : (wv == 4 || wv == 5)) {
     int* pd = &s_pdone[side];
     const int nblk = (side == 0 ? m : nB) / 16;
     for (int p = 0; p < nblk; ++p) {
       while (__hip_atomic_load(pd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= p) __builtin_amdgcn_s_sleep(1);
+      TR1(56 + 32 * side + 2 * p);   // dbg[256 + 32 side + 2 p]
       me.linv(16 * p);
+      TR1(57 + 32 * side + 2 * p);
     }
     TR1(10 + side);
   } else if (wv < 2) {
@@ -2913,7 +3018,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, ctx->stream));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
 #ifdef LORB_CHOL_TRACE
-  LORB_TRY(dalloc(P, (size_t)nw * 256, &d.dbg));
+  LORB_TRY(dalloc(P, (size_t)nw * 512, &d.dbg));
 #else
   LORB_TRY(dalloc(P, (size_t)nw * 8, &d.dbg));
 #endif
@@ -3444,7 +3549,7 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
   LORB_TRY(dalloc(P, n, &d.ycam));
 #ifdef LORB_CHOL_TRACE
-  LORB_TRY(dalloc(P, (size_t)256, &d.dbg));
+  LORB_TRY(dalloc(P, (size_t)512, &d.dbg));
 #else
   LORB_TRY(dalloc(P, (size_t)8, &d.dbg));
 #endif
@@ -3724,7 +3829,7 @@ int lorb_ba_plan_read(lorb_ba_plan* plan, double* const* pose_out, double* const
 int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8) {
   if (!plan || !out8) return LORB_E_INVALID;
 #ifdef LORB_CHOL_TRACE
-  const size_t nst = 256;  // trace builds: the caller passes 256 entries
+  const size_t nst = 512;  // trace builds: the caller passes 512 entries
 #else
   const size_t nst = 8;
 #endif

@@ -11,7 +11,7 @@ plan = BAPlan(ctx, [synth.ba_window(seed=4, n_kf=50, n_pts=10000, n_fixed=5, fix
 for _ in range(4):
     plan.solve(opt)
 ctx.sync()
-out = (C.c_ulonglong * 256)()
+out = (C.c_ulonglong * 512)()
 lib().lorb_ba_plan_debug_stamps(plan._p, out)
 v = list(out)
 def chain(base, n):
@@ -30,3 +30,5 @@ names = ["w2 T done", "w2 got X", "w3 X written", "w0 M start", "w0 M done", "w0
          "w0 bs T done", "stage top done", "stage bot done", "linv top done", "linv bot done", "w1 bs B done", "end"]
 for k, nm in enumerate(names): print(f"{nm:16s} {v[200 + k]}")
 plan.close()
+print("linv top (start, end):", [(v[256 + 2 * p], v[257 + 2 * p]) for p in range(8)])
+print("linv bot (start, end):", [(v[288 + 2 * p], v[289 + 2 * p]) for p in range(8)])
