@@ -2094,7 +2094,9 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int rho = 16 * I + (lane >> 4) + 4 * r, kap = 16 * J + (lane & 15);
-          if (kap <= rho) X[(47 - kap) * 48 + (47 - rho)] = T[tri4(I, J)][r];
+          // unconditional: the upper-triangle slots are never read (no exec-mask branches)
+          X[(47 - kap) * 48 + (47 - rho)] = T[tri4(I, J)][r];
+          (void)kap; (void)rho;
         }
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     TR1(2);
@@ -2120,10 +2122,12 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int rho = 16 * I + (lane >> 4) + 4 * r, kap = 16 * J + (lane & 15);
-          if (kap <= rho) T[tri4(I, J)][r] += X[rho * 48 + kap] - top.get(m + rho, m + kap);
+          // branch-free: above the diagonal the tiles hold values nobody reads
+          T[tri4(I, J)][r] += X[rho * 48 + kap] - top.get(m + rho, m + kap);
         }
 #pragma unroll
     for (int J = 0; J < 4; ++J) T[tri4(3, J)] = v4d{0.0, 0.0, 0.0, 0.0};
+    TR1(14);
     BandSide topM = top;
     topM.mask = nullptr; topM.pdone = nullptr;
     {  // M's first panel column to the chain wave
@@ -2135,6 +2139,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
         for (int r = 0; r < 4; ++r) pbt[(16 * I + ck + 4 * r) * 17 + ci] = T[tri4(I, 0)][r];
       if (lane == 0) __hip_atomic_fetch_add(&s_prd[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    TR1(15);
     topM.update(T, m, m + 48, &s_lrd[0], &s_prd[0], lwant, pbt, hgive);
   } else if (wv == 0) {
     zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
@@ -2169,7 +2174,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     BS_PH(5);
     TR1(7);
   } else if (wv == 1) {
-    wait_ge<false>(&s_hand[0], 2);
+    wait_ge<true>(&s_hand[0], 2);  // a long wait (the M phase): sleep, do not steal LDS cycles
     BS_PH(6);
     BandSide::BsWin S{bot.bs_init(nB - 16, 48)};
     bot.bs_run<true>(S, nB - 16, 0);                // y_B (reversed)
