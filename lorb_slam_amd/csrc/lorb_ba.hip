@@ -590,6 +590,11 @@ __global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
   if ((int)blockIdx.x >= d.live[0]) return;
   const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x;
+  // most iterations relinearise (k_ba_lin did the prep): test the state before any other load
+  {
+    const WinState& S0 = d.st[g.win];
+    if (S0.done || S0.last_successful) return;
+  }
   // the point's terms go out together with the window state
   const int pf = g.p0 + min(t, max(g.cnt - 1, 0));
   double sp[3] = {0, 0, 0}, b[3] = {0, 0, 0}, Eu[6] = {0, 0, 0, 0, 0, 0};
