@@ -1314,33 +1314,9 @@ __device__ __forceinline__ void wait_ge(int* c, int v) {
     if (SLEEP) __builtin_amdgcn_s_sleep(1);
 }
 
-// LORB_CHOL_EARLY: 0 = the chain posts a panel after storing L to the band and to xch (row
-// layout); 1 = xch first, post, then the band; 2 = the update wave reads the panel's L columns
-// from the chain's own column buffer, posted right after the factorization, the band stores
-// overlap the update (C4: 58.0 -> 53.8 us); 3 = 2 + tile (3, 1) of the next column computed by
-// the chain wave (measured slower, 55.7 us)
-#ifndef LORB_CHOL_EARLY
-#define LORB_CHOL_EARLY 2
-#endif
-#ifndef LORB_CHOL_G4
-#define LORB_CHOL_G4 0
-#endif
-// LORB_CHOL_SP: 2 = software-pipelined panel columns (the previous column's updates issued
-// inside the pivot chain behind a scheduling barrier; factor 4.7k -> 3.9k cycles per panel)
-#ifndef LORB_CHOL_SP
-#define LORB_CHOL_SP 2
-#endif
-#ifndef LORB_CHOL_LINV6
-#define LORB_CHOL_LINV6 0
-#endif
-// LORB_CHOL_LINV4: 1 = diagonal-block inverses on all 64 lanes (10k -> 5k cycles per block;
-// with SP they were the back-substitution's critical path)
-#ifndef LORB_CHOL_LINV4
-#define LORB_CHOL_LINV4 1
-#endif
-// column stride of the chain's L columns in xch (padded against bank conflicts when the update
-// wave reads them in MFMA operand layout)
-constexpr int kCS = LORB_CHOL_EARLY >= 2 ? 65 : 64;
+// Column stride of the chain's L columns in xch, padded against bank conflicts when the update
+// wave reads them in MFMA operand layout.
+constexpr int kCS = 65;
 struct BandSide {
   double* A;     // band storage of the whole matrix (row-major, rows x (bw + 1), row i holds cols
                  // i-bw .. i); the diagonal slot holds 1 / L(i, i) (its only use is the
@@ -1357,8 +1333,6 @@ struct BandSide {
   int nbk = 0, dir = 0;                // row blocks; +1 top view, -1 reversed bottom view
   int zslot = 0;                       // A[zslot] == 0.0 (out-of-band reads of the back-substitution)
   unsigned long long* phases = nullptr;  // LORB_CHOL_PHASES diagnostics: chain wait / factor / store cycles
-  int* hrd = nullptr;                    // LORB_CHOL_EARLY >= 3: hand-overs consumed by the chain
-  int* ppr = nullptr;                    //   and pre-update tiles (3, 1) posted by the update wave
   unsigned long long* trace = nullptr;   // LORB_CHOL_TRACE diagnostics: per-panel event times
   int tslot = 0;                         // (slot of this wave's next panel; cycles since t0)
   unsigned long long t0 = 0;
@@ -1397,21 +1371,18 @@ struct BandSide {
   // the rest of the window and slides it by 16 -- off the chain's critical path.
   //   chain(): P = the first panel when `pre` (else it comes from pb); pwant counts the pb posts
   //   consumed so far (continues across phases).
-  //   LORB_CHOL_EARLY >= 3 splits the next-column update: the update wave computes tiles (1, 1)
-  //   and (2, 1), the chain wave tile (3, 1) from a pre-update copy the update wave posted early
-  //   (ppwant counts those), so the 12 MFMAs of the hand-over run on two SIMDs.
   __device__ __forceinline__ void chain(double (&P)[NB], double& zr, bool& bad, int kb0, int kend, bool pre,
-                                        int* lrd, int* prd, int& pwant, double* pb, int& ppwant) const {
+                                        int* lrd, int* prd, int& pwant, const double* pb) const {
     const int dstep = 16 * (si + sj);  // address step of one panel along the diagonal
     unsigned l_ok = 0;
 #pragma unroll
     for (int q = 0; q < NB; ++q) l_ok |= (unsigned)(q <= lane && lane - q <= bw) << q;
     int l_base = idx(kb0 + lane, kb0);  // slot of (kb0 + lane, kb0 + q) = l_base + q sj
-    // L column q of the panel at colbuf[q * kCS + row] during the factorization (xch is idle
-    // then); with LORB_CHOL_EARLY >= 2 it is also what the update wave reads
+    // L column q of the panel at colbuf[q * kCS + row]: the chain's multipliers and what the
+    // update wave reads (in MFMA operand layout)
     double* colbuf = xch;
-    // dummy target of the masked band stores: outside colbuf when the update wave reads colbuf
-    double* dummy = LORB_CHOL_EARLY >= 2 ? xch + 16 * kCS + lane : xch + lane * 17 + 16;
+    // dummy target of the masked band stores (outside colbuf)
+    double* dummy = xch + 16 * kCS + lane;
 #ifdef LORB_CHOL_PHASES
     unsigned long long ph_w = 0, ph_c = 0, ph_s = 0, tq = __builtin_amdgcn_s_memtime();
 #define CH_PH(v) do { const unsigned long long q_ = __builtin_amdgcn_s_memtime(); v += q_ - tq; tq = q_; } while (0)
@@ -1427,17 +1398,15 @@ struct BandSide {
         wait_ge<false>(prd, ++pwant);
 #pragma unroll
         for (int q = 0; q < NB; ++q) P[q] = pb[lane * 17 + q];  // lanes < q: upper garbage, never used
-        // pb consumed (the release orders the reads above before the post)
-        if (LORB_CHOL_EARLY >= 3 && lane == 0) __hip_atomic_fetch_add(hrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       CH_PH(ph_w);
       tr(0);
       const double zin = kb + 16 + lane < rows ? z[kb + 16 + lane] : 0.0;
       double yq = 0.0;
-#if LORB_CHOL_SP
-      // software-pipelined columns: column q-1's updates of the later columns (multipliers loaded
-      // from colbuf at the end of iteration q-1) are issued inside column q's pivot chain, which
-      // no longer waits on LDS.  Every P[q2] still receives its FMAs in column order (same bits).
+      // Software-pipelined columns: column q-1's updates of the later columns (multipliers loaded
+      // from colbuf at the end of iteration q-1) are issued inside column q's pivot chain, behind
+      // a scheduling barrier after the first Newton step of its rsqrt, so the chain no longer
+      // waits on LDS.  Every P[q2] still receives its FMAs in column order (same bits).
       double mp[NB];
 #pragma unroll
       for (int q2 = 0; q2 < NB; ++q2) mp[q2] = 0.0;
@@ -1450,7 +1419,7 @@ struct BandSide {
           const double e = fma(-akk * y, y, 1.0);
           y = fma(0.5 * y, e, y);
         }
-        if (LORB_CHOL_SP >= 2) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
         if (q >= 1) {
 #pragma unroll
           for (int q2 = q + 1; q2 < NB; ++q2) P[q2] = fma(-P[q - 1], mp[q2], P[q2]);
@@ -1472,80 +1441,12 @@ struct BandSide {
           for (int q2 = q + 2; q2 < NB; ++q2) mp[q2] = colbuf[q * kCS + q2];
         }
       }
-#elif LORB_CHOL_G4
-      // columns in groups of four: inside a group the multipliers come by v_readlane (no LDS
-      // wait on the pivot chain), then one rank-4 update of the panel's later columns with
-      // multipliers broadcast from colbuf.  Every P[q2] receives the same FMAs in the same
-      // (column) order as the column-by-column loop, so the bits are the same.
-#pragma unroll
-      for (int g0 = 0; g0 < NB; g0 += 4) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int q = g0 + j;
-          const double akk = readlane_d(P[q], q);
-          bad |= !(akk > 0.0);
-          const double y = rsqrt_refined(akk);
-          P[q] *= y;
-          yq = lane == q ? y : yq;
-          const double zk = readlane_d(zr, q) * y;
-          zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
-          colbuf[q * kCS + lane] = P[q];
-#pragma unroll
-          for (int i = j + 1; i < 4; ++i) {
-            const double l = readlane_d(P[q], g0 + i);
-            P[g0 + i] = fma(-P[q], l, P[g0 + i]);
-          }
-        }
-#pragma unroll
-        for (int q2 = g0 + 4; q2 < NB; ++q2)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) P[q2] = fma(-P[g0 + j], colbuf[(g0 + j) * kCS + q2], P[q2]);
-      }
-#else
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const double akk = readlane_d(P[q], q);
-        bad |= !(akk > 0.0);
-        const double y = rsqrt_refined(akk);
-        P[q] *= y;  // lane q: akk * y = L(k, k)
-        yq = lane == q ? y : yq;
-        const double zk = readlane_d(zr, q) * y;
-        zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
-        if (q + 1 < NB) {
-          colbuf[q * kCS + lane] = P[q];
-          const double l1 = readlane_d(P[q], q + 1);
-          P[q + 1] = fma(-P[q], l1, P[q + 1]);
-#pragma unroll
-          for (int q2 = q + 2; q2 < NB; ++q2) P[q2] = fma(-P[q], colbuf[q * kCS + q2], P[q2]);
-        } else if (LORB_CHOL_EARLY >= 2) {
-          colbuf[q * kCS + lane] = P[q];
-        }
-      }
-#endif
       CH_PH(ph_c);
       tr(1);
       const bool rowvalid = kb + lane < rows;
-#if LORB_CHOL_EARLY >= 2
       // the update wave reads L from colbuf: post it now, then store L to the band (for the
       // diagonal-block inverses and the back-substitution) while the update runs
       if (lane == 0) __hip_atomic_fetch_add(lrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if LORB_CHOL_EARLY >= 3
-      // tile (3, 1) of the next panel column: pre-update copy from pb, this panel's L from colbuf
-      const bool nxt = kb + 16 < kend;
-      v4d C31 = {0.0, 0.0, 0.0, 0.0};
-      double o1[4], o3[4];
-      const int ci = lane & 15, ck = lane >> 4;
-      if (nxt) {
-        wait_ge<false>(ppr, ++ppwant);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) C31[r] = pb[(32 + ck + 4 * r) * 17 + ci];
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          o1[kk] = colbuf[(4 * kk + ck) * kCS + 16 + ci];
-          o3[kk] = colbuf[(4 * kk + ck) * kCS + 48 + ci];
-        }
-      }
-#endif
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
         const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
@@ -1554,44 +1455,6 @@ struct BandSide {
       l_base += dstep;
       if (lane < NB) z[kb + lane] = zr;
       if (lane == 0 && pdone) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if LORB_CHOL_EARLY >= 3
-      if (nxt) {
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) C31 = __builtin_amdgcn_mfma_f64_16x16x4f64(-o3[kk], o1[kk], C31, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pb[(32 + ck + 4 * r) * 17 + ci] = C31[r];
-      }
-#endif
-#elif LORB_CHOL_EARLY
-      wave_sync_lds();  // colbuf reads done before xch is rewritten
-      // the update wave needs only xch: post it first, then store L to the band (for the
-      // diagonal-block inverses and the back-substitution) while the update runs
-#pragma unroll
-      for (int q = 0; q < NB; ++q) xch[lane * 17 + q] = P[q];
-      if (lane == 0) __hip_atomic_fetch_add(lrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
-        *(ok ? A + l_base + q * sj : dummy) = q == lane ? yq : P[q];
-      }
-      l_base += dstep;
-      if (lane < NB) z[kb + lane] = zr;
-      if (lane == 0 && pdone) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-      wave_sync_lds();  // colbuf reads done before xch is rewritten
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
-        *(ok ? A + l_base + q * sj : dummy) = q == lane ? yq : P[q];
-        xch[lane * 17 + q] = P[q];
-      }
-      l_base += dstep;
-      if (lane < NB) z[kb + lane] = zr;
-      if (lane == 0) {  // the release orders the whole wave's stores above
-        if (pdone) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(lrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-#endif
       const double zs = __shfl_down(zr, 16, 64);
       zr = lane < 48 ? zs : zin;
       CH_PH(ph_s);
@@ -1606,7 +1469,7 @@ struct BandSide {
   //   update(): T = the window at kb0 (column 0 unused); on return the window at kend (all ten
   //   tiles).  lwant counts the L posts consumed so far.
   __device__ __forceinline__ void update(v4d (&T)[10], int kb0, int kend, int* lrd, int* prd, int& lwant,
-                                         double* pb, int& hgive) const {
+                                         double* pb) const {
     const int ci = lane & 15, ck = lane >> 4;
     const int dstep = 16 * (si + sj);
     int tn_addr = idx(kb0 + 64 + ck, kb0 + 16 + ci);  // entering tile (J, r) adds 4 r si + 16 J sj (below)
@@ -1639,18 +1502,6 @@ struct BandSide {
         }
       tn_addr += dstep;
       const bool nxt = kb + 16 < kend;
-#if LORB_CHOL_EARLY >= 3
-      if (nxt) {  // the pre-update tile (3, 1) and the entering rows, before this panel's L
-        wait_ge<true>(hrd, hgive);  // the chain has read the previous hand-over
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pb[(32 + ck + 4 * r) * 17 + ci] = T[tri4(3, 1)][r];
-          pb[(48 + ck + 4 * r) * 17 + ci] = Tn[0][r];
-        }
-        ++hgive;
-        if (lane == 0) __hip_atomic_fetch_add(ppr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-#endif
       tr(0);
       wait_ge<true>(lrd, ++lwant);
       tr(1);
@@ -1659,28 +1510,21 @@ struct BandSide {
       for (int I = 1; I < 4; ++I)
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk)
-          opA[I][kk] = LORB_CHOL_EARLY >= 2 ? xch[(4 * kk + ck) * kCS + 16 * I + ci] : xch[(16 * I + ci) * 17 + 4 * kk + ck];
-      // the next panel's column first, then hand it over (EARLY >= 3: tile (3, 1) is the chain's)
-      constexpr int IH = LORB_CHOL_EARLY >= 3 ? 3 : 4;
+          opA[I][kk] = xch[(4 * kk + ck) * kCS + 16 * I + ci];  // L(kb + 16 I + ci, kb + 4 kk + ck)
+      // the next panel's column first, then hand it over
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-        for (int I = 1; I < IH; ++I)
+        for (int I = 1; I < 4; ++I)
           T[tri4(I, 1)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[1][kk], T[tri4(I, 1)], 0, 0, 0);
       if (nxt) {
 #pragma unroll
-        for (int I = 1; I < IH; ++I)
+        for (int I = 1; I < 4; ++I)
 #pragma unroll
           for (int r = 0; r < 4; ++r) pb[(16 * (I - 1) + ck + 4 * r) * 17 + ci] = T[tri4(I, 1)][r];
-        if (LORB_CHOL_EARLY < 3) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) pb[(48 + ck + 4 * r) * 17 + ci] = Tn[0][r];
-        }
+        for (int r = 0; r < 4; ++r) pb[(48 + ck + 4 * r) * 17 + ci] = Tn[0][r];
         if (lane == 0) __hip_atomic_fetch_add(prd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else if (LORB_CHOL_EARLY >= 3) {  // last panel of the phase: the window keeps column 1 whole
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-          T[tri4(3, 1)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[3][kk], opA[1][kk], T[tri4(3, 1)], 0, 0, 0);
       }
       tr(2);
       // k-step outer: the three tiles' accumulation chains interleave
@@ -1701,14 +1545,12 @@ struct BandSide {
     }
   }
   // The 16 x 16 diagonal block of L at view rows c0 .. c0+15 replaced in place by its inverse X
-  // (lower triangular; the diagonal slot already holds 1 / L(i, i) = X(i, i)).  Column j = lane
-  // (lanes 0..15): X(i, j) = -X(i, i) sum_{k=j}^{i-1} L(i, k) X(k, j).  Only the back-substitution
-  // reads the block afterwards.
-#if LORB_CHOL_LINV4
-  // All 64 lanes: lane = 4 j + r holds column j's rows i = 4 m + r (acc[m]).  Step k: the lane
+  // (lower triangular; the diagonal slot already holds 1 / L(i, i) = X(i, i)):
+  // X(i, j) = -X(i, i) sum_{k=j}^{i-1} L(i, k) X(k, j).  Only the back-substitution reads the
+  // block afterwards.  All 64 lanes: lane = 4 j + r holds column j's rows i = 4 m + r (acc[m]).  Step k: the lane
   // of row k (r = k & 3) forms X(k, j) and stores it, a quad broadcast hands it to the column's
   // four lanes, each adds L(i, k) X(k, j) to its rows.  The L loads (about 30 per lane) are all
-  // issued before the sweep.  Per row the FMAs run in k order as in the 16-lane sweep (same bits).
+  // issued before the sweep.  Per row the FMAs run in k order (the bits of a column sweep).
   template <int K>
   __device__ __forceinline__ void linv_step(int c0, int j, int r, double (&acc)[4], const double (&dv)[4],
                                             const double (&lv)[16][4]) const {
@@ -1744,29 +1586,6 @@ struct BandSide {
       }
     linv_sweep<0>(c0, j, r, acc, dv, lv);
   }
-#else
-  __device__ __forceinline__ void linv(int c0) const {
-    if (lane >= 16) return;
-    const int j = lane;
-    // column sweep: acc[i] collects sum_k L(i, k) X(k, j) as the X(k, j) become final; the
-    // L(i, k) loads do not depend on the chain
-    double acc[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const double dk = A[idx(c0 + k, c0 + k)];
-      const double xk = k == j ? dk : (k > j ? -dk * acc[k] : 0.0);
-      if (k > j && k - j <= bw) A[idx(c0 + k, c0 + j)] = xk;
-#pragma unroll
-      for (int i = k + 1; i < 16; ++i) {
-        const bool ok = i - k <= bw;
-        const double l = A[ok ? idx(c0 + i, c0 + k) : base];
-        acc[i] = fma(ok ? l : 0.0, xk, acc[i]);
-      }
-    }
-  }
-#endif
   // Back-substitution L^T y = z, push style: the 64 rows c0-48 .. c0+15 of the current block c0
   // live in registers (row r in lane r & 63, so sliding the window needs no shuffle).  A block
   // solves its 16 x 16 triangle -- as a v_readlane chain (c0 >= c_inv) or as one product with the
@@ -1975,7 +1794,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   __shared__ int s_pdone[2];
   __shared__ int s_lrd[2], s_prd[2];  // per side: L panels posted (chain), panel columns posted (update)
   __shared__ int s_hand[3];           // T / B -> M hand-over (below)
-  __shared__ int s_hrd[2], s_ppr[2];  // per side: hand-overs consumed, pre-update tiles posted (EARLY >= 3)
   const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
   const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
   const int nbk = n16 / 16, ib = 4;
@@ -2009,7 +1827,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     s_pdone[0] = 0; s_pdone[1] = 0;
     s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
     s_hand[0] = 0; s_hand[1] = 0; s_hand[2] = 0;
-    s_hrd[0] = 0; s_hrd[1] = 0; s_ppr[0] = 0; s_ppr[1] = 0;
     unsigned long long msk = 0;
     for (int b = 0; b < nbk; ++b) msk |= (unsigned long long)(!prog || b < ib || b >= nbk - ib) << (b & 63);
     s_mask = msk;
@@ -2018,7 +1835,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   BandSide top{Ab, zt, xt, rt, bw, lane, bw, bw, 1};
   BandSide bot{Ab, zb, xb, rb, bw, lane, (n16 - 1) * B1 + bw, -1, -bw};
   top.pdone = &s_pdone[0]; bot.pdone = &s_pdone[1];
-  top.hrd = &s_hrd[0]; bot.hrd = &s_hrd[1]; top.ppr = &s_ppr[0]; bot.ppr = &s_ppr[1];
   top.zslot = (int)(zero - Ab); bot.zslot = top.zslot;
   top.nbk = bot.nbk = nbk; top.dir = 1; bot.dir = -1;
   if (prog) { top.mask = &s_mask; bot.mask = &s_mask; }
@@ -2038,7 +1854,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   double* pb = side == 0 ? pbt : pbb;
   int* lrd = &s_lrd[side];
   int* prd = &s_prd[side];
-  int lwant = 0, pwant = 0, ppwant = 0, hgive = 0;
+  int lwant = 0, pwant = 0;
   bool bad = false;
   double zr = 0.0;
   double P[NB];
@@ -2062,9 +1878,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     }
     TR1(8 + side);
   }
-  // diagonal-block inverses: waves 4 / 5 share SIMDs with the chain waves; LORB_CHOL_LINV6 moves
-  // them to waves 6 / 7 after their staging (SIMDs of the MFMA-paced update waves)
-  if (LORB_CHOL_LINV6 ? wv >= 6 : (wv == 4 || wv == 5)) {
+  // diagonal-block inverses (waves 4 / 5)
+  if (wv == 4 || wv == 5) {
     int* pd = &s_pdone[side];
     const int nblk = (side == 0 ? m : nB) / 16;
     for (int p = 0; p < nblk; ++p) {
@@ -2080,10 +1895,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     unsigned long long* phv = d.dbg + 8 * w;  // wave 0, T phase: [0] wait [1] factor [2] store
     if (wv == 0) { if (lane == 0) { phv[0] = phv[1] = phv[2] = 0; } const_cast<BandSide&>(me).phases = phv; }
 #endif
-    me.chain(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, pwant, pb, ppwant);
+    me.chain(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, pwant, pb);
   } else if (wv < 4) {
     me.init_tiles(T);
-    me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb, hgive);
+    me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb);
   }
   if (wv < 6) C2_STAMP(wv);
   // Hand-over to the M phase by flags, not barriers (the diagonal-block inverses of waves 4 / 5
@@ -2137,7 +1952,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
     topM.mask = nullptr; topM.pdone = nullptr;
     {  // M's first panel column to the chain wave
       const int ci = lane & 15, ck = lane >> 4;
-      if (LORB_CHOL_EARLY >= 3) { wait_ge<true>(&s_hrd[0], hgive); ++hgive; }
 #pragma unroll
       for (int I = 0; I < 4; ++I)
 #pragma unroll
@@ -2145,13 +1959,13 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
       if (lane == 0) __hip_atomic_fetch_add(&s_prd[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     TR1(15);
-    topM.update(T, m, m + 48, &s_lrd[0], &s_prd[0], lwant, pbt, hgive);
+    topM.update(T, m, m + 48, &s_lrd[0], &s_prd[0], lwant, pbt);
   } else if (wv == 0) {
     zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
     BandSide topM = top;
     topM.mask = nullptr; topM.pdone = nullptr;
     TR1(3);
-    topM.chain(P, zr, bad, m, m + 48, false, &s_lrd[0], &s_prd[0], pwant, pbt, ppwant);
+    topM.chain(P, zr, bad, m, m + 48, false, &s_lrd[0], &s_prd[0], pwant, pbt);
     TR1(4);
     if (bad) s_bad = 1;
     C2_STAMP(6);
