@@ -2165,6 +2165,7 @@ __device__ int lm_decide(BaDev d, const LMOpt& o, int w, WinState S, bool valid,
       S.radius = S.radius / S.decrease_factor;
       S.decrease_factor *= 2.0;
       S.last_successful = 0;
+      if (S.iter >= o.max_iter) { S.done = 1; S.term = LORB_TERM_NO_CONVERGENCE; }
     }
     d.st[w] = S;
     return 0;
@@ -2183,6 +2184,7 @@ __device__ int lm_decide(BaDev d, const LMOpt& o, int w, WinState S, bool valid,
   if (rel > o.min_rel) {
     S.cur ^= 1;
     S.relin = 1;
+    S.cost = new_cost;  // the accepted point's cost (k_ba_lm_begin recomputes it when relinearising)
     S.n_success++;
     const double tt = 2.0 * rel - 1.0;
     S.radius = S.radius / fmax(1.0 / 3.0, 1.0 - tt * tt * tt);
@@ -2193,6 +2195,9 @@ __device__ int lm_decide(BaDev d, const LMOpt& o, int w, WinState S, bool valid,
     S.radius = S.radius / S.decrease_factor;
     S.decrease_factor *= 2.0;
   }
+  // the head of the next iteration would stop here (iteration budget spent): the solve needs no
+  // final linearisation, S.cost is the cost at the final point
+  if (S.iter >= o.max_iter) { S.done = 1; S.term = LORB_TERM_NO_CONVERGENCE; }
   d.st[w] = S;
   return rel > o.min_rel;
 }
@@ -2944,13 +2949,8 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   return LORB_OK;
 }
 
-int enqueue_finalize(lorb_ba_plan* P, const LMOpt& o) {
-  LORB_TRY(enqueue_linearize(P, o));
-  LORB_CHECK_LAUNCH(P->ctx);
-  return LORB_OK;
-}
-
-// the whole solve: x <- initial values, max_iter LM iterations, the final linearisation
+// the whole solve: x <- initial values, max_iter LM iterations (k_ba_lm_end closes the solve when
+// the budget is spent: no final linearisation)
 int enqueue_solve(lorb_ba_plan* P, const LMOpt& o) {
   lorb_ctx* ctx = P->ctx;
   {
@@ -2959,8 +2959,10 @@ int enqueue_solve(lorb_ba_plan* P, const LMOpt& o) {
                        P->Ctot, P->pt_launch, o);
   }
   LORB_CHECK_LAUNCH(ctx);
+  // no iterations: one linearisation (cost, termination) as the head of a first iteration
+  if (o.max_iter <= 0) return enqueue_linearize(P, o);
   for (int it = 0; it < o.max_iter; ++it) LORB_TRY(enqueue_iteration(P, o));
-  return enqueue_finalize(P, o);
+  return LORB_OK;
 }
 
 int plan_solve(lorb_ba_plan* P, const lorb_lm_options* opt) {
