@@ -3451,11 +3451,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&b.pinned), sizeof(int) * nrb));
     b.pinned_n = nrb;
   }
-  LORB_HIP(ctx, hipMemcpyAsync(b.pinned, b.hdr, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
-  if (C > 0) {
-    LORB_HIP(ctx, hipMemcpyAsync(b.pinned + 8, b.cam_cnt, sizeof(int) * C, hipMemcpyDeviceToHost, s));
-    LORB_HIP(ctx, hipMemcpyAsync(b.pinned + 8 + C, b.cov, sizeof(int) * C * C, hipMemcpyDeviceToHost, s));
-  }
+  // hdr | cov | cam_cnt are contiguous in the scratch: one copy
+  LORB_HIP(ctx, hipMemcpyAsync(b.pinned, b.hdr, sizeof(int) * nrb, hipMemcpyDeviceToHost, s));
   LORB_HIP(ctx, hipStreamSynchronize(s));
   const int* H = b.pinned;
   const int K = H[0], maxk = H[1], err = H[2], Pn = H[3];
@@ -3463,8 +3460,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   if (err & 2) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a frame index >= n_poses");
   if (err & 4) return lorb::set_error(ctx, LORB_E_INVALID, "a point observed twice by one camera");
   if (Pn < 0 || Pn > b.P_cap) return lorb::set_error(ctx, LORB_E_INVALID, "n_points %d outside [0, %d]", Pn, b.P_cap);
-  const int* cam_cnt = H + 8;
-  const int* cov = H + 8 + C;
+  const int* cov = H + 8;
+  const int* cam_cnt = H + 8 + (size_t)C * C;
   // 3. host: camera order, blocks, band, groups
   std::vector<char> adj((size_t)C * C, 0);
   for (int i = 0; i < C; ++i)

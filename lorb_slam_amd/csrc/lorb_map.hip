@@ -72,7 +72,7 @@ __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Po
   }
   if (t == 0) {
     s_ok = (P0 + n_new <= m.P_cap) && (K0 + n_obs <= m.K_cap);
-    if (!s_ok) m.cnt[2] |= 1;
+    m.cnt[2] = s_ok ? 0 : 1;  // this step's capacity flag (no separate clear)
   }
   __syncthreads();
   if (!s_ok) return;
@@ -146,7 +146,9 @@ __device__ __forceinline__ int new_pos(const MapDev& m, int ntP, int i) {
 // stable gathers into the alternate buffers; observation slots as lorb_ba_window_dev wants them
 __global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, int t0, int ntP) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < Pb && m.flag_pt[i]) {
+  const int fp = i < Pb ? m.flag_pt[i] : 0;
+  if (fp) {
+    m.flag_pt[i] = 0;  // cleared for the next slide (only this thread reads it here)
     const int d = new_id(m, i);
     m.pos2[3 * d + 0] = m.pos[3 * i + 0];
     m.pos2[3 * d + 1] = m.pos[3 * i + 1];
@@ -244,6 +246,8 @@ int map_alloc(lorb_map* M, const lorb_map_init* in) {
   LORB_TRY(malloc_n(M, K, &m.obs_frame));
   LORB_TRY(malloc_n(M, (size_t)8, &m.cnt));
   LORB_TRY(malloc_n(M, P + 1, &m.flag_pt)); LORB_TRY(malloc_n(M, P + 1, &m.newid));
+  // point flags start clear and are cleared again by the compaction that consumes them
+  LORB_HIP(M->ctx, hipMemsetAsync(m.flag_pt, 0, sizeof(int) * ((size_t)P + 1), M->ctx->stream));
   LORB_TRY(malloc_n(M, K + 1, &m.flag_obs)); LORB_TRY(malloc_n(M, K + 1, &m.newpos));
   LORB_TRY(malloc_n(M, (P + 1 + K + 1) / lorb::kScanTile + 2, &m.tile_tot));
   LORB_TRY(malloc_n(M, 6 * (size_t)m.R, &m.ring));
@@ -274,7 +278,6 @@ int map_slide(lorb_map* M, int t0, int Pb, int Kb) {
   lorb_ctx* ctx = M->ctx;
   hipStream_t s = ctx->stream;
   MapDev& m = M->m;
-  LORB_HIP(ctx, hipMemsetAsync(m.flag_pt, 0, sizeof(int) * ((size_t)Pb + 1), s));
   if (Kb > 0) hipLaunchKernelGGL(k_map_mark, dim3(lorb::ceil_div(Kb, 256)), dim3(256), 0, s, m, Kb, t0);
   hipLaunchKernelGGL(k_map_obs_flag, dim3(lorb::ceil_div(Kb + 1, 256)), dim3(256), 0, s, m, Kb, t0);
   const int ntP = lorb::ceil_div(Pb + 1, lorb::kScanTile), ntK = lorb::ceil_div(Kb + 1, lorb::kScanTile);
@@ -392,7 +395,6 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   // 3. AddObservation / new points, keyframe pose into the ring
   Pose6 p6;
   for (int q = 0; q < 6; ++q) p6.v[q] = pose[q];
-  LORB_HIP(ctx, hipMemsetAsync(m.cnt + 2, 0, sizeof(int), s));
   hipLaunchKernelGGL(k_map_append, dim3(1), dim3(1024), 0, s, m, n, kf, p6, M->mt, M->xyz, d_desc, d_x, d_y, d_depth);
   LORB_CHECK_LAUNCH(ctx);
   LORB_TRY(mark(2));
