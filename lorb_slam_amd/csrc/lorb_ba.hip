@@ -3453,7 +3453,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   }
   // hdr | cov | cam_cnt are contiguous in the scratch: one copy
   LORB_HIP(ctx, hipMemcpyAsync(b.pinned, b.hdr, sizeof(int) * nrb, hipMemcpyDeviceToHost, s));
-  LORB_HIP(ctx, hipStreamSynchronize(s));
+  LORB_HIP(ctx, lorb::spin_sync(ctx));
   const int* H = b.pinned;
   const int K = H[0], maxk = H[1], err = H[2], Pn = H[3];
   if (err & 1) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a point index outside [0, n_points)");

@@ -33,7 +33,22 @@ struct lorb_ctx {
   // pinned host staging
   void* pinned = nullptr;
   size_t pinned_sz = 0;
+  // spin_sync's event (no timing)
+  hipEvent_t spin_ev = nullptr;
 };
+
+namespace lorb {
+// Wait for the stream by polling an event from the host instead of a blocking synchronize: the
+// device plan build's one readback sits on the step's critical path, and a blocked host thread
+// wakes up tens of microseconds after the copy lands.
+inline hipError_t spin_sync(lorb_ctx* ctx) {
+  hipError_t e = hipEventRecord(ctx->spin_ev, ctx->stream);
+  if (e != hipSuccess) return e;
+  while ((e = hipEventQuery(ctx->spin_ev)) == hipErrorNotReady) {
+  }
+  return e;
+}
+}  // namespace lorb
 
 // multi-GPU communicator (lorb_comm.hip): RCCL over xGMI, or a host callback transport
 struct lorb_comm {

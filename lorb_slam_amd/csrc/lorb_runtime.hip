@@ -92,6 +92,7 @@ int lorb_create(int device, lorb_ctx** out) {
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   for (int i = 0; i < 64 && e == hipSuccess; i++) e = hipEventCreate(&ctx->ev[i]);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->spin_ev, hipEventDisableTiming);
   if (e != hipSuccess) {
     delete ctx;
     return LORB_E_DEVICE;
@@ -109,6 +110,7 @@ int lorb_destroy(lorb_ctx* ctx) {
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   for (int i = 0; i < 64; i++)
     if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
+  if (ctx->spin_ev) (void)hipEventDestroy(ctx->spin_ev);
   for (int k = 0; k < LORB_K_COUNT; k++)
     for (auto& pr : ctx->kev[k]) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto e : ctx->kev_pool) (void)hipEventDestroy(e);
