@@ -265,8 +265,8 @@ __device__ __forceinline__ void block_red3(double& a, double& b, double& c, doub
   for (int k = 1; k < kGW; ++k) { a += red[0][k]; b = M1 ? fmax(b, red[1][k]) : b + red[1][k]; c += red[2][k]; }
 }
 
-// Point-block prep shared by k_ba_lin (iterations that relinearise) and k_ba_point_prep (the
-// iterations after a rejected step, where only the radius changed): the point's scaled
+// Point-block prep of k_ba_lin (from on-chip values when it relinearises, from the stored
+// linearisation after a rejected step, where only the radius changed): the point's scaled
 // E^T E + D^2 inverted, and per optimised observation Jps (scaled Jp), Q = Jps E^-1, g = Q b.
 // Returns false when the 3x3 block is not invertible (Ei = 0).
 __device__ __forceinline__ bool prep_point(const double (&Eu)[6], const double (&bu)[3], const double (&sp)[3],
@@ -309,11 +309,57 @@ __device__ __forceinline__ void prep_obs(const BaDev& d, int m, const double (&J
   d.obs_g[2 * m + 1] = Q[3] * b[0] + Q[4] * b[1] + Q[5] * b[2];
 }
 
+// Point-group Schur prep after a rejected step (only the radius changed since the last
+// linearisation): scaled E^T E + D^2 -> inverse (point phase), then per optimised observation
+// Jps, Q = Jps E^-1 and g = Q b (observation phase).  Runs inside k_ba_lin, whose relinearising
+// iterations do the same prep from on-chip values; sh[t] holds Ei (0..5) and b (6..8).
+__device__ __forceinline__ void prep_after_reject(const BaDev& d, const LMOpt& o, const PBlk& g, int t, double rad,
+                                                  double (*sh)[9], double (*ssp)[3]) {
+  const int pf = g.p0 + min(t, max(g.cnt - 1, 0));
+  double sp[3] = {0, 0, 0}, b[3] = {0, 0, 0}, Eu[6] = {0, 0, 0, 0, 0, 0};
+  if (g.cnt > 0) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * pf + k]; b[k] = d.etb[3 * pf + k]; }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Eu[k] = d.ete[6 * pf + k];
+  }
+  const int ef = g.o0 + min(t, max(g.no - 1, 0));
+  int m_f = -1, pt_f = 0;
+  double Jp_f[6] = {0, 0, 0, 0, 0, 0};
+  if (g.no > 0) {
+    m_f = d.obs_cm[ef]; pt_f = d.obs_pt[ef];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Jp_f[k] = d.obs_Jp[6 * ef + k];
+  }
+  if (t < g.cnt) {
+    const int p = g.p0 + t;
+    double Ei[6], bs[3];
+    if (!prep_point(Eu, b, sp, rad, o, Ei, bs)) prep_fail(d, g.win);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { d.pinv[6 * p + k] = Ei[k]; sh[t][k] = Ei[k]; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { sh[t][6 + k] = bs[k]; ssp[t][k] = sp[k]; }
+  }
+  __syncthreads();
+  for (int c0 = t; c0 < g.no; c0 += kGB) {
+    const int e = g.o0 + c0;
+    const bool first = c0 == t;
+    const int m = first ? m_f : d.obs_cm[e];
+    if (m < 0) continue;
+    const int lp = (first ? pt_f : d.obs_pt[e]) - g.p0;
+    double Jp[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Jp[k] = first ? Jp_f[k] : d.obs_Jp[6 * e + k];
+    prep_obs(d, m, Jp, sh[lp], sh[lp] + 6, ssp[lp]);
+  }
+}
+
 // K1: linearisation of a point group (windows that (re)linearise this iteration): per
 // observation residual + Jacobians, per point E^T E / E^T r (unscaled), Jacobi scale
 // (iteration 0), gradient-max / point-norm / cost partials, and the point-block prep of this
 // iteration (prep_point / prep_obs at the current radius: the radius only changes in
-// k_ba_lm_end), so the observations' Jp and the point's E, b never make an HBM round trip.
+// k_ba_lm_end), so the observations' Jp and the point's E, b never make an HBM round trip.  After
+// a rejected step it only redoes the prep at the new radius (prep_after_reject).
 __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d, LMOpt o) {
   __shared__ double sh[kGB][9];   // observation terms; then the points' Ei (6) and b (3)
   __shared__ double ssp[kGB][3];
@@ -327,7 +373,11 @@ __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d, LMOpt o) {
   int po0 = 0, po1 = 0;
   if (t < g.cnt) { po0 = d.pt_obs_off[g.p0 + t]; po1 = d.pt_obs_off[g.p0 + t + 1]; }
   const WinState& S = d.st[g.win];
-  if (S.done || !S.relin) return;
+  if (S.done) return;
+  if (!S.relin) {  // after a rejected step: the prep at the new radius only
+    prep_after_reject(d, o, g, t, S.radius, sh, ssp);
+    return;
+  }
   const BaWin& W = d.win[g.win];
   const int cur = S.cur;
   const double rad = S.radius;
@@ -578,63 +628,6 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
     else if (S.radius <= o.min_radius) { S.done = 1; S.term = LORB_TERM_MIN_RADIUS; }
     else S.iter++;
     d.st[w] = S;
-  }
-}
-
-// K4: point-group Schur prep after a rejected step (only the radius changed since k_ba_lin's
-// prep): scaled E^T E + D^2 -> inverse (point phase), then per optimised observation Jps, Q =
-// Jps E^-1 and g = Q b (observation phase).  Iterations that relinearised (last_successful, set
-// by k_ba_lm_begin) were prepared by k_ba_lin.
-__global__ __launch_bounds__(kGB) void k_ba_point_prep(BaDev d, LMOpt o) {
-  __shared__ double sEi[kGB][6], sb[kGB][3], ssp[kGB][3];
-  if ((int)blockIdx.x >= d.live[0]) return;
-  const PBlk g = d.pblk[blockIdx.x];
-  const int t = threadIdx.x;
-  // most iterations relinearise (k_ba_lin did the prep): test the state before any other load
-  {
-    const WinState& S0 = d.st[g.win];
-    if (S0.done || S0.last_successful) return;
-  }
-  // the point's terms go out together with the window state
-  const int pf = g.p0 + min(t, max(g.cnt - 1, 0));
-  double sp[3] = {0, 0, 0}, b[3] = {0, 0, 0}, Eu[6] = {0, 0, 0, 0, 0, 0};
-  if (g.cnt > 0) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * pf + k]; b[k] = d.etb[3 * pf + k]; }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Eu[k] = d.ete[6 * pf + k];
-  }
-  // ... and so do the first chunk's observation terms (used after the point phase)
-  const int ef = g.o0 + min(t, max(g.no - 1, 0));
-  int m_f = -1, pt_f = 0;
-  double Jp_f[6] = {0, 0, 0, 0, 0, 0};
-  if (g.no > 0) {
-    m_f = d.obs_cm[ef]; pt_f = d.obs_pt[ef];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Jp_f[k] = d.obs_Jp[6 * ef + k];
-  }
-  const WinState& S = d.st[g.win];
-  if (S.done || S.last_successful) return;
-  if (t < g.cnt) {
-    const int p = g.p0 + t;
-    double Ei[6], bs[3];
-    if (!prep_point(Eu, b, sp, S.radius, o, Ei, bs)) prep_fail(d, g.win);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { d.pinv[6 * p + k] = Ei[k]; sEi[t][k] = Ei[k]; }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { sb[t][k] = bs[k]; ssp[t][k] = sp[k]; }
-  }
-  __syncthreads();
-  for (int c0 = t; c0 < g.no; c0 += kGB) {
-    const int e = g.o0 + c0;
-    const bool first = c0 == t;
-    const int m = first ? m_f : d.obs_cm[e];
-    if (m < 0) continue;
-    const int lp = (first ? pt_f : d.obs_pt[e]) - g.p0;
-    double Jp[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Jp[k] = first ? Jp_f[k] : d.obs_Jp[6 * e + k];
-    prep_obs(d, m, Jp, sEi[lp], sb[lp], ssp[lp]);
   }
 }
 
@@ -2905,7 +2898,6 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = ctx->stream;
   const BaDev& d = P->dev;
   LORB_TRY(enqueue_linearize(P, o));
-  if (P->grid_pblk) hipLaunchKernelGGL(k_ba_point_prep, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
   // The LDS Cholesky never writes env, and k_ba_schur rewrites every stored entry of every
   // block each iteration, so the band's structural zeros (set at plan creation) persist; the
   // in-place global variant needs them restored.
