@@ -509,6 +509,48 @@ def sub_c2(ctx, D, args):
             "cpu_baseline": cpu, "check": chk}
 
 
+def sub_dropin(ctx, D, args):
+    """The drop-in BA::LocalPoseOptimization call (include/lorb/adapters.hpp -> lorb_ba_solver_solve):
+    a C4 window (50 KF + 5 fixed, 10,000 points, ~77 k observations) in the reference's camera order
+    ([curr] + covisible by ascending weight, src/bundle_adjust.cpp:210-220), handed over as HOST arrays
+    every call, 10 LM iterations, double results back on the host.  Each call = pack + one H2D copy +
+    device plan build + LM graph + one D2H copy, synchronous, timed end to end on the host clock."""
+    from lorb_slam_amd import _abi as A
+    from lorb_slam_amd import synth
+    from lorb_slam_amd.runtime import BASolver
+    w0 = synth.ba_window(seed=4 + 1009 * D.rank, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400)
+    w, _ = synth.reference_window_order(w0)
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    s = BASolver(ctx)
+    prep = s.prepare(w)
+    t0 = time.perf_counter()
+    s.solve_prepared(prep, opt)  # first call: plan creation + graph capture
+    first_ms = (time.perf_counter() - t0) * 1e3
+    for _ in range(max(2, args.warmup)):
+        s.solve_prepared(prep, opt)
+    steps = max(10, args.steps)
+    D.barrier()
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        s.solve_prepared(prep, opt)
+        ts.append(time.perf_counter() - t0)
+    D.barrier()
+    _, _, summ = s.solve_prepared(prep, opt)
+    info = s.info()
+    s.close()
+    mean = D.reduce(sum(ts) / steps, "MAX")
+    med = D.reduce(float(np.median(ts)), "MAX")
+    return {"workload": "dropin_local_ba_c4", "unit": "ms per call", "ms_per_call": mean * 1e3,
+            "ms_per_call_median": med * 1e3, "first_call_ms": first_ms, "calls": steps,
+            "lm_iterations_per_sec": 10.0 / mean,
+            "config": {"kf": 50, "fixed_kf": 5, "points": len(w["point_init"]), "observations": len(w["obs_point"]),
+                       "camera_order": "reference ([curr] + covisible by ascending weight)", "lm_iterations": 10,
+                       "call": "lorb_ba_solver_solve: host arrays in, double results out (the adapter's C-ABI call)"},
+            "solver": info, "final_cost": summ["final_cost"], "iterations": summ["iterations"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -521,6 +563,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 sub-record of the default run")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in LocalPoseOptimization sub-record")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -559,6 +602,7 @@ def main():
     total_matches = D.reduce(wl["matches"] * args.steps, "SUM")
     cpu = wl["cpu"]() if (D.rank == 0 and not args.no_cpu_baseline and D.world == 1 and wl["cpu"]) else None
     c2 = sub_c2(ctx, D, args) if (args.workload == "c4" and not args.no_c2) else None
+    dropin = sub_dropin(ctx, D, args) if (args.workload == "c4" and not args.no_dropin) else None
     if D.rank == 0:
         if args.workload in ("c4", "shared"):
             value, unit = total_iters / elapsed, "BA iterations/s"
@@ -576,7 +620,8 @@ def main():
             "config": dict(wl["config"], parallelism=par),
             "matches_per_sec": total_matches / elapsed, "plan_build_ms": wl["plan_ms"],
             "map_create_ms": wl.get("create_ms"),
-            "roofline": roofline_entry(kt, wl, pn), "cpu_baseline": cpu, "c2": c2, "check": check,
+            "roofline": roofline_entry(kt, wl, pn), "cpu_baseline": cpu, "c2": c2, "dropin_local_ba": dropin,
+            "check": check,
         }
         if rehearse:
             out["rehearsal"] = "no GPU: launcher + gloo path only; value is not a hot-path measurement"

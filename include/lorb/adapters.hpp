@@ -45,6 +45,23 @@ inline lorb_ctx* thread_ctx(int device = 0) {
   return h.ctx;
 }
 
+// The calling thread's BA solver (device-built plans resident across LocalPoseOptimization calls).
+// Created after the thread's ctx, so it is destroyed before it.
+inline lorb_ba_solver* thread_ba_solver(lorb_ctx* ctx) {
+  struct Holder {
+    lorb_ba_solver* s = nullptr;
+    lorb_ctx* ctx = nullptr;
+    ~Holder() { if (s) lorb_ba_solver_destroy(s); }
+  };
+  thread_local Holder h;
+  if (h.s && h.ctx != ctx) { lorb_ba_solver_destroy(h.s); h.s = nullptr; }
+  if (!h.s) {
+    if (lorb_ba_solver_create(ctx, &h.s) != LORB_OK) throw Error("lorb_ba_solver_create failed");
+    h.ctx = ctx;
+  }
+  return h.s;
+}
+
 inline void check(lorb_ctx* ctx, int rc, const char* what) {
   if (rc != LORB_OK) throw Error(std::string(what) + " failed: " + lorb_last_error(ctx));
 }
@@ -339,7 +356,9 @@ void LocalPoseOptimization(lorb_ctx* ctx, FrameT* cur) {
   double* pp = po.data();
   double* qq = pt.data();
   lorb_ba_summary s;
-  check(ctx, lorb_ba_local(ctx, 1, &w, &opt, &pp, &qq, &s), "lorb_ba_local");
+  // the thread's solver: the window's device-built plan stays resident between calls (no per-call
+  // plan construction; lorb_c.h lorb_ba_solver_solve)
+  check(ctx, lorb_ba_solver_solve(thread_ba_solver(ctx), &w, &opt, pp, qq, &s), "lorb_ba_solver_solve");
   for (size_t i = 0; i < frames.size(); ++i) {  // float write-back, :317-329
     const float R[3] = {(float)po[6 * i], (float)po[6 * i + 1], (float)po[6 * i + 2]};
     const float T[3] = {(float)po[6 * i + 3], (float)po[6 * i + 4], (float)po[6 * i + 5]};

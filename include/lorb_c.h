@@ -483,6 +483,24 @@ typedef struct lorb_ba_window_dev {
 int lorb_ba_plan_create_dev(lorb_ctx* ctx, const lorb_ba_window_dev* win, lorb_ba_plan** out);
 int lorb_ba_plan_update_dev(lorb_ba_plan* plan, const lorb_ba_window_dev* win);
 int lorb_ba_plan_result_dev(lorb_ba_plan* plan, float* d_pose_out, float* d_point_out);
+/* (a13) BA::LocalPoseOptimization for a caller that gathers a NEW window on every call -- the drop-in
+ * (src/bundle_adjust.cpp:207-330; the call site src/local_mapping.cpp:32).  Same inputs, outputs and
+ * errors as lorb_ba_local with one window, but the solver keeps device-built plans
+ * (lorb_ba_plan_create_dev) resident across calls, one per camera count (a small LRU), with capacities
+ * that grow, so a call costs one host-to-device copy of the window, the device plan build (one small
+ * readback), the captured LM graph and one device-to-host copy of the solution -- no per-call plan
+ * construction, allocation or graph capture.  Windows the device plans do not take (no cameras /
+ * points / observations, a point observed twice by one camera, a point with 256 or more observations)
+ * run through lorb_ba_local's host-built plan on the same GPU kernels.  One solver per ctx / thread.
+ * pose_out: n_poses x 6 doubles (caller order), point_out: n_points x 3 doubles.  Synchronous. */
+typedef struct lorb_ba_solver lorb_ba_solver;
+int lorb_ba_solver_create(lorb_ctx* ctx, lorb_ba_solver** out);
+int lorb_ba_solver_solve(lorb_ba_solver* solver, const lorb_ba_window* window, const lorb_lm_options* opt,
+                         double* pose_out, double* point_out, lorb_ba_summary* summary);
+/* first n of: [0] resident plans, [1] plan creations so far, [2] 1 if the last call ran on the host-built
+ * plan, [3] its S half band, [4] its Cholesky kernel, [5] 1 if its cameras were reordered (RCM) */
+int lorb_ba_solver_info(lorb_ba_solver* solver, int32_t* info, int32_t n);
+int lorb_ba_solver_destroy(lorb_ba_solver* solver);
 /* plan structure, first n of: [0] S half band (max over windows, scalar rows), [1] Cholesky kernel of
  * the last solve (0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s, -1 none yet), [2] (camera, camera)
  * blocks, [3] point groups, [4] observations, [5] points, [6] cameras, [7] 1 if some window's

@@ -3054,8 +3054,14 @@ __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, in
                                                  int* __restrict__ pt_cnt, int* __restrict__ hdr,
                                                  unsigned long long* __restrict__ bits) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  const int n_obs = *w.d_n_obs, n_pt = *w.d_n_points;
-  if (k == 0) hdr[3] = n_pt;
+  const int n_obs_in = *w.d_n_obs, n_pt_in = *w.d_n_points;
+  // live counts beyond the capacities are an error (flag 8); clamped, so nothing is touched past
+  // the plan's allocations
+  const int n_obs = min(n_obs_in, w.max_obs), n_pt = min(n_pt_in, w.max_points);
+  if (k == 0) {
+    hdr[3] = n_pt;
+    if (n_obs_in > w.max_obs || n_pt_in > w.max_points || n_obs_in < 0 || n_pt_in < 0) atomicOr(&hdr[2], 8);
+  }
   if (k >= n_obs) return;
   const int q = w.d_obs_point[k], f = w.d_obs_frame[k];
   if (f >= -F && f < C) {
@@ -3096,7 +3102,7 @@ __global__ __launch_bounds__(256) void k_db_scatter(lorb_ba_window_dev w, int C,
                                                     const int* __restrict__ pt_off, int* __restrict__ pt_cnt,
                                                     int* __restrict__ val) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  const int n_obs = *w.d_n_obs, n_pt = *w.d_n_points;
+  const int n_obs = min(*w.d_n_obs, w.max_obs), n_pt = min(*w.d_n_points, w.max_points);
   if (k >= n_obs) return;
   const int q = w.d_obs_point[k], f = w.d_obs_frame[k];
   if (f < -F || f >= C || q < 0 || q >= n_pt) return;
@@ -3108,7 +3114,7 @@ __global__ __launch_bounds__(256) void k_db_scatter(lorb_ba_window_dev w, int C,
 __global__ __launch_bounds__(256) void k_db_segsort(lorb_ba_window_dev w, const int* __restrict__ pt_off,
                                                     int* __restrict__ val, int* __restrict__ key) {
   const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= *w.d_n_points) return;
+  if (p >= min(*w.d_n_points, w.max_points)) return;
   const int a0 = pt_off[p], a1 = pt_off[p + 1], m = a1 - a0;
   if (m <= 16) {
     int v[16];
@@ -3296,8 +3302,38 @@ __global__ __launch_bounds__(256) void k_db_result(BaDev d, int C, int P, const 
     for (int k = i; k < 3 * P; k += gridDim.x * 256) pt_out[k] = (float)d.x_pt[cur][k];
 }
 
+// the same in double (the Ceres parameter blocks after Solve) plus the summary, into one buffer for
+// one D2H copy: [poses 6C (caller order) | points 3P | iterations, successful steps, termination,
+// initial cost, final cost]
+__global__ __launch_bounds__(256) void k_db_result64(BaDev d, int C, int P, const int* __restrict__ perm,
+                                                     double* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const WinState& st = d.st[0];
+  const int cur = st.cur;
+  if (i < 6 * C) {
+    const int c = i / 6, q = i - 6 * c;
+    out[i] = d.x_pose[cur][6 * perm[c] + q];
+  }
+  for (int k = i; k < 3 * P; k += gridDim.x * 256) out[6 * C + k] = d.x_pt[cur][k];
+  if (i == 0) {
+    double* s = out + 6 * C + 3 * P;
+    s[0] = st.iter; s[1] = st.n_success; s[2] = st.term; s[3] = st.initial_cost; s[4] = st.cost;
+  }
+}
 
 }  // namespace
+
+namespace lorb {
+int ba_plan_result64_dev(lorb_ba_plan* P, double* d_out) {
+  if (!P || !P->devb || !d_out) return LORB_E_INVALID;
+  const int C = P->Ctot, Pn = P->Ptot;
+  const int m = std::max(std::max(6 * C, 1), std::min(3 * Pn, 256 * 1024));
+  hipLaunchKernelGGL(k_db_result64, dim3(lorb::ceil_div(m, 256)), dim3(256), 0, P->ctx->stream, P->dev, C, Pn,
+                     P->devb->perm, d_out);
+  LORB_CHECK_LAUNCH(P->ctx);
+  return LORB_OK;
+}
+}  // namespace lorb
 
 namespace {
 
@@ -3451,6 +3487,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   if (err & 1) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a point index outside [0, n_points)");
   if (err & 2) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a frame index >= n_poses");
   if (err & 4) return lorb::set_error(ctx, LORB_E_INVALID, "a point observed twice by one camera");
+  if (err & 8) return lorb::set_error(ctx, LORB_E_INVALID, "live point / observation count outside [0, capacity] (%d / %d)",
+                                      b.P_cap, b.K_cap);
   if (Pn < 0 || Pn > b.P_cap) return lorb::set_error(ctx, LORB_E_INVALID, "n_points %d outside [0, %d]", Pn, b.P_cap);
   const int* cov = H + 8;
   const int* cam_cnt = H + 8 + (size_t)C * C;

@@ -86,6 +86,11 @@ int comm_allreduce_host(lorb_comm* comm, double* h_buf, size_t n, int op);
     if (rc_ != LORB_OK) return rc_; \
   } while (0)
 
+// device-built plan (lorb_ba_plan_create_dev): the solution in double, caller camera order, plus
+// the LM summary, into d_out = [poses 6C | points 3P | iterations, successful, termination, initial
+// cost, final cost] (async on the plan's stream)
+int ba_plan_result64_dev(lorb_ba_plan* P, double* d_out);
+
 // grow-only scratch: returns device pointer in *out
 int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out);
 template <typename T>

@@ -57,7 +57,6 @@ __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Po
   __shared__ int s_ok;
   const int t = threadIdx.x;
   const int P0 = m.cnt[0], K0 = m.cnt[1];
-  if (t < 6) m.ring[6 * ring_slot(kf, m.R) + t] = pose.v[t];
   // pass 1: totals
   int n_obs = 0, n_new = 0, n_mat = 0;
   for (int base = 0; base < n; base += 1024) {
@@ -73,9 +72,11 @@ __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Po
   if (t == 0) {
     s_ok = (P0 + n_new <= m.P_cap) && (K0 + n_obs <= m.K_cap);
     m.cnt[2] = s_ok ? 0 : 1;  // this step's capacity flag (no separate clear)
+    if (!s_ok) { m.cnt[3] = 0; m.cnt[4] = 0; m.cnt[5] = n_mat; }  // the attempt appended nothing
   }
   __syncthreads();
-  if (!s_ok) return;
+  if (!s_ok) return;  // the map is left exactly as it was (the host stops the step here)
+  if (t < 6) m.ring[6 * ring_slot(kf, m.R) + t] = pose.v[t];
   int ro = 0, rn = 0;
   for (int base = 0; base < n; base += 1024) {
     const int q = base + t;
@@ -397,6 +398,17 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   for (int q = 0; q < 6; ++q) p6.v[q] = pose[q];
   hipLaunchKernelGGL(k_map_append, dim3(1), dim3(1024), 0, s, m, n, kf, p6, M->mt, M->xyz, d_desc, d_x, d_y, d_depth);
   LORB_CHECK_LAUNCH(ctx);
+  M->last_n = n;
+  // Capacity: n keypoints add at most n points and n observations.  When that bound does not fit,
+  // read the append's verdict before anything else changes: a refused append leaves the map as it
+  // was (no ring write, no slide, no cull), so the map stays usable after the error.
+  if (M->h_P + n > m.P_cap || M->h_K + n > m.K_cap) {
+    LORB_HIP(ctx, hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
+    LORB_HIP(ctx, hipStreamSynchronize(s));
+    if (M->pinned[2] & 1)
+      return lorb::set_error(ctx, LORB_E_NOMEM, "map capacity exceeded (points %d + %d new / %d, observations %d + %d new / %d)",
+                             M->h_P, n, m.P_cap, M->h_K, n, m.K_cap);
+  }
   LORB_TRY(mark(2));
   // 4. slide the window by one keyframe; cull and compact
   LORB_TRY(map_slide(M, M->t0 + 1, std::min(M->h_P + n, m.P_cap), std::min(M->h_K + n, m.K_cap)));
@@ -406,10 +418,6 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   const lorb_ba_window_dev w = window_of(M);
   LORB_TRY(lorb_ba_plan_update_dev(M->plan, &w));
   LORB_TRY(mark(4));
-  M->last_n = n;
-  if (M->pinned[2] & 1)
-    return lorb::set_error(ctx, LORB_E_NOMEM, "map capacity exceeded (points %d/%d, observations %d/%d)", M->pinned[0],
-                           m.P_cap, M->pinned[1], m.K_cap);
   M->h_P = M->pinned[0]; M->h_K = M->pinned[1];
   // 6. LocalPoseOptimization + float write-back of poses (ring) and points (map)
   LORB_TRY(lorb_ba_plan_solve(M->plan, opt));

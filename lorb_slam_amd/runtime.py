@@ -346,6 +346,52 @@ class BAPlan:
             pass
 
 
+class BASolver:
+    """lorb_ba_solver: BA::LocalPoseOptimization for a caller that gathers a new window every call
+    (the drop-in's path, include/lorb/adapters.hpp); device-built plans stay resident across calls."""
+
+    INFO_KEYS = ("resident_plans", "plan_creations", "host_plan_fallback", "band", "cholesky", "reordered")
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+        self._p = C.c_void_p()
+        ctx.check(lib().lorb_ba_solver_create(ctx.handle, C.byref(self._p)), "lorb_ba_solver_create")
+
+    def prepare(self, w):
+        """ctypes window of one dict window (kept alive by the returned tuple) and its output arrays"""
+        keep = A.KeepAlive()
+        arr = A.make_windows([w], keep)
+        pose = np.zeros((len(w["pose_init"]), 6))
+        pts = np.zeros((len(w["point_init"]), 3))
+        return (arr, keep, pose, pts, A.BASummary())
+
+    def solve_prepared(self, prep, opt):
+        arr, _, pose, pts, summ = prep
+        self.ctx.check(lib().lorb_ba_solver_solve(self._p, arr, C.byref(opt), A.ptr(pose, C.c_double),
+                                                  A.ptr(pts, C.c_double), C.byref(summ)), "lorb_ba_solver_solve")
+        return pose, pts, summ.as_dict()
+
+    def solve(self, w, opt=None):
+        """(poses n_poses x 6, points n_points x 3, summary) of one window dict"""
+        return self.solve_prepared(self.prepare(w), opt or A.LMOptions.default())
+
+    def info(self):
+        v = (C.c_int32 * 6)()
+        self.ctx.check(lib().lorb_ba_solver_info(self._p, v, C.c_int32(6)), "lorb_ba_solver_info")
+        return dict(zip(self.INFO_KEYS, [int(x) for x in v]))
+
+    def close(self):
+        if self._p:
+            lib().lorb_ba_solver_destroy(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class BAPlanDev(BAPlan):
     """Device-built plan (lorb_ba_plan_create_dev / _update_dev) of one window held in device
     memory: `arrays` is a dict of DeviceArrays (n_points, n_obs: 1 int each; pose_init, fixed_pose,

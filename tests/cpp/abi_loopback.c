@@ -70,6 +70,31 @@ int lorb_ba_local(lorb_ctx* ctx, int32_t n_windows, const lorb_ba_window* window
   return or_ba_local(n_windows, windows, opt, pose_out, point_out, summaries);
 }
 
+struct lorb_ba_solver {
+  lorb_ctx* ctx;
+};
+
+int lorb_ba_solver_create(lorb_ctx* ctx, lorb_ba_solver** out) {
+  if (!ctx || !out) return LORB_E_INVALID;
+  *out = (lorb_ba_solver*)calloc(1, sizeof(lorb_ba_solver));
+  if (!*out) return LORB_E_NOMEM;
+  (*out)->ctx = ctx;
+  return LORB_OK;
+}
+
+int lorb_ba_solver_solve(lorb_ba_solver* s, const lorb_ba_window* w, const lorb_lm_options* opt, double* pose_out,
+                         double* point_out, lorb_ba_summary* summary) {
+  if (!s || !w || !opt) return LORB_E_INVALID;
+  double* const po[1] = {pose_out};
+  double* const pt[1] = {point_out};
+  return or_ba_local(1, w, opt, po, pt, summary);
+}
+
+int lorb_ba_solver_destroy(lorb_ba_solver* s) {
+  free(s);
+  return LORB_OK;
+}
+
 int lorb_compute_stereo_matches(lorb_ctx* ctx, const lorb_frame_params* frame, const lorb_stereo_keys* left,
                                 const lorb_stereo_keys* right, const lorb_image_pyramid* left_pyr,
                                 const lorb_image_pyramid* right_pyr, float* u_right, float* depth) {
@@ -109,4 +134,9 @@ int lorb_track_local_map(lorb_ctx* ctx, const lorb_frame_params* frame, const fl
   lorb_local_points lp = {n, in_view, pts->is_bad, pts->locked, track, track + n, track + 2 * n, level, track + 3 * n,
                           pts->desc};
   return or_search_by_projection_local(frame, kps, slot_state, &lp, th, assign, nmatches);
+}
+
+int lorb_ba_solver_info(lorb_ba_solver* s, int32_t* info, int32_t n) {
+  (void)s; (void)info; (void)n;
+  return LORB_E_UNSUPPORTED;  /* no resident plans in the loopback */
 }

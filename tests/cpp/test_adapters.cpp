@@ -2,6 +2,7 @@
 // local_mapping.hpp) driven exactly like the reference's VisualOdometry drives Matcher / BA /
 // LocalMapping, with plain test frames standing in for Simple_ORB_SLAM::Frame/MapPoint.  Every
 // GPU result is checked against the oracle (test infrastructure, linked only here).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -306,6 +307,124 @@ int main() {
         md = std::max(md, fabs((double)wp[q]->pos[i] - (double)(float)ppt[3 * q + i]) / std::max(1.0, fabs(ppt[3 * q + i])));
     EXPECT(md <= 1e-5, "local BA point rel diff %g", md);
     printf("LocalPoseOptimization: %zu points, %zu obs (max rel diff %.2e)\n", wp.size(), op.size(), md);
+  }
+
+  // ---- BA::LocalPoseOptimization at C4 size, twice ---------------------
+  // 50 window keyframes (cur + 49 covisible, in the reference's ascending-weight order,
+  // src/bundle_adjust.cpp:210-220 / src/frame.cpp:754-774) + 5 older fixed keyframes, 10,000
+  // points on 7-8 consecutive keyframes.  The adapter runs on the thread's resident solver; the
+  // second call (the window after the first call's float write-back) reuses the plan.
+  {
+#ifdef LORB_LOOPBACK  // sanitizer builds (the oracle behind the ABI): the same gather at a smaller size
+    const int NW = 12, NFX = 3, NP = 1500;
+#else
+    const int NW = 50, NFX = 5, NP = 10000;
+#endif
+    std::vector<MiniFrame*> kf(NFX + NW);
+    std::vector<float> tr(6 * (NFX + NW));
+    for (int i = 0; i < NFX + NW; i++) {
+      const float r[3] = {0.0f, 0.01f * i, 0.0f}, t[3] = {-0.1f * i, 0.0f, 0.0f};
+      memcpy(&tr[6 * i], r, 12); memcpy(&tr[6 * i + 3], t, 12);
+      kf[i] = new MiniFrame();
+      kf[i]->id = 100 + i;
+      kf[i]->fp = make_fp();
+      memcpy(kf[i]->rvec, r, 12); memcpy(kf[i]->tvec, t, 12);
+      lorb_pose_to_Tcw(r, t, kf[i]->Tcw);
+    }
+    auto observe = [&](MiniPoint* p, MiniFrame* f, const float* Xtrue) {
+      float u, v;
+      project(f->Tcw, Xtrue, f->fp, &u, &v);
+      p->obs[f] = f->x.size();
+      f->x.push_back(u + urand(-0.8f, 0.8f)); f->y.push_back(v + urand(-0.8f, 0.8f));
+      f->octave.push_back(0); f->angle.push_back(0.0f);
+      f->mps.push_back(p); f->outlier.push_back(false);
+      p->nobs++;
+    };
+    std::vector<MiniPoint*> cpts;
+    for (int q = 0; q < NP; q++) {
+      MiniPoint* p = new MiniPoint();
+      const float X[3] = {urand(-6, 8), urand(-3, 3), urand(4, 20)};
+      const int len = 7 + (int)(rnd() % 2), s = (int)(rnd() % (NW - len + 1));
+      for (int j = s; j < s + len; j++) observe(p, kf[NFX + j], X);
+      if (s < 3 && rnd() % 3 == 0) observe(p, kf[rnd() % NFX], X);  // fixed keyframes (MPCost)
+      for (int c = 0; c < 3; c++) p->pos[c] = X[c] + urand(-0.05f, 0.05f);
+      cpts.push_back(p);
+    }
+    for (int i = NFX; i < NFX + NW; i++) {  // perturbed window poses
+      for (int c = 0; c < 3; c++) { kf[i]->rvec[c] += urand(-2e-3f, 2e-3f); kf[i]->tvec[c] += urand(-2e-2f, 2e-2f); }
+      lorb_pose_to_Tcw(kf[i]->rvec, kf[i]->tvec, kf[i]->Tcw);
+    }
+    MiniFrame* c4 = kf[NFX + NW - 1];
+    {  // GetCovisibleFrames: the other window keyframes by ascending shared-point weight
+      std::map<MiniFrame*, int> wgt;
+      for (MiniPoint* p : cpts)
+        if (p->obs.count(c4))
+          for (auto& ob : p->obs)
+            if (ob.first != c4) wgt[ob.first]++;
+      std::vector<std::pair<int, MiniFrame*>> v;
+      for (int i = NFX; i < NFX + NW - 1; i++) v.push_back({wgt.count(kf[i]) ? wgt[kf[i]] : 0, kf[i]});
+      std::stable_sort(v.begin(), v.end(), [](const std::pair<int, MiniFrame*>& a, const std::pair<int, MiniFrame*>& b) { return a.first < b.first; });
+      for (auto& e : v) c4->covis.push_back(e.second);
+    }
+    lorb_lm_options opt;
+    lorb_lm_options_default(&opt);
+    for (int call = 0; call < 2; call++) {
+      // the window as src/bundle_adjust.cpp:207-330 gathers it: [cur] + covisible, points in
+      // first-seen order, each point's observations in std::map<Frame*, size_t> order
+      std::vector<MiniFrame*> fr{c4};
+      for (MiniFrame* f : c4->covis) fr.push_back(f);
+      std::map<MiniFrame*, int> fidx, xidx;
+      for (size_t i = 0; i < fr.size(); i++) fidx[fr[i]] = (int)i;
+      std::vector<MiniPoint*> wp;
+      std::set<MiniPoint*> seen;
+      for (MiniFrame* f : fr)
+        for (MiniPoint* p : f->mps)
+          if (p && seen.insert(p).second) wp.push_back(p);
+      std::vector<float> pi, fx, X, uv;
+      for (MiniFrame* f : fr) { pi.insert(pi.end(), f->rvec, f->rvec + 3); pi.insert(pi.end(), f->tvec, f->tvec + 3); }
+      std::vector<int32_t> op, of;
+      for (size_t q = 0; q < wp.size(); q++) {
+        X.insert(X.end(), wp[q]->pos, wp[q]->pos + 3);
+        for (auto& ob : wp[q]->obs) {
+          int code;
+          if (fidx.count(ob.first)) {
+            code = fidx[ob.first];
+          } else {
+            if (!xidx.count(ob.first)) {
+              const int j = (int)xidx.size();
+              xidx[ob.first] = j;
+              fx.insert(fx.end(), ob.first->rvec, ob.first->rvec + 3); fx.insert(fx.end(), ob.first->tvec, ob.first->tvec + 3);
+            }
+            code = -1 - xidx[ob.first];
+          }
+          op.push_back((int32_t)q); of.push_back(code);
+          uv.push_back(ob.first->x[ob.second]); uv.push_back(ob.first->y[ob.second]);
+        }
+      }
+      lorb_ba_window w{(int32_t)fr.size(), (int32_t)xidx.size(), (int32_t)wp.size(), (int32_t)op.size(), c4->fp.fx,
+                       c4->fp.fy, c4->fp.cx, c4->fp.cy, pi.data(), fx.data(), X.data(), op.data(), of.data(), uv.data()};
+      std::vector<double> po(6 * fr.size()), ppt(3 * wp.size());
+      double* a = po.data();
+      double* bpt = ppt.data();
+      lorb_ba_summary so;
+      or_ba_local(1, &w, &opt, &a, &bpt, &so);
+      lorb::LocalPoseOptimization(ctx, c4);
+      double md = 0;
+      for (size_t q = 0; q < wp.size(); q++)
+        for (int i = 0; i < 3; i++)
+          md = std::max(md, fabs((double)wp[q]->pos[i] - (double)(float)ppt[3 * q + i]) / std::max(1.0, fabs(ppt[3 * q + i])));
+      for (size_t f = 0; f < fr.size(); f++)
+        for (int i = 0; i < 3; i++) {
+          md = std::max(md, fabs((double)fr[f]->rvec[i] - (double)(float)po[6 * f + i]) / std::max(1.0, fabs(po[6 * f + i])));
+          md = std::max(md, fabs((double)fr[f]->tvec[i] - (double)(float)po[6 * f + 3 + i]) / std::max(1.0, fabs(po[6 * f + 3 + i])));
+        }
+      EXPECT(md <= 1e-5, "C4 local BA call %d rel diff %g", call, md);
+      printf("LocalPoseOptimization C4 call %d: %zu frames + %zu fixed, %zu points, %zu obs, oracle %d its (max rel diff %.2e)\n",
+             call, fr.size(), xidx.size(), wp.size(), op.size(), so.iterations, md);
+    }
+    int32_t si[6];
+    if (lorb_ba_solver_info(lorb::thread_ba_solver(ctx), si, 6) == LORB_OK)
+      EXPECT(si[1] <= 2 && si[2] == 0 && si[3] <= 47, "solver: %d plan creations, fallback %d, band %d", si[1], si[2], si[3]);
   }
 
   // ---- Matcher::SearchLocalPoints(curr, set) ------------------------------------------------

@@ -86,11 +86,32 @@ def test_local_mapping_ragged_keyframes(ctx):
 
 
 def test_local_mapping_capacity_error(ctx):
-    seq = synth.mapping_sequence(seed=5, n_kf=10, n_fixed=2, n_new=40, obs_lens=(3, 4), steps=1, n_kps=300)
+    """a step that would overflow the map's point capacity is refused and leaves the map unchanged;
+    the next step (a keyframe without stereo depth: matches only, no new points) runs from the
+    unchanged map and equals the oracle's step from the same state"""
+    seq = synth.mapping_sequence(seed=5, n_kf=10, n_fixed=2, n_new=40, obs_lens=(3, 4), steps=2, n_kps=300)
     n_pts = len(seq["init"]["point_init"])
+    fp = synth.frame_params()
     M = LocalMap(ctx, seq["init"], max_points=n_pts + 5, max_keypoints=512)
     try:
+        before = M.read()
         with pytest.raises(LorbError, match="capacity"):
-            M.step(synth.frame_params(), seq["steps"][0], OPT10)
+            M.step(fp, seq["steps"][0], OPT10)
+        after = M.read()
+        same_structure(after, before)
+        for k in ("point", "pose", "fixed_pose"):
+            assert np.array_equal(after[k], before[k]), k
+        assert after["new_points"] == 0 and after["new_observations"] == 0
+        k1 = dict(seq["steps"][1], depth=np.full_like(seq["steps"][1]["depth"], -1.0))
+        ref = MapOracle.from_state(after, seq["init"]["intr"])
+        M.step(fp, k1, OPT10)
+        g = M.read()
+        r = ref.step(fp, k1, OPT10)
+        o = ref.state()
+        assert np.array_equal(g["match_train"], r["match_train"])
+        assert g["new_points"] == 0 and g["matches"] == r["n_matches"]
+        same_structure(g, o)
+        assert close(g["pose"], o["pose"]) and close(g["point"], o["point"])
+        lm_match(g["summary"], r["summary"])
     finally:
         M.close()

@@ -1,0 +1,90 @@
+"""GPU parity: lorb_ba_solver (the drop-in BA::LocalPoseOptimization path, src/bundle_adjust.cpp:207-330,
+with device-built plans resident across calls) vs the oracle's or_ba_local on the same windows, within
+north_star's 1e-5 (test_gpu_ba.close) -- for windows that change from call to call the way a caller's
+covisibility windows do: the same camera count again (plan reused), a larger window (capacities
+grow), another camera count (a second resident plan), and the structures only the host-built plan
+takes (fallback on the same GPU kernels)."""
+import numpy as np
+import pytest
+
+import oracle as O
+from lorb_slam_amd import _abi as A
+from lorb_slam_amd import synth
+from lorb_slam_amd.runtime import BASolver, LorbError
+from test_gpu_ba import close, lm_match
+
+pytestmark = pytest.mark.gpu
+OPT10 = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                            parameter_tolerance=0.0)
+
+
+def check(solver, w, opt):
+    Pg, Xg, sg = solver.solve(w, opt)
+    Po, Xo, so = O.ba_local([w], opt)
+    lm_match(sg, so[0])
+    assert close(Pg, Po[0]), np.abs(Pg - Po[0]).max()
+    assert close(Xg, Xo[0]), np.abs(Xg - Xo[0]).max()
+    return Pg, Xg, sg
+
+
+def test_solver_c4_reference_order_twice(ctx):
+    """C4 window in the reference's camera order, solved twice (the second call with the first
+    call's float write-back as its start, as the drop-in's next call sees it): one plan creation,
+    band 47 after the RCM relabelling, no host-built fallback."""
+    w0 = synth.ba_window(seed=4, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400)
+    w, _ = synth.reference_window_order(w0)
+    s = BASolver(ctx)
+    try:
+        P1, X1, _ = check(s, w, OPT10)
+        w2 = dict(w, pose_init=P1.astype(np.float32), point_init=X1.astype(np.float32))
+        check(s, w2, OPT10)
+        info = s.info()
+        assert info["plan_creations"] == 1 and info["host_plan_fallback"] == 0, info
+        assert info["band"] == 47 and info["cholesky"] == 2 and info["reordered"] == 1, info
+    finally:
+        s.close()
+
+
+def test_solver_windows_that_change(ctx):
+    """default Ceres options; camera counts 12 -> 12 (more points: capacities grow) -> 20 -> 12"""
+    s = BASolver(ctx)
+    try:
+        a = synth.ba_window(seed=21, n_kf=12, n_pts=800, n_fixed=2, fixed_obs_per_kf=80)
+        b = synth.ba_window(seed=22, n_kf=12, n_pts=3000, n_fixed=3, fixed_obs_per_kf=200)
+        c = synth.ba_window(seed=23, n_kf=20, n_pts=1500, n_fixed=1, fixed_obs_per_kf=100)
+        for w in (a, b, c, a):
+            check(s, w, A.LMOptions.default())
+        info = s.info()
+        assert info["resident_plans"] == 2 and info["host_plan_fallback"] == 0, info
+    finally:
+        s.close()
+
+
+def test_solver_fallback_and_errors(ctx):
+    """a point observed twice by one camera (the reference's std::map<Frame*, size_t> cannot hold
+    it, but lorb_ba_local accepts it) runs on the host-built plan; bad indices are rejected like
+    lorb_ba_local rejects them; an empty window returns."""
+    s = BASolver(ctx)
+    try:
+        w = synth.ba_window(seed=24, n_kf=6, n_pts=300, n_fixed=1, fixed_obs_per_kf=40)
+        k = int(np.flatnonzero(np.asarray(w["obs_frame"]) >= 0)[0])
+        dup = dict(w, obs_point=np.append(w["obs_point"], w["obs_point"][k]),
+                   obs_frame=np.append(w["obs_frame"], w["obs_frame"][k]),
+                   obs_uv=np.concatenate([np.asarray(w["obs_uv"]).reshape(-1, 2), np.asarray(w["obs_uv"]).reshape(-1, 2)[k:k + 1]]))
+        check(s, dup, OPT10)
+        assert s.info()["host_plan_fallback"] == 1
+        check(s, w, OPT10)
+        assert s.info()["host_plan_fallback"] == 0
+        bad = dict(w, obs_frame=np.where(np.arange(len(w["obs_frame"])) == 3, -5, w["obs_frame"]))
+        with pytest.raises(LorbError, match="bad frame"):
+            s.solve(bad, OPT10)
+        bad = dict(w, obs_point=np.where(np.arange(len(w["obs_point"])) == 3, len(w["point_init"]), w["obs_point"]))
+        with pytest.raises(LorbError, match="bad point"):
+            s.solve(bad, OPT10)
+        empty = dict(w, point_init=np.zeros((0, 3), np.float32), obs_point=np.zeros(0, np.int32),
+                     obs_frame=np.zeros(0, np.int32), obs_uv=np.zeros((0, 2), np.float32))
+        P, X, sm = s.solve(empty, OPT10)
+        assert P.shape == (6, 6) and X.shape == (0, 3)
+        check(s, w, OPT10)  # still usable after the errors
+    finally:
+        s.close()

@@ -144,8 +144,16 @@ def orb():
                 kx += list(fx + rx); ky += list(fy + ry); kr += list(fr)
             keep = pyref.distribute_octree(kx, ky, kr, 16, pyr[l].shape[1] - 16, 16, pyr[l].shape[0] - 16, nd[l])
             s = sf[l] if l else np.float32(1)
-            gx = (np.asarray(kx, np.float32)[keep] + np.float32(16)) * s if l else np.asarray(kx, np.float32)[keep] + 16
-            assert np.array_equal(e["x"][lo[l]:lo[l + 1]], np.asarray(gx, np.float32)), (nfeat, l)
+            sl = slice(lo[l], lo[l + 1])
+            for key, v in (("x", kx), ("y", ky)):
+                g = np.asarray(v, np.float32)[keep] + np.float32(16)
+                g = g * s if l else g
+                assert np.array_equal(e[key][sl], np.asarray(g, np.float32)), (nfeat, l, key)
+            # response = the FAST score, octave = the level, size = PATCH_SIZE * scale truncated to
+            # int (src/ORBextractor.cpp:878-882), all independent of the oracle
+            assert np.array_equal(e["response"][sl], np.asarray(kr, np.float32)[keep]), (nfeat, l, "response")
+            assert np.all(e["octave"][sl] == l), (nfeat, l, "octave")
+            assert np.all(e["size"][sl] == np.float32(int(np.float32(31) * np.float32(sf[l])))), (nfeat, l, "size")
         d = O.orb_detect(pyr, nd, sf)
         ang, desc = pyref.orb_describe(pyr, d["x"], d["y"], d["octave"], pattern)
         assert np.array_equal(ang, e["angle"]) and np.array_equal(desc, e["desc"]), nfeat
