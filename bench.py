@@ -285,18 +285,22 @@ def cpu_baseline_c4(seq, budget_s):
 
 def workload_shared(ctx, args, rank, D, comm):
     """BASELINE C5 shared-window variant: ONE 50-KF window with 80,000 points
-    (~600,000 observations) point-partitioned over the N ranks, 10 LM iterations per step with
-    the three RCCL all-reduces per iteration; plus the new keyframe's 2,000 descriptors matched
+    (~600,000 observations) point-partitioned over the N ranks (each rank's points with all of their
+    observations, resident in HBM).  A step is: the new keyframe's 2,000 descriptors matched
     (crossCheck) against the window's 80,000 map-point descriptors with the query rows split over
-    the ranks.  Strong scaling: total work is fixed as N grows."""
+    the ranks, the device-built sharded BA plan rebuilt from the resident shard (collective: one
+    all-reduce of the camera structure), and 10 LM iterations with three RCCL all-reduces each.
+    Strong scaling: total work is fixed as N grows."""
     from lorb_slam_amd import _abi as A
     from lorb_slam_amd import shard, synth
-    from lorb_slam_amd.runtime import BAPlan, lib
-    world = D.world
+    from lorb_slam_amd.runtime import BAPlanDev, lib
+    world = comm.size()[0] if comm is not None else 1
     win = synth.ba_window(seed=11, n_kf=50, n_pts=args.shared_points, n_fixed=5, fixed_obs_per_kf=400)
     sh = shard.shard_window(win, rank, world)
+    arrays = BAPlanDev.upload(ctx, sh)
     t0 = time.perf_counter()
-    plan = BAPlan(ctx, [sh], comm=comm)
+    plan = BAPlanDev(ctx, arrays, 50, 5, win["intr"], comm=comm)
+    ctx.sync()
     plan_ms = (time.perf_counter() - t0) * 1e3
     opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
@@ -318,12 +322,18 @@ def workload_shared(ctx, args, rank, D, comm):
                                               A.ptr(q_off, C.c_int32), A.ptr(q_base, C.c_int32), dt.as_ptr(C.c_uint8),
                                               A.ptr(t_off, C.c_int32), *[o.as_ptr(C.c_int32) for o in outs],
                                               nm.as_ptr(C.c_int32)), "lorb_bf_match_sharded_dev")
+        plan.update()
         plan.solve(opt)
 
     def check():
         _, _, summ = plan.read()
         return {"n_matches": int(nm.numpy()[0]), "ba_final_cost": summ[0]["final_cost"],
                 "ba_iterations": summ[0]["iterations"]}
+
+    def cleanup():
+        plan.close()
+        for x in (dq, dt, nm, *outs, *arrays.values()):
+            x.free()
 
     n_obs = len(win["obs_point"])
     opt_obs = int((sh["obs_frame"] >= 0).sum())
@@ -335,11 +345,12 @@ def workload_shared(ctx, args, rank, D, comm):
     }
     # whole-job units: the shared window's iterations / matches are counted once (rank 0 only)
     return dict(step=step, check=check, ba_iters=10.0 if rank == 0 else 0.0, matches=float(nq) if rank == 0 else 0.0,
-                pairs=float(b - a) * nt, plan_ms=plan_ms, cleanup=plan.close, kspec=kspec,
-                traffic_key=f"shared_w{world}",
+                pairs=float(b - a) * nt, plan_ms=plan_ms, cleanup=cleanup, kspec=kspec,
+                traffic_key=f"shared_w{world}", n_ranks=world,
                 config={"workload": "c5_shared_window", "kf": 50, "fixed_kf": 5, "points": len(win["point_init"]),
                         "observations": n_obs, "lm_iterations": 10, "new_kf_keypoints": nq,
-                        "match": f"{nq}x{nt} bf crossCheck, query rows sharded", "points_this_rank": len(sh["point_init"])},
+                        "match": f"{nq}x{nt} bf crossCheck, query rows sharded", "points_this_rank": len(sh["point_init"]),
+                        "step": "sharded match + device-built sharded plan (collective) + 10 LM its (3 RCCL all-reduces each)"},
                 cpu=None, scaling="strong")
 
 
@@ -509,6 +520,52 @@ def sub_c2(ctx, D, args):
             "cpu_baseline": cpu, "check": chk}
 
 
+def workload_shared_rehearse(ctx, args, rank, D, comm):
+    """CPU rehearsal of the shared sub-record (no GPU): the same three exchanges per LM iteration,
+    sized as the C5 window's (camera blocks + costs, the S band + rhs, the step sums), all-reduced
+    over gloo, so the launcher, the sub-record's keys and its max-over-ranks timing are exercised.
+    It measures nothing about the hot path."""
+    import torch
+    bufs = [torch.zeros(n, dtype=torch.float64) for n in (50 * 27 + 2, 32 * 10 + 300 * 48, 3)]
+
+    def step():
+        for _ in range(10):
+            for b in bufs:
+                D.dist.all_reduce(b) if D.dist else None
+
+    def profile(steps):
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        ms = (time.perf_counter() - t0) * 1e3
+        return {7: (ms, 3 * 10 * steps)}, steps
+    return dict(step=step, check=lambda: {}, ba_iters=10.0 if rank == 0 else 0.0, matches=0.0, pairs=0.0,
+                plan_ms=0.0, cleanup=lambda: None, kspec={}, traffic_key=None, profile=profile, n_ranks=D.world,
+                config={"workload": "rehearsal_shared_exchanges_cpu"}, cpu=None, scaling="strong")
+
+
+def sub_shared(ctx, D, args, comm):
+    """BASELINE C5 shared-window variant inside the default run: the point-partitioned
+    window over the N ranks of this job, strong scaling, with the per-iteration time of the three
+    RCCL all-reduces from the profile pass (HIP events around the collectives on the ctx stream)."""
+    rehearse = args.workload == "rehearse"
+    wl = (workload_shared_rehearse if rehearse else workload_shared)(ctx, args, D.rank, D, comm)
+    steps = max(5, min(args.steps, 20))
+    elapsed = timed(ctx, D, wl, steps, max(2, args.warmup))
+    kt, pn = wl["profile"](steps) if rehearse else profile_pass(ctx, wl, steps)
+    chk = wl["check"]()
+    total = D.reduce(wl["ba_iters"] * steps, "SUM")
+    ar = kt.pop(7, (0.0, 0))
+    its = 10.0 * pn
+    ar_ms = D.reduce(ar[0] / its if its else 0.0, "MAX")
+    wl["cleanup"]()
+    return {"workload": wl["config"]["workload"], "n_ranks": wl["n_ranks"], "scaling": "strong",
+            "value": total / elapsed, "unit": "BA iterations/s", "steps": steps, "ms_per_step": elapsed / steps * 1e3,
+            "plan_create_ms": wl["plan_ms"], "allreduce_ms_per_iteration": ar_ms,
+            "allreduce_launches_per_iteration": (ar[1] / its) if its else 0.0,
+            "roofline": roofline_entry(kt, wl, pn), "config": wl["config"], "check": chk}
+
+
 def sub_dropin(ctx, D, args):
     """The drop-in BA::LocalPoseOptimization call (include/lorb/adapters.hpp -> lorb_ba_solver_solve):
     a C4 window (50 KF + 5 fixed, 10,000 points, ~77 k observations) in the reference's camera order
@@ -564,6 +621,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 sub-record of the default run")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in LocalPoseOptimization sub-record")
+    ap.add_argument("--no-shared", action="store_true", help="skip the shared-window (RCCL) sub-record")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -585,7 +643,7 @@ def main():
     n_gpus = D.world
     if not rehearse:
         ctx = Context(D.local_rank)
-        if D.world > 1 or args.workload == "shared":
+        if D.world > 1 or args.workload == "shared" or (args.workload == "c4" and not args.no_shared):
             from lorb_slam_amd.runtime import Comm, unique_id
             uid = D.broadcast_bytes(unique_id() if D.rank == 0 else None)
             comm = Comm.rccl(ctx, D.world, D.rank, uid)
@@ -603,6 +661,8 @@ def main():
     cpu = wl["cpu"]() if (D.rank == 0 and not args.no_cpu_baseline and D.world == 1 and wl["cpu"]) else None
     c2 = sub_c2(ctx, D, args) if (args.workload == "c4" and not args.no_c2) else None
     dropin = sub_dropin(ctx, D, args) if (args.workload == "c4" and not args.no_dropin) else None
+    shared = (sub_shared(ctx, D, args, comm) if (args.workload in ("c4", "rehearse") and not args.no_shared)
+              else None)
     if D.rank == 0:
         if args.workload in ("c4", "shared"):
             value, unit = total_iters / elapsed, "BA iterations/s"
@@ -620,7 +680,7 @@ def main():
             "config": dict(wl["config"], parallelism=par),
             "matches_per_sec": total_matches / elapsed, "plan_build_ms": wl["plan_ms"],
             "map_create_ms": wl.get("create_ms"),
-            "roofline": roofline_entry(kt, wl, pn), "cpu_baseline": cpu, "c2": c2, "dropin_local_ba": dropin,
+            "roofline": roofline_entry(kt, wl, pn), "cpu_baseline": cpu, "c2": c2, "dropin_local_ba": dropin, "shared": shared,
             "check": check,
         }
         if rehearse:

@@ -85,6 +85,7 @@ int lorb_timer_elapsed_ms(lorb_ctx* ctx, int slot_begin, int slot_end, float* ms
 #define LORB_K_BA_CHOLESKY  4
 #define LORB_K_WINDOW_CAND  5
 #define LORB_K_STEREO       6
+#define LORB_K_ALLREDUCE    7   /* the sharded plans' ncclAllReduce exchanges (eager, timed runs) */
 #define LORB_K_COUNT        8
 int lorb_kernel_timing_enable(lorb_ctx* ctx, int enable);
 /* sums (and resets) the recorded launches of kernel id k: total ms and launch count */
@@ -609,6 +610,15 @@ int lorb_comm_allreduce_f64(lorb_comm* comm, const double* d_send, double* d_rec
  * read returns the (replicated) poses and this rank's points. */
 int lorb_ba_plan_create_sharded(lorb_ctx* ctx, lorb_comm* comm, int32_t n_windows,
                                 const lorb_ba_window* shards, lorb_ba_plan** out);
+
+/* the device-built plan (lorb_ba_plan_create_dev) over this rank's shard of ONE window: the shard's
+ * points with all of their observations in device arrays (lorb_ba_window_dev; point indices local to
+ * the shard), the same n_poses / n_fixed / poses on every rank.  Each build all-reduces the camera
+ * covisibility and counts (camera order, band and activity are global; the block pair lists are this
+ * rank's), so lorb_ba_plan_update_dev is collective: every rank calls it, and an error on any rank
+ * is returned on all of them.  solve / read / result_dev as for lorb_ba_plan_create_sharded. */
+int lorb_ba_plan_create_sharded_dev(lorb_ctx* ctx, lorb_comm* comm, const lorb_ba_window_dev* shard,
+                                    lorb_ba_plan** out);
 
 /* (a2/a3) with query rows split over ranks.  This rank holds queries
  * [q_base[p], q_base[p] + q_off[p+1] - q_off[p]) of problem p (global numbering) and ALL of its

@@ -2449,9 +2449,12 @@ struct lorb_ba_devbuild {
   int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0, gs_cap = 0;
   std::vector<int> h_hdr, h_cov, h_cam;
   int* pinned = nullptr; size_t pinned_n = 0;
+  double* sol_part = nullptr; size_t sol_n = 0;  // this rank's solve block (== the global one unsharded)
+  std::vector<double> h_red;                     // sharded: the build's host all-reduce
   // per-build structure uploaded in one copy: [BaWin | live (2) | perm (C) | cam_obs_off (C+1) | bp (up_bp_cap)]
   unsigned char* up_dev = nullptr; unsigned char* up_host = nullptr; int up_bp_cap = 0;
-  size_t off_live = 0, off_perm = 0, off_camoff = 0, off_bp = 0, up_bytes = 0;
+  size_t off_live = 0, off_perm = 0, off_camoff = 0, off_gcam = 0, off_bp = 0, up_bytes = 0;
+  int* gcam = nullptr;  // device: observations per input camera over all ranks (camera activity)
 };
 
 struct lorb_ba_plan {
@@ -2470,13 +2473,18 @@ struct lorb_ba_plan {
   // launch shape of the captured solve: a rebuild that keeps it (device-built plans launch the
   // point-group / block-pair kernels at capacity) replays the graph without a new capture
   struct GraphKey {
-    int kind = -1, lds = 0, memset_env = 0, env_total = 0, grid_pblk = 0, grid_bp = 0, pt_launch = 0;
+    int kind = -1, lds = 0, memset_env = 0, env_total = 0, grid_pblk = 0, grid_bp = 0, pt_launch = 0, x2_n = 0;
     bool operator==(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) == 0; }
   } gkey;
   int grid_pblk = 0, grid_bp = 0;  // launch grids of the point-group and block-pair kernels
   int pt_launch = 0;               // points k_ba_init copies (Ptot, or the capacity)
   int* live = nullptr;             // device [n_pblk, n_bp] (BaDev::live)
   lorb_comm* comm = nullptr;  // sharded plan (not owned)
+  // exchange 2 of a sharded plan: [send, send + n) -> [recv, ...) (host plans: env | rhs | wfail;
+  // device-built plans: rhs | wfail | pad | env, the band's size decides n)
+  double* x2_send = nullptr;
+  double* x2_recv = nullptr;
+  size_t x2_off = 0;  // device-built: offset of env after rhs | wfail | pad
   // per window: camera relabelling (input pose index -> plan camera index; RCM order, §8 item 4)
   std::vector<std::vector<int>> cam_map;
   int chol_kind = -1;         // last launched Cholesky: 0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s
@@ -2828,6 +2836,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   d.U_part = linp; d.V_part = linp + C * 21; d.wlin_part = linp + C * 27; d.wmax_part = mxp;
   d.env = sol; d.rhs = sol + P->env_total; d.wfail = sol + P->env_total + P->n_total;
   d.env_part = solp; d.rhs_part = solp + P->env_total; d.wfail_part = solp + P->env_total + P->n_total;
+  P->x2_send = solp; P->x2_recv = sol;
   d.wstep = stp; d.wstep_part = stpp;
   d.sharded = comm ? 1 : 0;
   d.rank0 = comm ? (comm->rank == 0) : 1;
@@ -2862,6 +2871,11 @@ int chol_kind_of(const lorb_ba_plan* P) {
   return chol_2s ? 2 : chol_w ? 1 : 0;
 }
 
+// doubles of exchange 2 (reduced camera system, rhs, failure flags)
+size_t x2_count(const lorb_ba_plan* P) {
+  return P->devb ? P->x2_off + (size_t)P->env_total : (size_t)P->env_total + P->n_total + P->W;
+}
+
 lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
   lorb_ba_plan::GraphKey k;
   k.kind = chol_kind_of(P);
@@ -2869,6 +2883,7 @@ lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
   k.memset_env = sizeof(double) * (size_t)P->max_env > (size_t)kLdsBudget;
   k.env_total = k.memset_env ? P->env_total : 0;
   k.grid_pblk = P->grid_pblk; k.grid_bp = P->grid_bp; k.pt_launch = P->pt_launch;
+  k.x2_n = P->comm ? (int)x2_count(P) : 0;  // the captured all-reduce's count
   return k;
 }
 
@@ -2883,8 +2898,11 @@ int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(256), 0, s, d);
   if (P->comm) {  // exchange 1: camera blocks + cost / |x|^2 (sum), gradient max (max)
     hipLaunchKernelGGL(k_ba_win_reduce<0>, dim3(P->W), dim3(64), 0, s, d);
-    LORB_TRY(lorb::comm_allreduce(P->comm, d.U_part, d.U, (size_t)P->Ctot * 27 + 2 * P->W, LORB_OP_SUM));
-    LORB_TRY(lorb::comm_allreduce(P->comm, d.wmax_part, d.wmax, (size_t)P->W, LORB_OP_MAX));
+    {
+      lorb::KernelTimer kt(P->ctx, LORB_K_ALLREDUCE);
+      LORB_TRY(lorb::comm_allreduce(P->comm, d.U_part, d.U, (size_t)P->Ctot * 27 + 2 * P->W, LORB_OP_SUM));
+      LORB_TRY(lorb::comm_allreduce(P->comm, d.wmax_part, d.wmax, (size_t)P->W, LORB_OP_MAX));
+    }
     hipLaunchKernelGGL(k_ba_lm_begin<true>, dim3(P->W), dim3(64), 0, s, d, o);
   } else {
     hipLaunchKernelGGL(k_ba_lm_begin<false>, dim3(P->W), dim3(64), 0, s, d, o);
@@ -2907,8 +2925,10 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
     hipLaunchKernelGGL(k_ba_schur, dim3(P->grid_bp), dim3(256), 0, s, d, o);
   }
-  if (P->comm)  // exchange 2: reduced camera system, rhs, point-block failure flags
-    LORB_TRY(lorb::comm_allreduce(P->comm, d.env_part, d.env, (size_t)P->env_total + P->n_total + P->W, LORB_OP_SUM));
+  if (P->comm) {  // exchange 2: reduced camera system, rhs, point-block failure flags
+    lorb::KernelTimer kt(ctx, LORB_K_ALLREDUCE);
+    LORB_TRY(lorb::comm_allreduce(P->comm, P->x2_send, P->x2_recv, x2_count(P), LORB_OP_SUM));
+  }
   const int kind = chol_kind_of(P);
   const bool chol_2s = kind == 2, chol_w = kind == 1 || kind == 2;
   P->chol_kind = kind;
@@ -2932,7 +2952,10 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   if (P->grid_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
   if (P->comm) {  // exchange 3: model cost change, candidate cost, point |step|^2
     hipLaunchKernelGGL(k_ba_win_reduce<1>, dim3(P->W), dim3(64), 0, s, d);
-    LORB_TRY(lorb::comm_allreduce(P->comm, d.wstep_part, d.wstep, 3 * (size_t)P->W, LORB_OP_SUM));
+    {
+      lorb::KernelTimer kt(ctx, LORB_K_ALLREDUCE);
+      LORB_TRY(lorb::comm_allreduce(P->comm, d.wstep_part, d.wstep, 3 * (size_t)P->W, LORB_OP_SUM));
+    }
     hipLaunchKernelGGL(k_ba_lm_end<true>, dim3(P->W), dim3(64), 0, s, d, o);
   } else {
     hipLaunchKernelGGL(k_ba_lm_end<false>, dim3(P->W), dim3(64), 0, s, d, o);
@@ -3384,18 +3407,38 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(dalloc(P, Pn * 3, &d.x_pt[0])); LORB_TRY(dalloc(P, Pn * 3, &d.x_pt[1]));
   LORB_TRY(dalloc(P, C * 6, &d.scale_pose)); LORB_TRY(dalloc(P, Pn * 3, &d.scale_pt));
   LORB_TRY(dalloc(P, Pn * 6, &d.ete)); LORB_TRY(dalloc(P, Pn * 3, &d.etb)); LORB_TRY(dalloc(P, Pn * 6, &d.pinv));
-  const size_t n = 6 * C, lin_n = C * 27 + 2, solve_n = n * n + n + 1;
+  // the solve block is rhs (n) | wfail (1) | pad | env (up to the dense n x n): rhs and wfail at fixed
+  // places, so the captured solve survives a rebuild that changes the band, and a sharded plan's
+  // exchange 2 is one contiguous all-reduce of x2_off + env_total doubles
+  const size_t n = 6 * C, lin_n = C * 27 + 2, x2_off = (n + 1 + 31) & ~(size_t)31, solve_n = x2_off + n * n;
+  lorb_comm* comm = P->comm;
   double *lin, *mx, *sol, *stp;
   LORB_TRY(dalloc(P, lin_n, &lin)); LORB_TRY(dalloc(P, (size_t)1, &mx));
   LORB_TRY(dalloc(P, solve_n, &sol)); LORB_TRY(dalloc(P, (size_t)3, &stp));
   d.U = lin; d.V = lin + C * 21; d.wlin = lin + C * 27; d.wmax = mx;
-  d.U_part = d.U; d.V_part = d.V; d.wlin_part = d.wlin; d.wmax_part = d.wmax;
-  // rhs / wfail at a fixed place after the largest band (n x n), so the captured solve survives a
-  // rebuild that changes the band
-  d.env = sol; d.env_part = sol;
-  d.rhs = sol + n * n; d.wfail = d.rhs + n; d.rhs_part = d.rhs; d.wfail_part = d.wfail;
-  d.wstep = stp; d.wstep_part = stp;
-  d.sharded = 0; d.rank0 = 1;
+  d.rhs = sol; d.wfail = sol + n; d.env = sol + x2_off;
+  d.wstep = stp;
+  P->x2_off = x2_off;
+  b.sol_n = solve_n;
+  if (comm) {  // this rank's partial sums (see BaDev), all-reduced into the global buffers
+    double *linp, *mxp, *solp, *stpp;
+    LORB_TRY(dalloc(P, lin_n, &linp)); LORB_TRY(dalloc(P, (size_t)1, &mxp));
+    LORB_TRY(dalloc(P, solve_n, &solp)); LORB_TRY(dalloc(P, (size_t)3, &stpp));
+    LORB_HIP(ctx, hipMemsetAsync(linp, 0, sizeof(double) * lin_n, ctx->stream));
+    LORB_HIP(ctx, hipMemsetAsync(solp, 0, sizeof(double) * solve_n, ctx->stream));
+    d.U_part = linp; d.V_part = linp + C * 21; d.wlin_part = linp + C * 27; d.wmax_part = mxp;
+    d.rhs_part = solp; d.wfail_part = solp + n; d.env_part = solp + x2_off;
+    d.wstep_part = stpp;
+    b.sol_part = solp;
+  } else {
+    d.U_part = d.U; d.V_part = d.V; d.wlin_part = d.wlin; d.wmax_part = d.wmax;
+    d.rhs_part = d.rhs; d.wfail_part = d.wfail; d.env_part = d.env;
+    d.wstep_part = d.wstep;
+    b.sol_part = sol;
+  }
+  P->x2_send = b.sol_part; P->x2_recv = sol;
+  d.sharded = comm ? 1 : 0;
+  d.rank0 = comm ? (comm->rank == 0) : 1;
   LORB_TRY(dalloc(P, C, &d.cam_gmax));
   LORB_TRY(dalloc(P, K * 2, &d.obs_r)); LORB_TRY(dalloc(P, K * 6, &d.obs_Jp)); LORB_TRY(dalloc(P, K * 12, &d.obs_Jc));
   LORB_TRY(dalloc(P, K * 2, &d.cam_r));
@@ -3425,7 +3468,8 @@ int up_alloc(lorb_ba_plan* P, int bp_need) {
   b.off_live = al(sizeof(BaWin));
   b.off_perm = b.off_live + 256;
   b.off_camoff = b.off_perm + al(4 * C);
-  b.off_bp = b.off_camoff + al(4 * (C + 1));
+  b.off_gcam = b.off_camoff + al(4 * (C + 1));
+  b.off_bp = b.off_gcam + al(4 * C);
   b.up_bytes = b.off_bp + sizeof(BlockPair) * (size_t)cap;
   if (b.up_dev) {
     LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -3442,6 +3486,7 @@ int up_alloc(lorb_ba_plan* P, int bp_need) {
   d.win = reinterpret_cast<const BaWin*>(b.up_dev);
   d.live = reinterpret_cast<const int*>(b.up_dev + b.off_live);
   b.perm = reinterpret_cast<int*>(b.up_dev + b.off_perm);
+  b.gcam = reinterpret_cast<int*>(b.up_dev + b.off_gcam);
   d.cam_obs_off = reinterpret_cast<const int*>(b.up_dev + b.off_camoff);
   d.bp = reinterpret_cast<const BlockPair*>(b.up_dev + b.off_bp);
   P->grid_bp = cap;
@@ -3484,18 +3529,49 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_HIP(ctx, lorb::spin_sync(ctx));
   const int* H = b.pinned;
   const int K = H[0], maxk = H[1], err = H[2], Pn = H[3];
-  if (err & 1) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a point index outside [0, n_points)");
-  if (err & 2) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a frame index >= n_poses");
-  if (err & 4) return lorb::set_error(ctx, LORB_E_INVALID, "a point observed twice by one camera");
-  if (err & 8) return lorb::set_error(ctx, LORB_E_INVALID, "live point / observation count outside [0, capacity] (%d / %d)",
-                                      b.P_cap, b.K_cap);
-  if (Pn < 0 || Pn > b.P_cap) return lorb::set_error(ctx, LORB_E_INVALID, "n_points %d outside [0, %d]", Pn, b.P_cap);
   const int* cov = H + 8;
   const int* cam_cnt = H + 8 + (size_t)C * C;
-  // 3. host: camera order, blocks, band, groups
+  // sharded: the camera-level structure is global -- sum the ranks' covisibility and camera counts
+  // (camera order, band and camera activity must agree on every rank) and their error flags (every
+  // rank returns the same error, so none is left waiting in a later collective)
+  const int* gcov = cov;
+  const int* gcam = cam_cnt;
+  int K_all = K, gerr = err, gmaxk = maxk;
+  std::vector<int> g_int;
+  if (P->comm) {
+    // [cov | cam_cnt (contiguous, m) | K | n_points out of range | error bits 0..3] summed; the largest
+    // per-point count (the group size check) by a max
+    const size_t m = (size_t)C * C + C;
+    b.h_red.assign(m + 6, 0.0);
+    for (size_t i = 0; i < m; ++i) b.h_red[i] = (double)cov[i];
+    b.h_red[m] = K;
+    b.h_red[m + 1] = (Pn < 0 || Pn > b.P_cap) ? 1.0 : 0.0;
+    for (int q = 0; q < 4; ++q) b.h_red[m + 2 + q] = (err >> q) & 1;
+    LORB_TRY(lorb::comm_allreduce_host(P->comm, b.h_red.data(), b.h_red.size(), LORB_OP_SUM));
+    double mk = maxk;
+    LORB_TRY(lorb::comm_allreduce_host(P->comm, &mk, 1, LORB_OP_MAX));
+    g_int.resize(m);
+    for (size_t i = 0; i < m; ++i) g_int[i] = (int)b.h_red[i];
+    gcov = g_int.data();
+    gcam = g_int.data() + (size_t)C * C;
+    K_all = (int)b.h_red[m];
+    gerr = b.h_red[m + 1] > 0.0 ? 16 : 0;
+    for (int q = 0; q < 4; ++q) gerr |= b.h_red[m + 2 + q] > 0.0 ? 1 << q : 0;
+    gmaxk = (int)mk;
+  }
+  if (gerr & 1) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a point index outside [0, n_points)");
+  if (gerr & 2) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a frame index >= n_poses");
+  if (gerr & 4) return lorb::set_error(ctx, LORB_E_INVALID, "a point observed twice by one camera");
+  if (gerr & 8) return lorb::set_error(ctx, LORB_E_INVALID, "live point / observation count outside [0, capacity] (%d / %d)",
+                                       b.P_cap, b.K_cap);
+  if ((gerr & 16) || Pn < 0 || Pn > b.P_cap) return lorb::set_error(ctx, LORB_E_INVALID, "n_points %d outside [0, %d]", Pn, b.P_cap);
+  if (kGB - gmaxk < 1)
+    return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "a point with %d observations (device plans hold <= %d)", gmaxk, kGB - 1);
+  // 3. host: camera order, blocks, band, groups (order, band, activity from the global structure;
+  //    the block pair lists from this rank's observations)
   std::vector<char> adj((size_t)C * C, 0);
   for (int i = 0; i < C; ++i)
-    for (int j = 0; j < C; ++j) adj[(size_t)i * C + j] = (i == j && cam_cnt[i] > 0) || cov[(size_t)i * C + j] > 0;
+    for (int j = 0; j < C; ++j) adj[(size_t)i * C + j] = (i == j && gcam[i] > 0) || gcov[(size_t)i * C + j] > 0;
   const std::vector<int> map = camera_order(C, adj);
   std::vector<int> inv(C);
   for (int c = 0; c < C; ++c) inv[map[c]] = c;
@@ -3509,8 +3585,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     fc[ch] = ch;
     for (int cl = 0; cl <= ch; ++cl) {
       const int cnt = ch == cl ? cam_cnt[inv[ch]] : cov[(size_t)inv[ch] * C + inv[cl]];
+      if (ch != cl && gcov[(size_t)inv[ch] * C + inv[cl]] > 0) fc[ch] = std::min(fc[ch], cl);
       if (ch != cl && cnt == 0) continue;
-      if (ch != cl) fc[ch] = std::min(fc[ch], cl);
       bps.push_back(BlockPair{0, ch, cl, n_pairs, cnt});
       n_pairs += cnt;
     }
@@ -3519,13 +3595,12 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   int bwid = 0;
   for (int c = 0; c < C; ++c) bwid = std::max(bwid, 6 * c + 5 - 6 * fc[c]);
   if (n == 0) bwid = 0;
-  const int S = kGB - (maxk + 1) + 1;
-  if (S < 1) return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "a point with %d observations (device plans hold <= %d)", maxk, kGB - 1);
+  const int S = kGB - (maxk + 1) + 1;  // >= 1 (checked above)
   const int G = Pn > 0 ? (K + Pn - 1) / S + 1 : 0;
   BaWin bw{};
   bw.pose_base = 0; bw.n_poses = C; bw.point_base = 0; bw.n_points = Pn; bw.pblk_base = 0; bw.n_pblk = G;
   bw.env_base = 0; bw.env_size = n * (bwid + 1); bw.n = n; bw.row_base = 0; bw.bw = bwid;
-  bw.obs_base = 0; bw.n_obs = K; bw.n_obs_all = K;
+  bw.obs_base = 0; bw.n_obs = K; bw.n_obs_all = K_all;
   bw.fx = w->fx; bw.fy = w->fy; bw.cx = w->cx; bw.cy = w->cy;
   P->hwin[0] = bw;
   P->Ctot = C; P->Ptot = Pn; P->K = K; P->NF = F; P->n_pblk = G; P->n_bp = (int)bps.size(); P->n_pairs = n_pairs;
@@ -3566,6 +3641,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     memcpy(h + b.off_live, live, sizeof(live));
     memcpy(h + b.off_perm, map.data(), sizeof(int) * C);
     memcpy(h + b.off_camoff, cam_off.data(), sizeof(int) * (C + 1));
+    memcpy(h + b.off_gcam, gcam, sizeof(int) * C);
     if (!bps.empty()) memcpy(h + b.off_bp, bps.data(), sizeof(BlockPair) * bps.size());
     const size_t bytes = b.off_bp + sizeof(BlockPair) * bps.size();
     LORB_HIP(ctx, hipMemcpyAsync(b.up_dev, h, bytes, hipMemcpyHostToDevice, s));
@@ -3592,9 +3668,11 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   {
     const int m = std::max(std::max(6 * C, 6 * F), std::min(3 * Pn, 256 * 1024));
     if (m > 0)
-      hipLaunchKernelGGL(k_db_init, dim3(lorb::ceil_div(m, 256)), dim3(256), 0, s, *w, d, C, F, Pn, b.perm, b.cam_cnt);
+      hipLaunchKernelGGL(k_db_init, dim3(lorb::ceil_div(m, 256)), dim3(256), 0, s, *w, d, C, F, Pn, b.perm, b.gcam);
   }
-  if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
+  // this rank's band starts from zeros (blocks it has no pairs of stay zero; sharded: the all-reduce
+  // writes the global band every iteration)
+  if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env_part, 0, sizeof(double) * P->env_total, s));
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
 }
@@ -3642,6 +3720,28 @@ int lorb_ba_plan_create_dev(lorb_ctx* ctx, const lorb_ba_window_dev* win, lorb_b
   P->devb = new (std::nothrow) lorb_ba_devbuild();
   int rc = P->devb ? dev_alloc(ctx, win, P) : LORB_E_NOMEM;
   if (rc == LORB_OK) rc = dev_build(ctx, win, P);
+  if (rc != LORB_OK) { delete P; return rc; }
+  *out = P;
+  return LORB_OK;
+}
+
+int lorb_ba_plan_create_sharded_dev(lorb_ctx* ctx, lorb_comm* comm, const lorb_ba_window_dev* shard,
+                                    lorb_ba_plan** out) {
+  if (!ctx || !comm || !shard || !out) return LORB_E_INVALID;
+  if (comm->ctx != ctx) return lorb::set_error(ctx, LORB_E_INVALID, "communicator belongs to another context");
+  if (shard->n_poses < 0 || shard->n_fixed < 0 || shard->max_points < 0 || shard->max_obs < 0 || !shard->d_n_points ||
+      !shard->d_n_obs || (shard->n_poses > 0 && !shard->d_pose_init) || (shard->n_fixed > 0 && !shard->d_fixed_pose) ||
+      (shard->max_points > 0 && !shard->d_point_init) ||
+      (shard->max_obs > 0 && (!shard->d_obs_point || !shard->d_obs_frame || !shard->d_obs_uv)))
+    return LORB_E_INVALID;
+  *out = nullptr;
+  lorb_ba_plan* P = new (std::nothrow) lorb_ba_plan();
+  if (!P) return LORB_E_NOMEM;
+  P->ctx = ctx;
+  P->comm = comm;
+  P->devb = new (std::nothrow) lorb_ba_devbuild();
+  int rc = P->devb ? dev_alloc(ctx, shard, P) : LORB_E_NOMEM;
+  if (rc == LORB_OK) rc = dev_build(ctx, shard, P);
   if (rc != LORB_OK) { delete P; return rc; }
   *out = P;
   return LORB_OK;

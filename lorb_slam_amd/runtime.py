@@ -397,12 +397,33 @@ class BAPlanDev(BAPlan):
     memory: `arrays` is a dict of DeviceArrays (n_points, n_obs: 1 int each; pose_init, fixed_pose,
     point_init, obs_point, obs_frame, obs_uv), `intr` = (fx, fy, cx, cy)."""
 
-    def __init__(self, ctx, arrays, n_poses, n_fixed, intr):  # noqa: D107 -- BAPlan's fields, another constructor
-        self.ctx, self.comm, self._keep = ctx, None, A.KeepAlive()
+    def __init__(self, ctx, arrays, n_poses, n_fixed, intr, comm=None):  # noqa: D107 -- BAPlan's fields
+        self.ctx, self.comm, self._keep = ctx, comm, A.KeepAlive()
         self._p = C.c_void_p()
         self.n_poses, self.n_fixed = n_poses, n_fixed
         self.win = self._window(arrays, intr)
-        ctx.check(lib().lorb_ba_plan_create_dev(ctx.handle, C.byref(self.win), C.byref(self._p)), "lorb_ba_plan_create_dev")
+        if comm is None:
+            ctx.check(lib().lorb_ba_plan_create_dev(ctx.handle, C.byref(self.win), C.byref(self._p)),
+                      "lorb_ba_plan_create_dev")
+        else:  # this rank's shard; every build is collective (lorb_ba_plan_create_sharded_dev)
+            ctx.check(lib().lorb_ba_plan_create_sharded_dev(ctx.handle, comm.handle, C.byref(self.win), C.byref(self._p)),
+                      "lorb_ba_plan_create_sharded_dev")
+
+    @staticmethod
+    def upload(ctx, w, extra_points=0, extra_obs=0):
+        """device arrays of a window dict (synth.ba_window / shard.shard_window) with spare capacity"""
+        P, K = len(w["point_init"]), len(w["obs_point"])
+
+        def pad(a, n):
+            a = np.asarray(a)
+            return np.concatenate([a, np.zeros((n - len(a),) + a.shape[1:], a.dtype)])
+        return dict(n_points=ctx.to_device(np.array([P], np.int32)), n_obs=ctx.to_device(np.array([K], np.int32)),
+                    pose_init=ctx.to_device(A.f32(w["pose_init"]).reshape(-1, 6)),
+                    fixed_pose=ctx.to_device(A.f32(w["fixed_pose"]).reshape(-1, 6)),
+                    point_init=ctx.to_device(pad(A.f32(w["point_init"]).reshape(-1, 3), max(P + extra_points, 1))),
+                    obs_point=ctx.to_device(pad(A.i32(w["obs_point"]), max(K + extra_obs, 1))),
+                    obs_frame=ctx.to_device(pad(A.i32(w["obs_frame"]), max(K + extra_obs, 1))),
+                    obs_uv=ctx.to_device(pad(A.f32(w["obs_uv"]).reshape(-1, 2), max(K + extra_obs, 1))))
 
     def _window(self, a, intr):
         self.arrays = a

@@ -90,6 +90,23 @@ def main():
             res[f"{name}_range{i}"] = np.array(shards[i]["point_range"])
             res[f"{name}_iters{i}"] = np.array([S[i]["iterations"], S[i]["successful_steps"]])
             res[f"{name}_cost{i}"] = np.array([S[i]["final_cost"]])
+    # the device-built sharded plan (lorb_ba_plan_create_sharded_dev), one plan per window, built,
+    # solved, rebuilt in place (collective update) and solved again
+    from lorb_slam_amd.runtime import BAPlanDev
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    for i, sh in enumerate(shards):
+        arrays = BAPlanDev.upload(ctx, sh, extra_points=11, extra_obs=97)
+        plan = BAPlanDev(ctx, arrays, len(sh["pose_init"]), len(sh["fixed_pose"]), sh["intr"], comm=comm)
+        plan.solve(opt)
+        plan.update()
+        plan.solve(opt)
+        P, X, S = plan.read()
+        res[f"dev_pose{i}"], res[f"dev_pts{i}"] = P[0], X[0]
+        res[f"dev_iters{i}"] = np.array([S[0]["iterations"], S[0]["successful_steps"]])
+        plan.close()
+        for a in arrays.values():
+            a.free()
     comm.close()
     ctx.close()
     np.savez(out, **res)

@@ -29,6 +29,14 @@ def test_two_rank_rehearsal_prints_one_line_with_n_gpus_2():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 3 and out["warmup"] == 1
     assert out["value"] > 0 and "rehearsal" in out
+    # the shared-window sub-record: the keys the GPU line carries, from the
+    # same sub_shared code path over gloo
+    sh = out["shared"]
+    for k in ("workload", "n_ranks", "scaling", "value", "unit", "steps", "ms_per_step", "plan_create_ms",
+              "allreduce_ms_per_iteration", "allreduce_launches_per_iteration", "roofline", "config", "check"):
+        assert k in sh, k
+    assert sh["n_ranks"] == 2 and sh["scaling"] == "strong" and sh["allreduce_launches_per_iteration"] == 3
+    assert sh["value"] > 0 and sh["allreduce_ms_per_iteration"] > 0
 
 
 def test_world_size_mismatch_refused():

@@ -92,3 +92,35 @@ def test_sharded_two_ranks_host_transport(ctx, tmp_path):
                 X[a:b] = R[r][f"{name}_pts{i}"]
             assert close(X, Xg[i]) and close(X, Xo[i])
             assert list(R[0][f"{name}_iters{i}"]) == [Sg[i]["iterations"], Sg[i]["successful_steps"]]
+    # the device-built sharded plans (10 iterations, tolerances 0) against the unsharded solve
+    opt = OPTS["ten"]
+    Pg, Xg, Sg = ctx.ba_local(wins, opt)
+    for i in range(len(wins)):
+        assert np.array_equal(R[0][f"dev_pose{i}"], R[1][f"dev_pose{i}"])
+        assert close(R[0][f"dev_pose{i}"], Pg[i])
+        X = np.zeros_like(Xg[i])
+        for r in range(2):
+            a, b = R[r][f"ten_range{i}"]
+            X[a:b] = R[r][f"dev_pts{i}"]
+        assert close(X, Xg[i])
+        assert R[0][f"dev_iters{i}"][0] == Sg[i]["iterations"]
+
+
+def test_sharded_dev_rccl_world1(ctx):
+    """the device-built sharded plan at world 1 over RCCL equals the unsharded device-built plan"""
+    from lorb_slam_amd.runtime import BAPlanDev, Comm, unique_id
+    w = synth.ba_window(**shard_rank.WINDOWS[1])
+    comm = Comm.rccl(ctx, 1, 0, unique_id())
+    arrays = BAPlanDev.upload(ctx, w, extra_points=5, extra_obs=50)
+    try:
+        opt = OPTS["ten"]
+        ref = BAPlanDev(ctx, arrays, len(w["pose_init"]), len(w["fixed_pose"]), w["intr"])
+        ref.solve(opt); Pr, Xr, Sr = ref.read(); ref.close()
+        pl = BAPlanDev(ctx, arrays, len(w["pose_init"]), len(w["fixed_pose"]), w["intr"], comm=comm)
+        pl.solve(opt); pl.update(); pl.solve(opt); Ps, Xs, Ss = pl.read(); pl.close()
+        assert close(Ps[0], Pr[0], 1e-9) and close(Xs[0], Xr[0], 1e-9)
+        assert Ss[0]["iterations"] == Sr[0]["iterations"]
+    finally:
+        comm.close()
+        for a in arrays.values():
+            a.free()
