@@ -491,8 +491,9 @@ int lorb_ba_plan_result_dev(lorb_ba_plan* plan, float* d_pose_out, float* d_poin
  * that grow, so a call costs one host-to-device copy of the window, the device plan build (one small
  * readback), the captured LM graph and one device-to-host copy of the solution -- no per-call plan
  * construction, allocation or graph capture.  Windows the device plans do not take (no cameras /
- * points / observations, a point observed twice by one camera, a point with 256 or more observations)
- * run through lorb_ba_local's host-built plan on the same GPU kernels.  One solver per ctx / thread.
+ * points / observations, a point with 256 or more observations) run through lorb_ba_local's
+ * host-built plan on the same GPU kernels.  A point observed twice by one camera is an error (both
+ * plan builders; the reference keys observations by Frame*).  One solver per ctx / thread.
  * pose_out: n_poses x 6 doubles (caller order), point_out: n_points x 3 doubles.  Synchronous. */
 typedef struct lorb_ba_solver lorb_ba_solver;
 int lorb_ba_solver_create(lorb_ctx* ctx, lorb_ba_solver** out);

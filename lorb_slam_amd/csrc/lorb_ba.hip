@@ -588,14 +588,10 @@ __global__ __launch_bounds__(64) void k_ba_win_reduce(BaDev d) {
 // K3: per-window iteration head: finalise the (re)linearisation, termination checks
 // Camera terms (gradient max, |x|^2, iteration-0 Jacobi scale) come from the (all-reduced)
 // U / V blocks; point terms from the point-group partials (SH: from the exchange buffers).
+// One wavefront; returns the state after the head (lane 0 has stored it).  k_ba_lm_begin runs it
+// as a kernel; the fused iteration runs it on an otherwise idle wave of the Cholesky (lm_head).
 template <bool SH>
-__global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
-  const int w = blockIdx.x;
-  const WinState* Sp = d.st + w;
-  WinState S = *Sp;
-  const BaWin W = d.win[w];  // issued with the state, before the done test
-  if (S.done) return;
-  const int lane = threadIdx.x;
+__device__ __forceinline__ WinState lm_head(const BaDev& d, const LMOpt& o, int w, int lane, WinState S, const BaWin& W) {
   if (S.relin) {
     // fixed lane assignment + fixed butterfly => deterministic
     double cost = 0.0, gm = 0.0, xn2 = 0.0;
@@ -629,6 +625,17 @@ __global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
     else S.iter++;
     d.st[w] = S;
   }
+  return S;
+}
+
+template <bool SH>
+__global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
+  const int w = blockIdx.x;
+  const WinState* Sp = d.st + w;
+  const WinState S = *Sp;
+  const BaWin W = d.win[w];  // issued with the state, before the done test
+  if (S.done) return;
+  (void)lm_head<SH>(d, o, w, threadIdx.x, S, W);
 }
 
 typedef double v4d __attribute__((ext_vector_type(4)));
@@ -645,17 +652,31 @@ __device__ __forceinline__ double& band(double* A, int bw, int i, int j) {
 // are re-read from that XCD's L2 instead of from the fabric.
 // DIAG (a diagonal block: pr.x == pr.y, pairs in camera-slot order): the camera's rhs term
 // Jc^T g of the same observation is accumulated from the tiles already loaded
-template <bool DIAG>
-__device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc)[36], double (&r6)[6]) {
-  double Qh[6], Jl[6], Ch[12], Cl[12], g0 = 0.0, g1 = 0.0;
+// FU (diagonal blocks of the fused iteration, k_ba_schur<true>): the camera's normal block
+// U = Jc^T Jc (21, packed upper) and V = Jc^T r (6) of the same observation, accumulated with the
+// expressions and in the per-thread order of k_ba_camera (same bits)
+template <bool DIAG, bool FU = false>
+__device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc)[36], double (&r6)[6],
+                                           double* U = nullptr, double* V = nullptr) {
+  double Qh[6], Jl[6], Ch[12], Cl[12], g0 = 0.0, g1 = 0.0, cr0 = 0.0, cr1 = 0.0;
 #pragma unroll
   for (int k = 0; k < 6; ++k) { Qh[k] = d.obs_Q[6 * pr.x + k]; Jl[k] = d.obs_Jps[6 * pr.y + k]; }
 #pragma unroll
   for (int k = 0; k < 12; ++k) { Ch[k] = d.obs_Jc[12 * pr.x + k]; Cl[k] = DIAG ? Ch[k] : d.obs_Jc[12 * pr.y + k]; }
+  if (FU) { cr0 = d.cam_r[2 * pr.x]; cr1 = d.cam_r[2 * pr.x + 1]; }
   if (DIAG) {
     g0 = d.obs_g[2 * pr.x]; g1 = d.obs_g[2 * pr.x + 1];
 #pragma unroll
     for (int k = 0; k < 6; ++k) r6[k] += Ch[k] * g0 + Ch[6 + k] * g1;
+  }
+  if (FU) {
+    int q = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      V[a] += Ch[a] * cr0 + Ch[6 + a] * cr1;
+#pragma unroll
+      for (int b = a; b < 6; ++b) U[q++] += Ch[a] * Ch[b] + Ch[6 + a] * Ch[6 + b];
+    }
   }
   double M[4], N[12];
 #pragma unroll
@@ -680,8 +701,14 @@ __device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc
 // 36 doubles read); the camera Jacobi scales are applied once per block.  Block pairs are sorted
 // by camera and remapped so that each XCD (blockIdx % 8 group) takes a contiguous run: the tiles
 // of a camera are re-read from that XCD's L2 instead of from the fabric.
+// FU (the fused iteration of unsharded plans, after the first): the diagonal block of camera c
+// also forms c's normal block U, V (k_ba_camera's work, same bits) and writes them for the head of
+// the iteration, which runs inside the Cholesky kernel (lm_head); the Jacobi scale is the one of
+// iteration 0.
+template <bool FU>
 __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
   __shared__ double red[4][37];
+  __shared__ double redu[4][27];
   const int n_bp = d.live[1];
   if ((int)blockIdx.x >= n_bp) return;
   int bid;
@@ -703,6 +730,11 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
   // indices are read while this step's tiles load (same pairs, same order)
   const bool diag = bp.ch == bp.cl;
   double r6[6] = {0, 0, 0, 0, 0, 0};
+  double Uc[FU ? 21 : 1], Vc[FU ? 6 : 1];
+#pragma unroll
+  for (int k = 0; k < (FU ? 21 : 1); ++k) Uc[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < (FU ? 6 : 1); ++k) Vc[k] = 0.0;
   // A diagonal block's pairs are (e, e) for the camera's slots e in order (both plan builders),
   // so thread t meets the observations a0 + t, a0 + t + 256, ... of the rhs sum in its order.
   auto run = [&](auto diag_c) {
@@ -715,12 +747,30 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
       const bool two = q + 256 < end;
       const int qn = q + 512;
       if (qn < end) { p0n = d.pairs[qn]; p1n = d.pairs[qn + 256 < end ? qn + 256 : qn]; }
-      schur_pair<DG>(d, p0, acc, r6);
-      if (two) schur_pair<DG>(d, p1, acc, r6);
+      schur_pair<DG, DG && FU>(d, p0, acc, r6, Uc, Vc);
+      if (two) schur_pair<DG, DG && FU>(d, p1, acc, r6, Uc, Vc);
     }
   };
   if (diag) run(std::true_type{});
   else run(std::false_type{});
+  if (FU && diag) {  // the camera's U, V: k_ba_camera's reduction (wave butterfly, waves in order)
+#pragma unroll
+    for (int k = 0; k < 21; ++k) {
+      const double v = wave_sum(Uc[k]);
+      if (lane == 0) redu[wv][k] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const double v = wave_sum(Vc[k]);
+      if (lane == 0) redu[wv][21 + k] = v;
+    }
+    __syncthreads();
+    if (t < 27) {
+      const double v = ((redu[0][t] + redu[1][t]) + redu[2][t]) + redu[3][t];
+      if (t < 21) d.U_part[21 * bp.ch + t] = v;
+      else d.V_part[6 * bp.ch + t - 21] = v;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < 36; ++k) {
     const double v = wave_sum(acc[k]);
@@ -738,7 +788,9 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
         double v = 0.0;
         if (d.rank0) {  // camera block J^T J + D^2 once (sharded: U is already global)
           const double* sc = d.scale_pose + 6 * bp.ch;
-          v = d.U[21 * bp.ch + u21(i, j)] * sc[i] * sc[j];
+          const double u = FU ? ((redu[0][u21(i, j)] + redu[1][u21(i, j)]) + redu[2][u21(i, j)]) + redu[3][u21(i, j)]
+                              : d.U[21 * bp.ch + u21(i, j)];
+          v = u * sc[i] * sc[j];
           if (i == j) v += fmin(fmax(v, o.min_diag), o.max_diag) / S.radius;
         }
         band(A, W.bw, 6 * lh + i, 6 * lh + j) = v - a;
@@ -757,7 +809,8 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
     __syncthreads();
     if (t < 6) {
       const double r = (((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]) * d.scale_pose[6 * bp.ch + t];
-      const double vs = d.rank0 ? d.V[6 * bp.ch + t] * d.scale_pose[6 * bp.ch + t] : 0.0;
+      const double vv = FU ? ((redu[0][21 + t] + redu[1][21 + t]) + redu[2][21 + t]) + redu[3][21 + t] : d.V[6 * bp.ch + t];
+      const double vs = d.rank0 ? vv * d.scale_pose[6 * bp.ch + t] : 0.0;
       d.rhs_part[W.row_base + 6 * (bp.ch - W.pose_base) + t] = vs - r;
     }
   }
@@ -1747,16 +1800,21 @@ __host__ __device__ constexpr int chol2s_words(int n16, int bw) {
 
 // Waves: 0 / 1 chain (top / bottom side), 2 / 3 their update waves, 4 / 5 the inverses of L's
 // diagonal blocks (for the back-substitution), 6 / 7 the progressive staging of the band.
-__global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
+// HEAD (the fused iteration): wave 4 first runs the iteration head (lm_head, k_ba_lm_begin's work)
+// while the first panels factor; a head that ends the solve leaves the candidate unwritten.
+template <bool HEAD>
+__global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_bad;
+  __shared__ int s_head_done;
 #ifdef LORB_CHOL_STAMPS
   const unsigned long long st_entry = __builtin_amdgcn_s_memtime();
 #endif
   const int w = blockIdx.x;
   // window, state and failure flag requested together (one round trip before the band copy)
   const BaWin W = d.win[w];
-  const int done = d.st[w].done;
+  const WinState S0 = d.st[w];
+  const int done = S0.done;
   const double wfail = d.sharded ? d.wfail[w] : 0.0;
   if (done) return;
   if (wfail > 0.0) {
@@ -1817,6 +1875,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   if (t == 0) {
     *zero = 0.0;
     s_bad = 0;
+    s_head_done = 0;
     s_pdone[0] = 0; s_pdone[1] = 0;
     s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
     s_hand[0] = 0; s_hand[1] = 0; s_hand[2] = 0;
@@ -1870,6 +1929,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
       }
     }
     TR1(8 + side);
+  }
+  if (HEAD && wv == 4) {  // the iteration head while the first panels factor
+    const WinState S = lm_head<false>(d, o, w, lane, S0, W);
+    if (lane == 0) s_head_done = S.done;
   }
   // diagonal-block inverses (waves 4 / 5)
   if (wv == 4 || wv == 5) {
@@ -1999,8 +2062,9 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d) {
   TR1(13);
 #undef C2_STAMP
 #undef TR1
+  if (HEAD && s_head_done) return;  // the head ended the solve: no candidate
   for (int k = t; k < n; k += NT) d.ycam[W.row_base + k] = k < rt ? zt[k] : zb[n16 - 1 - k];
-  const int cur = d.st[w].cur;
+  const int cur = S0.cur;
   for (int ci2 = t; ci2 < W.n_poses; ci2 += NT) {
     const int c = W.pose_base + ci2;
     double xn[6];
@@ -2718,6 +2782,10 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
         for (int b = e0; b < e1; ++b) {
           const int cb = obs_cam[b];
           if (cb < 0 || cb > ca) continue;
+          // the reference keys a point's observations by Frame* (include/map_point.h:83): one per
+          // camera; the diagonal blocks rely on it (their pairs are (e, e))
+          if (cb == ca && a != b)
+            return lorb::set_error(ctx, LORB_E_INVALID, "window %d: a point observed twice by one camera", w);
           bmap[{ca - pose_base, cb - pose_base}].push_back(make_int2(obs_cm[a], obs_cm[b]));
           fc[ca - pose_base] = std::min(fc[ca - pose_base], cb - pose_base);
         }
@@ -2910,12 +2978,25 @@ int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   return LORB_OK;
 }
 
-// one LM iteration on the ctx stream
-int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
+// one LM iteration on the ctx stream.  first: the full sequence lin -> camera -> lm_begin -> schur
+// -> chol -> backsub -> lm_end.  Later iterations of an unsharded plan on the two-sided Cholesky run
+// fused: the diagonal Schur blocks form the camera normal blocks (k_ba_camera's work; the Jacobi
+// scale is iteration 0's) and the head runs inside the Cholesky (k_ba_lm_begin's work), so lin ->
+// schur -> chol -> backsub -> lm_end -- five launches instead of seven, the same bits.
+int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
   lorb_ctx* ctx = P->ctx;
   hipStream_t s = ctx->stream;
   const BaDev& d = P->dev;
-  LORB_TRY(enqueue_linearize(P, o));
+  static const bool no_fuse = [] { const char* e = getenv("LORB_NO_FUSE"); return e && e[0] == '1'; }();
+  const bool fused = !first && !P->comm && chol_kind_of(P) == 2 && !no_fuse;
+  if (fused) {
+    if (P->grid_pblk) {
+      lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
+      hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
+    }
+  } else {
+    LORB_TRY(enqueue_linearize(P, o));
+  }
   // The LDS Cholesky never writes env, and k_ba_schur rewrites every stored entry of every
   // block each iteration, so the band's structural zeros (set at plan creation) persist; the
   // in-place global variant needs them restored.
@@ -2923,7 +3004,8 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   if (P->env_total && !chol_in_lds && !P->comm) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   if (P->grid_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
-    hipLaunchKernelGGL(k_ba_schur, dim3(P->grid_bp), dim3(256), 0, s, d, o);
+    if (fused) hipLaunchKernelGGL(k_ba_schur<true>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
+    else hipLaunchKernelGGL(k_ba_schur<false>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
   }
   if (P->comm) {  // exchange 2: reduced camera system, rhs, point-block failure flags
     lorb::KernelTimer kt(ctx, LORB_K_ALLREDUCE);
@@ -2934,7 +3016,10 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o) {
   P->chol_kind = kind;
   if (P->Ctot && chol_2s) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
-    hipLaunchKernelGGL(k_ba_chol_2s, dim3(P->W), dim3(kChol2sThreads), sizeof(double) * (size_t)P->max_env_w, s, d);
+    if (fused)
+      hipLaunchKernelGGL(k_ba_chol_2s<true>, dim3(P->W), dim3(kChol2sThreads), sizeof(double) * (size_t)P->max_env_w, s, d, o);
+    else
+      hipLaunchKernelGGL(k_ba_chol_2s<false>, dim3(P->W), dim3(kChol2sThreads), sizeof(double) * (size_t)P->max_env_w, s, d, o);
   } else if (P->Ctot && chol_w) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
     hipLaunchKernelGGL(k_ba_chol_w, dim3(P->W), dim3(256), sizeof(double) * (size_t)P->max_env_w, s, d);
@@ -2976,7 +3061,7 @@ int enqueue_solve(lorb_ba_plan* P, const LMOpt& o) {
   LORB_CHECK_LAUNCH(ctx);
   // no iterations: one linearisation (cost, termination) as the head of a first iteration
   if (o.max_iter <= 0) return enqueue_linearize(P, o);
-  for (int it = 0; it < o.max_iter; ++it) LORB_TRY(enqueue_iteration(P, o));
+  for (int it = 0; it < o.max_iter; ++it) LORB_TRY(enqueue_iteration(P, o, it == 0));
   return LORB_OK;
 }
 

@@ -14,8 +14,8 @@
 //   4. the solution in double, caller order, plus the summary: one kernel, ONE device-to-host copy.
 // Fixed poses are padded to the plan's capacity with rows no observation references, which the
 // device build ignores.  Windows the device plans do not take (no cameras / points / observations,
-// a point observed twice by one camera, a point with kGB or more observations) run through
-// lorb_ba_local (the host-built plan on the same GPU kernels): there is no CPU path.
+// a point with kGB or more observations) run through lorb_ba_local (the host-built plan on the
+// same GPU kernels): there is no CPU path.
 #include <algorithm>
 
 #include "lorb_internal.h"
@@ -214,13 +214,14 @@ int lorb_ba_solver_solve(lorb_ba_solver* S, const lorb_ba_window* w, const lorb_
   } else {
     rc = lorb_ba_plan_update_dev(sl->plan, &wd);
   }
-  if (rc == LORB_E_INVALID || rc == LORB_E_UNSUPPORTED) {
-    // the host validation passed, so this is a structure the device plans do not take (a point seen
-    // twice by one camera, or a point with too many observations): the host-built plan takes it
+  if (rc == LORB_E_UNSUPPORTED) {
+    // a point with more observations than a device plan's point group holds: the host-built plan
+    // takes it (a point observed twice by one camera is an error in both builders)
     LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (!sl->plan) release(*sl);
     return solve_fallback(S, w, opt, pose_out, point_out, summary);
   }
+  if (rc != LORB_OK && !sl->plan) release(*sl);
   LORB_TRY(rc);
   // 3. LM (captured graph)  4. result + summary, one copy
   LORB_TRY(lorb_ba_plan_solve(sl->plan, opt));

@@ -62,8 +62,8 @@ def test_solver_windows_that_change(ctx):
 
 def test_solver_fallback_and_errors(ctx):
     """a point observed twice by one camera (the reference's std::map<Frame*, size_t> cannot hold
-    it, but lorb_ba_local accepts it) runs on the host-built plan; bad indices are rejected like
-    lorb_ba_local rejects them; an empty window returns."""
+    it) is rejected by both plan builders; bad indices are rejected like lorb_ba_local rejects them;
+    an empty window runs on the host-built plan; the solver stays usable after every error."""
     s = BASolver(ctx)
     try:
         w = synth.ba_window(seed=24, n_kf=6, n_pts=300, n_fixed=1, fixed_obs_per_kf=40)
@@ -71,8 +71,10 @@ def test_solver_fallback_and_errors(ctx):
         dup = dict(w, obs_point=np.append(w["obs_point"], w["obs_point"][k]),
                    obs_frame=np.append(w["obs_frame"], w["obs_frame"][k]),
                    obs_uv=np.concatenate([np.asarray(w["obs_uv"]).reshape(-1, 2), np.asarray(w["obs_uv"]).reshape(-1, 2)[k:k + 1]]))
-        check(s, dup, OPT10)
-        assert s.info()["host_plan_fallback"] == 1
+        with pytest.raises(LorbError, match="twice"):
+            s.solve(dup, OPT10)
+        with pytest.raises(LorbError, match="twice"):
+            ctx.ba_local([dup], OPT10)
         check(s, w, OPT10)
         assert s.info()["host_plan_fallback"] == 0
         bad = dict(w, obs_frame=np.where(np.arange(len(w["obs_frame"])) == 3, -5, w["obs_frame"]))
@@ -84,7 +86,7 @@ def test_solver_fallback_and_errors(ctx):
         empty = dict(w, point_init=np.zeros((0, 3), np.float32), obs_point=np.zeros(0, np.int32),
                      obs_frame=np.zeros(0, np.int32), obs_uv=np.zeros((0, 2), np.float32))
         P, X, sm = s.solve(empty, OPT10)
-        assert P.shape == (6, 6) and X.shape == (0, 3)
+        assert P.shape == (6, 6) and X.shape == (0, 3) and s.info()["host_plan_fallback"] == 1
         check(s, w, OPT10)  # still usable after the errors
     finally:
         s.close()
