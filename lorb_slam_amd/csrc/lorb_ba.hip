@@ -2509,11 +2509,11 @@ struct lorb_ba_devbuild {
   int* hist = nullptr; int* hoff = nullptr; int hist_cap = 0;  // camera-major block histograms
   int* cam_pt = nullptr;      // K_cap: point of each camera-major slot
   int* perm = nullptr;        // C: input camera -> plan camera
-  int* gstart = nullptr;      // group starts
-  int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0, gs_cap = 0;
+  int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0;
   std::vector<int> h_hdr, h_cov, h_cam;
   int* pinned = nullptr; size_t pinned_n = 0;
   double* sol_part = nullptr; size_t sol_n = 0;  // this rank's solve block (== the global one unsharded)
+  bool dirty = true;  // the build scratch needs a clearing fill (first build, or after a failed one)
   std::vector<double> h_red;                     // sharded: the build's host all-reduce
   // per-build structure uploaded in one copy: [BaWin | live (2) | perm (C) | cam_obs_off (C+1) | bp (up_bp_cap)]
   unsigned char* up_dev = nullptr; unsigned char* up_host = nullptr; int up_bp_cap = 0;
@@ -3142,26 +3142,36 @@ int plan_read(lorb_ba_plan* P, double* const* pose_out, double* const* point_out
 //   k_db_scatter counting sort by point: slot order within a point restored by k_db_segsort
 //                (stable: the caller's order within a point, as a stable radix sort gives it)
 //   k_db_cov     covisibility counts of camera pairs = popcount(bits_a & bits_b), per-camera counts
-//   k_db_gather  point-sorted structure arrays, per-block camera histograms (RCM labels)
+//   k_db_gather  point-sorted structure arrays, per-block camera histograms (RCM labels), initial
+//                values (float -> double, camera relabelling), point groups of <= kGB observations
+//                (weights k + 1, fixed-size bins), and the zeros the next build starts from
 //   k_db_scan1   camera-major block offsets
 //   k_db_place   counting sort of the optimised observations by camera (stable), camera slots
-//   k_db_groups  point groups of <= kGB observations (weights k + 1, fixed-size bins)
 //   k_db_pairs   per block pair: the points both cameras observe (binary search of the lower
 //                camera's point list staged in LDS)
-//   k_db_init    initial values (float -> double, camera relabelling)
 // ==========================================================================================
 
 namespace {
 
 
 
-// Build-time scratch of the device plan (one allocation, one clear per build):
+// Build-time scratch of the device plan (one allocation, cleared by the build before -- k_db_gather):
 //   pt_cnt[P_cap + 1] | hdr[8] | cov[C * C] | cam_cnt[C] | bits[C * Wd] (u64 words)
 // hdr: [0] valid observations, [1] largest count per point, [2] error flags, [3] points.
+// Runs of equal keys in consecutive lanes are combined before the atomics: the observations of one
+// keyframe are consecutive slots (the LocalMapping append), so their bitset words repeat across a
+// wave (new points have consecutive ids), and the observations of one point are consecutive in a
+// point-ordered window (the drop-in's), so their counts do.  A segmented inclusive scan over the
+// wave (runs end where the key changes) leaves each run's OR / count in its last lane, which does
+// one atomic; two lanes of one run setting the same bit are a point seen twice by one camera.
+__device__ __forceinline__ unsigned long long shfl_up_u64(unsigned long long v, int o) {
+  const int lo = __shfl_up((int)(v & 0xffffffffu), o, 64), hi = __shfl_up((int)(v >> 32), o, 64);
+  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
+}
 __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, int F, int Wd,
                                                  int* __restrict__ pt_cnt, int* __restrict__ hdr,
                                                  unsigned long long* __restrict__ bits) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
+  const int k = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63;
   const int n_obs_in = *w.d_n_obs, n_pt_in = *w.d_n_points;
   // live counts beyond the capacities are an error (flag 8); clamped, so nothing is touched past
   // the plan's allocations
@@ -3170,21 +3180,41 @@ __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, in
     hdr[3] = n_pt;
     if (n_obs_in > w.max_obs || n_pt_in > w.max_points || n_obs_in < 0 || n_pt_in < 0) atomicOr(&hdr[2], 8);
   }
-  if (k >= n_obs) return;
-  const int q = w.d_obs_point[k], f = w.d_obs_frame[k];
-  if (f >= -F && f < C) {
-    if (q < 0 || q >= n_pt) {
-      atomicOr(&hdr[2], 1);
-    } else {
-      atomicAdd(&pt_cnt[q], 1);
-      if (f >= 0) {
-        const unsigned long long m = 1ull << (q & 63);
-        if (atomicOr(&bits[(size_t)f * Wd + (q >> 6)], m) & m) atomicOr(&hdr[2], 4);
-      }
+  if ((k & ~63) >= n_obs) return;  // whole waves past the end (the scans below need full waves)
+  int q = -1, f = -1 - F - 1, err = 0;
+  if (k < n_obs) { q = w.d_obs_point[k]; f = w.d_obs_frame[k]; }
+  const bool slot = k < n_obs && f >= -F && f < C;  // an observation (fixed or optimised camera)
+  if (k < n_obs && f >= C) err |= 2;
+  if (slot && (q < 0 || q >= n_pt)) err |= 1;
+  const bool cnt = slot && !(err & 1);
+  const bool opt = cnt && f >= 0;
+  // per-point counts: runs of equal q
+  long long ckey = cnt ? q : -1 - (long long)lane;  // non-counting lanes are runs of their own
+  int c = cnt ? 1 : 0;
+  // camera x point bits: runs of equal (f, word)
+  long long bkey = opt ? (long long)f * Wd + (q >> 6) : -1 - (long long)lane;
+  unsigned long long m = opt ? 1ull << (q & 63) : 0ull;
+  bool dup = false;
+  bool cseg = lane == 0 || __shfl_up(ckey, 1, 64) != ckey;  // run heads
+  bool bseg = lane == 0 || __shfl_up(bkey, 1, 64) != bkey;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int cu = __shfl_up(c, o, 64);
+    const unsigned long long mu = shfl_up_u64(m, o);
+    const bool csu = __shfl_up((int)cseg, o, 64), bsu = __shfl_up((int)bseg, o, 64);
+    if (lane >= o) {
+      if (!cseg) { c += cu; cseg = csu; }
+      if (!bseg) { dup |= (m & mu) != 0; m |= mu; bseg = bsu; }
     }
-  } else if (f >= C) {
-    atomicOr(&hdr[2], 2);
   }
+  const bool ctail = lane == 63 || __shfl_down(ckey, 1, 64) != ckey;
+  const bool btail = lane == 63 || __shfl_down(bkey, 1, 64) != bkey;
+  if (cnt && ctail) atomicAdd(&pt_cnt[q], c);
+  if (opt && btail) {
+    if (atomicOr(&bits[(size_t)f * Wd + (q >> 6)], m) & m) err |= 4;
+  }
+  if (dup) err |= 4;
+  if (err) atomicOr(&hdr[2], err);
 }
 
 // One workgroup: out[0 .. n) = exclusive prefix sums of in[0 .. n) (n_dev: n = *n_dev + 1, the
@@ -3274,12 +3304,60 @@ __global__ __launch_bounds__(256) void k_db_cov(int C, int Wd, const unsigned lo
   }
 }
 
-// point-sorted structure arrays; per 256-observation block the plan-camera histogram (camera-major
-// hist[c * NB + block], fixed-camera observations not counted)
+// The work of a build that only needs the pre-readback results and the upload, in one launch:
+//  * point-sorted structure arrays; per 256-observation block (blocks < NB) the plan-camera
+//    histogram (camera-major hist[c * NB + block], fixed-camera observations not counted);
+//  * initial values (float -> double, camera relabelling) and camera activity (k_db_init);
+//  * point groups: group g = points [start(g), start(g + 1)), start(g) = the first point p with
+//    off[p] + p >= g S (weights k_p + 1, so a group holds <= kGB observations and points; trailing
+//    groups can be empty);
+//  * zeros: this rank's band, and the build scratch the next build accumulates into (camera x point
+//    bitsets, header max / error words; pt_cnt is left zero by k_db_scatter, cov / cam_cnt are
+//    rewritten whole by k_db_cov), so the next build needs no clearing fill.
+struct DbFused {
+  const int* perm;   // input camera -> plan camera
+  const int* gcam;   // observations per input camera, all ranks
+  int C, F, P, G, S, env_n, bits_n;
+  unsigned long long* bits;
+  int* hdr;
+};
+__device__ __forceinline__ int first_in_group(const int* __restrict__ pt_off, int P, long long bound) {
+  int lo = 0, hi = P;  // smallest p with pt_off[p] + p >= bound (P if none)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((long long)pt_off[mid] + mid >= bound) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
 __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d, int K, int C, int NB,
                                                    const int* __restrict__ key, const int* __restrict__ val,
-                                                   const int* __restrict__ perm, int* __restrict__ hist) {
+                                                   const int* __restrict__ perm, int* __restrict__ hist, DbFused f) {
   extern __shared__ int s_h[];  // C
+  const int gt = blockIdx.x * 256 + threadIdx.x, gs = gridDim.x * 256;
+  {  // initial values and camera activity
+    const int m = max(max(6 * f.C, 6 * f.F), 3 * f.P);
+    for (int i = gt; i < m; i += gs) {
+      if (i < 6 * f.C) {
+        const int c = i / 6, q = i - 6 * c;
+        d.x_init_pose[6 * f.perm[c] + q] = (double)w.d_pose_init[i];
+        if (q == 0) const_cast<int*>(d.cam_active)[f.perm[c]] = f.gcam[c] > 0;
+        if (q == 0) const_cast<int*>(d.cam_win)[c] = 0;
+      }
+      if (i < 6 * f.F) const_cast<double*>(d.fixed_pose)[i] = (double)w.d_fixed_pose[i];
+      if (i < 3 * f.P) d.x_init_pt[i] = (double)w.d_point_init[i];
+    }
+  }
+  for (int g = gt; g < f.G; g += gs) {  // point groups
+    const int s0 = first_in_group(d.pt_obs_off, f.P, (long long)g * f.S);
+    const int s1 = first_in_group(d.pt_obs_off, f.P, (long long)(g + 1) * f.S);
+    PBlk b;
+    b.win = 0; b.p0 = s0; b.cnt = s1 - s0; b.o0 = d.pt_obs_off[s0]; b.no = d.pt_obs_off[s1] - d.pt_obs_off[s0];
+    const_cast<PBlk*>(d.pblk)[g] = b;
+  }
+  for (int i = gt; i < f.env_n; i += gs) d.env_part[i] = 0.0;
+  for (int i = gt; i < f.bits_n; i += gs) f.bits[i] = 0ull;
+  if (gt == 0) { f.hdr[1] = 0; f.hdr[2] = 0; }
+  if ((int)blockIdx.x >= NB) return;  // uniform per workgroup
   for (int i = threadIdx.x; i < C; i += 256) s_h[i] = 0;
   __syncthreads();
   const int e = blockIdx.x * 256 + threadIdx.x;
@@ -3316,95 +3394,81 @@ __global__ __launch_bounds__(256) void k_db_place(BaDev d, int K, int NB, const 
   cam_pt[j] = d.obs_pt[e];
 }
 
-// point groups: point p (weight k_p + 1, exclusive weight prefix off[p] + p) goes to group
-// (off[p] + p) / S with S = kGB - max_weight + 1, so a group holds <= kGB observations and points
-__global__ __launch_bounds__(256) void k_db_group_starts(const int* __restrict__ pt_off, int P, int S,
-                                                         int* __restrict__ gstart) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= P) return;
-  const int g = (pt_off[p] + p) / S;
-  if (p == 0 || (pt_off[p - 1] + p - 1) / S != g) gstart[g] = p;
-}
 
-// group g = points [start(g), start(g + 1)); an empty bin starts where the next non-empty one does
-// (bins are at least as wide as any point's weight, so only trailing bins can be empty and the
-// forward search is short)
-__global__ __launch_bounds__(256) void k_db_groups(BaDev d, const int* __restrict__ pt_off, int P, int G,
-                                                   const int* __restrict__ gstart) {
-  const int g = blockIdx.x * 256 + threadIdx.x;
-  if (g >= G) return;
-  int s = P, e = P;
-  for (int h = g; h < G; ++h)
-    if (gstart[h] >= 0) { s = gstart[h]; break; }
-  for (int h = g + 1; h < G; ++h)
-    if (gstart[h] >= 0) { e = gstart[h]; break; }
-  PBlk b;
-  b.win = 0; b.p0 = s; b.cnt = e - s; b.o0 = pt_off[s]; b.no = pt_off[e] - pt_off[s];
-  const_cast<PBlk*>(d.pblk)[g] = b;
-}
 
-// one workgroup per (camera, camera) block: its pair list in point order.  The lower camera's
-// point ids (ascending) are staged in LDS for the binary searches when they fit.
-constexpr int kPairsLds = 8192;
+// one workgroup per (camera, camera) block: its pair list in point order.  A diagonal block's pairs
+// are (e, e) over the camera's slots.  Otherwise the lower camera's point ids (ascending) are staged
+// in LDS for the binary searches when they fit; each thread owns a run of up to kPR consecutive
+// slots of the higher camera, loads their point ids together (one memory round trip per batch, not
+// one per 256 slots), searches them and places its matches after one block scan of the run counts.
+constexpr int kPairsLds = 8192, kPR = 8;
 __global__ __launch_bounds__(256) void k_db_pairs(BaDev d, const int* __restrict__ cam_pt) {
   __shared__ int wsum[4];
   __shared__ int s_pt[kPairsLds];
   const BlockPair B = d.bp[blockIdx.x];
   const int h0 = d.cam_obs_off[B.ch], h1 = d.cam_obs_off[B.ch + 1];
   const int l0 = d.cam_obs_off[B.cl], l1 = d.cam_obs_off[B.cl + 1];
-  const int nl = l1 - l0;
-  const bool diag = B.ch == B.cl, lds = nl <= kPairsLds;
-  if (!diag && lds) {
-    for (int i = threadIdx.x; i < nl; i += 256) s_pt[i] = cam_pt[l0 + i];
+  const int nl = l1 - l0, t = threadIdx.x;
+  int2* out = const_cast<int2*>(d.pairs) + B.off;
+  if (B.ch == B.cl) {
+    for (int i = h0 + t; i < h1 && i - h0 < B.cnt; i += 256) out[i - h0] = make_int2(i, i);
+    return;
+  }
+  const bool lds = nl <= kPairsLds;
+  if (lds) {
+    for (int i = t; i < nl; i += 256) s_pt[i] = cam_pt[l0 + i];
     __syncthreads();
   }
   const int* lp = lds ? s_pt : cam_pt + l0;
-  int2* out = const_cast<int2*>(d.pairs) + B.off;
   int run = 0;
-  for (int base = h0; base < h1; base += 256) {
-    const int i = base + threadIdx.x;
-    int j = -1;
-    if (i < h1) {
-      if (diag) {
-        j = i;
-      } else {
-        const int p = cam_pt[i];
+  for (int base = h0; base < h1; base += 256 * kPR) {
+    const int nb = min(h1 - base, 256 * kPR), r0 = base + t * kPR;
+    int p[kPR], jv[kPR];
+#pragma unroll
+    for (int u = 0; u < kPR; ++u) p[u] = r0 + u < base + nb ? cam_pt[r0 + u] : -1;
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < kPR; ++u) {
+      int j = -1;
+      if (p[u] >= 0) {
         int lo = 0, hi = nl;
         while (lo < hi) {
           const int m = (lo + hi) >> 1;
-          if (lp[m] < p) lo = m + 1; else hi = m;
+          if (lp[m] < p[u]) lo = m + 1; else hi = m;
         }
-        if (lo < nl && lp[lo] == p) j = l0 + lo;
+        if (lo < nl && lp[lo] == p[u]) j = l0 + lo;
       }
+      jv[u] = j;
+      c += j >= 0;
     }
     int tot;
-    const int ex = lorb::block_excl_scan<256>(j >= 0 ? 1 : 0, wsum, &tot);
-    if (j >= 0 && run + ex < B.cnt) out[run + ex] = make_int2(i, j);
+    int o = run + lorb::block_excl_scan<256>(c, wsum, &tot);
+#pragma unroll
+    for (int u = 0; u < kPR; ++u)
+      if (jv[u] >= 0) {
+        if (o < B.cnt) out[o] = make_int2(r0 + u, jv[u]);
+        ++o;
+      }
     run += tot;
   }
 }
 
-__global__ __launch_bounds__(256) void k_db_init(lorb_ba_window_dev w, BaDev d, int C, int F, int P,
-                                                 const int* __restrict__ perm, const int* __restrict__ cam_cnt) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < 6 * C) {
-    const int c = i / 6, q = i - 6 * c;
-    d.x_init_pose[6 * perm[c] + q] = (double)w.d_pose_init[i];
-    if (q == 0) const_cast<int*>(d.cam_active)[perm[c]] = cam_cnt[c] > 0;
-    if (q == 0) const_cast<int*>(d.cam_win)[c] = 0;
-  }
-  if (i < 6 * F) const_cast<double*>(d.fixed_pose)[i] = (double)w.d_fixed_pose[i];
-  for (int k = i; k < 3 * P; k += gridDim.x * 256) d.x_init_pt[k] = (double)w.d_point_init[k];
-}
 
-// plan camera order -> caller order, as float (Frame::SetPose / MapPoint::SetWorldPos write-back)
+// plan camera order -> caller order, as float (Frame::SetPose / MapPoint::SetWorldPos write-back).
+// ring (the LocalMapping map's keyframe ring of R slots): caller pose c goes to slot (t0 + c) mod R.
 __global__ __launch_bounds__(256) void k_db_result(BaDev d, int C, int P, const int* __restrict__ perm,
-                                                   float* __restrict__ pose_out, float* __restrict__ pt_out) {
+                                                   float* __restrict__ pose_out, float* __restrict__ pt_out,
+                                                   float* __restrict__ ring, int R, int t0) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int cur = d.st[0].cur;
-  if (pose_out && i < 6 * C) {
+  if ((pose_out || ring) && i < 6 * C) {
     const int c = i / 6, q = i - 6 * c;
-    pose_out[i] = (float)d.x_pose[cur][6 * perm[c] + q];
+    const float v = (float)d.x_pose[cur][6 * perm[c] + q];
+    if (pose_out) pose_out[i] = v;
+    if (ring) {
+      const int r = (t0 + c) % R;
+      ring[6 * (r < 0 ? r + R : r) + q] = v;
+    }
   }
   if (pt_out)
     for (int k = i; k < 3 * P; k += gridDim.x * 256) pt_out[k] = (float)d.x_pt[cur][k];
@@ -3432,6 +3496,16 @@ __global__ __launch_bounds__(256) void k_db_result64(BaDev d, int C, int P, cons
 }  // namespace
 
 namespace lorb {
+int ba_plan_result_ring_dev(lorb_ba_plan* P, float* ring, int R, int t0, float* d_point_out) {
+  if (!P || !P->devb || !ring || R < 1) return LORB_E_INVALID;
+  const int C = P->Ctot, Pn = P->Ptot;
+  const int m = std::max(std::max(6 * C, 1), std::min(3 * Pn, 256 * 1024));
+  hipLaunchKernelGGL(k_db_result, dim3(lorb::ceil_div(m, 256)), dim3(256), 0, P->ctx->stream, P->dev, C, Pn,
+                     P->devb->perm, (float*)nullptr, d_point_out, ring, R, t0);
+  LORB_CHECK_LAUNCH(P->ctx);
+  return LORB_OK;
+}
+
 int ba_plan_result64_dev(lorb_ba_plan* P, double* d_out) {
   if (!P || !P->devb || !d_out) return LORB_E_INVALID;
   const int C = P->Ctot, Pn = P->Ptot;
@@ -3588,8 +3662,10 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   BaDev& d = P->dev;
   const int C = b.C, F = b.F, Kc = w->max_obs;
   // 1. per-point counts and camera x point bitsets; point offsets; counting sort by point
-  //    (stable); covisibility counts from the bitsets
-  LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
+  //    (stable); covisibility counts from the bitsets.  The scratch is left clear by the previous
+  //    build's k_db_gather; only a build that stopped before it (an error) leaves it dirty.
+  if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
+  b.dirty = true;
   const int nb_obs = lorb::ceil_div(std::max(Kc, 1), 256), nb_pt = lorb::ceil_div(std::max(b.P_cap, 1), 256);
   hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);
   hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1,
@@ -3707,7 +3783,6 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   PBlk* pb = const_cast<PBlk*>(d.pblk);
   int2* pr = const_cast<int2*>(d.pairs);
   LORB_TRY(grow(P, &pb, &b.pblk_cap, (size_t)std::max(G, 1)));
-  LORB_TRY(grow(P, &b.gstart, &b.gs_cap, (size_t)std::max(G, 1)));
   LORB_TRY(grow(P, &pr, &b.pairs_cap, (size_t)std::max(n_pairs, 1)));
   d.pblk = pb; d.pairs = pr;
   {
@@ -3731,33 +3806,27 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     const size_t bytes = b.off_bp + sizeof(BlockPair) * bps.size();
     LORB_HIP(ctx, hipMemcpyAsync(b.up_dev, h, bytes, hipMemcpyHostToDevice, s));
   }
-  // 4. structure kernels
+  // 4. structure kernels: gather (+ initial values, point groups, zeros), the camera-major block
+  //    offsets, the stable placement by camera, the block pair lists
+  const int NB = lorb::ceil_div(K, 256);
+  if ((size_t)std::max(NB, 1) * C > (size_t)b.hist_cap) {
+    LORB_TRY(grow(P, &b.hist, &b.hist_cap, (size_t)std::max(NB, 1) * C));
+    int cap2 = 0;
+    LORB_TRY(grow(P, &b.hoff, &cap2, (size_t)b.hist_cap));
+  }
+  {
+    // this rank's band starts from zeros (blocks it has no pairs of stay zero; sharded: the
+    // all-reduce writes the global band every iteration)
+    DbFused f{b.perm, b.gcam, C, F, Pn, G, S, P->env_total, C * b.Wd, b.bits, b.hdr};
+    hipLaunchKernelGGL(k_db_gather, dim3(std::max(NB, 1)), dim3(256), sizeof(int) * C, s, *w, d, K, C, NB, b.key_out,
+                       b.val_out, b.perm, b.hist, f);
+    b.dirty = false;
+  }
   if (K > 0) {
-    const int NB = lorb::ceil_div(K, 256);
-    if ((size_t)NB * C > (size_t)b.hist_cap) {
-      LORB_TRY(grow(P, &b.hist, &b.hist_cap, (size_t)NB * C));
-      int cap2 = 0;
-      LORB_TRY(grow(P, &b.hoff, &cap2, (size_t)b.hist_cap));
-    }
-    hipLaunchKernelGGL(k_db_gather, dim3(NB), dim3(256), sizeof(int) * C, s, *w, d, K, C, NB, b.key_out, b.val_out,
-                       b.perm, b.hist);
     hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.hist, b.hoff, NB * C, nullptr, nullptr);
     hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), 0, s, d, K, NB, b.hoff, b.cam_pt);
   }
-  if (G > 0) {
-    LORB_HIP(ctx, hipMemsetAsync(b.gstart, 0xff, sizeof(int) * G, s));
-    hipLaunchKernelGGL(k_db_group_starts, dim3(lorb::ceil_div(Pn, 256)), dim3(256), 0, s, d.pt_obs_off, Pn, S, b.gstart);
-    hipLaunchKernelGGL(k_db_groups, dim3(lorb::ceil_div(G, 256)), dim3(256), 0, s, d, d.pt_obs_off, Pn, G, b.gstart);
-  }
   if (!bps.empty()) hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), 0, s, d, b.cam_pt);
-  {
-    const int m = std::max(std::max(6 * C, 6 * F), std::min(3 * Pn, 256 * 1024));
-    if (m > 0)
-      hipLaunchKernelGGL(k_db_init, dim3(lorb::ceil_div(m, 256)), dim3(256), 0, s, *w, d, C, F, Pn, b.perm, b.gcam);
-  }
-  // this rank's band starts from zeros (blocks it has no pairs of stay zero; sharded: the all-reduce
-  // writes the global band every iteration)
-  if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env_part, 0, sizeof(double) * P->env_total, s));
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
 }
@@ -3845,7 +3914,7 @@ int lorb_ba_plan_result_dev(lorb_ba_plan* plan, float* d_pose_out, float* d_poin
   const int m = std::max(6 * C, std::min(3 * Pn, 256 * 1024));
   if (m > 0)
     hipLaunchKernelGGL(k_db_result, dim3(lorb::ceil_div(m, 256)), dim3(256), 0, plan->ctx->stream, plan->dev, C, Pn,
-                       plan->devb->perm, d_pose_out, d_point_out);
+                       plan->devb->perm, d_pose_out, d_point_out, (float*)nullptr, 1, 0);
   LORB_CHECK_LAUNCH(plan->ctx);
   return LORB_OK;
 }

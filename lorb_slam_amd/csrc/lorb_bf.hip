@@ -69,12 +69,9 @@ __device__ __forceinline__ uint32_t hamming256(const uint4& a0, const uint4& a1,
 // QPL = lane-side descriptors per thread (1, 2 or 4; LORB_BF_QPL): a block covers 256*QPL lane items; every
 // uniform descriptor loaded into SGPRs feeds QPL distance chains.
 template <bool TOP2, int QPL>
-__global__ __launch_bounds__(256) void k_bf_scan(const uint4* __restrict__ lane_desc,
-                                                 const uint4* __restrict__ uni_desc,
-                                                 const BfTile* __restrict__ tiles,
-                                                 uint32_t* __restrict__ k1_out,
-                                                 uint32_t* __restrict__ k2_out) {
-  const BfTile tl = tiles[blockIdx.x];
+__device__ __forceinline__ void scan_tile(const uint4* __restrict__ lane_desc, const uint4* __restrict__ uni_desc,
+                                          const BfTile& tl, uint32_t* __restrict__ k1_out,
+                                          uint32_t* __restrict__ k2_out) {
   uint4 a[QPL][2];
   uint32_t k1[QPL], k2[QPL];
 #pragma unroll
@@ -134,6 +131,52 @@ __global__ __launch_bounds__(256) void k_bf_scan(const uint4* __restrict__ lane_
       if (TOP2) k2_out[tl.out_base + l] = k2[r];
     }
   }
+}
+
+template <bool TOP2, int QPL>
+__global__ __launch_bounds__(256) void k_bf_scan(const uint4* __restrict__ lane_desc,
+                                                 const uint4* __restrict__ uni_desc,
+                                                 const BfTile* __restrict__ tiles,
+                                                 uint32_t* __restrict__ k1_out,
+                                                 uint32_t* __restrict__ k2_out) {
+  scan_tile<TOP2, QPL>(lane_desc, uni_desc, tiles[blockIdx.x], k1_out, k2_out);
+}
+
+// One problem (the LocalMapping step's SearchLocalPoints): the tile of workgroup b is computed,
+// not read from an uploaded table -- chunk c = b / lane_tiles, lane tile b % lane_tiles, the order
+// of build_tiles -- and the crossCheck query keys (kinit) are set to all-ones on the way.
+struct BfGrid1 {
+  int nl, nu, n_chunks, lt, lane_tiles;
+};
+template <bool TOP2, int QPL>
+__global__ __launch_bounds__(256) void k_bf_scan1(const uint4* __restrict__ lane_desc,
+                                                  const uint4* __restrict__ uni_desc, BfGrid1 g,
+                                                  uint32_t* __restrict__ k1_out, uint32_t* __restrict__ k2_out,
+                                                  unsigned long long* __restrict__ kinit, int n_init) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n_init; i += gridDim.x * 256) kinit[i] = ~0ull;
+  const int c = blockIdx.x / g.lane_tiles, t = (blockIdx.x - c * g.lane_tiles) * g.lt;
+  const int a = (int)((int64_t)g.nu * c / g.n_chunks), b = (int)((int64_t)g.nu * (c + 1) / g.n_chunks);
+  BfTile tl;
+  tl.lane_base = t;
+  tl.lane_count = min(g.lt, g.nl - t);
+  tl.uni_base = a;
+  tl.uni_count = b - a;
+  tl.uni_local0 = a;
+  tl.out_base = c * g.nl + t;
+  scan_tile<TOP2, QPL>(lane_desc, uni_desc, tl, k1_out, k2_out);
+}
+
+// One problem, crossCheck: each train's nearest query (the minimum over the chunks' keys) offered
+// to that query (k_cc_scatter's atomicMin) in the same launch
+__global__ __launch_bounds__(256) void k_cc_merge1(const uint32_t* __restrict__ k1p, int nt, int n_chunks,
+                                                   unsigned long long* __restrict__ qkey) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nt) return;
+  uint32_t k = kSentinel;
+  for (int c = 0; c < n_chunks; ++c) k = min(k, k1p[(size_t)c * nt + t]);
+  if (k >= kSentinel) return;
+  const unsigned long long v = ((unsigned long long)(k >> kIdxBits) << 32) | (unsigned)t;
+  atomicMin(&qkey[k & kIdxMask], v);
 }
 
 // merge chunk partials: part[c * n + i] -> out[i]
@@ -239,10 +282,11 @@ __global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* _
                                                      int32_t* __restrict__ cc_dist,
                                                      int32_t* __restrict__ match_train,
                                                      int32_t* __restrict__ n_matches,
-                                                     double* __restrict__ ex, int np) {
+                                                     double* __restrict__ ex, int np, int nq1 = 0, int nt1 = 0) {
   const int p = blockIdx.x;
-  const int q0 = q_off[p], q1 = q_off[p + 1];
-  const bool has_t = t_off[p + 1] > t_off[p];
+  // q_off == nullptr: one problem with nq1 queries and nt1 trains (offsets passed by value)
+  const int q0 = q_off ? q_off[p] : 0, q1 = q_off ? q_off[p + 1] : nq1;
+  const bool has_t = q_off ? t_off[p + 1] > t_off[p] : nt1 > 0;
   __shared__ int s_min[256];
   __shared__ int s_cnt[256];
   int mn = 0x7fffffff;
@@ -471,6 +515,52 @@ int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, con
   return LORB_OK;
 }
 
+// lorb_bf_match_dev for ONE problem with nothing uploaded: tiles computed in the scan kernel (which
+// also clears the query keys), chunk merge + crossCheck scatter in one launch, offsets passed by
+// value to the finalisation.  Same outputs, bit for bit, as the general path.
+int match1_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int32_t* d_cc_train,
+               int32_t* d_cc_dist, int32_t* d_match_train, int32_t* d_n_matches) {
+  unsigned long long* qkey = nullptr;
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_QKEY, (size_t)std::max(nq, 1), &qkey));
+  if (nt > 0 && nq > 0) {
+    // reverse pass: lanes = trains, uniform = queries -> nearest query per train
+    if (nq > (int)kIdxMask) return lorb::set_error(ctx, LORB_E_INVALID, "problem 0: %d uniform items > 2^23-1", nq);
+    static const int qpl = [] {
+      const char* e = getenv("LORB_BF_QPL");
+      const int v = e ? atoi(e) : 2;
+      return v == 1 || v == 4 ? v : 2;
+    }();
+    const int32_t l_off[2] = {0, nt}, u_off[2] = {0, nq};
+    std::vector<BfTile> tiles;  // (only the chunk count is used)
+    int n_chunks = 1;
+    LORB_TRY(build_tiles(ctx, 1, l_off, u_off, 256 * qpl, tiles, &n_chunks));
+    const int lt = 256 * qpl;
+    BfGrid1 g{nt, nq, n_chunks, lt, (nt + lt - 1) / lt};
+    uint32_t* k1 = nullptr;
+    LORB_TRY(lorb::scratch_t(ctx, S_BF_K1, (size_t)nt * n_chunks, &k1));
+    const unsigned nb = (unsigned)(g.lane_tiles * n_chunks);
+    {
+      lorb::KernelTimer kt(ctx, LORB_K_BF_SCAN_TOP1);
+      if (qpl == 2)
+        hipLaunchKernelGGL((k_bf_scan1<false, 2>), dim3(nb), dim3(256), 0, ctx->stream, reinterpret_cast<const uint4*>(d_t),
+                           reinterpret_cast<const uint4*>(d_q), g, k1, (uint32_t*)nullptr, qkey, nq);
+      else if (qpl == 4)
+        hipLaunchKernelGGL((k_bf_scan1<false, 4>), dim3(nb), dim3(256), 0, ctx->stream, reinterpret_cast<const uint4*>(d_t),
+                           reinterpret_cast<const uint4*>(d_q), g, k1, (uint32_t*)nullptr, qkey, nq);
+      else
+        hipLaunchKernelGGL((k_bf_scan1<false, 1>), dim3(nb), dim3(256), 0, ctx->stream, reinterpret_cast<const uint4*>(d_t),
+                           reinterpret_cast<const uint4*>(d_q), g, k1, (uint32_t*)nullptr, qkey, nq);
+    }
+    hipLaunchKernelGGL(k_cc_merge1, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, k1, nt, n_chunks, qkey);
+  } else if (nq > 0) {
+    LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, ctx->stream));
+  }
+  hipLaunchKernelGGL(k_cc_finalize<0>, dim3(1), dim3(256), 0, ctx->stream, qkey, (const int32_t*)nullptr,
+                     (const int32_t*)nullptr, d_cc_train, d_cc_dist, d_match_train, d_n_matches, (double*)nullptr, 1, nq, nt);
+  LORB_CHECK_LAUNCH(ctx);
+  return LORB_OK;
+}
+
 int check_offsets(lorb_ctx* ctx, int np, const int32_t* a, const int32_t* b) {
   if (!ctx) return LORB_E_INVALID;
   if (np < 0 || (np > 0 && (!a || !b))) return lorb::set_error(ctx, LORB_E_INVALID, "bad problem offsets");
@@ -534,6 +624,7 @@ int lorb_bf_match_dev(lorb_ctx* ctx, int32_t np, const uint8_t* d_q, const int32
   LORB_TRY(check_offsets(ctx, np, q_off, t_off));
   if (np == 0) return LORB_OK;
   const int nq = q_off[np], nt = t_off[np];
+  if (np == 1) return match1_dev(ctx, d_q, nq, d_t, nt, d_cc_train, d_cc_dist, d_match_train, d_n_matches);
   uint32_t *k1 = nullptr, *k2 = nullptr;
   unsigned long long* qkey = nullptr;
   int32_t* d_off = nullptr;

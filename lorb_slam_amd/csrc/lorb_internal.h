@@ -90,6 +90,9 @@ int comm_allreduce_host(lorb_comm* comm, double* h_buf, size_t n, int op);
 // the LM summary, into d_out = [poses 6C | points 3P | iterations, successful, termination, initial
 // cost, final cost] (async on the plan's stream)
 int ba_plan_result64_dev(lorb_ba_plan* P, double* d_out);
+// the same as lorb_ba_plan_result_dev with the poses written into a keyframe ring (pose c of the
+// window to slot (t0 + c) mod R, 6 floats each) instead of a pose array
+int ba_plan_result_ring_dev(lorb_ba_plan* P, float* ring, int R, int t0, float* d_point_out);
 
 // grow-only scratch: returns device pointer in *out
 int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out);
@@ -257,6 +260,28 @@ __device__ __forceinline__ int block_excl_max(int v, int lo, int* wmax) {
   __syncthreads();
   return max(pre, ex);
 }
+
+// A 4x4 float matrix passed by value as a kernel argument (no upload).
+struct Mat4f {
+  float v[16];
+};
+
+// Frame::UnprojectStereo for one keypoint with depth z > 0 (src/frame.cpp:335-356): camera
+// coordinates in float, then Twc * [x y z 1] accumulated in double as cv::Mat's float gemm does.
+// Shared by k_unproject and the LocalMapping append (compiled -ffp-contract=off: same bits).
+__device__ __forceinline__ void unproject_point(float fx, float fy, float cx, float cy, const Mat4f& Twc, float u,
+                                                float v, float z, float* out) {
+  const float xx = (u - cx) * z / fx;
+  const float yy = (v - cy) * z / fy;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const double s = (double)Twc.v[4 * r] * xx + (double)Twc.v[4 * r + 1] * yy + (double)Twc.v[4 * r + 2] * z +
+                     (double)Twc.v[4 * r + 3] * 1.0f;
+    out[r] = (float)s;
+  }
+}
+// cv::Mat::inv() of a 4x4 CV_32F (hal::LU32f), host side (lorb_window.hip)
+bool inv4_lu32f(const float* A, float* out);
 
 // Four counters (plain POD: HIP's int4 member proxies are avoided in arithmetic-heavy code).
 struct I4 {

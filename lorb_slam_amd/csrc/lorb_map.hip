@@ -38,7 +38,7 @@ struct MapDev {
   int* flag_pt; int* newid; int* flag_obs; int* newpos;  // newid / newpos: scans within kScanTile tiles
   int* tile_tot;  // tile sums of the two scans: [0, ntP) points, then observations
   float* ring;   // R x 6 keyframe poses, slot = kf mod R
-  float* pose_init; float* fixed; float* pose_out;
+  float* pose_init; float* fixed;
   int P_cap, K_cap, W, F, R;
 };
 
@@ -47,69 +47,58 @@ struct Pose6 { float v[6]; };
 __device__ __forceinline__ int ring_slot(int kf, int R) { const int r = kf % R; return r < 0 ? r + R : r; }
 
 // step 1 + 2: one workgroup, keypoints in order.  A matched keypoint adds an observation of its map
-// point; an unmatched one with depth > 0 adds a new point (and its observation).  Observations and
-// new points are appended in keypoint order.
+// point; an unmatched one with depth > 0 adds a new point at Frame::UnprojectStereo
+// (src/frame.cpp:335-356, lorb::unproject_point) and its observation.  Observations and new points
+// are appended in keypoint order: thread t owns a run of consecutive keypoints, one block scan of
+// three counters (observations, new points, matches) places every run.
 __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Pose6 pose, const int* __restrict__ mt,
-                                                     const float* __restrict__ xyz, const uint8_t* __restrict__ kdesc,
-                                                     const float* __restrict__ x, const float* __restrict__ y,
-                                                     const float* __restrict__ depth) {
-  __shared__ int wsum[16];
-  __shared__ int s_ok;
+                                                     lorb::Mat4f Twc, float fx, float fy, float cx, float cy,
+                                                     const uint8_t* __restrict__ kdesc, const float* __restrict__ x,
+                                                     const float* __restrict__ y, const float* __restrict__ depth) {
+  __shared__ lorb::I4 wsum[16];
   const int t = threadIdx.x;
   const int P0 = m.cnt[0], K0 = m.cnt[1];
-  // pass 1: totals
-  int n_obs = 0, n_new = 0, n_mat = 0;
-  for (int base = 0; base < n; base += 1024) {
-    const int q = base + t;
-    const bool mat = q < n && mt[q] >= 0;
-    const bool nw = q < n && !mat && depth[q] > 0.0f;
-    int a, b, c;
-    lorb::block_excl_scan_1024(mat || nw, wsum, &a);
-    lorb::block_excl_scan_1024(nw, wsum, &b);
-    lorb::block_excl_scan_1024(mat, wsum, &c);
-    n_obs += a; n_new += b; n_mat += c;
+  const int R = (n + 1023) / 1024, q0 = min(t * R, n), q1 = min(q0 + R, n);
+  lorb::I4 c = {{0, 0, 0, 0}};
+  for (int q = q0; q < q1; ++q) {
+    const bool mat = mt[q] >= 0;
+    const bool nw = !mat && depth[q] > 0.0f;
+    c.v[0] += mat || nw; c.v[1] += nw; c.v[2] += mat;
   }
+  lorb::I4 tot;
+  const lorb::I4 ex = lorb::block_excl_scan4<1024>(c, wsum, &tot);
+  const bool ok = (P0 + tot.v[1] <= m.P_cap) && (K0 + tot.v[0] <= m.K_cap);
   if (t == 0) {
-    s_ok = (P0 + n_new <= m.P_cap) && (K0 + n_obs <= m.K_cap);
-    m.cnt[2] = s_ok ? 0 : 1;  // this step's capacity flag (no separate clear)
-    if (!s_ok) { m.cnt[3] = 0; m.cnt[4] = 0; m.cnt[5] = n_mat; }  // the attempt appended nothing
+    m.cnt[2] = ok ? 0 : 1;  // this step's capacity flag (no separate clear)
+    if (!ok) { m.cnt[3] = 0; m.cnt[4] = 0; m.cnt[5] = tot.v[2]; }  // the attempt appended nothing
   }
-  __syncthreads();
-  if (!s_ok) return;  // the map is left exactly as it was (the host stops the step here)
+  if (!ok) return;  // the map is left exactly as it was (the host stops the step here)
   if (t < 6) m.ring[6 * ring_slot(kf, m.R) + t] = pose.v[t];
-  int ro = 0, rn = 0;
-  for (int base = 0; base < n; base += 1024) {
-    const int q = base + t;
-    const bool mat = q < n && mt[q] >= 0;
-    const bool nw = q < n && !mat && depth[q] > 0.0f;
-    int to, tn;
-    const int eo = lorb::block_excl_scan_1024(mat || nw, wsum, &to);
-    const int en = lorb::block_excl_scan_1024(nw, wsum, &tn);
-    if (mat || nw) {
-      int p;
-      if (nw) {
-        p = P0 + rn + en;
-        m.pos[3 * p + 0] = xyz[3 * q + 0];
-        m.pos[3 * p + 1] = xyz[3 * q + 1];
-        m.pos[3 * p + 2] = xyz[3 * q + 2];
-        const uint4* s = reinterpret_cast<const uint4*>(kdesc + 32 * (size_t)q);
-        uint4* d = reinterpret_cast<uint4*>(m.desc + 32 * (size_t)p);
-        d[0] = s[0]; d[1] = s[1];
-      } else {
-        p = mt[q];
-      }
-      const int k = K0 + ro + eo;
-      m.obs_pt[k] = p;
-      m.obs_kf[k] = kf;
-      m.obs_uv[2 * k + 0] = x[q];
-      m.obs_uv[2 * k + 1] = y[q];
+  int ko = K0 + ex.v[0], pn = P0 + ex.v[1];
+  for (int q = q0; q < q1; ++q) {
+    const int a = mt[q];
+    const float z = depth[q];
+    const bool mat = a >= 0, nw = !mat && z > 0.0f;
+    if (!(mat || nw)) continue;
+    int p = a;
+    if (nw) {
+      p = pn++;
+      float X[3];
+      lorb::unproject_point(fx, fy, cx, cy, Twc, x[q], y[q], z, X);
+      m.pos[3 * p + 0] = X[0]; m.pos[3 * p + 1] = X[1]; m.pos[3 * p + 2] = X[2];
+      const uint4* sd = reinterpret_cast<const uint4*>(kdesc + 32 * (size_t)q);
+      uint4* dd = reinterpret_cast<uint4*>(m.desc + 32 * (size_t)p);
+      dd[0] = sd[0]; dd[1] = sd[1];
     }
-    ro += to; rn += tn;
+    const int k = ko++;
+    m.obs_pt[k] = p;
+    m.obs_kf[k] = kf;
+    m.obs_uv[2 * k + 0] = x[q];
+    m.obs_uv[2 * k + 1] = y[q];
   }
-  __syncthreads();
   if (t == 0) {
-    m.cnt[0] = P0 + n_new; m.cnt[1] = K0 + n_obs;
-    m.cnt[3] = n_new; m.cnt[4] = n_obs; m.cnt[5] = n_mat;
+    m.cnt[0] = P0 + tot.v[1]; m.cnt[1] = K0 + tot.v[0];
+    m.cnt[3] = tot.v[1]; m.cnt[4] = tot.v[0]; m.cnt[5] = tot.v[2];
   }
 }
 
@@ -144,9 +133,15 @@ __device__ __forceinline__ int new_pos(const MapDev& m, int ntP, int i) {
   return m.newpos[i] + tile_base(m.tile_tot + ntP, i / lorb::kScanTile);
 }
 
-// stable gathers into the alternate buffers; observation slots as lorb_ba_window_dev wants them
+// stable gathers into the alternate buffers; observation slots as lorb_ba_window_dev wants them.
+// Workgroup 0 also writes the new counts and the window's initial / fixed poses from the ring.
 __global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, int t0, int ntP) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0) {
+    if (i == 0) { m.cnt[0] = new_id(m, Pb); m.cnt[1] = new_pos(m, ntP, Kb); }
+    for (int j = i; j < 6 * m.W; j += 256) m.pose_init[j] = m.ring[6 * ring_slot(t0 + j / 6, m.R) + j % 6];
+    for (int j = i; j < 6 * m.F; j += 256) m.fixed[j] = m.ring[6 * ring_slot(t0 - 1 - j / 6, m.R) + j % 6];
+  }
   const int fp = i < Pb ? m.flag_pt[i] : 0;
   if (fp) {
     m.flag_pt[i] = 0;  // cleared for the next slide (only this thread reads it here)
@@ -182,19 +177,6 @@ __global__ __launch_bounds__(1024) void k_map_scans(MapDev m, int Pb, int Kb, in
   if (threadIdx.x == 0) m.tile_tot[blockIdx.x] = tot;
 }
 
-// new counts; the window's initial poses and the fixed poses from the ring
-__global__ __launch_bounds__(256) void k_map_window(MapDev m, int Pb, int Kb, int t0, int ntP) {
-  const int i = threadIdx.x;
-  if (i == 0) { m.cnt[0] = new_id(m, Pb); m.cnt[1] = new_pos(m, ntP, Kb); }
-  for (int j = i; j < 6 * m.W; j += 256) m.pose_init[j] = m.ring[6 * ring_slot(t0 + j / 6, m.R) + j % 6];
-  for (int j = i; j < 6 * m.F; j += 256) m.fixed[j] = m.ring[6 * ring_slot(t0 - 1 - j / 6, m.R) + j % 6];
-}
-
-// Frame::SetPose write-back of the solved window poses into the ring
-__global__ __launch_bounds__(256) void k_map_writeback(MapDev m, int t0) {
-  for (int j = threadIdx.x; j < 6 * m.W; j += 256) m.ring[6 * ring_slot(t0 + j / 6, m.R) + j % 6] = m.pose_out[j];
-}
-
 }  // namespace
 
 struct lorb_map {
@@ -208,7 +190,7 @@ struct lorb_map {
   bool prof = false;
   double prof_ms[8] = {};
   int prof_n = 0;
-  int* cc_t = nullptr; int* cc_d = nullptr; int* mt = nullptr; int* nm = nullptr; float* xyz = nullptr;
+  int* cc_t = nullptr; int* cc_d = nullptr; int* mt = nullptr; int* nm = nullptr;
   int* pinned = nullptr;
   lorb_ba_plan* plan = nullptr;
   std::vector<void*> allocs;
@@ -252,12 +234,12 @@ int map_alloc(lorb_map* M, const lorb_map_init* in) {
   LORB_TRY(malloc_n(M, K + 1, &m.flag_obs)); LORB_TRY(malloc_n(M, K + 1, &m.newpos));
   LORB_TRY(malloc_n(M, (P + 1 + K + 1) / lorb::kScanTile + 2, &m.tile_tot));
   LORB_TRY(malloc_n(M, 6 * (size_t)m.R, &m.ring));
-  LORB_TRY(malloc_n(M, 6 * (size_t)m.W, &m.pose_init)); LORB_TRY(malloc_n(M, 6 * (size_t)m.W, &m.pose_out));
+  LORB_TRY(malloc_n(M, 6 * (size_t)m.W, &m.pose_init));
   LORB_TRY(malloc_n(M, 6 * (size_t)std::max(m.F, 1), &m.fixed));
   const size_t n = (size_t)std::max(in->max_keypoints, 1);
   M->n_cap = (int)n;
   LORB_TRY(malloc_n(M, n, &M->cc_t)); LORB_TRY(malloc_n(M, n, &M->cc_d)); LORB_TRY(malloc_n(M, n, &M->mt));
-  LORB_TRY(malloc_n(M, (size_t)1, &M->nm)); LORB_TRY(malloc_n(M, 3 * n, &M->xyz));
+  LORB_TRY(malloc_n(M, (size_t)1, &M->nm));
   LORB_HIP(M->ctx, hipHostMalloc(reinterpret_cast<void**>(&M->pinned), sizeof(int) * 8));
   return LORB_OK;
 }
@@ -283,9 +265,8 @@ int map_slide(lorb_map* M, int t0, int Pb, int Kb) {
   hipLaunchKernelGGL(k_map_obs_flag, dim3(lorb::ceil_div(Kb + 1, 256)), dim3(256), 0, s, m, Kb, t0);
   const int ntP = lorb::ceil_div(Pb + 1, lorb::kScanTile), ntK = lorb::ceil_div(Kb + 1, lorb::kScanTile);
   hipLaunchKernelGGL(k_map_scans, dim3(ntP + ntK), dim3(1024), 0, s, m, Pb, Kb, ntP);
-  const int nmax = std::max(Pb, Kb);
-  if (nmax > 0) hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, t0, ntP);
-  hipLaunchKernelGGL(k_map_window, dim3(1), dim3(256), 0, s, m, Pb, Kb, t0, ntP);
+  const int nmax = std::max(std::max(Pb, Kb), 1);
+  hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, t0, ntP);
   LORB_CHECK_LAUNCH(ctx);
   std::swap(m.pos, m.pos2); std::swap(m.desc, m.desc2); std::swap(m.obs_pt, m.obs_pt2);
   std::swap(m.obs_kf, m.obs_kf2); std::swap(m.obs_uv, m.obs_uv2);
@@ -390,13 +371,15 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
     LORB_HIP(ctx, hipMemsetAsync(M->mt, 0xff, sizeof(int) * (size_t)n, s));
   }
   LORB_TRY(mark(0));
-  // 2. UnprojectStereo of every keypoint (used where depth > 0 and unmatched)
-  if (n > 0) LORB_TRY(lorb_unproject_stereo_dev(ctx, frame, Tcw, n, d_x, d_y, d_depth, M->xyz));
   LORB_TRY(mark(1));
-  // 3. AddObservation / new points, keyframe pose into the ring
+  // 2 + 3. AddObservation / new points at UnprojectStereo (Twc = mTcw.inv(), src/frame.cpp:350),
+  // keyframe pose into the ring
   Pose6 p6;
   for (int q = 0; q < 6; ++q) p6.v[q] = pose[q];
-  hipLaunchKernelGGL(k_map_append, dim3(1), dim3(1024), 0, s, m, n, kf, p6, M->mt, M->xyz, d_desc, d_x, d_y, d_depth);
+  lorb::Mat4f Twc;
+  lorb::inv4_lu32f(Tcw, Twc.v);
+  hipLaunchKernelGGL(k_map_append, dim3(1), dim3(1024), 0, s, m, n, kf, p6, M->mt, Twc, frame->fx, frame->fy, frame->cx,
+                     frame->cy, d_desc, d_x, d_y, d_depth);
   LORB_CHECK_LAUNCH(ctx);
   M->last_n = n;
   // Capacity: n keypoints add at most n points and n observations.  When that bound does not fit,
@@ -422,9 +405,8 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   // 6. LocalPoseOptimization + float write-back of poses (ring) and points (map)
   LORB_TRY(lorb_ba_plan_solve(M->plan, opt));
   LORB_TRY(mark(5));
-  LORB_TRY(lorb_ba_plan_result_dev(M->plan, m.pose_out, m.pos));
-  hipLaunchKernelGGL(k_map_writeback, dim3(1), dim3(256), 0, s, m, M->t0);
-  LORB_CHECK_LAUNCH(ctx);
+  // float write-back: poses straight into the ring (Frame::SetPose), points into the map
+  LORB_TRY(lorb::ba_plan_result_ring_dev(M->plan, m.ring, m.R, M->t0, m.pos));
   LORB_TRY(mark(6));
   if (M->prof) M->prof_n++;
   return LORB_OK;

@@ -458,27 +458,23 @@ __global__ __launch_bounds__(256) void k_frustum(lorb_frame_params fp, const flo
 }
 
 // (a20) Frame::UnprojectStereo, one thread per keypoint; Twc = mTcw.inv() given
-__global__ __launch_bounds__(256) void k_unproject(lorb_frame_params fp, const float* __restrict__ Twc, int n,
+__global__ __launch_bounds__(256) void k_unproject(lorb_frame_params fp, lorb::Mat4f Twc, int n,
                                                    const float* __restrict__ x, const float* __restrict__ y,
                                                    const float* __restrict__ depth, float* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const float z = depth[i];
   if (z > 0) {
-    const float xx = (x[i] - fp.cx) * z / fp.fx;
-    const float yy = (y[i] - fp.cy) * z / fp.fy;
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-      const double s = (double)Twc[4 * r] * xx + (double)Twc[4 * r + 1] * yy + (double)Twc[4 * r + 2] * z + (double)Twc[4 * r + 3] * 1.0f;
-      out[3 * i + r] = (float)s;
-    }
+    lorb::unproject_point(fp.fx, fp.fy, fp.cx, fp.cy, Twc, x[i], y[i], z, out + 3 * i);
   } else {
     out[3 * i] = 0.0f; out[3 * i + 1] = 0.0f; out[3 * i + 2] = 0.0f;
   }
 }
 
+}  // namespace
+
 // cv::Mat::inv() for 4x4 CV_32F: hal::LU32f (partial pivoting, float), host side
-bool inv4_lu32f(const float* Ain, float* out) {
+bool lorb::inv4_lu32f(const float* Ain, float* out) {
   float A[16], b[16];
   memcpy(A, Ain, sizeof(A));
   for (int i = 0; i < 16; i++) b[i] = (i % 5 == 0) ? 1.0f : 0.0f;
@@ -508,6 +504,9 @@ bool inv4_lu32f(const float* Ain, float* out) {
   memcpy(out, b, sizeof(b));
   return true;
 }
+
+namespace {
+using lorb::inv4_lu32f;
 
 int upload_kps(lorb_ctx* ctx, const lorb_keypoints* k, const uint8_t* slot_state, int slot0, KpDev* K,
                const lorb_frame_params* fp) {
@@ -838,9 +837,9 @@ int lorb_unproject_stereo_dev(lorb_ctx* ctx, const lorb_frame_params* frame, con
   if (n <= 0) return LORB_OK;
   float Twc[16];
   inv4_lu32f(Tcw, Twc);
-  float* dT;
-  LORB_TRY(lorb::upload_t(ctx, S_WX + 7, Twc, 16, &dT));
-  hipLaunchKernelGGL(k_unproject, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, *frame, dT, n, d_x, d_y,
+  lorb::Mat4f T;
+  memcpy(T.v, Twc, sizeof(T.v));
+  hipLaunchKernelGGL(k_unproject, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, *frame, T, n, d_x, d_y,
                      d_depth, d_out);
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
@@ -852,13 +851,14 @@ int lorb_unproject_stereo(lorb_ctx* ctx, const lorb_frame_params* frame, const f
   if (n <= 0) return LORB_OK;
   float Twc[16];
   inv4_lu32f(Tcw, Twc);
-  float *dT, *dx, *dy, *dd, *o;
-  LORB_TRY(lorb::upload_t(ctx, S_W0, Twc, 16, &dT));
+  float *dx, *dy, *dd, *o;
+  lorb::Mat4f T;
+  memcpy(T.v, Twc, sizeof(T.v));
   LORB_TRY(lorb::upload_t(ctx, S_W1, x, n, &dx));
   LORB_TRY(lorb::upload_t(ctx, S_W2, y, n, &dy));
   LORB_TRY(lorb::upload_t(ctx, S_W3, depth, n, &dd));
   LORB_TRY(lorb::scratch_t(ctx, S_W4, (size_t)n * 3, &o));
-  hipLaunchKernelGGL(k_unproject, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, *frame, dT, n, dx, dy, dd, o);
+  hipLaunchKernelGGL(k_unproject, dim3(lorb::ceil_div(n, 256)), dim3(256), 0, ctx->stream, *frame, T, n, dx, dy, dd, o);
   LORB_CHECK_LAUNCH(ctx);
   LORB_HIP(ctx, hipMemcpyAsync(out_xyz, o, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
