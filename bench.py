@@ -137,7 +137,9 @@ def host_cpu():
 
 def cpu_threads():
     """host threads for the nproc leg: the cores this process may use, capped at the GPU box's
-    per-GPU CPU share (OMP_NUM_THREADS is 16 there)"""
+    per-GPU CPU share -- OMP_NUM_THREADS is 16 there and the pool's rules allot one GPU's job 16 of
+    the host's hardware threads (the other GPUs' jobs share the rest), so 16 is the fair host-side
+    comparison for one MI355X; the cap is stated next to every nproc number"""
     _, avail = host_cpu()
     cap = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
     return max(1, min(avail, cap, 16))
@@ -276,11 +278,75 @@ def cpu_baseline_c4(seq, budget_s):
     return {"value": 10.0 * n1 / d1, "unit": "BA iterations/s", "cores": 1, "kind": "port",
             "matches_per_sec": nq * n1 / d1, "steps_per_sec": n1 / d1,
             "sample": f"{n1} x C4 chained local-mapping step (1 window: {nq}x{len(base['point'])} crossCheck + "
-                      f"unproject + append/slide + 10 LM its), oracle C restatement gcc -O2 + numpy bookkeeping, "
+                      f"unproject + append/slide + 10 LM its), oracle C restatement gcc -O3 + numpy bookkeeping, "
                       f"1 thread (Ceres default num_threads=1), {d1:.1f}s",
             "nproc": {"value": 10.0 * nn / dn, "cores": nt, "matches_per_sec": nq * nn / dn,
-                      "sample": f"{nn} steps on {nt} threads (independent windows), {dn:.1f}s"},
+                      "sample": f"{nn} steps on {nt} threads (independent windows; {nt} = the box's per-GPU CPU share), {dn:.1f}s"},
             "host_cpu": model, "host_cpus_available": avail}
+
+
+def sub_c1(ctx, D, args):
+    """BASELINE C1 on the GPU through the host C-ABI (the calls a per-frame caller issues): the a2 BF
+    crossCheck match, SearchByProjection(curr, last, 15) (a4) and ProjectPoseOptimization of 200
+    matched points (a12), host arrays in and out, synchronous, median of 30 sequences.  Latency-bound:
+    a few thousand items per call."""
+    import lorb_slam_amd.window  # noqa: F401  (Context.search_by_projection_frame)
+    from lorb_slam_amd import synth
+    pr = synth.two_frames(seed=1, n_kps=500, n_shared=200)
+    last, cur = pr["last"], pr["cur_kps"]
+    tdesc = np.ascontiguousarray(last["mp_desc"][last["has_mp"] > 0])
+    pb = synth.pose_only_batch(seed=1, n_frames=1, n_res=200)
+    stages = {"a2_bf_match": lambda: ctx.bf_match([cur["desc"]], [tdesc]),
+              "a4_search_by_projection_th15": lambda: ctx.search_by_projection_frame(
+                  pr["fp"], pr["cur_Tcw"], cur, pr["slot_state"], last, 15.0),
+              "a12_pose_only_200": lambda: ctx.ba_pose_only(pb)}
+    for fn in stages.values():
+        fn()
+    per = {}
+    for name, fn in stages.items():
+        ts = []
+        for _ in range(30):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        per[name] = D.reduce(float(np.median(ts)), "MAX") * 1e3
+    total = sum(per.values())
+    return {"workload": "c1_two_frames_500kps", "value": 1e3 / total, "unit": "C1 sequences/s (a2 + a4 + a12)",
+            "ms_per_sequence": total, "stage_ms_median": per,
+            "call": "host C-ABI (lorb_bf_match, lorb_search_by_projection_frame, lorb_ba_pose_only), synchronous"}
+
+
+def cpu_baseline_c1(budget_s):
+    """BASELINE C1 (the reference's CPU-runnable case): two synthetic frames of 500 ORB
+    keypoints, 200 shared map points -- the BF crossCheck match of the current frame against the last
+    frame's map points (a2), SearchByProjection(curr, last, 15) (a4) and ProjectPoseOptimization of
+    the 200 matched points (a12) -- on the oracle (C restatement, gcc -O3 -ffp-contract=off), 1
+    thread, median of >= 30 runs."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from lorb_slam_amd import synth
+    pr = synth.two_frames(seed=1, n_kps=500, n_shared=200)
+    last, cur = pr["last"], pr["cur_kps"]
+    tdesc = np.ascontiguousarray(last["mp_desc"][last["has_mp"] > 0])
+    pb = synth.pose_only_batch(seed=1, n_frames=1, n_res=200)
+    stages = {"a2_bf_match_500x%d" % len(tdesc): lambda: O.bf_match(cur["desc"], tdesc),
+              "a4_search_by_projection_th15": lambda: O.search_by_projection_frame(
+                  pr["fp"], pr["cur_Tcw"], cur, pr["slot_state"], last, 15.0),
+              "a12_pose_only_200": lambda: O.ba_pose_only(pb)}
+    per = {}
+    t_end = time.perf_counter() + budget_s
+    for name, fn in stages.items():
+        ts = []
+        while len(ts) < 30 or (time.perf_counter() < t_end and len(ts) < 2000):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        per[name] = float(np.median(ts)) * 1e3
+    total = sum(per.values())
+    return {"value": 1e3 / total, "unit": "C1 sequences/s (a2 + a4 + a12)", "cores": 1, "kind": "port",
+            "ms_per_sequence": total, "stage_ms_median": per,
+            "sample": "2 frames x 500 kps, 200 shared MPs (synth.two_frames seed 1): a2 + a4 th=15 + a12, oracle C "
+                      "gcc -O3 -ffp-contract=off via ctypes, 1 thread, median of >= 30 runs per stage"}
 
 
 def workload_shared(ctx, args, rank, D, comm):
@@ -389,9 +455,9 @@ def workload_c2(ctx, args, rank):
         nn, dn = run_parallel(lambda: O.bf_top2(qs[0], ts[0], ls[0]), nt, budget) if nt > 1 else (n1, d1)
         model, avail = host_cpu()
         return {"value": n1 * 2000 / d1, "unit": "matches/s", "cores": 1, "kind": "port",
-                "sample": f"{n1} x (2000x2000 bf top-2 + ratio test), oracle C -O2, 1 thread, {d1:.1f}s",
+                "sample": f"{n1} x (2000x2000 bf top-2 + ratio test), oracle C -O3, 1 thread, {d1:.1f}s",
                 "nproc": {"value": nn * 2000 / dn, "cores": nt,
-                          "sample": f"{nn} problems on {nt} threads, {dn:.1f}s"},
+                          "sample": f"{nn} problems on {nt} threads ({nt} = the box's per-GPU CPU share), {dn:.1f}s"},
                 "host_cpu": model, "host_cpus_available": avail}
 
     def cleanup():
@@ -659,8 +725,11 @@ def main():
     total_iters = D.reduce(wl["ba_iters"] * args.steps, "SUM")
     total_matches = D.reduce(wl["matches"] * args.steps, "SUM")
     cpu = wl["cpu"]() if (D.rank == 0 and not args.no_cpu_baseline and D.world == 1 and wl["cpu"]) else None
+    if cpu is not None and args.workload == "c4":
+        cpu["c1"] = cpu_baseline_c1(max(2.0, args.cpu_budget / 2))
     c2 = sub_c2(ctx, D, args) if (args.workload == "c4" and not args.no_c2) else None
     dropin = sub_dropin(ctx, D, args) if (args.workload == "c4" and not args.no_dropin) else None
+    c1 = sub_c1(ctx, D, args) if (args.workload == "c4" and not args.no_c2) else None
     shared = (sub_shared(ctx, D, args, comm) if (args.workload in ("c4", "rehearse") and not args.no_shared)
               else None)
     if D.rank == 0:
@@ -680,7 +749,7 @@ def main():
             "config": dict(wl["config"], parallelism=par),
             "matches_per_sec": total_matches / elapsed, "plan_build_ms": wl["plan_ms"],
             "map_create_ms": wl.get("create_ms"),
-            "roofline": roofline_entry(kt, wl, pn), "cpu_baseline": cpu, "c2": c2, "dropin_local_ba": dropin, "shared": shared,
+            "roofline": roofline_entry(kt, wl, pn), "cpu_baseline": cpu, "c2": c2, "dropin_local_ba": dropin, "shared": shared, "c1": c1,
             "check": check,
         }
         if rehearse:
