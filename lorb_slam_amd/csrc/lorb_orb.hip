@@ -370,12 +370,11 @@ struct FastCell {
   int level, ini_x, ini_y, w, h, out_base, rel_x, rel_y;  // rel = (j wCell, i hCell), :865-866
 };
 
-// cornerScore<16> (OpenCV 3.1 fast_score.cpp) on the LDS cell image (row stride w)
-__device__ __forceinline__ int fast_score(const uint8_t* ptr, const int* pixel, int threshold) {
+// cornerScore<16> (OpenCV 3.1 fast_score.cpp) from the 16 circle pixels in registers
+__device__ __forceinline__ int fast_score(int v, const int (&ring)[16], int threshold) {
   int d[25];
-  const int v = ptr[0];
 #pragma unroll
-  for (int k = 0; k < 25; k++) d[k] = v - ptr[pixel[k]];
+  for (int k = 0; k < 25; k++) d[k] = v - ring[k & 15];
   int a0 = threshold;
 #pragma unroll
   for (int k = 0; k < 16; k += 2) {
@@ -411,7 +410,6 @@ __global__ __launch_bounds__(kFastThreads) void k_orb_fast(const uint8_t* __rest
                                                            float* __restrict__ oresp, int* __restrict__ ocount) {
   __shared__ uint8_t img[kCellMax * kCellMax], score[kCellMax * kCellMax], corner[kCellMax * kCellMax];
   __shared__ int s_count, wsum[kFastThreads / 64];
-  __shared__ int pixel[25];
   const FastCell c = cells[blockIdx.x];
   const int w = c.w, h = c.h, n = w * h, t = threadIdx.x;
   const uint8_t* src = data + P.offset[c.level] + (int64_t)c.ini_y * P.step[c.level] + c.ini_x;
@@ -428,7 +426,6 @@ __global__ __launch_bounds__(kFastThreads) void k_orb_fast(const uint8_t* __rest
     for (int u = 0; u < 8; u++)
       if (p0 + kFastThreads * u < n) img[p0 + kFastThreads * u] = v[u];
   }
-  if (t < 25) pixel[t] = kOff16[t & 15][0] + kOff16[t & 15][1] * w;
   for (int pass = 0; pass < 2; ++pass) {
     const int th = min(max(pass ? min_th : ini_th, 0), 255);
     for (int p = t; p < n; p += kFastThreads) { score[p] = 0; corner[p] = 0; }
@@ -439,35 +436,27 @@ __global__ __launch_bounds__(kFastThreads) void k_orb_fast(const uint8_t* __rest
       if (i < 3 || i >= h - 3 || j < 3 || j >= w - 3) continue;
       const uint8_t* ptr = img + p;
       const int v = ptr[0];
-      auto cat = [&](int k) { const int e = ptr[pixel[k]] - v; return e < -th ? 1 : (e > th ? 2 : 0); };
-      int d = cat(0) | cat(8);
-      if (d == 0) continue;
-      d &= cat(2) | cat(10);
-      d &= cat(4) | cat(12);
-      d &= cat(6) | cat(14);
-      if (d == 0) continue;
-      d &= cat(1) | cat(9);
-      d &= cat(3) | cat(11);
-      d &= cat(5) | cat(13);
-      d &= cat(7) | cat(15);
-      bool is = false;
-      if (d & 1) {
-        const int vt = v - th;
-        int count = 0;
-        for (int k = 0; k < 25; k++) {
-          if (ptr[pixel[k]] < vt) { if (++count > 8) { is = true; break; } }
-          else count = 0;
-        }
+      // the 16 circle pixels, all loads issued together (no dependent LDS chains)
+      int ring[16];
+#pragma unroll
+      for (int k = 0; k < 16; k++) ring[k] = ptr[kOff16[k][0] + kOff16[k][1] * w];
+      // FAST_t<16>'s test: 9 contiguous circle pixels all darker than v - th, or all brighter than
+      // v + th, along k = 0 .. 24 (indices mod 16) -- i.e. a circular run of 9 in the 16-bit masks.
+      // (OpenCV's quick tests on pixels 0/8, 2/10, ... are necessary conditions of this: they
+      // only skip work and never change the answer.)
+      unsigned dk = 0, br = 0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) {
+        dk |= (unsigned)(ring[k] < v - th) << k;
+        br |= (unsigned)(ring[k] > v + th) << k;
       }
-      if (!is && (d & 2)) {
-        const int vt = v + th;
-        int count = 0;
-        for (int k = 0; k < 25; k++) {
-          if (ptr[pixel[k]] > vt) { if (++count > 8) { is = true; break; } }
-          else count = 0;
-        }
-      }
-      if (is) { corner[p] = 1; score[p] = (uint8_t)fast_score(ptr, pixel, th); }
+      auto run9 = [](unsigned m) {
+        unsigned x = m | (m << 16), r = x;
+#pragma unroll
+        for (int s2 = 1; s2 < 9; s2++) r &= x >> s2;
+        return (r & 0xffffu) != 0u;
+      };
+      if (run9(dk) || run9(br)) { corner[p] = 1; score[p] = (uint8_t)fast_score(v, ring, th); }
     }
     __syncthreads();
     int mine = 0;
