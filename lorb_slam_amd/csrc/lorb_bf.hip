@@ -515,11 +515,14 @@ int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, con
   return LORB_OK;
 }
 
-// lorb_bf_match_dev for ONE problem with nothing uploaded: tiles computed in the scan kernel (which
-// also clears the query keys), chunk merge + crossCheck scatter in one launch, offsets passed by
-// value to the finalisation.  Same outputs, bit for bit, as the general path.
-int match1_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int32_t* d_cc_train,
-               int32_t* d_cc_dist, int32_t* d_match_train, int32_t* d_n_matches) {
+}  // namespace
+
+// The crossCheck keys of ONE problem: per query (dist << 32 | train) of the train whose nearest
+// query it is, all-ones where none (lorb_bf_match_dev up to the finalisation, which the caller does:
+// k_cc_finalize<0>, or the LocalMapping append).  Nothing is uploaded: the scan computes its tiles and
+// clears the keys, the chunk merge and the scatter are one launch.
+int lorb::match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
+                          unsigned long long** qkey_out) {
   unsigned long long* qkey = nullptr;
   LORB_TRY(lorb::scratch_t(ctx, S_BF_QKEY, (size_t)std::max(nq, 1), &qkey));
   if (nt > 0 && nq > 0) {
@@ -555,6 +558,19 @@ int match1_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, in
   } else if (nq > 0) {
     LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, ctx->stream));
   }
+  LORB_CHECK_LAUNCH(ctx);
+  *qkey_out = qkey;
+  return LORB_OK;
+}
+
+namespace {
+
+// lorb_bf_match_dev for ONE problem: the keys (match1_keys_dev) and the finalisation with the offsets
+// passed by value.  Same outputs, bit for bit, as the general path.
+int match1_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int32_t* d_cc_train,
+               int32_t* d_cc_dist, int32_t* d_match_train, int32_t* d_n_matches) {
+  unsigned long long* qkey = nullptr;
+  LORB_TRY(lorb::match1_keys_dev(ctx, d_q, nq, d_t, nt, &qkey));
   hipLaunchKernelGGL(k_cc_finalize<0>, dim3(1), dim3(256), 0, ctx->stream, qkey, (const int32_t*)nullptr,
                      (const int32_t*)nullptr, d_cc_train, d_cc_dist, d_match_train, d_n_matches, (double*)nullptr, 1, nq, nt);
   LORB_CHECK_LAUNCH(ctx);

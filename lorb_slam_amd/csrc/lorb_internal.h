@@ -94,6 +94,11 @@ int ba_plan_result64_dev(lorb_ba_plan* P, double* d_out);
 // window to slot (t0 + c) mod R, 6 floats each) instead of a pose array
 int ba_plan_result_ring_dev(lorb_ba_plan* P, float* ring, int R, int t0, float* d_point_out);
 
+// crossCheck keys of ONE brute-force problem (lorb_bf_match_dev without its finalisation): per
+// query (dist << 32 | train) or all-ones; *qkey_out is ctx scratch valid until the next matcher call
+int match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
+                    unsigned long long** qkey_out);
+
 // grow-only scratch: returns device pointer in *out
 int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out);
 template <typename T>

@@ -46,19 +46,43 @@ struct Pose6 { float v[6]; };
 
 __device__ __forceinline__ int ring_slot(int kf, int R) { const int r = kf % R; return r < 0 ? r + R : r; }
 
-// step 1 + 2: one workgroup, keypoints in order.  A matched keypoint adds an observation of its map
-// point; an unmatched one with depth > 0 adds a new point at Frame::UnprojectStereo
-// (src/frame.cpp:335-356, lorb::unproject_point) and its observation.  Observations and new points
-// are appended in keypoint order: thread t owns a run of consecutive keypoints, one block scan of
-// three counters (observations, new points, matches) places every run.
-__global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Pose6 pose, const int* __restrict__ mt,
-                                                     lorb::Mat4f Twc, float fx, float fy, float cx, float cy,
-                                                     const uint8_t* __restrict__ kdesc, const float* __restrict__ x,
-                                                     const float* __restrict__ y, const float* __restrict__ depth) {
+// step 1 + 2: one workgroup, keypoints in order.  First the matcher's finalisation (k_cc_finalize's
+// work on the crossCheck keys: the DMatches, minDist and the d <= max(2 minDist, 30) filter,
+// src/matcher.cpp:342-362) into mt.  A matched keypoint adds an observation of its map point; an
+// unmatched one with depth > 0 adds a new point at Frame::UnprojectStereo (src/frame.cpp:335-356,
+// lorb::unproject_point) and its observation.  Observations and new points are appended in keypoint
+// order: thread t owns a run of consecutive keypoints, one block scan of three counters
+// (observations, new points, matches) places every run.
+__global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Pose6 pose,
+                                                     const unsigned long long* __restrict__ qkey, int has_t,
+                                                     int* __restrict__ mt, lorb::Mat4f Twc, float fx, float fy,
+                                                     float cx, float cy, const uint8_t* __restrict__ kdesc,
+                                                     const float* __restrict__ x, const float* __restrict__ y,
+                                                     const float* __restrict__ depth) {
   __shared__ lorb::I4 wsum[16];
+  __shared__ int s_min[16];
   const int t = threadIdx.x;
   const int P0 = m.cnt[0], K0 = m.cnt[1];
   const int R = (n + 1023) / 1024, q0 = min(t * R, n), q1 = min(q0 + R, n);
+  {
+    int mn = 0x7fffffff;
+    for (int q = q0; q < q1; ++q) {
+      const unsigned long long v = has_t ? qkey[q] : ~0ull;
+      if (v != ~0ull) mn = min(mn, (int)(v >> 32));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mn = min(mn, __shfl_xor(mn, o, 64));
+    if ((t & 63) == 0) s_min[t >> 6] = mn;
+    __syncthreads();
+    mn = s_min[0];
+#pragma unroll
+    for (int w = 1; w < 16; ++w) mn = min(mn, s_min[w]);
+    const int thr = max(2 * mn, 30);  // d > max(2 * minDist, 30.0) rejects (exact in integers)
+    for (int q = q0; q < q1; ++q) {
+      const unsigned long long v = has_t ? qkey[q] : ~0ull;
+      mt[q] = (v != ~0ull && (int)(v >> 32) <= thr) ? (int)(v & 0xffffffffu) : -1;
+    }
+  }
   lorb::I4 c = {{0, 0, 0, 0}};
   for (int q = q0; q < q1; ++q) {
     const bool mat = mt[q] >= 0;
@@ -190,7 +214,7 @@ struct lorb_map {
   bool prof = false;
   double prof_ms[8] = {};
   int prof_n = 0;
-  int* cc_t = nullptr; int* cc_d = nullptr; int* mt = nullptr; int* nm = nullptr;
+  int* mt = nullptr;
   int* pinned = nullptr;
   lorb_ba_plan* plan = nullptr;
   std::vector<void*> allocs;
@@ -238,8 +262,7 @@ int map_alloc(lorb_map* M, const lorb_map_init* in) {
   LORB_TRY(malloc_n(M, 6 * (size_t)std::max(m.F, 1), &m.fixed));
   const size_t n = (size_t)std::max(in->max_keypoints, 1);
   M->n_cap = (int)n;
-  LORB_TRY(malloc_n(M, n, &M->cc_t)); LORB_TRY(malloc_n(M, n, &M->cc_d)); LORB_TRY(malloc_n(M, n, &M->mt));
-  LORB_TRY(malloc_n(M, (size_t)1, &M->nm));
+  LORB_TRY(malloc_n(M, n, &M->mt));
   LORB_HIP(M->ctx, hipHostMalloc(reinterpret_cast<void**>(&M->pinned), sizeof(int) * 8));
   return LORB_OK;
 }
@@ -363,13 +386,11 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
     return LORB_OK;
   };
   LORB_TRY(mark(7));
-  // 1. SearchLocalPoints: the keyframe's descriptors against the map's points (crossCheck + minDist filter)
-  if (n > 0 && M->h_P > 0) {
-    const int32_t q_off[2] = {0, n}, t_off[2] = {0, M->h_P};
-    LORB_TRY(lorb_bf_match_dev(ctx, 1, d_desc, q_off, m.desc, t_off, M->cc_t, M->cc_d, M->mt, M->nm));
-  } else if (n > 0) {
-    LORB_HIP(ctx, hipMemsetAsync(M->mt, 0xff, sizeof(int) * (size_t)n, s));
-  }
+  // 1. SearchLocalPoints: the keyframe's descriptors against the map's points -- the crossCheck keys
+  //    here, the finalisation (minDist filter) inside the append
+  unsigned long long* qkey = nullptr;
+  const bool has_t = M->h_P > 0;
+  if (n > 0 && has_t) LORB_TRY(lorb::match1_keys_dev(ctx, d_desc, n, m.desc, M->h_P, &qkey));
   LORB_TRY(mark(0));
   LORB_TRY(mark(1));
   // 2 + 3. AddObservation / new points at UnprojectStereo (Twc = mTcw.inv(), src/frame.cpp:350),
@@ -378,8 +399,9 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   for (int q = 0; q < 6; ++q) p6.v[q] = pose[q];
   lorb::Mat4f Twc;
   lorb::inv4_lu32f(Tcw, Twc.v);
-  hipLaunchKernelGGL(k_map_append, dim3(1), dim3(1024), 0, s, m, n, kf, p6, M->mt, Twc, frame->fx, frame->fy, frame->cx,
-                     frame->cy, d_desc, d_x, d_y, d_depth);
+  hipLaunchKernelGGL(k_map_append, dim3(1), dim3(1024), 0, s, m, n, kf, p6, (const unsigned long long*)qkey,
+                     (int)(has_t && qkey), M->mt, Twc, frame->fx, frame->fy, frame->cx, frame->cy, d_desc, d_x, d_y,
+                     d_depth);
   LORB_CHECK_LAUNCH(ctx);
   M->last_n = n;
   // Capacity: n keypoints add at most n points and n observations.  When that bound does not fit,
