@@ -185,15 +185,22 @@ int lorb_ba_solver_solve(lorb_ba_solver* S, const lorb_ba_window* w, const lorb_
   if (F > 0) memcpy(fx, w->fixed_pose, sizeof(float) * 6 * (size_t)F);
   std::fill(fx + 6 * (size_t)F, fx + 6 * (size_t)sl->F_cap, 0.0f);
   memcpy(h + L.point, w->point_init, sizeof(float) * 3 * (size_t)P);
-  int32_t* op = reinterpret_cast<int32_t*>(h + L.opt);
-  int32_t* of = reinterpret_cast<int32_t*>(h + L.ofr);
-  for (int k = 0; k < K; ++k) {
-    const int p = w->obs_point[k], f = w->obs_frame[k];
-    if (p < 0 || p >= P) return lorb::set_error(ctx, LORB_E_INVALID, "window 0 obs %d: bad point %d", k, p);
-    if (f >= C || f < -F) return lorb::set_error(ctx, LORB_E_INVALID, "window 0 obs %d: bad frame %d", k, f);
-    op[k] = p;
-    of[k] = f;
+  {  // index validation as min / max reductions (vectorisable); the offending slot only on failure
+    int pmn = 0, pmx = 0, fmn = 0, fmx = 0;
+    if (K > 0) { pmn = pmx = w->obs_point[0]; fmn = fmx = w->obs_frame[0]; }
+    for (int k = 0; k < K; ++k) {
+      pmn = std::min(pmn, w->obs_point[k]); pmx = std::max(pmx, w->obs_point[k]);
+      fmn = std::min(fmn, w->obs_frame[k]); fmx = std::max(fmx, w->obs_frame[k]);
+    }
+    if (pmn < 0 || pmx >= P || fmn < -F || fmx >= C)
+      for (int k = 0; k < K; ++k) {
+        const int p = w->obs_point[k], f = w->obs_frame[k];
+        if (p < 0 || p >= P) return lorb::set_error(ctx, LORB_E_INVALID, "window 0 obs %d: bad point %d", k, p);
+        if (f >= C || f < -F) return lorb::set_error(ctx, LORB_E_INVALID, "window 0 obs %d: bad frame %d", k, f);
+      }
   }
+  memcpy(h + L.opt, w->obs_point, sizeof(int32_t) * (size_t)K);
+  memcpy(h + L.ofr, w->obs_frame, sizeof(int32_t) * (size_t)K);
   memcpy(h + L.uv, w->obs_uv, sizeof(float) * 2 * (size_t)K);
   LORB_HIP(ctx, hipMemcpyAsync(sl->d_in, h, L.end, hipMemcpyHostToDevice, ctx->stream));
   lorb_ba_window_dev wd{};
