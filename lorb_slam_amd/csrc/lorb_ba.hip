@@ -2514,6 +2514,7 @@ struct lorb_ba_devbuild {
   int* pinned = nullptr; size_t pinned_n = 0;
   double* sol_part = nullptr; size_t sol_n = 0;  // this rank's solve block (== the global one unsharded)
   bool dirty = true;  // the build scratch needs a clearing fill (first build, or after a failed one)
+  bool sorted_hint = false;  // the caller's slots are sorted by point: try k_db_sorted first
   std::vector<double> h_red;                     // sharded: the build's host all-reduce
   // per-build structure uploaded in one copy: [BaWin | live (2) | perm (C) | cam_obs_off (C+1) | bp (up_bp_cap)]
   unsigned char* up_dev = nullptr; unsigned char* up_host = nullptr; int up_bp_cap = 0;
@@ -3217,6 +3218,55 @@ __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, in
   if (err) atomicOr(&hdr[2], err);
 }
 
+// The build's first phase when the observation slots are already sorted by point (the LocalMapping
+// map keeps them so; the drop-in's windows are gathered point by point): no counting sort.  Per
+// observation: validity, the camera x point bits (a bit already set: a point seen twice by one
+// camera); per point p <= n_points: its first slot (a binary search, so points without
+// observations get the next point's), and the largest count per point.  A slot out of order or
+// unused (frame < -n_fixed) sets flag 16: the host then runs the general phase instead.
+__global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, int F, int Wd, int* __restrict__ pt_off,
+                                                   int* __restrict__ hdr, unsigned long long* __restrict__ bits) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int n_obs_in = *w.d_n_obs, n_pt_in = *w.d_n_points;
+  const int n_obs = max(min(n_obs_in, w.max_obs), 0), n_pt = max(min(n_pt_in, w.max_points), 0);
+  const int* __restrict__ op = w.d_obs_point;
+  int err = 0;
+  if (i == 0) {
+    hdr[3] = n_pt;
+    hdr[0] = n_obs;
+    if (n_obs_in > w.max_obs || n_pt_in > w.max_points || n_obs_in < 0 || n_pt_in < 0) err |= 8;
+  }
+  if (i < n_obs) {
+    const int q = op[i], f = w.d_obs_frame[i];
+    if (f < -F) err |= 16;
+    else if (f >= C) err |= 2;
+    else if (q < 0 || q >= n_pt) err |= 1;
+    else if (f >= 0) {
+      const unsigned long long m = 1ull << (q & 63);
+      if (atomicOr(&bits[(size_t)f * Wd + (q >> 6)], m) & m) err |= 4;
+    }
+    if (i > 0 && op[i - 1] > q) err |= 16;
+  }
+  int cnt = 0;
+  if (i <= n_pt) {
+    auto lb = [&](int p) {
+      int lo = 0, hi = n_obs;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (op[mid] < p) lo = mid + 1; else hi = mid;
+      }
+      return lo;
+    };
+    const int a = lb(i);
+    pt_off[i] = a;
+    if (i < n_pt) cnt = lb(i + 1) - a;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt = max(cnt, __shfl_xor(cnt, o, 64));
+  if ((threadIdx.x & 63) == 0 && cnt) atomicMax(&hdr[1], cnt);
+  if (err) atomicOr(&hdr[2], err);
+}
+
 // One workgroup: out[0 .. n) = exclusive prefix sums of in[0 .. n) (n_dev: n = *n_dev + 1, the
 // live points and one past them).  hdr (optional): hdr[0] = total, hdr[1] = max(in).
 __global__ __launch_bounds__(1024) void k_db_scan1(const int* __restrict__ in, int* __restrict__ out, int n,
@@ -3318,6 +3368,7 @@ struct DbFused {
   const int* perm;   // input camera -> plan camera
   const int* gcam;   // observations per input camera, all ranks
   int C, F, P, G, S, env_n, bits_n;
+  int sorted;        // the slots were sorted by point (k_db_sorted): slot e is sorted position e
   unsigned long long* bits;
   int* hdr;
 };
@@ -3362,11 +3413,11 @@ __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d
   __syncthreads();
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e < K) {
-    const int k = val[e], f = w.d_obs_frame[k];
-    const int c = f >= 0 ? perm[f] : -1;
-    const_cast<int*>(d.obs_pt)[e] = key[e];
+    const int k = f.sorted ? e : val[e], fr = w.d_obs_frame[k];
+    const int c = fr >= 0 ? perm[fr] : -1;
+    const_cast<int*>(d.obs_pt)[e] = f.sorted ? w.d_obs_point[e] : key[e];
     const_cast<int*>(d.obs_cam)[e] = c;
-    const_cast<int*>(d.obs_fix)[e] = f >= 0 ? -1 : -1 - f;
+    const_cast<int*>(d.obs_fix)[e] = fr >= 0 ? -1 : -1 - fr;
     const_cast<double2*>(d.obs_uv)[e] = make_double2(w.d_obs_uv[2 * k], w.d_obs_uv[2 * k + 1]);
     const_cast<int*>(d.obs_cm)[e] = -1;
     if (c >= 0) atomicAdd(&s_h[c], 1);
@@ -3496,6 +3547,10 @@ __global__ __launch_bounds__(256) void k_db_result64(BaDev d, int C, int P, cons
 }  // namespace
 
 namespace lorb {
+void ba_plan_sorted_hint(lorb_ba_plan* P, bool sorted) {
+  if (P && P->devb) P->devb->sorted_hint = sorted;
+}
+
 int ba_plan_result_ring_dev(lorb_ba_plan* P, float* ring, int R, int t0, float* d_point_out) {
   if (!P || !P->devb || !ring || R < 1) return LORB_E_INVALID;
   const int C = P->Ctot, Pn = P->Ptot;
@@ -3664,30 +3719,41 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   // 1. per-point counts and camera x point bitsets; point offsets; counting sort by point
   //    (stable); covisibility counts from the bitsets.  The scratch is left clear by the previous
   //    build's k_db_gather; only a build that stopped before it (an error) leaves it dirty.
-  if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
-  b.dirty = true;
   const int nb_obs = lorb::ceil_div(std::max(Kc, 1), 256), nb_pt = lorb::ceil_div(std::max(b.P_cap, 1), 256);
-  hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);
-  hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1,
-                     w->d_n_points, b.hdr);
-  if (Kc > 0) {
-    hipLaunchKernelGGL(k_db_scatter, dim3(nb_obs), dim3(256), 0, s, *w, C, F, d.pt_obs_off, b.pt_cnt, b.val_out);
-    hipLaunchKernelGGL(k_db_segsort, dim3(nb_pt), dim3(256), 0, s, *w, d.pt_obs_off, b.val_out, b.key_out);
-  }
-  if (C > 0)
-    hipLaunchKernelGGL(k_db_cov, dim3(lorb::ceil_div(C * (C + 1) / 2, 4)), dim3(256), 0, s, C, b.Wd, b.bits, b.cov,
-                       b.cam_cnt);
-  LORB_CHECK_LAUNCH(ctx);
-  // 2. the one readback: counts and the covisibility structure
   const size_t nrb = 8 + (size_t)C + (size_t)C * C;
   if (b.pinned_n < nrb) {
     if (b.pinned) (void)hipHostFree(b.pinned);
     LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&b.pinned), sizeof(int) * nrb));
     b.pinned_n = nrb;
   }
-  // hdr | cov | cam_cnt are contiguous in the scratch: one copy
-  LORB_HIP(ctx, hipMemcpyAsync(b.pinned, b.hdr, sizeof(int) * nrb, hipMemcpyDeviceToHost, s));
-  LORB_HIP(ctx, lorb::spin_sync(ctx));
+  bool sorted = b.sorted_hint;
+  for (;;) {
+    if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
+    b.dirty = true;
+    if (sorted) {
+      hipLaunchKernelGGL(k_db_sorted, dim3(std::max<unsigned>(nb_obs, lorb::ceil_div(b.P_cap + 1, 256))), dim3(256), 0, s, *w, C,
+                         F, b.Wd, const_cast<int*>(d.pt_obs_off), b.hdr, b.bits);
+    } else {
+      hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);
+      hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1,
+                         w->d_n_points, b.hdr);
+      if (Kc > 0) {
+        hipLaunchKernelGGL(k_db_scatter, dim3(nb_obs), dim3(256), 0, s, *w, C, F, d.pt_obs_off, b.pt_cnt, b.val_out);
+        hipLaunchKernelGGL(k_db_segsort, dim3(nb_pt), dim3(256), 0, s, *w, d.pt_obs_off, b.val_out, b.key_out);
+      }
+    }
+    if (C > 0)
+      hipLaunchKernelGGL(k_db_cov, dim3(lorb::ceil_div(C * (C + 1) / 2, 4)), dim3(256), 0, s, C, b.Wd, b.bits, b.cov,
+                         b.cam_cnt);
+    LORB_CHECK_LAUNCH(ctx);
+    // 2. the one readback: counts and the covisibility structure (hdr | cov | cam_cnt are
+    //    contiguous in the scratch: one copy)
+    LORB_HIP(ctx, hipMemcpyAsync(b.pinned, b.hdr, sizeof(int) * nrb, hipMemcpyDeviceToHost, s));
+    LORB_HIP(ctx, lorb::spin_sync(ctx));
+    if (!(sorted && (b.pinned[2] & 16))) break;
+    sorted = false;  // slots out of order (or unused): the general phase, from a cleared scratch
+    b.sorted_hint = false;
+  }
   const int* H = b.pinned;
   const int K = H[0], maxk = H[1], err = H[2], Pn = H[3];
   const int* cov = H + 8;
@@ -3817,7 +3883,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   {
     // this rank's band starts from zeros (blocks it has no pairs of stay zero; sharded: the
     // all-reduce writes the global band every iteration)
-    DbFused f{b.perm, b.gcam, C, F, Pn, G, S, P->env_total, C * b.Wd, b.bits, b.hdr};
+    DbFused f{b.perm, b.gcam, C, F, Pn, G, S, P->env_total, C * b.Wd, sorted ? 1 : 0, b.bits, b.hdr};
     hipLaunchKernelGGL(k_db_gather, dim3(std::max(NB, 1)), dim3(256), sizeof(int) * C, s, *w, d, K, C, NB, b.key_out,
                        b.val_out, b.perm, b.hist, f);
     b.dirty = false;

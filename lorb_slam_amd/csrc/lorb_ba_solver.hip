@@ -58,6 +58,7 @@ struct lorb_ba_solver {
   unsigned char* h_in = nullptr; size_t h_in_sz = 0;    // pinned staging
   double* h_out = nullptr; size_t h_out_n = 0;
   int creations = 0, last_fallback = 0, last_slot = -1;
+  bool sorted = false;  // the current window's observations are sorted by point
   ~lorb_ba_solver() {
     if (ctx) (void)hipStreamSynchronize(ctx->stream);
     for (Slot& s : slot) {
@@ -186,12 +187,16 @@ int lorb_ba_solver_solve(lorb_ba_solver* S, const lorb_ba_window* w, const lorb_
   std::fill(fx + 6 * (size_t)F, fx + 6 * (size_t)sl->F_cap, 0.0f);
   memcpy(h + L.point, w->point_init, sizeof(float) * 3 * (size_t)P);
   {  // index validation as min / max reductions (vectorisable); the offending slot only on failure
-    int pmn = 0, pmx = 0, fmn = 0, fmx = 0;
+    int pmn = 0, pmx = 0, fmn = 0, fmx = 0, unsorted = 0;
     if (K > 0) { pmn = pmx = w->obs_point[0]; fmn = fmx = w->obs_frame[0]; }
     for (int k = 0; k < K; ++k) {
       pmn = std::min(pmn, w->obs_point[k]); pmx = std::max(pmx, w->obs_point[k]);
       fmn = std::min(fmn, w->obs_frame[k]); fmx = std::max(fmx, w->obs_frame[k]);
+      unsorted |= k > 0 && w->obs_point[k - 1] > w->obs_point[k];
     }
+    // the drop-in gathers a window point by point: its slots are sorted and the device build needs
+    // no counting sort
+    S->sorted = !unsorted;
     if (pmn < 0 || pmx >= P || fmn < -F || fmx >= C)
       for (int k = 0; k < K; ++k) {
         const int p = w->obs_point[k], f = w->obs_frame[k];
@@ -219,6 +224,7 @@ int lorb_ba_solver_solve(lorb_ba_solver* S, const lorb_ba_window* w, const lorb_
     rc = lorb_ba_plan_create_dev(ctx, &wd, &sl->plan);
     if (rc == LORB_OK) S->creations++;
   } else {
+    lorb::ba_plan_sorted_hint(sl->plan, S->sorted);
     rc = lorb_ba_plan_update_dev(sl->plan, &wd);
   }
   if (rc == LORB_E_UNSUPPORTED) {

@@ -93,6 +93,9 @@ int ba_plan_result64_dev(lorb_ba_plan* P, double* d_out);
 // the same as lorb_ba_plan_result_dev with the poses written into a keyframe ring (pose c of the
 // window to slot (t0 + c) mod R, 6 floats each) instead of a pose array
 int ba_plan_result_ring_dev(lorb_ba_plan* P, float* ring, int R, int t0, float* d_point_out);
+// a device-built plan whose callers keep the observation slots sorted by point (stably, no unused
+// slots) builds without the counting sort; slots found out of order fall back to it (same result)
+void ba_plan_sorted_hint(lorb_ba_plan* P, bool sorted);
 
 // crossCheck keys of ONE brute-force problem (lorb_bf_match_dev without its finalisation): per
 // query (dist << 32 | train) or all-ones; *qkey_out is ctx scratch valid until the next matcher call

@@ -36,7 +36,9 @@ struct MapDev {
   int* obs_frame;                                                            // BA slot of each observation
   int* cnt;      // [0] points, [1] observations, [2] error flags, [3] new points, [4] new observations, [5] matches
   int* flag_pt; int* newid; int* flag_obs; int* newpos;  // newid / newpos: scans within kScanTile tiles
-  int* tile_tot;  // tile sums of the two scans: [0, ntP) points, then observations
+  int* flag_new; int* newnew;  // points that got an observation this step, and their scan
+  int* tile_tot;  // tile sums of the three scans: [0, ntP) kept points, [ntP, 2 ntP) new-observation
+                  // points, then observations
   float* ring;   // R x 6 keyframe poses, slot = kf mod R
   float* pose_init; float* fixed;
   int P_cap, K_cap, W, F, R;
@@ -116,6 +118,7 @@ __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Po
     }
     const int k = ko++;
     m.obs_pt[k] = p;
+    m.flag_new[p] = 1;  // at most one per point: crossCheck matches are one-to-one
     m.obs_kf[k] = kf;
     m.obs_uv[2 * k + 0] = x[q];
     m.obs_uv[2 * k + 1] = y[q];
@@ -154,12 +157,21 @@ __device__ __forceinline__ int new_id(const MapDev& m, int i) {
   return m.newid[i] + tile_base(m.tile_tot, i / lorb::kScanTile);
 }
 __device__ __forceinline__ int new_pos(const MapDev& m, int ntP, int i) {
-  return m.newpos[i] + tile_base(m.tile_tot + ntP, i / lorb::kScanTile);
+  return m.newpos[i] + tile_base(m.tile_tot + 2 * ntP, i / lorb::kScanTile);
+}
+// observations this step added to points with (pre-compaction) id < p
+__device__ __forceinline__ int new_before(const MapDev& m, int ntP, int p) {
+  return m.newnew[p] + tile_base(m.tile_tot + ntP, p / lorb::kScanTile);
 }
 
 // stable gathers into the alternate buffers; observation slots as lorb_ba_window_dev wants them.
+// The observations stay sorted by point (stably): slots [0, K0) hold the earlier ones, sorted; the
+// step's new ones (slots >= K0, keypoint order, one per point at most) go after their point's
+// earlier ones.  A kept earlier observation moves to (kept ones before it) + (new ones of points
+// before its point); a new one of point p to (kept earlier ones of points <= p: the kept count
+// before the first earlier slot of a point > p, a binary search) + (new ones of points before p).
 // Workgroup 0 also writes the new counts and the window's initial / fixed poses from the ring.
-__global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, int t0, int ntP) {
+__global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, int K0, int t0, int ntP) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (blockIdx.x == 0) {
     if (i == 0) { m.cnt[0] = new_id(m, Pb); m.cnt[1] = new_pos(m, ntP, Kb); }
@@ -167,6 +179,7 @@ __global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, i
     for (int j = i; j < 6 * m.F; j += 256) m.fixed[j] = m.ring[6 * ring_slot(t0 - 1 - j / 6, m.R) + j % 6];
   }
   const int fp = i < Pb ? m.flag_pt[i] : 0;
+  if (i < Pb && m.flag_new[i]) m.flag_new[i] = 0;  // cleared for the next slide (scanned already)
   if (fp) {
     m.flag_pt[i] = 0;  // cleared for the next slide (only this thread reads it here)
     const int d = new_id(m, i);
@@ -178,8 +191,19 @@ __global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, i
     o[0] = s[0]; o[1] = s[1];
   }
   if (i < Kb && m.flag_obs[i]) {
-    const int d = new_pos(m, ntP, i), kf = m.obs_kf[i];
-    m.obs_pt2[d] = new_id(m, m.obs_pt[i]);
+    const int p = m.obs_pt[i], kf = m.obs_kf[i];
+    int d;
+    if (i < K0) {
+      d = new_pos(m, ntP, i) + new_before(m, ntP, p);
+    } else {
+      int lo = 0, hi = K0;  // first earlier slot of a point > p
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (m.obs_pt[mid] <= p) lo = mid + 1; else hi = mid;
+      }
+      d = new_pos(m, ntP, lo) + new_before(m, ntP, p);
+    }
+    m.obs_pt2[d] = new_id(m, p);
     m.obs_kf2[d] = kf;
     m.obs_uv2[2 * d + 0] = m.obs_uv[2 * i + 0];
     m.obs_uv2[2 * d + 1] = m.obs_uv[2 * i + 1];
@@ -187,16 +211,16 @@ __global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, i
   }
 }
 
-// the two compaction scans, tile-local: workgroups [0, ntP) the point flags, the rest the
-// observation flags
+// the three compaction scans, tile-local: workgroups [0, ntP) the kept-point flags, [ntP, 2 ntP)
+// the new-observation flags of the points, the rest the observation flags
 __global__ __launch_bounds__(1024) void k_map_scans(MapDev m, int Pb, int Kb, int ntP) {
   __shared__ int wsum[16];
   __shared__ int s_tile[lorb::kScanTileLds];
-  const bool pt = (int)blockIdx.x < ntP;
-  const int tile = pt ? blockIdx.x : blockIdx.x - ntP;
-  const int n = pt ? Pb + 1 : Kb + 1, base = tile * lorb::kScanTile;
-  const int* in = pt ? m.flag_pt : m.flag_obs;
-  int* out = pt ? m.newid : m.newpos;
+  const int seg = (int)blockIdx.x < ntP ? 0 : (int)blockIdx.x < 2 * ntP ? 1 : 2;
+  const int tile = blockIdx.x - seg * ntP;
+  const int n = seg < 2 ? Pb + 1 : Kb + 1, base = tile * lorb::kScanTile;
+  const int* in = seg == 0 ? m.flag_pt : seg == 1 ? m.flag_new : m.flag_obs;
+  int* out = seg == 0 ? m.newid : seg == 1 ? m.newnew : m.newpos;
   const int tot = lorb::wg_scan_tile(in + base, out + base, min(n - base, lorb::kScanTile), 0, s_tile, wsum);
   if (threadIdx.x == 0) m.tile_tot[blockIdx.x] = tot;
 }
@@ -255,8 +279,10 @@ int map_alloc(lorb_map* M, const lorb_map_init* in) {
   LORB_TRY(malloc_n(M, P + 1, &m.flag_pt)); LORB_TRY(malloc_n(M, P + 1, &m.newid));
   // point flags start clear and are cleared again by the compaction that consumes them
   LORB_HIP(M->ctx, hipMemsetAsync(m.flag_pt, 0, sizeof(int) * ((size_t)P + 1), M->ctx->stream));
+  LORB_TRY(malloc_n(M, P + 1, &m.flag_new)); LORB_TRY(malloc_n(M, P + 1, &m.newnew));
+  LORB_HIP(M->ctx, hipMemsetAsync(m.flag_new, 0, sizeof(int) * ((size_t)P + 1), M->ctx->stream));
   LORB_TRY(malloc_n(M, K + 1, &m.flag_obs)); LORB_TRY(malloc_n(M, K + 1, &m.newpos));
-  LORB_TRY(malloc_n(M, (P + 1 + K + 1) / lorb::kScanTile + 2, &m.tile_tot));
+  LORB_TRY(malloc_n(M, 2 * (P + 1) / lorb::kScanTile + (K + 1) / lorb::kScanTile + 4, &m.tile_tot));
   LORB_TRY(malloc_n(M, 6 * (size_t)m.R, &m.ring));
   LORB_TRY(malloc_n(M, 6 * (size_t)m.W, &m.pose_init));
   LORB_TRY(malloc_n(M, 6 * (size_t)std::max(m.F, 1), &m.fixed));
@@ -280,16 +306,17 @@ lorb_ba_window_dev window_of(const lorb_map* M) {
 
 // slide to window [t0, t0 + W): cull points no window keyframe observes, drop observations by
 // keyframes older than the fixed ones, compact (stable), rebuild the BA slots and window poses
-int map_slide(lorb_map* M, int t0, int Pb, int Kb) {
+int map_slide(lorb_map* M, int t0, int Pb, int Kb, int K0) {
   lorb_ctx* ctx = M->ctx;
   hipStream_t s = ctx->stream;
   MapDev& m = M->m;
   if (Kb > 0) hipLaunchKernelGGL(k_map_mark, dim3(lorb::ceil_div(Kb, 256)), dim3(256), 0, s, m, Kb, t0);
   hipLaunchKernelGGL(k_map_obs_flag, dim3(lorb::ceil_div(Kb + 1, 256)), dim3(256), 0, s, m, Kb, t0);
   const int ntP = lorb::ceil_div(Pb + 1, lorb::kScanTile), ntK = lorb::ceil_div(Kb + 1, lorb::kScanTile);
-  hipLaunchKernelGGL(k_map_scans, dim3(ntP + ntK), dim3(1024), 0, s, m, Pb, Kb, ntP);
+  hipLaunchKernelGGL(k_map_scans, dim3(2 * ntP + ntK), dim3(1024), 0, s, m, Pb, Kb, ntP);
   const int nmax = std::max(std::max(Pb, Kb), 1);
-  hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, t0, ntP);
+  hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, std::min(K0, Kb), t0,
+                     ntP);
   LORB_CHECK_LAUNCH(ctx);
   std::swap(m.pos, m.pos2); std::swap(m.desc, m.desc2); std::swap(m.obs_pt, m.obs_pt2);
   std::swap(m.obs_kf, m.obs_kf2); std::swap(m.obs_uv, m.obs_uv2);
@@ -343,17 +370,29 @@ int lorb_map_create(lorb_ctx* ctx, const lorb_map_init* in, lorb_map** out) {
     if (rc == LORB_OK) rc = up(m.cnt, cnt, sizeof(cnt));
     if (rc == LORB_OK) rc = up(m.pos, in->point, sizeof(float) * 3 * (size_t)in->n_points);
     if (rc == LORB_OK) rc = up(m.desc, in->point_desc, 32 * (size_t)in->n_points);
-    if (rc == LORB_OK) rc = up(m.obs_pt, in->obs_point, sizeof(int) * (size_t)in->n_obs);
-    if (rc == LORB_OK) rc = up(m.obs_kf, in->obs_kf, sizeof(int) * (size_t)in->n_obs);
-    if (rc == LORB_OK) rc = up(m.obs_uv, in->obs_uv, sizeof(float) * 2 * (size_t)in->n_obs);
+    // the map keeps its observations sorted by point (stably): sort the initial ones once
+    std::vector<int> ord(in->n_obs);
+    for (int k = 0; k < in->n_obs; ++k) ord[k] = k;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return in->obs_point[a] < in->obs_point[b]; });
+    std::vector<int> op(in->n_obs), ok(in->n_obs);
+    std::vector<float> ouv(2 * (size_t)in->n_obs);
+    for (int k = 0; k < in->n_obs; ++k) {
+      op[k] = in->obs_point[ord[k]]; ok[k] = in->obs_kf[ord[k]];
+      ouv[2 * k] = in->obs_uv[2 * ord[k]]; ouv[2 * k + 1] = in->obs_uv[2 * ord[k] + 1];
+    }
+    if (rc == LORB_OK) rc = up(m.obs_pt, op.data(), sizeof(int) * (size_t)in->n_obs);
+    if (rc == LORB_OK) rc = up(m.obs_kf, ok.data(), sizeof(int) * (size_t)in->n_obs);
+    if (rc == LORB_OK) rc = up(m.obs_uv, ouv.data(), sizeof(float) * 2 * (size_t)in->n_obs);
     if (rc == LORB_OK) {
       // the initial window [0, W): obs slots / window poses, no culling of a consistent input
-      rc = map_slide(M, 0, in->n_points, in->n_obs);
+      rc = map_slide(M, 0, in->n_points, in->n_obs, in->n_obs);
       M->h_P = in->n_points; M->h_K = in->n_obs;  // upper bounds until the first readback
     }
     if (rc == LORB_OK) {
       const lorb_ba_window_dev w = window_of(M);
       rc = lorb_ba_plan_create_dev(ctx, &w, &M->plan);
+      // the map keeps its observations sorted by point: later builds skip the counting sort
+      if (rc == LORB_OK) lorb::ba_plan_sorted_hint(M->plan, true);
     }
     if (rc == LORB_OK) {
       LORB_HIP(ctx, hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
@@ -416,7 +455,7 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   }
   LORB_TRY(mark(2));
   // 4. slide the window by one keyframe; cull and compact
-  LORB_TRY(map_slide(M, M->t0 + 1, std::min(M->h_P + n, m.P_cap), std::min(M->h_K + n, m.K_cap)));
+  LORB_TRY(map_slide(M, M->t0 + 1, std::min(M->h_P + n, m.P_cap), std::min(M->h_K + n, m.K_cap), M->h_K));
   LORB_TRY(mark(3));
   LORB_HIP(ctx, hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
   // 5. BA plan of the slid window (its readback synchronises the stream, so the counts above are in)

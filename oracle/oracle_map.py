@@ -12,6 +12,9 @@ LocalMapping::ProcessNewFrames' disabled steps (src/local_mapping.cpp:55-76) wri
   3. the window slides by one keyframe (the sliding-window policy of DESIGN.md §5): points no window
      keyframe observes leave, observations by keyframes older than the F fixed ones are dropped,
      order is kept;
+  observations are kept sorted by point, stably (a point's observations in the order they were
+  added): the initial ones are sorted once, a step's new observations go after their point's
+  earlier ones (the BA plan then needs no sort by point);
   4. LocalPoseOptimization of the window, float write-back (src/bundle_adjust.cpp:317-329).
 Parity of the composed pieces is pinned where theirs is (oracle/lorb_oracle.h); the bookkeeping has
 no reference counterpart to pin against (the reference's step is commented out).
@@ -37,7 +40,12 @@ class MapOracle:
         self.obs_point = np.asarray(init["obs_point"], np.int32).copy()
         self.obs_kf = np.asarray(init["obs_kf"], np.int32).copy()
         self.obs_uv = np.asarray(init["obs_uv"], np.float32).reshape(-1, 2).copy()
+        self._sort_obs()
         self._slide(t0)
+
+    def _sort_obs(self):
+        o = np.argsort(self.obs_point, kind="stable")
+        self.obs_point, self.obs_kf, self.obs_uv = self.obs_point[o], self.obs_kf[o], self.obs_uv[o]
 
     @classmethod
     def from_state(cls, st, intr):
@@ -88,6 +96,7 @@ class MapOracle:
         self.obs_kf = np.concatenate([self.obs_kf, np.full(int(sel.sum()), t_new, np.int32)])
         self.obs_uv = np.concatenate([self.obs_uv, uv])
         self.ring[t_new] = np.asarray(kf["pose"], np.float32).copy()
+        self._sort_obs()
         self._slide(self.t0 + 1)
         poses, pts, summ = O.ba_local([self.window()], opt)
         for j in range(self.W):

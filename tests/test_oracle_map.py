@@ -26,6 +26,8 @@ def check_invariants(m):
     assert np.array_equal(np.unique(m.obs_point[m.obs_kf >= t0]), np.arange(P))
     pairs = m.obs_point.astype(np.int64) * 1_000_000 + (m.obs_kf - t0 + F)
     assert len(np.unique(pairs)) == K
+    # observations sorted by point (stable), the order the device map keeps
+    assert np.all(np.diff(m.obs_point) >= 0)
     fr = m.obs_frame
     assert np.array_equal(fr >= 0, m.obs_kf >= t0)
     assert np.array_equal(np.where(fr >= 0, t0 + fr, t0 - 1 - (-1 - fr)), m.obs_kf)
