@@ -3159,20 +3159,10 @@ namespace {
 // Build-time scratch of the device plan (one allocation, cleared by the build before -- k_db_gather):
 //   pt_cnt[P_cap + 1] | hdr[8] | cov[C * C] | cam_cnt[C] | bits[C * Wd] (u64 words)
 // hdr: [0] valid observations, [1] largest count per point, [2] error flags, [3] points.
-// Runs of equal keys in consecutive lanes are combined before the atomics: the observations of one
-// keyframe are consecutive slots (the LocalMapping append), so their bitset words repeat across a
-// wave (new points have consecutive ids), and the observations of one point are consecutive in a
-// point-ordered window (the drop-in's), so their counts do.  A segmented inclusive scan over the
-// wave (runs end where the key changes) leaves each run's OR / count in its last lane, which does
-// one atomic; two lanes of one run setting the same bit are a point seen twice by one camera.
-__device__ __forceinline__ unsigned long long shfl_up_u64(unsigned long long v, int o) {
-  const int lo = __shfl_up((int)(v & 0xffffffffu), o, 64), hi = __shfl_up((int)(v >> 32), o, 64);
-  return ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo;
-}
 __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, int F, int Wd,
                                                  int* __restrict__ pt_cnt, int* __restrict__ hdr,
                                                  unsigned long long* __restrict__ bits) {
-  const int k = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 256 + threadIdx.x;
   const int n_obs_in = *w.d_n_obs, n_pt_in = *w.d_n_points;
   // live counts beyond the capacities are an error (flag 8); clamped, so nothing is touched past
   // the plan's allocations
@@ -3181,41 +3171,21 @@ __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, in
     hdr[3] = n_pt;
     if (n_obs_in > w.max_obs || n_pt_in > w.max_points || n_obs_in < 0 || n_pt_in < 0) atomicOr(&hdr[2], 8);
   }
-  if ((k & ~63) >= n_obs) return;  // whole waves past the end (the scans below need full waves)
-  int q = -1, f = -1 - F - 1, err = 0;
-  if (k < n_obs) { q = w.d_obs_point[k]; f = w.d_obs_frame[k]; }
-  const bool slot = k < n_obs && f >= -F && f < C;  // an observation (fixed or optimised camera)
-  if (k < n_obs && f >= C) err |= 2;
-  if (slot && (q < 0 || q >= n_pt)) err |= 1;
-  const bool cnt = slot && !(err & 1);
-  const bool opt = cnt && f >= 0;
-  // per-point counts: runs of equal q
-  long long ckey = cnt ? q : -1 - (long long)lane;  // non-counting lanes are runs of their own
-  int c = cnt ? 1 : 0;
-  // camera x point bits: runs of equal (f, word)
-  long long bkey = opt ? (long long)f * Wd + (q >> 6) : -1 - (long long)lane;
-  unsigned long long m = opt ? 1ull << (q & 63) : 0ull;
-  bool dup = false;
-  bool cseg = lane == 0 || __shfl_up(ckey, 1, 64) != ckey;  // run heads
-  bool bseg = lane == 0 || __shfl_up(bkey, 1, 64) != bkey;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int cu = __shfl_up(c, o, 64);
-    const unsigned long long mu = shfl_up_u64(m, o);
-    const bool csu = __shfl_up((int)cseg, o, 64), bsu = __shfl_up((int)bseg, o, 64);
-    if (lane >= o) {
-      if (!cseg) { c += cu; cseg = csu; }
-      if (!bseg) { dup |= (m & mu) != 0; m |= mu; bseg = bsu; }
+  if (k >= n_obs) return;
+  const int q = w.d_obs_point[k], f = w.d_obs_frame[k];
+  if (f >= -F && f < C) {
+    if (q < 0 || q >= n_pt) {
+      atomicOr(&hdr[2], 1);
+    } else {
+      atomicAdd(&pt_cnt[q], 1);
+      if (f >= 0) {
+        const unsigned long long m = 1ull << (q & 63);
+        if (atomicOr(&bits[(size_t)f * Wd + (q >> 6)], m) & m) atomicOr(&hdr[2], 4);
+      }
     }
+  } else if (f >= C) {
+    atomicOr(&hdr[2], 2);
   }
-  const bool ctail = lane == 63 || __shfl_down(ckey, 1, 64) != ckey;
-  const bool btail = lane == 63 || __shfl_down(bkey, 1, 64) != bkey;
-  if (cnt && ctail) atomicAdd(&pt_cnt[q], c);
-  if (opt && btail) {
-    if (atomicOr(&bits[(size_t)f * Wd + (q >> 6)], m) & m) err |= 4;
-  }
-  if (dup) err |= 4;
-  if (err) atomicOr(&hdr[2], err);
 }
 
 // The build's first phase when the observation slots are already sorted by point (the LocalMapping
