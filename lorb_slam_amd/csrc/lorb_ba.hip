@@ -652,32 +652,19 @@ __device__ __forceinline__ double& band(double* A, int bw, int i, int j) {
 // are re-read from that XCD's L2 instead of from the fabric.
 // DIAG (a diagonal block: pr.x == pr.y, pairs in camera-slot order): the camera's rhs term
 // Jc^T g of the same observation is accumulated from the tiles already loaded
-// FU (diagonal blocks of the fused iteration, k_ba_schur<true>): the camera's normal block
-// U = Jc^T Jc (21, packed upper) and V = Jc^T r (6) of the same observation, accumulated with the
-// expressions and in the per-thread order of k_ba_camera (same bits)
-template <bool DIAG, bool FU = false>
-__device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc)[36], double (&r6)[6],
-                                           double* U = nullptr, double* V = nullptr) {
-  double Qh[6], Jl[6], Ch[12], Cl[12], g0 = 0.0, g1 = 0.0, cr0 = 0.0, cr1 = 0.0;
+template <bool DIAG>
+__device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc)[36], double (&r6)[6]) {
+  double Qh[6], Jl[6], Ch[12], Cl[12], g0 = 0.0, g1 = 0.0;
 #pragma unroll
   for (int k = 0; k < 6; ++k) { Qh[k] = d.obs_Q[6 * pr.x + k]; Jl[k] = d.obs_Jps[6 * pr.y + k]; }
 #pragma unroll
   for (int k = 0; k < 12; ++k) { Ch[k] = d.obs_Jc[12 * pr.x + k]; Cl[k] = DIAG ? Ch[k] : d.obs_Jc[12 * pr.y + k]; }
-  if (FU) { cr0 = d.cam_r[2 * pr.x]; cr1 = d.cam_r[2 * pr.x + 1]; }
   if (DIAG) {
     g0 = d.obs_g[2 * pr.x]; g1 = d.obs_g[2 * pr.x + 1];
 #pragma unroll
     for (int k = 0; k < 6; ++k) r6[k] += Ch[k] * g0 + Ch[6 + k] * g1;
   }
-  if (FU) {
-    int q = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      V[a] += Ch[a] * cr0 + Ch[6 + a] * cr1;
-#pragma unroll
-      for (int b = a; b < 6; ++b) U[q++] += Ch[a] * Ch[b] + Ch[6 + a] * Ch[6 + b];
-    }
-  }
+
   double M[4], N[12];
 #pragma unroll
   for (int r = 0; r < 2; ++r)
@@ -730,11 +717,6 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
   // indices are read while this step's tiles load (same pairs, same order)
   const bool diag = bp.ch == bp.cl;
   double r6[6] = {0, 0, 0, 0, 0, 0};
-  double Uc[FU ? 21 : 1], Vc[FU ? 6 : 1];
-#pragma unroll
-  for (int k = 0; k < (FU ? 21 : 1); ++k) Uc[k] = 0.0;
-#pragma unroll
-  for (int k = 0; k < (FU ? 6 : 1); ++k) Vc[k] = 0.0;
   // A diagonal block's pairs are (e, e) for the camera's slots e in order (both plan builders),
   // so thread t meets the observations a0 + t, a0 + t + 256, ... of the rhs sum in its order.
   auto run = [&](auto diag_c) {
@@ -747,13 +729,40 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
       const bool two = q + 256 < end;
       const int qn = q + 512;
       if (qn < end) { p0n = d.pairs[qn]; p1n = d.pairs[qn + 256 < end ? qn + 256 : qn]; }
-      schur_pair<DG, DG && FU>(d, p0, acc, r6, Uc, Vc);
-      if (two) schur_pair<DG, DG && FU>(d, p1, acc, r6, Uc, Vc);
+      schur_pair<DG>(d, p0, acc, r6);
+      if (two) schur_pair<DG>(d, p1, acc, r6);
     }
   };
   if (diag) run(std::true_type{});
   else run(std::false_type{});
-  if (FU && diag) {  // the camera's U, V: k_ba_camera's reduction (wave butterfly, waves in order)
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    const double v = wave_sum(acc[k]);
+    if (lane == 0) red[wv][k] = v;
+  }
+  if (FU && diag) {
+    // the camera's U = Jc^T Jc, V = Jc^T r (k_ba_camera's work and bits: per thread the slots
+    // a0 + t, a0 + t + 256, ..., then the wave butterfly and the waves in order), a second pass over
+    // the camera's tiles (L2-resident) once the Schur accumulators are free
+    double Uc[21], Vc[6];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) Uc[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Vc[k] = 0.0;
+    for (int q = bp.off + t; q < end; q += 256) {
+      const int e = d.pairs[q].x;
+      double J[12];
+#pragma unroll
+      for (int k = 0; k < 12; ++k) J[k] = d.obs_Jc[12 * e + k];
+      const double r0 = d.cam_r[2 * e], r1 = d.cam_r[2 * e + 1];
+      int qq = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        Vc[a] += J[a] * r0 + J[6 + a] * r1;
+#pragma unroll
+        for (int b = a; b < 6; ++b) Uc[qq++] += J[a] * J[b] + J[6 + a] * J[6 + b];
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 21; ++k) {
       const double v = wave_sum(Uc[k]);
@@ -770,11 +779,6 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
       if (t < 21) d.U_part[21 * bp.ch + t] = v;
       else d.V_part[6 * bp.ch + t - 21] = v;
     }
-  }
-#pragma unroll
-  for (int k = 0; k < 36; ++k) {
-    const double v = wave_sum(acc[k]);
-    if (lane == 0) red[wv][k] = v;
   }
   __syncthreads();
   if (t < 36) {

@@ -343,10 +343,22 @@ int main() {
     std::vector<MiniPoint*> cpts;
     for (int q = 0; q < NP; q++) {
       MiniPoint* p = new MiniPoint();
-      const float X[3] = {urand(-6, 8), urand(-3, 3), urand(4, 20)};
       const int len = 7 + (int)(rnd() % 2), s = (int)(rnd() % (NW - len + 1));
+      // in front of the keyframe in the middle of its range, inside its image (X = R^T (pc - t))
+      float X[3];
+      {
+        const MiniFrame* fm = kf[NFX + s + len / 2];
+        const float z = urand(4, 20), u = urand(60, 692), v = urand(60, 420);
+        const float pc[3] = {(u - fm->fp.cx) / fm->fp.fx * z - fm->Tcw[3], (v - fm->fp.cy) / fm->fp.fy * z - fm->Tcw[7],
+                             z - fm->Tcw[11]};
+        for (int c = 0; c < 3; c++) X[c] = fm->Tcw[c] * pc[0] + fm->Tcw[4 + c] * pc[1] + fm->Tcw[8 + c] * pc[2];
+      }
       for (int j = s; j < s + len; j++) observe(p, kf[NFX + j], X);
-      if (s < 3 && rnd() % 3 == 0) observe(p, kf[rnd() % NFX], X);  // fixed keyframes (MPCost)
+      if (s < 6) {  // the older points are also seen by two of the fixed keyframes (MPCost): the gauge
+        const int a = (int)(rnd() % NFX), b = (a + 1 + (int)(rnd() % (NFX - 1))) % NFX;
+        observe(p, kf[std::min(a, b)], X);
+        observe(p, kf[std::max(a, b)], X);
+      }
       for (int c = 0; c < 3; c++) p->pos[c] = X[c] + urand(-0.05f, 0.05f);
       cpts.push_back(p);
     }
