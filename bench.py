@@ -229,8 +229,11 @@ def workload_c4(ctx, args, rank):
         # Schur block accumulation: compulsory bytes = the W and Y tiles (2 x 18 doubles per
         # optimised observation) read once + the S band written once
         2: ("hbm", W * opt_obs * 36 * 8.0 + W * (6 * F) * (bw + 1) * 8.0, "GB/s"),
-        # linearisation: residual + 2x3 + 2x6 Jacobian per observation: reads pose/point/uv, writes 20 doubles
-        3: ("hbm", W * n_obs * (20 * 8.0 + 16 + 8), "GB/s"),
+        # linearisation with the point-block prep fused in (k_ba_lin): per observation it writes the
+        # residual (2), Jp (2x3) and Jc (2x6), and the Schur inputs Jps (2x3), Q (2x3), g (2) -- 34
+        # doubles (the camera-major residual copy, 2 more, is layout, not counted) -- and reads uv
+        # (16 B) and three structure indices (12 B); per point it reads X (24 B)
+        3: ("hbm", W * (n_obs * (34 * 8.0 + 16 + 12) + n_pts * 24.0), "GB/s"),
         # banded Cholesky + 2 triangular solves: n*bw^2 + 4*n*bw flops
         4: ("fp64", W * ((6 * F) * bw * bw + 4.0 * (6 * F) * bw), "TFLOP/s"),
     }
@@ -513,7 +516,9 @@ def pmc_traffic(workload, kernel):
 
 def roofline_entry(kt, wl, steps):
     """Dominant kernel (largest total device time in the profile pass) vs its roofline."""
-    best = max(kt.items(), key=lambda kv: kv[1][0]) if kt else None
+    # kernels with an algorithmic figure only (the all-reduce timer, K 7, is not a kernel)
+    cand = {k: v for k, v in kt.items() if k in (0, 1) or k in wl.get("kspec", {})}
+    best = max(cand.items(), key=lambda kv: kv[1][0]) if cand else None
     if not best or best[1][1] == 0:
         return None
     k, (ms, n) = best

@@ -489,14 +489,17 @@ __global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d, LMOpt o) {
   if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[0] = cost; P[1] = gm; P[2] = xn2; }
 }
 
-// K2: per-camera normal blocks (one wavefront per optimised camera)
-__global__ __launch_bounds__(256) void k_ba_camera(BaDev d) {
-  __shared__ double red[4][27];
-  const int c = blockIdx.x;
+// K2: per-camera normal blocks U = Jc^T Jc (21, packed upper), V = Jc^T r (6): one 256-thread
+// workgroup per optimised camera, lanes stride the camera's slots, fixed-order wave + LDS reduction.
+// Also the trailing workgroups of the fused iteration's k_ba_schur<true>.
+template <bool FU>
+__device__ __forceinline__ void camera_block(const BaDev& d, int c, double (&red)[4][27]) {
   const int w = d.cam_win[c];
   const int a0 = d.cam_obs_off[c], a1 = d.cam_obs_off[c + 1];  // issued with cam_win
   const WinState& S = d.st[w];
-  if (S.done || !S.relin) return;
+  // FU: also after a rejected step (same U, V: the tiles are the linearisation's), since the
+  // diagonal Schur block is combined with them every iteration
+  if (S.done || (!FU && !S.relin)) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   double U[21], V[6];
 #pragma unroll
@@ -527,16 +530,15 @@ __global__ __launch_bounds__(256) void k_ba_camera(BaDev d) {
     if (lane == 0) red[wv][21 + k] = v;
   }
   __syncthreads();
-  if (t == 0) {
-#pragma unroll
-    for (int k = 0; k < 21; ++k) U[k] = ((red[0][k] + red[1][k]) + red[2][k]) + red[3][k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) V[k] = ((red[0][21 + k] + red[1][21 + k]) + red[2][21 + k]) + red[3][21 + k];
-#pragma unroll
-    for (int k = 0; k < 21; ++k) d.U_part[21 * c + k] = U[k];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) d.V_part[6 * c + k] = V[k];
+  if (t < 27) {
+    const double v = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    if (t < 21) d.U_part[21 * c + t] = v;
+    else d.V_part[6 * c + t - 21] = v;
   }
+}
+__global__ __launch_bounds__(256) void k_ba_camera(BaDev d) {
+  __shared__ double red[4][27];
+  camera_block<false>(d, blockIdx.x, red);
 }
 
 // Lane-strided partial sums over a window's point groups (b = lane, lane + 64, ... in that order,
@@ -688,14 +690,20 @@ __device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc
 // 36 doubles read); the camera Jacobi scales are applied once per block.  Block pairs are sorted
 // by camera and remapped so that each XCD (blockIdx % 8 group) takes a contiguous run: the tiles
 // of a camera are re-read from that XCD's L2 instead of from the fabric.
-// FU (the fused iteration of unsharded plans, after the first): the diagonal block of camera c
-// also forms c's normal block U, V (k_ba_camera's work, same bits) and writes them for the head of
-// the iteration, which runs inside the Cholesky kernel (lm_head); the Jacobi scale is the one of
-// iteration 0.
+// FU (the fused iteration of unsharded plans, after the first): Ctot trailing workgroups do
+// k_ba_camera's work (U, V for the head of the iteration, which runs inside the Cholesky kernel,
+// lm_head) concurrently with the pair blocks.  The diagonal blocks write -a and -r only; the
+// Cholesky (k_ba_chol_2s<true>) adds U sc sc^T + D^2 and V sc as it stages the band and loads the
+// rhs: (-a) + v == v - a exactly, so the bits are those of k_ba_schur<false>.  The Jacobi scale is
+// iteration 0's.
 template <bool FU>
-__global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
+__global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o, int grid_bp) {
   __shared__ double red[4][37];
-  __shared__ double redu[4][27];
+  if (FU && (int)blockIdx.x >= grid_bp) {  // the trailing workgroups: k_ba_camera's work
+    __shared__ double redu[4][27];
+    camera_block<true>(d, blockIdx.x - grid_bp, redu);
+    return;
+  }
   const int n_bp = d.live[1];
   if ((int)blockIdx.x >= n_bp) return;
   int bid;
@@ -740,46 +748,6 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
     const double v = wave_sum(acc[k]);
     if (lane == 0) red[wv][k] = v;
   }
-  if (FU && diag) {
-    // the camera's U = Jc^T Jc, V = Jc^T r (k_ba_camera's work and bits: per thread the slots
-    // a0 + t, a0 + t + 256, ..., then the wave butterfly and the waves in order), a second pass over
-    // the camera's tiles (L2-resident) once the Schur accumulators are free
-    double Uc[21], Vc[6];
-#pragma unroll
-    for (int k = 0; k < 21; ++k) Uc[k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Vc[k] = 0.0;
-    for (int q = bp.off + t; q < end; q += 256) {
-      const int e = d.pairs[q].x;
-      double J[12];
-#pragma unroll
-      for (int k = 0; k < 12; ++k) J[k] = d.obs_Jc[12 * e + k];
-      const double r0 = d.cam_r[2 * e], r1 = d.cam_r[2 * e + 1];
-      int qq = 0;
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        Vc[a] += J[a] * r0 + J[6 + a] * r1;
-#pragma unroll
-        for (int b = a; b < 6; ++b) Uc[qq++] += J[a] * J[b] + J[6 + a] * J[6 + b];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 21; ++k) {
-      const double v = wave_sum(Uc[k]);
-      if (lane == 0) redu[wv][k] = v;
-    }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const double v = wave_sum(Vc[k]);
-      if (lane == 0) redu[wv][21 + k] = v;
-    }
-    __syncthreads();
-    if (t < 27) {
-      const double v = ((redu[0][t] + redu[1][t]) + redu[2][t]) + redu[3][t];
-      if (t < 21) d.U_part[21 * bp.ch + t] = v;
-      else d.V_part[6 * bp.ch + t - 21] = v;
-    }
-  }
   __syncthreads();
   if (t < 36) {
     const int i = t / 6, j = t % 6;
@@ -789,15 +757,17 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
     double* A = d.env_part + W.env_base;
     if (diag) {
       if (j <= i) {
-        double v = 0.0;
-        if (d.rank0) {  // camera block J^T J + D^2 once (sharded: U is already global)
-          const double* sc = d.scale_pose + 6 * bp.ch;
-          const double u = FU ? ((redu[0][u21(i, j)] + redu[1][u21(i, j)]) + redu[2][u21(i, j)]) + redu[3][u21(i, j)]
-                              : d.U[21 * bp.ch + u21(i, j)];
-          v = u * sc[i] * sc[j];
-          if (i == j) v += fmin(fmax(v, o.min_diag), o.max_diag) / S.radius;
+        if (FU) {  // -a: k_ba_chol_2s<true> adds the camera block while staging the band
+          band(A, W.bw, 6 * lh + i, 6 * lh + j) = -a;
+        } else {
+          double v = 0.0;
+          if (d.rank0) {  // camera block J^T J + D^2 once (sharded: U is already global)
+            const double* sc = d.scale_pose + 6 * bp.ch;
+            v = d.U[21 * bp.ch + u21(i, j)] * sc[i] * sc[j];
+            if (i == j) v += fmin(fmax(v, o.min_diag), o.max_diag) / S.radius;
+          }
+          band(A, W.bw, 6 * lh + i, 6 * lh + j) = v - a;
         }
-        band(A, W.bw, 6 * lh + i, 6 * lh + j) = v - a;
       }
     } else {
       band(A, W.bw, 6 * lh + i, 6 * ll + j) = -a;
@@ -813,9 +783,12 @@ __global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o) {
     __syncthreads();
     if (t < 6) {
       const double r = (((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]) * d.scale_pose[6 * bp.ch + t];
-      const double vv = FU ? ((redu[0][21 + t] + redu[1][21 + t]) + redu[2][21 + t]) + redu[3][21 + t] : d.V[6 * bp.ch + t];
-      const double vs = d.rank0 ? vv * d.scale_pose[6 * bp.ch + t] : 0.0;
-      d.rhs_part[W.row_base + 6 * (bp.ch - W.pose_base) + t] = vs - r;
+      if (FU) {  // -r: k_ba_chol_2s<true> adds V sc when it loads the rhs
+        d.rhs_part[W.row_base + 6 * (bp.ch - W.pose_base) + t] = -r;
+      } else {
+        const double vs = d.rank0 ? d.V[6 * bp.ch + t] * d.scale_pose[6 * bp.ch + t] : 0.0;
+        d.rhs_part[W.row_base + 6 * (bp.ch - W.pose_base) + t] = vs - r;
+      }
     }
   }
 }
@@ -1465,15 +1438,13 @@ struct BandSide {
       for (int q = 0; q < NB; ++q) {
         bad |= !(akk > 0.0);
         double y = __builtin_amdgcn_rsq(akk);
-        {
-          const double e = fma(-akk * y, y, 1.0);
-          y = fma(0.5 * y, e, y);
-        }
         __builtin_amdgcn_sched_barrier(0);
         if (q >= 1) {
 #pragma unroll
           for (int q2 = q + 1; q2 < NB; ++q2) P[q2] = fma(-P[q - 1], mp[q2], P[q2]);
         }
+        // The chain wave is VALU-issue bound (about 45 instructions per column): one Newton step on
+        // v_rsq_f64 (about 2^-23 relative) leaves ~1e-14, far inside north_star's 1e-5
         {
           const double e = fma(-akk * y, y, 1.0);
           y = fma(0.5 * y, e, y);
@@ -1795,6 +1766,25 @@ __device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, doub
   }
 }
 
+// The fused iteration's camera blocks (k_ba_schur<true> leaves -a on the diagonal camera blocks):
+// rows [r0, r1) of the staged band get v = U sc sc^T (+ D^2 on the diagonal), k_ba_schur<false>'s
+// expression, added as (-a) + v == v - a.  Threads tid, tid + nthr, ... of the caller.
+__device__ __forceinline__ void stage_fix(const BaDev& d, const LMOpt& o, double* Ab, const BaWin& W, double radius,
+                                          int r0, int r1, int tid, int nthr) {
+  r1 = min(r1, W.n);
+  const int B1 = W.bw + 1;
+  for (int q = tid; q < (r1 - r0) * 6; q += nthr) {
+    const int i = r0 + q / 6, i6 = i % 6, j6 = q % 6;
+    if (j6 > i6) continue;
+    const int c = W.pose_base + i / 6;
+    const double* sc = d.scale_pose + 6 * c;
+    double v = d.U[21 * c + u21(i6, j6)] * sc[i6] * sc[j6];
+    if (i6 == j6) v += fmin(fmax(v, o.min_diag), o.max_diag) / radius;
+    double& e = Ab[i * B1 + (j6 - i6 + W.bw)];
+    e = e + v;
+  }
+}
+
 constexpr int kChol2sThreads = 512;
 // LDS words of k_ba_chol_2s: band (n16 rows), both sides' rhs (n16 + 48), two 64 x 18 exchanges
 // (together the 48 x 48 combine), zX (48), two 64 x 17 panel hand-off buffers, a zero word
@@ -1863,6 +1853,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   {
     const int row = t < rt ? t : n16 - 1 - (t - rt);
     rz = (t < rt + rb && row < n) ? d.rhs[W.row_base + row] : 0.0;
+    // fused: the rhs holds -r; + V sc (k_ba_schur<false>'s vs - r, same bits)
+    if (HEAD && t < rt + rb && row < n) rz = rz + d.V[6 * W.pose_base + row] * d.scale_pose[6 * W.pose_base + row];
   }
   if (prog) {  // both sides' first ib blocks in one batch
     stage_band2<7>(S2, Ab, 0, ib * cpb, (nbk - ib) * cpb, nch, t, NT, n, bw, nsrc);
@@ -1873,7 +1865,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   else if (t < rt + rb) zb[t - rt] = rz;
   for (int k = t + NT; k < rt + rb; k += NT) {  // (n16 > 464 only)
     const int row = k < rt ? k : n16 - 1 - (k - rt);
-    const double v = row < n ? d.rhs[W.row_base + row] : 0.0;
+    double v = row < n ? d.rhs[W.row_base + row] : 0.0;
+    if (HEAD && row < n) v = v + d.V[6 * W.pose_base + row] * d.scale_pose[6 * W.pose_base + row];
     if (k < rt) zt[k] = v; else zb[k - rt] = v;
   }
   if (t == 0) {
@@ -1888,6 +1881,15 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     s_mask = msk;
   }
   __syncthreads();
+  if (HEAD) {  // the camera blocks of the rows staged so far
+    if (prog) {
+      stage_fix(d, o, Ab, W, S0.radius, 0, 16 * ib, t, NT);
+      stage_fix(d, o, Ab, W, S0.radius, 16 * (nbk - ib), n16, t, NT);
+    } else {
+      stage_fix(d, o, Ab, W, S0.radius, 0, n16, t, NT);
+    }
+    __syncthreads();
+  }
   BandSide top{Ab, zt, xt, rt, bw, lane, bw, bw, 1};
   BandSide bot{Ab, zb, xb, rb, bw, lane, (n16 - 1) * B1 + bw, -1, -bw};
   top.pdone = &s_pdone[0]; bot.pdone = &s_pdone[1];
@@ -1929,6 +1931,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
       for (int k = 0; k < (side == 0 ? mid - lo : hi - mid); ++k) {
         const int b = side == 0 ? lo + k : hi - 1 - k;
         stage_band<7>(S2, Ab, b * cpb, min((b + 1) * cpb, nch), lane, 64, n, bw, nsrc);
+        if (HEAD) {
+          wave_sync_lds();
+          stage_fix(d, o, Ab, W, S0.radius, 16 * b, 16 * b + 16, lane, 64);
+        }
         if (lane == 0) __hip_atomic_fetch_or(&s_mask, 1ull << b, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
@@ -1938,7 +1944,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     const WinState S = lm_head<false>(d, o, w, lane, S0, W);
     if (lane == 0) s_head_done = S.done;
   }
-  // diagonal-block inverses (waves 4 / 5)
+  // diagonal-block inverses (waves 4 / 5; on waves 6 / 7 after their staging, off the chain waves'
+  // SIMDs, they measured no faster)
   if (wv == 4 || wv == 5) {
     int* pd = &s_pdone[side];
     const int nblk = (side == 0 ? m : nB) / 16;
@@ -3009,8 +3016,8 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
   if (P->env_total && !chol_in_lds && !P->comm) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   if (P->grid_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
-    if (fused) hipLaunchKernelGGL(k_ba_schur<true>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
-    else hipLaunchKernelGGL(k_ba_schur<false>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
+    if (fused) hipLaunchKernelGGL(k_ba_schur<true>, dim3(P->grid_bp + P->Ctot), dim3(256), 0, s, d, o, (int)P->grid_bp);
+    else hipLaunchKernelGGL(k_ba_schur<false>, dim3(P->grid_bp), dim3(256), 0, s, d, o, (int)P->grid_bp);
   }
   if (P->comm) {  // exchange 2: reduced camera system, rhs, point-block failure flags
     lorb::KernelTimer kt(ctx, LORB_K_ALLREDUCE);
@@ -3193,47 +3200,48 @@ __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, in
 }
 
 // The build's first phase when the observation slots are already sorted by point (the LocalMapping
-// map keeps them so; the drop-in's windows are gathered point by point): no counting sort.  Per
-// observation: validity, the camera x point bits (a bit already set: a point seen twice by one
-// camera); per point p <= n_points: its first slot (a binary search, so points without
-// observations get the next point's), and the largest count per point.  A slot out of order or
-// unused (frame < -n_fixed) sets flag 16: the host then runs the general phase instead.
+// map keeps them so; the drop-in's windows are gathered point by point): no counting sort.  One
+// thread per slot i <= n_obs: validity, the camera x point bits (a bit already set: a point seen
+// twice by one camera); the point offsets from the run boundaries (slot i is the first slot of the
+// points (op[i - 1], op[i]], so points without observations get the next point's, and slot n_obs
+// closes the points after the last one); the run length of the point starting at i (its largest
+// over points).  A slot out of order or unused (frame < -n_fixed) sets flag 16: the host then runs
+// the general phase instead.
 __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, int F, int Wd, int* __restrict__ pt_off,
                                                    int* __restrict__ hdr, unsigned long long* __restrict__ bits) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int n_obs_in = *w.d_n_obs, n_pt_in = *w.d_n_points;
   const int n_obs = max(min(n_obs_in, w.max_obs), 0), n_pt = max(min(n_pt_in, w.max_points), 0);
   const int* __restrict__ op = w.d_obs_point;
-  int err = 0;
+  int err = 0, cnt = 0;
   if (i == 0) {
     hdr[3] = n_pt;
     hdr[0] = n_obs;
     if (n_obs_in > w.max_obs || n_pt_in > w.max_points || n_obs_in < 0 || n_pt_in < 0) err |= 8;
   }
-  if (i < n_obs) {
-    const int q = op[i], f = w.d_obs_frame[i];
-    if (f < -F) err |= 16;
-    else if (f >= C) err |= 2;
-    else if (q < 0 || q >= n_pt) err |= 1;
-    else if (f >= 0) {
-      const unsigned long long m = 1ull << (q & 63);
-      if (atomicOr(&bits[(size_t)f * Wd + (q >> 6)], m) & m) err |= 4;
-    }
-    if (i > 0 && op[i - 1] > q) err |= 16;
-  }
-  int cnt = 0;
-  if (i <= n_pt) {
-    auto lb = [&](int p) {
-      int lo = 0, hi = n_obs;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (op[mid] < p) lo = mid + 1; else hi = mid;
+  if (i <= n_obs) {
+    const int prev = i > 0 ? op[i - 1] : -1;
+    const int q = i < n_obs ? op[i] : n_pt;
+    if (i < n_obs) {
+      const int f = w.d_obs_frame[i];
+      if (f < -F) err |= 16;
+      else if (f >= C) err |= 2;
+      else if (q < 0 || q >= n_pt) err |= 1;
+      else if (f >= 0) {
+        const unsigned long long m = 1ull << (q & 63);
+        if (atomicOr(&bits[(size_t)f * Wd + (q >> 6)], m) & m) err |= 4;
       }
-      return lo;
-    };
-    const int a = lb(i);
-    pt_off[i] = a;
-    if (i < n_pt) cnt = lb(i + 1) - a;
+    }
+    if (prev > q) err |= 16;
+    else if (prev != q) {
+      const int p1 = min(q, n_pt);
+      for (int p = max(prev + 1, 0); p <= p1; ++p) pt_off[p] = i;
+      if (i < n_obs) {
+        int j = i + 1;
+        while (j < n_obs && op[j] == q) ++j;
+        cnt = j - i;
+      }
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cnt = max(cnt, __shfl_xor(cnt, o, 64));
@@ -3705,7 +3713,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
     b.dirty = true;
     if (sorted) {
-      hipLaunchKernelGGL(k_db_sorted, dim3(std::max<unsigned>(nb_obs, lorb::ceil_div(b.P_cap + 1, 256))), dim3(256), 0, s, *w, C,
+      hipLaunchKernelGGL(k_db_sorted, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), 0, s, *w, C,
                          F, b.Wd, const_cast<int*>(d.pt_obs_off), b.hdr, b.bits);
     } else {
       hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);

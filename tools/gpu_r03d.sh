@@ -11,6 +11,10 @@ mkdir -p $O $P
 export TMPDIR=/tmp
 TESTS=${TESTS:-"test_gpu_solver test_gpu_map test_gpu_ba test_gpu_host_cpp"}
 fail=0
+if [ -n "$CHOL" ]; then  # Cholesky timing and the per-panel trace (tools/build_variant.sh trace -DLORB_CHOL_TRACE)
+  tools/gpu_step.sh 200 $O/d_time_ba.log python tools/time_ba.py || exit $?
+  LORB_LIB_PATH=$R/lorb_slam_amd/liblorb_trace.so tools/gpu_step.sh 120 $O/d_chol_trace.log python tools/chol_trace.py || exit $?
+fi
 for t in $TESTS; do
   tools/gpu_step.sh 300 $O/d_$t.log python -u -m pytest tests/$t.py -m gpu -q --timeout 200 --timeout-method thread
   rc=$?
