@@ -3207,46 +3207,100 @@ __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, in
 // closes the points after the last one); the run length of the point starting at i (its largest
 // over points).  A slot out of order or unused (frame < -n_fixed) sets flag 16: the host then runs
 // the general phase instead.
+// The camera x point bits of a workgroup's slots (consecutive points: a few 64-point words) are
+// OR-ed in LDS and flushed with one non-returning atomic per (camera, word); a point seen twice by
+// one camera is found by the thread that starts the point's run, among the run's frames (the run
+// ends at the next run start of the wave's ballot, or by a scan for the wave's last run).  The
+// largest run and the error bits are reduced per workgroup before their one atomic each.
+constexpr int kDbWords = 4;  // 64-point words per workgroup held in LDS (more: global atomics)
 __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, int F, int Wd, int* __restrict__ pt_off,
                                                    int* __restrict__ hdr, unsigned long long* __restrict__ bits) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  extern __shared__ unsigned long long s_bits[];  // C * kDbWords
+  __shared__ int s_cnt, s_err;
+  const int t = threadIdx.x, lane = t & 63;
+  const int i = blockIdx.x * 256 + t;
   const int n_obs_in = *w.d_n_obs, n_pt_in = *w.d_n_points;
   const int n_obs = max(min(n_obs_in, w.max_obs), 0), n_pt = max(min(n_pt_in, w.max_points), 0);
   const int* __restrict__ op = w.d_obs_point;
+  const int* __restrict__ of = w.d_obs_frame;
+  for (int k = t; k < C * kDbWords; k += 256) s_bits[k] = 0ull;
+  if (t == 0) { s_cnt = 0; s_err = 0; }
+  const int i0 = blockIdx.x * 256;
+  const int w0 = i0 < n_obs ? max(op[i0], 0) >> 6 : 0;  // the workgroup's first word
   int err = 0, cnt = 0;
   if (i == 0) {
     hdr[3] = n_pt;
     hdr[0] = n_obs;
     if (n_obs_in > w.max_obs || n_pt_in > w.max_points || n_obs_in < 0 || n_pt_in < 0) err |= 8;
   }
-  if (i <= n_obs) {
-    const int prev = i > 0 ? op[i - 1] : -1;
-    const int q = i < n_obs ? op[i] : n_pt;
-    if (i < n_obs) {
-      const int f = w.d_obs_frame[i];
-      if (f < -F) err |= 16;
-      else if (f >= C) err |= 2;
-      else if (q < 0 || q >= n_pt) err |= 1;
-      else if (f >= 0) {
-        const unsigned long long m = 1ull << (q & 63);
-        if (atomicOr(&bits[(size_t)f * Wd + (q >> 6)], m) & m) err |= 4;
-      }
+  const int prev = (i > 0 && i <= n_obs) ? op[i - 1] : -1;
+  const int q = i < n_obs ? op[i] : n_pt;
+  const int f = i < n_obs ? of[i] : -1;
+  const bool bound = i <= n_obs && (i == n_obs || prev != q);  // a run starts (or the slots end) here
+  const unsigned long long bal = __ballot(bound);
+  __syncthreads();
+  if (i < n_obs) {
+    if (f < -F) err |= 16;
+    else if (f >= C) err |= 2;
+    else if (q < 0 || q >= n_pt) err |= 1;
+    else if (f >= 0) {
+      const unsigned long long m = 1ull << (q & 63);
+      const int wl = (q >> 6) - w0;
+      if (wl >= 0 && wl < kDbWords) atomicOr(&s_bits[f * kDbWords + wl], m);
+      else __hip_atomic_fetch_or(&bits[(size_t)f * Wd + (q >> 6)], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+  if (i <= n_obs) {
     if (prev > q) err |= 16;
     else if (prev != q) {
       const int p1 = min(q, n_pt);
       for (int p = max(prev + 1, 0); p <= p1; ++p) pt_off[p] = i;
       if (i < n_obs) {
-        int j = i + 1;
-        while (j < n_obs && op[j] == q) ++j;
-        cnt = j - i;
+        // run end: the next boundary of this wave, else scanned past the wave
+        const unsigned long long above = lane < 63 ? bal & (~0ull << (lane + 1)) : 0ull;
+        int e;
+        if (above) {
+          e = i - lane + __builtin_ctzll(above);
+        } else {
+          e = i - lane + 64;
+          while (e < n_obs && op[e] == q) ++e;
+          e = min(max(e, i + 1), n_obs);
+        }
+        cnt = e - i;
+        // duplicate cameras within the run (optimised cameras only, as the bitset flags them)
+        constexpr int kR = 16;
+        int fr[kR];
+#pragma unroll
+        for (int k = 0; k < kR; ++k) fr[k] = k < cnt ? of[i + k] : -1 - k;
+#pragma unroll
+        for (int a = 1; a < kR; ++a)
+#pragma unroll
+          for (int b = 0; b < a; ++b)
+            if (fr[a] >= 0 && fr[a] == fr[b]) err |= 4;
+        for (int a = kR; a < cnt; ++a) {  // long runs: the rest against everything before it
+          const int fa = of[i + a];
+          if (fa < 0) continue;
+          for (int b = 0; b < a; ++b)
+            if (of[i + b] == fa) err |= 4;
+        }
       }
     }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) cnt = max(cnt, __shfl_xor(cnt, o, 64));
-  if ((threadIdx.x & 63) == 0 && cnt) atomicMax(&hdr[1], cnt);
-  if (err) atomicOr(&hdr[2], err);
+  if (lane == 0 && cnt) atomicMax(&s_cnt, cnt);
+  if (err) atomicOr(&s_err, err);
+  __syncthreads();
+  for (int k = t; k < C * kDbWords; k += 256) {
+    const unsigned long long v = s_bits[k];
+    const int wd = w0 + k % kDbWords;
+    if (v && wd < Wd)
+      __hip_atomic_fetch_or(&bits[(size_t)(k / kDbWords) * Wd + wd], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (t == 0) {
+    if (s_cnt > __hip_atomic_load(&hdr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&hdr[1], s_cnt);
+    if (s_err) atomicOr(&hdr[2], s_err);
+  }
 }
 
 // One workgroup: out[0 .. n) = exclusive prefix sums of in[0 .. n) (n_dev: n = *n_dev + 1, the
@@ -3713,7 +3767,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
     b.dirty = true;
     if (sorted) {
-      hipLaunchKernelGGL(k_db_sorted, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), 0, s, *w, C,
+      hipLaunchKernelGGL(k_db_sorted, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256),
+                         sizeof(unsigned long long) * kDbWords * std::max(C, 1), s, *w, C,
                          F, b.Wd, const_cast<int*>(d.pt_obs_off), b.hdr, b.bits);
     } else {
       hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);

@@ -60,6 +60,32 @@ def test_solver_windows_that_change(ctx):
         s.close()
 
 
+def test_solver_sorted_duplicate(ctx):
+    """point-sorted slots (the device build's k_db_sorted path, no counting sort): a camera seen twice
+    inside one point's run -- next to the first slot, and at the run's end -- is rejected; the sorted
+    window itself solves like the oracle, and the solver stays usable after the errors."""
+    s = BASolver(ctx)
+    try:
+        w0 = synth.ba_window(seed=25, n_kf=12, n_pts=3000, n_fixed=2, fixed_obs_per_kf=150)
+        o = np.argsort(np.asarray(w0["obs_point"]), kind="stable")
+        uv = np.asarray(w0["obs_uv"]).reshape(-1, 2)
+        w = dict(w0, obs_point=np.asarray(w0["obs_point"])[o], obs_frame=np.asarray(w0["obs_frame"])[o], obs_uv=uv[o])
+        check(s, w, OPT10)
+        opt_slots = np.flatnonzero(np.asarray(w["obs_frame"]) >= 0)
+        for k, at in ((int(opt_slots[len(opt_slots) // 2]), 1), (int(opt_slots[len(opt_slots) // 3]), 0)):
+            p = w["obs_point"][k]
+            run_end = int(np.searchsorted(w["obs_point"], p, side="right"))
+            pos = k + 1 if at == 1 else run_end
+            dup = dict(w, obs_point=np.insert(w["obs_point"], pos, p), obs_frame=np.insert(w["obs_frame"], pos, w["obs_frame"][k]),
+                       obs_uv=np.insert(w["obs_uv"], pos, w["obs_uv"][k], axis=0))
+            with pytest.raises(LorbError, match="twice"):
+                s.solve(dup, OPT10)
+        check(s, w, OPT10)
+        assert s.info()["host_plan_fallback"] == 0
+    finally:
+        s.close()
+
+
 def test_solver_fallback_and_errors(ctx):
     """a point observed twice by one camera (the reference's std::map<Frame*, size_t> cannot hold
     it) is rejected by both plan builders; bad indices are rejected like lorb_ba_local rejects them;
