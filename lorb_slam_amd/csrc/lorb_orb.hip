@@ -605,11 +605,21 @@ __device__ int oct_scan(int* a, int n, int* wsum) {
   return tot;
 }
 
-__global__ __launch_bounds__(kOctThreads) void k_orb_octree(OctArgs A) {
-  __shared__ int wsum[kOctThreads / 64];
-  __shared__ lorb::I4 wsum4[kOctThreads / 64];
-  __shared__ int s_L, s_mode, s_state, s_cm, s_E;
-  __shared__ long long s_key[kOctKeyChunk];
+// Shared LDS of k_orb_octree: the small scalars, and (fast path) the node list in LDS.
+struct OctSh {
+  int wsum[kOctThreads / 64];
+  lorb::I4 wsum4[kOctThreads / 64];
+  int L, mode, state, cm, E;
+};
+// The general path: every per-key and per-node array in global memory (any key / node count).
+__device__ __forceinline__ void oct_global(const OctArgs& A, OctSh& sh, long long* s_key) {
+  int* wsum = sh.wsum;
+  lorb::I4* wsum4 = sh.wsum4;
+  int& s_L = sh.L;
+  int& s_mode = sh.mode;
+  int& s_state = sh.state;
+  int& s_cm = sh.cm;
+  int& s_E = sh.E;
   const int l = blockIdx.x, t = threadIdx.x;
   const OctLevel V = A.lv[l];
   float* kx = A.kx + V.key_base;
@@ -874,6 +884,541 @@ __global__ __launch_bounds__(kOctThreads) void k_orb_octree(OctArgs A) {
     A.out_key[V.node_base + i] = best;
   }
   if (t == 0) A.out_cnt[l] = L;
+}
+
+// LDS layout of the octree fast path (oct_lds below).
+constexpr int kOctNC = 1024, kOctCells = 2048;
+constexpr int kQB = 8;  // sweep steps whose loads are issued together
+struct OctLds {
+  OctNode na[kOctNC], nb[kOctNC];  // nb first holds the cell offsets / output bases (gathering)
+  int act[kOctNC], rank[kOctNC], ech[kOctNC], tmp[kOctNC], surv[kOctNC];
+  lorb::I4 cnt[kOctNC], exb[kOctNC];
+  int2 mid[kOctNC];  // DivideNode's split point of a dividing candidate (x = -1: not dividing)
+};
+static_assert(sizeof(OctNode) * kOctNC >= sizeof(int) * 2 * (kOctCells + 1), "cell arrays alias nb");
+
+// register-resident four counters indexed by a runtime class (selects, no scratch indexing)
+__device__ __forceinline__ int i4get(const lorb::I4& a, int c) {
+  return c == 0 ? a.v[0] : c == 1 ? a.v[1] : c == 2 ? a.v[2] : a.v[3];
+}
+__device__ __forceinline__ lorb::I4 i4one(int c) {  // one-hot (c < 0: zeros)
+  lorb::I4 r;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) r.v[u] = c == u;
+  return r;
+}
+__device__ __forceinline__ void i4add(lorb::I4& a, const lorb::I4& b) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a.v[u] += b.v[u];
+}
+// inclusive scans across the 64 lanes of a wavefront on DPP (no LDS): within rows of 16 by
+// row_shr 1, 2, 4, 8, then row_bcast:15 into rows 1 / 3 and row_bcast:31 into rows 2 / 3 (GFX9 DPP)
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_i(int old, int x) {
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, RM, 0xf, false);
+}
+__device__ __forceinline__ int wave_iadd(int x) {
+  x += dpp_i<0x111, 0xf>(0, x);
+  x += dpp_i<0x112, 0xf>(0, x);
+  x += dpp_i<0x114, 0xf>(0, x);
+  x += dpp_i<0x118, 0xf>(0, x);
+  x += dpp_i<0x142, 0xa>(0, x);
+  x += dpp_i<0x143, 0xc>(0, x);
+  return x;
+}
+__device__ __forceinline__ int wave_imax(int x, int /*lane*/) {
+  constexpr int lo = (int)0x80000000;
+  x = max(x, dpp_i<0x111, 0xf>(lo, x));
+  x = max(x, dpp_i<0x112, 0xf>(lo, x));
+  x = max(x, dpp_i<0x114, 0xf>(lo, x));
+  x = max(x, dpp_i<0x118, 0xf>(lo, x));
+  x = max(x, dpp_i<0x142, 0xa>(lo, x));
+  x = max(x, dpp_i<0x143, 0xc>(lo, x));
+  return x;
+}
+__device__ __forceinline__ int wave_prev(int x, int old) { return dpp_i<0x138, 0xf>(old, x); }  // wave_shr:1
+__device__ __forceinline__ int lane63(int x) { return __builtin_amdgcn_readlane(x, 63); }
+
+// Per-wave sweep state shared across the workgroup's 16 waves (exclusive carries between waves).
+struct OctWaves {
+  int last[kOctThreads / 64];        // last segment head (position << 11 | node) of each wave's chunk
+  lorb::I4 cnt[kOctThreads / 64];    // class (or bucket) counts of each wave's chunk
+};
+// carry into wave wv: the last head before its chunk (or -1); the class counts before its chunk
+__device__ __forceinline__ int oct_wave_last(const OctWaves& ww, int wv) {
+  int c = -1;
+  for (int w = 0; w < wv; ++w) c = max(c, ww.last[w]);
+  return c;
+}
+__device__ __forceinline__ lorb::I4 oct_wave_base(const OctWaves& ww, int wv) {
+  lorb::I4 b = {{0, 0, 0, 0}};
+  for (int w = 0; w < wv; ++w) i4add(b, ww.cnt[w]);
+  return b;
+}
+
+// The LDS path (a level whose node list fits kOctNC nodes and cells kOctCells): the passes of
+// oct_global with the node list and every per-node array in LDS and the keys kept in position
+// order (key index, x | y << 16), each wave sweeping a contiguous chunk of positions 64 at a time
+// (coalesced loads and stores; segment owners and class ranks by wave scans with carries between
+// chunks and waves).  Segment heads are pass-stamped (hd[p] = (pass + 1) << 16 | node): no
+// clearing pass.  The keys are gathered from the cells one thread per key.
+__device__ __forceinline__ void oct_lds(const OctArgs& A, OctSh& sh, OctLds& S, OctWaves& ww, long long* s_key) {
+  // lorb_orb_debug_octree only: cycle stamps of the phases in the trace's spare words
+  const unsigned long long oct_t0 = __builtin_amdgcn_s_memtime();
+  int oct_ns = 0;
+#define OCT_STAMP() do { if (A.trace && threadIdx.x == 0 && oct_ns < 60) \
+    A.trace[A.n_levels * 64 * 72 + blockIdx.x * 16384 + oct_ns++] = (int)(__builtin_amdgcn_s_memtime() - oct_t0); } while (0)
+  int* wsum = sh.wsum;
+  const int l = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const OctLevel V = A.lv[l];
+  float* kx = A.kx + V.key_base;
+  float* ky = A.ky + V.key_base;
+  float* kr = A.kr + V.key_base;
+  int* hd = A.hd + V.key_base;
+  // position-ordered keys (double-buffered): key index, and x | y << 16 (FAST keys sit on integer
+  // pixel coordinates, k_orb_fast, below 2^16); per position the pass's owner | class | head word
+  // and class prefix
+  int* pk0 = A.perm + V.key_base;
+  int* pk1 = A.perm2 + V.key_base;
+  int* pxy0 = A.cls + V.key_base;
+  int* pxy1 = A.own + V.key_base;
+  int* meta = reinterpret_cast<int*>(A.ex + V.key_base + l);  // (key_cap + 1) I4 >= 2 key_cap ints
+  int* rk = meta + V.key_cap;
+  const int ncell = V.cell_end - V.cell_begin;
+
+  // 1. vToDistributeKeys (:827-872): cell offsets, then one thread per key
+  int* coff = reinterpret_cast<int*>(S.nb);
+  int* cob = coff + kOctCells + 1;
+  int n = 0;
+  for (int base = 0; base < ncell; base += kOctThreads) {
+    const int c = base + t;
+    const int v = c < ncell ? A.cell_cnt[V.cell_begin + c] : 0;
+    const int ob = c < ncell ? A.cells[V.cell_begin + c].out_base : 0;
+    int tot;
+    const int e0 = lorb::block_excl_scan<kOctThreads>(v, wsum, &tot);
+    if (c < ncell) { coff[c] = n + e0; cob[c] = ob; }
+    n += tot;
+  }
+  if (t == 0) coff[ncell] = n;
+  __syncthreads();
+  if (n > V.key_cap) { if (t == 0) A.out_cnt[l] = -1; return; }
+  if (n == 0) { if (t == 0) A.out_cnt[l] = 0; return; }
+  for (int k0 = t; k0 < n; k0 += 4 * kOctThreads) {  // four keys per thread in flight
+    int src[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * kOctThreads;
+      int lo = 0, hi = ncell - 1;  // the last cell whose offset is <= k (a non-empty one)
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (coff[mid] <= k) lo = mid; else hi = mid - 1;
+      }
+      src[u] = k < n ? cob[lo] + (k - coff[lo]) : 0;
+    }
+    float fx[4], fy[4], fr[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { fx[u] = A.fx[src[u]]; fy[u] = A.fy[src[u]]; fr[u] = A.fr[src[u]]; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + u * kOctThreads;
+      if (k < n) { kx[k] = fx[u]; ky[k] = fy[u]; kr[k] = fr[u]; }
+    }
+  }
+  __syncthreads();  // the keys written above are read by other threads below
+  OCT_STAMP();
+  // wave wv sweeps positions [c0, c1), 64 per step
+  const int chunk = (n + kOctThreads - 1) / kOctThreads * 64;
+  const int c0 = min(n, wv * chunk), c1 = min(n, c0 + chunk);
+
+  // 2. initial nodes (:575-609): keys bucketed by x / hX, stable; empty nodes erased
+  {
+    lorb::I4 cnt = {{0, 0, 0, 0}};
+    for (int p0 = c0 + lane; p0 < c1; p0 += 64 * kQB) {
+      float xv[kQB];
+#pragma unroll
+      for (int q = 0; q < kQB; ++q) xv[q] = p0 + 64 * q < c1 ? kx[p0 + 64 * q] : 0.f;
+#pragma unroll
+      for (int q = 0; q < kQB; ++q) {
+        const int p = p0 + 64 * q;
+        if (p < c1) {
+          i4add(cnt, i4one(min((int)(xv[q] / V.hx), V.n_ini - 1)));
+          hd[p] = 0;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cnt.v[u] = __reduce_add_sync(~0ull, cnt.v[u]);
+    if (lane == 0) ww.cnt[wv] = cnt;
+    __syncthreads();
+    lorb::I4 tot = {{0, 0, 0, 0}}, run = oct_wave_base(ww, wv);
+    for (int w = 0; w < kOctThreads / 64; ++w) i4add(tot, ww.cnt[w]);
+    const int start[4] = {0, tot.v[0], tot.v[0] + tot.v[1], tot.v[0] + tot.v[1] + tot.v[2]};
+    for (int pb0 = c0; pb0 < c1; pb0 += 64 * kQB) {
+    float xv[kQB], yv[kQB];
+#pragma unroll
+    for (int q = 0; q < kQB; ++q) {
+      const int p = pb0 + 64 * q + lane;
+      xv[q] = p < c1 ? kx[p] : 0.f;
+      yv[q] = p < c1 ? ky[p] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < kQB; ++q) {
+      const int p = pb0 + 64 * q + lane;
+      const float x = xv[q], y = yv[q];
+      const int b = p < c1 ? min((int)(x / V.hx), V.n_ini - 1) : -1;
+      // the four bucket counters packed 8 bits each (a step counts at most 64)
+      const int inc = wave_iadd(b >= 0 ? 1 << (8 * b) : 0);
+      if (p < c1) {
+        const int pos = (b == 0 ? 0 : b == 1 ? start[1] : b == 2 ? start[2] : start[3]) + i4get(run, b) +
+                        ((inc >> (8 * b)) & 0xff) - 1;
+        pk0[pos] = p; pxy0[pos] = (int)x | ((int)y << 16);
+      }
+      const int wt = lane63(inc);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) run.v[u] += (wt >> (8 * u)) & 0xff;
+    }
+    }
+    if (t == 0) {
+      int L = 0, beg = 0;
+      for (int b = 0; b < V.n_ini; b++) {
+        const int k = tot.v[b];
+        if (k > 0) {
+          OctNode nd;
+          nd.x0 = (int)(V.hx * (float)b); nd.x1 = (int)(V.hx * (float)(b + 1)); nd.y0 = 0; nd.y1 = V.ht;
+          nd.beg = beg; nd.end = beg + k; nd.cre = b; nd.pend = 0;
+          S.na[L++] = nd;
+        }
+        beg += k;
+      }
+      sh.L = L; sh.mode = 0; sh.state = 0;
+    }
+    __syncthreads();
+  }
+  OCT_STAMP();
+
+  // the owner sweep shared by the passes and the final step: ww.last = each wave's last head
+  auto wave_last_head = [&](int stamp) {
+    int last = -1;
+    for (int p0 = c0 + lane; p0 < c1; p0 += 64 * kQB) {
+      int hv[kQB];
+#pragma unroll
+      for (int q = 0; q < kQB; ++q) hv[q] = p0 + 64 * q < c1 ? hd[p0 + 64 * q] : 0;
+#pragma unroll
+      for (int q = 0; q < kQB; ++q)
+        if (p0 + 64 * q < c1 && (hv[q] >> 16) == stamp) last = max(last, ((p0 + 64 * q) << 11) | (hv[q] & 0x7ff));
+    }
+    last = __reduce_max_sync(~0ull, last);
+    if (lane == 0) ww.last[wv] = last;
+  };
+
+  // 3. division passes (:619-772)
+  OctNode* cur = S.na;
+  OctNode* nxt = S.nb;
+  for (int pass = 0;; pass++) {
+    const int L = sh.L, mode = sh.mode;
+    if (sh.state != 0) break;
+    if (pass >= kOctMaxPasses) { if (t == 0) A.out_cnt[l] = -1; return; }
+    const int stamp = pass + 1;
+    // A. dividing candidates (split points); segment heads (stamped)
+    for (int i = t; i < L; i += kOctThreads) {
+      const OctNode nd = cur[i];
+      const int a = mode == 0 ? (nd.end - nd.beg >= 2) : nd.pend;
+      S.act[i] = a;
+      S.mid[i] = a ? make_int2(nd.x0 + (int)ceilf((float)(nd.x1 - nd.x0) / 2), nd.y0 + (int)ceilf((float)(nd.y1 - nd.y0) / 2))
+                   : make_int2(-1, 0);
+      hd[nd.beg] = (stamp << 16) | i;
+    }
+    __syncthreads();
+    // B. owners (segment heads + a max-scan), classes (DivideNode's quadrant, :527-541), class counts
+    wave_last_head(stamp);
+    __syncthreads();
+    {
+      int own = oct_wave_last(ww, wv);  // (position << 11 | node) of the head owning the next position
+      lorb::I4 cnt = {{0, 0, 0, 0}};
+      for (int pb0 = c0; pb0 < c1; pb0 += 64 * kQB) {
+      int hv[kQB], xyv[kQB];
+#pragma unroll
+      for (int q = 0; q < kQB; ++q) {
+        const int p = pb0 + 64 * q + lane;
+        hv[q] = p < c1 ? hd[p] : 0;
+        xyv[q] = p < c1 ? pxy0[p] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < kQB; ++q) {
+        const int p = pb0 + 64 * q + lane;
+        const bool in = p < c1;
+        const int h = hv[q], xy = xyv[q];
+        const bool head = in && (h >> 16) == stamp;
+        const int sc = wave_imax(head ? (p << 11) | (h & 0x7ff) : -1, lane);
+        const int o = max(own, sc) & 0x7ff;
+        int c = -1;
+        if (in) {
+          const int2 md = S.mid[o];  // oct_class on integer coordinates (exact)
+          if (md.x >= 0) c = ((xy & 0xffff) < md.x ? 0 : 1) + ((xy >> 16) < md.y ? 0 : 2);
+          meta[p] = o | ((c + 1) << 11) | ((int)head << 14);
+        }
+        i4add(cnt, i4one(c));
+        own = max(own, lane63(sc));
+      }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cnt.v[u] = __reduce_add_sync(~0ull, cnt.v[u]);
+      if (lane == 0) ww.cnt[wv] = cnt;
+    }
+    __syncthreads();
+    // B'. class prefix per position (for the placement) and per node at its segment start (exb)
+    //     and end (cnt, turned into counts in C)
+    {
+      lorb::I4 run = oct_wave_base(ww, wv);
+      int prev = oct_wave_last(ww, wv);  // owner of the position before this wave's chunk
+      prev = prev >= 0 ? (prev & 0x7ff) : -1;
+      for (int pb0 = c0; pb0 < c1; pb0 += 64 * kQB) {
+      int mv[kQB];
+#pragma unroll
+      for (int q = 0; q < kQB; ++q) mv[q] = pb0 + 64 * q + lane < c1 ? meta[pb0 + 64 * q + lane] : 0;
+#pragma unroll
+      for (int q = 0; q < kQB; ++q) {
+        const int p = pb0 + 64 * q + lane;
+        const bool in = p < c1;
+        const int m = mv[q];
+        const int o = m & 0x7ff, c = in ? ((m >> 11) & 7) - 1 : -1;
+        const int inc = wave_iadd(c >= 0 ? 1 << (8 * c) : 0);  // class counters packed 8 bits each
+        lorb::I4 pre = run;  // exclusive prefix at p
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pre.v[u] += ((inc >> (8 * u)) & 0xff) - (c == u);
+        const int po = wave_prev(o, prev);  // owner of p - 1 (lane 0: the carried owner)
+        if (in) {
+          if ((m >> 14) & 1) {
+            S.exb[o] = pre;
+            if (po >= 0) S.cnt[po] = pre;  // the previous segment ends here
+          }
+          if (c >= 0) rk[p] = i4get(pre, c);
+          if (p == n - 1) {  // the last segment ends at n
+            lorb::I4 e = pre;
+            i4add(e, i4one(c));
+            S.cnt[o] = e;
+          }
+        }
+        prev = lane63(o);
+        const int wt = lane63(inc);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) run.v[u] += (wt >> (8 * u)) & 0xff;
+      }
+      }
+    }
+    __syncthreads();
+    OCT_STAMP();
+    // C. children per dividing node; processing order
+    for (int i = t; i < L; i += kOctThreads) {
+      if (!S.act[i]) { S.ech[i] = 0; continue; }
+      const lorb::I4 a = S.exb[i], b = S.cnt[i];
+      lorb::I4 k;
+      int e = 0;
+      for (int q = 0; q < 4; q++) { k.v[q] = b.v[q] - a.v[q]; e += k.v[q] > 0; }
+      S.cnt[i] = k;
+      S.ech[i] = e;
+    }
+    if (mode == 0) {
+      for (int i = t; i < L; i += kOctThreads) S.tmp[i] = S.act[i];
+      __syncthreads();
+      oct_scan(S.tmp, L, wsum);
+      for (int i = t; i < L; i += kOctThreads) S.rank[i] = S.tmp[i];
+    } else {  // descending (size, creation): sort(vPrev...) then j from the back (:717-718)
+      for (int i = t; i < L; i += kOctThreads) S.rank[i] = 0;
+      for (int q0 = 0; q0 < L; q0 += kOctKeyChunk) {
+        const int cn = min(kOctKeyChunk, L - q0);
+        __syncthreads();
+        for (int j = t; j < cn; j += kOctThreads) {
+          const OctNode nd = cur[q0 + j];
+          s_key[j] = S.act[q0 + j] ? ((long long)(nd.end - nd.beg) << 32) | (unsigned)nd.cre : -1ll;
+        }
+        __syncthreads();
+        for (int i = t; i < L; i += kOctThreads) {
+          if (!S.act[i]) continue;
+          const long long ki = ((long long)(cur[i].end - cur[i].beg) << 32) | (unsigned)cur[i].cre;
+          int r = 0;
+          for (int j = 0; j < cn; j++) r += s_key[j] > ki;
+          S.rank[i] += r;
+        }
+      }
+    }
+    __syncthreads();
+    // D. children counts in processing order; the focused loop's break (:763-764)
+    for (int i = t; i < L; i += kOctThreads) if (S.act[i]) S.tmp[S.rank[i]] = S.ech[i];
+    __syncthreads();
+    int n_act = 0;
+    {
+      int s2 = 0;
+      for (int i = t; i < L; i += kOctThreads) s2 += S.act[i];
+      int tt;
+      (void)lorb::block_excl_scan<kOctThreads>(s2, wsum, &tt);
+      n_act = tt;
+    }
+    for (int r = t; r < n_act; r += kOctThreads) S.surv[r] = S.tmp[r];
+    __syncthreads();
+    (void)oct_scan(S.surv, n_act, wsum);  // surv[r] = exclusive prefix in processing order
+    if (t == 0) sh.cm = n_act;
+    __syncthreads();
+    if (mode == 1) {
+      for (int r = t; r < n_act; r += kOctThreads) {
+        const int live = L + (S.surv[r] + S.tmp[r]) - (r + 1);  // after processing r
+        if (live >= V.N) atomicMin(&sh.cm, r + 1);
+      }
+    }
+    __syncthreads();
+    if (t == 0) sh.E = sh.cm > 0 ? S.surv[sh.cm - 1] + S.tmp[sh.cm - 1] : 0;
+    __syncthreads();
+    const int cm = sh.cm, E = sh.E;
+    // E. survivors (not divided this pass) keep their order after the new children
+    for (int i = t; i < L; i += kOctThreads) {
+      const bool div = S.act[i] && S.rank[i] < cm;
+      S.act[i] = div;
+      S.tmp[i] = div ? 0 : 1;
+    }
+    __syncthreads();
+    const int n_surv = oct_scan(S.tmp, L, wsum);  // tmp[i] = survivor rank
+    const int newL = E + n_surv;
+    OCT_STAMP();
+    if (newL > V.node_cap || newL > kOctNC) { if (t == 0) A.out_cnt[l] = -1; return; }
+    // F. the keys in their new positions (stable partition of the divided segments), the new list
+    for (int p0 = c0 + lane; p0 < c1; p0 += 64 * kQB) {
+      int mv[kQB], rv[kQB], kv[kQB], xv[kQB];
+#pragma unroll
+      for (int q = 0; q < kQB; ++q) {
+        const int p = p0 + 64 * q;
+        const bool in = p < c1;
+        mv[q] = in ? meta[p] : 0;
+        rv[q] = in ? rk[p] : 0;
+        kv[q] = in ? pk0[p] : 0;
+        xv[q] = in ? pxy0[p] : 0;
+      }
+#pragma unroll
+      for (int q = 0; q < kQB; ++q) {
+        const int p = p0 + 64 * q;
+        if (p < c1) {
+          const int m = mv[q], o = m & 0x7ff, c = ((m >> 11) & 7) - 1;
+          int dst = p;
+          if (S.act[o]) {
+            const lorb::I4 k = S.cnt[o];
+            const int off = (c > 0 ? k.v[0] : 0) + (c > 1 ? k.v[1] : 0) + (c > 2 ? k.v[2] : 0);
+            dst = cur[o].beg + off + (rv[q] - i4get(S.exb[o], c));
+          }
+          pk1[dst] = kv[q]; pxy1[dst] = xv[q];
+        }
+      }
+    }
+    int n_pend = 0;
+    for (int i = t; i < L; i += kOctThreads) {
+      const OctNode nd = cur[i];
+      if (!S.act[i]) {
+        OctNode s2 = nd;
+        s2.pend = 0;
+        nxt[E + S.tmp[i]] = s2;
+        continue;
+      }
+      const int r = S.rank[i];
+      const int incl = S.surv[r] + S.ech[i];
+      int slot = E - incl;  // children of the last processed parent come first
+      const lorb::I4 k = S.cnt[i];
+      int beg = nd.beg + k.v[0] + k.v[1] + k.v[2] + k.v[3];
+      for (int c = 3; c >= 0; c--) {  // push_front n1, n2, n3, n4 -> the list reads n4 n3 n2 n1
+        const int kc = k.v[c];
+        beg -= kc;
+        if (kc == 0) continue;
+        nxt[slot++] = oct_child(nd, c, beg, kc, 4 * r + c);
+        n_pend += kc > 1;
+      }
+    }
+    {
+      int tt;
+      (void)lorb::block_excl_scan<kOctThreads>(n_pend, wsum, &tt);
+      n_pend = tt;
+    }
+    __syncthreads();
+    // G. termination (:703-707, :767-768)
+    if (t == 0) {
+      if (A.trace && pass < 64) {
+        int* tr = A.trace + (l * 64 + pass) * 72;
+        tr[0] = L; tr[1] = mode; tr[2] = n_act; tr[3] = cm; tr[4] = E; tr[5] = n_surv; tr[6] = newL; tr[7] = n_pend;
+        for (int q = 0; q < 16 && q < newL; q++) {
+          tr[8 + 4 * q] = nxt[q].beg; tr[9 + 4 * q] = nxt[q].end; tr[10 + 4 * q] = nxt[q].x0; tr[11 + 4 * q] = nxt[q].y0;
+        }
+      }
+      int state = 0, m = mode;
+      if (newL >= V.N || newL == L) state = 1;
+      else if (mode == 0 && newL + 3 * n_pend > V.N) m = 1;
+      sh.state = state; sh.mode = m; sh.L = newL;
+    }
+    {
+      OctNode* nw = cur; cur = nxt; nxt = nw;
+      int* w1 = pk0; pk0 = pk1; pk1 = w1;
+      int* w2 = pxy0; pxy0 = pxy1; pxy1 = w2;
+    }
+    __syncthreads();
+    OCT_STAMP();
+  }
+  // 4. the strongest key of each node (:776-794: strict >, so the first of the strongest in vKeys
+  //    order): the final segment heads stamped once more, every key's owner as in a pass, and a
+  //    per-node LDS max of (response as an ordered int) << 32 | ~position
+  const int L = sh.L;
+  {
+    const int sf = kOctMaxPasses + 1;  // above every pass stamp
+    for (int i = t; i < L; i += kOctThreads) {
+      hd[cur[i].beg] = (sf << 16) | i;
+      s_key[i] = 0;
+    }
+    __syncthreads();
+    wave_last_head(sf);
+    __syncthreads();
+    int own = oct_wave_last(ww, wv);
+    for (int pb0 = c0; pb0 < c1; pb0 += 64 * kQB) {
+    int hv[kQB];
+    float rv[kQB];
+#pragma unroll
+    for (int q = 0; q < kQB; ++q) {
+      const int p = pb0 + 64 * q + lane;
+      hv[q] = p < c1 ? hd[p] : 0;
+      rv[q] = p < c1 ? kr[pk0[p]] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < kQB; ++q) {
+      const int p = pb0 + 64 * q + lane;
+      const bool in = p < c1;
+      const int h = hv[q];
+      const bool head = in && (h >> 16) == sf;
+      const int sc = wave_imax(head ? (p << 11) | (h & 0x7ff) : -1, lane);
+      const int o = max(own, sc) & 0x7ff;
+      if (in) {
+        const unsigned b = __float_as_uint(rv[q]);
+        const unsigned ord = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+        atomicMax(reinterpret_cast<unsigned long long*>(&s_key[o]),
+                  ((unsigned long long)ord << 32) | (unsigned)(0xffffffffu - (unsigned)p));
+      }
+      own = max(own, lane63(sc));
+    }
+    }
+    __syncthreads();
+    for (int i = t; i < L; i += kOctThreads) {
+      const unsigned pos = 0xffffffffu - (unsigned)(s_key[i] & 0xffffffffull);
+      A.out_key[V.node_base + i] = pk0[pos];
+    }
+  }
+  OCT_STAMP();
+#undef OCT_STAMP
+  if (t == 0) A.out_cnt[l] = L;
+}
+
+__global__ __launch_bounds__(kOctThreads) void k_orb_octree(OctArgs A) {
+  __shared__ OctSh sh;
+  __shared__ long long s_key[kOctKeyChunk];
+  __shared__ OctLds S;
+  __shared__ OctWaves ww;
+  const OctLevel& V = A.lv[blockIdx.x];
+  // the LDS path when the level's node list and cells fit
+  if (V.node_cap <= kOctNC && V.cell_end - V.cell_begin <= kOctCells)
+    oct_lds(A, sh, S, ww, s_key);
+  else
+    oct_global(A, sh, s_key);
 }
 
 // Gathers the per-level results in level order: level coordinates, octave, size, response and the
