@@ -97,6 +97,21 @@ __device__ __forceinline__ double wave_max(double v) {
   v = fmax(v, dpp_d<0xB1>(v));
   return v;
 }
+__device__ __forceinline__ int wave_isum(int v) {
+  {
+    const auto p = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    v = (int)(p[0] + p[1]);  // v_i + v_(i^32), whichever copy holds which
+  }
+  {
+    const auto p = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    v = (int)(p[0] + p[1]);
+  }
+  v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+  return v;
+}
 template <int N>
 __device__ __forceinline__ void block_sum(double (&v)[N], double* sh /* [N*256] */) {
   // deterministic fixed tree over a 256-thread block
@@ -2517,7 +2532,7 @@ struct lorb_ba_devbuild {
   int* cov = nullptr;         // C * C
   int* cam_cnt = nullptr;     // C
   unsigned long long* bits = nullptr;
-  int* hist = nullptr; int* hoff = nullptr; int hist_cap = 0;  // camera-major block histograms
+  int* hist = nullptr; int hist_cap = 0;  // camera-major block histograms
   int* cam_pt = nullptr;      // K_cap: point of each camera-major slot
   int* perm = nullptr;        // C: input camera -> plan camera
   int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0;
@@ -3408,13 +3423,37 @@ struct DbFused {
   unsigned long long* bits;
   int* hdr;
 };
-__device__ __forceinline__ int first_in_group(const int* __restrict__ pt_off, int P, long long bound) {
-  int lo = 0, hi = P;  // smallest p with pt_off[p] + p >= bound (P if none)
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if ((long long)pt_off[mid] + mid >= bound) hi = mid; else lo = mid + 1;
+// Point groups: group g = points [start(g), start(g + 1)), start(g) = the smallest p with
+// off[p] + p >= g S (P if none), found by one wavefront, 32-ary: each half-wave probes 32 points spread over its
+// range per step (one memory round trip) and keeps the gap where the predicate turns true, so a
+// 10 k-point window takes 3 round trips instead of 14 dependent loads.  Lanes 0-31 find the start
+// of bound b0, lanes 32-63 that of b1.
+__device__ __forceinline__ void group_bounds(const int* __restrict__ off, int P, long long b0, long long b1, int lane,
+                                             int& s0, int& s1) {
+  const int half = lane >> 5, j = lane & 31;
+  const long long bound = half ? b1 : b0;
+  int lo = 0, hi = P;  // the answer is in [lo, hi] (hi = P: none below P)
+  while (__ballot(hi > lo)) {
+    const int n = hi - lo;
+    bool pr = false;
+    if (n > 0) {
+      const int q = lo + (int)(((long long)n * (j + 1)) / 33);  // < hi
+      pr = (long long)off[q] + q >= bound;
+    }
+    const unsigned long long bal = __ballot(pr);
+    const unsigned msk = half ? (unsigned)(bal >> 32) : (unsigned)bal;
+    if (n > 0) {
+      if (msk) {
+        const int f = __builtin_ctz(msk);
+        hi = lo + (int)(((long long)n * (f + 1)) / 33);
+        if (f > 0) lo = lo + (int)(((long long)n * f) / 33) + 1;
+      } else {
+        lo = lo + (int)(((long long)n * 32) / 33) + 1;
+      }
+    }
   }
-  return lo;
+  s0 = __shfl(lo, 0, 64);
+  s1 = __shfl(lo, 32, 64);
 }
 __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d, int K, int C, int NB,
                                                    const int* __restrict__ key, const int* __restrict__ val,
@@ -3434,12 +3473,14 @@ __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d
       if (i < 3 * f.P) d.x_init_pt[i] = (double)w.d_point_init[i];
     }
   }
-  for (int g = gt; g < f.G; g += gs) {  // point groups
-    const int s0 = first_in_group(d.pt_obs_off, f.P, (long long)g * f.S);
-    const int s1 = first_in_group(d.pt_obs_off, f.P, (long long)(g + 1) * f.S);
-    PBlk b;
-    b.win = 0; b.p0 = s0; b.cnt = s1 - s0; b.o0 = d.pt_obs_off[s0]; b.no = d.pt_obs_off[s1] - d.pt_obs_off[s0];
-    const_cast<PBlk*>(d.pblk)[g] = b;
+  for (int g = gt >> 6; g < f.G; g += gs >> 6) {  // point groups, one wavefront each
+    int s0, s1;
+    group_bounds(d.pt_obs_off, f.P, (long long)g * f.S, (long long)(g + 1) * f.S, threadIdx.x & 63, s0, s1);
+    if ((threadIdx.x & 63) == 0) {
+      PBlk b;
+      b.win = 0; b.p0 = s0; b.cnt = s1 - s0; b.o0 = d.pt_obs_off[s0]; b.no = d.pt_obs_off[s1] - d.pt_obs_off[s0];
+      const_cast<PBlk*>(d.pblk)[g] = b;
+    }
   }
   for (int i = gt; i < f.env_n; i += gs) d.env_part[i] = 0.0;
   for (int i = gt; i < f.bits_n; i += gs) f.bits[i] = 0ull;
@@ -3462,46 +3503,73 @@ __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d
   for (int i = threadIdx.x; i < C; i += 256) hist[(size_t)i * NB + blockIdx.x] = s_h[i];
 }
 
-// counting sort of the optimised observations by plan camera, stable: slot = camera-major block
-// offset + rank among the block's earlier observations of the same camera.  Writes the camera-major
-// list, its point ids and each observation's camera slot.
-__global__ __launch_bounds__(256) void k_db_place(BaDev d, int K, int NB, const int* __restrict__ hoff,
+// counting sort of the optimised observations by plan camera, stable: slot = camera offset (the
+// uploaded cam_obs_off: observations of the plan cameras before c) + this camera's observations in
+// the earlier blocks (a column prefix of the camera-major histogram, summed here by one wavefront
+// per camera present in the block -- no separate scan launch) + rank among the block's earlier
+// observations of the same camera.  Writes the camera-major list, its point ids and each
+// observation's camera slot.
+__global__ __launch_bounds__(256) void k_db_place(BaDev d, int K, int NB, int C, const int* __restrict__ hist,
                                                   int* __restrict__ cam_pt) {
+  extern __shared__ int s_off[];  // C: this block's first slot per camera (-1: camera absent)
   __shared__ int s_c[256];
-  const int e = blockIdx.x * 256 + threadIdx.x, t = threadIdx.x;
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int e = b * 256 + t;
+  for (int i = t; i < C; i += 256) s_off[i] = -1;
+  __syncthreads();
   const int c = e < K ? d.obs_cam[e] : -1;
   s_c[t] = c;
+  if (c >= 0) s_off[c] = 0;
+  __syncthreads();
+  for (int cc = wv; cc < C; cc += 4) {
+    if (s_off[cc] < 0) continue;  // uniform per wavefront
+    const int* h = hist + (size_t)cc * NB;
+    int v = 0;
+    for (int i = lane; i < b; i += 64) v += h[i];
+    v = wave_isum(v);
+    if (lane == 0) s_off[cc] = d.cam_obs_off[cc] + v;
+  }
   __syncthreads();
   if (c < 0) return;
   int rank = 0;
   for (int u = 0; u < t; ++u) rank += s_c[u] == c;
-  const int j = hoff[(size_t)c * NB + blockIdx.x] + rank;
+  const int j = s_off[c] + rank;
   const_cast<int*>(d.cam_obs)[j] = e;
   const_cast<int*>(d.obs_cm)[e] = j;
   cam_pt[j] = d.obs_pt[e];
 }
 
-
-
 // one workgroup per (camera, camera) block: its pair list in point order.  A diagonal block's pairs
 // are (e, e) over the camera's slots.  Otherwise the lower camera's point ids (ascending) are staged
 // in LDS for the binary searches when they fit; each thread owns a run of up to kPR consecutive
 // slots of the higher camera, loads their point ids together (one memory round trip per batch, not
-// one per 256 slots), searches them and places its matches after one block scan of the run counts.
+// one per 256 slots; the first batch's go out with the staging loads), searches them and places its
+// matches after one block scan of the run counts.  The camera offsets come in whole (C + 1 ints,
+// issued with the block pair) so the slot ranges cost no dependent load.
 constexpr int kPairsLds = 8192, kPR = 8;
-__global__ __launch_bounds__(256) void k_db_pairs(BaDev d, const int* __restrict__ cam_pt) {
+__global__ __launch_bounds__(256) void k_db_pairs(BaDev d, int C, const int* __restrict__ cam_pt) {
   __shared__ int wsum[4];
   __shared__ int s_pt[kPairsLds];
+  extern __shared__ int s_co[];  // C + 1 camera offsets
   const BlockPair B = d.bp[blockIdx.x];
-  const int h0 = d.cam_obs_off[B.ch], h1 = d.cam_obs_off[B.ch + 1];
-  const int l0 = d.cam_obs_off[B.cl], l1 = d.cam_obs_off[B.cl + 1];
-  const int nl = l1 - l0, t = threadIdx.x;
+  const int t = threadIdx.x;
+  for (int i = t; i <= C; i += 256) s_co[i] = d.cam_obs_off[i];
+  __syncthreads();
+  const int h0 = s_co[B.ch], h1 = s_co[B.ch + 1];
+  const int l0 = s_co[B.cl], l1 = s_co[B.cl + 1];
+  const int nl = l1 - l0;
   int2* out = const_cast<int2*>(d.pairs) + B.off;
   if (B.ch == B.cl) {
     for (int i = h0 + t; i < h1 && i - h0 < B.cnt; i += 256) out[i - h0] = make_int2(i, i);
     return;
   }
   const bool lds = nl <= kPairsLds;
+  int p[kPR], jv[kPR];
+  {  // the first batch's point ids, issued before the staging waits
+    const int nb = min(h1 - h0, 256 * kPR), r0 = h0 + t * kPR;
+#pragma unroll
+    for (int u = 0; u < kPR; ++u) p[u] = r0 + u < h0 + nb ? cam_pt[r0 + u] : -1;
+  }
   if (lds) {
     for (int i = t; i < nl; i += 256) s_pt[i] = cam_pt[l0 + i];
     __syncthreads();
@@ -3510,9 +3578,10 @@ __global__ __launch_bounds__(256) void k_db_pairs(BaDev d, const int* __restrict
   int run = 0;
   for (int base = h0; base < h1; base += 256 * kPR) {
     const int nb = min(h1 - base, 256 * kPR), r0 = base + t * kPR;
-    int p[kPR], jv[kPR];
+    if (base != h0) {
 #pragma unroll
-    for (int u = 0; u < kPR; ++u) p[u] = r0 + u < base + nb ? cam_pt[r0 + u] : -1;
+      for (int u = 0; u < kPR; ++u) p[u] = r0 + u < base + nb ? cam_pt[r0 + u] : -1;
+    }
     int c = 0;
 #pragma unroll
     for (int u = 0; u < kPR; ++u) {
@@ -3585,6 +3654,13 @@ __global__ __launch_bounds__(256) void k_db_result64(BaDev d, int C, int P, cons
 namespace lorb {
 void ba_plan_sorted_hint(lorb_ba_plan* P, bool sorted) {
   if (P && P->devb) P->devb->sorted_hint = sorted;
+}
+
+const int* ba_plan_point_offsets(const lorb_ba_plan* P) { return P && P->devb ? P->dev.pt_obs_off : nullptr; }
+
+void ba_plan_window_counts(const lorb_ba_plan* P, int* n_points, int* n_obs) {
+  *n_points = P->Ptot;  // the live counts the last device build read back (its header)
+  *n_obs = P->K;
 }
 
 int ba_plan_result_ring_dev(lorb_ba_plan* P, float* ring, int R, int t0, float* d_point_out) {
@@ -3914,8 +3990,6 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   const int NB = lorb::ceil_div(K, 256);
   if ((size_t)std::max(NB, 1) * C > (size_t)b.hist_cap) {
     LORB_TRY(grow(P, &b.hist, &b.hist_cap, (size_t)std::max(NB, 1) * C));
-    int cap2 = 0;
-    LORB_TRY(grow(P, &b.hoff, &cap2, (size_t)b.hist_cap));
   }
   {
     // this rank's band starts from zeros (blocks it has no pairs of stay zero; sharded: the
@@ -3925,11 +3999,9 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
                        b.val_out, b.perm, b.hist, f);
     b.dirty = false;
   }
-  if (K > 0) {
-    hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.hist, b.hoff, NB * C, nullptr, nullptr);
-    hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), 0, s, d, K, NB, b.hoff, b.cam_pt);
-  }
-  if (!bps.empty()) hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), 0, s, d, b.cam_pt);
+  if (K > 0) hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), sizeof(int) * std::max(C, 1), s, d, K, NB, C, b.hist, b.cam_pt);
+  if (!bps.empty())
+    hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), sizeof(int) * (C + 1), s, d, C, b.cam_pt);
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
 }

@@ -68,7 +68,9 @@ __device__ __forceinline__ uint32_t hamming256(const uint4& a0, const uint4& a1,
 
 // QPL = lane-side descriptors per thread (1, 2 or 4; LORB_BF_QPL): a block covers 256*QPL lane items; every
 // uniform descriptor loaded into SGPRs feeds QPL distance chains.
-template <bool TOP2, int QPL>
+// ATOM (top-1 only): the chunk's key is combined into k1_out[lane item] by atomicMin (one key per
+// lane item for all chunks, no partial array and no serial merge over chunks)
+template <bool TOP2, int QPL, bool ATOM = false>
 __device__ __forceinline__ void scan_tile(const uint4* __restrict__ lane_desc, const uint4* __restrict__ uni_desc,
                                           const BfTile& tl, uint32_t* __restrict__ k1_out,
                                           uint32_t* __restrict__ k2_out) {
@@ -127,8 +129,12 @@ __device__ __forceinline__ void scan_tile(const uint4* __restrict__ lane_desc, c
   for (int r = 0; r < QPL; ++r) {
     const int l = threadIdx.x + 256 * r;
     if (l < tl.lane_count) {
-      k1_out[tl.out_base + l] = k1[r];
-      if (TOP2) k2_out[tl.out_base + l] = k2[r];
+      if (ATOM) {
+        if (k1[r] < kSentinel) atomicMin(&k1_out[tl.lane_base + l], k1[r]);
+      } else {
+        k1_out[tl.out_base + l] = k1[r];
+        if (TOP2) k2_out[tl.out_base + l] = k2[r];
+      }
     }
   }
 }
@@ -163,18 +169,18 @@ __global__ __launch_bounds__(256) void k_bf_scan1(const uint4* __restrict__ lane
   tl.uni_count = b - a;
   tl.uni_local0 = a;
   tl.out_base = c * g.nl + t;
-  scan_tile<TOP2, QPL>(lane_desc, uni_desc, tl, k1_out, k2_out);
+  scan_tile<TOP2, QPL, !TOP2>(lane_desc, uni_desc, tl, k1_out, k2_out);
 }
 
-// One problem, crossCheck: each train's nearest query (the minimum over the chunks' keys) offered
-// to that query (k_cc_scatter's atomicMin) in the same launch
-__global__ __launch_bounds__(256) void k_cc_merge1(const uint32_t* __restrict__ k1p, int nt, int n_chunks,
+// One problem, crossCheck: each train's nearest query (the scan's atomicMin over the chunks) offered
+// to that query (k_cc_scatter's atomicMin); the train key is reset to all-ones for the next call
+__global__ __launch_bounds__(256) void k_cc_merge1(uint32_t* __restrict__ tkey, int nt,
                                                    unsigned long long* __restrict__ qkey) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nt) return;
-  uint32_t k = kSentinel;
-  for (int c = 0; c < n_chunks; ++c) k = min(k, k1p[(size_t)c * nt + t]);
+  const uint32_t k = tkey[t];
   if (k >= kSentinel) return;
+  tkey[t] = 0xffffffffu;
   const unsigned long long v = ((unsigned long long)(k >> kIdxBits) << 32) | (unsigned)t;
   atomicMin(&qkey[k & kIdxMask], v);
 }
@@ -533,28 +539,40 @@ int lorb::match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8
       const int v = e ? atoi(e) : 2;
       return v == 1 || v == 4 ? v : 2;
     }();
-    const int32_t l_off[2] = {0, nt}, u_off[2] = {0, nq};
-    std::vector<BfTile> tiles;  // (only the chunk count is used)
-    int n_chunks = 1;
-    LORB_TRY(build_tiles(ctx, 1, l_off, u_off, 256 * qpl, tiles, &n_chunks));
-    const int lt = 256 * qpl;
-    BfGrid1 g{nt, nq, n_chunks, lt, (nt + lt - 1) / lt};
-    uint32_t* k1 = nullptr;
-    LORB_TRY(lorb::scratch_t(ctx, S_BF_K1, (size_t)nt * n_chunks, &k1));
+    // Chunks of the query range: the chunks' keys meet in one atomicMin per train, so chunks are
+    // cheap -- aim at ~6 workgroups per CU (latency hiding on the VALU-bound scan), >= 32 queries
+    // per chunk (LORB_BF_NC overrides: diagnostics).
+    const int lt = 256 * qpl, lane_tiles = (nt + lt - 1) / lt;
+    static const int nc_env = [] { const char* e = getenv("LORB_BF_NC"); return e ? atoi(e) : 0; }();
+    int n_chunks = std::max(1, std::min((1536 + lane_tiles - 1) / lane_tiles, nq / 32));
+    if (nc_env > 0) n_chunks = std::min(nc_env, nq);
+    BfGrid1 g{nt, nq, n_chunks, lt, lane_tiles};
+    uint32_t* tkey = nullptr;
+    LORB_TRY(lorb::scratch_t(ctx, S_BF_TKEY, (size_t)nt, &tkey));
+    if (ctx->tkey_buf != (void*)tkey || ctx->tkey_ready < (size_t)nt) {  // a fresh or grown buffer: all-ones once
+      LORB_HIP(ctx, hipMemsetAsync(tkey, 0xff, sizeof(uint32_t) * (ctx->scratch_sz[S_BF_TKEY] / sizeof(uint32_t)),
+                                   ctx->stream));
+      ctx->tkey_ready = ctx->scratch_sz[S_BF_TKEY] / sizeof(uint32_t);
+      ctx->tkey_buf = tkey;
+    }
+    const size_t ready = ctx->tkey_ready;
+    ctx->tkey_ready = 0;  // until the merge has been enqueued (it restores the all-ones)
     const unsigned nb = (unsigned)(g.lane_tiles * n_chunks);
     {
       lorb::KernelTimer kt(ctx, LORB_K_BF_SCAN_TOP1);
       if (qpl == 2)
         hipLaunchKernelGGL((k_bf_scan1<false, 2>), dim3(nb), dim3(256), 0, ctx->stream, reinterpret_cast<const uint4*>(d_t),
-                           reinterpret_cast<const uint4*>(d_q), g, k1, (uint32_t*)nullptr, qkey, nq);
+                           reinterpret_cast<const uint4*>(d_q), g, tkey, (uint32_t*)nullptr, qkey, nq);
       else if (qpl == 4)
         hipLaunchKernelGGL((k_bf_scan1<false, 4>), dim3(nb), dim3(256), 0, ctx->stream, reinterpret_cast<const uint4*>(d_t),
-                           reinterpret_cast<const uint4*>(d_q), g, k1, (uint32_t*)nullptr, qkey, nq);
+                           reinterpret_cast<const uint4*>(d_q), g, tkey, (uint32_t*)nullptr, qkey, nq);
       else
         hipLaunchKernelGGL((k_bf_scan1<false, 1>), dim3(nb), dim3(256), 0, ctx->stream, reinterpret_cast<const uint4*>(d_t),
-                           reinterpret_cast<const uint4*>(d_q), g, k1, (uint32_t*)nullptr, qkey, nq);
+                           reinterpret_cast<const uint4*>(d_q), g, tkey, (uint32_t*)nullptr, qkey, nq);
     }
-    hipLaunchKernelGGL(k_cc_merge1, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, k1, nt, n_chunks, qkey);
+    hipLaunchKernelGGL(k_cc_merge1, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, tkey, nt, qkey);
+    LORB_CHECK_LAUNCH(ctx);
+    ctx->tkey_ready = ready;
   } else if (nq > 0) {
     LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, ctx->stream));
   }

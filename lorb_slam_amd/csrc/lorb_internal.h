@@ -30,6 +30,9 @@ struct lorb_ctx {
   bool ktime = false;
   std::vector<hipEvent_t> kev_pool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> kev[LORB_K_COUNT];
+  // S_BF_TKEY entries known to hold all-ones (0: re-fill before use), for the buffer tkey_buf
+  size_t tkey_ready = 0;
+  void* tkey_buf = nullptr;
   // pinned host staging
   void* pinned = nullptr;
   size_t pinned_sz = 0;
@@ -96,6 +99,10 @@ int ba_plan_result_ring_dev(lorb_ba_plan* P, float* ring, int R, int t0, float* 
 // a device-built plan whose callers keep the observation slots sorted by point (stably, no unused
 // slots) builds without the counting sort; slots found out of order fall back to it (same result)
 void ba_plan_sorted_hint(lorb_ba_plan* P, bool sorted);
+// the window's live point / observation counts as the last lorb_ba_plan_update_dev read them
+void ba_plan_window_counts(const lorb_ba_plan* P, int* n_points, int* n_obs);
+// the last device build's per-point observation offsets (point-sorted slots), device pointer
+const int* ba_plan_point_offsets(const lorb_ba_plan* P);
 
 // crossCheck keys of ONE brute-force problem (lorb_bf_match_dev without its finalisation): per
 // query (dist << 32 | train) or all-ones; *qkey_out is ctx scratch valid until the next matcher call
@@ -337,5 +344,6 @@ enum {
   S_BF_OUT2, S_BF_OUT3, S_BF_OUT4, S_BF_OUT5, S_BF_OFF,
   S_W0 = 14, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7, S_W8, S_W9,
   S_KP = 24,   /* 10 slots: keypoint upload + grid */
-  S_WX = 34    /* 8 slots: windowed-matcher scratch */
+  S_WX = 34,   /* 8 slots: windowed-matcher scratch */
+  S_BF_TKEY = 120  /* crossCheck per-train keys: all-ones between calls (the merge resets them) */
 };

@@ -54,7 +54,10 @@ __device__ __forceinline__ int ring_slot(int kf, int R) { const int r = kf % R; 
 // unmatched one with depth > 0 adds a new point at Frame::UnprojectStereo (src/frame.cpp:335-356,
 // lorb::unproject_point) and its observation.  Observations and new points are appended in keypoint
 // order: thread t owns a run of consecutive keypoints, one block scan of three counters
-// (observations, new points, matches) places every run.
+// (observations, new points, matches) places every run.  RM > 0 (n <= 1024 RM): every input of the
+// thread's keypoints is loaded in one batch up front and stays in registers, so the kernel pays one
+// memory round trip instead of one per phase; RM = 0 re-reads them (any n).
+template <int RM>
 __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Pose6 pose,
                                                      const unsigned long long* __restrict__ qkey, int has_t,
                                                      int* __restrict__ mt, lorb::Mat4f Twc, float fx, float fy,
@@ -65,11 +68,41 @@ __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Po
   __shared__ int s_min[16];
   const int t = threadIdx.x;
   const int P0 = m.cnt[0], K0 = m.cnt[1];
-  const int R = (n + 1023) / 1024, q0 = min(t * R, n), q1 = min(q0 + R, n);
+  const int R = RM > 0 ? RM : (n + 1023) / 1024, q0 = min(t * R, n), q1 = min(q0 + R, n);
+  constexpr int RA = RM > 0 ? RM : 1;
+  unsigned long long kv[RA];
+  float xv[RA], yv[RA], zv[RA];
+  uint4 d0[RA], d1[RA];
+  int mv[RA];
+  if constexpr (RM > 0) {
+#pragma unroll
+    for (int u = 0; u < RM; ++u) {
+      const int q = q0 + u;
+      const bool ok = q < q1;
+      kv[u] = ok && has_t ? qkey[q] : ~0ull;
+      xv[u] = ok ? x[q] : 0.0f; yv[u] = ok ? y[q] : 0.0f; zv[u] = ok ? depth[q] : 0.0f;
+      d0[u] = d1[u] = make_uint4(0, 0, 0, 0);
+      if (ok) {
+        const uint4* sd = reinterpret_cast<const uint4*>(kdesc + 32 * (size_t)q);
+        d0[u] = sd[0]; d1[u] = sd[1];
+      }
+    }
+  }
+  auto key_of = [&](int u, int q) -> unsigned long long {
+    if constexpr (RM > 0) return kv[u];
+    else return has_t ? qkey[q] : ~0ull;
+  };
+  auto depth_of = [&](int u, int q) -> float {
+    if constexpr (RM > 0) return zv[u];
+    else return depth[q];
+  };
   {
     int mn = 0x7fffffff;
-    for (int q = q0; q < q1; ++q) {
-      const unsigned long long v = has_t ? qkey[q] : ~0ull;
+#pragma unroll RA
+    for (int u = 0; u < (RM > 0 ? RM : 1 << 30); ++u) {
+      const int q = q0 + u;
+      if (q >= q1) break;
+      const unsigned long long v = key_of(u, q);
       if (v != ~0ull) mn = min(mn, (int)(v >> 32));
     }
 #pragma unroll
@@ -80,15 +113,27 @@ __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Po
 #pragma unroll
     for (int w = 1; w < 16; ++w) mn = min(mn, s_min[w]);
     const int thr = max(2 * mn, 30);  // d > max(2 * minDist, 30.0) rejects (exact in integers)
-    for (int q = q0; q < q1; ++q) {
-      const unsigned long long v = has_t ? qkey[q] : ~0ull;
-      mt[q] = (v != ~0ull && (int)(v >> 32) <= thr) ? (int)(v & 0xffffffffu) : -1;
+#pragma unroll RA
+    for (int u = 0; u < (RM > 0 ? RM : 1 << 30); ++u) {
+      const int q = q0 + u;
+      if (q >= q1) break;
+      const unsigned long long v = key_of(u, q);
+      const int a = (v != ~0ull && (int)(v >> 32) <= thr) ? (int)(v & 0xffffffffu) : -1;
+      mt[q] = a;
+      if constexpr (RM > 0) mv[u] = a;
     }
   }
+  auto match_of = [&](int u, int q) -> int {
+    if constexpr (RM > 0) return mv[u];
+    else return mt[q];
+  };
   lorb::I4 c = {{0, 0, 0, 0}};
-  for (int q = q0; q < q1; ++q) {
-    const bool mat = mt[q] >= 0;
-    const bool nw = !mat && depth[q] > 0.0f;
+#pragma unroll RA
+  for (int u = 0; u < (RM > 0 ? RM : 1 << 30); ++u) {
+    const int q = q0 + u;
+    if (q >= q1) break;
+    const bool mat = match_of(u, q) >= 0;
+    const bool nw = !mat && depth_of(u, q) > 0.0f;
     c.v[0] += mat || nw; c.v[1] += nw; c.v[2] += mat;
   }
   lorb::I4 tot;
@@ -101,27 +146,36 @@ __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Po
   if (!ok) return;  // the map is left exactly as it was (the host stops the step here)
   if (t < 6) m.ring[6 * ring_slot(kf, m.R) + t] = pose.v[t];
   int ko = K0 + ex.v[0], pn = P0 + ex.v[1];
-  for (int q = q0; q < q1; ++q) {
-    const int a = mt[q];
-    const float z = depth[q];
+#pragma unroll RA
+  for (int u = 0; u < (RM > 0 ? RM : 1 << 30); ++u) {
+    const int q = q0 + u;
+    if (q >= q1) break;
+    const int a = match_of(u, q);
+    const float z = depth_of(u, q);
     const bool mat = a >= 0, nw = !mat && z > 0.0f;
     if (!(mat || nw)) continue;
+    float xq, yq;
+    if constexpr (RM > 0) { xq = xv[u]; yq = yv[u]; }
+    else { xq = x[q]; yq = y[q]; }
     int p = a;
     if (nw) {
       p = pn++;
       float X[3];
-      lorb::unproject_point(fx, fy, cx, cy, Twc, x[q], y[q], z, X);
+      lorb::unproject_point(fx, fy, cx, cy, Twc, xq, yq, z, X);
       m.pos[3 * p + 0] = X[0]; m.pos[3 * p + 1] = X[1]; m.pos[3 * p + 2] = X[2];
-      const uint4* sd = reinterpret_cast<const uint4*>(kdesc + 32 * (size_t)q);
       uint4* dd = reinterpret_cast<uint4*>(m.desc + 32 * (size_t)p);
-      dd[0] = sd[0]; dd[1] = sd[1];
+      if constexpr (RM > 0) { dd[0] = d0[u]; dd[1] = d1[u]; }
+      else {
+        const uint4* sd = reinterpret_cast<const uint4*>(kdesc + 32 * (size_t)q);
+        dd[0] = sd[0]; dd[1] = sd[1];
+      }
     }
     const int k = ko++;
     m.obs_pt[k] = p;
     m.flag_new[p] = 1;  // at most one per point: crossCheck matches are one-to-one
     m.obs_kf[k] = kf;
-    m.obs_uv[2 * k + 0] = x[q];
-    m.obs_uv[2 * k + 1] = y[q];
+    m.obs_uv[2 * k + 0] = xq;
+    m.obs_uv[2 * k + 1] = yq;
   }
   if (t == 0) {
     m.cnt[0] = P0 + tot.v[1]; m.cnt[1] = K0 + tot.v[0];
@@ -129,21 +183,43 @@ __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Po
   }
 }
 
-// cull, part 1: a point stays while a window keyframe (id >= t0) observes it
-__global__ __launch_bounds__(256) void k_map_mark(MapDev m, int Kb, int t0) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= Kb || k >= m.cnt[1]) return;
-  if (m.obs_kf[k] >= t0) m.flag_pt[m.obs_pt[k]] = 1;
-}
-
-// cull, part 2: an observation stays while its point stays and its keyframe is in the window or
-// among the F fixed keyframes before it; flags beyond the count are 0 (scan tail)
-__global__ __launch_bounds__(256) void k_map_obs_flag(MapDev m, int Kb, int t0) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
+// cull, one launch: a point stays while a window keyframe (id >= t0) observes it; an observation
+// stays while its point stays and its keyframe is in the window or among the F fixed keyframes
+// before it; flags beyond the count are 0 (scan tail).  Slots [0, K0) are sorted by point: each
+// thread finds its point's run inside its wavefront from two ballots (run starts, window
+// keyframes) and ORs the run's window bits; a run that crosses the wavefront's edge also walks the
+// slots beyond it.  The step's new observations (slots >= K0, keyframe = the newest, in the
+// window) keep themselves and their points (flag_new marks a point that got one).
+__global__ __launch_bounds__(256) void k_map_cull(MapDev m, int Kb, int K0, int t0) {
+  const int k = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63;
+  const int kc = min(m.cnt[1], Kb), k0 = min(K0, kc);
+  const bool old = k < k0;
+  int p = -1, kfv = 0, pprev = -1;
+  if (k < kc) { p = m.obs_pt[k]; kfv = m.obs_kf[k]; }
+  if (old && k > 0) pprev = m.obs_pt[k - 1];
+  const bool start = old && (k == 0 || pprev != p);
+  // every slot that is not an earlier one ends the runs before it
+  const unsigned long long B = __ballot(start || !old), Wb = __ballot(old && kfv >= t0);
   if (k > Kb) return;
-  int f = 0;
-  if (k < m.cnt[1]) f = m.flag_pt[m.obs_pt[k]] && m.obs_kf[k] >= t0 - m.F;
-  m.flag_obs[k] = f;
+  if (k >= kc) { m.flag_obs[k] = 0; return; }
+  if (!old) {
+    m.flag_obs[k] = kfv >= t0 - m.F;  // (a new observation: its keyframe is the newest)
+    if (kfv >= t0) m.flag_pt[p] = 1;
+    return;
+  }
+  const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1;
+  const unsigned long long below = B & upto, above = B & ~upto;
+  const int s0 = below ? 63 - __builtin_clzll(below) : 0;   // run's first lane in this wavefront
+  const int e0 = above ? __builtin_ctzll(above) : 64;       // one past its last lane
+  const unsigned long long run = (e0 == 64 ? ~0ull : (1ull << e0) - 1) & ~((1ull << s0) - 1);
+  bool keep = (Wb & run) != 0 || m.flag_new[p] != 0;
+  const int wbase = k - lane;
+  if (!below)  // the run began in an earlier wavefront
+    for (int j = wbase - 1; !keep && j >= 0 && m.obs_pt[j] == p; --j) keep = m.obs_kf[j] >= t0;
+  if (!above)  // the run goes on past this wavefront
+    for (int j = wbase + 64; !keep && j < k0 && m.obs_pt[j] == p; ++j) keep = m.obs_kf[j] >= t0;
+  m.flag_obs[k] = keep && kfv >= t0 - m.F;
+  if (start && keep) m.flag_pt[p] = 1;
 }
 
 // the flag scans are tile-local (one workgroup per tile, all tiles of both arrays in one launch);
@@ -169,9 +245,12 @@ __device__ __forceinline__ int new_before(const MapDev& m, int ntP, int p) {
 // step's new ones (slots >= K0, keypoint order, one per point at most) go after their point's
 // earlier ones.  A kept earlier observation moves to (kept ones before it) + (new ones of points
 // before its point); a new one of point p to (kept earlier ones of points <= p: the kept count
-// before the first earlier slot of a point > p, a binary search) + (new ones of points before p).
+// before the first earlier slot of a point > p) + (new ones of points before p).  That slot is
+// pt_off[p + 1] of the BA plan built on the earlier slots (its per-point offsets, points [0, P0)),
+// or a binary search over them when there is no such plan.
 // Workgroup 0 also writes the new counts and the window's initial / fixed poses from the ring.
-__global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, int K0, int t0, int ntP) {
+__global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, int K0, int P0, int t0, int ntP,
+                                                     const int* __restrict__ pt_off) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (blockIdx.x == 0) {
     if (i == 0) { m.cnt[0] = new_id(m, Pb); m.cnt[1] = new_pos(m, ntP, Kb); }
@@ -197,9 +276,13 @@ __global__ __launch_bounds__(256) void k_map_compact(MapDev m, int Pb, int Kb, i
       d = new_pos(m, ntP, i) + new_before(m, ntP, p);
     } else {
       int lo = 0, hi = K0;  // first earlier slot of a point > p
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (m.obs_pt[mid] <= p) lo = mid + 1; else hi = mid;
+      if (pt_off) {
+        lo = pt_off[min(p + 1, P0)];
+      } else {
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (m.obs_pt[mid] <= p) lo = mid + 1; else hi = mid;
+        }
       }
       d = new_pos(m, ntP, lo) + new_before(m, ntP, p);
     }
@@ -241,6 +324,7 @@ struct lorb_map {
   int* mt = nullptr;
   int* pinned = nullptr;
   lorb_ba_plan* plan = nullptr;
+  bool plan_ok = false;  // plan built on the current slots (its point offsets serve the compaction)
   std::vector<void*> allocs;
   ~lorb_map() {
     if (prof && prof_n)
@@ -306,17 +390,16 @@ lorb_ba_window_dev window_of(const lorb_map* M) {
 
 // slide to window [t0, t0 + W): cull points no window keyframe observes, drop observations by
 // keyframes older than the fixed ones, compact (stable), rebuild the BA slots and window poses
-int map_slide(lorb_map* M, int t0, int Pb, int Kb, int K0) {
+int map_slide(lorb_map* M, int t0, int Pb, int Kb, int K0, int P0, const int* pt_off) {
   lorb_ctx* ctx = M->ctx;
   hipStream_t s = ctx->stream;
   MapDev& m = M->m;
-  if (Kb > 0) hipLaunchKernelGGL(k_map_mark, dim3(lorb::ceil_div(Kb, 256)), dim3(256), 0, s, m, Kb, t0);
-  hipLaunchKernelGGL(k_map_obs_flag, dim3(lorb::ceil_div(Kb + 1, 256)), dim3(256), 0, s, m, Kb, t0);
+  hipLaunchKernelGGL(k_map_cull, dim3(lorb::ceil_div(Kb + 1, 256)), dim3(256), 0, s, m, Kb, std::min(K0, Kb), t0);
   const int ntP = lorb::ceil_div(Pb + 1, lorb::kScanTile), ntK = lorb::ceil_div(Kb + 1, lorb::kScanTile);
   hipLaunchKernelGGL(k_map_scans, dim3(2 * ntP + ntK), dim3(1024), 0, s, m, Pb, Kb, ntP);
   const int nmax = std::max(std::max(Pb, Kb), 1);
-  hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, std::min(K0, Kb), t0,
-                     ntP);
+  hipLaunchKernelGGL(k_map_compact, dim3(lorb::ceil_div(nmax, 256)), dim3(256), 0, s, m, Pb, Kb, std::min(K0, Kb), P0, t0,
+                     ntP, pt_off);
   LORB_CHECK_LAUNCH(ctx);
   std::swap(m.pos, m.pos2); std::swap(m.desc, m.desc2); std::swap(m.obs_pt, m.obs_pt2);
   std::swap(m.obs_kf, m.obs_kf2); std::swap(m.obs_uv, m.obs_uv2);
@@ -385,7 +468,7 @@ int lorb_map_create(lorb_ctx* ctx, const lorb_map_init* in, lorb_map** out) {
     if (rc == LORB_OK) rc = up(m.obs_uv, ouv.data(), sizeof(float) * 2 * (size_t)in->n_obs);
     if (rc == LORB_OK) {
       // the initial window [0, W): obs slots / window poses, no culling of a consistent input
-      rc = map_slide(M, 0, in->n_points, in->n_obs, in->n_obs);
+      rc = map_slide(M, 0, in->n_points, in->n_obs, in->n_obs, in->n_points, nullptr);
       M->h_P = in->n_points; M->h_K = in->n_obs;  // upper bounds until the first readback
     }
     if (rc == LORB_OK) {
@@ -393,6 +476,7 @@ int lorb_map_create(lorb_ctx* ctx, const lorb_map_init* in, lorb_map** out) {
       rc = lorb_ba_plan_create_dev(ctx, &w, &M->plan);
       // the map keeps its observations sorted by point: later builds skip the counting sort
       if (rc == LORB_OK) lorb::ba_plan_sorted_hint(M->plan, true);
+      M->plan_ok = rc == LORB_OK;
     }
     if (rc == LORB_OK) {
       LORB_HIP(ctx, hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
@@ -438,9 +522,15 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   for (int q = 0; q < 6; ++q) p6.v[q] = pose[q];
   lorb::Mat4f Twc;
   lorb::inv4_lu32f(Tcw, Twc.v);
-  hipLaunchKernelGGL(k_map_append, dim3(1), dim3(1024), 0, s, m, n, kf, p6, (const unsigned long long*)qkey,
-                     (int)(has_t && qkey), M->mt, Twc, frame->fx, frame->fy, frame->cx, frame->cy, d_desc, d_x, d_y,
-                     d_depth);
+#define LORB_APPEND(RM)                                                                                       \
+  hipLaunchKernelGGL(k_map_append<RM>, dim3(1), dim3(1024), 0, s, m, n, kf, p6, (const unsigned long long*)qkey, \
+                     (int)(has_t && qkey), M->mt, Twc, frame->fx, frame->fy, frame->cx, frame->cy, d_desc, d_x, d_y, \
+                     d_depth)
+  if (n <= 1024) LORB_APPEND(1);
+  else if (n <= 2048) LORB_APPEND(2);
+  else if (n <= 4096) LORB_APPEND(4);
+  else LORB_APPEND(0);
+#undef LORB_APPEND
   LORB_CHECK_LAUNCH(ctx);
   M->last_n = n;
   // Capacity: n keypoints add at most n points and n observations.  When that bound does not fit,
@@ -455,14 +545,16 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   }
   LORB_TRY(mark(2));
   // 4. slide the window by one keyframe; cull and compact
-  LORB_TRY(map_slide(M, M->t0 + 1, std::min(M->h_P + n, m.P_cap), std::min(M->h_K + n, m.K_cap), M->h_K));
+  LORB_TRY(map_slide(M, M->t0 + 1, std::min(M->h_P + n, m.P_cap), std::min(M->h_K + n, m.K_cap), M->h_K, M->h_P,
+                      M->plan_ok ? lorb::ba_plan_point_offsets(M->plan) : nullptr));
   LORB_TRY(mark(3));
-  LORB_HIP(ctx, hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s));
-  // 5. BA plan of the slid window (its readback synchronises the stream, so the counts above are in)
+  // 5. BA plan of the slid window; its one readback carries the window's live counts too
   const lorb_ba_window_dev w = window_of(M);
+  M->plan_ok = false;
   LORB_TRY(lorb_ba_plan_update_dev(M->plan, &w));
+  M->plan_ok = true;
   LORB_TRY(mark(4));
-  M->h_P = M->pinned[0]; M->h_K = M->pinned[1];
+  lorb::ba_plan_window_counts(M->plan, &M->h_P, &M->h_K);
   // 6. LocalPoseOptimization + float write-back of poses (ring) and points (map)
   LORB_TRY(lorb_ba_plan_solve(M->plan, opt));
   LORB_TRY(mark(5));
