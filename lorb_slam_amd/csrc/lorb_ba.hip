@@ -3227,10 +3227,24 @@ __global__ __launch_bounds__(256) void k_db_keys(lorb_ba_window_dev w, int C, in
 // one camera is found by the thread that starts the point's run, among the run's frames (the run
 // ends at the next run start of the wave's ballot, or by a scan for the wave's last run).  The
 // largest run and the error bits are reduced per workgroup before their one atomic each.
+// FUSE (C * C ints fit the LDS): the covisibility counts come from the runs too -- the run's start
+// thread adds each camera pair of its point (lower triangle: row = the larger camera; the host
+// mirrors it after the readback) and each camera's count into LDS tables, flushed with one atomic
+// per non-zero entry -- so k_db_cov does not run; and the workgroup's
+// histogram of optimised observations by input camera goes to hist[f * NB + block] (NB = 256-slot
+// blocks of the live slots, the blocks k_db_gather<true> places), so the placement needs no
+// histogram pass of its own.
 constexpr int kDbWords = 4;  // 64-point words per workgroup held in LDS (more: global atomics)
+constexpr int kDbFuseLds = 64 * 1024;  // LDS bytes the FUSE tables may take
+template <bool FUSE>
 __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, int F, int Wd, int* __restrict__ pt_off,
-                                                   int* __restrict__ hdr, unsigned long long* __restrict__ bits) {
-  extern __shared__ unsigned long long s_bits[];  // C * kDbWords
+                                                   int* __restrict__ hdr, unsigned long long* __restrict__ bits,
+                                                   int* __restrict__ cov, int* __restrict__ cam_cnt,
+                                                   int* __restrict__ hist) {
+  extern __shared__ unsigned long long s_bits[];  // C * kDbWords; FUSE: then cov C * C | cam C | hist C (ints)
+  int* s_cov = reinterpret_cast<int*>(s_bits + C * kDbWords);
+  int* s_cam = s_cov + C * C;
+  int* s_hist = s_cam + C;
   __shared__ int s_cnt, s_err;
   const int t = threadIdx.x, lane = t & 63;
   const int i = blockIdx.x * 256 + t;
@@ -3239,6 +3253,8 @@ __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, 
   const int* __restrict__ op = w.d_obs_point;
   const int* __restrict__ of = w.d_obs_frame;
   for (int k = t; k < C * kDbWords; k += 256) s_bits[k] = 0ull;
+  if (FUSE)
+    for (int k = t; k < C * C + 2 * C; k += 256) s_cov[k] = 0;
   if (t == 0) { s_cnt = 0; s_err = 0; }
   const int i0 = blockIdx.x * 256;
   const int w0 = i0 < n_obs ? max(op[i0], 0) >> 6 : 0;  // the workgroup's first word
@@ -3259,6 +3275,7 @@ __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, 
     else if (f >= C) err |= 2;
     else if (q < 0 || q >= n_pt) err |= 1;
     else if (f >= 0) {
+      if (FUSE) atomicAdd(&s_hist[f], 1);
       const unsigned long long m = 1ull << (q & 63);
       const int wl = (q >> 6) - w0;
       if (wl >= 0 && wl < kDbWords) atomicOr(&s_bits[f * kDbWords + wl], m);
@@ -3298,6 +3315,26 @@ __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, 
           for (int b = 0; b < a; ++b)
             if (of[i + b] == fa) err |= 4;
         }
+        if (FUSE && q >= 0 && q < n_pt) {  // the point's camera pairs and camera counts
+#pragma unroll
+          for (int a = 0; a < kR; ++a) {
+            if (fr[a] < 0 || fr[a] >= C) continue;
+            atomicAdd(&s_cam[fr[a]], 1);
+#pragma unroll
+            for (int b = 0; b < a; ++b)
+              if (fr[b] >= 0 && fr[b] < C && fr[b] != fr[a])
+                atomicAdd(&s_cov[max(fr[a], fr[b]) * C + min(fr[a], fr[b])], 1);
+          }
+          for (int a = kR; a < cnt; ++a) {
+            const int fa = of[i + a];
+            if (fa < 0 || fa >= C) continue;
+            atomicAdd(&s_cam[fa], 1);
+            for (int b = 0; b < a; ++b) {
+              const int fb = of[i + b];
+              if (fb >= 0 && fb < C && fb != fa) atomicAdd(&s_cov[max(fa, fb) * C + min(fa, fb)], 1);
+            }
+          }
+        }
       }
     }
   }
@@ -3311,6 +3348,15 @@ __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, 
     const int wd = w0 + k % kDbWords;
     if (v && wd < Wd)
       __hip_atomic_fetch_or(&bits[(size_t)(k / kDbWords) * Wd + wd], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (FUSE) {
+    for (int k = t; k < C * C + C; k += 256) {
+      const int v = s_cov[k];  // (cam_cnt follows cov in LDS and in the scratch)
+      if (v) __hip_atomic_fetch_add(k < C * C ? &cov[k] : &cam_cnt[k - C * C], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int NB = (n_obs + 255) / 256;
+    if ((int)blockIdx.x < NB)
+      for (int k = t; k < C; k += 256) hist[(size_t)k * NB + blockIdx.x] = s_hist[k];
   }
   if (t == 0) {
     if (s_cnt > __hip_atomic_load(&hdr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&hdr[1], s_cnt);
@@ -3413,8 +3459,11 @@ __global__ __launch_bounds__(256) void k_db_cov(int C, int Wd, const unsigned lo
 //    off[p] + p >= g S (weights k_p + 1, so a group holds <= kGB observations and points; trailing
 //    groups can be empty);
 //  * zeros: this rank's band, and the build scratch the next build accumulates into (camera x point
-//    bitsets, header max / error words; pt_cnt is left zero by k_db_scatter, cov / cam_cnt are
-//    rewritten whole by k_db_cov), so the next build needs no clearing fill.
+//    bitsets, header max / error words, cov / cam_cnt; pt_cnt is left zero by k_db_scatter), so the
+//    next build needs no clearing fill.
+// FUSE (after k_db_sorted<true>): also k_db_place's work -- the block's first slot per camera from
+// the camera offsets and the column prefix of k_db_sorted's input-camera histogram, then the rank
+// of each observation among the block's earlier ones of its camera.
 struct DbFused {
   const int* perm;   // input camera -> plan camera
   const int* gcam;   // observations per input camera, all ranks
@@ -3422,6 +3471,8 @@ struct DbFused {
   int sorted;        // the slots were sorted by point (k_db_sorted): slot e is sorted position e
   unsigned long long* bits;
   int* hdr;
+  int* cov;          // cov | cam_cnt (C * C + C ints): zeroed for the next build's k_db_sorted<true>
+  int cov_n;
 };
 // Point groups: group g = points [start(g), start(g + 1)), start(g) = the smallest p with
 // off[p] + p >= g S (P if none), found by one wavefront, 32-ary: each half-wave probes 32 points spread over its
@@ -3455,10 +3506,13 @@ __device__ __forceinline__ void group_bounds(const int* __restrict__ off, int P,
   s0 = __shfl(lo, 0, 64);
   s1 = __shfl(lo, 32, 64);
 }
+template <bool FUSE>
 __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d, int K, int C, int NB,
                                                    const int* __restrict__ key, const int* __restrict__ val,
-                                                   const int* __restrict__ perm, int* __restrict__ hist, DbFused f) {
-  extern __shared__ int s_h[];  // C
+                                                   const int* __restrict__ perm, int* __restrict__ hist, DbFused f,
+                                                   int* __restrict__ cam_pt) {
+  extern __shared__ int s_h[];  // C: histogram; FUSE: first slot per input camera (-1: absent)
+  __shared__ int s_c[FUSE ? 256 : 1];
   const int gt = blockIdx.x * 256 + threadIdx.x, gs = gridDim.x * 256;
   {  // initial values and camera activity
     const int m = max(max(6 * f.C, 6 * f.F), 3 * f.P);
@@ -3484,23 +3538,52 @@ __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d
   }
   for (int i = gt; i < f.env_n; i += gs) d.env_part[i] = 0.0;
   for (int i = gt; i < f.bits_n; i += gs) f.bits[i] = 0ull;
+  for (int i = gt; i < f.cov_n; i += gs) f.cov[i] = 0;
   if (gt == 0) { f.hdr[1] = 0; f.hdr[2] = 0; }
   if ((int)blockIdx.x >= NB) return;  // uniform per workgroup
-  for (int i = threadIdx.x; i < C; i += 256) s_h[i] = 0;
+  const int t = threadIdx.x;
+  for (int i = t; i < C; i += 256) s_h[i] = FUSE ? -1 : 0;
   __syncthreads();
-  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int e = blockIdx.x * 256 + t;
+  int c = -1, fr = -1, pt = 0;
   if (e < K) {
-    const int k = f.sorted ? e : val[e], fr = w.d_obs_frame[k];
-    const int c = fr >= 0 ? perm[fr] : -1;
-    const_cast<int*>(d.obs_pt)[e] = f.sorted ? w.d_obs_point[e] : key[e];
+    const int k = f.sorted ? e : val[e];
+    fr = w.d_obs_frame[k];
+    c = fr >= 0 ? perm[fr] : -1;
+    pt = f.sorted ? w.d_obs_point[e] : key[e];
+    const_cast<int*>(d.obs_pt)[e] = pt;
     const_cast<int*>(d.obs_cam)[e] = c;
     const_cast<int*>(d.obs_fix)[e] = fr >= 0 ? -1 : -1 - fr;
     const_cast<double2*>(d.obs_uv)[e] = make_double2(w.d_obs_uv[2 * k], w.d_obs_uv[2 * k + 1]);
-    const_cast<int*>(d.obs_cm)[e] = -1;
-    if (c >= 0) atomicAdd(&s_h[c], 1);
+    if (!FUSE || c < 0) const_cast<int*>(d.obs_cm)[e] = -1;
+    if (!FUSE && c >= 0) atomicAdd(&s_h[c], 1);
+  }
+  if (!FUSE) {
+    __syncthreads();
+    for (int i = t; i < C; i += 256) hist[(size_t)i * NB + blockIdx.x] = s_h[i];
+    return;
+  }
+  s_c[t] = c;
+  if (c >= 0) s_h[fr] = 0;
+  __syncthreads();
+  // column prefixes of the present cameras, one wavefront per camera (lanes stride the blocks)
+  const int lane = t & 63;
+  for (int cc = t >> 6; cc < C; cc += 4) {
+    if (s_h[cc] < 0) continue;  // uniform per wavefront
+    const int* h = hist + (size_t)cc * NB;
+    int v = 0;
+    for (int i = lane; i < (int)blockIdx.x; i += 64) v += h[i];
+    v = wave_isum(v);
+    if (lane == 0) s_h[cc] = d.cam_obs_off[perm[cc]] + v;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < C; i += 256) hist[(size_t)i * NB + blockIdx.x] = s_h[i];
+  if (c < 0) return;
+  int rank = 0;
+  for (int u = 0; u < t; ++u) rank += s_c[u] == c;
+  const int j = s_h[fr] + rank;
+  const_cast<int*>(d.cam_obs)[j] = e;
+  const_cast<int*>(d.obs_cm)[e] = j;
+  cam_pt[j] = pt;
 }
 
 // counting sort of the optimised observations by plan camera, stable: slot = camera offset (the
@@ -3719,6 +3802,10 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     b.pt_cnt = b.scr; b.hdr = b.pt_cnt + Pn + 1; b.cov = b.hdr + 8; b.cam_cnt = b.cov + C * C;
     b.bits = reinterpret_cast<unsigned long long*>(b.scr + ints);
   }
+  {  // camera-major block histograms: k_db_sorted<true> writes them before the readback
+    const size_t nb = (K + 1 + 255) / 256;
+    LORB_TRY(grow(P, &b.hist, &b.hist_cap, nb * C));
+  }
   int *a_pt, *a_cam, *a_fix, *a_cm, *a_camobs, *a_win, *a_act, *a_ptoff;
   double2* a_uv;
   double* a_fixp;
@@ -3838,14 +3925,20 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&b.pinned), sizeof(int) * nrb));
     b.pinned_n = nrb;
   }
-  bool sorted = b.sorted_hint;
+  bool sorted = b.sorted_hint, fuse = false;
   for (;;) {
     if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
     b.dirty = true;
+    fuse = sorted && C > 0 && sizeof(int) * ((size_t)C * C + 2 * C) <= (size_t)kDbFuseLds;
     if (sorted) {
-      hipLaunchKernelGGL(k_db_sorted, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256),
-                         sizeof(unsigned long long) * kDbWords * std::max(C, 1), s, *w, C,
-                         F, b.Wd, const_cast<int*>(d.pt_obs_off), b.hdr, b.bits);
+      const size_t lds = sizeof(unsigned long long) * kDbWords * std::max(C, 1) +
+                         (fuse ? sizeof(int) * ((size_t)C * C + 2 * C) : 0);
+      if (fuse)
+        hipLaunchKernelGGL(k_db_sorted<true>, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), lds, s, *w, C, F, b.Wd,
+                           const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt, b.hist);
+      else
+        hipLaunchKernelGGL(k_db_sorted<false>, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), lds, s, *w, C, F, b.Wd,
+                           const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt, b.hist);
     } else {
       hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);
       hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1,
@@ -3855,7 +3948,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
         hipLaunchKernelGGL(k_db_segsort, dim3(nb_pt), dim3(256), 0, s, *w, d.pt_obs_off, b.val_out, b.key_out);
       }
     }
-    if (C > 0)
+    if (C > 0 && !fuse)
       hipLaunchKernelGGL(k_db_cov, dim3(lorb::ceil_div(C * (C + 1) / 2, 4)), dim3(256), 0, s, C, b.Wd, b.bits, b.cov,
                          b.cam_cnt);
     LORB_CHECK_LAUNCH(ctx);
@@ -3867,7 +3960,10 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     sorted = false;  // slots out of order (or unused): the general phase, from a cleared scratch
     b.sorted_hint = false;
   }
-  const int* H = b.pinned;
+  int* H = b.pinned;
+  if (fuse)  // k_db_sorted<true> filled the lower triangle
+    for (int i = 0; i < C; ++i)
+      for (int j = i + 1; j < C; ++j) H[8 + (size_t)i * C + j] = H[8 + (size_t)j * C + i];
   const int K = H[0], maxk = H[1], err = H[2], Pn = H[3];
   const int* cov = H + 8;
   const int* cam_cnt = H + 8 + (size_t)C * C;
@@ -3994,12 +4090,17 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   {
     // this rank's band starts from zeros (blocks it has no pairs of stay zero; sharded: the
     // all-reduce writes the global band every iteration)
-    DbFused f{b.perm, b.gcam, C, F, Pn, G, S, P->env_total, C * b.Wd, sorted ? 1 : 0, b.bits, b.hdr};
-    hipLaunchKernelGGL(k_db_gather, dim3(std::max(NB, 1)), dim3(256), sizeof(int) * C, s, *w, d, K, C, NB, b.key_out,
-                       b.val_out, b.perm, b.hist, f);
+    DbFused f{b.perm, b.gcam, C, F, Pn, G, S, P->env_total, C * b.Wd, sorted ? 1 : 0, b.bits, b.hdr, b.cov, C * C + C};
+    if (fuse)
+      hipLaunchKernelGGL(k_db_gather<true>, dim3(std::max(NB, 1)), dim3(256), sizeof(int) * std::max(C, 1), s, *w, d, K,
+                         C, NB, b.key_out, b.val_out, b.perm, b.hist, f, b.cam_pt);
+    else
+      hipLaunchKernelGGL(k_db_gather<false>, dim3(std::max(NB, 1)), dim3(256), sizeof(int) * std::max(C, 1), s, *w, d,
+                         K, C, NB, b.key_out, b.val_out, b.perm, b.hist, f, b.cam_pt);
     b.dirty = false;
   }
-  if (K > 0) hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), sizeof(int) * std::max(C, 1), s, d, K, NB, C, b.hist, b.cam_pt);
+  if (K > 0 && !fuse)
+    hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), sizeof(int) * std::max(C, 1), s, d, K, NB, C, b.hist, b.cam_pt);
   if (!bps.empty())
     hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), sizeof(int) * (C + 1), s, d, C, b.cam_pt);
   LORB_CHECK_LAUNCH(ctx);
