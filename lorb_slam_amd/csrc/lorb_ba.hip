@@ -3293,9 +3293,18 @@ __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, 
         int e;
         if (above) {
           e = i - lane + __builtin_ctzll(above);
-        } else {
+        } else {  // the slots past the wave in batches of 8 (one round trip per batch, not per slot)
           e = i - lane + 64;
-          while (e < n_obs && op[e] == q) ++e;
+          for (bool more = true; more;) {
+            bool eq[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) eq[u] = e + u < n_obs && op[e + u] == q;
+            int run = 0;
+#pragma unroll
+            for (int u = 7; u >= 0; --u) run = eq[u] ? run + 1 : 0;  // leading matches
+            e += run;
+            more = run == 8;
+          }
           e = min(max(e, i + 1), n_obs);
         }
         cnt = e - i;
@@ -3665,17 +3674,25 @@ __global__ __launch_bounds__(256) void k_db_pairs(BaDev d, int C, const int* __r
 #pragma unroll
       for (int u = 0; u < kPR; ++u) p[u] = r0 + u < base + nb ? cam_pt[r0 + u] : -1;
     }
+    // the kPR lower bounds advance together, one halving per step (the step lengths depend on nl
+    // only), so each step's kPR LDS reads are in flight at once instead of kPR serial searches
+    int bs[kPR];
+#pragma unroll
+    for (int u = 0; u < kPR; ++u) bs[u] = 0;
+    for (int len = nl; len > 1;) {
+      const int half = len >> 1;
+#pragma unroll
+      for (int u = 0; u < kPR; ++u) bs[u] = lp[bs[u] + half] < p[u] ? bs[u] + half : bs[u];
+      len -= half;
+    }
     int c = 0;
 #pragma unroll
     for (int u = 0; u < kPR; ++u) {
       int j = -1;
-      if (p[u] >= 0) {
-        int lo = 0, hi = nl;
-        while (lo < hi) {
-          const int m = (lo + hi) >> 1;
-          if (lp[m] < p[u]) lo = m + 1; else hi = m;
-        }
-        if (lo < nl && lp[lo] == p[u]) j = l0 + lo;
+      if (p[u] >= 0 && nl > 0) {
+        const int v = lp[bs[u]];
+        const int lo = bs[u] + (v < p[u] ? 1 : 0);
+        if (lo < nl && (v < p[u] ? lp[lo] : v) == p[u]) j = l0 + lo;
       }
       jv[u] = j;
       c += j >= 0;
