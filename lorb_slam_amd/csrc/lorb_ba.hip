@@ -2544,6 +2544,7 @@ struct lorb_ba_devbuild {
   std::vector<double> h_red;                     // sharded: the build's host all-reduce
   // per-build structure uploaded in one copy: [BaWin | live (2) | perm (C) | cam_obs_off (C+1) | bp (up_bp_cap)]
   unsigned char* up_dev = nullptr; unsigned char* up_host = nullptr; int up_bp_cap = 0;
+  const unsigned char* up_host_dev = nullptr;  // up_host as the device reads it (pinned, mapped)
   size_t off_live = 0, off_perm = 0, off_camoff = 0, off_gcam = 0, off_bp = 0, up_bytes = 0;
   int* gcam = nullptr;  // device: observations per input camera over all ranks (camera activity)
 };
@@ -3482,6 +3483,16 @@ struct DbFused {
   int* hdr;
   int* cov;          // cov | cam_cnt (C * C + C ints): zeroed for the next build's k_db_sorted<true>
   int cov_n;
+  // ARGS (C <= kDbArgC): the upload is not copied before the launch -- the workgroups copy it from
+  // the mapped pinned staging (src -> dst, words), and read perm / gcam / cam_obs_off from `cams`
+  // (kernel arguments), not from the copy
+  const int* up_src;
+  int* up_dst;
+  int up_words;
+};
+constexpr int kDbArgC = 160;
+struct DbCams {
+  int perm[kDbArgC], gcam[kDbArgC], coff[kDbArgC + 1];
 };
 // Point groups: group g = points [start(g), start(g + 1)), start(g) = the smallest p with
 // off[p] + p >= g S (P if none), found by one wavefront, 32-ary: each half-wave probes 32 points spread over its
@@ -3515,21 +3526,26 @@ __device__ __forceinline__ void group_bounds(const int* __restrict__ off, int P,
   s0 = __shfl(lo, 0, 64);
   s1 = __shfl(lo, 32, 64);
 }
-template <bool FUSE>
+template <bool FUSE, bool ARGS>
 __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d, int K, int C, int NB,
                                                    const int* __restrict__ key, const int* __restrict__ val,
-                                                   const int* __restrict__ perm, int* __restrict__ hist, DbFused f,
-                                                   int* __restrict__ cam_pt) {
+                                                   const int* __restrict__ perm_dev, int* __restrict__ hist, DbFused f,
+                                                   int* __restrict__ cam_pt, DbCams cams) {
   extern __shared__ int s_h[];  // C: histogram; FUSE: first slot per input camera (-1: absent)
   __shared__ int s_c[FUSE ? 256 : 1];
   const int gt = blockIdx.x * 256 + threadIdx.x, gs = gridDim.x * 256;
+  if (ARGS)  // the upload, from the mapped staging (PCIe reads, no copy launch before this kernel)
+    for (int i = gt; i < f.up_words; i += gs) f.up_dst[i] = f.up_src[i];
+  const int* __restrict__ perm = ARGS ? cams.perm : perm_dev;
+  const int* __restrict__ gcam = ARGS ? cams.gcam : f.gcam;
+  const int* __restrict__ coff = ARGS ? cams.coff : d.cam_obs_off;
   {  // initial values and camera activity
     const int m = max(max(6 * f.C, 6 * f.F), 3 * f.P);
     for (int i = gt; i < m; i += gs) {
       if (i < 6 * f.C) {
         const int c = i / 6, q = i - 6 * c;
-        d.x_init_pose[6 * f.perm[c] + q] = (double)w.d_pose_init[i];
-        if (q == 0) const_cast<int*>(d.cam_active)[f.perm[c]] = f.gcam[c] > 0;
+        d.x_init_pose[6 * perm[c] + q] = (double)w.d_pose_init[i];
+        if (q == 0) const_cast<int*>(d.cam_active)[perm[c]] = gcam[c] > 0;
         if (q == 0) const_cast<int*>(d.cam_win)[c] = 0;
       }
       if (i < 6 * f.F) const_cast<double*>(d.fixed_pose)[i] = (double)w.d_fixed_pose[i];
@@ -3583,7 +3599,7 @@ __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d
     int v = 0;
     for (int i = lane; i < (int)blockIdx.x; i += 64) v += h[i];
     v = wave_isum(v);
-    if (lane == 0) s_h[cc] = d.cam_obs_off[perm[cc]] + v;
+    if (lane == 0) s_h[cc] = coff[perm[cc]] + v;
   }
   __syncthreads();
   if (c < 0) return;
@@ -3911,6 +3927,11 @@ int up_alloc(lorb_ba_plan* P, int bp_need) {
   }
   LORB_TRY(dalloc(P, b.up_bytes, &b.up_dev));
   LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&b.up_host), b.up_bytes));
+  {
+    void* hd = nullptr;
+    LORB_HIP(ctx, hipHostGetDevicePointer(&hd, b.up_host, 0));
+    b.up_host_dev = static_cast<const unsigned char*>(hd);
+  }
   b.up_bp_cap = cap;
   BaDev& d = P->dev;
   d.win = reinterpret_cast<const BaWin*>(b.up_dev);
@@ -4085,7 +4106,10 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   P->grid_pblk = b.pblk_cap;
   LORB_TRY(up_alloc(P, (int)bps.size()));
   // one upload (pinned staging, stream-ordered; the next build writes the staging only after its
-  // own readback synchronised the stream)
+  // own readback synchronised the stream).  C <= kDbArgC: no copy launch -- k_db_gather copies the
+  // staging over the bus and takes the camera tables as kernel arguments (the step's host phase
+  // ends with the gather's launch)
+  int up_words = 0;
   {
     unsigned char* h = b.up_host;
     memcpy(h, &P->hwin[0], sizeof(BaWin));
@@ -4096,7 +4120,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     memcpy(h + b.off_gcam, gcam, sizeof(int) * C);
     if (!bps.empty()) memcpy(h + b.off_bp, bps.data(), sizeof(BlockPair) * bps.size());
     const size_t bytes = b.off_bp + sizeof(BlockPair) * bps.size();
-    LORB_HIP(ctx, hipMemcpyAsync(b.up_dev, h, bytes, hipMemcpyHostToDevice, s));
+    up_words = (int)((bytes + 3) / 4);
+    if (C > kDbArgC) LORB_HIP(ctx, hipMemcpyAsync(b.up_dev, h, bytes, hipMemcpyHostToDevice, s));
   }
   // 4. structure kernels: gather (+ initial values, point groups, zeros), the camera-major block
   //    offsets, the stable placement by camera, the block pair lists
@@ -4107,13 +4132,21 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   {
     // this rank's band starts from zeros (blocks it has no pairs of stay zero; sharded: the
     // all-reduce writes the global band every iteration)
-    DbFused f{b.perm, b.gcam, C, F, Pn, G, S, P->env_total, C * b.Wd, sorted ? 1 : 0, b.bits, b.hdr, b.cov, C * C + C};
-    if (fuse)
-      hipLaunchKernelGGL(k_db_gather<true>, dim3(std::max(NB, 1)), dim3(256), sizeof(int) * std::max(C, 1), s, *w, d, K,
-                         C, NB, b.key_out, b.val_out, b.perm, b.hist, f, b.cam_pt);
-    else
-      hipLaunchKernelGGL(k_db_gather<false>, dim3(std::max(NB, 1)), dim3(256), sizeof(int) * std::max(C, 1), s, *w, d,
-                         K, C, NB, b.key_out, b.val_out, b.perm, b.hist, f, b.cam_pt);
+    const bool args = C <= kDbArgC;
+    DbFused f{b.perm, b.gcam, C, F, Pn, G, S, P->env_total, C * b.Wd, sorted ? 1 : 0, b.bits, b.hdr, b.cov, C * C + C,
+              reinterpret_cast<const int*>(b.up_host_dev), reinterpret_cast<int*>(b.up_dev), args ? up_words : 0};
+    DbCams cams;
+    if (args) {
+      for (int c = 0; c < C; ++c) { cams.perm[c] = map[c]; cams.gcam[c] = gcam[c]; }
+      for (int c = 0; c <= C; ++c) cams.coff[c] = cam_off[c];
+    }
+    const size_t lds = sizeof(int) * std::max(C, 1);
+    const dim3 g(std::max(NB, 1));
+#define LORB_GATHER(FU, AR) hipLaunchKernelGGL((k_db_gather<FU, AR>), g, dim3(256), lds, s, *w, d, K, C, NB, b.key_out, \
+                                                b.val_out, b.perm, b.hist, f, b.cam_pt, cams)
+    if (fuse) { if (args) LORB_GATHER(true, true); else LORB_GATHER(true, false); }
+    else { if (args) LORB_GATHER(false, true); else LORB_GATHER(false, false); }
+#undef LORB_GATHER
     b.dirty = false;
   }
   if (K > 0 && !fuse)
