@@ -86,6 +86,23 @@ def test_solver_sorted_duplicate(ctx):
         s.close()
 
 
+def test_solver_many_cameras(ctx):
+    """a window of more cameras than the device build passes as kernel arguments (kDbArgC = 160) and
+    than its fused covisibility tables hold in LDS: the upload goes by copy, k_db_cov and k_db_place
+    run -- in caller order and point-sorted, both against the oracle"""
+    s = BASolver(ctx)
+    try:
+        w = synth.ba_window(seed=26, n_kf=170, n_pts=2500, n_fixed=2, fixed_obs_per_kf=40)
+        check(s, w, OPT10)
+        o = np.argsort(np.asarray(w["obs_point"]), kind="stable")
+        uv = np.asarray(w["obs_uv"]).reshape(-1, 2)
+        ws = dict(w, obs_point=np.asarray(w["obs_point"])[o], obs_frame=np.asarray(w["obs_frame"])[o], obs_uv=uv[o])
+        check(s, ws, OPT10)
+        assert s.info()["host_plan_fallback"] == 0
+    finally:
+        s.close()
+
+
 def test_solver_fallback_and_errors(ctx):
     """a point observed twice by one camera (the reference's std::map<Frame*, size_t> cannot hold
     it) is rejected by both plan builders; bad indices are rejected like lorb_ba_local rejects them;
