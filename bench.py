@@ -682,8 +682,8 @@ def sub_dropin(ctx, D, args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="c4", choices=["c4", "c2", "shared", "rehearse"])
     ap.add_argument("--shared-points", type=int, default=80000)
     ap.add_argument("--windows", type=int, default=1)
