@@ -212,8 +212,10 @@ def workload_c4(ctx, args, rank):
 
     def check():
         out = {"keyframes_stepped": pos[0], "windows": []}
-        for m in maps:
+        for i, m in enumerate(maps):
             st = m.read()
+            if i == 0:  # the window of the last step, for roofline_iteration
+                out["_window"] = {"obs_point": st["obs_point"], "obs_frame": st["obs_frame"], "point_init": st["point"]}
             out["windows"].append({k: st[k] for k in ("t0", "points", "observations", "matches", "new_points")}
                                   | {"ba_final_cost": st["summary"]["final_cost"],
                                      "ba_iterations": st["summary"]["iterations"]})
@@ -288,35 +290,62 @@ def cpu_baseline_c4(seq, budget_s):
             "host_cpu": model, "host_cpus_available": avail}
 
 
+C1_PAIRS = 32  # distinct frame pairs the C1 timings cycle through (every call sees new inputs)
+
+
+def c1_inputs(n=C1_PAIRS):
+    """n distinct C1 frame pairs (synth.two_frames seeds 1..n: 2 x 500 kps, 200 shared map points)
+    with their a2 train sets and a12 problems (200 residuals each)"""
+    from lorb_slam_amd import synth
+    out = []
+    for s in range(1, n + 1):
+        pr = synth.two_frames(seed=s, n_kps=500, n_shared=200)
+        last = pr["last"]
+        out.append(dict(pr=pr, tdesc=np.ascontiguousarray(last["mp_desc"][last["has_mp"] > 0]),
+                        pb=synth.pose_only_batch(seed=s, n_frames=1, n_res=200)))
+    return out
+
+
+def c1_stages(ctx_or_oracle, oracle=False):
+    """the three C1 calls on input set x: a2 BF crossCheck, a4 SearchByProjection(th 15), a12"""
+    if oracle:
+        O = ctx_or_oracle
+        return {"a2_bf_match": lambda x: O.bf_match(x["pr"]["cur_kps"]["desc"], x["tdesc"]),
+                "a4_search_by_projection_th15": lambda x: O.search_by_projection_frame(
+                    x["pr"]["fp"], x["pr"]["cur_Tcw"], x["pr"]["cur_kps"], x["pr"]["slot_state"], x["pr"]["last"], 15.0),
+                "a12_pose_only_200": lambda x: O.ba_pose_only(x["pb"])}
+    ctx = ctx_or_oracle
+    return {"a2_bf_match": lambda x: ctx.bf_match([x["pr"]["cur_kps"]["desc"]], [x["tdesc"]]),
+            "a4_search_by_projection_th15": lambda x: ctx.search_by_projection_frame(
+                x["pr"]["fp"], x["pr"]["cur_Tcw"], x["pr"]["cur_kps"], x["pr"]["slot_state"], x["pr"]["last"], 15.0),
+            "a12_pose_only_200": lambda x: ctx.ba_pose_only(x["pb"])}
+
+
 def sub_c1(ctx, D, args):
     """BASELINE C1 on the GPU through the host C-ABI (the calls a per-frame caller issues): the a2 BF
     crossCheck match, SearchByProjection(curr, last, 15) (a4) and ProjectPoseOptimization of 200
-    matched points (a12), host arrays in and out, synchronous, median of 30 sequences.  Latency-bound:
-    a few thousand items per call."""
+    matched points (a12), host arrays in and out, synchronous.  Every call takes the next of 32
+    distinct frame pairs (new inputs each time: nothing is resident from an earlier call); median
+    over 3 passes of the 32.  Latency-bound: a few thousand items per call."""
     import lorb_slam_amd.window  # noqa: F401  (Context.search_by_projection_frame)
-    from lorb_slam_amd import synth
-    pr = synth.two_frames(seed=1, n_kps=500, n_shared=200)
-    last, cur = pr["last"], pr["cur_kps"]
-    tdesc = np.ascontiguousarray(last["mp_desc"][last["has_mp"] > 0])
-    pb = synth.pose_only_batch(seed=1, n_frames=1, n_res=200)
-    stages = {"a2_bf_match": lambda: ctx.bf_match([cur["desc"]], [tdesc]),
-              "a4_search_by_projection_th15": lambda: ctx.search_by_projection_frame(
-                  pr["fp"], pr["cur_Tcw"], cur, pr["slot_state"], last, 15.0),
-              "a12_pose_only_200": lambda: ctx.ba_pose_only(pb)}
+    xs = c1_inputs()
+    stages = c1_stages(ctx)
     for fn in stages.values():
-        fn()
+        fn(xs[0])
     per = {}
     for name, fn in stages.items():
         ts = []
-        for _ in range(30):
-            t0 = time.perf_counter()
-            fn()
-            ts.append(time.perf_counter() - t0)
+        for _ in range(3):
+            for x in xs:
+                t0 = time.perf_counter()
+                fn(x)
+                ts.append(time.perf_counter() - t0)
         per[name] = D.reduce(float(np.median(ts)), "MAX") * 1e3
     total = sum(per.values())
     return {"workload": "c1_two_frames_500kps", "value": 1e3 / total, "unit": "C1 sequences/s (a2 + a4 + a12)",
-            "ms_per_sequence": total, "stage_ms_median": per,
-            "call": "host C-ABI (lorb_bf_match, lorb_search_by_projection_frame, lorb_ba_pose_only), synchronous"}
+            "ms_per_sequence": total, "stage_ms_median": per, "distinct_inputs": len(xs),
+            "call": "host C-ABI (lorb_bf_match, lorb_search_by_projection_frame, lorb_ba_pose_only), synchronous; "
+                    "one packed H2D copy and one D2H copy per call"}
 
 
 def cpu_baseline_c1(budget_s):
@@ -327,29 +356,104 @@ def cpu_baseline_c1(budget_s):
     thread, median of >= 30 runs."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    from lorb_slam_amd import synth
-    pr = synth.two_frames(seed=1, n_kps=500, n_shared=200)
-    last, cur = pr["last"], pr["cur_kps"]
-    tdesc = np.ascontiguousarray(last["mp_desc"][last["has_mp"] > 0])
-    pb = synth.pose_only_batch(seed=1, n_frames=1, n_res=200)
-    stages = {"a2_bf_match_500x%d" % len(tdesc): lambda: O.bf_match(cur["desc"], tdesc),
-              "a4_search_by_projection_th15": lambda: O.search_by_projection_frame(
-                  pr["fp"], pr["cur_Tcw"], cur, pr["slot_state"], last, 15.0),
-              "a12_pose_only_200": lambda: O.ba_pose_only(pb)}
+    xs = c1_inputs()
+    stages = c1_stages(O, oracle=True)
     per = {}
     t_end = time.perf_counter() + budget_s
     for name, fn in stages.items():
         ts = []
-        while len(ts) < 30 or (time.perf_counter() < t_end and len(ts) < 2000):
+        while len(ts) < 3 * len(xs) or (time.perf_counter() < t_end and len(ts) < 2000):
+            x = xs[len(ts) % len(xs)]
             t0 = time.perf_counter()
-            fn()
+            fn(x)
             ts.append(time.perf_counter() - t0)
         per[name] = float(np.median(ts)) * 1e3
     total = sum(per.values())
     return {"value": 1e3 / total, "unit": "C1 sequences/s (a2 + a4 + a12)", "cores": 1, "kind": "port",
             "ms_per_sequence": total, "stage_ms_median": per,
-            "sample": "2 frames x 500 kps, 200 shared MPs (synth.two_frames seed 1): a2 + a4 th=15 + a12, oracle C "
-                      "gcc -O3 -ffp-contract=off via ctypes, 1 thread, median of >= 30 runs per stage"}
+            "sample": f"{len(xs)} distinct pairs of 2 frames x 500 kps, 200 shared MPs (synth.two_frames seeds 1..{len(xs)}): "
+                      "a2 + a4 th=15 + a12, oracle C gcc -O3 -ffp-contract=off via ctypes, 1 thread, median of >= 96 "
+                      "runs per stage (the same inputs as the GPU leg)"}
+
+
+def workload_c3(ctx, args, rank):
+    """BASELINE config 2: local BA on 20 keyframes / 4,000 points / 30,000 window
+    observations (+2 fixed keyframes, 800 observations), exactly 10 LM iterations (tolerances 0).
+    A step = the device-built plan of the resident window (lorb_ba_plan_update_dev: the reference
+    rebuilds its Ceres problem every call) + the 10-iteration solve from the initial values."""
+    from lorb_slam_amd import _abi as A
+    from lorb_slam_amd import synth
+    from lorb_slam_amd.runtime import BAPlanDev
+    w = synth.ba_window(seed=3 + 1009 * rank, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400)
+    arrays = BAPlanDev.upload(ctx, w)
+    t0 = time.perf_counter()
+    plan = BAPlanDev(ctx, arrays, 20, 2, w["intr"])
+    ctx.sync()
+    plan_ms = (time.perf_counter() - t0) * 1e3
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+
+    def step():
+        plan.update()
+        plan.solve(opt)
+
+    def check():
+        _, _, summ = plan.read()
+        return {"ba_final_cost": summ[0]["final_cost"], "ba_iterations": summ[0]["iterations"]}
+
+    def cleanup():
+        plan.close()
+        for x in arrays.values():
+            x.free()
+
+    n_obs, n_pts, F = len(w["obs_point"]), len(w["point_init"]), 20
+    bw = 6 * 8 - 1
+    kspec = {  # the C4 figures of workload_c4 for this window
+        2: ("hbm", n_obs * 36 * 8.0 + (6 * F) * (bw + 1) * 8.0, "GB/s"),
+        3: ("hbm", n_obs * (34 * 8.0 + 16 + 12) + n_pts * 24.0, "GB/s"),
+        4: ("fp64", (6 * F) * bw * bw + 4.0 * (6 * F) * bw, "TFLOP/s"),
+    }
+
+    def cpu():
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        budget = max(2.0, args.cpu_budget / 2)
+        n1, d1 = run_parallel(lambda: O.ba_local([w], opt), 1, budget)
+        nt = cpu_threads()
+        nn, dn = run_parallel(lambda: O.ba_local([w], opt), nt, budget) if nt > 1 else (n1, d1)
+        model, avail = host_cpu()
+        return {"value": 10.0 * n1 / d1, "unit": "BA iterations/s", "cores": 1, "kind": "port",
+                "sample": f"{n1} x C3 solve (10 LM its, Schur + dense LLT), oracle C restatement gcc -O3, "
+                          f"1 thread (Ceres default num_threads=1), {d1:.1f}s",
+                "nproc": {"value": 10.0 * nn / dn, "cores": nt,
+                          "sample": f"{nn} solves on {nt} threads (independent windows; {nt} = the box's per-GPU CPU share), {dn:.1f}s"},
+                "host_cpu": model, "host_cpus_available": avail}
+
+    return dict(step=step, check=check, ba_iters=10.0, matches=0.0, pairs=0.0, plan_ms=plan_ms, cleanup=cleanup,
+                kspec=kspec, traffic_key="c3", window=w, n_poses=F,
+                config={"workload": "c3_local_ba", "kf": F, "fixed_kf": 2, "points": n_pts, "observations": n_obs,
+                        "window_observations": int((np.asarray(w["obs_frame"]) >= 0).sum()), "lm_iterations": 10,
+                        "step": "device-built plan of the resident window + 10 LM its from the initial values"},
+                cpu=cpu)
+
+
+def sub_c3(ctx, D, args):
+    """BASELINE C3 (20 KF / 4k points / 30k observations, 10 LM its) inside the default run."""
+    wl = workload_c3(ctx, args, D.rank)
+    steps = max(10, min(args.steps, 100))
+    elapsed = timed(ctx, D, wl, steps, max(2, args.warmup))
+    kt, pn = profile_pass(ctx, wl, steps)
+    total = D.reduce(wl["ba_iters"] * steps, "SUM")
+    chk = wl["check"]()
+    cpu = wl["cpu"]() if (D.rank == 0 and not args.no_cpu_baseline and D.world == 1) else None
+    ms = elapsed / steps * 1e3
+    out = {"workload": wl["config"]["workload"], "config": wl["config"], "value": total / elapsed,
+           "unit": "BA iterations/s", "steps": steps, "ms_per_step": ms, "plan_create_ms": wl["plan_ms"],
+           "roofline": roofline_entry(kt, wl, pn),
+           "roofline_iteration": roofline_iteration(wl["window"], wl["n_poses"], ms / 10.0, "c3"),
+           "cpu_baseline": cpu, "check": chk}
+    wl["cleanup"]()
+    return out
 
 
 def workload_shared(ctx, args, rank, D, comm):
@@ -543,6 +647,53 @@ def roofline_entry(kt, wl, steps):
             "all_kernels_ms_per_step": {K_NAMES.get(kk, str(kk)): v[0] / steps for kk, v in kt.items()}}
 
 
+def pmc_bytes_per_iteration(workload):
+    """HBM bytes per LM iteration of the BA kernels (k_ba_*: every launch of a solve, k_ba_init's
+    amortised) from this round's committed PMC summary, with the per-kernel breakdown; None when the
+    workload has no summary.  Iterations = k_ba_lm_end launches (one per LM iteration)."""
+    for path in TRAFFIC:
+        try:
+            with open(path) as f:
+                tab = json.load(f)
+        except (OSError, ValueError):
+            continue
+        ks = (tab.get("workloads") or {}).get(workload, {}).get("kernels", {})
+        its = ks.get("k_ba_lm_end", {}).get("calls", 0)
+        if not its:
+            continue
+        per = {k: e["calls"] * e["hbm_bytes_per_launch"] / its for k, e in ks.items()
+               if k.startswith("k_ba_") and e.get("hbm_bytes_per_launch") is not None and e.get("calls")}
+        return {"bytes": sum(per.values()), "per_kernel": per, "source": os.path.relpath(path, ROOT)}
+    return None
+
+
+def roofline_iteration(win, n_poses, ms_per_iteration, traffic_key):
+    """SURVEY §8(d)'s whole-iteration roofline of one LM iteration on a window:
+       F_it = sum_obs 380 + sum_pts (60 + 108 k_p + 108 k_p (k_p + 1)) + (6F)^3 / 3 + 4 (6F)^2 + sum_obs 40
+       B_it = 24 N_obs + 48 N_pts + 16 (6F)^2
+    (k_p = window observations of point p, F = optimised poses; the (6F)^3/3 term is the dense LLT
+    that §8(d) prices, not the banded one this build runs), against the measured time per iteration
+    (the whole step / 10: conservative, it includes the match and the plan build), with the PMC
+    bytes per iteration beside B_it."""
+    obs_point = np.asarray(win["obs_point"])
+    opt = np.asarray(win["obs_frame"]) >= 0
+    n_obs = len(obs_point)
+    n_pts = len(win["point_init"])
+    kp = np.bincount(obs_point[opt], minlength=n_pts).astype(np.float64)
+    n6 = 6.0 * n_poses
+    f_it = 420.0 * n_obs + float(np.sum(60.0 + 108.0 * kp + 108.0 * kp * (kp + 1.0))) + n6 ** 3 / 3.0 + 4.0 * n6 ** 2
+    b_it = 24.0 * n_obs + 48.0 * n_pts + 16.0 * n6 ** 2
+    t = ms_per_iteration * 1e-3
+    pmc = pmc_bytes_per_iteration(traffic_key)
+    return {"flop_per_iteration": f_it, "bytes_per_iteration": b_it, "ms_per_iteration": ms_per_iteration,
+            "achieved_tflops": f_it / t / 1e12, "peak_tflops": FP64_PEAK / 1e12, "frac_fp64": f_it / t / FP64_PEAK,
+            "achieved_gbs": b_it / t / 1e9, "peak_gbs": HBM_PEAK / 1e9, "frac_hbm": b_it / t / HBM_PEAK,
+            "pmc_bytes_per_iteration": pmc["bytes"] if pmc else None,
+            "pmc_over_algorithmic": pmc["bytes"] / b_it if pmc else None,
+            "pmc_per_kernel": pmc["per_kernel"] if pmc else None, "traffic_source": pmc["source"] if pmc else None,
+            "definition": "SURVEY 8(d) F_it / B_it per LM iteration; time = step / 10"}
+
+
 def timed(ctx, D, wl, steps, warmup):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync; max over ranks."""
     for _ in range(warmup):
@@ -684,7 +835,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="c4", choices=["c4", "c2", "shared", "rehearse"])
+    ap.add_argument("--workload", default="c4", choices=["c4", "c3", "c2", "shared", "rehearse"])
     ap.add_argument("--shared-points", type=int, default=80000)
     ap.add_argument("--windows", type=int, default=1)
     ap.add_argument("--pairs", type=int, default=256)
@@ -693,6 +844,7 @@ def main():
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 sub-record of the default run")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in LocalPoseOptimization sub-record")
     ap.add_argument("--no-shared", action="store_true", help="skip the shared-window (RCCL) sub-record")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 local-BA sub-record")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -722,10 +874,14 @@ def main():
     if args.workload == "shared":
         wl = workload_shared(ctx, args, D.rank, D, comm)
     else:
-        wl = {"c4": workload_c4, "c2": workload_c2, "rehearse": workload_rehearse}[args.workload](ctx, args, D.rank)
+        wl = {"c4": workload_c4, "c3": workload_c3, "c2": workload_c2,
+              "rehearse": workload_rehearse}[args.workload](ctx, args, D.rank)
 
     elapsed = timed(ctx, D, wl, args.steps, args.warmup)
     check = wl["check"]()
+    rwin = check.pop("_window", None) if isinstance(check, dict) else None
+    if rwin is None and wl.get("window") is not None:
+        rwin = wl["window"]
     kt, pn = ({}, 1) if rehearse else profile_pass(ctx, wl, args.steps)
     total_iters = D.reduce(wl["ba_iters"] * args.steps, "SUM")
     total_matches = D.reduce(wl["matches"] * args.steps, "SUM")
@@ -735,10 +891,11 @@ def main():
     c2 = sub_c2(ctx, D, args) if (args.workload == "c4" and not args.no_c2) else None
     dropin = sub_dropin(ctx, D, args) if (args.workload == "c4" and not args.no_dropin) else None
     c1 = sub_c1(ctx, D, args) if (args.workload == "c4" and not args.no_c2) else None
+    c3 = sub_c3(ctx, D, args) if (args.workload == "c4" and not args.no_c3) else None
     shared = (sub_shared(ctx, D, args, comm) if (args.workload in ("c4", "rehearse") and not args.no_shared)
               else None)
     if D.rank == 0:
-        if args.workload in ("c4", "shared"):
+        if args.workload in ("c4", "c3", "shared"):
             value, unit = total_iters / elapsed, "BA iterations/s"
         elif args.workload == "c2":
             value, unit = total_matches / elapsed, "matches/s"
@@ -754,7 +911,12 @@ def main():
             "config": dict(wl["config"], parallelism=par),
             "matches_per_sec": total_matches / elapsed, "plan_build_ms": wl["plan_ms"],
             "map_create_ms": wl.get("create_ms"),
-            "roofline": roofline_entry(kt, wl, pn), "cpu_baseline": cpu, "c2": c2, "dropin_local_ba": dropin, "shared": shared, "c1": c1,
+            "roofline": roofline_entry(kt, wl, pn),
+            "roofline_iteration": (roofline_iteration(rwin, wl.get("n_poses", wl["config"].get("kf", 50)),
+                                                      elapsed / args.steps * 1e3 / max(wl["ba_iters"], 1.0),
+                                                      wl["traffic_key"])
+                                   if rwin is not None and wl["ba_iters"] > 0 else None),
+            "cpu_baseline": cpu, "c2": c2, "c3": c3, "dropin_local_ba": dropin, "shared": shared, "c1": c1,
             "check": check,
         }
         if rehearse:

@@ -45,21 +45,13 @@ inline lorb_ctx* thread_ctx(int device = 0) {
   return h.ctx;
 }
 
-// The calling thread's BA solver (device-built plans resident across LocalPoseOptimization calls).
-// Created after the thread's ctx, so it is destroyed before it.
+// The ctx's BA solver (device-built plans resident across LocalPoseOptimization calls).  The ctx
+// owns it (lorb_ctx_ba_solver): it is destroyed by lorb_destroy, so it never outlives the ctx
+// whatever ctx the caller passes.
 inline lorb_ba_solver* thread_ba_solver(lorb_ctx* ctx) {
-  struct Holder {
-    lorb_ba_solver* s = nullptr;
-    lorb_ctx* ctx = nullptr;
-    ~Holder() { if (s) lorb_ba_solver_destroy(s); }
-  };
-  thread_local Holder h;
-  if (h.s && h.ctx != ctx) { lorb_ba_solver_destroy(h.s); h.s = nullptr; }
-  if (!h.s) {
-    if (lorb_ba_solver_create(ctx, &h.s) != LORB_OK) throw Error("lorb_ba_solver_create failed");
-    h.ctx = ctx;
-  }
-  return h.s;
+  lorb_ba_solver* s = nullptr;
+  if (lorb_ctx_ba_solver(ctx, &s) != LORB_OK) throw Error("lorb_ctx_ba_solver failed");
+  return s;
 }
 
 inline void check(lorb_ctx* ctx, int rc, const char* what) {

@@ -503,6 +503,10 @@ int lorb_ba_solver_solve(lorb_ba_solver* solver, const lorb_ba_window* window, c
  * plan, [3] its S half band, [4] its Cholesky kernel, [5] 1 if its cameras were reordered (RCM) */
 int lorb_ba_solver_info(lorb_ba_solver* solver, int32_t* info, int32_t n);
 int lorb_ba_solver_destroy(lorb_ba_solver* solver);
+/* The ctx's own solver: created on the first call, destroyed by lorb_destroy(ctx) (so it never
+ * outlives its ctx, and a new ctx never inherits it).  Not to be passed to lorb_ba_solver_destroy.
+ * The adapters' LocalPoseOptimization uses it (include/lorb/adapters.hpp). */
+int lorb_ctx_ba_solver(lorb_ctx* ctx, lorb_ba_solver** out);
 /* plan structure, first n of: [0] S half band (max over windows, scalar rows), [1] Cholesky kernel of
  * the last solve (0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s, -1 none yet), [2] (camera, camera)
  * blocks, [3] point groups, [4] observations, [5] points, [6] cameras, [7] 1 if some window's
@@ -531,6 +535,11 @@ int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8);
  *   4. BA::LocalPoseOptimization of the window (device-built plan, LM with `opt`), then the float
  *      write-back of the window's poses and all points (src/bundle_adjust.cpp:317-329).
  * step_dev is asynchronous except for one small readback (the plan's counts and covisibility).
+ * Errors: a step whose new points / observations would exceed the capacities returns LORB_E_NOMEM
+ * and leaves the map as it was.  A step that fails later (the plan build of step 4, e.g. a point
+ * with 256 or more observations) returns that error with steps 1-3 applied: the map stays usable
+ * (its host counts are re-read from the device) and the next step rebuilds the plan.  If even that
+ * re-read fails, the map is marked broken and every later step returns LORB_E_DEVICE.
  * ---------------------------------------------------------------------------------------- */
 typedef struct lorb_map lorb_map;
 typedef struct lorb_map_init {

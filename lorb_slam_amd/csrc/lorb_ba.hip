@@ -18,6 +18,7 @@
 
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <map>
 
@@ -218,6 +219,9 @@ struct BaDev {
   double* ycam;              // sum n (solution, scaled space, y = -step)
   double* part;              // n_pblk * 8 partials
   unsigned long long* dbg;   // diagnostic stamps (LORB_CHOL_STAMPS builds only)
+  double* kco;               // k_ba_chol_2s back-substitution operators: per window
+                             // ((row_base >> 4) + w) * 1024 doubles, top side's blocks then the
+                             // bottom side's, [block][16][64] (BandSide::bsk_block)
   WinState* st;
   // [0] point groups, [1] block pairs in use.  Launch grids may be larger (device-built plans
   // launch at capacity so that the captured LM graph survives a rebuild); the extra workgroups exit.
@@ -1273,8 +1277,8 @@ __global__ __launch_bounds__(256) void k_ba_chol_w(BaDev d) {
       const int j = c0 + jc;
       double lk[NB];
 #pragma unroll
-      for (int k = 0; k < NB; ++k) {  // L(c0 + k, j), k > jc
-        const bool ok = k > jc;
+      for (int k = 0; k < NB; ++k) {  // L(c0 + k, j), k > jc, inside the band (bw < 15: not all of them)
+        const bool ok = k > jc && k - jc <= bw;
         const double v = A[ok ? (c0 + k) * (bw + 1) + (j - (c0 + k) + bw) : 0];
         lk[k] = ok ? v : 0.0;
       }
@@ -1370,6 +1374,7 @@ struct BandSide {
   int* pdone = nullptr;                // panels whose L is in the band (release-counted, for linv)
   int nbk = 0, dir = 0;                // row blocks; +1 top view, -1 reversed bottom view
   int zslot = 0;                       // A[zslot] == 0.0 (out-of-band reads of the back-substitution)
+  double* kco = nullptr;               // this side's back-substitution operators (bsk_block)
   unsigned long long* phases = nullptr;  // LORB_CHOL_PHASES diagnostics: chain wait / factor / store cycles
   unsigned long long* trace = nullptr;   // LORB_CHOL_TRACE diagnostics: per-panel event times
   int tslot = 0;                         // (slot of this wave's next panel; cycles since t0)
@@ -1710,6 +1715,73 @@ struct BandSide {
       S.zw = zw;
     }
   }
+  // Back-substitution operator of T / B block c0, built off the critical path (after the block's
+  // diagonal inverse X): the block's step -- y = X^T z_b, then the push of y into the 47 rows
+  // above -- folded into ONE product with z_b.  Lane l (window row r = bs_row(c0)) gets
+  //   block rows (j = r - c0 >= 0):  coef[k] = X(k, j)                          (y_j = sum_k coef[k] z_k)
+  //   rows above:                    coef[k] = sum_{j <= k} L(c0 + j, r) X(k, j) (zw_r -= sum_k coef[k] z_k)
+  // at kco[(c0 / 16) * 1024 + 64 k + l].  The bs_run_k step is then one LDS round trip (publish z_b,
+  // 16 broadcast reads) where bs_run<true> has two.  X is the full 16 x 16 block: bw >= 15.
+  __device__ __forceinline__ void bsk_block(int c0) const {
+    const int row = bs_row(c0), j = row - c0;
+    const bool blk = j >= 0;
+    double lj[16], acc[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int dd = c0 + jj - row;  // L(c0 + jj, row) lies in the band iff 1 <= dd <= bw
+      const bool ok = !blk && row >= 0 && dd >= 1 && dd <= bw;
+      const double v = A[ok ? idx(c0 + jj, row) : zslot];
+      lj[jj] = blk ? (jj == j ? 1.0 : 0.0) : v;  // a block row picks column j of X (exact)
+      acc[jj] = 0.0;
+    }
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj)
+#pragma unroll
+      for (int k = jj; k < 16; ++k) acc[k] = fma(lj[jj], A[idx(c0 + k, c0 + jj)], acc[k]);  // X(k, jj)
+    double* o = kco + (c0 >> 4) * 1024 + lane;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[64 * k] = acc[k];
+  }
+  __device__ __forceinline__ void bsk_load(int c0, double (&cf)[16]) const {
+    const double* p = kco + (c0 >> 4) * 1024 + lane;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) cf[k] = p[64 * k];
+  }
+  // blocks c_from, c_from - 16, ..., c_to through their bsk_block operators; cf holds block
+  // c_from's on entry, the next block's are loaded (L2) while this one runs.  Rows entering above
+  // are merged before the product, as in bs_run.
+  __device__ __forceinline__ void bs_run_k(BsWin& S, int c_from, int c_to, double (&cf)[16]) const {
+    for (int c0 = c_from; c0 >= c_to; c0 -= 16) {
+      int row = bs_row(c0);
+      asm volatile("" : "+v"(row));
+      const int j = row - c0;
+      const bool blk = j >= 0;
+      double cn[16];
+      bsk_load(c0 - 16 >= c_to ? c0 - 16 : c0, cn);
+      double zw = S.zw;
+      if (blk) z[row] = zw;  // z_b is final: publish it
+      zw = S.pend ? S.zin : zw;
+      wave_sync_lds();
+      const double2* zb2 = reinterpret_cast<const double2*>(z + c0);
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k2 = 0; k2 < 8; ++k2) {
+        const double2 v = zb2[k2];
+        a4[(2 * k2) & 3] = fma(cf[2 * k2], v.x, a4[(2 * k2) & 3]);
+        a4[(2 * k2 + 1) & 3] = fma(cf[2 * k2 + 1], v.y, a4[(2 * k2 + 1) & 3]);
+      }
+      const double s = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      zw = blk ? s : zw - s;
+      if (blk) {
+        z[row] = zw;                                  // y_b (after every lane's broadcast read)
+        S.zin = row - 64 >= 0 ? z[row - 64] : 0.0;    // the row entering above
+      }
+      S.pend = blk;
+      S.zw = zw;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) cf[k] = cn[k];
+    }
+  }
 };
 
 // Flat copy of band chunks [j0, j1) (16-byte chunks of the row-major n x (bw + 1) band) by nthr
@@ -1801,6 +1873,10 @@ __device__ __forceinline__ void stage_fix(const BaDev& d, const LMOpt& o, double
 }
 
 constexpr int kChol2sThreads = 512;
+// 1: the T / B back-substitution runs one LDS round trip per block (BandSide::bsk_block / bs_run_k)
+#ifndef LORB_BSK
+#define LORB_BSK 1
+#endif
 // LDS words of k_ba_chol_2s: band (n16 rows), both sides' rhs (n16 + 48), two 64 x 18 exchanges
 // (together the 48 x 48 combine), zX (48), two 64 x 17 panel hand-off buffers, a zero word
 __host__ __device__ constexpr int chol2s_words(int n16, int bw) {
@@ -1852,6 +1928,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   // of L as the panels finish, for the back-substitution.
   __shared__ unsigned long long s_mask;
   __shared__ int s_pdone[2];
+  __shared__ int s_linv[2];           // diagonal-block inverses done, per side (LORB_BSK)
   __shared__ int s_lrd[2], s_prd[2];  // per side: L panels posted (chain), panel columns posted (update)
   __shared__ int s_hand[3];           // T / B -> M hand-over (below)
   const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
@@ -1889,6 +1966,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     s_bad = 0;
     s_head_done = 0;
     s_pdone[0] = 0; s_pdone[1] = 0;
+    s_linv[0] = 0; s_linv[1] = 0;
     s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
     s_hand[0] = 0; s_hand[1] = 0; s_hand[2] = 0;
     unsigned long long msk = 0;
@@ -1909,6 +1987,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   BandSide bot{Ab, zb, xb, rb, bw, lane, (n16 - 1) * B1 + bw, -1, -bw};
   top.pdone = &s_pdone[0]; bot.pdone = &s_pdone[1];
   top.zslot = (int)(zero - Ab); bot.zslot = top.zslot;
+  top.kco = d.kco + (size_t)((W.row_base >> 4) + w) * 1024;
+  bot.kco = top.kco + (size_t)(m >> 4) * 1024;
   top.nbk = bot.nbk = nbk; top.dir = 1; bot.dir = -1;
   if (prog) { top.mask = &s_mask; bot.mask = &s_mask; }
 #ifdef LORB_CHOL_TRACE
@@ -1968,6 +2048,9 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
       while (__hip_atomic_load(pd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= p) __builtin_amdgcn_s_sleep(1);
       TR1(56 + 32 * side + 2 * p);   // dbg[256 + 32 side + 2 p]
       me.linv(16 * p);
+#if LORB_BSK
+      if (lane == 0) __hip_atomic_fetch_add(&s_linv[side], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
       TR1(57 + 32 * side + 2 * p);
     }
     TR1(10 + side);
@@ -1983,6 +2066,23 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb);
   }
   if (wv < 6) C2_STAMP(wv);
+#if LORB_BSK
+  // The T / B back-substitution operators (bsk_block), once a side's diagonal inverses are done:
+  // wave 5 builds the top side's (after its own bottom-side inverses), wave 7 the bottom side's
+  // (after the staging), in the order the back-substitution needs them.  Both run beside the
+  // combine and the M phase on SIMDs whose waves are idle then; the stores drain before the
+  // barrier that precedes the back-substitution.
+  if (wv == 5 || wv == 7) {
+    const int ks = wv == 5 ? 0 : 1;
+    const BandSide& kside = ks == 0 ? top : bot;
+    const int nkb = (ks == 0 ? m : nB) / 16;
+    wait_ge<true>(&s_linv[ks], nkb);
+    TR1(16 + 2 * ks);
+    for (int b = nkb - 1; b >= 0; --b) kside.bsk_block(16 * b);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the operators are in L2 before the barrier
+    TR1(17 + 2 * ks);
+  }
+#endif
   // Hand-over to the M phase by flags, not barriers (the diagonal-block inverses of waves 4 / 5
   // may still be running): wave 2 posts that it has read its last L from xt, wave 3 then writes
   // the bottom side's window on M into X = xt (+ xb) and posts it, wave 1 posts zX.
@@ -2064,6 +2164,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
 #endif
   if (wv == 0) {
     BS_PH(3);
+#if LORB_BSK
+    double cf[16];
+    top.bsk_load(m - 16, cf);  // the first T block's operator, loaded under the M blocks
+#endif
     BandSide::BsWin S{top.bs_init(m + 32, 0)};
     TR1(5);
     top.bs_run<false>(S, m + 32, m);                   // y_M (chained triangles)
@@ -2071,14 +2175,26 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     TR1(6);
     if (lane < 48) zb[nB + 47 - lane] = zt[m + lane];  // into the reversed bottom rows
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if LORB_BSK
+    top.bs_run_k(S, m - 16, 0, cf);                   // y_T (one product per block)
+#else
     top.bs_run<true>(S, m - 16, 0);                   // y_T (inverted diagonal blocks)
+#endif
     BS_PH(5);
     TR1(7);
   } else if (wv == 1) {
+#if LORB_BSK
+    double cf[16];
+    bot.bsk_load(nB - 16, cf);
+#endif
     wait_ge<true>(&s_hand[0], 2);  // a long wait (the M phase): sleep, do not steal LDS cycles
     BS_PH(6);
     BandSide::BsWin S{bot.bs_init(nB - 16, 48)};
+#if LORB_BSK
+    bot.bs_run_k(S, nB - 16, 0, cf);                // y_B (reversed)
+#else
     bot.bs_run<true>(S, nB - 16, 0);                // y_B (reversed)
+#endif
     BS_PH(7);
     TR1(12);
   }
@@ -2547,12 +2663,21 @@ struct lorb_ba_devbuild {
   const unsigned char* up_host_dev = nullptr;  // up_host as the device reads it (pinned, mapped)
   size_t off_live = 0, off_perm = 0, off_camoff = 0, off_gcam = 0, off_bp = 0, up_bytes = 0;
   int* gcam = nullptr;  // device: observations per input camera over all ranks (camera activity)
+  // camera_order is a function of the adjacency pattern alone: a build whose pattern equals the
+  // previous one's (a sliding window usually keeps its banded pattern) reuses that order
+  std::vector<char> last_adj;
+  std::vector<int> last_map;
 };
 
 struct lorb_ba_plan {
   lorb_ctx* ctx = nullptr;
   int W = 0, Ctot = 0, Ptot = 0, K = 0, NF = 0, n_pblk = 0, n_bp = 0, n_pairs = 0;
   int env_total = 0, n_total = 0, max_env = 0, max_bw = 0, max_env_w = 0, min_n16 = 1 << 30;
+  int min_bw = 1 << 30;  // narrowest band of a non-empty window (k_ba_chol_2s needs >= 15)
+  // LORB_HOST_PHASE=1 (diagnostics): host time of the device builds' host phase (readback landed ->
+  // k_db_gather launched), printed at destruction
+  double hp_us = 0.0;
+  int hp_n = 0;
   std::vector<BaWin> hwin;
   std::vector<void*> allocs;
   BaDev dev{};
@@ -2582,6 +2707,7 @@ struct lorb_ba_plan {
   int chol_kind = -1;         // last launched Cholesky: 0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s
   lorb_ba_devbuild* devb = nullptr;  // device-built plan (lorb_ba_plan_create_dev)
   ~lorb_ba_plan() {
+    if (hp_n) fprintf(stderr, "lorb_ba_plan: host phase %.2f us per device build (%d builds)\n", hp_us / hp_n, hp_n);
     if (devb) {
       if (devb->pinned) (void)hipHostFree(devb->pinned);
       if (devb->up_host) (void)hipHostFree(devb->up_host);
@@ -2837,6 +2963,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
     bw.env_base = env_base; bw.env_size = n * (bwid + 1); bw.n = n; bw.row_base = row_base; bw.bw = bwid;
     P->max_env = std::max(P->max_env, bw.env_size + 2 * n);
     P->max_bw = std::max(P->max_bw, bwid);
+    if (n > 0) P->min_bw = std::min(P->min_bw, bwid);
     {
       const int n16 = (n + 15) & ~15;
       // one-sided K6w: band + z + invd + exchange; two-sided K6t: (n16 + 48) band rows, z, invd,
@@ -2949,6 +3076,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
 #else
   LORB_TRY(dalloc(P, (size_t)nw * 8, &d.dbg));
 #endif
+  LORB_TRY(dalloc(P, ((size_t)P->n_total / 16 + nw + 1) * 1024, &d.kco));
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
   if (!obs_cam.empty()) { /* keep obs arrays alive via allocs */ }
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -2963,7 +3091,9 @@ int chol_kind_of(const lorb_ba_plan* P) {
   static const bool no_2s = [] { const char* e = getenv("LORB_CHOL"); return e && e[0] == 'w'; }();
   if (!P->Ctot) return -1;
   const bool chol_w = !force_old && P->max_bw <= 48 && sizeof(double) * (size_t)P->max_env_w <= (size_t)kLdsBudget;
-  const bool chol_2s = chol_w && !no_2s && P->min_n16 >= 128;
+  // two-sided: its back-substitution uses the full inverse of each 16 x 16 diagonal block, which
+  // the band storage holds only for bw >= 15
+  const bool chol_2s = chol_w && !no_2s && P->min_n16 >= 128 && P->min_bw >= 15;
   return chol_2s ? 2 : chol_w ? 1 : 0;
 }
 
@@ -3896,6 +4026,7 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
 #else
   LORB_TRY(dalloc(P, (size_t)8, &d.dbg));
 #endif
+  LORB_TRY(dalloc(P, ((size_t)n / 16 + 2) * 1024, &d.kco));
   LORB_TRY(dalloc(P, (size_t)1, &P->d_state)); d.st = P->d_state;
   P->W = 1;
   P->hwin.assign(1, BaWin{});
@@ -3947,23 +4078,30 @@ int up_alloc(lorb_ba_plan* P, int bp_need) {
 
 int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   lorb_ba_devbuild& b = *P->devb;
-  if (w->n_poses != b.C || w->n_fixed != b.F || w->max_obs > b.K_cap || w->max_points > b.P_cap)
+  const bool shape_ok = w->n_poses == b.C && w->n_fixed == b.F && w->max_obs <= b.K_cap && w->max_points <= b.P_cap;
+  // Sharded plans are collective: a rank-local failure before the exchange below (a shape that
+  // differs from the plan's, a failed allocation or copy) is not returned here -- it becomes an
+  // error bit of the all-reduce, so every rank reaches the exchange and every rank returns the error.
+  if (!shape_ok && !P->comm)
     return lorb::set_error(ctx, LORB_E_INVALID, "window shape differs from the plan's (cameras %d/%d, fixed %d/%d)",
                            w->n_poses, b.C, w->n_fixed, b.F);
   hipStream_t s = ctx->stream;
   BaDev& d = P->dev;
   const int C = b.C, F = b.F, Kc = w->max_obs;
+  const size_t nrb = 8 + (size_t)C + (size_t)C * C;
+  bool sorted = b.sorted_hint, fuse = false;
+  int lerr = shape_ok ? 0 : 32;  // rank-local failures (bits 5, 6 of the exchanged error word)
   // 1. per-point counts and camera x point bitsets; point offsets; counting sort by point
   //    (stable); covisibility counts from the bitsets.  The scratch is left clear by the previous
   //    build's k_db_gather; only a build that stopped before it (an error) leaves it dirty.
+  const int phase_rc = !shape_ok ? LORB_OK : [&]() -> int {
   const int nb_obs = lorb::ceil_div(std::max(Kc, 1), 256), nb_pt = lorb::ceil_div(std::max(b.P_cap, 1), 256);
-  const size_t nrb = 8 + (size_t)C + (size_t)C * C;
   if (b.pinned_n < nrb) {
     if (b.pinned) (void)hipHostFree(b.pinned);
+    b.pinned = nullptr; b.pinned_n = 0;
     LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&b.pinned), sizeof(int) * nrb));
     b.pinned_n = nrb;
   }
-  bool sorted = b.sorted_hint, fuse = false;
   for (;;) {
     if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
     b.dirty = true;
@@ -3998,7 +4136,17 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     sorted = false;  // slots out of order (or unused): the general phase, from a cleared scratch
     b.sorted_hint = false;
   }
-  int* H = b.pinned;
+  return LORB_OK;
+  }();
+  static const bool hp_log = [] { const char* e = getenv("LORB_HOST_PHASE"); return e && e[0] == '1'; }();
+  const auto hp_t0 = std::chrono::steady_clock::now();
+  if (phase_rc != LORB_OK) {
+    if (!P->comm) return phase_rc;
+    lerr |= 64;
+  }
+  std::vector<int> h_zero;  // a failed rank contributes an empty structure to the exchange
+  if (lerr) h_zero.assign(nrb, 0);
+  int* H = lerr ? h_zero.data() : b.pinned;
   if (fuse)  // k_db_sorted<true> filled the lower triangle
     for (int i = 0; i < C; ++i)
       for (int j = i + 1; j < C; ++j) H[8 + (size_t)i * C + j] = H[8 + (size_t)j * C + i];
@@ -4013,14 +4161,14 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   int K_all = K, gerr = err, gmaxk = maxk;
   std::vector<int> g_int;
   if (P->comm) {
-    // [cov | cam_cnt (contiguous, m) | K | n_points out of range | error bits 0..3] summed; the largest
+    // [cov | cam_cnt (contiguous, m) | K | n_points out of range | error bits 0..6] summed; the largest
     // per-point count (the group size check) by a max
     const size_t m = (size_t)C * C + C;
-    b.h_red.assign(m + 6, 0.0);
+    b.h_red.assign(m + 9, 0.0);
     for (size_t i = 0; i < m; ++i) b.h_red[i] = (double)cov[i];
     b.h_red[m] = K;
     b.h_red[m + 1] = (Pn < 0 || Pn > b.P_cap) ? 1.0 : 0.0;
-    for (int q = 0; q < 4; ++q) b.h_red[m + 2 + q] = (err >> q) & 1;
+    for (int q = 0; q < 7; ++q) b.h_red[m + 2 + q] = ((err | lerr) >> q) & 1;
     LORB_TRY(lorb::comm_allreduce_host(P->comm, b.h_red.data(), b.h_red.size(), LORB_OP_SUM));
     double mk = maxk;
     LORB_TRY(lorb::comm_allreduce_host(P->comm, &mk, 1, LORB_OP_MAX));
@@ -4030,9 +4178,15 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     gcam = g_int.data() + (size_t)C * C;
     K_all = (int)b.h_red[m];
     gerr = b.h_red[m + 1] > 0.0 ? 16 : 0;
-    for (int q = 0; q < 4; ++q) gerr |= b.h_red[m + 2 + q] > 0.0 ? 1 << q : 0;
+    for (int q = 0; q < 7; ++q) gerr |= b.h_red[m + 2 + q] > 0.0 ? 1 << q : 0;
     gmaxk = (int)mk;
   }
+  if (gerr & 32)
+    return lorb::set_error(ctx, LORB_E_INVALID, "window shape differs from the plan's on %s (cameras %d/%d, fixed %d/%d)",
+                           shape_ok ? "another rank" : "this rank", w->n_poses, b.C, w->n_fixed, b.F);
+  if (gerr & 64)
+    return phase_rc != LORB_OK ? phase_rc
+                               : lorb::set_error(ctx, LORB_E_DEVICE, "device plan build failed on another rank");
   if (gerr & 1) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a point index outside [0, n_points)");
   if (gerr & 2) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a frame index >= n_poses");
   if (gerr & 4) return lorb::set_error(ctx, LORB_E_INVALID, "a point observed twice by one camera");
@@ -4046,7 +4200,11 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   std::vector<char> adj((size_t)C * C, 0);
   for (int i = 0; i < C; ++i)
     for (int j = 0; j < C; ++j) adj[(size_t)i * C + j] = (i == j && gcam[i] > 0) || gcov[(size_t)i * C + j] > 0;
-  const std::vector<int> map = camera_order(C, adj);
+  if (b.last_adj != adj) {
+    b.last_map = camera_order(C, adj);
+    b.last_adj.swap(adj);
+  }
+  const std::vector<int>& map = b.last_map;
   std::vector<int> inv(C);
   for (int c = 0; c < C; ++c) inv[map[c]] = c;
   P->cam_map.assign(1, map);
@@ -4080,6 +4238,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   P->Ctot = C; P->Ptot = Pn; P->K = K; P->NF = F; P->n_pblk = G; P->n_bp = (int)bps.size(); P->n_pairs = n_pairs;
   P->env_total = bw.env_size; P->n_total = n;
   P->max_env = bw.env_size + 2 * n; P->max_bw = bwid;
+  P->min_bw = n > 0 ? bwid : (1 << 30);
   {
     // the Cholesky's LDS is sized for a band of 48 (the widest k_ba_chol_w / _2s take) when that
     // fits, so that a narrower band after a rebuild keeps the captured solve
@@ -4148,6 +4307,10 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     else { if (args) LORB_GATHER(false, true); else LORB_GATHER(false, false); }
 #undef LORB_GATHER
     b.dirty = false;
+    if (hp_log) {
+      P->hp_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - hp_t0).count();
+      P->hp_n++;
+    }
   }
   if (K > 0 && !fuse)
     hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), sizeof(int) * std::max(C, 1), s, d, K, NB, C, b.hist, b.cam_pt);
@@ -4198,6 +4361,9 @@ int lorb_ba_plan_create_dev(lorb_ctx* ctx, const lorb_ba_window_dev* win, lorb_b
   if (!P) return LORB_E_NOMEM;
   P->ctx = ctx;
   P->devb = new (std::nothrow) lorb_ba_devbuild();
+  // slots sorted by point take k_db_sorted (no counting sort); unsorted ones fall back once and the
+  // plan keeps the general path from then on
+  if (P->devb) P->devb->sorted_hint = true;
   int rc = P->devb ? dev_alloc(ctx, win, P) : LORB_E_NOMEM;
   if (rc == LORB_OK) rc = dev_build(ctx, win, P);
   if (rc != LORB_OK) { delete P; return rc; }
@@ -4220,6 +4386,7 @@ int lorb_ba_plan_create_sharded_dev(lorb_ctx* ctx, lorb_comm* comm, const lorb_b
   P->ctx = ctx;
   P->comm = comm;
   P->devb = new (std::nothrow) lorb_ba_devbuild();
+  if (P->devb) P->devb->sorted_hint = true;  // as lorb_ba_plan_create_dev (shard.shard_window sorts by point)
   int rc = P->devb ? dev_alloc(ctx, shard, P) : LORB_E_NOMEM;
   if (rc == LORB_OK) rc = dev_build(ctx, shard, P);
   if (rc != LORB_OK) { delete P; return rc; }
@@ -4309,27 +4476,22 @@ int lorb_ba_pose_only(lorb_ctx* ctx, const lorb_pose_problem_batch* prob,
   const int nf = prob->n_frames;
   if (nf <= 0) return LORB_OK;
   const int nr = prob->res_off[nf];
-  int32_t* roff; float *intr, *pinit, *pts, *obs;
-  double* dpose; lorb_ba_summary* dsum;
-  LORB_TRY(lorb::upload_t(ctx, S_W0, prob->res_off, (size_t)nf + 1, &roff));
-  LORB_TRY(lorb::upload_t(ctx, S_W1, prob->intr, (size_t)nf * 4, &intr));
-  LORB_TRY(lorb::upload_t(ctx, S_W2, prob->pose_init, (size_t)nf * 6, &pinit));
-  LORB_TRY(lorb::scratch_t(ctx, S_W3, (size_t)std::max(nr, 1) * 3, &pts));
-  LORB_TRY(lorb::scratch_t(ctx, S_W4, (size_t)std::max(nr, 1) * 2, &obs));
-  if (nr > 0) {
-    LORB_HIP(ctx, hipMemcpyAsync(pts, prob->pts3d, sizeof(float) * 3 * nr, hipMemcpyHostToDevice, ctx->stream));
-    LORB_HIP(ctx, hipMemcpyAsync(obs, prob->obs2d, sizeof(float) * 2 * nr, hipMemcpyHostToDevice, ctx->stream));
-  }
-  LORB_TRY(lorb::scratch_t(ctx, S_W5, (size_t)nf * 6, &dpose));
-  LORB_TRY(lorb::scratch_t(ctx, S_W6, (size_t)nf, &dsum));
-  hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(256), 0, ctx->stream, roff, intr, pinit, pts, obs,
-                     to_dev_opt(opt), dpose, dsum);
+  // every input in one H2D copy, poses and summaries in one D2H copy
+  lorb::InPack in(ctx);
+  const int i_roff = in.add_t(prob->res_off, (size_t)nf + 1), i_intr = in.add_t(prob->intr, (size_t)nf * 4),
+            i_pinit = in.add_t(prob->pose_init, (size_t)nf * 6), i_pts = in.add_t(prob->pts3d, (size_t)nr * 3),
+            i_obs = in.add_t(prob->obs2d, (size_t)nr * 2);
+  LORB_TRY(in.commit());
+  lorb::OutPack out(ctx);
+  const int o_pose = out.add(sizeof(double) * 6 * nf), o_sum = out.add(sizeof(lorb_ba_summary) * nf);
+  LORB_TRY(out.alloc());
+  hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(256), 0, ctx->stream, in.dev<int32_t>(i_roff), in.dev<float>(i_intr),
+                     in.dev<float>(i_pinit), in.dev<float>(i_pts), in.dev<float>(i_obs), to_dev_opt(opt),
+                     out.dev<double>(o_pose), out.dev<lorb_ba_summary>(o_sum));
   LORB_CHECK_LAUNCH(ctx);
-  LORB_HIP(ctx, hipMemcpyAsync(pose_out, dpose, sizeof(double) * 6 * nf, hipMemcpyDeviceToHost, ctx->stream));
-  std::vector<lorb_ba_summary> hs(nf);
-  LORB_HIP(ctx, hipMemcpyAsync(hs.data(), dsum, sizeof(lorb_ba_summary) * nf, hipMemcpyDeviceToHost, ctx->stream));
-  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  if (summaries) std::copy(hs.begin(), hs.end(), summaries);
+  LORB_TRY(out.fetch());
+  memcpy(pose_out, out.host<double>(o_pose), sizeof(double) * 6 * nf);
+  if (summaries) memcpy(summaries, out.host<lorb_ba_summary>(o_sum), sizeof(lorb_ba_summary) * nf);
   if (Tcw_out)
     for (int f = 0; f < nf; ++f) {
       const float R[3] = {(float)pose_out[6 * f], (float)pose_out[6 * f + 1], (float)pose_out[6 * f + 2]};

@@ -270,4 +270,14 @@ int lorb_ba_solver_destroy(lorb_ba_solver* S) {
   return LORB_OK;
 }
 
+int lorb_ctx_ba_solver(lorb_ctx* ctx, lorb_ba_solver** out) {
+  if (!ctx || !out) return LORB_E_INVALID;
+  if (!ctx->solver) {
+    const int rc = lorb_ba_solver_create(ctx, &ctx->solver);
+    if (rc != LORB_OK) return rc;
+  }
+  *out = ctx->solver;
+  return LORB_OK;
+}
+
 }  // extern "C"

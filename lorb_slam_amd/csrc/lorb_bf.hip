@@ -321,7 +321,8 @@ __global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* _
     return;
   }
   const int minDist = MODE == 2 ? (int)ex[p] : s_min[0];
-  const int thr = max(2 * minDist, 30);  // d > max(2*minDist, 30.0) rejects (exact in integers)
+  // d > max(2*minDist, 30.0) rejects (exact in integers); no key at all: 2 * INT_MAX is not formed
+  const int thr = minDist >= (1 << 30) ? 30 : max(2 * minDist, 30);
   int cnt = 0;
   for (int q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
     const unsigned long long v = has_t ? qkey[q] : ~0ull;
@@ -779,19 +780,24 @@ int lorb_bf_match(lorb_ctx* ctx, int32_t np, const uint8_t* q, const int32_t* q_
   LORB_TRY(check_offsets(ctx, np, q_off, t_off));
   if (np == 0) return LORB_OK;
   const int nq = q_off[np], nt = t_off[np];
-  uint8_t *dq = nullptr, *dt = nullptr;
-  int32_t* o = nullptr;
-  if (nq > 0) LORB_TRY(lorb::upload_t(ctx, S_BF_Q, q, (size_t)nq * 32, &dq));
-  if (nt > 0) LORB_TRY(lorb::upload_t(ctx, S_BF_T, t, (size_t)nt * 32, &dt));
-  LORB_TRY(lorb::scratch_t(ctx, S_BF_OUT0, (size_t)nq * 3 + np, &o));
-  LORB_TRY(lorb_bf_match_dev(ctx, np, dq, q_off, dt, t_off, o, o + nq, o + 2 * nq, o + 3 * nq));
+  // both descriptor sets in one H2D copy, the four outputs in one D2H copy
+  lorb::InPack in(ctx);
+  const int iq = in.add(q, (size_t)nq * 32), it = in.add(t, (size_t)nt * 32);
+  LORB_TRY(in.commit());
+  lorb::OutPack out(ctx);
+  const int io = out.add(sizeof(int32_t) * ((size_t)nq * 3 + np));
+  LORB_TRY(out.alloc());
+  int32_t* o = out.dev<int32_t>(io);
+  LORB_TRY(lorb_bf_match_dev(ctx, np, in.dev<uint8_t>(iq), q_off, in.dev<uint8_t>(it), t_off, o, o + nq, o + 2 * nq,
+                             o + 3 * nq));
+  LORB_TRY(out.fetch());
+  const int32_t* h = out.host<int32_t>(io);
   if (nq > 0) {
-    LORB_HIP(ctx, hipMemcpyAsync(cc_train, o, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
-    LORB_HIP(ctx, hipMemcpyAsync(cc_dist, o + nq, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
-    LORB_HIP(ctx, hipMemcpyAsync(match_train, o + 2 * nq, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+    memcpy(cc_train, h, sizeof(int32_t) * nq);
+    memcpy(cc_dist, h + nq, sizeof(int32_t) * nq);
+    memcpy(match_train, h + 2 * nq, sizeof(int32_t) * nq);
   }
-  LORB_HIP(ctx, hipMemcpyAsync(n_matches, o + 3 * nq, sizeof(int32_t) * np, hipMemcpyDeviceToHost, ctx->stream));
-  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  memcpy(n_matches, h + 3 * nq, sizeof(int32_t) * np);
   return LORB_OK;
 }
 

@@ -38,6 +38,14 @@ struct lorb_ctx {
   size_t pinned_sz = 0;
   // spin_sync's event (no timing)
   hipEvent_t spin_ev = nullptr;
+  // lorb_ctx_ba_solver's solver (destroyed with the ctx)
+  lorb_ba_solver* solver = nullptr;
+  // pinned staging of lorb::InPack / OutPack
+  void* io_in = nullptr;
+  size_t io_in_sz = 0;
+  void* io_out = nullptr;
+  size_t io_out_sz = 0;
+  hipEvent_t io_ev = nullptr;  // the last InPack copy (the staging is rewritten only after it)
 };
 
 namespace lorb {
@@ -130,6 +138,57 @@ int upload_t(lorb_ctx* ctx, int slot, const T* host, size_t count, T** dev) {
   *dev = static_cast<T*>(p);
   return rc;
 }
+
+// Host-array entry points (the per-frame calls a host caller issues, e.g. SearchByProjection on the
+// live tracking path): every input array is packed into ONE pinned staging buffer and moved by ONE
+// host-to-device copy; the outputs live in ONE device block that ONE device-to-host copy brings
+// back into pinned memory.  Usage: InPack::add() per input (before commit), commit() (pack + copy),
+// dev<T>(i) per input; OutPack::add() per output, alloc(), dev<T>(i), fetch() (copy + wait), then
+// host<T>(i).  One of each per ctx is in use at a time (calls on one ctx are serialized).
+class InPack {
+ public:
+  explicit InPack(lorb_ctx* c) : ctx(c) {}
+  int add(const void* host, size_t bytes) {  // returns the part index
+    parts.push_back({host, bytes, total});
+    total += (bytes + 255) & ~size_t(255);
+    return (int)parts.size() - 1;
+  }
+  template <typename T>
+  int add_t(const T* host, size_t count) { return add(host, host ? count * sizeof(T) : 0); }
+  int commit();
+  template <typename T>
+  T* dev(int i) const { return parts[i].bytes ? reinterpret_cast<T*>(static_cast<unsigned char*>(base) + parts[i].off) : nullptr; }
+
+ private:
+  struct Part { const void* host; size_t bytes, off; };
+  lorb_ctx* ctx;
+  std::vector<Part> parts;
+  size_t total = 0;
+  void* base = nullptr;
+};
+class OutPack {
+ public:
+  explicit OutPack(lorb_ctx* c) : ctx(c) {}
+  int add(size_t bytes) {
+    parts.push_back({bytes, total});
+    total += (bytes + 255) & ~size_t(255);
+    return (int)parts.size() - 1;
+  }
+  int alloc();
+  int fetch();  // one D2H copy into pinned memory, then waits for the stream
+  template <typename T>
+  T* dev(int i) const { return reinterpret_cast<T*>(static_cast<unsigned char*>(dbase) + parts[i].off); }
+  template <typename T>
+  const T* host(int i) const { return reinterpret_cast<const T*>(static_cast<const unsigned char*>(hbase) + parts[i].off); }
+
+ private:
+  struct Part { size_t bytes, off; };
+  lorb_ctx* ctx;
+  std::vector<Part> parts;
+  size_t total = 0;
+  void* dbase = nullptr;
+  void* hbase = nullptr;
+};
 
 // brackets one kernel launch with events when ctx->ktime is set
 struct KernelTimer {
@@ -345,5 +404,7 @@ enum {
   S_W0 = 14, S_W1, S_W2, S_W3, S_W4, S_W5, S_W6, S_W7, S_W8, S_W9,
   S_KP = 24,   /* 10 slots: keypoint upload + grid */
   S_WX = 34,   /* 8 slots: windowed-matcher scratch */
-  S_BF_TKEY = 120  /* crossCheck per-train keys: all-ones between calls (the merge resets them) */
+  S_BF_TKEY = 120, /* crossCheck per-train keys: all-ones between calls (the merge resets them) */
+  S_IO_IN = 121,   /* InPack device block */
+  S_IO_OUT = 122   /* OutPack device block */
 };

@@ -112,7 +112,9 @@ __global__ __launch_bounds__(1024) void k_map_append(MapDev m, int n, int kf, Po
     mn = s_min[0];
 #pragma unroll
     for (int w = 1; w < 16; ++w) mn = min(mn, s_min[w]);
-    const int thr = max(2 * mn, 30);  // d > max(2 * minDist, 30.0) rejects (exact in integers)
+    // d > max(2 * minDist, 30.0) rejects (exact in integers); no crossCheck key at all: no
+    // threshold is compared, and 2 * INT_MAX is not formed
+    const int thr = mn == 0x7fffffff ? 30 : max(2 * mn, 30);
 #pragma unroll RA
     for (int u = 0; u < (RM > 0 ? RM : 1 << 30); ++u) {
       const int q = q0 + u;
@@ -325,6 +327,7 @@ struct lorb_map {
   int* pinned = nullptr;
   lorb_ba_plan* plan = nullptr;
   bool plan_ok = false;  // plan built on the current slots (its point offsets serve the compaction)
+  bool broken = false;   // a failed step whose counts could not be re-read: the map is unusable
   std::vector<void*> allocs;
   ~lorb_map() {
     if (prof && prof_n)
@@ -496,6 +499,7 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   lorb_ctx* ctx = M->ctx;
   if (n > M->n_cap) return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints > the map's max_keypoints %d", n, M->n_cap);
   if (n > 0 && (!d_desc || !d_x || !d_y || !d_depth)) return LORB_E_INVALID;
+  if (M->broken) return lorb::set_error(ctx, LORB_E_DEVICE, "the map is unusable after an earlier failed step");
   hipStream_t s = ctx->stream;
   MapDev& m = M->m;
   const int kf = M->t0 + m.W;  // the new keyframe's id
@@ -551,7 +555,17 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   // 5. BA plan of the slid window; its one readback carries the window's live counts too
   const lorb_ba_window_dev w = window_of(M);
   M->plan_ok = false;
-  LORB_TRY(lorb_ba_plan_update_dev(M->plan, &w));
+  if (const int rc = lorb_ba_plan_update_dev(M->plan, &w); rc != LORB_OK) {
+    // the append and the slide have run: the live counts are the device's now, and the next slide
+    // takes h_K as the end of the point-sorted slots -- re-read them, or mark the map unusable
+    if (hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipStreamSynchronize(s) == hipSuccess) {
+      M->h_P = M->pinned[0]; M->h_K = M->pinned[1];
+    } else {
+      M->broken = true;
+    }
+    return rc;
+  }
   M->plan_ok = true;
   LORB_TRY(mark(4));
   lorb::ba_plan_window_counts(M->plan, &M->h_P, &M->h_K);

@@ -1,6 +1,8 @@
 // lorb_runtime.hip -- context, memory and timer entry points of the C-ABI (include/lorb_c.h).
 #include "lorb_internal.h"
 
+#include <algorithm>
+
 namespace lorb {
 
 int set_error(lorb_ctx* ctx, int code, const char* fmt, ...) {
@@ -45,6 +47,48 @@ int upload(lorb_ctx* ctx, int slot, const void* host, size_t bytes, void** dev) 
   if (m.size() == bytes && std::memcmp(m.data(), host, bytes) == 0) return LORB_OK;  // already resident
   LORB_HIP(ctx, hipMemcpyAsync(*dev, host, bytes, hipMemcpyHostToDevice, ctx->stream));
   m.assign(static_cast<const unsigned char*>(host), static_cast<const unsigned char*>(host) + bytes);
+  return LORB_OK;
+}
+
+static int pinned_grow(lorb_ctx* ctx, void** p, size_t* sz, size_t want) {
+  if (*sz >= want) return LORB_OK;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr; *sz = 0;
+  want += want / 4;
+  LORB_HIP(ctx, hipHostMalloc(p, want));
+  *sz = want;
+  return LORB_OK;
+}
+
+int InPack::commit() {
+  if (!total) return LORB_OK;
+  // a call that failed after its commit may have left its copy in flight
+  if (ctx->io_ev) LORB_HIP(ctx, hipEventSynchronize(ctx->io_ev));
+  else LORB_HIP(ctx, hipEventCreateWithFlags(&ctx->io_ev, hipEventDisableTiming));
+  LORB_TRY(pinned_grow(ctx, &ctx->io_in, &ctx->io_in_sz, total));
+  unsigned char* h = static_cast<unsigned char*>(ctx->io_in);
+  for (const Part& p : parts)
+    if (p.bytes) std::memcpy(h + p.off, p.host, p.bytes);
+  LORB_TRY(scratch(ctx, S_IO_IN, total, &base));
+  size_t used = 0;
+  for (const Part& p : parts) used = std::max(used, p.off + p.bytes);
+  LORB_HIP(ctx, hipMemcpyAsync(base, h, used, hipMemcpyHostToDevice, ctx->stream));
+  LORB_HIP(ctx, hipEventRecord(ctx->io_ev, ctx->stream));
+  return LORB_OK;
+}
+
+int OutPack::alloc() {
+  LORB_TRY(scratch(ctx, S_IO_OUT, std::max<size_t>(total, 16), &dbase));
+  LORB_TRY(pinned_grow(ctx, &ctx->io_out, &ctx->io_out_sz, std::max<size_t>(total, 16)));
+  hbase = ctx->io_out;
+  return LORB_OK;
+}
+
+int OutPack::fetch() {
+  size_t used = 0;
+  for (const Part& p : parts) used = std::max(used, p.off + p.bytes);
+  if (used) LORB_HIP(ctx, hipMemcpyAsync(hbase, dbase, used, hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, spin_sync(ctx));
   return LORB_OK;
 }
 
@@ -105,9 +149,14 @@ int lorb_destroy(lorb_ctx* ctx) {
   if (!ctx) return LORB_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->solver) (void)lorb_ba_solver_destroy(ctx->solver);  // its plans use the ctx's stream
+  ctx->solver = nullptr;
   for (int i = 0; i < lorb_ctx::kScratch; i++)
     if (ctx->scratch[i]) (void)hipFree(ctx->scratch[i]);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  if (ctx->io_in) (void)hipHostFree(ctx->io_in);
+  if (ctx->io_out) (void)hipHostFree(ctx->io_out);
+  if (ctx->io_ev) (void)hipEventDestroy(ctx->io_ev);
   for (int i = 0; i < 64; i++)
     if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
   if (ctx->spin_ev) (void)hipEventDestroy(ctx->spin_ev);

@@ -508,29 +508,31 @@ bool lorb::inv4_lu32f(const float* Ain, float* out) {
 namespace {
 using lorb::inv4_lu32f;
 
-int upload_kps(lorb_ctx* ctx, const lorb_keypoints* k, const uint8_t* slot_state, int slot0, KpDev* K,
-               const lorb_frame_params* fp) {
-  const int n = k->n;
-  float *x, *y, *ang, *ur = nullptr;
-  int* oc;
-  uint8_t *desc, *ss;
-  LORB_TRY(lorb::upload_t(ctx, slot0 + 0, k->x, n, &x));
-  LORB_TRY(lorb::upload_t(ctx, slot0 + 1, k->y, n, &y));
-  LORB_TRY(lorb::upload_t(ctx, slot0 + 2, k->angle, n, &ang));
-  LORB_TRY(lorb::upload_t(ctx, slot0 + 3, k->octave, n, &oc));
-  LORB_TRY(lorb::upload_t(ctx, slot0 + 4, k->desc, (size_t)n * 32, &desc));
-  if (k->u_right) LORB_TRY(lorb::upload_t(ctx, slot0 + 5, k->u_right, n, &ur));
+// a frame's keypoints (Frame::mvKeysUn, mDescriptors, slot states) for the host-array entry points:
+// packed into their InPack (one H2D copy for every input), then the device grid built
+struct KpParts {
+  int x, y, ang, oc, desc, ur, ss;
   std::vector<uint8_t> zeros;
-  if (!slot_state) { zeros.assign(n, 0); slot_state = zeros.data(); }
-  LORB_TRY(lorb::upload_t(ctx, slot0 + 6, slot_state, n, &ss));
+};
+void kps_add(lorb::InPack& in, const lorb_keypoints* k, const uint8_t* slot_state, KpParts& p) {
+  const size_t n = (size_t)k->n;
+  p.x = in.add_t(k->x, n); p.y = in.add_t(k->y, n); p.ang = in.add_t(k->angle, n);
+  p.oc = in.add_t(k->octave, n); p.desc = in.add_t(k->desc, n * 32); p.ur = in.add_t(k->u_right, n);
+  if (!slot_state) { p.zeros.assign(n, 0); slot_state = p.zeros.data(); }
+  p.ss = in.add_t(slot_state, n);
+}
+int kps_finish(lorb_ctx* ctx, const lorb::InPack& in, const KpParts& p, int n, int slot0, KpDev* K,
+               const lorb_frame_params* fp) {
+  const float* x = in.dev<float>(p.x);
+  const float* y = in.dev<float>(p.y);
   int *cell_off, *cell_idx, *kp_cell;
   LORB_TRY(lorb::scratch_t(ctx, slot0 + 7, kCells + 1, &cell_off));
   LORB_TRY(lorb::scratch_t(ctx, slot0 + 8, (size_t)std::max(n, 1), &cell_idx));
   LORB_TRY(lorb::scratch_t(ctx, slot0 + 9, (size_t)std::max(n, 1), &kp_cell));
   hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, ctx->stream, x, y, n, *fp, cell_off, cell_idx, kp_cell);
   LORB_CHECK_LAUNCH(ctx);
-  K->x = x; K->y = y; K->angle = ang; K->uR = ur; K->octave = oc;
-  K->desc = reinterpret_cast<const uint4*>(desc); K->slot_state = ss;
+  K->x = x; K->y = y; K->angle = in.dev<float>(p.ang); K->uR = in.dev<float>(p.ur); K->octave = in.dev<int>(p.oc);
+  K->desc = in.dev<const uint4>(p.desc); K->slot_state = in.dev<uint8_t>(p.ss);
   K->cell_off = cell_off; K->cell_idx = cell_idx; K->n = n;
   return LORB_OK;
 }
@@ -550,21 +552,21 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
     if (pts->track_in_view[i] && !(pts->is_bad && pts->is_bad[i]) &&
         (pts->pred_level[i] < 0 || pts->pred_level[i] >= LORB_MAX_LEVELS))
       return lorb::set_error(ctx, LORB_E_INVALID, "point %d: predicted level %d out of range", i, pts->pred_level[i]);
+  // every input in one H2D copy, the result in one D2H copy
+  lorb::InPack in(ctx);
+  KpParts kp;
+  kps_add(in, kps, slot_state, kp);
+  const int i_iv = in.add_t(pts->track_in_view, np), i_bad = in.add_t(pts->is_bad, np), i_lk = in.add_t(pts->locked, np),
+            i_px = in.add_t(pts->proj_x, np), i_py = in.add_t(pts->proj_y, np), i_pxr = in.add_t(pts->proj_xr, np),
+            i_pl = in.add_t(pts->pred_level, np), i_vc = in.add_t(pts->view_cos, np),
+            i_pd = in.add_t(pts->desc, (size_t)np * 32);
+  LORB_TRY(in.commit());
   KpDev K;
-  LORB_TRY(upload_kps(ctx, kps, slot_state, S_KP, &K, frame));
-  uint8_t *iv, *bad = nullptr, *lk;
-  float *px, *py, *pxr, *vc;
-  int* pl;
-  uint8_t* pd;
-  LORB_TRY(lorb::upload_t(ctx, S_W0, pts->track_in_view, np, &iv));
-  if (pts->is_bad) LORB_TRY(lorb::upload_t(ctx, S_W1, pts->is_bad, np, &bad));
-  LORB_TRY(lorb::upload_t(ctx, S_W2, pts->locked, np, &lk));
-  LORB_TRY(lorb::upload_t(ctx, S_W3, pts->proj_x, np, &px));
-  LORB_TRY(lorb::upload_t(ctx, S_W4, pts->proj_y, np, &py));
-  LORB_TRY(lorb::upload_t(ctx, S_W5, pts->proj_xr, np, &pxr));
-  LORB_TRY(lorb::upload_t(ctx, S_W6, pts->pred_level, np, &pl));
-  LORB_TRY(lorb::upload_t(ctx, S_W7, pts->view_cos, np, &vc));
-  LORB_TRY(lorb::upload_t(ctx, S_W8, pts->desc, (size_t)np * 32, &pd));
+  LORB_TRY(kps_finish(ctx, in, kp, nk, S_KP, &K, frame));
+  const uint8_t *iv = in.dev<uint8_t>(i_iv), *bad = in.dev<uint8_t>(i_bad), *lk = in.dev<uint8_t>(i_lk);
+  const float *px = in.dev<float>(i_px), *py = in.dev<float>(i_py), *pxr = in.dev<float>(i_pxr), *vc = in.dev<float>(i_vc);
+  const int* pl = in.dev<int>(i_pl);
+  const uint8_t* pd = in.dev<uint8_t>(i_pd);
   WinParams P{};
   P.fp = *frame;
   P.th = th;
@@ -573,7 +575,10 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 1, (size_t)np + 1, &off));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 2, (size_t)np + 1, &res));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 3, (size_t)nk + 1, &claim));
-  LORB_TRY(lorb::scratch_t(ctx, S_WX + 4, (size_t)nk + 2, &dassign));
+  lorb::OutPack out(ctx);
+  const int o_as = out.add(sizeof(int) * ((size_t)nk + 1));
+  LORB_TRY(out.alloc());
+  dassign = out.dev<int>(o_as);
   dnm = dassign + nk;
   const unsigned g = lorb::ceil_div(std::max(np, 1), kCandWaves);
   if (np > 0) {
@@ -591,9 +596,9 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
                      (const float*)nullptr, (const float*)nullptr, res, claim, dassign, (int*)nullptr, (int*)nullptr, dnm,
                      (int)(resolve_lds_bytes(np, nk) > 0));
   LORB_CHECK_LAUNCH(ctx);
-  LORB_HIP(ctx, hipMemcpyAsync(assign, dassign, sizeof(int) * nk, hipMemcpyDeviceToHost, ctx->stream));
-  LORB_HIP(ctx, hipMemcpyAsync(nmatches, dnm, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  LORB_TRY(out.fetch());
+  memcpy(assign, out.host<int>(o_as), sizeof(int) * nk);
+  *nmatches = out.host<int>(o_as)[nk];
   return LORB_OK;
 }
 
@@ -626,26 +631,31 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
   const float tlc2 = (float)(s2 + (double)L[11]);
   P.mode_forward = tlc2 > cur->b;
   P.mode_backward = -tlc2 > cur->b;
+  // every input in one H2D copy, the result in one D2H copy
+  lorb::InPack in(ctx);
+  KpParts kp;
+  kps_add(in, cur_kps, cur_slot_state, kp);
+  const int i_hm = in.add_t(last->has_mp, nl), i_ol = in.add_t(last->outlier, nl), i_lk = in.add_t(last->mp_locked, nl),
+            i_pos = in.add_t(last->mp_pos, (size_t)nl * 3), i_ld = in.add_t(last->mp_desc, (size_t)nl * 32),
+            i_lo = in.add_t(last->octave, nl), i_la = in.add_t(last->angle, nl);
+  LORB_TRY(in.commit());
   KpDev K;
-  LORB_TRY(upload_kps(ctx, cur_kps, cur_slot_state, S_KP, &K, cur));
-  uint8_t *hm, *ol = nullptr, *lk, *ld;
-  float *pos, *la;
-  int* lo;
-  LORB_TRY(lorb::upload_t(ctx, S_W0, last->has_mp, nl, &hm));
-  if (last->outlier) LORB_TRY(lorb::upload_t(ctx, S_W1, last->outlier, nl, &ol));
-  LORB_TRY(lorb::upload_t(ctx, S_W2, last->mp_locked, nl, &lk));
-  LORB_TRY(lorb::upload_t(ctx, S_W3, last->mp_pos, (size_t)nl * 3, &pos));
-  LORB_TRY(lorb::upload_t(ctx, S_W4, last->mp_desc, (size_t)nl * 32, &ld));
-  LORB_TRY(lorb::upload_t(ctx, S_W5, last->octave, nl, &lo));
-  LORB_TRY(lorb::upload_t(ctx, S_W6, last->angle, nl, &la));
+  LORB_TRY(kps_finish(ctx, in, kp, nk, S_KP, &K, cur));
+  const uint8_t *hm = in.dev<uint8_t>(i_hm), *ol = in.dev<uint8_t>(i_ol), *lk = in.dev<uint8_t>(i_lk),
+                *ld = in.dev<uint8_t>(i_ld);
+  const float *pos = in.dev<float>(i_pos), *la = in.dev<float>(i_la);
+  const int* lo = in.dev<int>(i_lo);
   int *cnt, *off, *res, *claim, *dassign, *dnm, *bins, *nulls;
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 0, (size_t)nl + 1, &cnt));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 1, (size_t)nl + 1, &off));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 2, (size_t)nl + 1, &res));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 3, (size_t)nk + 1, &claim));
-  LORB_TRY(lorb::scratch_t(ctx, S_WX + 4, (size_t)nk + 2, &dassign));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 5, (size_t)nl + 1, &bins));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 6, (size_t)nk + 1, &nulls));
+  lorb::OutPack out(ctx);
+  const int o_as = out.add(sizeof(int) * ((size_t)nk + 1));
+  LORB_TRY(out.alloc());
+  dassign = out.dev<int>(o_as);
   dnm = dassign + nk;
   const unsigned g = lorb::ceil_div(std::max(nl, 1), kCandWaves);
   if (nl > 0) {
@@ -663,9 +673,9 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
                      la, K.angle, res, claim, dassign, bins, nulls, dnm,
                      (int)(resolve_lds_bytes(nl, nk) > 0));
   LORB_CHECK_LAUNCH(ctx);
-  LORB_HIP(ctx, hipMemcpyAsync(assign, dassign, sizeof(int) * nk, hipMemcpyDeviceToHost, ctx->stream));
-  LORB_HIP(ctx, hipMemcpyAsync(nmatches, dnm, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
-  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  LORB_TRY(out.fetch());
+  memcpy(assign, out.host<int>(o_as), sizeof(int) * nk);
+  *nmatches = out.host<int>(o_as)[nk];
   return LORB_OK;
 }
 

@@ -20,11 +20,13 @@ def point_ranges(win, world):
 
 
 def shard_window(win, rank, world):
-    """This rank's shard: same poses, its point range (re-indexed from 0) and their observations
-    (original relative order kept)."""
+    """This rank's shard: same poses, its point range (re-indexed from 0) and their observations,
+    sorted by point (stably: a point's observations keep their relative order), so that the
+    device-built plan takes its sorted path (k_db_sorted, no counting sort) every step."""
     a, b = point_ranges(win, world)[rank]
     op = np.asarray(win["obs_point"])
-    sel = (op >= a) & (op < b)
+    sel = np.flatnonzero((op >= a) & (op < b))
+    sel = sel[np.argsort(op[sel], kind="stable")]
     out = dict(win)
     out["point_init"] = np.ascontiguousarray(win["point_init"][a:b])
     out["obs_point"] = np.ascontiguousarray(op[sel] - a, dtype=np.int32)

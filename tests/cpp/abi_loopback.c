@@ -8,8 +8,10 @@
 
 #include "../../oracle/lorb_oracle.h"
 
+struct lorb_ba_solver;
 struct lorb_ctx {
   int device;
+  struct lorb_ba_solver* solver; /* lorb_ctx_ba_solver's, freed with the ctx */
 };
 
 int lorb_create(int device, lorb_ctx** out) {
@@ -21,6 +23,7 @@ int lorb_create(int device, lorb_ctx** out) {
 }
 
 int lorb_destroy(lorb_ctx* ctx) {
+  if (ctx) free(ctx->solver);
   free(ctx);
   return LORB_OK;
 }
@@ -92,6 +95,16 @@ int lorb_ba_solver_solve(lorb_ba_solver* s, const lorb_ba_window* w, const lorb_
 
 int lorb_ba_solver_destroy(lorb_ba_solver* s) {
   free(s);
+  return LORB_OK;
+}
+
+int lorb_ctx_ba_solver(lorb_ctx* ctx, lorb_ba_solver** out) {
+  if (!ctx || !out) return LORB_E_INVALID;
+  if (!ctx->solver) {
+    const int rc = lorb_ba_solver_create(ctx, &ctx->solver);
+    if (rc != LORB_OK) return rc;
+  }
+  *out = ctx->solver;
   return LORB_OK;
 }
 

@@ -134,6 +134,27 @@ def test_local_ba_dense_covisibility(ctx, n_kf, n_pts):
     assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
 
 
+@pytest.mark.parametrize("obs_len,kind", [(2, 1), (3, 2), (8, 2)])
+def test_local_ba_narrow_band(ctx, obs_len, kind):
+    """Points seen by obs_len consecutive KFs: band 6*obs_len - 1 (11, 17, 47).  The two-sided
+    Cholesky's back-substitution needs the full inverse of each 16 x 16 diagonal block, which the
+    band holds only for bw >= 15, so a band of 11 takes k_ba_chol_w (kind 1)."""
+    from lorb_slam_amd.runtime import BAPlan
+    w = synth.ba_window(seed=23, n_kf=30, n_pts=1500, n_fixed=2, fixed_obs_per_kf=100, obs_lens=(obs_len,))
+    opt = A.LMOptions.default(max_num_iterations=8, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    plan = BAPlan(ctx, [w])
+    plan.solve(opt)
+    (Pg,), (Xg,), (sg,) = plan.read()
+    info = plan.info()
+    plan.close()
+    Po, Xo, so = O.ba_local([w], opt)
+    assert info["band"] == 6 * obs_len - 1 and info["cholesky"] == kind, info
+    assert sg["iterations"] == so[0]["iterations"]
+    lm_match(sg, so[0])
+    assert close(Pg, Po[0]), np.abs(Pg - Po[0]).max()
+    assert close(Xg, Xo[0]), np.abs(Xg - Xo[0]).max()
+
+
 def test_local_ba_c4_full_size(ctx):
     """BASELINE config 3 (the bench workload): 50 KF / 10k points / 77k obs (+5 fixed KFs), 10 LM its,
     at full size against the oracle."""

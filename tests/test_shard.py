@@ -18,7 +18,12 @@ def test_partition_covers_points_once_and_keeps_observations(world):
         assert np.array_equal(s["point_init"], w["point_init"][a:b])
         assert s["obs_point"].min(initial=0) >= 0 and s["obs_point"].max(initial=-1) < b - a
         assert np.array_equal(s["pose_init"], w["pose_init"]) and np.array_equal(s["fixed_pose"], w["fixed_pose"])
-        sel = (w["obs_point"] >= a) & (w["obs_point"] < b)
+        # the shard's observations are the point range's, sorted by point, stably (a point's
+        # observations keep their relative order): what the device plan's sorted path takes
+        sel = np.flatnonzero((w["obs_point"] >= a) & (w["obs_point"] < b))
+        sel = sel[np.argsort(w["obs_point"][sel], kind="stable")]
+        assert np.all(np.diff(s["obs_point"]) >= 0)
+        assert np.array_equal(s["obs_point"], w["obs_point"][sel] - a)
         assert np.array_equal(s["obs_frame"], w["obs_frame"][sel]) and np.array_equal(s["obs_uv"], w["obs_uv"][sel])
     if world > 1:
         nobs = [len(s["obs_point"]) for s in shards]

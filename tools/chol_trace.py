@@ -28,7 +28,7 @@ print("bottom update:")
 for p, e in enumerate(upd(160, 8)): print("  ", p, e)
 names = ["w2 T done", "w2 got X", "w3 X written", "w0 M start", "w0 M done", "w0 bs start", "w0 bs M done",
          "w0 bs T done", "stage top done", "stage bot done", "linv top done", "linv bot done", "w1 bs B done", "end",
-         "w2 combined", "w2 M handed"]
+         "w2 combined", "w2 M handed", "K top start", "K top done", "K bot start", "K bot done"]
 for k, nm in enumerate(names): print(f"{nm:16s} {v[200 + k]}")
 plan.close()
 print("linv top (start, end):", [(v[256 + 2 * p], v[257 + 2 * p]) for p in range(8)])

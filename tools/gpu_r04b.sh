@@ -1,0 +1,12 @@
+#!/bin/bash
+# r04: back-substitution operators (LORB_BSK): BA parity tests, Cholesky trace, timings vs the r03 build
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 1
+O=$R/gpurun_out; mkdir -p $O
+tools/gpu_step.sh 400 $O/b_tests.log python -u -m pytest tests/test_gpu_ba.py tests/test_gpu_solver.py tests/test_gpu_map.py tests/test_gpu_shard.py -m gpu -x -q --timeout 120 --timeout-method thread || exit $?
+LORB_LIB_PATH=$R/lorb_slam_amd/liblorb_trace.so tools/gpu_step.sh 120 $O/b_trace.log python tools/chol_trace.py || exit $?
+for k in 1 2; do
+tools/gpu_step.sh 200 $O/b_tba_new$k.log python tools/time_ba.py || exit $?
+LORB_LIB_PATH=$R/lorb_slam_amd/liblorb_base.so tools/gpu_step.sh 200 $O/b_tba_old$k.log python tools/time_ba.py || exit $?
+done
+tools/gpu_step.sh 120 $O/b_iolat.log tools/micro/io_lat || exit $?
