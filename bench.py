@@ -513,7 +513,9 @@ def workload_shared(ctx, args, rank, D, comm):
     bw = 6 * 8 - 1
     kspec = {
         2: ("hbm", opt_obs * 36 * 8.0 + (6 * 50) * (bw + 1) * 8.0, "GB/s"),
-        3: ("hbm", len(sh["obs_point"]) * (20 * 8.0 + 16 + 8), "GB/s"),
+        # k_ba_lin with the point-block prep fused in: the C4 figure of workload_c4 (34 doubles
+        # written per observation, uv + three structure indices read; X read per point)
+        3: ("hbm", len(sh["obs_point"]) * (34 * 8.0 + 16 + 12) + len(sh["point_init"]) * 24.0, "GB/s"),
         4: ("fp64", (6 * 50) * bw * bw + 4.0 * (6 * 50) * bw, "TFLOP/s"),
     }
     # whole-job units: the shared window's iterations / matches are counted once (rank 0 only)

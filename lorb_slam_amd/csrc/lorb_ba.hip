@@ -885,6 +885,7 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_fail;
   __shared__ __attribute__((aligned(16))) double s_col[80];
+  __shared__ double s_l[NB][NB + 1], s_zk[NB], s_y[NB];  // a factored panel's diagonal block (extra rows)
   const int w = blockIdx.x;
   if (d.st[w].done) return;
   if (d.sharded && d.wfail[w] > 0.0) {  // a rank's point block was not PD: the step is invalid
@@ -1024,6 +1025,43 @@ __global__ __launch_bounds__(256) void k_ba_chol(BaDev d) {
           }
           z[row] = zr[r];
         }
+      }
+      // Rows below the register panel (bw + NB > 64 RPL: a dense window of more than ~80 cameras):
+      // the panel's column operations replayed 64 rows at a time from its diagonal block (L(kb+q2,
+      // kb+q) in lane q2's P[0][q], z_k in lane q's zr[0], 1 / L(k, k) in invd) -- per row the same
+      // operations in the same order as a register row's.
+      if (!bad && kb + 64 * RPL <= rlast) {
+        const int nq = ke - kb;
+        if (lane < NB) {
+#pragma unroll
+          for (int q = 0; q < NB; ++q) s_l[lane][q] = P[0][q];
+          s_zk[lane] = zr[0];
+          s_y[lane] = lane < nq ? invd[kb + lane] : 0.0;
+        }
+        wave_sync_lds();
+        for (int r0 = kb + 64 * RPL; r0 <= rlast; r0 += 64) {
+          const int row = r0 + lane;
+          const bool vr = row <= rlast;
+          double X[NB], zx = vr ? z[row] : 0.0;
+#pragma unroll
+          for (int q = 0; q < NB; ++q) X[q] = (vr && q < nq && row - (kb + q) <= bw) ? band(A, bw, row, kb + q) : 0.0;
+#pragma unroll
+          for (int q = 0; q < NB; ++q) {
+            if (q < nq) {
+              X[q] *= s_y[q];
+              zx = fma(-X[q], s_zk[q], zx);
+#pragma unroll
+              for (int q2 = q + 1; q2 < NB; ++q2) X[q2] = fma(-X[q], s_l[q2][q], X[q2]);
+            }
+          }
+          if (vr) {
+#pragma unroll
+            for (int q = 0; q < NB; ++q)
+              if (q < nq && row - (kb + q) <= bw) band(A, bw, row, kb + q) = X[q];
+            z[row] = zx;
+          }
+        }
+        wave_sync_lds();
       }
       if (bad && lane == 0) s_fail = 1;
     }
@@ -1585,6 +1623,197 @@ struct BandSide {
       const_cast<BandSide*>(this)->tslot += 4;
     }
   }
+  // LORB_CHAIN_DELTA: the lookahead split with the next column block's update on the CHAIN wave.
+  // Panel p's own contribution to the next column block, D = L_p(rows) L_p(kb+16 .. kb+31)^T, is
+  // accumulated by the chain in its factor loop -- one rank-1 VALU update per column, multipliers read
+  // back from colbuf a column late (as mp), issued in the latency gaps of the pivot chain.  The update
+  // wave hands over the next column block with the EARLIER panels' contributions at the start of its
+  // iteration (it no longer waits for this panel's L), so at the end of the panel the next panel is
+  // pb - D (D shifted up 16 rows through pb) with no hand-over on the critical path; the update wave
+  // applies L_p to the two column blocks after it (and to all three on a phase's last panel, whose
+  // window the M combine reads).  L goes to the band inside the column loop.
+  //   ord: the update wave has read its operands of the previous panel's L (the chain may overwrite
+  //   colbuf); pbr: the chain has read pb (the update wave may rewrite it).
+  __device__ __forceinline__ void chain_d(double (&P)[NB], double& zr, bool& bad, int kb0, int kend, bool pre,
+                                          int* lrd, int* prd, int* ord, int* pbr, int& pwant, int& owant,
+                                          double* pb) const {
+    const int dstep = 16 * (si + sj);
+    unsigned l_ok = 0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) l_ok |= (unsigned)(q <= lane && lane - q <= bw) << q;
+    int l_base = idx(kb0 + lane, kb0);
+    double* colbuf = xch;
+    double* dummy = xch + 16 * kCS + lane;
+    if (!pre) {  // the phase's first panel from pb
+      wait_ge<false>(prd, ++pwant);
+#pragma unroll
+      for (int q = 0; q < NB; ++q) P[q] = pb[lane * 17 + q];
+      wave_sync_lds();
+      if (lane == 0) __hip_atomic_fetch_add(pbr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    for (int kb = kb0; kb < kend; kb += 16) {
+      int lane = this->lane, lok = (int)l_ok;
+      asm volatile("" : "+v"(lane), "+v"(lok));
+      const bool nxt = kb + 16 < kend, first = pre && kb == kb0;
+      tr(0);
+      const double zin = kb + 16 + lane < rows ? z[kb + 16 + lane] : 0.0;
+      const bool rowvalid = kb + lane < rows;
+      double yq = 0.0;
+      double mp[NB], md[NB], dl[NB];
+#pragma unroll
+      for (int q2 = 0; q2 < NB; ++q2) { mp[q2] = 0.0; md[q2] = 0.0; dl[q2] = 0.0; }
+      double akk = readlane_d(P[0], 0);
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        bad |= !(akk > 0.0);
+        double y = __builtin_amdgcn_rsq(akk);
+        __builtin_amdgcn_sched_barrier(0);
+        if (q >= 1) {
+#pragma unroll
+          for (int q2 = q + 1; q2 < NB; ++q2) P[q2] = fma(-P[q - 1], mp[q2], P[q2]);
+#pragma unroll
+          for (int c = 0; c < NB; ++c) {
+            dl[c] = fma(P[q - 1], md[c], dl[c]);  // column q-1 into D
+            // pinned here: otherwise the FMAs sink to D's use after the loop and all 16 columns'
+            // multipliers stay live (spills)
+            asm volatile("" : "+v"(dl[c]));
+          }
+        }
+        {
+          const double e = fma(-akk * y, y, 1.0);
+          y = fma(0.5 * y, e, y);
+        }
+        P[q] *= y;  // lane q: akk * y = L(k, k)
+        yq = lane == q ? y : yq;
+        const double zk = readlane_d(zr, q) * y;
+        zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
+        if (q == 0 && !first) wait_ge<false>(ord, ++owant);  // colbuf free (previous L consumed)
+        colbuf[q * kCS + lane] = P[q];
+        {  // L column q into the band (its diagonal slot holds 1 / L(k, k))
+          const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
+          *(ok ? A + l_base + q * sj : dummy) = q == lane ? y : P[q];
+        }
+        if (q + 1 < NB) {
+          const double l1 = readlane_d(P[q], q + 1);
+          P[q + 1] = fma(-P[q], l1, P[q + 1]);
+          akk = readlane_d(P[q + 1], q + 1);
+#pragma unroll
+          for (int q2 = q + 2; q2 < NB; ++q2) mp[q2] = colbuf[q * kCS + q2];
+        }
+#pragma unroll
+        for (int c = 0; c < NB; ++c) md[c] = colbuf[q * kCS + 16 + c];  // L(kb + 16 + c, kb + q)
+      }
+#pragma unroll
+      for (int c = 0; c < NB; ++c) dl[c] = fma(P[NB - 1], md[c], dl[c]);
+      tr(1);
+      // L is complete in colbuf: post it, then the next panel = pb - D
+      if (lane == 0) __hip_atomic_fetch_add(lrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (nxt) {
+        wait_ge<false>(prd, ++pwant);
+        double Pn[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) Pn[q] = pb[lane * 17 + q];
+        wave_sync_lds();
+        if (lane >= 16) {
+#pragma unroll
+          for (int c = 0; c < NB; ++c) pb[(lane - 16) * 17 + c] = dl[c];
+        }
+        wave_sync_lds();
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+          const double dv = pb[(lane < 48 ? lane : 0) * 17 + c];
+          P[c] = Pn[c] - (lane < 48 ? dv : 0.0);  // rows kb+64 .. kb+79 enter untouched
+        }
+        wave_sync_lds();
+        if (lane == 0) __hip_atomic_fetch_add(pbr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      l_base += dstep;
+      if (lane < NB) z[kb + lane] = zr;
+      if (lane == 0 && pdone) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const double zs = __shfl_down(zr, 16, 64);
+      zr = lane < 48 ? zs : zin;
+      tr(2);
+      const_cast<BandSide*>(this)->tslot += 3;
+    }
+  }
+  //   update_d(): the update wave of chain_d.  pre_u: the phase's first hand-over needs no pb
+  //   release (the chain's first panel did not come from pb).
+  __device__ __forceinline__ void update_d(v4d (&T)[10], int kb0, int kend, int* lrd, int* prd, int* ord, int* pbr,
+                                           int& lwant, int& bwant, double* pb, bool pre_u) const {
+    const int ci = lane & 15, ck = lane >> 4;
+    const int dstep = 16 * (si + sj);
+    int tn_addr = idx(kb0 + 64 + ck, kb0 + 16 + ci);
+    unsigned tn_ok = 0;
+#pragma unroll
+    for (int J = 0; J < 4; ++J)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 64 + ck + 4 * r, j = 16 + 16 * J + ci;
+        tn_ok |= (unsigned)(j <= i && i - j <= bw) << (4 * J + r);
+      }
+    for (int kb = kb0; kb < kend; kb += 16) {
+      int tok = (int)tn_ok;
+      asm volatile("" : "+v"(tok));
+      if (mask) {
+        const int b = dir > 0 ? kb / 16 + 4 : nbk - 5 - kb / 16;
+        if (b >= 0 && b < nbk) wait_bit(mask, b);
+      }
+      v4d Tn[4];
+#pragma unroll
+      for (int J = 0; J < 4; ++J)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = (((unsigned)tok >> (4 * J + r)) & 1u) && kb + 64 + ck + 4 * r < rows;
+          const double v = A[ok ? tn_addr + 4 * r * si + 16 * J * sj : base];
+          Tn[J][r] = ok ? v : 0.0;
+        }
+      tn_addr += dstep;
+      const bool nxt = kb + 16 < kend;
+      tr(0);
+      if (nxt) {  // the next panel's column with the earlier panels' contributions
+        if (!(pre_u && kb == kb0)) wait_ge<true>(pbr, ++bwant);
+#pragma unroll
+        for (int I = 1; I < 4; ++I)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pb[(16 * (I - 1) + ck + 4 * r) * 17 + ci] = T[tri4(I, 1)][r];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pb[(48 + ck + 4 * r) * 17 + ci] = Tn[0][r];
+        if (lane == 0) __hip_atomic_fetch_add(prd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      wait_ge<true>(lrd, ++lwant);
+      tr(1);
+      double opA[4][4];
+#pragma unroll
+      for (int I = 1; I < 4; ++I)
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          opA[I][kk] = xch[(4 * kk + ck) * kCS + 16 * I + ci];  // L(kb + 16 I + ci, kb + 4 kk + ck)
+      wave_sync_lds();
+      if (lane == 0) __hip_atomic_fetch_add(ord, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      tr(2);
+      if (!nxt) {  // the phase's last panel: its window (read by the M combine / the M phase) in full
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int I = 1; I < 4; ++I)
+            T[tri4(I, 1)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[1][kk], T[tri4(I, 1)], 0, 0, 0);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int J = 2; J < 4; ++J)
+#pragma unroll
+          for (int I = J; I < 4; ++I)
+            T[tri4(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[J][kk], T[tri4(I, J)], 0, 0, 0);
+      T[tri4(0, 0)] = T[tri4(1, 1)];
+      T[tri4(1, 0)] = T[tri4(2, 1)]; T[tri4(1, 1)] = T[tri4(2, 2)];
+      T[tri4(2, 0)] = T[tri4(3, 1)]; T[tri4(2, 1)] = T[tri4(3, 2)]; T[tri4(2, 2)] = T[tri4(3, 3)];
+#pragma unroll
+      for (int J = 0; J < 4; ++J) T[tri4(3, J)] = Tn[J];
+      tr(3);
+      const_cast<BandSide*>(this)->tslot += 4;
+    }
+  }
   // The 16 x 16 diagonal block of L at view rows c0 .. c0+15 replaced in place by its inverse X
   // (lower triangular; the diagonal slot already holds 1 / L(i, i) = X(i, i)):
   // X(i, j) = -X(i, i) sum_{k=j}^{i-1} L(i, k) X(k, j).  Only the back-substitution reads the
@@ -1877,6 +2106,10 @@ constexpr int kChol2sThreads = 512;
 #ifndef LORB_BSK
 #define LORB_BSK 1
 #endif
+// 1: the next column block's update on the chain wave (BandSide::chain_d / update_d)
+#ifndef LORB_CHAIN_DELTA
+#define LORB_CHAIN_DELTA 0
+#endif
 // LDS words of k_ba_chol_2s: band (n16 rows), both sides' rhs (n16 + 48), two 64 x 18 exchanges
 // (together the 48 x 48 combine), zX (48), two 64 x 17 panel hand-off buffers, a zero word
 __host__ __device__ constexpr int chol2s_words(int n16, int bw) {
@@ -1902,8 +2135,15 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   const int done = S0.done;
   const double wfail = d.sharded ? d.wfail[w] : 0.0;
   if (done) return;
-  if (wfail > 0.0) {
-    if (threadIdx.x == 0) d.st[w].chol_fail = 1;
+  if (wfail > 0.0) {  // a rank's point block was not PD: the step is invalid
+    if (HEAD) {       // the fused sharded iteration's head still runs (it advances the iteration)
+      if (threadIdx.x < 64) {
+        const WinState S = lm_head<true>(d, o, w, threadIdx.x, S0, W);
+        if (threadIdx.x == 0 && !S.done) d.st[w].chol_fail = 1;
+      }
+    } else if (threadIdx.x == 0) {
+      d.st[w].chol_fail = 1;
+    }
     return;
   }
   constexpr int NT = kChol2sThreads;
@@ -1930,6 +2170,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   __shared__ int s_pdone[2];
   __shared__ int s_linv[2];           // diagonal-block inverses done, per side (LORB_BSK)
   __shared__ int s_lrd[2], s_prd[2];  // per side: L panels posted (chain), panel columns posted (update)
+  __shared__ int s_ord[2], s_pbr[2];  // per side (LORB_CHAIN_DELTA): L operands read (update), pb read (chain)
   __shared__ int s_hand[3];           // T / B -> M hand-over (below)
   const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
   const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
@@ -1968,6 +2209,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     s_pdone[0] = 0; s_pdone[1] = 0;
     s_linv[0] = 0; s_linv[1] = 0;
     s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
+    s_ord[0] = 0; s_ord[1] = 0; s_pbr[0] = 0; s_pbr[1] = 0;
     s_hand[0] = 0; s_hand[1] = 0; s_hand[2] = 0;
     unsigned long long msk = 0;
     for (int b = 0; b < nbk; ++b) msk |= (unsigned long long)(!prog || b < ib || b >= nbk - ib) << (b & 63);
@@ -2008,6 +2250,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   int* lrd = &s_lrd[side];
   int* prd = &s_prd[side];
   int lwant = 0, pwant = 0;
+  [[maybe_unused]] int owant = 0, bwant = 0;  // LORB_CHAIN_DELTA
   bool bad = false;
   double zr = 0.0;
   double P[NB];
@@ -2036,7 +2279,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     TR1(8 + side);
   }
   if (HEAD && wv == 4) {  // the iteration head while the first panels factor
-    const WinState S = lm_head<false>(d, o, w, lane, S0, W);
+    const WinState S = d.sharded ? lm_head<true>(d, o, w, lane, S0, W) : lm_head<false>(d, o, w, lane, S0, W);
     if (lane == 0) s_head_done = S.done;
   }
   // diagonal-block inverses (waves 4 / 5; on waves 6 / 7 after their staging, off the chain waves'
@@ -2060,10 +2303,18 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     unsigned long long* phv = d.dbg + 8 * w;  // wave 0, T phase: [0] wait [1] factor [2] store
     if (wv == 0) { if (lane == 0) { phv[0] = phv[1] = phv[2] = 0; } const_cast<BandSide&>(me).phases = phv; }
 #endif
+#if LORB_CHAIN_DELTA
+    me.chain_d(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, &s_ord[side], &s_pbr[side], pwant, owant, pb);
+#else
     me.chain(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, pwant, pb);
+#endif
   } else if (wv < 4) {
     me.init_tiles(T);
+#if LORB_CHAIN_DELTA
+    me.update_d(T, 0, side == 0 ? m : nB, lrd, prd, &s_ord[side], &s_pbr[side], lwant, bwant, pb, true);
+#else
     me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb);
+#endif
   }
   if (wv < 6) C2_STAMP(wv);
 #if LORB_BSK
@@ -2141,13 +2392,21 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
       if (lane == 0) __hip_atomic_fetch_add(&s_prd[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     TR1(15);
+#if LORB_CHAIN_DELTA
+    topM.update_d(T, m, m + 48, &s_lrd[0], &s_prd[0], &s_ord[0], &s_pbr[0], lwant, bwant, pbt, false);
+#else
     topM.update(T, m, m + 48, &s_lrd[0], &s_prd[0], lwant, pbt);
+#endif
   } else if (wv == 0) {
     zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
     BandSide topM = top;
     topM.mask = nullptr; topM.pdone = nullptr;
     TR1(3);
+#if LORB_CHAIN_DELTA
+    topM.chain_d(P, zr, bad, m, m + 48, false, &s_lrd[0], &s_prd[0], &s_ord[0], &s_pbr[0], pwant, owant, pbt);
+#else
     topM.chain(P, zr, bad, m, m + 48, false, &s_lrd[0], &s_prd[0], pwant, pbt);
+#endif
     TR1(4);
     if (bad) s_bad = 1;
     C2_STAMP(6);
@@ -2701,6 +2960,9 @@ struct lorb_ba_plan {
   // device-built plans: rhs | wfail | pad | env, the band's size decides n)
   double* x2_send = nullptr;
   double* x2_recv = nullptr;
+  // sharded fused iteration: exchanges 1 and 2 as ONE all-reduce over [lin | pad | solve], which are
+  // contiguous (U_part -> U, fx_n doubles)
+  size_t fx_n = 0;
   size_t x2_off = 0;  // device-built: offset of env after rhs | wfail | pad
   // per window: camera relabelling (input pose index -> plan camera index; RCM order, §8 item 4)
   std::vector<std::vector<int>> cam_map;
@@ -3045,13 +3307,18 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   // exchange buffers (see BaDev); unsharded plans alias *_part to the global buffers
   const size_t W8 = (size_t)nw, lin_n = C * 27 + 2 * W8, solve_n = (size_t)P->env_total + P->n_total + W8;
   double *lin, *linp, *mx, *mxp, *sol, *solp, *stp, *stpp;
-  LORB_TRY(dalloc(P, lin_n, &lin)); LORB_TRY(dalloc(P, W8, &mx));
-  LORB_TRY(dalloc(P, solve_n, &sol)); LORB_TRY(dalloc(P, 3 * W8, &stp));
+  // [lin | pad | solve] in one block (the sharded fused iteration all-reduces both at once; solve
+  // starts 256-byte aligned)
+  const size_t lin_pad = (lin_n + 31) & ~(size_t)31;
+  LORB_TRY(dalloc(P, lin_pad + solve_n, &lin)); LORB_TRY(dalloc(P, W8, &mx));
+  sol = lin + lin_pad;
+  LORB_TRY(dalloc(P, 3 * W8, &stp));
+  P->fx_n = lin_pad + solve_n;
   if (comm) {
-    LORB_TRY(dalloc(P, lin_n, &linp)); LORB_TRY(dalloc(P, W8, &mxp));
-    LORB_TRY(dalloc(P, solve_n, &solp)); LORB_TRY(dalloc(P, 3 * W8, &stpp));
-    LORB_HIP(ctx, hipMemsetAsync(solp, 0, sizeof(double) * solve_n, ctx->stream));
-    LORB_HIP(ctx, hipMemsetAsync(linp, 0, sizeof(double) * lin_n, ctx->stream));
+    LORB_TRY(dalloc(P, lin_pad + solve_n, &linp)); LORB_TRY(dalloc(P, W8, &mxp));
+    solp = linp + lin_pad;
+    LORB_TRY(dalloc(P, 3 * W8, &stpp));
+    LORB_HIP(ctx, hipMemsetAsync(linp, 0, sizeof(double) * (lin_pad + solve_n), ctx->stream));
   } else {
     linp = lin; mxp = mx; solp = sol; stpp = stp;
   }
@@ -3146,7 +3413,7 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
   hipStream_t s = ctx->stream;
   const BaDev& d = P->dev;
   static const bool no_fuse = [] { const char* e = getenv("LORB_NO_FUSE"); return e && e[0] == '1'; }();
-  const bool fused = !first && !P->comm && chol_kind_of(P) == 2 && !no_fuse;
+  const bool fused = !first && chol_kind_of(P) == 2 && !no_fuse;
   if (fused) {
     if (P->grid_pblk) {
       lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
@@ -3165,7 +3432,16 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
     if (fused) hipLaunchKernelGGL(k_ba_schur<true>, dim3(P->grid_bp + P->Ctot), dim3(256), 0, s, d, o, (int)P->grid_bp);
     else hipLaunchKernelGGL(k_ba_schur<false>, dim3(P->grid_bp), dim3(256), 0, s, d, o, (int)P->grid_bp);
   }
-  if (P->comm) {  // exchange 2: reduced camera system, rhs, point-block failure flags
+  if (P->comm && fused) {
+    // the fused sharded iteration: the point partials of the head, then exchanges 1 and 2 as one
+    // sum over the contiguous [U | V | cost, |x|^2 | pad | band | rhs | failure flags] (the band's
+    // camera blocks and the rhs carry -a / -r only: the Cholesky adds the global U sc sc^T + D^2 and
+    // V sc as it stages them) and the gradient max
+    hipLaunchKernelGGL(k_ba_win_reduce<0>, dim3(P->W), dim3(64), 0, s, d);
+    lorb::KernelTimer kt(ctx, LORB_K_ALLREDUCE);
+    LORB_TRY(lorb::comm_allreduce(P->comm, d.U_part, d.U, P->fx_n, LORB_OP_SUM));
+    LORB_TRY(lorb::comm_allreduce(P->comm, d.wmax_part, d.wmax, (size_t)P->W, LORB_OP_MAX));
+  } else if (P->comm) {  // exchange 2: reduced camera system, rhs, point-block failure flags
     lorb::KernelTimer kt(ctx, LORB_K_ALLREDUCE);
     LORB_TRY(lorb::comm_allreduce(P->comm, P->x2_send, P->x2_recv, x2_count(P), LORB_OP_SUM));
   }
@@ -3989,8 +4265,12 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   const size_t n = 6 * C, lin_n = C * 27 + 2, x2_off = (n + 1 + 31) & ~(size_t)31, solve_n = x2_off + n * n;
   lorb_comm* comm = P->comm;
   double *lin, *mx, *sol, *stp;
-  LORB_TRY(dalloc(P, lin_n, &lin)); LORB_TRY(dalloc(P, (size_t)1, &mx));
-  LORB_TRY(dalloc(P, solve_n, &sol)); LORB_TRY(dalloc(P, (size_t)3, &stp));
+  // [lin | pad | solve] in one block, as in build_plan
+  const size_t lin_pad = (lin_n + 31) & ~(size_t)31;
+  LORB_TRY(dalloc(P, lin_pad + solve_n, &lin)); LORB_TRY(dalloc(P, (size_t)1, &mx));
+  sol = lin + lin_pad;
+  LORB_TRY(dalloc(P, (size_t)3, &stp));
+  P->fx_n = lin_pad + solve_n;
   d.U = lin; d.V = lin + C * 21; d.wlin = lin + C * 27; d.wmax = mx;
   d.rhs = sol; d.wfail = sol + n; d.env = sol + x2_off;
   d.wstep = stp;
@@ -3998,10 +4278,10 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   b.sol_n = solve_n;
   if (comm) {  // this rank's partial sums (see BaDev), all-reduced into the global buffers
     double *linp, *mxp, *solp, *stpp;
-    LORB_TRY(dalloc(P, lin_n, &linp)); LORB_TRY(dalloc(P, (size_t)1, &mxp));
-    LORB_TRY(dalloc(P, solve_n, &solp)); LORB_TRY(dalloc(P, (size_t)3, &stpp));
-    LORB_HIP(ctx, hipMemsetAsync(linp, 0, sizeof(double) * lin_n, ctx->stream));
-    LORB_HIP(ctx, hipMemsetAsync(solp, 0, sizeof(double) * solve_n, ctx->stream));
+    LORB_TRY(dalloc(P, lin_pad + solve_n, &linp)); LORB_TRY(dalloc(P, (size_t)1, &mxp));
+    solp = linp + lin_pad;
+    LORB_TRY(dalloc(P, (size_t)3, &stpp));
+    LORB_HIP(ctx, hipMemsetAsync(linp, 0, sizeof(double) * (lin_pad + solve_n), ctx->stream));
     d.U_part = linp; d.V_part = linp + C * 21; d.wlin_part = linp + C * 27; d.wmax_part = mxp;
     d.rhs_part = solp; d.wfail_part = solp + n; d.env_part = solp + x2_off;
     d.wstep_part = stpp;

@@ -133,3 +133,66 @@ def test_solver_fallback_and_errors(ctx):
         check(s, w, OPT10)  # still usable after the errors
     finally:
         s.close()
+
+
+def wide_window(seed, n_kf, n_pts, obs_len, n_fixed=2, fixed_obs=60, fx=435.2, fy=435.2, cx=367.5, cy=252.2):
+    """a long straight window (camera i at (0.1 i, 0, 0), no rotation: every point in front of every
+    camera), each point seen by obs_len consecutive keyframes, and point 0 by ALL of them"""
+    rng = np.random.default_rng(seed)
+    C = np.stack([0.1 * np.arange(-n_fixed, n_kf), np.zeros(n_kf + n_fixed), np.zeros(n_kf + n_fixed)], 1)
+    poses = np.concatenate([np.zeros((n_kf + n_fixed, 3)), -C], 1)  # rows: fixed -n_fixed..-1, then window
+    pts = np.stack([rng.uniform(-6, 0.1 * n_kf + 6, n_pts), rng.uniform(-3, 3, n_pts), rng.uniform(4, 20, n_pts)], 1)
+    obs_p, obs_f = [], []
+    for q in range(n_pts):
+        fr = range(n_kf) if q == 0 else range(s0 := int(rng.integers(0, n_kf - obs_len + 1)), s0 + obs_len)
+        for f in fr:
+            obs_p.append(q); obs_f.append(f)
+    for j in range(n_fixed):
+        for q in np.sort(rng.choice(np.arange(1, n_pts), size=fixed_obs, replace=False)):
+            obs_p.append(q); obs_f.append(-1 - j)
+    obs_p = np.asarray(obs_p, np.int32); obs_f = np.asarray(obs_f, np.int32)
+    row = np.where(obs_f >= 0, n_fixed + obs_f, n_fixed - 1 - (-1 - obs_f))
+    Xc = pts[obs_p] + poses[row, 3:]
+    uv = np.stack([fx * Xc[:, 0] / Xc[:, 2] + cx, fy * Xc[:, 1] / Xc[:, 2] + cy], 1) + rng.normal(0, 0.5, (len(obs_p), 2))
+    pose_init = poses[n_fixed:].copy()
+    pose_init[:, :3] += rng.normal(0, 2e-3, (n_kf, 3))
+    pose_init[:, 3:] += rng.normal(0, 2e-2, (n_kf, 3))
+    return dict(pose_init=pose_init.astype(np.float32), fixed_pose=poses[n_fixed - 1::-1].astype(np.float32).reshape(-1, 6),
+                point_init=(pts + rng.normal(0, 5e-2, pts.shape)).astype(np.float32), obs_point=obs_p, obs_frame=obs_f,
+                obs_uv=uv.astype(np.float32), intr=(np.float32(fx), np.float32(fy), np.float32(cx), np.float32(cy)))
+
+
+def test_solver_kgb_fallback_between_normal_windows(ctx):
+    """a resident plan, then a window with one point observed by 260 cameras (>= kGB = 256
+    observations: the device plan refuses it, LORB_E_UNSUPPORTED -> lorb_ba_local's host-built plan on
+    the same GPU kernels), then the first window again on its resident plan: every result against
+    the oracle, and the failed build leaves no stale plan or scratch behind"""
+    opt = A.LMOptions.default(max_num_iterations=3, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    s = BASolver(ctx)
+    try:
+        a = synth.ba_window(seed=31, n_kf=12, n_pts=900, n_fixed=2, fixed_obs_per_kf=90)
+        check(s, a, opt)
+        big = wide_window(seed=32, n_kf=260, n_pts=1200, obs_len=3)
+        assert int(np.sum(np.asarray(big["obs_point"]) == 0)) == 260
+        check(s, big, opt)
+        assert s.info()["host_plan_fallback"] == 1, s.info()
+        check(s, a, opt)
+        info = s.info()
+        assert info["host_plan_fallback"] == 0 and info["plan_creations"] == 1, info
+    finally:
+        s.close()
+
+
+def test_solver_lru_eviction(ctx):
+    """six camera counts through the four resident plans (least recently used evicted), then the
+    evicted counts again: every call against the oracle"""
+    s = BASolver(ctx)
+    try:
+        wins = [synth.ba_window(seed=40 + k, n_kf=k, n_pts=80 * k, n_fixed=1, fixed_obs_per_kf=30) for k in range(6, 12)]
+        for w in wins + wins[:2]:
+            check(s, w, OPT10)
+        info = s.info()
+        assert info["resident_plans"] == 4 and info["plan_creations"] == 8 and info["host_plan_fallback"] == 0, info
+    finally:
+        s.close()

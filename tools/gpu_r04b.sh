@@ -10,3 +10,6 @@ tools/gpu_step.sh 200 $O/b_tba_new$k.log python tools/time_ba.py || exit $?
 LORB_LIB_PATH=$R/lorb_slam_amd/liblorb_base.so tools/gpu_step.sh 200 $O/b_tba_old$k.log python tools/time_ba.py || exit $?
 done
 tools/gpu_step.sh 120 $O/b_iolat.log tools/micro/io_lat || exit $?
+export TMPDIR=/tmp
+tools/gpu_step.sh 120 $O/b_fc_fetch.log timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $O/fc/fetch -o fc --output-format csv -- tools/micro/fetch_cal || exit $?
+tools/gpu_step.sh 120 $O/b_fc_write.log timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $O/fc/write -o fc --output-format csv -- tools/micro/fetch_cal || exit $?
