@@ -1623,197 +1623,6 @@ struct BandSide {
       const_cast<BandSide*>(this)->tslot += 4;
     }
   }
-  // LORB_CHAIN_DELTA: the lookahead split with the next column block's update on the CHAIN wave.
-  // Panel p's own contribution to the next column block, D = L_p(rows) L_p(kb+16 .. kb+31)^T, is
-  // accumulated by the chain in its factor loop -- one rank-1 VALU update per column, multipliers read
-  // back from colbuf a column late (as mp), issued in the latency gaps of the pivot chain.  The update
-  // wave hands over the next column block with the EARLIER panels' contributions at the start of its
-  // iteration (it no longer waits for this panel's L), so at the end of the panel the next panel is
-  // pb - D (D shifted up 16 rows through pb) with no hand-over on the critical path; the update wave
-  // applies L_p to the two column blocks after it (and to all three on a phase's last panel, whose
-  // window the M combine reads).  L goes to the band inside the column loop.
-  //   ord: the update wave has read its operands of the previous panel's L (the chain may overwrite
-  //   colbuf); pbr: the chain has read pb (the update wave may rewrite it).
-  __device__ __forceinline__ void chain_d(double (&P)[NB], double& zr, bool& bad, int kb0, int kend, bool pre,
-                                          int* lrd, int* prd, int* ord, int* pbr, int& pwant, int& owant,
-                                          double* pb) const {
-    const int dstep = 16 * (si + sj);
-    unsigned l_ok = 0;
-#pragma unroll
-    for (int q = 0; q < NB; ++q) l_ok |= (unsigned)(q <= lane && lane - q <= bw) << q;
-    int l_base = idx(kb0 + lane, kb0);
-    double* colbuf = xch;
-    double* dummy = xch + 16 * kCS + lane;
-    if (!pre) {  // the phase's first panel from pb
-      wait_ge<false>(prd, ++pwant);
-#pragma unroll
-      for (int q = 0; q < NB; ++q) P[q] = pb[lane * 17 + q];
-      wave_sync_lds();
-      if (lane == 0) __hip_atomic_fetch_add(pbr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    for (int kb = kb0; kb < kend; kb += 16) {
-      int lane = this->lane, lok = (int)l_ok;
-      asm volatile("" : "+v"(lane), "+v"(lok));
-      const bool nxt = kb + 16 < kend, first = pre && kb == kb0;
-      tr(0);
-      const double zin = kb + 16 + lane < rows ? z[kb + 16 + lane] : 0.0;
-      const bool rowvalid = kb + lane < rows;
-      double yq = 0.0;
-      double mp[NB], md[NB], dl[NB];
-#pragma unroll
-      for (int q2 = 0; q2 < NB; ++q2) { mp[q2] = 0.0; md[q2] = 0.0; dl[q2] = 0.0; }
-      double akk = readlane_d(P[0], 0);
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        bad |= !(akk > 0.0);
-        double y = __builtin_amdgcn_rsq(akk);
-        __builtin_amdgcn_sched_barrier(0);
-        if (q >= 1) {
-#pragma unroll
-          for (int q2 = q + 1; q2 < NB; ++q2) P[q2] = fma(-P[q - 1], mp[q2], P[q2]);
-#pragma unroll
-          for (int c = 0; c < NB; ++c) {
-            dl[c] = fma(P[q - 1], md[c], dl[c]);  // column q-1 into D
-            // pinned here: otherwise the FMAs sink to D's use after the loop and all 16 columns'
-            // multipliers stay live (spills)
-            asm volatile("" : "+v"(dl[c]));
-          }
-        }
-        {
-          const double e = fma(-akk * y, y, 1.0);
-          y = fma(0.5 * y, e, y);
-        }
-        P[q] *= y;  // lane q: akk * y = L(k, k)
-        yq = lane == q ? y : yq;
-        const double zk = readlane_d(zr, q) * y;
-        zr = lane > q ? fma(-P[q], zk, zr) : (lane == q ? zk : zr);
-        if (q == 0 && !first) wait_ge<false>(ord, ++owant);  // colbuf free (previous L consumed)
-        colbuf[q * kCS + lane] = P[q];
-        {  // L column q into the band (its diagonal slot holds 1 / L(k, k))
-          const bool ok = rowvalid && (((unsigned)lok >> q) & 1u);
-          *(ok ? A + l_base + q * sj : dummy) = q == lane ? y : P[q];
-        }
-        if (q + 1 < NB) {
-          const double l1 = readlane_d(P[q], q + 1);
-          P[q + 1] = fma(-P[q], l1, P[q + 1]);
-          akk = readlane_d(P[q + 1], q + 1);
-#pragma unroll
-          for (int q2 = q + 2; q2 < NB; ++q2) mp[q2] = colbuf[q * kCS + q2];
-        }
-#pragma unroll
-        for (int c = 0; c < NB; ++c) md[c] = colbuf[q * kCS + 16 + c];  // L(kb + 16 + c, kb + q)
-      }
-#pragma unroll
-      for (int c = 0; c < NB; ++c) dl[c] = fma(P[NB - 1], md[c], dl[c]);
-      tr(1);
-      // L is complete in colbuf: post it, then the next panel = pb - D
-      if (lane == 0) __hip_atomic_fetch_add(lrd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (nxt) {
-        wait_ge<false>(prd, ++pwant);
-        double Pn[NB];
-#pragma unroll
-        for (int q = 0; q < NB; ++q) Pn[q] = pb[lane * 17 + q];
-        wave_sync_lds();
-        if (lane >= 16) {
-#pragma unroll
-          for (int c = 0; c < NB; ++c) pb[(lane - 16) * 17 + c] = dl[c];
-        }
-        wave_sync_lds();
-#pragma unroll
-        for (int c = 0; c < NB; ++c) {
-          const double dv = pb[(lane < 48 ? lane : 0) * 17 + c];
-          P[c] = Pn[c] - (lane < 48 ? dv : 0.0);  // rows kb+64 .. kb+79 enter untouched
-        }
-        wave_sync_lds();
-        if (lane == 0) __hip_atomic_fetch_add(pbr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      l_base += dstep;
-      if (lane < NB) z[kb + lane] = zr;
-      if (lane == 0 && pdone) __hip_atomic_fetch_add(pdone, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const double zs = __shfl_down(zr, 16, 64);
-      zr = lane < 48 ? zs : zin;
-      tr(2);
-      const_cast<BandSide*>(this)->tslot += 3;
-    }
-  }
-  //   update_d(): the update wave of chain_d.  pre_u: the phase's first hand-over needs no pb
-  //   release (the chain's first panel did not come from pb).
-  __device__ __forceinline__ void update_d(v4d (&T)[10], int kb0, int kend, int* lrd, int* prd, int* ord, int* pbr,
-                                           int& lwant, int& bwant, double* pb, bool pre_u) const {
-    const int ci = lane & 15, ck = lane >> 4;
-    const int dstep = 16 * (si + sj);
-    int tn_addr = idx(kb0 + 64 + ck, kb0 + 16 + ci);
-    unsigned tn_ok = 0;
-#pragma unroll
-    for (int J = 0; J < 4; ++J)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 64 + ck + 4 * r, j = 16 + 16 * J + ci;
-        tn_ok |= (unsigned)(j <= i && i - j <= bw) << (4 * J + r);
-      }
-    for (int kb = kb0; kb < kend; kb += 16) {
-      int tok = (int)tn_ok;
-      asm volatile("" : "+v"(tok));
-      if (mask) {
-        const int b = dir > 0 ? kb / 16 + 4 : nbk - 5 - kb / 16;
-        if (b >= 0 && b < nbk) wait_bit(mask, b);
-      }
-      v4d Tn[4];
-#pragma unroll
-      for (int J = 0; J < 4; ++J)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = (((unsigned)tok >> (4 * J + r)) & 1u) && kb + 64 + ck + 4 * r < rows;
-          const double v = A[ok ? tn_addr + 4 * r * si + 16 * J * sj : base];
-          Tn[J][r] = ok ? v : 0.0;
-        }
-      tn_addr += dstep;
-      const bool nxt = kb + 16 < kend;
-      tr(0);
-      if (nxt) {  // the next panel's column with the earlier panels' contributions
-        if (!(pre_u && kb == kb0)) wait_ge<true>(pbr, ++bwant);
-#pragma unroll
-        for (int I = 1; I < 4; ++I)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pb[(16 * (I - 1) + ck + 4 * r) * 17 + ci] = T[tri4(I, 1)][r];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pb[(48 + ck + 4 * r) * 17 + ci] = Tn[0][r];
-        if (lane == 0) __hip_atomic_fetch_add(prd, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      wait_ge<true>(lrd, ++lwant);
-      tr(1);
-      double opA[4][4];
-#pragma unroll
-      for (int I = 1; I < 4; ++I)
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-          opA[I][kk] = xch[(4 * kk + ck) * kCS + 16 * I + ci];  // L(kb + 16 I + ci, kb + 4 kk + ck)
-      wave_sync_lds();
-      if (lane == 0) __hip_atomic_fetch_add(ord, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      tr(2);
-      if (!nxt) {  // the phase's last panel: its window (read by the M combine / the M phase) in full
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-          for (int I = 1; I < 4; ++I)
-            T[tri4(I, 1)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[1][kk], T[tri4(I, 1)], 0, 0, 0);
-      }
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-        for (int J = 2; J < 4; ++J)
-#pragma unroll
-          for (int I = J; I < 4; ++I)
-            T[tri4(I, J)] = __builtin_amdgcn_mfma_f64_16x16x4f64(-opA[I][kk], opA[J][kk], T[tri4(I, J)], 0, 0, 0);
-      T[tri4(0, 0)] = T[tri4(1, 1)];
-      T[tri4(1, 0)] = T[tri4(2, 1)]; T[tri4(1, 1)] = T[tri4(2, 2)];
-      T[tri4(2, 0)] = T[tri4(3, 1)]; T[tri4(2, 1)] = T[tri4(3, 2)]; T[tri4(2, 2)] = T[tri4(3, 3)];
-#pragma unroll
-      for (int J = 0; J < 4; ++J) T[tri4(3, J)] = Tn[J];
-      tr(3);
-      const_cast<BandSide*>(this)->tslot += 4;
-    }
-  }
   // The 16 x 16 diagonal block of L at view rows c0 .. c0+15 replaced in place by its inverse X
   // (lower triangular; the diagonal slot already holds 1 / L(i, i) = X(i, i)):
   // X(i, j) = -X(i, i) sum_{k=j}^{i-1} L(i, k) X(k, j).  Only the back-substitution reads the
@@ -1951,25 +1760,39 @@ struct BandSide {
   //   rows above:                    coef[k] = sum_{j <= k} L(c0 + j, r) X(k, j) (zw_r -= sum_k coef[k] z_k)
   // at kco[(c0 / 16) * 1024 + 64 k + l].  The bs_run_k step is then one LDS round trip (publish z_b,
   // 16 broadcast reads) where bs_run<true> has two.  X is the full 16 x 16 block: bw >= 15.
+  // On the matrix cores: C(k, r) = sum_j X(k, j) Lx(j, r), rows r = c0-48 .. c0+15 as four 16-row
+  // tiles (N), j in four steps of 4 (K), 16 v_mfma_f64_16x16x4f64; Lx(j, r) = L(c0 + j, r) above the
+  // block (0 outside the band / matrix) and the identity on the block's own rows.  Per lane 4 + 12
+  // independent LDS loads (no broadcasts); C lands as kco[64 k + (r & 63)], the lane of row r in
+  // bs_run_k's window.
   __device__ __forceinline__ void bsk_block(int c0) const {
-    const int row = bs_row(c0), j = row - c0;
-    const bool blk = j >= 0;
-    double lj[16], acc[16];
+    const int ci = lane & 15, ck = lane >> 4;
+    double xa[4], lb[3][4];
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) {
-      const int dd = c0 + jj - row;  // L(c0 + jj, row) lies in the band iff 1 <= dd <= bw
-      const bool ok = !blk && row >= 0 && dd >= 1 && dd <= bw;
-      const double v = A[ok ? idx(c0 + jj, row) : zslot];
-      lj[jj] = blk ? (jj == j ? 1.0 : 0.0) : v;  // a block row picks column j of X (exact)
-      acc[jj] = 0.0;
+    for (int st = 0; st < 4; ++st) {
+      const int j = 4 * st + ck;  // A: X(ci, j), lower triangle
+      xa[st] = A[j <= ci ? idx(c0 + ci, c0 + j) : zslot];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {  // B: L(c0 + j, r) for the rows above
+        const int r = c0 - 48 + 16 * t + ci, dd = c0 + j - r;
+        lb[t][st] = A[(r >= 0 && dd >= 1 && dd <= bw) ? idx(c0 + j, r) : zslot];
+      }
     }
+    v4d acc[4];
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj)
+    for (int t = 0; t < 4; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int k = jj; k < 16; ++k) acc[k] = fma(lj[jj], A[idx(c0 + k, c0 + jj)], acc[k]);  // X(k, jj)
-    double* o = kco + (c0 >> 4) * 1024 + lane;
+    for (int st = 0; st < 4; ++st) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) o[64 * k] = acc[k];
+      for (int t = 0; t < 3; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[st], lb[t][st], acc[t], 0, 0, 0);
+      const double id = (4 * st + ck) == ci ? 1.0 : 0.0;  // the block's rows: X(k, r - c0)
+      acc[3] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[st], id, acc[3], 0, 0, 0);
+    }
+    double* o = kco + (c0 >> 4) * 1024;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[64 * (4 * q + ck) + ((c0 - 48 + 16 * t + ci) & 63)] = acc[t][q];
   }
   __device__ __forceinline__ void bsk_load(int c0, double (&cf)[16]) const {
     const double* p = kco + (c0 >> 4) * 1024 + lane;
@@ -1977,38 +1800,43 @@ struct BandSide {
     for (int k = 0; k < 16; ++k) cf[k] = p[64 * k];
   }
   // blocks c_from, c_from - 16, ..., c_to through their bsk_block operators; cf holds block
-  // c_from's on entry, the next block's are loaded (L2) while this one runs.  Rows entering above
+  // c_from's on entry.  Two coefficient sets alternate, so the next block's loads (L2) stay in
+  // flight while this block runs (a copy between sets would wait for them).  Rows entering above
   // are merged before the product, as in bs_run.
+  __device__ __forceinline__ void bsk_step(BsWin& S, int c0, const double (&cf)[16]) const {
+    int row = bs_row(c0);
+    asm volatile("" : "+v"(row));
+    const int j = row - c0;
+    const bool blk = j >= 0;
+    double zw = S.zw;
+    if (blk) z[row] = zw;  // z_b is final: publish it
+    zw = S.pend ? S.zin : zw;
+    wave_sync_lds();
+    const double2* zb2 = reinterpret_cast<const double2*>(z + c0);
+    double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      const double2 v = zb2[k2];
+      a4[(2 * k2) & 3] = fma(cf[2 * k2], v.x, a4[(2 * k2) & 3]);
+      a4[(2 * k2 + 1) & 3] = fma(cf[2 * k2 + 1], v.y, a4[(2 * k2 + 1) & 3]);
+    }
+    const double sum = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    zw = blk ? sum : zw - sum;
+    if (blk) {
+      z[row] = zw;                                // y_b (after every lane's broadcast read)
+      S.zin = row - 64 >= 0 ? z[row - 64] : 0.0;  // the row entering above
+    }
+    S.pend = blk;
+    S.zw = zw;
+  }
   __device__ __forceinline__ void bs_run_k(BsWin& S, int c_from, int c_to, double (&cf)[16]) const {
-    for (int c0 = c_from; c0 >= c_to; c0 -= 16) {
-      int row = bs_row(c0);
-      asm volatile("" : "+v"(row));
-      const int j = row - c0;
-      const bool blk = j >= 0;
-      double cn[16];
-      bsk_load(c0 - 16 >= c_to ? c0 - 16 : c0, cn);
-      double zw = S.zw;
-      if (blk) z[row] = zw;  // z_b is final: publish it
-      zw = S.pend ? S.zin : zw;
-      wave_sync_lds();
-      const double2* zb2 = reinterpret_cast<const double2*>(z + c0);
-      double a4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int k2 = 0; k2 < 8; ++k2) {
-        const double2 v = zb2[k2];
-        a4[(2 * k2) & 3] = fma(cf[2 * k2], v.x, a4[(2 * k2) & 3]);
-        a4[(2 * k2 + 1) & 3] = fma(cf[2 * k2 + 1], v.y, a4[(2 * k2 + 1) & 3]);
-      }
-      const double s = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-      zw = blk ? s : zw - s;
-      if (blk) {
-        z[row] = zw;                                  // y_b (after every lane's broadcast read)
-        S.zin = row - 64 >= 0 ? z[row - 64] : 0.0;    // the row entering above
-      }
-      S.pend = blk;
-      S.zw = zw;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) cf[k] = cn[k];
+    double cg[16];
+    for (int c0 = c_from; c0 >= c_to; c0 -= 32) {
+      bsk_load(c0 - 16 >= c_to ? c0 - 16 : c0, cg);
+      bsk_step(S, c0, cf);
+      if (c0 - 16 < c_to) break;
+      bsk_load(c0 - 32 >= c_to ? c0 - 32 : c0, cf);
+      bsk_step(S, c0 - 16, cg);
     }
   }
 };
@@ -2106,10 +1934,7 @@ constexpr int kChol2sThreads = 512;
 #ifndef LORB_BSK
 #define LORB_BSK 1
 #endif
-// 1: the next column block's update on the chain wave (BandSide::chain_d / update_d)
-#ifndef LORB_CHAIN_DELTA
-#define LORB_CHAIN_DELTA 0
-#endif
+
 // LDS words of k_ba_chol_2s: band (n16 rows), both sides' rhs (n16 + 48), two 64 x 18 exchanges
 // (together the 48 x 48 combine), zX (48), two 64 x 17 panel hand-off buffers, a zero word
 __host__ __device__ constexpr int chol2s_words(int n16, int bw) {
@@ -2170,7 +1995,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   __shared__ int s_pdone[2];
   __shared__ int s_linv[2];           // diagonal-block inverses done, per side (LORB_BSK)
   __shared__ int s_lrd[2], s_prd[2];  // per side: L panels posted (chain), panel columns posted (update)
-  __shared__ int s_ord[2], s_pbr[2];  // per side (LORB_CHAIN_DELTA): L operands read (update), pb read (chain)
   __shared__ int s_hand[3];           // T / B -> M hand-over (below)
   const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
   const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
@@ -2209,7 +2033,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     s_pdone[0] = 0; s_pdone[1] = 0;
     s_linv[0] = 0; s_linv[1] = 0;
     s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
-    s_ord[0] = 0; s_ord[1] = 0; s_pbr[0] = 0; s_pbr[1] = 0;
     s_hand[0] = 0; s_hand[1] = 0; s_hand[2] = 0;
     unsigned long long msk = 0;
     for (int b = 0; b < nbk; ++b) msk |= (unsigned long long)(!prog || b < ib || b >= nbk - ib) << (b & 63);
@@ -2250,7 +2073,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   int* lrd = &s_lrd[side];
   int* prd = &s_prd[side];
   int lwant = 0, pwant = 0;
-  [[maybe_unused]] int owant = 0, bwant = 0;  // LORB_CHAIN_DELTA
   bool bad = false;
   double zr = 0.0;
   double P[NB];
@@ -2303,36 +2125,28 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     unsigned long long* phv = d.dbg + 8 * w;  // wave 0, T phase: [0] wait [1] factor [2] store
     if (wv == 0) { if (lane == 0) { phv[0] = phv[1] = phv[2] = 0; } const_cast<BandSide&>(me).phases = phv; }
 #endif
-#if LORB_CHAIN_DELTA
-    me.chain_d(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, &s_ord[side], &s_pbr[side], pwant, owant, pb);
-#else
     me.chain(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, pwant, pb);
-#endif
   } else if (wv < 4) {
     me.init_tiles(T);
-#if LORB_CHAIN_DELTA
-    me.update_d(T, 0, side == 0 ? m : nB, lrd, prd, &s_ord[side], &s_pbr[side], lwant, bwant, pb, true);
-#else
     me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb);
-#endif
   }
   if (wv < 6) C2_STAMP(wv);
 #if LORB_BSK
-  // The T / B back-substitution operators (bsk_block), once a side's diagonal inverses are done:
-  // wave 5 builds the top side's (after its own bottom-side inverses), wave 7 the bottom side's
-  // (after the staging), in the order the back-substitution needs them.  Both run beside the
-  // combine and the M phase on SIMDs whose waves are idle then; the stores drain before the
-  // barrier that precedes the back-substitution.
-  if (wv == 5 || wv == 7) {
-    const int ks = wv == 5 ? 0 : 1;
+  // The T / B back-substitution operators (bsk_block, on the matrix cores), once a side's diagonal
+  // inverses are done, on SIMDs 1 and 3 (the M phase's chain and update waves are on 0 and 2): waves
+  // 5 / 7 build the top side's (alternate blocks, in the order the back-substitution needs them),
+  // waves 1 / 3 the bottom side's after their hand-over to the M phase (below).  The stores drain
+  // before the barrier that precedes the back-substitution.
+  auto build_ops = [&](int ks, int par) {
     const BandSide& kside = ks == 0 ? top : bot;
     const int nkb = (ks == 0 ? m : nB) / 16;
     wait_ge<true>(&s_linv[ks], nkb);
     TR1(16 + 2 * ks);
-    for (int b = nkb - 1; b >= 0; --b) kside.bsk_block(16 * b);
+    for (int b = nkb - 1 - par; b >= 0; b -= 2) kside.bsk_block(16 * b);
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the operators are in L2 before the barrier
     TR1(17 + 2 * ks);
-  }
+  };
+  if (wv == 5 || wv == 7) build_ops(0, wv == 7);
 #endif
   // Hand-over to the M phase by flags, not barriers (the diagonal-block inverses of waves 4 / 5
   // may still be running): wave 2 posts that it has read its last L from xt, wave 3 then writes
@@ -2359,6 +2173,9 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     if (bad) s_bad = 1;
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[2], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
+#if LORB_BSK
+  if (wv == 1 || wv == 3) build_ops(1, wv == 3);
+#endif
   if (wv == 2) {
     TR1(0);
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2392,21 +2209,13 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
       if (lane == 0) __hip_atomic_fetch_add(&s_prd[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     TR1(15);
-#if LORB_CHAIN_DELTA
-    topM.update_d(T, m, m + 48, &s_lrd[0], &s_prd[0], &s_ord[0], &s_pbr[0], lwant, bwant, pbt, false);
-#else
     topM.update(T, m, m + 48, &s_lrd[0], &s_prd[0], lwant, pbt);
-#endif
   } else if (wv == 0) {
     zr = lane < 48 ? zr + zX[lane] - zt[m + lane] : 0.0;
     BandSide topM = top;
     topM.mask = nullptr; topM.pdone = nullptr;
     TR1(3);
-#if LORB_CHAIN_DELTA
-    topM.chain_d(P, zr, bad, m, m + 48, false, &s_lrd[0], &s_prd[0], &s_ord[0], &s_pbr[0], pwant, owant, pbt);
-#else
     topM.chain(P, zr, bad, m, m + 48, false, &s_lrd[0], &s_prd[0], pwant, pbt);
-#endif
     TR1(4);
     if (bad) s_bad = 1;
     C2_STAMP(6);

@@ -529,7 +529,8 @@ int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, con
 // k_cc_finalize<0>, or the LocalMapping append).  Nothing is uploaded: the scan computes its tiles and
 // clears the keys, the chunk merge and the scatter are one launch.
 int lorb::match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
-                          unsigned long long** qkey_out) {
+                          unsigned long long** qkey_out, hipStream_t stream) {
+  hipStream_t st = stream ? stream : ctx->stream;
   unsigned long long* qkey = nullptr;
   LORB_TRY(lorb::scratch_t(ctx, S_BF_QKEY, (size_t)std::max(nq, 1), &qkey));
   if (nt > 0 && nq > 0) {
@@ -552,7 +553,7 @@ int lorb::match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8
     LORB_TRY(lorb::scratch_t(ctx, S_BF_TKEY, (size_t)nt, &tkey));
     if (ctx->tkey_buf != (void*)tkey || ctx->tkey_ready < (size_t)nt) {  // a fresh or grown buffer: all-ones once
       LORB_HIP(ctx, hipMemsetAsync(tkey, 0xff, sizeof(uint32_t) * (ctx->scratch_sz[S_BF_TKEY] / sizeof(uint32_t)),
-                                   ctx->stream));
+                                   st));
       ctx->tkey_ready = ctx->scratch_sz[S_BF_TKEY] / sizeof(uint32_t);
       ctx->tkey_buf = tkey;
     }
@@ -562,20 +563,20 @@ int lorb::match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8
     {
       lorb::KernelTimer kt(ctx, LORB_K_BF_SCAN_TOP1);
       if (qpl == 2)
-        hipLaunchKernelGGL((k_bf_scan1<false, 2>), dim3(nb), dim3(256), 0, ctx->stream, reinterpret_cast<const uint4*>(d_t),
+        hipLaunchKernelGGL((k_bf_scan1<false, 2>), dim3(nb), dim3(256), 0, st, reinterpret_cast<const uint4*>(d_t),
                            reinterpret_cast<const uint4*>(d_q), g, tkey, (uint32_t*)nullptr, qkey, nq);
       else if (qpl == 4)
-        hipLaunchKernelGGL((k_bf_scan1<false, 4>), dim3(nb), dim3(256), 0, ctx->stream, reinterpret_cast<const uint4*>(d_t),
+        hipLaunchKernelGGL((k_bf_scan1<false, 4>), dim3(nb), dim3(256), 0, st, reinterpret_cast<const uint4*>(d_t),
                            reinterpret_cast<const uint4*>(d_q), g, tkey, (uint32_t*)nullptr, qkey, nq);
       else
-        hipLaunchKernelGGL((k_bf_scan1<false, 1>), dim3(nb), dim3(256), 0, ctx->stream, reinterpret_cast<const uint4*>(d_t),
+        hipLaunchKernelGGL((k_bf_scan1<false, 1>), dim3(nb), dim3(256), 0, st, reinterpret_cast<const uint4*>(d_t),
                            reinterpret_cast<const uint4*>(d_q), g, tkey, (uint32_t*)nullptr, qkey, nq);
     }
-    hipLaunchKernelGGL(k_cc_merge1, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, ctx->stream, tkey, nt, qkey);
+    hipLaunchKernelGGL(k_cc_merge1, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, st, tkey, nt, qkey);
     LORB_CHECK_LAUNCH(ctx);
     ctx->tkey_ready = ready;
   } else if (nq > 0) {
-    LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, ctx->stream));
+    LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, st));
   }
   LORB_CHECK_LAUNCH(ctx);
   *qkey_out = qkey;

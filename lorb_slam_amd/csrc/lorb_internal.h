@@ -115,7 +115,7 @@ const int* ba_plan_point_offsets(const lorb_ba_plan* P);
 // crossCheck keys of ONE brute-force problem (lorb_bf_match_dev without its finalisation): per
 // query (dist << 32 | train) or all-ones; *qkey_out is ctx scratch valid until the next matcher call
 int match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
-                    unsigned long long** qkey_out);
+                    unsigned long long** qkey_out, hipStream_t stream = nullptr);  // null: ctx->stream
 
 // grow-only scratch: returns device pointer in *out
 int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out);

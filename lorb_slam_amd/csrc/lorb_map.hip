@@ -328,14 +328,25 @@ struct lorb_map {
   lorb_ba_plan* plan = nullptr;
   bool plan_ok = false;  // plan built on the current slots (its point offsets serve the compaction)
   bool broken = false;   // a failed step whose counts could not be re-read: the map is unusable
+  // Overlap (LORB_MAP_OVERLAP, default on): a step's match and append touch only the map's point
+  // descriptors, its new slots / points and counts -- nothing the previous step's LM solve and
+  // write-back read or write -- so they run on a side stream as soon as the previous step's plan
+  // build has read the map (ev_built), concurrently with that solve; the slide waits for both.
+  hipStream_t side = nullptr;
+  hipEvent_t ev_built = nullptr, ev_app = nullptr;
+  bool built = false;  // ev_built recorded by the previous step
   std::vector<void*> allocs;
   ~lorb_map() {
     if (prof && prof_n)
       fprintf(stderr, "lorb_map profile over %d steps (ms/step): match %.3f unproject %.3f append %.3f slide %.3f "
               "plan %.3f solve %.3f writeback %.3f\n", prof_n, prof_ms[0] / prof_n, prof_ms[1] / prof_n,
               prof_ms[2] / prof_n, prof_ms[3] / prof_n, prof_ms[4] / prof_n, prof_ms[5] / prof_n, prof_ms[6] / prof_n);
+    if (side) (void)hipStreamSynchronize(side);
     if (plan) (void)lorb_ba_plan_destroy(plan);
     if (pinned) (void)hipHostFree(pinned);
+    if (ev_built) (void)hipEventDestroy(ev_built);
+    if (ev_app) (void)hipEventDestroy(ev_app);
+    if (side) (void)hipStreamDestroy(side);
     for (void* p : allocs) (void)hipFree(p);
   }
 };
@@ -513,11 +524,19 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
     return LORB_OK;
   };
   LORB_TRY(mark(7));
+  static const bool ovl_env = [] { const char* e = getenv("LORB_MAP_OVERLAP"); return !(e && e[0] == '0'); }();
+  const bool ovl = ovl_env && M->built && !M->prof && !ctx->ktime;
+  if (ovl && !M->side) {
+    LORB_HIP(ctx, hipStreamCreateWithFlags(&M->side, hipStreamNonBlocking));
+    LORB_HIP(ctx, hipEventCreateWithFlags(&M->ev_app, hipEventDisableTiming));
+  }
+  hipStream_t ms = ovl ? M->side : s;  // the match + append stream
+  if (ovl) LORB_HIP(ctx, hipStreamWaitEvent(ms, M->ev_built, 0));
   // 1. SearchLocalPoints: the keyframe's descriptors against the map's points -- the crossCheck keys
   //    here, the finalisation (minDist filter) inside the append
   unsigned long long* qkey = nullptr;
   const bool has_t = M->h_P > 0;
-  if (n > 0 && has_t) LORB_TRY(lorb::match1_keys_dev(ctx, d_desc, n, m.desc, M->h_P, &qkey));
+  if (n > 0 && has_t) LORB_TRY(lorb::match1_keys_dev(ctx, d_desc, n, m.desc, M->h_P, &qkey, ms));
   LORB_TRY(mark(0));
   LORB_TRY(mark(1));
   // 2 + 3. AddObservation / new points at UnprojectStereo (Twc = mTcw.inv(), src/frame.cpp:350),
@@ -527,7 +546,7 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   lorb::Mat4f Twc;
   lorb::inv4_lu32f(Tcw, Twc.v);
 #define LORB_APPEND(RM)                                                                                       \
-  hipLaunchKernelGGL(k_map_append<RM>, dim3(1), dim3(1024), 0, s, m, n, kf, p6, (const unsigned long long*)qkey, \
+  hipLaunchKernelGGL(k_map_append<RM>, dim3(1), dim3(1024), 0, ms, m, n, kf, p6, (const unsigned long long*)qkey, \
                      (int)(has_t && qkey), M->mt, Twc, frame->fx, frame->fy, frame->cx, frame->cy, d_desc, d_x, d_y, \
                      d_depth)
   if (n <= 1024) LORB_APPEND(1);
@@ -536,6 +555,10 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   else LORB_APPEND(0);
 #undef LORB_APPEND
   LORB_CHECK_LAUNCH(ctx);
+  if (ovl) {  // the rest of the step follows the previous step's write-back on the main stream
+    LORB_HIP(ctx, hipEventRecord(M->ev_app, ms));
+    LORB_HIP(ctx, hipStreamWaitEvent(s, M->ev_app, 0));
+  }
   M->last_n = n;
   // Capacity: n keypoints add at most n points and n observations.  When that bound does not fit,
   // read the append's verdict before anything else changes: a refused append leaves the map as it
@@ -556,6 +579,7 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   const lorb_ba_window_dev w = window_of(M);
   M->plan_ok = false;
   if (const int rc = lorb_ba_plan_update_dev(M->plan, &w); rc != LORB_OK) {
+    M->built = false;  // the next step's match waits for this step's kernels on the main stream
     // the append and the slide have run: the live counts are the device's now, and the next slide
     // takes h_K as the end of the point-sorted slots -- re-read them, or mark the map unusable
     if (hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
@@ -567,6 +591,10 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
     return rc;
   }
   M->plan_ok = true;
+  // the plan build has read the map: the next step's match and append may start (see `side`)
+  if (!M->ev_built) LORB_HIP(ctx, hipEventCreateWithFlags(&M->ev_built, hipEventDisableTiming));
+  LORB_HIP(ctx, hipEventRecord(M->ev_built, s));
+  M->built = true;
   LORB_TRY(mark(4));
   lorb::ba_plan_window_counts(M->plan, &M->h_P, &M->h_K);
   // 6. LocalPoseOptimization + float write-back of poses (ring) and points (map)

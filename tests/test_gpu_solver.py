@@ -190,8 +190,10 @@ def test_solver_lru_eviction(ctx):
     s = BASolver(ctx)
     try:
         wins = [synth.ba_window(seed=40 + k, n_kf=k, n_pts=80 * k, n_fixed=1, fixed_obs_per_kf=30) for k in range(6, 12)]
+        # default Ceres tolerances: at tolerance 0 these small windows converge to machine precision
+        # and the stopping iteration is rounding-determined
         for w in wins + wins[:2]:
-            check(s, w, OPT10)
+            check(s, w, A.LMOptions.default())
         info = s.info()
         assert info["resident_plans"] == 4 and info["plan_creations"] == 8 and info["host_plan_fallback"] == 0, info
     finally:

@@ -7,12 +7,9 @@ O=$R/gpurun_out; mkdir -p $O
 export TMPDIR=/tmp
 tools/gpu_step.sh 600 $O/d_tests.log python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit $?
 LORB_LIB_PATH=$R/lorb_slam_amd/liblorb_trace.so tools/gpu_step.sh 120 $O/d_trace.log python tools/chol_trace.py || exit $?
-LORB_LIB_PATH=$R/lorb_slam_amd/liblorb_tracecd.so tools/gpu_step.sh 120 $O/d_trace_cd.log python tools/chol_trace.py || exit $?
-LORB_LIB_PATH=$R/lorb_slam_amd/liblorb_cd.so tools/gpu_step.sh 400 $O/d_tests_cd.log python -u -m pytest tests/test_gpu_ba.py tests/test_gpu_solver.py tests/test_gpu_map.py tests/test_gpu_shard.py -m gpu -x -q --timeout 120 --timeout-method thread || exit $?
 for k in 1 2; do
 LORB_LIB_PATH=$R/lorb_slam_amd/liblorb_base.so tools/gpu_step.sh 200 $O/d_tba_base$k.log python tools/time_ba.py || exit $?
 tools/gpu_step.sh 200 $O/d_tba_def$k.log python tools/time_ba.py || exit $?
-LORB_LIB_PATH=$R/lorb_slam_amd/liblorb_cd.so tools/gpu_step.sh 200 $O/d_tba_cd$k.log python tools/time_ba.py || exit $?
 done
 tools/gpu_step.sh 120 $O/d_iolat.log tools/micro/io_lat || exit $?
 tools/gpu_step.sh 120 $O/d_fc_fetch.log timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $O/fc/fetch -o fc --output-format csv -- tools/micro/fetch_cal || exit $?
