@@ -1416,6 +1416,7 @@ struct BandSide {
   unsigned long long* phases = nullptr;  // LORB_CHOL_PHASES diagnostics: chain wait / factor / store cycles
   unsigned long long* trace = nullptr;   // LORB_CHOL_TRACE diagnostics: per-panel event times
   int tslot = 0;                         // (slot of this wave's next panel; cycles since t0)
+  int bslot = 320;                       // (slot of this wave's next back-substitution block)
   unsigned long long t0 = 0;
   __device__ __forceinline__ void tr(int k) const {
 #ifdef LORB_CHOL_TRACE
@@ -1803,7 +1804,13 @@ struct BandSide {
   // c_from's on entry.  Two coefficient sets alternate, so the next block's loads (L2) stay in
   // flight while this block runs (a copy between sets would wait for them).  Rows entering above
   // are merged before the product, as in bs_run.
+  __device__ __forceinline__ void tr_bs(int k) const {  // LORB_CHOL_TRACE: back-substitution steps
+#ifdef LORB_CHOL_TRACE
+    if (trace && lane == 0 && bslot + k < 512) trace[bslot + k] = __builtin_amdgcn_s_memtime() - t0;
+#endif
+  }
   __device__ __forceinline__ void bsk_step(BsWin& S, int c0, const double (&cf)[16]) const {
+    tr_bs(0);
     int row = bs_row(c0);
     asm volatile("" : "+v"(row));
     const int j = row - c0;
@@ -1812,6 +1819,7 @@ struct BandSide {
     if (blk) z[row] = zw;  // z_b is final: publish it
     zw = S.pend ? S.zin : zw;
     wave_sync_lds();
+    tr_bs(1);
     const double2* zb2 = reinterpret_cast<const double2*>(z + c0);
     double a4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1822,6 +1830,8 @@ struct BandSide {
     }
     const double sum = (a4[0] + a4[1]) + (a4[2] + a4[3]);
     zw = blk ? sum : zw - sum;
+    tr_bs(2);
+    const_cast<BandSide*>(this)->bslot += 3;
     if (blk) {
       z[row] = zw;                                // y_b (after every lane's broadcast read)
       S.zin = row - 64 >= 0 ? z[row - 64] : 0.0;  // the row entering above
@@ -1829,16 +1839,30 @@ struct BandSide {
     S.pend = blk;
     S.zw = zw;
   }
+  // fully unrolled (at most kBskMax blocks): in a loop the compiler drains every load at the loop
+  // head (vmcnt(0)), which would make each block wait for its successor's prefetch
+  static constexpr int kBskMax = 32;
   __device__ __forceinline__ void bs_run_k(BsWin& S, int c_from, int c_to, double (&cf)[16]) const {
     double cg[16];
-    for (int c0 = c_from; c0 >= c_to; c0 -= 32) {
+    int c0 = c_from;
+#pragma unroll
+    for (int it = 0; it < kBskMax; it += 2) {
+      if (c0 < c_to) return;
       bsk_load(c0 - 16 >= c_to ? c0 - 16 : c0, cg);
       bsk_step(S, c0, cf);
-      if (c0 - 16 < c_to) break;
+      if (c0 - 16 < c_to) return;
       bsk_load(c0 - 32 >= c_to ? c0 - 32 : c0, cf);
       bsk_step(S, c0 - 16, cg);
+      c0 -= 32;
+    }
+    for (; c0 >= c_to; c0 -= 16) {  // more than kBskMax blocks (narrow bands of ~1000 rows)
+      bsk_load(c0 - 16 >= c_to ? c0 - 16 : c0, cg);
+      bsk_step(S, c0, cf);
+#pragma unroll
+      for (int k = 0; k < 16; ++k) cf[k] = cg[k];
     }
   }
+
 };
 
 // Flat copy of band chunks [j0, j1) (16-byte chunks of the row-major n x (bw + 1) band) by nthr
@@ -2063,6 +2087,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   unsigned long long* trb = d.dbg + 512 * w;
   top.trace = trb; bot.trace = trb; top.t0 = tr0; bot.t0 = tr0;
   top.tslot = wv == 0 ? 0 : 64; bot.tslot = wv == 1 ? 128 : 160;
+  top.bslot = 320; bot.bslot = 400;
 #define TR1(k) do { if (lane == 0) trb[200 + (k)] = __builtin_amdgcn_s_memtime() - tr0; } while (0)
 #else
 #define TR1(k) do {} while (0)

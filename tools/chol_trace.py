@@ -31,5 +31,8 @@ names = ["w2 T done", "w2 got X", "w3 X written", "w0 M start", "w0 M done", "w0
          "w2 combined", "w2 M handed", "K top start", "K top done", "K bot start", "K bot done"]
 for k, nm in enumerate(names): print(f"{nm:16s} {v[200 + k]}")
 plan.close()
+for nm, b in (("top", 320), ("bottom", 400)):
+    st = [(v[b + 3 * i], v[b + 3 * i + 1], v[b + 3 * i + 2]) for i in range(24) if v[b + 3 * i]]
+    print(f"bs {nm} blocks (start, after publish+wait, after product):", st)
 print("linv top (start, end):", [(v[256 + 2 * p], v[257 + 2 * p]) for p in range(8)])
 print("linv bot (start, end):", [(v[288 + 2 * p], v[289 + 2 * p]) for p in range(8)])
