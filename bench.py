@@ -306,19 +306,58 @@ def c1_inputs(n=C1_PAIRS):
     return out
 
 
-def c1_stages(ctx_or_oracle, oracle=False):
-    """the three C1 calls on input set x: a2 BF crossCheck, a4 SearchByProjection(th 15), a12"""
-    if oracle:
-        O = ctx_or_oracle
-        return {"a2_bf_match": lambda x: O.bf_match(x["pr"]["cur_kps"]["desc"], x["tdesc"]),
-                "a4_search_by_projection_th15": lambda x: O.search_by_projection_frame(
-                    x["pr"]["fp"], x["pr"]["cur_Tcw"], x["pr"]["cur_kps"], x["pr"]["slot_state"], x["pr"]["last"], 15.0),
-                "a12_pose_only_200": lambda x: O.ba_pose_only(x["pb"])}
-    ctx = ctx_or_oracle
-    return {"a2_bf_match": lambda x: ctx.bf_match([x["pr"]["cur_kps"]["desc"]], [x["tdesc"]]),
-            "a4_search_by_projection_th15": lambda x: ctx.search_by_projection_frame(
-                x["pr"]["fp"], x["pr"]["cur_Tcw"], x["pr"]["cur_kps"], x["pr"]["slot_state"], x["pr"]["last"], 15.0),
-            "a12_pose_only_200": lambda x: ctx.ba_pose_only(x["pb"])}
+def c1_calls(x, L, handle=None):
+    """The three C1 calls on input set x as zero-argument closures over PRE-MARSHALLED ctypes
+    arguments (the caller's arrays, structs and output buffers built once, outside the timing), so
+    that a timing covers the C-ABI call itself: a2 BF crossCheck, a4 SearchByProjection(th 15),
+    a12 ProjectPoseOptimization.  handle=None: the oracle library (or_*), else liblorb on that ctx."""
+    from lorb_slam_amd import _abi as A
+    keep = A.KeepAlive()
+    pr, tdesc, pb = x["pr"], x["tdesc"], x["pb"]
+    cur, last = pr["cur_kps"], pr["last"]
+    q = keep.keep(A.u8(cur["desc"]).reshape(-1, 32))
+    t = keep.keep(A.u8(tdesc).reshape(-1, 32))
+    nq = len(q)
+    o3 = [keep.keep(np.zeros(max(nq, 1), np.int32)) for _ in range(3)]
+    nm1 = keep.keep(np.zeros(1, np.int32))
+    qo = keep.keep(np.array([0, nq], np.int32))
+    to = keep.keep(np.array([0, len(t)], np.int32))
+    fps = A.make_frame_params(pr["fp"])
+    k = A.make_keypoints(cur, keep)
+    lf = A.make_last_frame(last, keep)
+    T = keep.keep(A.f32(pr["cur_Tcw"]).reshape(16))
+    ss = keep.keep(A.u8(pr["slot_state"])) if pr["slot_state"] is not None else None
+    assign = keep.keep(np.empty(max(1, k.n), np.int32))
+    nm = C.c_int32(0)
+    s = A.make_pose_batch(pb, keep)
+    opt = A.LMOptions.default()
+    pose = keep.keep(np.zeros((s.n_frames, 6)))
+    Tp = keep.keep(np.zeros((s.n_frames, 4, 4), np.float32))
+    summ = (A.BASummary * max(1, s.n_frames))()
+    ptr = A.ptr
+    if handle is None:
+        calls = {
+            "a2_bf_match": lambda: L.or_bf_match(ptr(q, C.c_uint8), C.c_int(nq), ptr(t, C.c_uint8), C.c_int(len(t)),
+                                                 ptr(o3[0], C.c_int32), ptr(o3[1], C.c_int32), ptr(o3[2], C.c_int32)),
+            "a4_search_by_projection_th15": lambda: L.or_search_by_projection_frame(
+                C.byref(fps), ptr(T, C.c_float), C.byref(k), ptr(ss, C.c_uint8), C.byref(lf), C.c_float(15.0),
+                ptr(assign, C.c_int32), C.byref(nm)),
+            "a12_pose_only_200": lambda: L.or_ba_pose_only(C.byref(s), C.byref(opt), ptr(pose, C.c_double),
+                                                           ptr(Tp, C.c_float), summ)}
+    else:
+        def chk(rc):
+            if rc != 0:
+                raise RuntimeError(f"C1 call failed: {rc}")
+        calls = {
+            "a2_bf_match": lambda: chk(L.lorb_bf_match(handle, C.c_int32(1), ptr(q, C.c_uint8), ptr(qo, C.c_int32),
+                                                       ptr(t, C.c_uint8), ptr(to, C.c_int32), ptr(o3[0], C.c_int32),
+                                                       ptr(o3[1], C.c_int32), ptr(o3[2], C.c_int32), ptr(nm1, C.c_int32))),
+            "a4_search_by_projection_th15": lambda: chk(L.lorb_search_by_projection_frame(
+                handle, C.byref(fps), ptr(T, C.c_float), C.byref(k), ptr(ss, C.c_uint8), C.byref(lf), C.c_float(15.0),
+                ptr(assign, C.c_int32), C.byref(nm))),
+            "a12_pose_only_200": lambda: chk(L.lorb_ba_pose_only(handle, C.byref(s), C.byref(opt), ptr(pose, C.c_double),
+                                                                 ptr(Tp, C.c_float), summ))}
+    return calls, (keep, fps, k, lf, nm, s, opt, summ)
 
 
 def sub_c1(ctx, D, args):
@@ -327,25 +366,25 @@ def sub_c1(ctx, D, args):
     matched points (a12), host arrays in and out, synchronous.  Every call takes the next of 32
     distinct frame pairs (new inputs each time: nothing is resident from an earlier call); median
     over 3 passes of the 32.  Latency-bound: a few thousand items per call."""
-    import lorb_slam_amd.window  # noqa: F401  (Context.search_by_projection_frame)
+    from lorb_slam_amd.runtime import lib
     xs = c1_inputs()
-    stages = c1_stages(ctx)
-    for fn in stages.values():
-        fn(xs[0])
+    prepared = [c1_calls(x, lib(), ctx.handle) for x in xs]
     per = {}
-    for name, fn in stages.items():
+    for name in prepared[0][0]:
+        prepared[0][0][name]()
         ts = []
         for _ in range(3):
-            for x in xs:
+            for calls, _ in prepared:
                 t0 = time.perf_counter()
-                fn(x)
+                calls[name]()
                 ts.append(time.perf_counter() - t0)
         per[name] = D.reduce(float(np.median(ts)), "MAX") * 1e3
     total = sum(per.values())
     return {"workload": "c1_two_frames_500kps", "value": 1e3 / total, "unit": "C1 sequences/s (a2 + a4 + a12)",
             "ms_per_sequence": total, "stage_ms_median": per, "distinct_inputs": len(xs),
-            "call": "host C-ABI (lorb_bf_match, lorb_search_by_projection_frame, lorb_ba_pose_only), synchronous; "
-                    "one packed H2D copy and one D2H copy per call"}
+            "call": "host C-ABI (lorb_bf_match, lorb_search_by_projection_frame, lorb_ba_pose_only), synchronous, "
+                    "timed around the ctypes call with the arguments marshalled beforehand; one packed H2D copy and "
+                    "one D2H copy per call"}
 
 
 def cpu_baseline_c1(budget_s):
@@ -357,23 +396,23 @@ def cpu_baseline_c1(budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     xs = c1_inputs()
-    stages = c1_stages(O, oracle=True)
+    prepared = [c1_calls(x, O.lib()) for x in xs]
     per = {}
     t_end = time.perf_counter() + budget_s
-    for name, fn in stages.items():
+    for name in prepared[0][0]:
         ts = []
         while len(ts) < 3 * len(xs) or (time.perf_counter() < t_end and len(ts) < 2000):
-            x = xs[len(ts) % len(xs)]
+            calls = prepared[len(ts) % len(xs)][0]
             t0 = time.perf_counter()
-            fn(x)
+            calls[name]()
             ts.append(time.perf_counter() - t0)
         per[name] = float(np.median(ts)) * 1e3
     total = sum(per.values())
     return {"value": 1e3 / total, "unit": "C1 sequences/s (a2 + a4 + a12)", "cores": 1, "kind": "port",
             "ms_per_sequence": total, "stage_ms_median": per,
             "sample": f"{len(xs)} distinct pairs of 2 frames x 500 kps, 200 shared MPs (synth.two_frames seeds 1..{len(xs)}): "
-                      "a2 + a4 th=15 + a12, oracle C gcc -O3 -ffp-contract=off via ctypes, 1 thread, median of >= 96 "
-                      "runs per stage (the same inputs as the GPU leg)"}
+                      "a2 + a4 th=15 + a12, oracle C gcc -O3 -ffp-contract=off, timed around the ctypes call with "
+                      "the arguments marshalled beforehand (as the GPU leg), 1 thread, median of >= 96 runs per stage"}
 
 
 def workload_c3(ctx, args, rank):
@@ -847,6 +886,7 @@ def main():
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in LocalPoseOptimization sub-record")
     ap.add_argument("--no-shared", action="store_true", help="skip the shared-window (RCCL) sub-record")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 local-BA sub-record")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 per-frame tracking sub-record")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -892,7 +932,7 @@ def main():
         cpu["c1"] = cpu_baseline_c1(max(2.0, args.cpu_budget / 2))
     c2 = sub_c2(ctx, D, args) if (args.workload == "c4" and not args.no_c2) else None
     dropin = sub_dropin(ctx, D, args) if (args.workload == "c4" and not args.no_dropin) else None
-    c1 = sub_c1(ctx, D, args) if (args.workload == "c4" and not args.no_c2) else None
+    c1 = sub_c1(ctx, D, args) if (args.workload == "c4" and not args.no_c1) else None
     c3 = sub_c3(ctx, D, args) if (args.workload == "c4" and not args.no_c3) else None
     shared = (sub_shared(ctx, D, args, comm) if (args.workload in ("c4", "rehearse") and not args.no_shared)
               else None)

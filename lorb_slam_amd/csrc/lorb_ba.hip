@@ -2539,48 +2539,43 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
 
 // ------------------------------------------------------------------------------------------
 // pose-only LM (BA::ProjectPoseOptimization), one workgroup per frame, whole solve in-kernel
-__global__ __launch_bounds__(256) void k_ba_pose_only(const int32_t* __restrict__ res_off,
-                                                      const float* __restrict__ intr,
-                                                      const float* __restrict__ pose_init,
-                                                      const float* __restrict__ pts3d,
-                                                      const float* __restrict__ obs2d, LMOpt o,
-                                                      double* __restrict__ pose_out,
-                                                      lorb_ba_summary* __restrict__ sums) {
-  __shared__ double sh[28 * 256];
-  __shared__ double xs[6], xn[6], sc[6], step[6];
-  __shared__ double s_cost, s_gmax, s_xnorm, s_new;
-  __shared__ double JtJ[21], Jtr[6];
-  __shared__ int s_flag;  // 0 continue, 1 stop
-  __shared__ int s_relin;
+// One WAVEFRONT per frame (a12 is the per-frame tracking call: a few hundred residuals): lanes stride
+// the frame's residuals, every reduction is a wave butterfly (wave_sum: every lane ends with the same
+// bits), and every lane carries the frame's LM state and solves the 6 x 6 system redundantly, so an
+// iteration has no LDS traffic and no barrier.
+__global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__ res_off,
+                                                     const float* __restrict__ intr,
+                                                     const float* __restrict__ pose_init,
+                                                     const float* __restrict__ pts3d,
+                                                     const float* __restrict__ obs2d, LMOpt o,
+                                                     double* __restrict__ pose_out,
+                                                     lorb_ba_summary* __restrict__ sums) {
   const int f = blockIdx.x;
-  const int t = threadIdx.x;
+  const int lane = threadIdx.x;
   const int r0 = res_off[f], r1 = res_off[f + 1];
   const double fx = intr[4 * f], fyv = intr[4 * f + 1], cx = intr[4 * f + 2], cy = intr[4 * f + 3];
-  if (t < 6) xs[t] = (double)pose_init[6 * f + t];
-  __syncthreads();
+  double xs[6], xn[6], sc[6], JtJ[21], Jtr[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) { xs[k] = (double)pose_init[6 * f + k]; xn[k] = xs[k]; sc[k] = 1.0; }
   if (r1 == r0) {
-    if (t < 6) pose_out[6 * f + t] = xs[t];
-    if (t == 0) { lorb_ba_summary z = {}; sums[f] = z; }
+    if (lane < 6) pose_out[6 * f + lane] = xs[lane];
+    if (lane == 0) { lorb_ba_summary z = {}; sums[f] = z; }
     return;
   }
   double radius = o.init_radius, df = 2.0;
   int iter = 0, n_success = 0, n_invalid = 0, term = LORB_TERM_NO_CONVERGENCE, last_successful = 1;
-  double initial_cost = 0.0;
-  if (t == 0) s_relin = 1;
-  __syncthreads();
+  double initial_cost = 0.0, cost = 0.0, gmax = 0.0, xnorm = 0.0;
+  bool relin = true;
   for (;;) {
-    if (s_relin) {
+    if (relin) {
       double v[28];
 #pragma unroll
       for (int k = 0; k < 28; ++k) v[k] = 0.0;
-      double pose[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) pose[k] = xs[k];
-      const lorb::RotJet R = lorb::rot_jet(pose);  // one frame: rotation state hoisted
-      for (int r = r0 + t; r < r1; r += 256) {
+      const lorb::RotJet R = lorb::rot_jet(xs);  // one frame: rotation state hoisted
+      for (int r = r0 + lane; r < r1; r += 64) {
         const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
         double rr[2], Jp[6], Jc[12];
-        residual_jac_s(R, pose + 3, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr, Jp, Jc);
+        residual_jac_s(R, xs + 3, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr, Jp, Jc);
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
@@ -2590,129 +2585,126 @@ __global__ __launch_bounds__(256) void k_ba_pose_only(const int32_t* __restrict_
         }
         v[27] += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
       }
-      block_sum<28>(v, sh);
-      if (t == 0) {
-        for (int k = 0; k < 21; ++k) JtJ[k] = v[k];
-        for (int k = 0; k < 6; ++k) Jtr[k] = v[21 + k];
-        s_cost = v[27];
-        double gm = 0.0, xn2 = 0.0;
-        for (int k = 0; k < 6; ++k) { gm = fmax(gm, fabs(xs[k] - (xs[k] + -Jtr[k]))); xn2 += xs[k] * xs[k]; }
-        s_gmax = gm;
-        s_xnorm = sqrt(xn2);
-        if (iter == 0) {
-          initial_cost = s_cost;
-          const int dg[6] = {0, 6, 11, 15, 18, 20};
-          for (int k = 0; k < 6; ++k) sc[k] = o.jacobi ? 1.0 / (1.0 + sqrt(JtJ[dg[k]])) : 1.0;
-        }
-        last_successful = 1;
-        s_relin = 0;
-      }
-      __syncthreads();
-    }
-    if (t == 0) {
-      s_flag = 0;
-      if (iter >= o.max_iter) { s_flag = 1; term = LORB_TERM_NO_CONVERGENCE; }
-      else if (last_successful && s_gmax <= o.gtol) { s_flag = 1; term = LORB_TERM_GRADIENT_TOL; }
-      else if (radius <= o.min_radius) { s_flag = 1; term = LORB_TERM_MIN_RADIUS; }
-      else {
-        iter++;
-        // (Js^T Js + D^2) y = Js^T r, D^2 = clamp(diag)/radius ; dense 6x6 Cholesky
-        double A[36], y[6];
-        for (int a = 0; a < 6; ++a) {
-          for (int b = 0; b < 6; ++b) A[6 * a + b] = JtJ[u21(a, b)] * sc[a] * sc[b];
-          y[a] = Jtr[a] * sc[a];
-        }
-        for (int a = 0; a < 6; ++a) A[7 * a] += fmin(fmax(A[7 * a], o.min_diag), o.max_diag) / radius;
-        bool ok = true;
-        for (int j = 0; j < 6 && ok; ++j) {
-          double dd = A[7 * j];
-          for (int k = 0; k < j; ++k) dd -= A[6 * j + k] * A[6 * j + k];
-          if (!(dd > 0.0)) { ok = false; break; }
-          const double l = sqrt(dd);
-          A[7 * j] = l;
-          for (int i = j + 1; i < 6; ++i) {
-            double s = A[6 * i + j];
-            for (int k = 0; k < j; ++k) s -= A[6 * i + k] * A[6 * j + k];
-            A[6 * i + j] = s / l;
-          }
-        }
-        double mcc = -1.0;
-        if (ok) {
-          for (int i = 0; i < 6; ++i) { double s = y[i]; for (int k = 0; k < i; ++k) s -= A[6 * i + k] * y[k]; y[i] = s / A[7 * i]; }
-          for (int i = 5; i >= 0; --i) { double s = y[i]; for (int k = i + 1; k < 6; ++k) s -= A[6 * k + i] * y[k]; y[i] = s / A[7 * i]; }
-          // model cost change = -(step.Js^T r + 0.5 step^T Js^T Js step), step = -y
-          double lin = 0.0, quad = 0.0;
-          for (int a = 0; a < 6; ++a) {
-            const double sa = -y[a];
-            lin += sa * Jtr[a] * sc[a];
-            for (int b = 0; b < 6; ++b) quad += sa * JtJ[u21(a, b)] * sc[a] * sc[b] * (-y[b]);
-          }
-          mcc = -(lin + 0.5 * quad);
-          for (int a = 0; a < 6; ++a) { step[a] = -y[a]; xn[a] = xs[a] + step[a] * sc[a]; }
-          ok = isfinite(mcc) && mcc > 0.0;
-        }
-        if (!ok) {
-          if (++n_invalid >= o.max_invalid) { s_flag = 1; term = LORB_TERM_FAILURE; }
-          else { radius /= df; df *= 2.0; last_successful = 0; s_flag = 2; }
-        } else {
-          n_invalid = 0;
-          s_new = mcc;  // stash model cost change
-          s_flag = 3;
-        }
-      }
-    }
-    __syncthreads();
-    if (s_flag == 1) break;
-    if (s_flag == 2) continue;
-    // candidate cost
-    double v[1] = {0.0};
-    double pose[6];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) pose[k] = xn[k];
-    const lorb::RotVal R = lorb::rot_val(pose);
-    for (int r = r0 + t; r < r1; r += 256) {
-      const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
-      double rr[2];
-      residual_s(R, pose + 3, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr);
-      v[0] += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
+      for (int k = 0; k < 28; ++k) v[k] = wave_sum(v[k]);
+#pragma unroll
+      for (int k = 0; k < 21; ++k) JtJ[k] = v[k];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) Jtr[k] = v[21 + k];
+      cost = v[27];
+      double gm = 0.0, xn2 = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { gm = fmax(gm, fabs(xs[k] - (xs[k] + -Jtr[k]))); xn2 += xs[k] * xs[k]; }
+      gmax = gm;
+      xnorm = sqrt(xn2);
+      if (iter == 0) {
+        initial_cost = cost;
+        const int dg[6] = {0, 6, 11, 15, 18, 20};
+#pragma unroll
+        for (int k = 0; k < 6; ++k) sc[k] = o.jacobi ? 1.0 / (1.0 + sqrt(JtJ[dg[k]])) : 1.0;
+      }
+      last_successful = 1;
+      relin = false;
     }
-    block_sum<1>(v, sh);
-    if (t == 0) {
-      const double mcc = s_new;
-      const double new_cost = isfinite(v[0]) ? v[0] : 1.7976931348623157e308;
-      double sn2 = 0.0;
-      for (int k = 0; k < 6; ++k) sn2 += (xs[k] - xn[k]) * (xs[k] - xn[k]);
-      s_flag = 0;
-      if (sqrt(sn2) <= o.ptol * (s_xnorm + o.ptol)) { s_flag = 1; term = LORB_TERM_PARAMETER_TOL; }
-      else {
-        const double cc = s_cost - new_cost;
-        if (fabs(cc) <= o.ftol * s_cost) { s_flag = 1; term = LORB_TERM_FUNCTION_TOL; }
-        else {
-          const double rel = cc / mcc;
-          if (rel > o.min_rel) {
-            for (int k = 0; k < 6; ++k) xs[k] = xn[k];
-            s_relin = 1;
-            n_success++;
-            const double tt = 2.0 * rel - 1.0;
-            radius = fmin(o.max_radius, radius / fmax(1.0 / 3.0, 1.0 - tt * tt * tt));
-            df = 2.0;
-          } else {
-            last_successful = 0;
-            radius /= df;
-            df *= 2.0;
-          }
-        }
+    if (iter >= o.max_iter) { term = LORB_TERM_NO_CONVERGENCE; break; }
+    if (last_successful && gmax <= o.gtol) { term = LORB_TERM_GRADIENT_TOL; break; }
+    if (radius <= o.min_radius) { term = LORB_TERM_MIN_RADIUS; break; }
+    iter++;
+    // (Js^T Js + D^2) y = Js^T r, D^2 = clamp(diag)/radius ; dense 6x6 Cholesky
+    double A[36], y[6];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+#pragma unroll
+      for (int b = 0; b < 6; ++b) A[6 * a + b] = JtJ[u21(a, b)] * sc[a] * sc[b];
+      y[a] = Jtr[a] * sc[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) A[7 * a] += fmin(fmax(A[7 * a], o.min_diag), o.max_diag) / radius;
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      double dd = A[7 * j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) dd -= A[6 * j + k] * A[6 * j + k];
+      ok = ok && dd > 0.0;
+      const double l = sqrt(dd);
+      A[7 * j] = l;
+#pragma unroll
+      for (int i = j + 1; i < 6; ++i) {
+        double sv = A[6 * i + j];
+#pragma unroll
+        for (int k = 0; k < j; ++k) sv -= A[6 * i + k] * A[6 * j + k];
+        A[6 * i + j] = sv / l;
       }
     }
-    __syncthreads();
-    if (s_flag == 1) break;
+    double mcc = -1.0;
+    if (ok) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) { double sv = y[i]; for (int k = 0; k < i; ++k) sv -= A[6 * i + k] * y[k]; y[i] = sv / A[7 * i]; }
+#pragma unroll
+      for (int i = 5; i >= 0; --i) { double sv = y[i]; for (int k = i + 1; k < 6; ++k) sv -= A[6 * k + i] * y[k]; y[i] = sv / A[7 * i]; }
+      // model cost change = -(step.Js^T r + 0.5 step^T Js^T Js step), step = -y
+      double lin = 0.0, quad = 0.0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const double sa = -y[a];
+        lin += sa * Jtr[a] * sc[a];
+#pragma unroll
+        for (int b = 0; b < 6; ++b) quad += sa * JtJ[u21(a, b)] * sc[a] * sc[b] * (-y[b]);
+      }
+      mcc = -(lin + 0.5 * quad);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) xn[a] = xs[a] + (-y[a]) * sc[a];
+      ok = isfinite(mcc) && mcc > 0.0;
+    }
+    if (!ok) {
+      if (++n_invalid >= o.max_invalid) { term = LORB_TERM_FAILURE; break; }
+      radius /= df; df *= 2.0; last_successful = 0;
+      continue;
+    }
+    n_invalid = 0;
+    // candidate cost
+    double cv = 0.0;
+    {
+      const lorb::RotVal R = lorb::rot_val(xn);
+      for (int r = r0 + lane; r < r1; r += 64) {
+        const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
+        double rr[2];
+        residual_s(R, xn + 3, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr);
+        cv += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
+      }
+    }
+    cv = wave_sum(cv);
+    const double new_cost = isfinite(cv) ? cv : 1.7976931348623157e308;
+    double sn2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) sn2 += (xs[k] - xn[k]) * (xs[k] - xn[k]);
+    if (sqrt(sn2) <= o.ptol * (xnorm + o.ptol)) { term = LORB_TERM_PARAMETER_TOL; break; }
+    const double cc = cost - new_cost;
+    if (fabs(cc) <= o.ftol * cost) { term = LORB_TERM_FUNCTION_TOL; break; }
+    const double rel = cc / mcc;
+    if (rel > o.min_rel) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) xs[k] = xn[k];
+      relin = true;
+      n_success++;
+      const double tt = 2.0 * rel - 1.0;
+      radius = fmin(o.max_radius, radius / fmax(1.0 / 3.0, 1.0 - tt * tt * tt));
+      df = 2.0;
+    } else {
+      last_successful = 0;
+      radius /= df;
+      df *= 2.0;
+    }
   }
-  if (t < 6) pose_out[6 * f + t] = xs[t];
-  if (t == 0) {
-    lorb_ba_summary s;
-    s.iterations = iter; s.successful_steps = n_success; s.termination = term; s.pad_ = 0;
-    s.initial_cost = initial_cost; s.final_cost = s_cost;
-    sums[f] = s;
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    if (lane == k) pose_out[6 * f + k] = xs[k];
+  if (lane == 0) {
+    lorb_ba_summary sm;
+    sm.iterations = iter; sm.successful_steps = n_success; sm.termination = term; sm.pad_ = 0;
+    sm.initial_cost = initial_cost; sm.final_cost = cost;
+    sums[f] = sm;
   }
 }
 
@@ -2769,7 +2761,7 @@ struct lorb_ba_plan {
   int min_bw = 1 << 30;  // narrowest band of a non-empty window (k_ba_chol_2s needs >= 15)
   // LORB_HOST_PHASE=1 (diagnostics): host time of the device builds' host phase (readback landed ->
   // k_db_gather launched), printed at destruction
-  double hp_us = 0.0;
+  double hp_us = 0.0, hp_sec[6] = {};
   int hp_n = 0;
   std::vector<BaWin> hwin;
   std::vector<void*> allocs;
@@ -2803,7 +2795,10 @@ struct lorb_ba_plan {
   int chol_kind = -1;         // last launched Cholesky: 0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s
   lorb_ba_devbuild* devb = nullptr;  // device-built plan (lorb_ba_plan_create_dev)
   ~lorb_ba_plan() {
-    if (hp_n) fprintf(stderr, "lorb_ba_plan: host phase %.2f us per device build (%d builds)\n", hp_us / hp_n, hp_n);
+    if (hp_n)
+      fprintf(stderr, "lorb_ba_plan: host phase %.2f us per device build (%d builds): checks %.2f order %.2f blocks %.2f "
+              "buffers %.2f staging %.2f launch %.2f\n", hp_us / hp_n, hp_n, hp_sec[0] / hp_n, hp_sec[1] / hp_n,
+              hp_sec[2] / hp_n, hp_sec[3] / hp_n, hp_sec[4] / hp_n, hp_sec[5] / hp_n);
     if (devb) {
       if (devb->pinned) (void)hipHostFree(devb->pinned);
       if (devb->up_host) (void)hipHostFree(devb->up_host);
@@ -4254,6 +4249,13 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   }();
   static const bool hp_log = [] { const char* e = getenv("LORB_HOST_PHASE"); return e && e[0] == '1'; }();
   const auto hp_t0 = std::chrono::steady_clock::now();
+  auto hp_last = hp_t0;
+  auto hp_mark = [&](int k) {
+    if (!hp_log) return;
+    const auto now = std::chrono::steady_clock::now();
+    P->hp_sec[k] += std::chrono::duration<double, std::micro>(now - hp_last).count();
+    hp_last = now;
+  };
   if (phase_rc != LORB_OK) {
     if (!P->comm) return phase_rc;
     lerr |= 64;
@@ -4309,6 +4311,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   if ((gerr & 16) || Pn < 0 || Pn > b.P_cap) return lorb::set_error(ctx, LORB_E_INVALID, "n_points %d outside [0, %d]", Pn, b.P_cap);
   if (kGB - gmaxk < 1)
     return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "a point with %d observations (device plans hold <= %d)", gmaxk, kGB - 1);
+  hp_mark(0);
   // 3. host: camera order, blocks, band, groups (order, band, activity from the global structure;
   //    the block pair lists from this rank's observations)
   std::vector<char> adj((size_t)C * C, 0);
@@ -4319,6 +4322,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     b.last_adj.swap(adj);
   }
   const std::vector<int>& map = b.last_map;
+  hp_mark(1);
   std::vector<int> inv(C);
   for (int c = 0; c < C; ++c) inv[map[c]] = c;
   P->cam_map.assign(1, map);
@@ -4365,6 +4369,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     if (bwid <= 48 && sizeof(double) * (size_t)env_w(48) <= (size_t)kLdsBudget) P->max_env_w = env_w(48);
     P->min_n16 = n16 > 0 ? n16 : (1 << 30);
   }
+  hp_mark(2);
   // grow-only structure buffers; the point-group kernels launch at capacity
   PBlk* pb = const_cast<PBlk*>(d.pblk);
   int2* pr = const_cast<int2*>(d.pairs);
@@ -4378,6 +4383,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   }
   P->grid_pblk = b.pblk_cap;
   LORB_TRY(up_alloc(P, (int)bps.size()));
+  hp_mark(3);
   // one upload (pinned staging, stream-ordered; the next build writes the staging only after its
   // own readback synchronised the stream).  C <= kDbArgC: no copy launch -- k_db_gather copies the
   // staging over the bus and takes the camera tables as kernel arguments (the step's host phase
@@ -4396,6 +4402,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     up_words = (int)((bytes + 3) / 4);
     if (C > kDbArgC) LORB_HIP(ctx, hipMemcpyAsync(b.up_dev, h, bytes, hipMemcpyHostToDevice, s));
   }
+  hp_mark(4);
   // 4. structure kernels: gather (+ initial values, point groups, zeros), the camera-major block
   //    offsets, the stable placement by camera, the block pair lists
   const int NB = lorb::ceil_div(K, 256);
@@ -4422,6 +4429,7 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
 #undef LORB_GATHER
     b.dirty = false;
     if (hp_log) {
+      hp_mark(5);
       P->hp_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - hp_t0).count();
       P->hp_n++;
     }
@@ -4599,7 +4607,7 @@ int lorb_ba_pose_only(lorb_ctx* ctx, const lorb_pose_problem_batch* prob,
   lorb::OutPack out(ctx);
   const int o_pose = out.add(sizeof(double) * 6 * nf), o_sum = out.add(sizeof(lorb_ba_summary) * nf);
   LORB_TRY(out.alloc());
-  hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(256), 0, ctx->stream, in.dev<int32_t>(i_roff), in.dev<float>(i_intr),
+  hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(64), 0, ctx->stream, in.dev<int32_t>(i_roff), in.dev<float>(i_intr),
                      in.dev<float>(i_pinit), in.dev<float>(i_pts), in.dev<float>(i_obs), to_dev_opt(opt),
                      out.dev<double>(o_pose), out.dev<lorb_ba_summary>(o_sum));
   LORB_CHECK_LAUNCH(ctx);

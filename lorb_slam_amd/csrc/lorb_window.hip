@@ -197,7 +197,7 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_cand_local(KpDev K, WinPara
                                                     const float* __restrict__ pxr, const int* __restrict__ plev,
                                                     const float* __restrict__ vcos, const uint4* __restrict__ pdesc,
                                                     int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
-                                                    int2* __restrict__ cand) {
+                                                    int2* __restrict__ cand, int stride = 0) {
   const int m = blockIdx.x * kCandWaves + (threadIdx.x >> 6);
   if (m >= np) return;
   int cnt = 0;
@@ -207,9 +207,9 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_cand_local(KpDev K, WinPara
     if (P.th != 1.0f) r *= P.th;
     const float rs = r * P.fp.scale_factors[lev];
     cnt = walk_candidates_wave<WRITE>(K, P.fp, px[m], py[m], rs, lev - 1, lev, pxr[m], rs, pdesc + 2 * (size_t)m,
-                                      WRITE ? cand + cand_off[m] : nullptr);
+                                      WRITE ? cand + (stride > 0 ? (size_t)m * stride : (size_t)cand_off[m]) : nullptr);
   }
-  if (!WRITE && (threadIdx.x & 63) == 0) cand_cnt[m] = cnt;
+  if ((!WRITE || stride > 0) && (threadIdx.x & 63) == 0) cand_cnt[m] = cnt;
 }
 
 // (a4) projection of last-frame map points + candidates, one wavefront per point
@@ -217,6 +217,8 @@ __device__ __forceinline__ float gemv3(const float* R, float a, float b, float c
   const double s = (double)R[0] * (double)a + (double)R[1] * (double)b + (double)R[2] * (double)c;
   return (float)(s + (double)t);
 }
+// WRITE: emit at cand_off[i] (two passes: count, scan, write); STRIDE > 0: one pass, emit at
+// i * STRIDE and write the count (STRIDE bounds a query's candidates: the frame's keypoint count)
 template <bool WRITE>
 __global__ __launch_bounds__(64 * kCandWaves) void k_cand_frame(KpDev K, WinParams P, int nl,
                                                     const uint8_t* __restrict__ has_mp,
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_cand_frame(KpDev K, WinPara
                                                     const int* __restrict__ loct,
                                                     const uint4* __restrict__ ldesc,
                                                     int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
-                                                    int2* __restrict__ cand) {
+                                                    int2* __restrict__ cand, int stride = 0) {
   const int i = blockIdx.x * kCandWaves + (threadIdx.x >> 6);
   if (i >= nl) return;
   int cnt = 0;
@@ -247,11 +249,11 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_cand_frame(KpDev K, WinPara
         else { mn = o - 1; mx = o + 1; }
         const float ur = u - P.fp.bf * invzc;
         cnt = walk_candidates_wave<WRITE>(K, P.fp, u, v, radius, mn, mx, ur, radius, ldesc + 2 * (size_t)i,
-                                          WRITE ? cand + cand_off[i] : nullptr);
+                                          WRITE ? cand + (stride > 0 ? (size_t)i * stride : (size_t)cand_off[i]) : nullptr);
       }
     }
   }
-  if (!WRITE && (threadIdx.x & 63) == 0) cand_cnt[i] = cnt;
+  if ((!WRITE || stride > 0) && (threadIdx.x & 63) == 0) cand_cnt[i] = cnt;
 }
 
 // exclusive scan of candidate counts (one workgroup, chunked)
@@ -268,6 +270,10 @@ __global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ cnt, int 
   }
   if (threadIdx.x == 0) off[n] = carry;
 }
+
+// one-pass candidate lists of the host-array matchers (a4, a5): up to this many entries (n_queries *
+// nk) the candidates go to a fixed stride per query
+constexpr size_t kCandStrided = size_t(1) << 20;
 
 // Candidate list of a windowed match: a query has at most nk candidates, so `bound` = n_queries *
 // nk entries always suffice.  Up to kCandBound entries that bound is allocated and the call needs
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __r
                                                   int* __restrict__ assign,  // nk output
                                                   int* __restrict__ bins,    // np scratch (MODE 1)
                                                   int* __restrict__ nulls,   // nk scratch (MODE 1)
-                                                  int* __restrict__ nmatches, int use_lds) {
+                                                  int* __restrict__ nmatches, int use_lds, int stride = 0) {
   // claim (nk) and res (np) live in LDS when they fit (dynamic shared memory), else in global
   extern __shared__ int s_dyn[];
   if (use_lds) { claim = s_dyn; res = s_dyn + nk; }
@@ -322,7 +328,8 @@ __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __r
     if (t == 0) s_changed = 0;
     __syncthreads();
     for (int m = t; m < np; m += 1024) {
-      const int a = cand_off[m], b = cand_off[m + 1];
+      // stride > 0: query m's candidates at [m stride, m stride + count), cand_off holds the counts
+      const int a = stride > 0 ? m * stride : cand_off[m], b = stride > 0 ? a + cand_off[m] : cand_off[m + 1];
       int bestDist = 256, bestIdx = -1;
       int bestLevel = -1, bestDist2 = 256, bestLevel2 = -1;
       for (int e = a; e < b; ++e) {
@@ -581,20 +588,31 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
   dassign = out.dev<int>(o_as);
   dnm = dassign + nk;
   const unsigned g = lorb::ceil_div(std::max(np, 1), kCandWaves);
-  if (np > 0) {
-    lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
-    hipLaunchKernelGGL(k_cand_local<false>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
-                       reinterpret_cast<const uint4*>(pd), cnt, (const int*)nullptr, (int2*)nullptr);
-  }
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, np, off);
+  const bool strided = (size_t)np * (size_t)nk <= kCandStrided;  // as lorb_search_by_projection_frame
   int2* cand;
-  LORB_TRY(alloc_candidates(ctx, off + np, (size_t)np * (size_t)nk, &cand));
-  if (np > 0)
-    hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
-                       reinterpret_cast<const uint4*>(pd), cnt, off, cand);
-  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), resolve_lds_bytes(np, nk), ctx->stream, np, nk, off, cand, K.octave, K.slot_state, lk,
+  if (strided) {
+    LORB_TRY(lorb::scratch_t(ctx, S_W9, std::max<size_t>((size_t)np * nk, 1), &cand));
+    if (np > 0) {
+      lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
+      hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
+                         reinterpret_cast<const uint4*>(pd), cnt, (const int*)nullptr, cand, nk);
+    }
+  } else {
+    if (np > 0) {
+      lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
+      hipLaunchKernelGGL(k_cand_local<false>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
+                         reinterpret_cast<const uint4*>(pd), cnt, (const int*)nullptr, (int2*)nullptr, 0);
+    }
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, np, off);
+    LORB_TRY(alloc_candidates(ctx, off + np, (size_t)np * (size_t)nk, &cand));
+    if (np > 0)
+      hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
+                         reinterpret_cast<const uint4*>(pd), cnt, off, cand, 0);
+  }
+  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), resolve_lds_bytes(np, nk), ctx->stream, np, nk,
+                     strided ? (const int*)cnt : (const int*)off, cand, K.octave, K.slot_state, lk,
                      (const float*)nullptr, (const float*)nullptr, res, claim, dassign, (int*)nullptr, (int*)nullptr, dnm,
-                     (int)(resolve_lds_bytes(np, nk) > 0));
+                     (int)(resolve_lds_bytes(np, nk) > 0), strided ? nk : 0);
   LORB_CHECK_LAUNCH(ctx);
   LORB_TRY(out.fetch());
   memcpy(assign, out.host<int>(o_as), sizeof(int) * nk);
@@ -658,20 +676,33 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
   dassign = out.dev<int>(o_as);
   dnm = dassign + nk;
   const unsigned g = lorb::ceil_div(std::max(nl, 1), kCandWaves);
-  if (nl > 0) {
-    lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
-    hipLaunchKernelGGL(k_cand_frame<false>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
-                       reinterpret_cast<const uint4*>(ld), cnt, (const int*)nullptr, (int2*)nullptr);
-  }
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, nl, off);
+  // a query has at most nk candidates: up to kCandBound entries one pass writes them at i * nk
+  // (no count pass, no scan); past it the count / scan / write passes size the list exactly
+  const bool strided = (size_t)nl * (size_t)nk <= kCandStrided;
   int2* cand;
-  LORB_TRY(alloc_candidates(ctx, off + nl, (size_t)nl * (size_t)nk, &cand));
-  if (nl > 0)
-    hipLaunchKernelGGL(k_cand_frame<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
-                       reinterpret_cast<const uint4*>(ld), cnt, off, cand);
-  hipLaunchKernelGGL(k_resolve<1>, dim3(1), dim3(1024), resolve_lds_bytes(nl, nk), ctx->stream, nl, nk, off, cand, K.octave, K.slot_state, lk,
+  if (strided) {
+    LORB_TRY(lorb::scratch_t(ctx, S_W9, std::max<size_t>((size_t)nl * nk, 1), &cand));
+    if (nl > 0) {
+      lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
+      hipLaunchKernelGGL(k_cand_frame<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
+                         reinterpret_cast<const uint4*>(ld), cnt, (const int*)nullptr, cand, nk);
+    }
+  } else {
+    if (nl > 0) {
+      lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
+      hipLaunchKernelGGL(k_cand_frame<false>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
+                         reinterpret_cast<const uint4*>(ld), cnt, (const int*)nullptr, (int2*)nullptr, 0);
+    }
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, cnt, nl, off);
+    LORB_TRY(alloc_candidates(ctx, off + nl, (size_t)nl * (size_t)nk, &cand));
+    if (nl > 0)
+      hipLaunchKernelGGL(k_cand_frame<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
+                         reinterpret_cast<const uint4*>(ld), cnt, off, cand, 0);
+  }
+  hipLaunchKernelGGL(k_resolve<1>, dim3(1), dim3(1024), resolve_lds_bytes(nl, nk), ctx->stream, nl, nk,
+                     strided ? (const int*)cnt : (const int*)off, cand, K.octave, K.slot_state, lk,
                      la, K.angle, res, claim, dassign, bins, nulls, dnm,
-                     (int)(resolve_lds_bytes(nl, nk) > 0));
+                     (int)(resolve_lds_bytes(nl, nk) > 0), strided ? nk : 0);
   LORB_CHECK_LAUNCH(ctx);
   LORB_TRY(out.fetch());
   memcpy(assign, out.host<int>(o_as), sizeof(int) * nk);
