@@ -4598,7 +4598,7 @@ int lorb_ba_pose_only(lorb_ctx* ctx, const lorb_pose_problem_batch* prob,
   const int nf = prob->n_frames;
   if (nf <= 0) return LORB_OK;
   const int nr = prob->res_off[nf];
-  // every input in one H2D copy, poses and summaries in one D2H copy
+  // every input in one pull, poses and summaries stored straight into pinned memory
   lorb::InPack in(ctx);
   const int i_roff = in.add_t(prob->res_off, (size_t)nf + 1), i_intr = in.add_t(prob->intr, (size_t)nf * 4),
             i_pinit = in.add_t(prob->pose_init, (size_t)nf * 6), i_pts = in.add_t(prob->pts3d, (size_t)nr * 3),
@@ -4606,7 +4606,7 @@ int lorb_ba_pose_only(lorb_ctx* ctx, const lorb_pose_problem_batch* prob,
   LORB_TRY(in.commit());
   lorb::OutPack out(ctx);
   const int o_pose = out.add(sizeof(double) * 6 * nf), o_sum = out.add(sizeof(lorb_ba_summary) * nf);
-  LORB_TRY(out.alloc());
+  LORB_TRY(out.alloc(true));  // the kernel stores poses and summaries into the mapped block
   hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(64), 0, ctx->stream, in.dev<int32_t>(i_roff), in.dev<float>(i_intr),
                      in.dev<float>(i_pinit), in.dev<float>(i_pts), in.dev<float>(i_obs), to_dev_opt(opt),
                      out.dev<double>(o_pose), out.dev<lorb_ba_summary>(o_sum));

@@ -781,13 +781,13 @@ int lorb_bf_match(lorb_ctx* ctx, int32_t np, const uint8_t* q, const int32_t* q_
   LORB_TRY(check_offsets(ctx, np, q_off, t_off));
   if (np == 0) return LORB_OK;
   const int nq = q_off[np], nt = t_off[np];
-  // both descriptor sets in one H2D copy, the four outputs in one D2H copy
+  // both descriptor sets in one pull, the four outputs stored straight into pinned memory
   lorb::InPack in(ctx);
   const int iq = in.add(q, (size_t)nq * 32), it = in.add(t, (size_t)nt * 32);
   LORB_TRY(in.commit());
   lorb::OutPack out(ctx);
   const int io = out.add(sizeof(int32_t) * ((size_t)nq * 3 + np));
-  LORB_TRY(out.alloc());
+  LORB_TRY(out.alloc(true));  // the finalize kernels write the four outputs with plain stores
   int32_t* o = out.dev<int32_t>(io);
   LORB_TRY(lorb_bf_match_dev(ctx, np, in.dev<uint8_t>(iq), q_off, in.dev<uint8_t>(it), t_off, o, o + nq, o + 2 * nq,
                              o + 3 * nq));

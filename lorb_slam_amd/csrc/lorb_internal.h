@@ -40,12 +40,14 @@ struct lorb_ctx {
   hipEvent_t spin_ev = nullptr;
   // lorb_ctx_ba_solver's solver (destroyed with the ctx)
   lorb_ba_solver* solver = nullptr;
-  // pinned staging of lorb::InPack / OutPack
+  // pinned (coherent, mapped) staging of lorb::InPack / OutPack and its device-side addresses
   void* io_in = nullptr;
+  void* io_in_dev = nullptr;
   size_t io_in_sz = 0;
   void* io_out = nullptr;
+  void* io_out_dev = nullptr;
   size_t io_out_sz = 0;
-  hipEvent_t io_ev = nullptr;  // the last InPack copy (the staging is rewritten only after it)
+  hipEvent_t io_ev = nullptr;  // the last InPack pull (the staging is rewritten only after it)
 };
 
 namespace lorb {
@@ -140,10 +142,13 @@ int upload_t(lorb_ctx* ctx, int slot, const T* host, size_t count, T** dev) {
 }
 
 // Host-array entry points (the per-frame calls a host caller issues, e.g. SearchByProjection on the
-// live tracking path): every input array is packed into ONE pinned staging buffer and moved by ONE
-// host-to-device copy; the outputs live in ONE device block that ONE device-to-host copy brings
-// back into pinned memory.  Usage: InPack::add() per input (before commit), commit() (pack + copy),
-// dev<T>(i) per input; OutPack::add() per output, alloc(), dev<T>(i), fetch() (copy + wait), then
+// live tracking path): every input array is packed into ONE pinned staging buffer that ONE pull
+// kernel on the ctx stream copies into a device block (a kernel reading the mapped host buffer: an
+// SDMA copy would cost the engine-to-queue hand-off, ~10 us on the tracking path); the outputs live
+// in ONE block: device memory that ONE device-to-host copy brings back, or (alloc(true)) the mapped
+// pinned buffer itself, written by the call's last kernel with plain stores (no atomics, no reads).
+// Usage: InPack::add() per input (before commit), commit() (pack + pull), dev<T>(i) per input;
+// OutPack::add() per output, alloc(direct), dev<T>(i), fetch() (copy if needed + wait), then
 // host<T>(i).  One of each per ctx is in use at a time (calls on one ctx are serialized).
 class InPack {
  public:
@@ -174,8 +179,8 @@ class OutPack {
     total += (bytes + 255) & ~size_t(255);
     return (int)parts.size() - 1;
   }
-  int alloc();
-  int fetch();  // one D2H copy into pinned memory, then waits for the stream
+  int alloc(bool direct = false);
+  int fetch();  // one D2H copy into pinned memory (unless direct), then waits for the stream
   template <typename T>
   T* dev(int i) const { return reinterpret_cast<T*>(static_cast<unsigned char*>(dbase) + parts[i].off); }
   template <typename T>
@@ -188,6 +193,7 @@ class OutPack {
   size_t total = 0;
   void* dbase = nullptr;
   void* hbase = nullptr;
+  bool direct = false;
 };
 
 // brackets one kernel launch with events when ctx->ktime is set

@@ -50,14 +50,28 @@ int upload(lorb_ctx* ctx, int slot, const void* host, size_t bytes, void** dev) 
   return LORB_OK;
 }
 
-static int pinned_grow(lorb_ctx* ctx, void** p, size_t* sz, size_t want) {
+// coherent + mapped: kernels read (InPack) and write (OutPack direct) it over PCIe, uncached on the
+// GPU side, so a call never sees a line of an earlier call's staging
+static int pinned_grow(lorb_ctx* ctx, void** p, void** pdev, size_t* sz, size_t want) {
   if (*sz >= want) return LORB_OK;
-  if (*p) (void)hipHostFree(*p);
-  *p = nullptr; *sz = 0;
+  if (*p) {
+    LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));  // no pull / direct write still in flight
+    (void)hipHostFree(*p);
+  }
+  *p = nullptr; *pdev = nullptr; *sz = 0;
   want += want / 4;
-  LORB_HIP(ctx, hipHostMalloc(p, want));
+  want = (want + 255) & ~size_t(255);
+  LORB_HIP(ctx, hipHostMalloc(p, want, hipHostMallocMapped | hipHostMallocCoherent));
+  LORB_HIP(ctx, hipHostGetDevicePointer(pdev, *p, 0));
   *sz = want;
   return LORB_OK;
+}
+
+// InPack's host-to-device move: 16-byte loads of the mapped staging (each lane one PCIe read in
+// flight per iteration), stores into the device block
+__global__ __launch_bounds__(256) void k_io_pull(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n16) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256)
+    dst[i] = src[i];
 }
 
 int InPack::commit() {
@@ -65,29 +79,37 @@ int InPack::commit() {
   // a call that failed after its commit may have left its copy in flight
   if (ctx->io_ev) LORB_HIP(ctx, hipEventSynchronize(ctx->io_ev));
   else LORB_HIP(ctx, hipEventCreateWithFlags(&ctx->io_ev, hipEventDisableTiming));
-  LORB_TRY(pinned_grow(ctx, &ctx->io_in, &ctx->io_in_sz, total));
+  LORB_TRY(pinned_grow(ctx, &ctx->io_in, &ctx->io_in_dev, &ctx->io_in_sz, total));
   unsigned char* h = static_cast<unsigned char*>(ctx->io_in);
   for (const Part& p : parts)
     if (p.bytes) std::memcpy(h + p.off, p.host, p.bytes);
   LORB_TRY(scratch(ctx, S_IO_IN, total, &base));
   size_t used = 0;
   for (const Part& p : parts) used = std::max(used, p.off + p.bytes);
-  LORB_HIP(ctx, hipMemcpyAsync(base, h, used, hipMemcpyHostToDevice, ctx->stream));
+  const size_t n16 = (used + 15) / 16;  // total is 256-aligned: the rounded tail stays inside
+  if (n16) {
+    const unsigned g = (unsigned)std::min<size_t>((n16 + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_io_pull, dim3(g), dim3(256), 0, ctx->stream, static_cast<const uint4*>(ctx->io_in_dev),
+                       static_cast<uint4*>(base), n16);
+    LORB_CHECK_LAUNCH(ctx);
+  }
   LORB_HIP(ctx, hipEventRecord(ctx->io_ev, ctx->stream));
   return LORB_OK;
 }
 
-int OutPack::alloc() {
-  LORB_TRY(scratch(ctx, S_IO_OUT, std::max<size_t>(total, 16), &dbase));
-  LORB_TRY(pinned_grow(ctx, &ctx->io_out, &ctx->io_out_sz, std::max<size_t>(total, 16)));
+int OutPack::alloc(bool direct_) {
+  direct = direct_;
+  LORB_TRY(pinned_grow(ctx, &ctx->io_out, &ctx->io_out_dev, &ctx->io_out_sz, std::max<size_t>(total, 16)));
   hbase = ctx->io_out;
+  if (direct) dbase = ctx->io_out_dev;
+  else LORB_TRY(scratch(ctx, S_IO_OUT, std::max<size_t>(total, 16), &dbase));
   return LORB_OK;
 }
 
 int OutPack::fetch() {
   size_t used = 0;
   for (const Part& p : parts) used = std::max(used, p.off + p.bytes);
-  if (used) LORB_HIP(ctx, hipMemcpyAsync(hbase, dbase, used, hipMemcpyDeviceToHost, ctx->stream));
+  if (used && !direct) LORB_HIP(ctx, hipMemcpyAsync(hbase, dbase, used, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, spin_sync(ctx));
   return LORB_OK;
 }

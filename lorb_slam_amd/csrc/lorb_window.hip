@@ -38,15 +38,20 @@ __device__ __forceinline__ int hamming(const uint4* a, const uint4* b) {
          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
-// (a7) grid: one workgroup; cell = PosInGrid; per-cell lists in keypoint (insertion) order
+// (a7) grid: one workgroup; cell = PosInGrid; per-cell lists in keypoint (insertion) order.  The
+// offsets and (up to kGridLds keypoints) the lists are built in LDS and stored once, coalesced.
+constexpr int kGridLds = 6144;
 __global__ __launch_bounds__(1024) void k_grid_build(const float* __restrict__ x, const float* __restrict__ y,
                                                      int n, lorb_frame_params fp,
                                                      int* __restrict__ cell_off,  // kCells+1
                                                      int* __restrict__ cell_idx, int* __restrict__ kp_cell) {
-  __shared__ int cnt[kCells];
+  __shared__ int off[kCells + 1];  // counts, then offsets
   __shared__ int cur[kCells];
+  __shared__ int s_idx[kGridLds];
+  const bool lds = n <= kGridLds;
+  int* idx = lds ? s_idx : cell_idx;
   const int t = threadIdx.x;
-  for (int c = t; c < kCells; c += 1024) cnt[c] = 0;
+  for (int c = t; c < kCells; c += 1024) off[c] = 0;
   __syncthreads();
   for (int i = t; i < n; i += 1024) {
     const int px = (int)roundf((x[i] - fp.min_x) * fp.grid_w_inv);
@@ -54,35 +59,41 @@ __global__ __launch_bounds__(1024) void k_grid_build(const float* __restrict__ x
     int c = -1;
     if (!(px < 0 || px >= LORB_GRID_COLS || py < 0 || py >= LORB_GRID_ROWS)) c = px * LORB_GRID_ROWS + py;
     kp_cell[i] = c;
-    if (c >= 0) atomicAdd(&cnt[c], 1);
+    if (c >= 0) atomicAdd(&off[c], 1);
   }
   __syncthreads();
   {  // 3072-entry exclusive scan: three consecutive cells per thread
     static_assert(kCells == 3 * 1024, "grid scan assumes 64 x 48 cells");
     __shared__ int wsum[16];
     const int c0 = 3 * t;
-    const int a = cnt[c0], b = cnt[c0 + 1], c = cnt[c0 + 2];
+    const int a = off[c0], b = off[c0 + 1], c = off[c0 + 2];
     int tot;
     const int ex = lorb::block_excl_scan_1024(a + b + c, wsum, &tot);
-    cell_off[c0] = ex; cell_off[c0 + 1] = ex + a; cell_off[c0 + 2] = ex + a + b;
+    off[c0] = ex; off[c0 + 1] = ex + a; off[c0 + 2] = ex + a + b;
     cur[c0] = ex; cur[c0 + 1] = ex + a; cur[c0 + 2] = ex + a + b;
-    if (t == 1023) cell_off[kCells] = tot;
+    if (t == 1023) off[kCells] = tot;
   }
   __syncthreads();
   for (int i = t; i < n; i += 1024) {
     const int c = kp_cell[i];
-    if (c >= 0) cell_idx[atomicAdd(&cur[c], 1)] = i;
+    if (c >= 0) idx[atomicAdd(&cur[c], 1)] = i;
   }
   __syncthreads();
   // restore insertion (index) order inside every cell: cells hold a handful of entries
   for (int c = t; c < kCells; c += 1024) {
-    const int a = cell_off[c], b = cell_off[c + 1];
+    const int a = off[c], b = off[c + 1];
     for (int i = a + 1; i < b; ++i) {
-      const int v = cell_idx[i];
+      const int v = idx[i];
       int j = i - 1;
-      while (j >= a && cell_idx[j] > v) { cell_idx[j + 1] = cell_idx[j]; --j; }
-      cell_idx[j + 1] = v;
+      while (j >= a && idx[j] > v) { idx[j + 1] = idx[j]; --j; }
+      idx[j + 1] = v;
     }
+  }
+  for (int c = t; c <= kCells; c += 1024) cell_off[c] = off[c];
+  if (lds) {
+    __syncthreads();
+    const int tot = off[kCells];
+    for (int i = t; i < tot; i += 1024) cell_idx[i] = s_idx[i];
   }
 }
 
@@ -219,17 +230,12 @@ __device__ __forceinline__ float gemv3(const float* R, float a, float b, float c
 }
 // WRITE: emit at cand_off[i] (two passes: count, scan, write); STRIDE > 0: one pass, emit at
 // i * STRIDE and write the count (STRIDE bounds a query's candidates: the frame's keypoint count)
+// the candidates of last-frame point i (one wavefront; returns the count, written at `out` if WRITE)
 template <bool WRITE>
-__global__ __launch_bounds__(64 * kCandWaves) void k_cand_frame(KpDev K, WinParams P, int nl,
-                                                    const uint8_t* __restrict__ has_mp,
-                                                    const uint8_t* __restrict__ outlier,
-                                                    const float* __restrict__ pos,
-                                                    const int* __restrict__ loct,
-                                                    const uint4* __restrict__ ldesc,
-                                                    int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
-                                                    int2* __restrict__ cand, int stride = 0) {
-  const int i = blockIdx.x * kCandWaves + (threadIdx.x >> 6);
-  if (i >= nl) return;
+__device__ __forceinline__ int cand_frame_one(const KpDev& K, const WinParams& P, int i,
+                                              const uint8_t* __restrict__ has_mp, const uint8_t* __restrict__ outlier,
+                                              const float* __restrict__ pos, const int* __restrict__ loct,
+                                              const uint4* __restrict__ ldesc, int2* out) {
   int cnt = 0;
   if (has_mp[i] && !(outlier && outlier[i])) {
     const float X = pos[3 * i], Y = pos[3 * i + 1], Z = pos[3 * i + 2];
@@ -248,11 +254,26 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_cand_frame(KpDev K, WinPara
         else if (P.mode_backward) { mn = 0; mx = o; }
         else { mn = o - 1; mx = o + 1; }
         const float ur = u - P.fp.bf * invzc;
-        cnt = walk_candidates_wave<WRITE>(K, P.fp, u, v, radius, mn, mx, ur, radius, ldesc + 2 * (size_t)i,
-                                          WRITE ? cand + (stride > 0 ? (size_t)i * stride : (size_t)cand_off[i]) : nullptr);
+        cnt = walk_candidates_wave<WRITE>(K, P.fp, u, v, radius, mn, mx, ur, radius, ldesc + 2 * (size_t)i, out);
       }
     }
   }
+  return cnt;
+}
+template <bool WRITE>
+__global__ __launch_bounds__(64 * kCandWaves) void k_cand_frame(KpDev K, WinParams P, int nl,
+                                                    const uint8_t* __restrict__ has_mp,
+                                                    const uint8_t* __restrict__ outlier,
+                                                    const float* __restrict__ pos,
+                                                    const int* __restrict__ loct,
+                                                    const uint4* __restrict__ ldesc,
+                                                    int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
+                                                    int2* __restrict__ cand, int stride = 0) {
+  const int i = blockIdx.x * kCandWaves + (threadIdx.x >> 6);
+  if (i >= nl) return;
+  const int cnt = cand_frame_one<WRITE>(
+      K, P, i, has_mp, outlier, pos, loct, ldesc,
+      WRITE ? cand + (stride > 0 ? (size_t)i * stride : (size_t)cand_off[i]) : nullptr);
   if ((!WRITE || stride > 0) && (threadIdx.x & 63) == 0) cand_cnt[i] = cnt;
 }
 
@@ -297,24 +318,19 @@ inline size_t resolve_lds_bytes(int np, int nk) {
 }
 
 // Jacobi fixpoint resolver (one workgroup per call).  MODE 0 = a5 (best/second + ratio test),
-// MODE 1 = a4 (best only + rotation histogram / ComputeThreeMaxima null-out).
+// MODE 1 = a4 (best only + rotation histogram / ComputeThreeMaxima null-out).  out != null: assign
+// and the count are also copied there (nk + 1 ints) at the end.
 template <int MODE>
-__global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __restrict__ cand_off,
-                                                  const int2* __restrict__ cand,
-                                                  const int* __restrict__ kp_octave,
-                                                  const uint8_t* __restrict__ slot_state,
-                                                  const uint8_t* __restrict__ pt_locked,
-                                                  const float* __restrict__ last_angle,
-                                                  const float* __restrict__ cur_angle,
-                                                  int* __restrict__ res,     // np: accepted slot or -1
-                                                  int* __restrict__ claim,   // nk (global scratch)
-                                                  int* __restrict__ assign,  // nk output
-                                                  int* __restrict__ bins,    // np scratch (MODE 1)
-                                                  int* __restrict__ nulls,   // nk scratch (MODE 1)
-                                                  int* __restrict__ nmatches, int use_lds, int stride = 0) {
-  // claim (nk) and res (np) live in LDS when they fit (dynamic shared memory), else in global
-  extern __shared__ int s_dyn[];
-  if (use_lds) { claim = s_dyn; res = s_dyn + nk; }
+__device__ __forceinline__ void resolve_run(int np, int nk, const int* cand_off, const int2* __restrict__ cand,
+                                            const uint8_t* __restrict__ pt_locked,
+                                            const float* __restrict__ last_angle,
+                                            const float* __restrict__ cur_angle,
+                                            int* res,                  // np: accepted slot or -1
+                                            int* claim,                // nk
+                                            int* __restrict__ assign,  // nk output
+                                            int* __restrict__ bins,    // np scratch (MODE 1)
+                                            int* __restrict__ nulls,   // nk scratch (MODE 1)
+                                            int* __restrict__ nmatches, int stride, int* __restrict__ out) {
   __shared__ int s_changed;
   __shared__ int hist[LORB_HISTO_LENGTH];
   __shared__ int s_ind[3];
@@ -324,6 +340,21 @@ __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __r
   for (int m = t; m < np; m += 1024) res[m] = -2;  // "never computed"
   if (t == 0) { s_acc = 0; s_rej = 0; }
   __syncthreads();
+  // np <= 1024 (one query per thread): the first kRegCand candidates of the thread's query are
+  // loaded once, all together, into registers; every round then reads them (and their claims, from
+  // LDS) without a global round trip per candidate.  Later candidates, if any, come from global.
+  constexpr int kRegCand = 8;
+  const bool regc = np <= 1024;
+  int2 rc[kRegCand];
+  int rn = 0;
+  if (regc && t < np) {
+    const int a = stride > 0 ? t * stride : cand_off[t], b = stride > 0 ? a + cand_off[t] : cand_off[t + 1];
+    rn = min(b - a, kRegCand);
+    if (rn > 0) {
+#pragma unroll
+      for (int k = 0; k < kRegCand; ++k) rc[k] = cand[a + min(k, rn - 1)];
+    }
+  }
   for (int round = 0; round <= np; ++round) {
     if (t == 0) s_changed = 0;
     __syncthreads();
@@ -332,10 +363,10 @@ __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __r
       const int a = stride > 0 ? m * stride : cand_off[m], b = stride > 0 ? a + cand_off[m] : cand_off[m + 1];
       int bestDist = 256, bestIdx = -1;
       int bestLevel = -1, bestDist2 = 256, bestLevel2 = -1;
-      for (int e = a; e < b; ++e) {
-        const int2 cd = cand[e];  // (slot, distance | octave << 16); pre-call locked slots removed
+      // candidates in list order (ties keep the first, as the reference's loop)
+      auto consider = [&](const int2 cd) {  // (slot, distance | octave << 16); pre-call locked slots removed
         const int j = cd.x;
-        if ((int)claim[j] < m) continue;  // locked by an earlier point during this call
+        if ((int)claim[j] < m) return;  // locked by an earlier point during this call
         const int dist = cd.y & 0xffff;
         if (MODE == 0) {
           const int oc = cd.y >> 16;
@@ -348,7 +379,15 @@ __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __r
         } else {
           if (dist < bestDist) { bestDist = dist; bestIdx = j; }
         }
+      };
+      int e0 = a;
+      if (regc) {
+#pragma unroll
+        for (int k = 0; k < kRegCand; ++k)
+          if (k < rn) consider(rc[k]);
+        e0 = a + rn;
       }
+      for (int e = e0; e < b; ++e) consider(cand[e]);
       int r = -1;
       if (bestDist <= LORB_TH_HIGH) {
         r = bestIdx;
@@ -412,6 +451,26 @@ __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __r
   }
   __syncthreads();
   if (t == 0) *nmatches = s_acc - s_rej;
+  if (out) {  // the host-array calls: assign + count into the mapped result block, plain stores
+    for (int c = t; c < nk; c += 1024) out[c] = assign[c];
+    if (t == 0) out[nk] = s_acc - s_rej;
+  }
+}
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __restrict__ cand_off,
+                                                  const int2* __restrict__ cand,
+                                                  const uint8_t* __restrict__ pt_locked,
+                                                  const float* __restrict__ last_angle,
+                                                  const float* __restrict__ cur_angle,
+                                                  int* __restrict__ res, int* __restrict__ claim,
+                                                  int* __restrict__ assign, int* __restrict__ bins,
+                                                  int* __restrict__ nulls, int* __restrict__ nmatches, int use_lds,
+                                                  int stride = 0, int* __restrict__ out = nullptr) {
+  // claim (nk) and res (np) live in LDS when they fit (dynamic shared memory), else in global
+  extern __shared__ int s_dyn[];
+  if (use_lds) { claim = s_dyn; res = s_dyn + nk; }
+  resolve_run<MODE>(np, nk, cand_off, cand, pt_locked, last_angle, cur_angle, res, claim, assign, bins, nulls,
+                    nmatches, stride, out);
 }
 
 // (a8) Frame::IsInFrustum + PredictScale, one thread per map point
@@ -516,7 +575,7 @@ namespace {
 using lorb::inv4_lu32f;
 
 // a frame's keypoints (Frame::mvKeysUn, mDescriptors, slot states) for the host-array entry points:
-// packed into their InPack (one H2D copy for every input), then the device grid built
+// packed into their InPack (one pull for every input), then the device grid built
 struct KpParts {
   int x, y, ang, oc, desc, ur, ss;
   std::vector<uint8_t> zeros;
@@ -559,7 +618,7 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
     if (pts->track_in_view[i] && !(pts->is_bad && pts->is_bad[i]) &&
         (pts->pred_level[i] < 0 || pts->pred_level[i] >= LORB_MAX_LEVELS))
       return lorb::set_error(ctx, LORB_E_INVALID, "point %d: predicted level %d out of range", i, pts->pred_level[i]);
-  // every input in one H2D copy, the result in one D2H copy
+  // every input in one pull, the result stored straight into pinned memory by k_resolve
   lorb::InPack in(ctx);
   KpParts kp;
   kps_add(in, kps, slot_state, kp);
@@ -582,11 +641,11 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 1, (size_t)np + 1, &off));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 2, (size_t)np + 1, &res));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 3, (size_t)nk + 1, &claim));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 4, (size_t)nk + 1, &dassign));
+  dnm = dassign + nk;
   lorb::OutPack out(ctx);
   const int o_as = out.add(sizeof(int) * ((size_t)nk + 1));
-  LORB_TRY(out.alloc());
-  dassign = out.dev<int>(o_as);
-  dnm = dassign + nk;
+  LORB_TRY(out.alloc(true));  // k_resolve writes assign + count into the mapped block
   const unsigned g = lorb::ceil_div(std::max(np, 1), kCandWaves);
   const bool strided = (size_t)np * (size_t)nk <= kCandStrided;  // as lorb_search_by_projection_frame
   int2* cand;
@@ -610,9 +669,9 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
                          reinterpret_cast<const uint4*>(pd), cnt, off, cand, 0);
   }
   hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), resolve_lds_bytes(np, nk), ctx->stream, np, nk,
-                     strided ? (const int*)cnt : (const int*)off, cand, K.octave, K.slot_state, lk,
+                     strided ? (const int*)cnt : (const int*)off, cand, lk,
                      (const float*)nullptr, (const float*)nullptr, res, claim, dassign, (int*)nullptr, (int*)nullptr, dnm,
-                     (int)(resolve_lds_bytes(np, nk) > 0), strided ? nk : 0);
+                     (int)(resolve_lds_bytes(np, nk) > 0), strided ? nk : 0, out.dev<int>(o_as));
   LORB_CHECK_LAUNCH(ctx);
   LORB_TRY(out.fetch());
   memcpy(assign, out.host<int>(o_as), sizeof(int) * nk);
@@ -649,7 +708,7 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
   const float tlc2 = (float)(s2 + (double)L[11]);
   P.mode_forward = tlc2 > cur->b;
   P.mode_backward = -tlc2 > cur->b;
-  // every input in one H2D copy, the result in one D2H copy
+  // every input in one pull, the result stored straight into pinned memory by k_resolve
   lorb::InPack in(ctx);
   KpParts kp;
   kps_add(in, cur_kps, cur_slot_state, kp);
@@ -670,11 +729,11 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 3, (size_t)nk + 1, &claim));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 5, (size_t)nl + 1, &bins));
   LORB_TRY(lorb::scratch_t(ctx, S_WX + 6, (size_t)nk + 1, &nulls));
+  LORB_TRY(lorb::scratch_t(ctx, S_WX + 4, (size_t)nk + 1, &dassign));
+  dnm = dassign + nk;
   lorb::OutPack out(ctx);
   const int o_as = out.add(sizeof(int) * ((size_t)nk + 1));
-  LORB_TRY(out.alloc());
-  dassign = out.dev<int>(o_as);
-  dnm = dassign + nk;
+  LORB_TRY(out.alloc(true));  // k_resolve writes assign + count into the mapped block
   const unsigned g = lorb::ceil_div(std::max(nl, 1), kCandWaves);
   // a query has at most nk candidates: up to kCandBound entries one pass writes them at i * nk
   // (no count pass, no scan); past it the count / scan / write passes size the list exactly
@@ -700,9 +759,9 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
                          reinterpret_cast<const uint4*>(ld), cnt, off, cand, 0);
   }
   hipLaunchKernelGGL(k_resolve<1>, dim3(1), dim3(1024), resolve_lds_bytes(nl, nk), ctx->stream, nl, nk,
-                     strided ? (const int*)cnt : (const int*)off, cand, K.octave, K.slot_state, lk,
+                     strided ? (const int*)cnt : (const int*)off, cand, lk,
                      la, K.angle, res, claim, dassign, bins, nulls, dnm,
-                     (int)(resolve_lds_bytes(nl, nk) > 0), strided ? nk : 0);
+                     (int)(resolve_lds_bytes(nl, nk) > 0), strided ? nk : 0, out.dev<int>(o_as));
   LORB_CHECK_LAUNCH(ctx);
   LORB_TRY(out.fetch());
   memcpy(assign, out.host<int>(o_as), sizeof(int) * nk);
@@ -813,7 +872,7 @@ int lorb_track_local_map_dev(lorb_ctx* ctx, const lorb_frame_params* frame, cons
     hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, d_in_view, pts->is_bad, tx,
                        tx + np, tx + 2 * np, d_level, tx + 3 * np, reinterpret_cast<const uint4*>(pts->desc), cnt, off,
                        cand);
-  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), resolve_lds_bytes(np, nk), ctx->stream, np, nk, off, cand, K.octave, K.slot_state,
+  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), resolve_lds_bytes(np, nk), ctx->stream, np, nk, off, cand,
                      pts->locked, (const float*)nullptr, (const float*)nullptr, res, claim, d_assign, (int*)nullptr,
                      (int*)nullptr, d_nmatches,
                      (int)(resolve_lds_bytes(np, nk) > 0));

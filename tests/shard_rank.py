@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 
 from lorb_slam_amd import _abi as A  # noqa: E402
 from lorb_slam_amd import shard, synth  # noqa: E402
-from lorb_slam_amd.runtime import BAPlan, Comm, Context  # noqa: E402
+from lorb_slam_amd.runtime import BAPlan, Comm, Context, LorbError  # noqa: E402
 
 WINDOWS = [dict(seed=3, n_kf=12, n_pts=1500, n_fixed=2, fixed_obs_per_kf=150),
            dict(seed=7, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400)]
@@ -107,6 +107,37 @@ def main():
         plan.close()
         for a in arrays.values():
             a.free()
+    # a build failure on ONE rank is collective: the other rank's build reaches the exchange, and both
+    # return the error (neither is left waiting); the plan then rebuilds and solves normally
+    sh = shards[0]
+    arrays = BAPlanDev.upload(ctx, sh, extra_points=11, extra_obs=97)
+    plan = BAPlanDev(ctx, arrays, len(sh["pose_init"]), len(sh["fixed_pose"]), sh["intr"], comm=comm)
+    over = dict(arrays)  # rank 1: a live observation count beyond its capacity (seen on the device)
+    n_live = len(sh["obs_point"]) + (97 + 5 if rank == 1 else 0)
+    over["n_obs"] = ctx.to_device(np.array([n_live], np.int32))
+    errs = []
+    try:
+        plan.update(over)
+        errs.append("")
+    except LorbError as e:
+        errs.append(str(e))
+    over["n_obs"].free()
+    plan.win.n_poses += rank  # rank 1: a window shape that differs from the plan's (seen on the host)
+    try:
+        plan.update(arrays)
+        errs.append("")
+    except LorbError as e:
+        errs.append(str(e))
+    plan.win.n_poses -= rank
+    plan.update(arrays)
+    plan.solve(opt)
+    P, X, S = plan.read()
+    res["fail_msgs"] = np.array(errs)
+    res["fail_pose"], res["fail_pts"] = P[0], X[0]
+    res["fail_iters"] = np.array([S[0]["iterations"], S[0]["successful_steps"]])
+    plan.close()
+    for a in arrays.values():
+        a.free()
     comm.close()
     ctx.close()
     np.savez(out, **res)

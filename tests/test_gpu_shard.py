@@ -104,6 +104,16 @@ def test_sharded_two_ranks_host_transport(ctx, tmp_path):
             X[a:b] = R[r][f"dev_pts{i}"]
         assert close(X, Xg[i])
         assert R[0][f"dev_iters{i}"][0] == Sg[i]["iterations"]
+    # one rank over its capacity, then one rank with a wrong shape: both ranks return each error
+    for r in range(2):
+        m = list(R[r]["fail_msgs"])
+        assert len(m) == 2 and all(m), (r, m)
+        assert "capacity" in m[0], (r, m[0])
+        assert "shape" in m[1] and ("this rank" if r == 1 else "another rank") in m[1], (r, m[1])
+    # ... and the plan rebuilds and solves as before
+    assert np.array_equal(R[0]["fail_pose"], R[1]["fail_pose"])
+    assert close(R[0]["fail_pose"], R[0]["dev_pose0"], 1e-9)
+    assert list(R[0]["fail_iters"]) == list(R[0]["dev_iters0"])
 
 
 def test_sharded_dev_rccl_world1(ctx):

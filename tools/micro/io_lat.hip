@@ -12,6 +12,8 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
 __global__ void k_empty(int* p) { if (threadIdx.x == 0 && p) p[0] += 1; }
+struct BigArgs { int v[200]; };
+__global__ void k_bigargs(int* p, BigArgs a) { if (threadIdx.x == 0 && p) p[0] += a.v[threadIdx.x]; }
 
 // one workgroup: copy `n` dwords from (mapped host) src to dst, then write `m` dwords back to out
 __global__ __launch_bounds__(1024) void k_inout(const int* __restrict__ src, int* __restrict__ dev, int n,
@@ -74,5 +76,23 @@ int main() {
     spin(ev, s);
   });
   bench("host memcpy 30KB into pinned", [&] { memcpy(h_pin_in, pg_in.data(), IN); });
+  // host-side cost of reading a 50 x 50 int matrix column-wise (the device plan build's covisibility
+  // fill) from pinned vs pageable memory, and of one launch with 800 bytes of arguments
+  {
+    int* hp = nullptr;
+    CK(hipHostMalloc(&hp, 4 * 2600));
+    std::vector<int> pv(2600, 1);
+    for (int i = 0; i < 2600; ++i) hp[i] = 1;
+    volatile int sink = 0;
+    auto colsum = [&](const int* m) { int s = 0; for (int i = 0; i < 50; ++i) for (int j = i + 1; j < 50; ++j) s += m[j * 50 + i]; sink = s; };
+    bench("column walk of 50x50 ints, pinned", [&] { colsum(hp); });
+    bench("column walk of 50x50 ints, pageable", [&] { colsum(pv.data()); });
+    BigArgs ba{};
+    bench("launch only (8-byte args)", [&] { hipLaunchKernelGGL(k_empty, 1, 64, 0, s, nullptr); });
+    (void)hipStreamSynchronize(s);
+    bench("launch only (808-byte args)", [&] { hipLaunchKernelGGL(k_bigargs, 1, 64, 0, s, nullptr, ba); });
+    (void)hipStreamSynchronize(s);
+    (void)hipHostFree(hp);
+  }
   return 0;
 }
