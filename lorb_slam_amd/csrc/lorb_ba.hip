@@ -98,6 +98,60 @@ __device__ __forceinline__ double wave_max(double v) {
   v = fmax(v, dpp_d<0xB1>(v));
   return v;
 }
+// Reduce-scatter of N <= 32 per-lane values (padded to 32): each step halves the values a lane
+// keeps -- the half its partner does not keep goes to the partner, which adds it to its own copy --
+// so 32 sums cost 31 exchanges instead of 32 full butterflies.  Partners: lane ^ 32, ^ 16
+// (permlane swaps of two different registers), ^ 8 (row_ror:8), the mirrored lane of the half row
+// (row_half_mirror: the other quad), ^ 2; a last ^ 1 step completes every sum, and sum k ends in
+// lanes 2k, 2k + 1, from where v_readlane broadcasts it.  Every lane returns all N sums.
+__device__ __forceinline__ double readlane_d(double v, int l);
+__device__ __forceinline__ void swap_pair(double x, double y, bool w32, double& r0, double& r1) {
+  const unsigned long long ux = __double_as_longlong(x), uy = __double_as_longlong(y);
+  const unsigned xl = (unsigned)ux, xh = (unsigned)(ux >> 32), yl = (unsigned)uy, yh = (unsigned)(uy >> 32);
+  const auto l = w32 ? __builtin_amdgcn_permlane32_swap(xl, yl, false, false)
+                     : __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+  const auto h = w32 ? __builtin_amdgcn_permlane32_swap(xh, yh, false, false)
+                     : __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+  r0 = __longlong_as_double(((unsigned long long)h[0] << 32) | l[0]);
+  r1 = __longlong_as_double(((unsigned long long)h[1] << 32) | l[1]);
+}
+template <int CTRL, int BIT, int H>
+__device__ __forceinline__ void rs_dpp_step(double (&v)[32], int lane) {
+  const bool up = (lane >> BIT) & 1;
+#pragma unroll
+  for (int k = 0; k < H; ++k) {
+    const double keep = up ? v[k + H] : v[k], send = up ? v[k] : v[k + H];
+    v[k] = keep + dpp_d<CTRL>(send);
+  }
+}
+// in place: v[0 .. N) in, the N sums out in every lane (v[N .. 32) are scratch)
+template <int N>
+__device__ __forceinline__ void wave_sum_all(double (&v)[32]) {
+  static_assert(N <= 32, "at most 32 values");
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = N; k < 32; ++k) v[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {  // ^32: lanes < 32 keep k, lanes >= 32 keep k + 16
+    double a, b;
+    swap_pair(v[k], v[k + 16], true, a, b);
+    v[k] = a + b;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {   // ^16 (rows of 16): even rows keep k, odd rows k + 8
+    double a, b;
+    swap_pair(v[k], v[k + 8], false, a, b);
+    v[k] = a + b;
+  }
+  rs_dpp_step<0x128, 3, 4>(v, lane);  // row_ror:8 = ^8
+  rs_dpp_step<0x141, 2, 2>(v, lane);  // row_half_mirror: the other quad of the half row
+  rs_dpp_step<0x4E, 1, 1>(v, lane);   // quad_perm [2,3,0,1] = ^2
+  v[0] += dpp_d<0xB1>(v[0]);          // quad_perm [1,0,3,2] = ^1
+  // lane l now holds sum (16 b5 + 8 b4 + 4 b3 + 2 b2 + b1) = l >> 1
+  const double r = v[0];
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = readlane_d(r, 2 * k);
+}
 __device__ __forceinline__ int wave_isum(int v) {
   {
     const auto p = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
@@ -2540,9 +2594,10 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
 // ------------------------------------------------------------------------------------------
 // pose-only LM (BA::ProjectPoseOptimization), one workgroup per frame, whole solve in-kernel
 // One WAVEFRONT per frame (a12 is the per-frame tracking call: a few hundred residuals): lanes stride
-// the frame's residuals, every reduction is a wave butterfly (wave_sum: every lane ends with the same
-// bits), and every lane carries the frame's LM state and solves the 6 x 6 system redundantly, so an
-// iteration has no LDS traffic and no barrier.
+// the frame's residuals (the first 256 held in registers for the whole solve), the 28 normal-equation
+// sums are one wave reduce-scatter (wave_sum_all), the candidate cost a butterfly (every lane ends
+// with the same bits), and every lane carries the frame's LM state and solves the 6 x 6 system
+// redundantly, so an iteration has no LDS traffic and no barrier.
 __global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__ res_off,
                                                      const float* __restrict__ intr,
                                                      const float* __restrict__ pose_init,
@@ -2566,16 +2621,26 @@ __global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__
   int iter = 0, n_success = 0, n_invalid = 0, term = LORB_TERM_NO_CONVERGENCE, last_successful = 1;
   double initial_cost = 0.0, cost = 0.0, gmax = 0.0, xnorm = 0.0;
   bool relin = true;
+  // the lane's first kPoC residuals (r0 + lane + 64 q) stay in registers for the whole solve; a frame
+  // with more than 64 kPoC residuals reads the rest from memory in each pass (same per-lane order)
+  constexpr int kPoC = 4;
+  double cX[kPoC][3], cuv[kPoC][2];
+#pragma unroll
+  for (int q = 0; q < kPoC; ++q) {
+    const int r = min(r0 + lane + 64 * q, r1 - 1);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cX[q][k] = pts3d[3 * r + k];
+    cuv[q][0] = obs2d[2 * r]; cuv[q][1] = obs2d[2 * r + 1];
+  }
   for (;;) {
     if (relin) {
-      double v[28];
+      double v[32];  // 21 JtJ + 6 Jtr + cost (+ wave_sum_all's padding)
 #pragma unroll
       for (int k = 0; k < 28; ++k) v[k] = 0.0;
       const lorb::RotJet R = lorb::rot_jet(xs);  // one frame: rotation state hoisted
-      for (int r = r0 + lane; r < r1; r += 64) {
-        const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
+      auto acc = [&](const double (&X)[3], double u, double w) {
         double rr[2], Jp[6], Jc[12];
-        residual_jac_s(R, xs + 3, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr, Jp, Jc);
+        residual_jac_s(R, xs + 3, X, fx, fyv, cx, cy, u, w, rr, Jp, Jc);
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
@@ -2584,9 +2649,15 @@ __global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__
           for (int b = a; b < 6; ++b) v[q++] += Jc[a] * Jc[b] + Jc[6 + a] * Jc[6 + b];
         }
         v[27] += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
-      }
+      };
 #pragma unroll
-      for (int k = 0; k < 28; ++k) v[k] = wave_sum(v[k]);
+      for (int q = 0; q < kPoC; ++q)
+        if (r0 + lane + 64 * q < r1) acc(cX[q], cuv[q][0], cuv[q][1]);
+      for (int r = r0 + lane + 64 * kPoC; r < r1; r += 64) {
+        const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
+        acc(X, obs2d[2 * r], obs2d[2 * r + 1]);
+      }
+      wave_sum_all<28>(v);
 #pragma unroll
       for (int k = 0; k < 21; ++k) JtJ[k] = v[k];
 #pragma unroll
@@ -2620,29 +2691,31 @@ __global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__
     }
 #pragma unroll
     for (int a = 0; a < 6; ++a) A[7 * a] += fmin(fmax(A[7 * a], o.min_diag), o.max_diag) / radius;
+    // the six pivots' reciprocals once (one IEEE division each); the column and both triangular
+    // solves multiply by them: the solve's dependent chain holds 6 divisions instead of 33
     bool ok = true;
+    double il[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       double dd = A[7 * j];
 #pragma unroll
       for (int k = 0; k < j; ++k) dd -= A[6 * j + k] * A[6 * j + k];
       ok = ok && dd > 0.0;
-      const double l = sqrt(dd);
-      A[7 * j] = l;
+      il[j] = 1.0 / sqrt(dd);
 #pragma unroll
       for (int i = j + 1; i < 6; ++i) {
         double sv = A[6 * i + j];
 #pragma unroll
         for (int k = 0; k < j; ++k) sv -= A[6 * i + k] * A[6 * j + k];
-        A[6 * i + j] = sv / l;
+        A[6 * i + j] = sv * il[j];
       }
     }
     double mcc = -1.0;
     if (ok) {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) { double sv = y[i]; for (int k = 0; k < i; ++k) sv -= A[6 * i + k] * y[k]; y[i] = sv / A[7 * i]; }
+      for (int i = 0; i < 6; ++i) { double sv = y[i]; for (int k = 0; k < i; ++k) sv -= A[6 * i + k] * y[k]; y[i] = sv * il[i]; }
 #pragma unroll
-      for (int i = 5; i >= 0; --i) { double sv = y[i]; for (int k = i + 1; k < 6; ++k) sv -= A[6 * k + i] * y[k]; y[i] = sv / A[7 * i]; }
+      for (int i = 5; i >= 0; --i) { double sv = y[i]; for (int k = i + 1; k < 6; ++k) sv -= A[6 * k + i] * y[k]; y[i] = sv * il[i]; }
       // model cost change = -(step.Js^T r + 0.5 step^T Js^T Js step), step = -y
       double lin = 0.0, quad = 0.0;
 #pragma unroll
@@ -2667,7 +2740,14 @@ __global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__
     double cv = 0.0;
     {
       const lorb::RotVal R = lorb::rot_val(xn);
-      for (int r = r0 + lane; r < r1; r += 64) {
+#pragma unroll
+      for (int q = 0; q < kPoC; ++q)
+        if (r0 + lane + 64 * q < r1) {
+          double rr[2];
+          residual_s(R, xn + 3, cX[q], fx, fyv, cx, cy, cuv[q][0], cuv[q][1], rr);
+          cv += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
+        }
+      for (int r = r0 + lane + 64 * kPoC; r < r1; r += 64) {
         const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
         double rr[2];
         residual_s(R, xn + 3, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr);
@@ -2751,6 +2831,7 @@ struct lorb_ba_devbuild {
   // camera_order is a function of the adjacency pattern alone: a build whose pattern equals the
   // previous one's (a sliding window usually keeps its banded pattern) reuses that order
   std::vector<char> last_adj;
+  std::vector<int> h_copy;  // host copy of the build's readback
   std::vector<int> last_map;
 };
 
@@ -4260,9 +4341,13 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     if (!P->comm) return phase_rc;
     lerr |= 64;
   }
-  std::vector<int> h_zero;  // a failed rank contributes an empty structure to the exchange
-  if (lerr) h_zero.assign(nrb, 0);
-  int* H = lerr ? h_zero.data() : b.pinned;
+  // the readback landed by DMA: none of its lines are in the CPU's caches.  One sequential copy
+  // (prefetched) into a reused host buffer, then the column-wise triangle fill and the scans below
+  // run on cached data instead of one DRAM round trip per line touched out of order.
+  b.h_copy.resize(nrb);
+  if (lerr) std::fill(b.h_copy.begin(), b.h_copy.end(), 0);  // a failed rank contributes an empty structure
+  else std::memcpy(b.h_copy.data(), b.pinned, sizeof(int) * nrb);
+  int* H = b.h_copy.data();
   if (fuse)  // k_db_sorted<true> filled the lower triangle
     for (int i = 0; i < C; ++i)
       for (int j = i + 1; j < C; ++j) H[8 + (size_t)i * C + j] = H[8 + (size_t)j * C + i];
@@ -4314,10 +4399,19 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   hp_mark(0);
   // 3. host: camera order, blocks, band, groups (order, band, activity from the global structure;
   //    the block pair lists from this rank's observations)
-  std::vector<char> adj((size_t)C * C, 0);
-  for (int i = 0; i < C; ++i)
-    for (int j = 0; j < C; ++j) adj[(size_t)i * C + j] = (i == j && gcam[i] > 0) || gcov[(size_t)i * C + j] > 0;
-  if (b.last_adj != adj) {
+  // the camera order depends only on the adjacency pattern: compared in place against the last
+  // build's (no allocation on the step's host phase), recomputed when it changed
+  bool same_adj = b.last_adj.size() == (size_t)C * C;
+  for (int i = 0; i < C && same_adj; ++i) {
+    const int* row = gcov + (size_t)i * C;
+    const char* last = b.last_adj.data() + (size_t)i * C;
+    for (int j = 0; j < C; ++j)
+      if (last[j] != (char)((i == j && gcam[i] > 0) || row[j] > 0)) { same_adj = false; break; }
+  }
+  if (!same_adj) {
+    std::vector<char> adj((size_t)C * C, 0);
+    for (int i = 0; i < C; ++i)
+      for (int j = 0; j < C; ++j) adj[(size_t)i * C + j] = (i == j && gcam[i] > 0) || gcov[(size_t)i * C + j] > 0;
     b.last_map = camera_order(C, adj);
     b.last_adj.swap(adj);
   }

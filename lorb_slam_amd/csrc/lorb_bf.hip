@@ -154,12 +154,7 @@ __global__ __launch_bounds__(256) void k_bf_scan(const uint4* __restrict__ lane_
 struct BfGrid1 {
   int nl, nu, n_chunks, lt, lane_tiles;
 };
-template <bool TOP2, int QPL>
-__global__ __launch_bounds__(256) void k_bf_scan1(const uint4* __restrict__ lane_desc,
-                                                  const uint4* __restrict__ uni_desc, BfGrid1 g,
-                                                  uint32_t* __restrict__ k1_out, uint32_t* __restrict__ k2_out,
-                                                  unsigned long long* __restrict__ kinit, int n_init) {
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < n_init; i += gridDim.x * 256) kinit[i] = ~0ull;
+__device__ __forceinline__ BfTile scan1_tile_of(const BfGrid1& g) {
   const int c = blockIdx.x / g.lane_tiles, t = (blockIdx.x - c * g.lane_tiles) * g.lt;
   const int a = (int)((int64_t)g.nu * c / g.n_chunks), b = (int)((int64_t)g.nu * (c + 1) / g.n_chunks);
   BfTile tl;
@@ -169,7 +164,20 @@ __global__ __launch_bounds__(256) void k_bf_scan1(const uint4* __restrict__ lane
   tl.uni_count = b - a;
   tl.uni_local0 = a;
   tl.out_base = c * g.nl + t;
-  scan_tile<TOP2, QPL, !TOP2>(lane_desc, uni_desc, tl, k1_out, k2_out);
+  return tl;
+}
+template <int QPL>
+__device__ __forceinline__ void scan1_tile(const uint4* __restrict__ lane_desc, const uint4* __restrict__ uni_desc,
+                                           const BfGrid1& g, uint32_t* __restrict__ k1_out) {
+  scan_tile<false, QPL, true>(lane_desc, uni_desc, scan1_tile_of(g), k1_out, nullptr);
+}
+template <bool TOP2, int QPL>
+__global__ __launch_bounds__(256) void k_bf_scan1(const uint4* __restrict__ lane_desc,
+                                                  const uint4* __restrict__ uni_desc, BfGrid1 g,
+                                                  uint32_t* __restrict__ k1_out, uint32_t* __restrict__ k2_out,
+                                                  unsigned long long* __restrict__ kinit, int n_init) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n_init; i += gridDim.x * 256) kinit[i] = ~0ull;
+  scan_tile<TOP2, QPL, !TOP2>(lane_desc, uni_desc, scan1_tile_of(g), k1_out, k2_out);
 }
 
 // One problem, crossCheck: each train's nearest query (the scan's atomicMin over the chunks) offered
@@ -281,15 +289,11 @@ __global__ __launch_bounds__(256) void k_cc_scatter(const uint32_t* __restrict__
 // local minDist (ex[p], as double) for an all-reduce(min); MODE 2 filters with the global
 // minDist and writes the local count (ex[np + p]) for an all-reduce(sum).
 template <int MODE>
-__global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* __restrict__ qkey,
-                                                     const int32_t* __restrict__ q_off,
-                                                     const int32_t* __restrict__ t_off,
-                                                     int32_t* __restrict__ cc_train,
-                                                     int32_t* __restrict__ cc_dist,
-                                                     int32_t* __restrict__ match_train,
-                                                     int32_t* __restrict__ n_matches,
-                                                     double* __restrict__ ex, int np, int nq1 = 0, int nt1 = 0) {
-  const int p = blockIdx.x;
+__device__ __forceinline__ void cc_finalize_body(int p, const unsigned long long* __restrict__ qkey,
+                                                 const int32_t* __restrict__ q_off, const int32_t* __restrict__ t_off,
+                                                 int32_t* __restrict__ cc_train, int32_t* __restrict__ cc_dist,
+                                                 int32_t* __restrict__ match_train, int32_t* __restrict__ n_matches,
+                                                 double* __restrict__ ex, int np, int nq1, int nt1) {
   // q_off == nullptr: one problem with nq1 queries and nt1 trains (offsets passed by value)
   const int q0 = q_off ? q_off[p] : 0, q1 = q_off ? q_off[p + 1] : nq1;
   const bool has_t = q_off ? t_off[p + 1] > t_off[p] : nt1 > 0;
@@ -340,6 +344,48 @@ __global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* _
     if (MODE == 2) ex[np + p] = (double)s_cnt[0];
     else n_matches[p] = s_cnt[0];
   }
+}
+template <int MODE>
+__global__ __launch_bounds__(256) void k_cc_finalize(const unsigned long long* __restrict__ qkey,
+                                                     const int32_t* __restrict__ q_off,
+                                                     const int32_t* __restrict__ t_off,
+                                                     int32_t* __restrict__ cc_train,
+                                                     int32_t* __restrict__ cc_dist,
+                                                     int32_t* __restrict__ match_train,
+                                                     int32_t* __restrict__ n_matches,
+                                                     double* __restrict__ ex, int np, int nq1 = 0, int nt1 = 0) {
+  cc_finalize_body<MODE>(blockIdx.x, qkey, q_off, t_off, cc_train, cc_dist, match_train, n_matches, ex, np, nq1, nt1);
+}
+
+// The one-problem crossCheck (lorb_bf_match, np == 1) in ONE launch: k_bf_scan1<false>'s tiles, then
+// the workgroup that finishes last (a device-scope counter) runs k_cc_merge1 and k_cc_finalize<0> for
+// the problem.  Every workgroup's key atomics and query-key initialisation are released (agent-scope
+// fence) before its count; the last one acquires before reading them and resets the counter.
+template <int QPL>
+__global__ __launch_bounds__(256) void k_bf_cc1(const uint4* __restrict__ lane_desc, const uint4* __restrict__ uni_desc,
+                                                BfGrid1 g, uint32_t* __restrict__ tkey,
+                                                unsigned long long* __restrict__ qkey, unsigned* __restrict__ done,
+                                                int32_t* __restrict__ cc_train, int32_t* __restrict__ cc_dist,
+                                                int32_t* __restrict__ match_train, int32_t* __restrict__ n_matches) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < g.nu; i += gridDim.x * 256) qkey[i] = ~0ull;
+  scan1_tile<QPL>(lane_desc, uni_desc, g, tkey);
+  __shared__ int s_last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int t = threadIdx.x; t < g.nl; t += 256) {  // k_cc_merge1
+    const uint32_t k = __hip_atomic_load(&tkey[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k >= kSentinel) continue;
+    tkey[t] = 0xffffffffu;
+    atomicMin(&qkey[k & kIdxMask], ((unsigned long long)(k >> kIdxBits) << 32) | (unsigned)t);
+  }
+  __threadfence();
+  __syncthreads();
+  cc_finalize_body<0>(0, qkey, nullptr, nullptr, cc_train, cc_dist, match_train, n_matches, nullptr, 1, g.nu, g.nl);
+  if (threadIdx.x == 0) *done = 0u;
 }
 
 // train keys <-> doubles for the all-reduce(min) (keys < 2^32 are exact in double); trains of
@@ -524,6 +570,36 @@ int scan(lorb_ctx* ctx, int np, const uint8_t* d_lane, const int32_t* l_off, con
 
 }  // namespace
 
+namespace {
+// grid of the one-problem scan (k_bf_scan1 / k_bf_cc1).  Chunks of the query range: the chunks'
+// keys meet in one atomicMin per train, so chunks are cheap -- aim at ~6 workgroups per CU
+// (latency hiding on the VALU-bound scan), >= 32 queries per chunk (LORB_BF_NC overrides:
+// diagnostics).  qpl: LORB_BF_QPL (1, 2 or 4).
+BfGrid1 grid1_of(int nq, int nt, int* qpl_out) {
+  static const int qpl = [] {
+    const char* e = getenv("LORB_BF_QPL");
+    const int v = e ? atoi(e) : 2;
+    return v == 1 || v == 4 ? v : 2;
+  }();
+  const int lt = 256 * qpl, lane_tiles = (nt + lt - 1) / lt;
+  static const int nc_env = [] { const char* e = getenv("LORB_BF_NC"); return e ? atoi(e) : 0; }();
+  int n_chunks = std::max(1, std::min((1536 + lane_tiles - 1) / lane_tiles, nq / 32));
+  if (nc_env > 0) n_chunks = std::min(nc_env, nq);
+  *qpl_out = qpl;
+  return BfGrid1{nt, nq, n_chunks, lt, lane_tiles};
+}
+// the per-train keys (all-ones between calls; a fresh or grown buffer is set once)
+int tkeys1(lorb_ctx* ctx, int nt, hipStream_t st, uint32_t** tkey) {
+  LORB_TRY(lorb::scratch_t(ctx, S_BF_TKEY, (size_t)nt, tkey));
+  if (ctx->tkey_buf != (void*)*tkey || ctx->tkey_ready < (size_t)nt) {
+    LORB_HIP(ctx, hipMemsetAsync(*tkey, 0xff, sizeof(uint32_t) * (ctx->scratch_sz[S_BF_TKEY] / sizeof(uint32_t)), st));
+    ctx->tkey_ready = ctx->scratch_sz[S_BF_TKEY] / sizeof(uint32_t);
+    ctx->tkey_buf = *tkey;
+  }
+  return LORB_OK;
+}
+}  // namespace
+
 // The crossCheck keys of ONE problem: per query (dist << 32 | train) of the train whose nearest
 // query it is, all-ones where none (lorb_bf_match_dev up to the finalisation, which the caller does:
 // k_cc_finalize<0>, or the LocalMapping append).  Nothing is uploaded: the scan computes its tiles and
@@ -536,30 +612,13 @@ int lorb::match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8
   if (nt > 0 && nq > 0) {
     // reverse pass: lanes = trains, uniform = queries -> nearest query per train
     if (nq > (int)kIdxMask) return lorb::set_error(ctx, LORB_E_INVALID, "problem 0: %d uniform items > 2^23-1", nq);
-    static const int qpl = [] {
-      const char* e = getenv("LORB_BF_QPL");
-      const int v = e ? atoi(e) : 2;
-      return v == 1 || v == 4 ? v : 2;
-    }();
-    // Chunks of the query range: the chunks' keys meet in one atomicMin per train, so chunks are
-    // cheap -- aim at ~6 workgroups per CU (latency hiding on the VALU-bound scan), >= 32 queries
-    // per chunk (LORB_BF_NC overrides: diagnostics).
-    const int lt = 256 * qpl, lane_tiles = (nt + lt - 1) / lt;
-    static const int nc_env = [] { const char* e = getenv("LORB_BF_NC"); return e ? atoi(e) : 0; }();
-    int n_chunks = std::max(1, std::min((1536 + lane_tiles - 1) / lane_tiles, nq / 32));
-    if (nc_env > 0) n_chunks = std::min(nc_env, nq);
-    BfGrid1 g{nt, nq, n_chunks, lt, lane_tiles};
+    int qpl = 2;
+    const BfGrid1 g = grid1_of(nq, nt, &qpl);
     uint32_t* tkey = nullptr;
-    LORB_TRY(lorb::scratch_t(ctx, S_BF_TKEY, (size_t)nt, &tkey));
-    if (ctx->tkey_buf != (void*)tkey || ctx->tkey_ready < (size_t)nt) {  // a fresh or grown buffer: all-ones once
-      LORB_HIP(ctx, hipMemsetAsync(tkey, 0xff, sizeof(uint32_t) * (ctx->scratch_sz[S_BF_TKEY] / sizeof(uint32_t)),
-                                   st));
-      ctx->tkey_ready = ctx->scratch_sz[S_BF_TKEY] / sizeof(uint32_t);
-      ctx->tkey_buf = tkey;
-    }
+    LORB_TRY(tkeys1(ctx, nt, st, &tkey));
     const size_t ready = ctx->tkey_ready;
     ctx->tkey_ready = 0;  // until the merge has been enqueued (it restores the all-ones)
-    const unsigned nb = (unsigned)(g.lane_tiles * n_chunks);
+    const unsigned nb = (unsigned)(g.lane_tiles * g.n_chunks);
     {
       lorb::KernelTimer kt(ctx, LORB_K_BF_SCAN_TOP1);
       if (qpl == 2)
@@ -589,6 +648,42 @@ namespace {
 // passed by value.  Same outputs, bit for bit, as the general path.
 int match1_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt, int32_t* d_cc_train,
                int32_t* d_cc_dist, int32_t* d_match_train, int32_t* d_n_matches) {
+  if (nq > 0 && nt > 0 && nq <= (int)kIdxMask) {  // scan + merge + finalize in one launch (k_bf_cc1)
+    int qpl = 2;
+    const BfGrid1 g = grid1_of(nq, nt, &qpl);
+    uint32_t* tkey = nullptr;
+    unsigned long long* qkey = nullptr;
+    unsigned* done = nullptr;
+    LORB_TRY(tkeys1(ctx, nt, ctx->stream, &tkey));
+    LORB_TRY(lorb::scratch_t(ctx, S_BF_QKEY, (size_t)nq, &qkey));
+    LORB_TRY(lorb::scratch_t(ctx, S_BF_DONE, 1, &done));
+    if (ctx->done_buf != (void*)done) {
+      LORB_HIP(ctx, hipMemsetAsync(done, 0, sizeof(unsigned), ctx->stream));
+      ctx->done_buf = done;
+    }
+    const size_t ready = ctx->tkey_ready;
+    ctx->tkey_ready = 0;  // until the launch is enqueued (its last workgroup restores the all-ones)
+    ctx->done_buf = nullptr;
+    const unsigned nb = (unsigned)(g.lane_tiles * g.n_chunks);
+    const uint4* lt = reinterpret_cast<const uint4*>(d_t);
+    const uint4* ut = reinterpret_cast<const uint4*>(d_q);
+    {
+      lorb::KernelTimer kt(ctx, LORB_K_BF_SCAN_TOP1);
+      if (qpl == 2)
+        hipLaunchKernelGGL(k_bf_cc1<2>, dim3(nb), dim3(256), 0, ctx->stream, lt, ut, g, tkey, qkey, done, d_cc_train,
+                           d_cc_dist, d_match_train, d_n_matches);
+      else if (qpl == 4)
+        hipLaunchKernelGGL(k_bf_cc1<4>, dim3(nb), dim3(256), 0, ctx->stream, lt, ut, g, tkey, qkey, done, d_cc_train,
+                           d_cc_dist, d_match_train, d_n_matches);
+      else
+        hipLaunchKernelGGL(k_bf_cc1<1>, dim3(nb), dim3(256), 0, ctx->stream, lt, ut, g, tkey, qkey, done, d_cc_train,
+                           d_cc_dist, d_match_train, d_n_matches);
+    }
+    LORB_CHECK_LAUNCH(ctx);
+    ctx->tkey_ready = ready;
+    ctx->done_buf = done;
+    return LORB_OK;
+  }
   unsigned long long* qkey = nullptr;
   LORB_TRY(lorb::match1_keys_dev(ctx, d_q, nq, d_t, nt, &qkey));
   hipLaunchKernelGGL(k_cc_finalize<0>, dim3(1), dim3(256), 0, ctx->stream, qkey, (const int32_t*)nullptr,

@@ -33,6 +33,7 @@ struct lorb_ctx {
   // S_BF_TKEY entries known to hold all-ones (0: re-fill before use), for the buffer tkey_buf
   size_t tkey_ready = 0;
   void* tkey_buf = nullptr;
+  void* done_buf = nullptr;  // S_BF_DONE as last zeroed
   // pinned host staging
   void* pinned = nullptr;
   size_t pinned_sz = 0;
@@ -412,5 +413,6 @@ enum {
   S_WX = 34,   /* 8 slots: windowed-matcher scratch */
   S_BF_TKEY = 120, /* crossCheck per-train keys: all-ones between calls (the merge resets them) */
   S_IO_IN = 121,   /* InPack device block */
-  S_IO_OUT = 122   /* OutPack device block */
+  S_IO_OUT = 122,  /* OutPack device block */
+  S_BF_DONE = 123  /* k_bf_cc1's workgroup counter: zero between calls (the last workgroup resets it) */
 };

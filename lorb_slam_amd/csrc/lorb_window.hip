@@ -41,6 +41,31 @@ __device__ __forceinline__ int hamming(const uint4* a, const uint4* b) {
 // (a7) grid: one workgroup; cell = PosInGrid; per-cell lists in keypoint (insertion) order.  The
 // offsets and (up to kGridLds keypoints) the lists are built in LDS and stored once, coalesced.
 constexpr int kGridLds = 6144;
+// scatter keypoints into their cells' lists (atomics: any order), then restore insertion (index)
+// order inside every cell (cells hold a handful of entries); indices only, never a pointer below a
+// cell's first entry
+__device__ __forceinline__ void grid_place(int* idx, const int* off, int* cur, const int* __restrict__ kp_cell,
+                                           int n, int t) {
+  for (int i = t; i < n; i += 1024) {
+    const int c = kp_cell[i];
+    if (c >= 0) idx[atomicAdd(&cur[c], 1)] = i;
+  }
+  __syncthreads();
+  for (int c = t; c < kCells; c += 1024) {
+    const int a = off[c], b = off[c + 1];
+    for (int i = a + 1; i < b; ++i) {
+      const int v = idx[i];
+      int j = i;
+      while (j > a) {
+        const int u = idx[j - 1];
+        if (u <= v) break;
+        idx[j] = u;
+        --j;
+      }
+      idx[j] = v;
+    }
+  }
+}
 __global__ __launch_bounds__(1024) void k_grid_build(const float* __restrict__ x, const float* __restrict__ y,
                                                      int n, lorb_frame_params fp,
                                                      int* __restrict__ cell_off,  // kCells+1
@@ -49,7 +74,6 @@ __global__ __launch_bounds__(1024) void k_grid_build(const float* __restrict__ x
   __shared__ int cur[kCells];
   __shared__ int s_idx[kGridLds];
   const bool lds = n <= kGridLds;
-  int* idx = lds ? s_idx : cell_idx;
   const int t = threadIdx.x;
   for (int c = t; c < kCells; c += 1024) off[c] = 0;
   __syncthreads();
@@ -74,21 +98,10 @@ __global__ __launch_bounds__(1024) void k_grid_build(const float* __restrict__ x
     if (t == 1023) off[kCells] = tot;
   }
   __syncthreads();
-  for (int i = t; i < n; i += 1024) {
-    const int c = kp_cell[i];
-    if (c >= 0) idx[atomicAdd(&cur[c], 1)] = i;
-  }
-  __syncthreads();
-  // restore insertion (index) order inside every cell: cells hold a handful of entries
-  for (int c = t; c < kCells; c += 1024) {
-    const int a = off[c], b = off[c + 1];
-    for (int i = a + 1; i < b; ++i) {
-      const int v = idx[i];
-      int j = i - 1;
-      while (j >= a && idx[j] > v) { idx[j + 1] = idx[j]; --j; }
-      idx[j + 1] = v;
-    }
-  }
+  // separate instantiations for the LDS and the global list: a pointer that may be either is a flat
+  // pointer, and the sort's walk below a cell's first entry must not be formed on the LDS aperture
+  if (lds) grid_place(s_idx, off, cur, kp_cell, n, t);
+  else grid_place(cell_idx, off, cur, kp_cell, n, t);
   for (int c = t; c <= kCells; c += 1024) cell_off[c] = off[c];
   if (lds) {
     __syncthreads();
