@@ -55,7 +55,7 @@ K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_schur", 3: "k_ba
 # rocprofv3 short names (tools/pmc_traffic.py) of the same kernels, for the PMC traffic lookup
 K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_2s"}
 # committed PMC summaries, newest first; each is keyed by workload (tools/pmc_traffic.py)
-TRAFFIC = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r03", "r02", "r01")]
+TRAFFIC = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r04", "r03", "r02", "r01")]
 METRIC = "ORB matches/sec + local-BA iterations/sec (50 KF, 10k pts) at 1/2/4/8 MI355X"
 
 
@@ -642,7 +642,8 @@ def workload_rehearse(ctx, args, rank):
 
 def pmc_traffic(workload, kernel):
     """HBM bytes per launch of `kernel` in `workload` from the committed rocprofv3 PMC passes
-    (FETCH_SIZE and WRITE_SIZE collected in separate runs, gfx950 FETCH_SIZE x2 correction;
+    (FETCH_SIZE and WRITE_SIZE collected in separate runs; the gfx950 FETCH_SIZE correction per kernel
+    from tools/micro/fetch_cal.hip's calibration, x2 for streaming kernels and x1 for record gathers;
     tools/pmc_traffic.py).  PMC counters cannot be read live from inside the timed process, so
     this is the profiled value of the same command; null when no summary for this workload
     and kernel is committed."""

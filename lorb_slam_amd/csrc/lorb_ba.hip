@@ -4388,11 +4388,12 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   if (gerr & 64)
     return phase_rc != LORB_OK ? phase_rc
                                : lorb::set_error(ctx, LORB_E_DEVICE, "device plan build failed on another rank");
+  // a count beyond capacity first: the slots read up to the capacity then hold no real observations
+  if (gerr & 8) return lorb::set_error(ctx, LORB_E_INVALID, "live point / observation count outside [0, capacity] (%d / %d)",
+                                       b.P_cap, b.K_cap);
   if (gerr & 1) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a point index outside [0, n_points)");
   if (gerr & 2) return lorb::set_error(ctx, LORB_E_INVALID, "observation with a frame index >= n_poses");
   if (gerr & 4) return lorb::set_error(ctx, LORB_E_INVALID, "a point observed twice by one camera");
-  if (gerr & 8) return lorb::set_error(ctx, LORB_E_INVALID, "live point / observation count outside [0, capacity] (%d / %d)",
-                                       b.P_cap, b.K_cap);
   if ((gerr & 16) || Pn < 0 || Pn > b.P_cap) return lorb::set_error(ctx, LORB_E_INVALID, "n_points %d outside [0, %d]", Pn, b.P_cap);
   if (kGB - gmaxk < 1)
     return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "a point with %d observations (device plans hold <= %d)", gmaxk, kGB - 1);

@@ -48,7 +48,7 @@ struct lorb_ctx {
   void* io_out = nullptr;
   void* io_out_dev = nullptr;
   size_t io_out_sz = 0;
-  hipEvent_t io_ev = nullptr;  // the last InPack pull (the staging is rewritten only after it)
+  bool io_pending = false;  // an InPack pull may still read the staging (cleared by OutPack::fetch)
 };
 
 namespace lorb {

@@ -77,8 +77,9 @@ __global__ __launch_bounds__(256) void k_io_pull(const uint4* __restrict__ src, 
 int InPack::commit() {
   if (!total) return LORB_OK;
   // a call that failed after its commit may have left its copy in flight
-  if (ctx->io_ev) LORB_HIP(ctx, hipEventSynchronize(ctx->io_ev));
-  else LORB_HIP(ctx, hipEventCreateWithFlags(&ctx->io_ev, hipEventDisableTiming));
+  // every host-array call ends waiting for its stream (OutPack::fetch); only a call that failed
+  // after its commit can leave a pull in flight
+  if (ctx->io_pending) LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   LORB_TRY(pinned_grow(ctx, &ctx->io_in, &ctx->io_in_dev, &ctx->io_in_sz, total));
   unsigned char* h = static_cast<unsigned char*>(ctx->io_in);
   for (const Part& p : parts)
@@ -93,7 +94,7 @@ int InPack::commit() {
                        static_cast<uint4*>(base), n16);
     LORB_CHECK_LAUNCH(ctx);
   }
-  LORB_HIP(ctx, hipEventRecord(ctx->io_ev, ctx->stream));
+  ctx->io_pending = true;
   return LORB_OK;
 }
 
@@ -111,6 +112,7 @@ int OutPack::fetch() {
   for (const Part& p : parts) used = std::max(used, p.off + p.bytes);
   if (used && !direct) LORB_HIP(ctx, hipMemcpyAsync(hbase, dbase, used, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, spin_sync(ctx));
+  ctx->io_pending = false;
   return LORB_OK;
 }
 
@@ -178,7 +180,6 @@ int lorb_destroy(lorb_ctx* ctx) {
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->io_in) (void)hipHostFree(ctx->io_in);
   if (ctx->io_out) (void)hipHostFree(ctx->io_out);
-  if (ctx->io_ev) (void)hipEventDestroy(ctx->io_ev);
   for (int i = 0; i < 64; i++)
     if (ctx->ev[i]) (void)hipEventDestroy(ctx->ev[i]);
   if (ctx->spin_ev) (void)hipEventDestroy(ctx->spin_ev);

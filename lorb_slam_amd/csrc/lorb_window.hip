@@ -38,6 +38,62 @@ __device__ __forceinline__ int hamming(const uint4* a, const uint4* b) {
          __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+// Frame::PosInGrid: the cell of a keypoint, or -1 outside the grid
+__device__ __forceinline__ int pos_in_grid(float x, float y, const lorb_frame_params& fp) {
+  const int px = (int)roundf((x - fp.min_x) * fp.grid_w_inv);
+  const int py = (int)roundf((y - fp.min_y) * fp.grid_h_inv);
+  if (px < 0 || px >= LORB_GRID_COLS || py < 0 || py >= LORB_GRID_ROWS) return -1;
+  return px * LORB_GRID_ROWS + py;
+}
+
+// The grid of n <= kGridLds keypoints built by one NT-thread workgroup in its own LDS (off: kCells + 1,
+// cur: kCells, idx: n), lists in keypoint order: the candidate kernels of the host-array calls build
+// it per workgroup instead of reading a grid built by a launch of its own.
+template <int NT>
+__device__ __forceinline__ void grid_lds(const float* __restrict__ x, const float* __restrict__ y, int n,
+                                         const lorb_frame_params& fp, int* off, int* cur, int* idx) {
+  constexpr int CPT = kCells / NT;  // consecutive cells per thread in the scan
+  static_assert(kCells % NT == 0, "cells per thread");
+  __shared__ int wsum[NT / 64];
+  const int t = threadIdx.x;
+  for (int c = t; c < kCells; c += NT) off[c] = 0;
+  __syncthreads();
+  for (int i = t; i < n; i += NT) {
+    const int c = pos_in_grid(x[i], y[i], fp);
+    if (c >= 0) atomicAdd(&off[c], 1);
+  }
+  __syncthreads();
+  int v[CPT], sum = 0;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) { v[k] = off[CPT * t + k]; sum += v[k]; }
+  int tot;
+  int run = lorb::block_excl_scan<NT>(sum, wsum, &tot);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) { off[CPT * t + k] = run; cur[CPT * t + k] = run; run += v[k]; }
+  if (t == NT - 1) off[kCells] = tot;
+  __syncthreads();
+  for (int i = t; i < n; i += NT) {
+    const int c = pos_in_grid(x[i], y[i], fp);
+    if (c >= 0) idx[atomicAdd(&cur[c], 1)] = i;
+  }
+  __syncthreads();
+  for (int c = t; c < kCells; c += NT) {  // insertion (keypoint) order inside every cell
+    const int a = off[c], b = off[c + 1];
+    for (int i = a + 1; i < b; ++i) {
+      const int w = idx[i];
+      int j = i;
+      while (j > a) {
+        const int u = idx[j - 1];
+        if (u <= w) break;
+        idx[j] = u;
+        --j;
+      }
+      idx[j] = w;
+    }
+  }
+  __syncthreads();
+}
+
 // (a7) grid: one workgroup; cell = PosInGrid; per-cell lists in keypoint (insertion) order.  The
 // offsets and (up to kGridLds keypoints) the lists are built in LDS and stored once, coalesced.
 constexpr int kGridLds = 6144;
@@ -78,10 +134,7 @@ __global__ __launch_bounds__(1024) void k_grid_build(const float* __restrict__ x
   for (int c = t; c < kCells; c += 1024) off[c] = 0;
   __syncthreads();
   for (int i = t; i < n; i += 1024) {
-    const int px = (int)roundf((x[i] - fp.min_x) * fp.grid_w_inv);
-    const int py = (int)roundf((y[i] - fp.min_y) * fp.grid_h_inv);
-    int c = -1;
-    if (!(px < 0 || px >= LORB_GRID_COLS || py < 0 || py >= LORB_GRID_ROWS)) c = px * LORB_GRID_ROWS + py;
+    const int c = pos_in_grid(x[i], y[i], fp);
     kp_cell[i] = c;
     if (c >= 0) atomicAdd(&off[c], 1);
   }
@@ -137,6 +190,24 @@ struct KpDev {
   const int *cell_off, *cell_idx;
   int n;
 };
+
+// The candidate kernels of the host-array calls (k_cand_*<., true>, n <= kStageKps keypoints) build
+// the frame's grid in their own LDS instead of reading one built by a launch of its own.  (Staging
+// the keypoints' coordinates, octaves and descriptors into LDS as well measured slower: 11.5 ->
+// 12.2 us per a4 launch.)
+constexpr int kStageKps = 1024;
+struct KpLds {
+  int off[kCells + 1], cur[kCells], idx[kStageKps];
+};
+template <int NT>
+__device__ __forceinline__ KpDev stage_grid(const KpDev& G, const lorb_frame_params& fp, KpLds& L) {
+  grid_lds<NT>(G.x, G.y, G.n, fp, L.off, L.cur, L.idx);  // ends with a barrier
+  KpDev K = G;
+  K.cell_off = L.off;
+  K.cell_idx = L.idx;
+  return K;
+}
+
 
 // Walk GetFeaturesInArea in reference order (ix outer, iy inner, cell insertion order) and apply
 // the level / window / stereo filters -- one WAVEFRONT per query.  The window's cells are taken 64
@@ -213,7 +284,7 @@ __device__ __forceinline__ int walk_candidates_wave(const KpDev& K, const lorb_f
 constexpr int kCandWaves = 4;  // queries (wavefronts) per 256-thread workgroup
 
 // (a5) candidates of each local map point, one wavefront per point
-template <bool WRITE>
+template <bool WRITE, bool GRID = false>
 __global__ __launch_bounds__(64 * kCandWaves) void k_cand_local(KpDev K, WinParams P, int np,
                                                     const uint8_t* __restrict__ in_view,
                                                     const uint8_t* __restrict__ is_bad,
@@ -223,14 +294,22 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_cand_local(KpDev K, WinPara
                                                     int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
                                                     int2* __restrict__ cand, int stride = 0) {
   const int m = blockIdx.x * kCandWaves + (threadIdx.x >> 6);
+  // the query's scalars requested first (GRID: they arrive while the keypoints are staged)
+  const int mq = min(m, np - 1);
+  const bool act = in_view[mq] && !(is_bad && is_bad[mq]);
+  const int lev = plev[mq];
+  const float vc = vcos[mq], qx = px[mq], qy = py[mq], qxr = pxr[mq];
+  if constexpr (GRID) {
+    __shared__ KpLds L;
+    K = stage_grid<64 * kCandWaves>(K, P.fp, L);
+  }
   if (m >= np) return;
   int cnt = 0;
-  if (in_view[m] && !(is_bad && is_bad[m])) {
-    const int lev = plev[m];
-    float r = ((double)vcos[m] > 0.998) ? 2.5f : 4.0f;  // RadiusByViewingCos
+  if (act) {
+    float r = ((double)vc > 0.998) ? 2.5f : 4.0f;  // RadiusByViewingCos
     if (P.th != 1.0f) r *= P.th;
     const float rs = r * P.fp.scale_factors[lev];
-    cnt = walk_candidates_wave<WRITE>(K, P.fp, px[m], py[m], rs, lev - 1, lev, pxr[m], rs, pdesc + 2 * (size_t)m,
+    cnt = walk_candidates_wave<WRITE>(K, P.fp, qx, qy, rs, lev - 1, lev, qxr, rs, pdesc + 2 * (size_t)m,
                                       WRITE ? cand + (stride > 0 ? (size_t)m * stride : (size_t)cand_off[m]) : nullptr);
   }
   if ((!WRITE || stride > 0) && (threadIdx.x & 63) == 0) cand_cnt[m] = cnt;
@@ -244,14 +323,26 @@ __device__ __forceinline__ float gemv3(const float* R, float a, float b, float c
 // WRITE: emit at cand_off[i] (two passes: count, scan, write); STRIDE > 0: one pass, emit at
 // i * STRIDE and write the count (STRIDE bounds a query's candidates: the frame's keypoint count)
 // the candidates of last-frame point i (one wavefront; returns the count, written at `out` if WRITE)
+struct FrameQuery {  // a last-frame point's inputs
+  bool act;          // has a map point and is not an outlier
+  float X, Y, Z;
+  int o;             // octave
+};
+__device__ __forceinline__ FrameQuery frame_query(int i, const uint8_t* __restrict__ has_mp,
+                                                  const uint8_t* __restrict__ outlier, const float* __restrict__ pos,
+                                                  const int* __restrict__ loct) {
+  FrameQuery q;
+  q.act = has_mp[i] && !(outlier && outlier[i]);
+  q.X = pos[3 * i]; q.Y = pos[3 * i + 1]; q.Z = pos[3 * i + 2];
+  q.o = loct[i];
+  return q;
+}
 template <bool WRITE>
-__device__ __forceinline__ int cand_frame_one(const KpDev& K, const WinParams& P, int i,
-                                              const uint8_t* __restrict__ has_mp, const uint8_t* __restrict__ outlier,
-                                              const float* __restrict__ pos, const int* __restrict__ loct,
-                                              const uint4* __restrict__ ldesc, int2* out) {
+__device__ __forceinline__ int cand_frame_one(const KpDev& K, const WinParams& P, const FrameQuery& q,
+                                              const uint4* qdesc, int2* out) {
   int cnt = 0;
-  if (has_mp[i] && !(outlier && outlier[i])) {
-    const float X = pos[3 * i], Y = pos[3 * i + 1], Z = pos[3 * i + 2];
+  if (q.act) {
+    const float X = q.X, Y = q.Y, Z = q.Z;
     const float xc = gemv3(P.Rcw + 0, X, Y, Z, P.tcw[0]);
     const float yc = gemv3(P.Rcw + 3, X, Y, Z, P.tcw[1]);
     const float zc = gemv3(P.Rcw + 6, X, Y, Z, P.tcw[2]);
@@ -260,20 +351,20 @@ __device__ __forceinline__ int cand_frame_one(const KpDev& K, const WinParams& P
       const float u = P.fp.fx * xc * invzc + P.fp.cx;
       const float v = P.fp.fy * yc * invzc + P.fp.cy;
       if (!(u < P.fp.min_x || u > P.fp.max_x) && !(v < P.fp.min_y || v > P.fp.max_y)) {
-        const int o = loct[i];
+        const int o = q.o;
         const float radius = P.th * P.fp.scale_factors[o];
         int mn, mx;
         if (P.mode_forward) { mn = o; mx = -1; }
         else if (P.mode_backward) { mn = 0; mx = o; }
         else { mn = o - 1; mx = o + 1; }
         const float ur = u - P.fp.bf * invzc;
-        cnt = walk_candidates_wave<WRITE>(K, P.fp, u, v, radius, mn, mx, ur, radius, ldesc + 2 * (size_t)i, out);
+        cnt = walk_candidates_wave<WRITE>(K, P.fp, u, v, radius, mn, mx, ur, radius, qdesc, out);
       }
     }
   }
   return cnt;
 }
-template <bool WRITE>
+template <bool WRITE, bool GRID = false>
 __global__ __launch_bounds__(64 * kCandWaves) void k_cand_frame(KpDev K, WinParams P, int nl,
                                                     const uint8_t* __restrict__ has_mp,
                                                     const uint8_t* __restrict__ outlier,
@@ -283,9 +374,15 @@ __global__ __launch_bounds__(64 * kCandWaves) void k_cand_frame(KpDev K, WinPara
                                                     int* __restrict__ cand_cnt, const int* __restrict__ cand_off,
                                                     int2* __restrict__ cand, int stride = 0) {
   const int i = blockIdx.x * kCandWaves + (threadIdx.x >> 6);
+  // the query's inputs requested first (GRID: they arrive while the keypoints are staged)
+  const FrameQuery q = frame_query(min(i, nl - 1), has_mp, outlier, pos, loct);
+  if constexpr (GRID) {
+    __shared__ KpLds L;
+    K = stage_grid<64 * kCandWaves>(K, P.fp, L);
+  }
   if (i >= nl) return;
   const int cnt = cand_frame_one<WRITE>(
-      K, P, i, has_mp, outlier, pos, loct, ldesc,
+      K, P, q, ldesc + 2 * (size_t)i,
       WRITE ? cand + (stride > 0 ? (size_t)i * stride : (size_t)cand_off[i]) : nullptr);
   if ((!WRITE || stride > 0) && (threadIdx.x & 63) == 0) cand_cnt[i] = cnt;
 }
@@ -324,12 +421,6 @@ int alloc_candidates(lorb_ctx* ctx, const int* d_total, size_t bound, int2** can
   return lorb::scratch_t(ctx, S_W9, std::max<size_t>(cap, 1), cand);
 }
 
-// resolver state in LDS when claim + res fit (nk + np ints <= 120 KiB)
-inline size_t resolve_lds_bytes(int np, int nk) {
-  const size_t b = sizeof(int) * ((size_t)np + (size_t)nk);
-  return b <= 120 * 1024 ? b : 0;
-}
-
 // Jacobi fixpoint resolver (one workgroup per call).  MODE 0 = a5 (best/second + ratio test),
 // MODE 1 = a4 (best only + rotation histogram / ComputeThreeMaxima null-out).  out != null: assign
 // and the count are also copied there (nk + 1 ints) at the end.
@@ -337,37 +428,43 @@ template <int MODE>
 __device__ __forceinline__ void resolve_run(int np, int nk, const int* cand_off, const int2* __restrict__ cand,
                                             const uint8_t* __restrict__ pt_locked,
                                             const float* __restrict__ last_angle,
-                                            const float* __restrict__ cur_angle,
-                                            int* res,                  // np: accepted slot or -1
-                                            int* claim,                // nk
-                                            int* __restrict__ assign,  // nk output
-                                            int* __restrict__ bins,    // np scratch (MODE 1)
-                                            int* __restrict__ nulls,   // nk scratch (MODE 1)
+                                            const float* cur_angle,
+                                            int* res,      // np: accepted slot or -1
+                                            int* claim,    // nk
+                                            int* assign,   // nk: the working assignment
+                                            int* bins,     // np scratch (MODE 1)
+                                            int* nulls,    // nk scratch (MODE 1)
+                                            int* __restrict__ assign_g,  // nk: where the assignment goes (or null)
                                             int* __restrict__ nmatches, int stride, int* __restrict__ out) {
   __shared__ int s_changed;
   __shared__ int hist[LORB_HISTO_LENGTH];
   __shared__ int s_ind[3];
   __shared__ int s_acc, s_rej;
   const int t = threadIdx.x;
-  for (int c = t; c < nk; c += 1024) claim[c] = kNoClaim;
-  for (int m = t; m < np; m += 1024) res[m] = -2;  // "never computed"
-  if (t == 0) { s_acc = 0; s_rej = 0; }
-  __syncthreads();
-  // np <= 1024 (one query per thread): the first kRegCand candidates of the thread's query are
-  // loaded once, all together, into registers; every round then reads them (and their claims, from
-  // LDS) without a global round trip per candidate.  Later candidates, if any, come from global.
+  // np <= 1024 (one query per thread): the first kRegCand candidates of the thread's query, its lock
+  // flag and (MODE 1) its angle are loaded once, all together, into registers; every round then reads
+  // them (and their claims, from LDS) without a global round trip.  Later candidates, if any, come
+  // from global.
   constexpr int kRegCand = 8;
   const bool regc = np <= 1024;
   int2 rc[kRegCand];
   int rn = 0;
+  bool lk_t = false;
+  float la_t = 0.0f;
   if (regc && t < np) {
     const int a = stride > 0 ? t * stride : cand_off[t], b = stride > 0 ? a + cand_off[t] : cand_off[t + 1];
+    lk_t = pt_locked[t];
+    if (MODE == 1) la_t = last_angle[t];
     rn = min(b - a, kRegCand);
     if (rn > 0) {
 #pragma unroll
       for (int k = 0; k < kRegCand; ++k) rc[k] = cand[a + min(k, rn - 1)];
     }
   }
+  for (int c = t; c < nk; c += 1024) claim[c] = kNoClaim;
+  for (int m = t; m < np; m += 1024) res[m] = -2;  // "never computed"
+  if (t == 0) { s_acc = 0; s_rej = 0; }
+  __syncthreads();
   for (int round = 0; round <= np; ++round) {
     if (t == 0) s_changed = 0;
     __syncthreads();
@@ -413,7 +510,7 @@ __device__ __forceinline__ void resolve_run(int np, int nk, const int* cand_off,
     for (int c = t; c < nk; c += 1024) claim[c] = kNoClaim;
     __syncthreads();
     for (int m = t; m < np; m += 1024)
-      if (res[m] >= 0 && pt_locked[m]) atomicMin(&claim[res[m]], m);
+      if (res[m] >= 0 && (regc ? lk_t : pt_locked[m] != 0)) atomicMin(&claim[res[m]], m);
     __syncthreads();
   }
   // final slot assignment: last accepted writer per slot
@@ -426,7 +523,7 @@ __device__ __forceinline__ void resolve_run(int np, int nk, const int* cand_off,
       atomicMax(&assign[r], m);
       atomicAdd(&s_acc, 1);
       if (MODE == 1) {
-        float rot = last_angle[m] - cur_angle[r];
+        float rot = (regc ? la_t : last_angle[m]) - cur_angle[r];
         if (rot < 0.0) rot += 360.0f;
         const float factor = LORB_HISTO_LENGTH / 360.0f;
         int bin = (int)roundf(rot * factor);
@@ -464,10 +561,21 @@ __device__ __forceinline__ void resolve_run(int np, int nk, const int* cand_off,
   }
   __syncthreads();
   if (t == 0) *nmatches = s_acc - s_rej;
-  if (out) {  // the host-array calls: assign + count into the mapped result block, plain stores
-    for (int c = t; c < nk; c += 1024) out[c] = assign[c];
-    if (t == 0) out[nk] = s_acc - s_rej;
+  for (int c = t; c < nk; c += 1024) {
+    const int v = assign[c];
+    if (assign_g && assign_g != assign) assign_g[c] = v;
+    if (out) out[c] = v;  // the host-array calls: the mapped result block, plain stores
   }
+  if (out && t == 0) out[nk] = s_acc - s_rej;
+}
+// LDS modes of k_resolve: 1 = claim and res (nk + np ints); 2 = also the working assignment, the
+// MODE-1 bins / nulls and a copy of the current frame's keypoint angles (4 nk + 2 np words).
+inline int resolve_lds_mode(int np, int nk, size_t* bytes) {
+  const size_t b2 = sizeof(int) * (4 * (size_t)nk + 2 * (size_t)np), b1 = sizeof(int) * ((size_t)np + (size_t)nk);
+  if (b2 <= 120 * 1024) { *bytes = b2; return 2; }
+  if (b1 <= 120 * 1024) { *bytes = b1; return 1; }
+  *bytes = 0;
+  return 0;
 }
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __restrict__ cand_off,
@@ -477,12 +585,23 @@ __global__ __launch_bounds__(1024) void k_resolve(int np, int nk, const int* __r
                                                   const float* __restrict__ cur_angle,
                                                   int* __restrict__ res, int* __restrict__ claim,
                                                   int* __restrict__ assign, int* __restrict__ bins,
-                                                  int* __restrict__ nulls, int* __restrict__ nmatches, int use_lds,
+                                                  int* __restrict__ nulls, int* __restrict__ nmatches, int lds_mode,
                                                   int stride = 0, int* __restrict__ out = nullptr) {
-  // claim (nk) and res (np) live in LDS when they fit (dynamic shared memory), else in global
+  // the working set in LDS (dynamic shared memory) as far as it fits (resolve_lds_mode), else global
   extern __shared__ int s_dyn[];
-  if (use_lds) { claim = s_dyn; res = s_dyn + nk; }
-  resolve_run<MODE>(np, nk, cand_off, cand, pt_locked, last_angle, cur_angle, res, claim, assign, bins, nulls,
+  int* wassign = assign;
+  const float* ca = cur_angle;
+  if (lds_mode >= 1) { claim = s_dyn; res = s_dyn + nk; }
+  if (lds_mode == 2) {
+    wassign = res + np;
+    nulls = wassign + nk;
+    bins = nulls + nk;
+    float* s_ca = reinterpret_cast<float*>(bins + np);
+    if (MODE == 1)
+      for (int c = threadIdx.x; c < nk; c += 1024) s_ca[c] = cur_angle[c];
+    ca = s_ca;  // resolve_run's first barrier orders these stores before any read
+  }
+  resolve_run<MODE>(np, nk, cand_off, cand, pt_locked, last_angle, ca, res, claim, wassign, bins, nulls, assign,
                     nmatches, stride, out);
 }
 
@@ -600,19 +719,22 @@ void kps_add(lorb::InPack& in, const lorb_keypoints* k, const uint8_t* slot_stat
   if (!slot_state) { p.zeros.assign(n, 0); slot_state = p.zeros.data(); }
   p.ss = in.add_t(slot_state, n);
 }
+// grid = false: the candidate kernel builds the grid in its own LDS (k_cand_*<., true>)
 int kps_finish(lorb_ctx* ctx, const lorb::InPack& in, const KpParts& p, int n, int slot0, KpDev* K,
-               const lorb_frame_params* fp) {
+               const lorb_frame_params* fp, bool grid = true) {
   const float* x = in.dev<float>(p.x);
   const float* y = in.dev<float>(p.y);
+  K->x = x; K->y = y; K->angle = in.dev<float>(p.ang); K->uR = in.dev<float>(p.ur); K->octave = in.dev<int>(p.oc);
+  K->desc = in.dev<const uint4>(p.desc); K->slot_state = in.dev<uint8_t>(p.ss);
+  K->cell_off = nullptr; K->cell_idx = nullptr; K->n = n;
+  if (!grid) return LORB_OK;
   int *cell_off, *cell_idx, *kp_cell;
   LORB_TRY(lorb::scratch_t(ctx, slot0 + 7, kCells + 1, &cell_off));
   LORB_TRY(lorb::scratch_t(ctx, slot0 + 8, (size_t)std::max(n, 1), &cell_idx));
   LORB_TRY(lorb::scratch_t(ctx, slot0 + 9, (size_t)std::max(n, 1), &kp_cell));
   hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, ctx->stream, x, y, n, *fp, cell_off, cell_idx, kp_cell);
   LORB_CHECK_LAUNCH(ctx);
-  K->x = x; K->y = y; K->angle = in.dev<float>(p.ang); K->uR = in.dev<float>(p.ur); K->octave = in.dev<int>(p.oc);
-  K->desc = in.dev<const uint4>(p.desc); K->slot_state = in.dev<uint8_t>(p.ss);
-  K->cell_off = cell_off; K->cell_idx = cell_idx; K->n = n;
+  K->cell_off = cell_off; K->cell_idx = cell_idx;
   return LORB_OK;
 }
 
@@ -640,8 +762,10 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
             i_pl = in.add_t(pts->pred_level, np), i_vc = in.add_t(pts->view_cos, np),
             i_pd = in.add_t(pts->desc, (size_t)np * 32);
   LORB_TRY(in.commit());
+  const bool strided = (size_t)np * (size_t)nk <= kCandStrided;  // as lorb_search_by_projection_frame
+  const bool lds_grid = strided && nk <= kStageKps;  // the candidate kernel builds the grid itself
   KpDev K;
-  LORB_TRY(kps_finish(ctx, in, kp, nk, S_KP, &K, frame));
+  LORB_TRY(kps_finish(ctx, in, kp, nk, S_KP, &K, frame, !lds_grid));
   const uint8_t *iv = in.dev<uint8_t>(i_iv), *bad = in.dev<uint8_t>(i_bad), *lk = in.dev<uint8_t>(i_lk);
   const float *px = in.dev<float>(i_px), *py = in.dev<float>(i_py), *pxr = in.dev<float>(i_pxr), *vc = in.dev<float>(i_vc);
   const int* pl = in.dev<int>(i_pl);
@@ -660,14 +784,17 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
   const int o_as = out.add(sizeof(int) * ((size_t)nk + 1));
   LORB_TRY(out.alloc(true));  // k_resolve writes assign + count into the mapped block
   const unsigned g = lorb::ceil_div(std::max(np, 1), kCandWaves);
-  const bool strided = (size_t)np * (size_t)nk <= kCandStrided;  // as lorb_search_by_projection_frame
   int2* cand;
   if (strided) {
     LORB_TRY(lorb::scratch_t(ctx, S_W9, std::max<size_t>((size_t)np * nk, 1), &cand));
     if (np > 0) {
       lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
-      hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
-                         reinterpret_cast<const uint4*>(pd), cnt, (const int*)nullptr, cand, nk);
+      if (lds_grid)
+        hipLaunchKernelGGL((k_cand_local<true, true>), dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr,
+                           pl, vc, reinterpret_cast<const uint4*>(pd), cnt, (const int*)nullptr, cand, nk);
+      else
+        hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl,
+                           vc, reinterpret_cast<const uint4*>(pd), cnt, (const int*)nullptr, cand, nk);
     }
   } else {
     if (np > 0) {
@@ -681,10 +808,12 @@ int lorb_search_by_projection_local(lorb_ctx* ctx, const lorb_frame_params* fram
       hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, iv, bad, px, py, pxr, pl, vc,
                          reinterpret_cast<const uint4*>(pd), cnt, off, cand, 0);
   }
-  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), resolve_lds_bytes(np, nk), ctx->stream, np, nk,
+  size_t rlds = 0;
+  const int rmode = resolve_lds_mode(np, nk, &rlds);
+  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), rlds, ctx->stream, np, nk,
                      strided ? (const int*)cnt : (const int*)off, cand, lk,
                      (const float*)nullptr, (const float*)nullptr, res, claim, dassign, (int*)nullptr, (int*)nullptr, dnm,
-                     (int)(resolve_lds_bytes(np, nk) > 0), strided ? nk : 0, out.dev<int>(o_as));
+                     rmode, strided ? nk : 0, out.dev<int>(o_as));
   LORB_CHECK_LAUNCH(ctx);
   LORB_TRY(out.fetch());
   memcpy(assign, out.host<int>(o_as), sizeof(int) * nk);
@@ -729,8 +858,12 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
             i_pos = in.add_t(last->mp_pos, (size_t)nl * 3), i_ld = in.add_t(last->mp_desc, (size_t)nl * 32),
             i_lo = in.add_t(last->octave, nl), i_la = in.add_t(last->angle, nl);
   LORB_TRY(in.commit());
+  // a query has at most nk candidates: up to kCandStrided entries one pass writes them at i * nk
+  // (no count pass, no scan); past it the count / scan / write passes size the list exactly
+  const bool strided = (size_t)nl * (size_t)nk <= kCandStrided;
+  const bool lds_grid = strided && nk <= kStageKps;  // the candidate kernel builds the grid itself
   KpDev K;
-  LORB_TRY(kps_finish(ctx, in, kp, nk, S_KP, &K, cur));
+  LORB_TRY(kps_finish(ctx, in, kp, nk, S_KP, &K, cur, !lds_grid));
   const uint8_t *hm = in.dev<uint8_t>(i_hm), *ol = in.dev<uint8_t>(i_ol), *lk = in.dev<uint8_t>(i_lk),
                 *ld = in.dev<uint8_t>(i_ld);
   const float *pos = in.dev<float>(i_pos), *la = in.dev<float>(i_la);
@@ -748,16 +881,17 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
   const int o_as = out.add(sizeof(int) * ((size_t)nk + 1));
   LORB_TRY(out.alloc(true));  // k_resolve writes assign + count into the mapped block
   const unsigned g = lorb::ceil_div(std::max(nl, 1), kCandWaves);
-  // a query has at most nk candidates: up to kCandBound entries one pass writes them at i * nk
-  // (no count pass, no scan); past it the count / scan / write passes size the list exactly
-  const bool strided = (size_t)nl * (size_t)nk <= kCandStrided;
   int2* cand;
   if (strided) {
     LORB_TRY(lorb::scratch_t(ctx, S_W9, std::max<size_t>((size_t)nl * nk, 1), &cand));
     if (nl > 0) {
       lorb::KernelTimer kt(ctx, LORB_K_WINDOW_CAND);
-      hipLaunchKernelGGL(k_cand_frame<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
-                         reinterpret_cast<const uint4*>(ld), cnt, (const int*)nullptr, cand, nk);
+      if (lds_grid)
+        hipLaunchKernelGGL((k_cand_frame<true, true>), dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
+                           reinterpret_cast<const uint4*>(ld), cnt, (const int*)nullptr, cand, nk);
+      else
+        hipLaunchKernelGGL(k_cand_frame<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
+                           reinterpret_cast<const uint4*>(ld), cnt, (const int*)nullptr, cand, nk);
     }
   } else {
     if (nl > 0) {
@@ -771,10 +905,12 @@ int lorb_search_by_projection_frame(lorb_ctx* ctx, const lorb_frame_params* cur,
       hipLaunchKernelGGL(k_cand_frame<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, nl, hm, ol, pos, lo,
                          reinterpret_cast<const uint4*>(ld), cnt, off, cand, 0);
   }
-  hipLaunchKernelGGL(k_resolve<1>, dim3(1), dim3(1024), resolve_lds_bytes(nl, nk), ctx->stream, nl, nk,
+  size_t rlds = 0;
+  const int rmode = resolve_lds_mode(nl, nk, &rlds);
+  hipLaunchKernelGGL(k_resolve<1>, dim3(1), dim3(1024), rlds, ctx->stream, nl, nk,
                      strided ? (const int*)cnt : (const int*)off, cand, lk,
                      la, K.angle, res, claim, dassign, bins, nulls, dnm,
-                     (int)(resolve_lds_bytes(nl, nk) > 0), strided ? nk : 0, out.dev<int>(o_as));
+                     rmode, strided ? nk : 0, out.dev<int>(o_as));
   LORB_CHECK_LAUNCH(ctx);
   LORB_TRY(out.fetch());
   memcpy(assign, out.host<int>(o_as), sizeof(int) * nk);
@@ -885,10 +1021,11 @@ int lorb_track_local_map_dev(lorb_ctx* ctx, const lorb_frame_params* frame, cons
     hipLaunchKernelGGL(k_cand_local<true>, dim3(g), dim3(256), 0, ctx->stream, K, P, np, d_in_view, pts->is_bad, tx,
                        tx + np, tx + 2 * np, d_level, tx + 3 * np, reinterpret_cast<const uint4*>(pts->desc), cnt, off,
                        cand);
-  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), resolve_lds_bytes(np, nk), ctx->stream, np, nk, off, cand,
+  size_t rlds = 0;
+  const int rmode = resolve_lds_mode(np, nk, &rlds);
+  hipLaunchKernelGGL(k_resolve<0>, dim3(1), dim3(1024), rlds, ctx->stream, np, nk, off, cand,
                      pts->locked, (const float*)nullptr, (const float*)nullptr, res, claim, d_assign, (int*)nullptr,
-                     (int*)nullptr, d_nmatches,
-                     (int)(resolve_lds_bytes(np, nk) > 0));
+                     (int*)nullptr, d_nmatches, rmode);
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
 }

@@ -55,6 +55,13 @@ int main() {
   };
   bench("empty kernel + hipStreamSynchronize", [&] { hipLaunchKernelGGL(k_empty, 1, 64, 0, s, nullptr); (void)hipStreamSynchronize(s); });
   bench("empty kernel + event spin", [&] { hipLaunchKernelGGL(k_empty, 1, 64, 0, s, nullptr); spin(ev, s); });
+  bench("empty kernel + hipStreamQuery spin", [&] {
+    hipLaunchKernelGGL(k_empty, 1, 64, 0, s, nullptr);
+    while (hipStreamQuery(s) == hipErrorNotReady) {
+    }
+  });
+  bench("hipEventRecord only", [&] { (void)hipEventRecord(ev, s); });
+  (void)hipStreamSynchronize(s);
   bench("5 empty kernels + event spin", [&] { for (int k = 0; k < 5; ++k) hipLaunchKernelGGL(k_empty, 1, 64, 0, s, nullptr); spin(ev, s); });
   bench("pinned H2D 30KB + event spin", [&] { (void)hipMemcpyAsync(d_in, h_pin_in, IN, hipMemcpyHostToDevice, s); spin(ev, s); });
   bench("pageable H2D 30KB + event spin", [&] { (void)hipMemcpyAsync(d_in, pg_in.data(), IN, hipMemcpyHostToDevice, s); spin(ev, s); });
