@@ -3224,7 +3224,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   sol = lin + lin_pad;
   LORB_TRY(dalloc(P, 3 * W8, &stp));
   P->fx_n = lin_pad + solve_n;
-  if (comm) {
+  if (comm && comm->nranks > 1) {  // one rank: the partials are the global buffers (in-place collectives)
     LORB_TRY(dalloc(P, lin_pad + solve_n, &linp)); LORB_TRY(dalloc(P, W8, &mxp));
     solp = linp + lin_pad;
     LORB_TRY(dalloc(P, 3 * W8, &stpp));
@@ -4186,7 +4186,9 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   d.wstep = stp;
   P->x2_off = x2_off;
   b.sol_n = solve_n;
-  if (comm) {  // this rank's partial sums (see BaDev), all-reduced into the global buffers
+  // over one rank the exchanges are the identity: the partial buffers are the global ones (the
+  // collectives then run in place, no copy)
+  if (comm && comm->nranks > 1) {  // this rank's partial sums (see BaDev), all-reduced into the global buffers
     double *linp, *mxp, *solp, *stpp;
     LORB_TRY(dalloc(P, lin_pad + solve_n, &linp)); LORB_TRY(dalloc(P, (size_t)1, &mxp));
     solp = linp + lin_pad;

@@ -15,6 +15,11 @@ static ncclRedOp_t nccl_op(int op) { return op == LORB_OP_MAX ? ncclMax : op == 
 int comm_allreduce(lorb_comm* c, const double* d_send, double* d_recv, size_t n, int op) {
   lorb_ctx* ctx = c->ctx;
   if (n == 0) return LORB_OK;
+  if (c->nranks == 1 && !c->rccl) {  // the identity (RCCL runs even over one rank: in place, no copy)
+    if (d_send != d_recv)
+      LORB_HIP(ctx, hipMemcpyAsync(d_recv, d_send, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    return LORB_OK;
+  }
   if (c->rccl) {
     const ncclResult_t r = ncclAllReduce(d_send, d_recv, n, ncclFloat64, nccl_op(op),
                                          static_cast<ncclComm_t>(c->nccl), ctx->stream);
@@ -23,6 +28,7 @@ int comm_allreduce(lorb_comm* c, const double* d_send, double* d_recv, size_t n,
   }
   if (c->pinned_n < n) {
     if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->dbuf) (void)hipFree(c->dbuf);
     c->pinned = nullptr;
     c->pinned_n = 0;
     LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&c->pinned), n * sizeof(double)));
@@ -36,18 +42,28 @@ int comm_allreduce(lorb_comm* c, const double* d_send, double* d_recv, size_t n,
   return LORB_OK;
 }
 
+// host arrays (the plan builds' structure exchanges): over one rank the reduction is the identity;
+// over RCCL through a grow-only device buffer of the communicator (no allocation per call)
 int comm_allreduce_host(lorb_comm* c, double* h, size_t n, int op) {
   lorb_ctx* ctx = c->ctx;
-  if (n == 0) return LORB_OK;
+  if (n == 0 || c->nranks == 1) return LORB_OK;
   if (!c->rccl) return c->fn(c->user, h, (int64_t)n, op) == 0 ? LORB_OK : set_error(ctx, LORB_E_COMM, "host all-reduce callback failed");
-  double* d = nullptr;
-  LORB_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&d), n * sizeof(double)));
+  if (c->dbuf_n < n) {
+    if (c->dbuf) {
+      LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      (void)hipFree(c->dbuf);
+    }
+    c->dbuf = nullptr;
+    c->dbuf_n = 0;
+    LORB_HIP(ctx, hipMalloc(reinterpret_cast<void**>(&c->dbuf), n * sizeof(double)));
+    c->dbuf_n = n;
+  }
   int rc = LORB_OK;
-  if (hipMemcpyAsync(d, h, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream) != hipSuccess) rc = LORB_E_DEVICE;
-  if (rc == LORB_OK) rc = comm_allreduce(c, d, d, n, op);
-  if (rc == LORB_OK && hipMemcpyAsync(h, d, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) rc = LORB_E_DEVICE;
+  if (hipMemcpyAsync(c->dbuf, h, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream) != hipSuccess) rc = LORB_E_DEVICE;
+  if (rc == LORB_OK) rc = comm_allreduce(c, c->dbuf, c->dbuf, n, op);
+  if (rc == LORB_OK && hipMemcpyAsync(h, c->dbuf, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
+    rc = LORB_E_DEVICE;
   if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == LORB_OK) rc = LORB_E_DEVICE;
-  (void)hipFree(d);
   return rc == LORB_OK ? LORB_OK : set_error(ctx, rc, "host-array all-reduce failed");
 }
 

@@ -74,6 +74,8 @@ struct lorb_comm {
   void* user = nullptr;
   double* pinned = nullptr;                // host staging for the callback transport
   size_t pinned_n = 0;
+  double* dbuf = nullptr;                  // device staging of comm_allreduce_host (RCCL; grow-only)
+  size_t dbuf_n = 0;
 };
 
 namespace lorb {
