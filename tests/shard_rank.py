@@ -122,14 +122,15 @@ def main():
     except LorbError as e:
         errs.append(str(e))
     over["n_obs"].free()
+    plan.win = plan._window(arrays, sh["intr"])
     plan.win.n_poses += rank  # rank 1: a window shape that differs from the plan's (seen on the host)
     try:
-        plan.update(arrays)
+        plan.update()
         errs.append("")
     except LorbError as e:
         errs.append(str(e))
     plan.win.n_poses -= rank
-    plan.update(arrays)
+    plan.update()
     plan.solve(opt)
     P, X, S = plan.read()
     res["fail_msgs"] = np.array(errs)
