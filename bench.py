@@ -424,6 +424,11 @@ def workload_c3(ctx, args, rank):
     from lorb_slam_amd import synth
     from lorb_slam_amd.runtime import BAPlanDev
     w = synth.ba_window(seed=3 + 1009 * rank, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400)
+    # observation slots grouped by point (stable), the order the reference's BA adds its residual
+    # blocks in (map point by map point, src/bundle_adjust.cpp:240-280) and the HBM map keeps: the
+    # device plan build takes its sorted path
+    order = np.argsort(np.asarray(w["obs_point"]), kind="stable")
+    w = dict(w, **{k: np.asarray(w[k])[order] for k in ("obs_point", "obs_frame", "obs_uv")})
     arrays = BAPlanDev.upload(ctx, w)
     t0 = time.perf_counter()
     plan = BAPlanDev(ctx, arrays, 20, 2, w["intr"])

@@ -2334,9 +2334,25 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     double cf[16];
     bot.bsk_load(nB - 16, cf);
 #endif
+    // the bottom window's pushes from M's 48 rows: L is final since the B phase, so its 48 entries
+    // per lane are loaded before the wait; after it only y_M's broadcast reads and the FMAs remain
+    // (bs_init's operands in bs_init's order: the same bits)
+    double lb[48];
+    const int brow = bot.bs_row(nB - 16);
+#pragma unroll
+    for (int k = 0; k < 48; ++k) {
+      const bool ok = brow >= 0 && nB + k - brow <= bw;
+      const double v = Ab[ok ? bot.idx(nB + k, brow) : bot.base];
+      lb[k] = ok ? v : 0.0;
+    }
     wait_ge<true>(&s_hand[0], 2);  // a long wait (the M phase): sleep, do not steal LDS cycles
     BS_PH(6);
-    BandSide::BsWin S{bot.bs_init(nB - 16, 48)};
+    TR1(20);
+    double bzw = brow >= 0 ? zb[brow] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 48; ++k) bzw = fma(-lb[k], zb[nB + k], bzw);
+    BandSide::BsWin S{bzw};
+    TR1(21);
 #if LORB_BSK
     bot.bs_run_k(S, nB - 16, 0, cf);                // y_B (reversed)
 #else
@@ -2548,15 +2564,17 @@ __device__ int lm_decide(BaDev d, const LMOpt& o, int w, WinState S, bool valid,
   return rel > o.min_rel;
 }
 
-// K8: per-window iteration tail: camera candidate, step validity, tolerances, accept/reject
+// K8: per-window iteration tail: camera candidate, step validity, tolerances, accept/reject, on one
+// wavefront (no workgroup barrier: the decision is broadcast with readfirstlane).  (Run instead by
+// the last-finishing point group of k_ba_backsub -- a per-window counter behind agent-scope
+// release / acquire fences -- it measured far slower: on the 8-XCD device those fences write back
+// and invalidate L2, C4 step 1.076 -> 1.294 ms.)
 template <bool SH>
-__global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
-  const int w = blockIdx.x;
+__device__ __forceinline__ void lm_end_run(const BaDev& d, const LMOpt& o, int w, int lane) {
   const WinState* Sp = d.st + w;
   WinState S = *Sp;
   const BaWin W = d.win[w];  // issued with the state, before the done test
   if (S.done) return;
-  const int lane = threadIdx.x;
   bool valid = !S.chol_fail;
   double mccs = 0.0, ncost = 0.0, sn2 = 0.0;
   double xc[6] = {0, 0, 0, 0, 0, 0};  // candidate pose of camera pose_base + lane (kept for its jet)
@@ -2575,20 +2593,24 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
     mccs = wave_sum(mccs); ncost = wave_sum(ncost); sn2 = wave_sum(sn2);
     if (SH) { mccs += d.wstep[3 * w]; ncost += d.wstep[3 * w + 1]; sn2 += d.wstep[3 * w + 2]; }
   }
-  __shared__ int s_accept;
   // point-block / Cholesky failures are per iteration: cleared here for the next one (k_ba_lin
   // sets them before k_ba_lm_begin runs)
   S.chol_fail = 0;
   if (SH && lane == 0) d.wfail_part[w] = 0.0;
-  if (lane == 0) s_accept = lm_decide(d, o, w, S, valid, mccs, ncost, sn2);
-  __syncthreads();
+  int acc = 0;
+  if (lane == 0) acc = lm_decide(d, o, w, S, valid, mccs, ncost, sn2);
+  acc = __builtin_amdgcn_readfirstlane(acc);  // lane 0's decision, wave-uniform
   // accepted: the candidate is the new linearisation point -> its rotation states for k_ba_lin
   // (an accepted step is a valid one, so the first 64 candidates are already in registers)
-  if (s_accept) {
+  if (acc) {
     if (lane < W.n_poses) d.rot_lin[W.pose_base + lane] = lorb::rot_jet(xc);
     for (int c = W.pose_base + lane + 64; c < W.pose_base + W.n_poses; c += 64)
       d.rot_lin[c] = lorb::rot_jet(d.x_pose[S.cur ^ 1] + 6 * c);
   }
+}
+template <bool SH>
+__global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
+  lm_end_run<SH>(d, o, blockIdx.x, threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------

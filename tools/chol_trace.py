@@ -28,7 +28,8 @@ print("bottom update:")
 for p, e in enumerate(upd(160, 8)): print("  ", p, e)
 names = ["w2 T done", "w2 got X", "w3 X written", "w0 M start", "w0 M done", "w0 bs start", "w0 bs M done",
          "w0 bs T done", "stage top done", "stage bot done", "linv top done", "linv bot done", "w1 bs B done", "end",
-         "w2 combined", "w2 M handed", "K top start", "K top done", "K bot start", "K bot done"]
+         "w2 combined", "w2 M handed", "K top start", "K top done", "K bot start", "K bot done",
+         "w1 woke", "w1 init done"]
 for k, nm in enumerate(names): print(f"{nm:16s} {v[200 + k]}")
 plan.close()
 for nm, b in (("top", 320), ("bottom", 400)):
