@@ -383,8 +383,9 @@ def sub_c1(ctx, D, args):
     return {"workload": "c1_two_frames_500kps", "value": 1e3 / total, "unit": "C1 sequences/s (a2 + a4 + a12)",
             "ms_per_sequence": total, "stage_ms_median": per, "distinct_inputs": len(xs),
             "call": "host C-ABI (lorb_bf_match, lorb_search_by_projection_frame, lorb_ba_pose_only), synchronous, "
-                    "timed around the ctypes call with the arguments marshalled beforehand; one packed H2D copy and "
-                    "one D2H copy per call"}
+                    "timed around the ctypes call with the arguments marshalled beforehand; the inputs packed into "
+                    "one pinned staging buffer that one kernel pulls into HBM, the results stored by the last "
+                    "kernel straight into pinned memory"}
 
 
 def cpu_baseline_c1(budget_s):
