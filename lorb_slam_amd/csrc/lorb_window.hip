@@ -452,13 +452,21 @@ __device__ __forceinline__ void resolve_run(int np, int nk, const int* cand_off,
   bool lk_t = false;
   float la_t = 0.0f;
   if (regc && t < np) {
-    const int a = stride > 0 ? t * stride : cand_off[t], b = stride > 0 ? a + cand_off[t] : cand_off[t + 1];
     lk_t = pt_locked[t];
     if (MODE == 1) la_t = last_angle[t];
-    rn = min(b - a, kRegCand);
-    if (rn > 0) {
+    if (stride > 0) {
+      // strided lists: the first slots are requested together with the count (one round trip)
+      const int a = t * stride, kmax = min(kRegCand, stride);
 #pragma unroll
-      for (int k = 0; k < kRegCand; ++k) rc[k] = cand[a + min(k, rn - 1)];
+      for (int k = 0; k < kRegCand; ++k) rc[k] = cand[a + min(k, kmax - 1)];
+      rn = min(cand_off[t], kmax);
+    } else {
+      const int a = cand_off[t], b = cand_off[t + 1];
+      rn = min(b - a, kRegCand);
+      if (rn > 0) {
+#pragma unroll
+        for (int k = 0; k < kRegCand; ++k) rc[k] = cand[a + min(k, rn - 1)];
+      }
     }
   }
   for (int c = t; c < nk; c += 1024) claim[c] = kNoClaim;
@@ -535,17 +543,26 @@ __device__ __forceinline__ void resolve_run(int np, int nk, const int* cand_off,
   }
   __syncthreads();
   if (MODE == 1) {
-    if (t == 0) {  // Matcher::ComputeThreeMaxima, src/matcher.cpp:387-428
-      int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-      for (int i = 0; i < LORB_HISTO_LENGTH; i++) {
-        const int s = hist[i];
-        if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-        else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-        else if (s > max3) { max3 = s; ind3 = i; }
+    if (t < 64) {  // Matcher::ComputeThreeMaxima, src/matcher.cpp:387-428, on one wavefront
+      // The reference's insertion loop (strict >, bins in order, counts starting at 0) keeps the
+      // three largest non-zero counts, ties to the lower bin.  Lane = bin; three wave argmax rounds
+      // over the key count * 64 + (63 - bin) (largest count, then lowest bin) give the same bins.
+      static_assert(LORB_HISTO_LENGTH <= 64, "one bin per lane");
+      const int cnt = t < LORB_HISTO_LENGTH ? hist[t] : 0;
+      int key = cnt > 0 ? cnt * 64 + (63 - t) : -1;
+      int ind[3], mx[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        int k = key;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) k = max(k, __shfl_xor(k, o, 64));
+        ind[r] = k >= 0 ? 63 - (k & 63) : -1;
+        mx[r] = k >= 0 ? k >> 6 : 0;
+        if (k >= 0 && t == ind[r]) key = -1;  // taken
       }
-      if ((float)max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
-      else if ((float)max3 < 0.1f * (float)max1) { ind3 = -1; }
-      s_ind[0] = ind1; s_ind[1] = ind2; s_ind[2] = ind3;
+      if ((float)mx[1] < 0.1f * (float)mx[0]) { ind[1] = -1; ind[2] = -1; }
+      else if ((float)mx[2] < 0.1f * (float)mx[0]) { ind[2] = -1; }
+      if (t == 0) { s_ind[0] = ind[0]; s_ind[1] = ind[1]; s_ind[2] = ind[2]; }
     }
     __syncthreads();
     for (int m = t; m < np; m += 1024) {
