@@ -28,10 +28,14 @@ print("bottom update:")
 for p, e in enumerate(upd(160, 8)): print("  ", p, e)
 names = ["w2 T done", "w2 got X", "w3 X written", "w0 M start", "w0 M done", "w0 bs start", "w0 bs M done",
          "w0 bs T done", "stage top done", "stage bot done", "linv top done", "linv bot done", "w1 bs B done", "end",
-         "w2 combined", "w2 M handed", "K top start", "K top done", "K bot start", "K bot done",
-         "w1 woke", "w1 init done"]
+         "w2 combined", "w2 M handed", "K/G top start", "K/G top done", "K/G bot start", "K/G bot done",
+         "w1 woke", "w1 init done", "w3 w top start", "w3 w top done", "w1 w bot start", "w1 w bot done",
+         "w4 comb start", "w5 comb start", "w6 comb start", "w7 comb start",
+         "w4 comb done", "w5 comb done", "w6 comb done", "w7 comb done"]
 for k, nm in enumerate(names): print(f"{nm:16s} {v[200 + k]}")
 plan.close()
+print("G steps top (wave 5):", [v[320 + i] for i in range(16)])
+print("G steps bottom (wave 7):", [v[400 + i] for i in range(16)])
 for nm, b in (("top", 320), ("bottom", 400)):
     st = [(v[b + 3 * i], v[b + 3 * i + 1], v[b + 3 * i + 2]) for i in range(24) if v[b + 3 * i]]
     print(f"bs {nm} blocks (start, after publish+wait, after product):", st)
