@@ -2173,6 +2173,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   __shared__ int s_lrd[2], s_prd[2];  // per side: L panels posted (chain), panel columns posted (update)
   __shared__ int s_hand[3];           // T / B -> M hand-over (below)
   __shared__ int s_cz, s_gd[2], s_wd[2];  // LORB_BSG: top z final; G tiles / w done, per side
+  __shared__ int s_kdone[2];          // LORB_BSK: operator builders done, per side
   const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
   const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
   const int nbk = n16 / 16, ib = 4;
@@ -2212,6 +2213,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
     s_hand[0] = 0; s_hand[1] = 0; s_hand[2] = 0;
     s_cz = 0; s_gd[0] = 0; s_gd[1] = 0; s_wd[0] = 0; s_wd[1] = 0;
+    s_kdone[0] = 0; s_kdone[1] = 0;
     unsigned long long msk = 0;
     for (int b = 0; b < nbk; ++b) msk |= (unsigned long long)(!prog || b < ib || b >= nbk - ib) << (b & 63);
     s_mask = msk;
@@ -2341,7 +2343,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     wait_ge<true>(&s_linv[ks], nkb);
     TR1(16 + 2 * ks);
     for (int b = nkb - 1 - par; b >= 0; b -= 2) kside.bsk_block(16 * b);
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the operators are in L2 before the barrier
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the operators are in L2 before the post
+    if (lane == 0) __hip_atomic_fetch_add(&s_kdone[ks], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     TR1(17 + 2 * ks);
   };
   if (wv == 5 || wv == 7) build_ops(0, wv == 7);
@@ -2434,24 +2437,34 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     if (bad) s_bad = 1;
     C2_STAMP(6);
   }
+#if LORB_BSG
   __syncthreads();
   if (s_bad) {
     if (t == 0) d.st[w].chol_fail = 1;
     return;
   }
+#endif
+  // (LORB_BSK: no barrier here.  Wave 0 goes from M's factor straight into the back-substitution,
+  // wave 1 waits for y_M by flag, the operators are complete by their builders' flags; a failed
+  // factorization (s_bad) only computes values nobody reads and is caught after the last barrier.)
 #ifdef LORB_CHOL_PHASES
 #define BS_PH(k) do { if (lane == 0) d.dbg[8 * w + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define BS_PH(k) do {} while (0)
 #endif
+  // non-LORB_BSG: the side's operator set and window (wave 0 top, wave 1 bottom), then ONE call site
+  // of the unrolled T / B back-substitution for both waves (one copy of its code in the
+  // instruction cache: the bottom side's copy missed it, 4 k cycles before its first block)
+  double cf[16];
+  BandSide::BsWin S{0.0};
   if (wv == 0) {
     BS_PH(3);
 #if LORB_BSK
-    double cf[16];
+    wait_ge<true>(&s_kdone[0], 2);
     top.bsk_load(m - 16, cf);  // the first T block's operator, loaded under the M blocks
 #endif
 #if LORB_BSG
-    BandSide::BsWin S{top.bs_init(m + 32, 0)};
+    S = BandSide::BsWin{top.bs_init(m + 32, 0)};
     TR1(5);
     top.bs_run<false>(S, m + 32, m);                   // y_M (chained triangles)
     BS_PH(4);
@@ -2492,28 +2505,21 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     TR1(30 + (wv - 4));
   }
 #else
-    BandSide::BsWin S{top.bs_init(m + 32, 0)};
+    S = BandSide::BsWin{top.bs_init(m + 32, 0)};
     TR1(5);
     top.bs_run<false>(S, m + 32, m);                   // y_M (chained triangles)
     BS_PH(4);
     TR1(6);
     if (lane < 48) zb[nB + 47 - lane] = zt[m + lane];  // into the reversed bottom rows
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if LORB_BSK
-    top.bs_run_k(S, m - 16, 0, cf);                   // y_T (one product per block)
-#else
-    top.bs_run<true>(S, m - 16, 0);                   // y_T (inverted diagonal blocks)
-#endif
-    BS_PH(5);
-    TR1(7);
   } else if (wv == 1) {
 #if LORB_BSK
-    double cf[16];
+    wait_ge<true>(&s_kdone[1], 2);
     bot.bsk_load(nB - 16, cf);
 #endif
     // the bottom window's pushes from M's 48 rows: L is final since the B phase, so its 48 entries
     // per lane are loaded before the wait; after it only y_M's broadcast reads and the FMAs remain
-    // (bs_init's operands in bs_init's order: the same bits)
+    // (four partial sums: a 48-long dependent FMA chain cost ~2 k cycles)
     double lb[48];
     const int brow = bot.bs_row(nB - 16);
 #pragma unroll
@@ -2522,21 +2528,32 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
       const double v = Ab[ok ? bot.idx(nB + k, brow) : bot.base];
       lb[k] = ok ? v : 0.0;
     }
+#pragma unroll
+    for (int k = 0; k < 48; ++k) asm volatile("" : "+v"(lb[k]));  // loaded here, not sunk past the wait
     wait_ge<true>(&s_hand[0], 2);  // a long wait (the M phase): sleep, do not steal LDS cycles
     BS_PH(6);
     TR1(20);
-    double bzw = brow >= 0 ? zb[brow] : 0.0;
+    double b4[4] = {0.0, 0.0, 0.0, 0.0};
+    const double2* zm2 = reinterpret_cast<const double2*>(zb + nB);
 #pragma unroll
-    for (int k = 0; k < 48; ++k) bzw = fma(-lb[k], zb[nB + k], bzw);
-    BandSide::BsWin S{bzw};
+    for (int k2 = 0; k2 < 24; ++k2) {
+      const double2 v = zm2[k2];
+      b4[(2 * k2) & 3] = fma(lb[2 * k2], v.x, b4[(2 * k2) & 3]);
+      b4[(2 * k2 + 1) & 3] = fma(lb[2 * k2 + 1], v.y, b4[(2 * k2 + 1) & 3]);
+    }
+    const double bzw = (brow >= 0 ? zb[brow] : 0.0) - ((b4[0] + b4[1]) + (b4[2] + b4[3]));
+    S = BandSide::BsWin{bzw};
     TR1(21);
+  }
+  if (wv < 2) {  // y_T (wave 0) / y_B (wave 1, reversed)
+    const BandSide g = wv == 0 ? top : bot;
 #if LORB_BSK
-    bot.bs_run_k(S, nB - 16, 0, cf);                // y_B (reversed)
+    g.bs_run_k(S, (wv == 0 ? m : nB) - 16, 0, cf);  // one product per block
 #else
-    bot.bs_run<true>(S, nB - 16, 0);                // y_B (reversed)
+    g.bs_run<true>(S, (wv == 0 ? m : nB) - 16, 0);  // inverted diagonal blocks
 #endif
-    BS_PH(7);
-    TR1(12);
+    BS_PH(5 + 2 * wv);
+    TR1(wv == 0 ? 7 : 12);
   }
 #endif
 #undef BS_PH
@@ -2545,6 +2562,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   TR1(13);
 #undef C2_STAMP
 #undef TR1
+  if (!LORB_BSG && s_bad) {
+    if (t == 0) d.st[w].chol_fail = 1;
+    return;
+  }
   if (HEAD && s_head_done) return;  // the head ended the solve: no candidate
   for (int k = t; k < n; k += NT) d.ycam[W.row_base + k] = k < rt ? zt[k] : zb[n16 - 1 - k];
   const int cur = S0.cur;
