@@ -1847,12 +1847,18 @@ struct BandSide {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) o[64 * (4 * q + ck) + ((c0 - 48 + 16 * t + ci) & 63)] = acc[t][q];
+      for (int q = 0; q < 4; ++q) {
+        const int k = 4 * q + ck;  // coefficient pairs (k, k + 1) of a lane adjacent: 16-byte loads
+        o[128 * (k >> 1) + 2 * ((c0 - 48 + 16 * t + ci) & 63) + (k & 1)] = acc[t][q];
+      }
   }
   __device__ __forceinline__ void bsk_load(int c0, double (&cf)[16]) const {
-    const double* p = kco + (c0 >> 4) * 1024 + lane;
+    const double2* p = reinterpret_cast<const double2*>(kco + (c0 >> 4) * 1024) + lane;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) cf[k] = p[64 * k];
+    for (int k2 = 0; k2 < 8; ++k2) {
+      const double2 v = p[64 * k2];
+      cf[2 * k2] = v.x; cf[2 * k2 + 1] = v.y;
+    }
   }
   // blocks c_from, c_from - 16, ..., c_to through their bsk_block operators; cf holds block
   // c_from's on entry.  Two coefficient sets alternate, so the next block's loads (L2) stay in
@@ -1863,15 +1869,24 @@ struct BandSide {
     if (trace && lane == 0 && bslot + k < 512) trace[bslot + k] = __builtin_amdgcn_s_memtime() - t0;
 #endif
   }
-  __device__ __forceinline__ void bsk_step(BsWin& S, int c0, const double (&cf)[16]) const {
+  // cn: the next block's operator is requested into cg once z_b is published (the issue of its
+  // loads overlaps the publish's round trip instead of sitting between two blocks)
+  __device__ __forceinline__ void bsk_step(BsWin& S, int c0, const double (&cf)[16], int cn, double (&cg)[16]) const {
     tr_bs(0);
     int row = bs_row(c0);
     asm volatile("" : "+v"(row));
     const int j = row - c0;
     const bool blk = j >= 0;
+    // branch-free: the other lanes' stores go to their dummy slot (xch column 16), their entering-
+    // row load to the zero word (an exec-masked branch made the compiler wait for that load on the
+    // chain right after the product)
+    double* pub = blk ? z + row : xch + 17 * lane + 16;
+    const double* ent = (blk && row >= 64) ? z + (row - 64) : A + zslot;
     double zw = S.zw;
-    if (blk) z[row] = zw;  // z_b is final: publish it
+    *pub = zw;  // z_b is final: publish it
     zw = S.pend ? S.zin : zw;
+    const double zin = *ent;  // the row entering above (never pushed yet: off the chain)
+    bsk_load(cn, cg);
     wave_sync_lds();
     tr_bs(1);
     const double2* zb2 = reinterpret_cast<const double2*>(z + c0);
@@ -1886,10 +1901,8 @@ struct BandSide {
     zw = blk ? sum : zw - sum;
     tr_bs(2);
     const_cast<BandSide*>(this)->bslot += 3;
-    if (blk) {
-      z[row] = zw;                                // y_b (after every lane's broadcast read)
-      S.zin = row - 64 >= 0 ? z[row - 64] : 0.0;  // the row entering above
-    }
+    *pub = zw;  // y_b (after every lane's broadcast read: a wave's LDS operations stay in order)
+    S.zin = zin;
     S.pend = blk;
     S.zw = zw;
   }
@@ -1902,16 +1915,13 @@ struct BandSide {
 #pragma unroll
     for (int it = 0; it < kBskMax; it += 2) {
       if (c0 < c_to) return;
-      bsk_load(c0 - 16 >= c_to ? c0 - 16 : c0, cg);
-      bsk_step(S, c0, cf);
+      bsk_step(S, c0, cf, c0 - 16 >= c_to ? c0 - 16 : c0, cg);
       if (c0 - 16 < c_to) return;
-      bsk_load(c0 - 32 >= c_to ? c0 - 32 : c0, cf);
-      bsk_step(S, c0 - 16, cg);
+      bsk_step(S, c0 - 16, cg, c0 - 32 >= c_to ? c0 - 32 : c0, cf);
       c0 -= 32;
     }
     for (; c0 >= c_to; c0 -= 16) {  // more than kBskMax blocks (narrow bands of ~1000 rows)
-      bsk_load(c0 - 16 >= c_to ? c0 - 16 : c0, cg);
-      bsk_step(S, c0, cf);
+      bsk_step(S, c0, cf, c0 - 16 >= c_to ? c0 - 16 : c0, cg);
 #pragma unroll
       for (int k = 0; k < 16; ++k) cf[k] = cg[k];
     }
