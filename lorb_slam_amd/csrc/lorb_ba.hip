@@ -2107,7 +2107,30 @@ __device__ __forceinline__ void stage_fix(const BaDev& d, const LMOpt& o, double
   }
 }
 
+// stage_fix's term for item q of rows [r0, r1) (one item per thread when (r1 - r0) * 6 <= the
+// threads): its value, and in `at` the band word it is added to (-1: none).  Computed before the
+// band copy, so its loads share the copy's round trip; the same expression, the same bits.
+__device__ __forceinline__ double stage_fix_val(const BaDev& d, const LMOpt& o, const BaWin& W, double radius,
+                                                int r0, int r1, int q, int& at) {
+  r1 = min(r1, W.n);
+  at = -1;
+  if (q >= (r1 - r0) * 6) return 0.0;
+  const int i = r0 + q / 6, i6 = i % 6, j6 = q % 6;
+  if (j6 > i6) return 0.0;
+  const int c = W.pose_base + i / 6;
+  const double* sc = d.scale_pose + 6 * c;
+  double v = d.U[21 * c + u21(i6, j6)] * sc[i6] * sc[j6];
+  if (i6 == j6) v += fmin(fmax(v, o.min_diag), o.max_diag) / radius;
+  at = i * (W.bw + 1) + (j6 - i6 + W.bw);
+  return v;
+}
+
 constexpr int kChol2sThreads = 512;
+// 1: the epilogue's pose state loaded at the kernel's start (registers live through the kernel:
+// 232 -> 256 VGPRs of k_ba_chol_2s<true>; same-box A/B 46.4 / 45.8 vs 46.4 / 45.9 us: off)
+#ifndef LORB_CHOL_EPI_PREFETCH
+#define LORB_CHOL_EPI_PREFETCH 0
+#endif
 // LORB_BSK 1: the T / B back-substitution runs one LDS round trip per block (BandSide::bsk_block /
 // bs_run_k).  LORB_BSG 1 (measured slower, kept for the record): y_T / y_B as w - G y_M, with G
 // and w computed during the M phase (BandSide::bsg_tiles); replaces LORB_BSK's operators.  G's 768
@@ -2139,6 +2162,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
 #ifdef LORB_CHOL_STAMPS
   const unsigned long long st_entry = __builtin_amdgcn_s_memtime();
 #endif
+
   const int w = blockIdx.x;
   // window, state and failure flag requested together (one round trip before the band copy)
   const BaWin W = d.win[w];
@@ -2157,6 +2181,9 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     }
     return;
   }
+#ifdef LORB_CHOL_TRACE
+  if (threadIdx.x == 0) d.dbg[512 * blockIdx.x + 250] = __builtin_amdgcn_s_memtime();  // raw: state loaded
+#endif
   constexpr int NT = kChol2sThreads;
   const int n = W.n, bw = W.bw, B1 = bw + 1;
   const int n16 = (n + 15) & ~15;
@@ -2193,7 +2220,27 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
 
   const bool prog = LORB_CHOL_PROG && nbk <= 64 && nbk > 2 * ib;
   const int cpb = 8 * B1;  // chunks per 16-row block
-  // rhs loads issued before the band copy (one round trip for both)
+  // rhs loads issued before the band copy (one round trip for both), with the fused iteration's
+  // camera-block terms of the rows staged first (16 ib rows per side: one item per thread), which
+  // would otherwise cost a round trip after the copy.  The epilogue's poses go to waves 6 / 7
+  // (camera t - 384), idle since their staging
+  static_assert(16 * 4 * 6 <= kChol2sThreads, "one stage_fix item per thread");
+  int fa0 = -1, fa1 = -1;
+  double fv0 = 0.0, fv1 = 0.0;
+  if (HEAD && prog) {
+    fv0 = stage_fix_val(d, o, W, S0.radius, 0, 16 * ib, t, fa0);
+    fv1 = stage_fix_val(d, o, W, S0.radius, 16 * (nbk - ib), n16, t, fa1);
+  }
+  const int cur = S0.cur, ep = t - (NT - 128);  // epilogue: camera ep (+ 128 k) of the window
+  double xp0[6] = {0, 0, 0, 0, 0, 0}, sp0[6] = {0, 0, 0, 0, 0, 0};
+  if (LORB_CHOL_EPI_PREFETCH && ep >= 0) {  // (waves 6 / 7: uniform)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int c = W.pose_base + (ep < W.n_poses ? ep : 0);
+      xp0[k] = d.x_pose[cur][6 * c + k];
+      sp0[k] = d.scale_pose[6 * c + k];
+    }
+  }
   double rz;
   {
     const int row = t < rt ? t : n16 - 1 - (t - rt);
@@ -2231,8 +2278,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   __syncthreads();
   if (HEAD) {  // the camera blocks of the rows staged so far
     if (prog) {
-      stage_fix(d, o, Ab, W, S0.radius, 0, 16 * ib, t, NT);
-      stage_fix(d, o, Ab, W, S0.radius, 16 * (nbk - ib), n16, t, NT);
+      if (fa0 >= 0) Ab[fa0] = Ab[fa0] + fv0;
+      if (fa1 >= 0) Ab[fa1] = Ab[fa1] + fv1;
     } else {
       stage_fix(d, o, Ab, W, S0.radius, 0, n16, t, NT);
     }
@@ -2252,6 +2299,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   const unsigned long long tr0 = __builtin_amdgcn_s_memtime();
   unsigned long long* trb = d.dbg + 512 * w;
   top.trace = trb; bot.trace = trb; top.t0 = tr0; bot.t0 = tr0;
+  if (t == 0) trb[252] = tr0;  // raw
   top.tslot = wv == 0 ? 0 : 64; bot.tslot = wv == 1 ? 128 : 160;
   top.bslot = 320; bot.bslot = 400;
 #define TR1(k) do { if (lane == 0) trb[200 + (k)] = __builtin_amdgcn_s_memtime() - tr0; } while (0)
@@ -2578,19 +2626,23 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   }
   if (HEAD && s_head_done) return;  // the head ended the solve: no candidate
   for (int k = t; k < n; k += NT) d.ycam[W.row_base + k] = k < rt ? zt[k] : zb[n16 - 1 - k];
-  const int cur = S0.cur;
-  for (int ci2 = t; ci2 < W.n_poses; ci2 += NT) {
+  for (int ci2 = ep; ep >= 0 && ci2 < W.n_poses; ci2 += 128) {
     const int c = W.pose_base + ci2;
     double xn[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
       const int row = 6 * ci2 + k;
       const double y = row < rt ? zt[row] : zb[n16 - 1 - row];
-      xn[k] = d.x_pose[cur][6 * c + k] + (-y) * d.scale_pose[6 * c + k];
+      const double xp = LORB_CHOL_EPI_PREFETCH && ci2 == ep ? xp0[k] : d.x_pose[cur][6 * c + k];
+      const double sp = LORB_CHOL_EPI_PREFETCH && ci2 == ep ? sp0[k] : d.scale_pose[6 * c + k];
+      xn[k] = xp + (-y) * sp;
       d.x_pose[cur ^ 1][6 * c + k] = xn[k];
     }
     d.rot_cand[c] = lorb::rot_val(xn);
   }
+#ifdef LORB_CHOL_TRACE
+  if (t == 0) d.dbg[512 * w + 251] = __builtin_amdgcn_s_memtime();  // raw: epilogue issued (thread 0)
+#endif
 }
 
 // K7: point-group back-substitution: b_p -= sum_e W_e^T y_c(e) (observation phase + ordered

@@ -34,6 +34,7 @@ names = ["w2 T done", "w2 got X", "w3 X written", "w0 M start", "w0 M done", "w0
          "w4 comb done", "w5 comb done", "w6 comb done", "w7 comb done"]
 for k, nm in enumerate(names): print(f"{nm:16s} {v[200 + k]}")
 plan.close()
+print("entry -> traced t0:", v[252] - v[250], " traced t0 -> epilogue issued (thread 0):", v[251] - v[252])
 print("G steps top (wave 5):", [v[320 + i] for i in range(16)])
 print("G steps bottom (wave 7):", [v[400 + i] for i in range(16)])
 for nm, b in (("top", 320), ("bottom", 400)):
