@@ -2657,18 +2657,50 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
   // plan-structure loads of the first chunk and the point's terms go out with the window state
   const int of = g.o0 + min(t, max(g.no - 1, 0));
   const int c_f = g.no > 0 ? d.obs_cam[of] : -1, m_f = g.no > 0 ? d.obs_cm[of] : -1;
-  double b[3] = {0, 0, 0};
+  // ... and so do the point phase's terms (both iterates: cur is not known yet) and the cost
+  // phase's first-chunk observation terms, so the kernel pays three dependent round trips (the
+  // group, these, the camera-indexed ones) instead of six
+  double b[3] = {0, 0, 0}, sp[3] = {0, 0, 0}, Xa[3] = {0, 0, 0}, Xb[3] = {0, 0, 0};
+  double Ei[6] = {0, 0, 0, 0, 0, 0};
   int po0 = 0, po1 = 0;
   if (t < g.cnt) {
     const int p = g.p0 + t;
     po0 = d.pt_obs_off[p]; po1 = d.pt_obs_off[p + 1];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) b[k] = d.etb[3 * p + k] * d.scale_pt[3 * p + k];
+    for (int k = 0; k < 3; ++k) {
+      sp[k] = d.scale_pt[3 * p + k];
+      b[k] = d.etb[3 * p + k] * sp[k];
+      Xa[k] = d.x_pt[0][3 * p + k];
+      Xb[k] = d.x_pt[1][3 * p + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Ei[k] = d.pinv[6 * p + k];
   }
+  const bool has_f = t < g.no;
+  const int lp_f = has_f ? d.obs_pt[of] - g.p0 : 0, fix_f = has_f ? d.obs_fix[of] : 0;
+  double Jp_f[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) Jp_f[k] = has_f ? d.obs_Jp[6 * of + k] : 0.0;
+  const double2 uv_f = has_f ? d.obs_uv[of] : double2{0.0, 0.0};
+  const double r0_f = has_f ? d.obs_r[2 * of] : 0.0, r1_f = has_f ? d.obs_r[2 * of + 1] : 0.0;
   const WinState& S = d.st[g.win];
   if (S.done || S.chol_fail) return;
   const BaWin& W = d.win[g.win];
   const int cur = S.cur;
+  // the first chunk's camera for the cost phase: the candidate pose (rotation state + translation,
+  // written by the Cholesky) or the fixed pose
+  lorb::RotVal R_f{};
+  double pc_f[6] = {0, 0, 0, 0, 0, 0};
+  if (has_f) {
+    if (c_f >= 0) {
+      R_f = d.rot_cand[c_f];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) pc_f[3 + k] = d.x_pose[cur ^ 1][6 * c_f + 3 + k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) pc_f[k] = d.fixed_pose[6 * fix_f + k];
+    }
+  }
   // Jcs y of this thread's first-chunk observation, kept for the model cost change below (the
   // camera part of J step is -Jcs y): Jc is read once
   double ya0 = 0.0, ya1 = 0.0;
@@ -2708,11 +2740,9 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
   double sn2 = 0.0;
   if (t < g.cnt) {
     const int p = g.p0 + t;
-    double sp[3], X[3], Ei[6], step[3];
+    double X[3], step[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * p + k]; X[k] = d.x_pt[cur][3 * p + k]; }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Ei[k] = d.pinv[6 * p + k];
+    for (int k = 0; k < 3; ++k) X[k] = cur ? Xb[k] : Xa[k];
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       step[j] = -(s3(Ei, j, 0) * b[0] + s3(Ei, j, 1) * b[1] + s3(Ei, j, 2) * b[2]);
@@ -2729,19 +2759,20 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
   double mcc = 0.0, ncost = 0.0;
   for (int c0 = t; c0 < g.no; c0 += kGB) {
     const int e = g.o0 + c0;
-    const int c = d.obs_cam[e];
-    const int lp = d.obs_pt[e] - g.p0;
+    const bool first = c0 == t;  // (the prefetched terms: e == of)
+    const int c = first ? c_f : d.obs_cam[e];
+    const int lp = first ? lp_f : d.obs_pt[e] - g.p0;
     const double Xn[3] = {sxn[lp][0], sxn[lp][1], sxn[lp][2]};
     double m0 = 0.0, m1 = 0.0;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
-      m0 += d.obs_Jp[6 * e + j] * sst[lp][j];
-      m1 += d.obs_Jp[6 * e + 3 + j] * sst[lp][j];
+      m0 += (first ? Jp_f[j] : d.obs_Jp[6 * e + j]) * sst[lp][j];
+      m1 += (first ? Jp_f[3 + j] : d.obs_Jp[6 * e + 3 + j]) * sst[lp][j];
     }
-    const double2 uv = d.obs_uv[e];
+    const double2 uv = first ? uv_f : d.obs_uv[e];
     double rn[2];
     if (c >= 0) {
-      if (c0 == t) {
+      if (first) {
         m0 -= ya0;
         m1 -= ya1;
       } else {  // observations beyond the first chunk (points with > kGB observations)
@@ -2758,14 +2789,15 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
         m1 -= a1;
       }
       // candidate camera (end of k_ba_chol): x_pose[cur ^ 1] with its rotation state
-      residual_s(d.rot_cand[c], d.x_pose[cur ^ 1] + 6 * c + 3, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
+      if (first) residual_s(R_f, pc_f + 3, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
+      else residual_s(d.rot_cand[c], d.x_pose[cur ^ 1] + 6 * c + 3, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
     } else {
       double pose[6];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[e] + k];
+      for (int k = 0; k < 6; ++k) pose[k] = first ? pc_f[k] : d.fixed_pose[6 * d.obs_fix[e] + k];
       residual(pose, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
     }
-    const double r0 = d.obs_r[2 * e], r1 = d.obs_r[2 * e + 1];
+    const double r0 = first ? r0_f : d.obs_r[2 * e], r1 = first ? r1_f : d.obs_r[2 * e + 1];
     mcc += m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0);
     ncost += 0.5 * (rn[0] * rn[0] + rn[1] * rn[1]);
   }
