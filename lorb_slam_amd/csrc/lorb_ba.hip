@@ -1448,6 +1448,9 @@ __device__ __forceinline__ void wait_ge(int* c, int v) {
     if (SLEEP) __builtin_amdgcn_s_sleep(1);
 }
 
+#ifndef LORB_UPD_SPIN
+#define LORB_UPD_SPIN 0
+#endif
 // Column stride of the chain's L columns in xch, padded against bank conflicts when the update
 // wave reads them in MFMA operand layout.
 constexpr int kCS = 65;
@@ -1637,7 +1640,7 @@ struct BandSide {
       tn_addr += dstep;
       const bool nxt = kb + 16 < kend;
       tr(0);
-      wait_ge<true>(lrd, ++lwant);
+      wait_ge<!LORB_UPD_SPIN>(lrd, ++lwant);
       tr(1);
       double opA[4][4];
 #pragma unroll
