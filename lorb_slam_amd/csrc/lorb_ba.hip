@@ -2026,9 +2026,10 @@ struct BandSide {
 // threads, U chunks per thread per batch with all loads of a batch issued before any store.
 // Element (i, off) keeps S's value inside the matrix; the left triangle of the first bw rows is
 // zeroed and rows n .. n16-1 are an identity pad.
-template <int U>
+struct StageFix;
+template <int U, bool FIX = false>
 __device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, double* Ab, int a0, int a1, int b0, int b1,
-                                            int tid, int nthr, int n, int bw, int nsrc);
+                                            int tid, int nthr, int n, int bw, int nsrc, const StageFix* fx = nullptr);
 template <int U>
 __device__ __forceinline__ void stage_band(const double2* __restrict__ S2, double* Ab, int j0, int j1, int tid,
                                            int nthr, int n, int bw, int nsrc) {
@@ -2059,19 +2060,45 @@ __device__ __forceinline__ void stage_band(const double2* __restrict__ S2, doubl
 }
 
 
-// the same over two chunk ranges [a0, a1) and [b0, b1), all loads of a batch before any store
-template <int U>
+// the fused iteration's camera-block terms (stage_fix's), added by the staging thread itself
+struct StageFix {
+  const double* U; const double* sc; int pose_base; double min_diag, max_diag, radius;
+  // element (i, j), i < n: the term of its camera block (0 off the 6 x 6 diagonal blocks); the
+  // loads go out with the band chunk's
+  __device__ __forceinline__ double term(int i, int j) const {
+    const int i6 = i % 6, cb = i - i6;
+    if (j < cb) return 0.0;
+    const int j6 = j - cb, c = pose_base + i / 6;
+    double v = U[21 * c + u21(i6, j6)] * sc[6 * c + i6] * sc[6 * c + j6];
+    if (i6 == j6) v += fmin(fmax(v, min_diag), max_diag) / radius;
+    return v;
+  }
+};
+
+// the same over two chunk ranges [a0, a1) and [b0, b1), all loads of a batch before any store;
+// FIX: every element of the batch also gets its camera-block term (e + v: stage_fix's bits)
+template <int U, bool FIX>
 __device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, double* Ab, int a0, int a1, int b0, int b1,
-                                            int tid, int nthr, int n, int bw, int nsrc) {
+                                            int tid, int nthr, int n, int bw, int nsrc, const StageFix* fx) {
   const int B1 = bw + 1, la = a1 - a0, tot = la + (b1 - b0);
   for (int vb = tid; vb < tot; vb += nthr * U) {
     double2 v[U];
     int jj[U];
+    double fv[FIX ? U : 1][2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int vv = vb + nthr * u;
       jj[u] = vv < la ? a0 + vv : b0 + (vv - la);
       v[u] = S2[(vv < tot && jj[u] < nsrc) ? jj[u] : 0];
+      if (FIX) {
+        int i = (2 * jj[u]) / B1, off = (2 * jj[u]) % B1;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const bool in = vv < tot && i < n && i - (bw - off) >= 0;
+          fv[u][h] = in ? fx->term(i, i + off - bw) : 0.0;
+          if (++off == B1) { off = 0; ++i; }
+        }
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -2083,6 +2110,7 @@ __device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, doub
         for (int h = 0; h < 2; ++h) {
           const bool in = i < n && i - (bw - off) >= 0;
           e[h] = in ? e[h] : ((i >= n && off == bw) ? 1.0 : 0.0);
+          if (FIX && in) e[h] = e[h] + fv[u][h];
           if (++off == B1) { off = 0; ++i; }
         }
         reinterpret_cast<double2*>(Ab)[j] = double2{e[0], e[1]};
@@ -2129,6 +2157,10 @@ __device__ __forceinline__ double stage_fix_val(const BaDev& d, const LMOpt& o, 
 }
 
 constexpr int kChol2sThreads = 512;
+// 1: the first batch's camera-block terms added by the staging threads (no fix pass + barrier)
+#ifndef LORB_CHOL_FFIX
+#define LORB_CHOL_FFIX 0
+#endif
 // 1: the epilogue's pose state loaded at the kernel's start (registers live through the kernel:
 // 232 -> 256 VGPRs of k_ba_chol_2s<true>; same-box A/B 46.4 / 45.8 vs 46.4 / 45.9 us: off)
 #ifndef LORB_CHOL_EPI_PREFETCH
@@ -2230,7 +2262,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   static_assert(16 * 4 * 6 <= kChol2sThreads, "one stage_fix item per thread");
   int fa0 = -1, fa1 = -1;
   double fv0 = 0.0, fv1 = 0.0;
-  if (HEAD && prog) {
+  if (HEAD && prog && !LORB_CHOL_FFIX) {
     fv0 = stage_fix_val(d, o, W, S0.radius, 0, 16 * ib, t, fa0);
     fv1 = stage_fix_val(d, o, W, S0.radius, 16 * (nbk - ib), n16, t, fa1);
   }
@@ -2251,7 +2283,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     // fused: the rhs holds -r; + V sc (k_ba_schur<false>'s vs - r, same bits)
     if (HEAD && t < rt + rb && row < n) rz = rz + d.V[6 * W.pose_base + row] * d.scale_pose[6 * W.pose_base + row];
   }
-  if (prog) {  // both sides' first ib blocks in one batch
+  if (prog && HEAD && LORB_CHOL_FFIX) {  // ... with the camera-block terms added as they are staged
+    const StageFix fx{d.U, d.scale_pose, W.pose_base, o.min_diag, o.max_diag, S0.radius};
+    stage_band2<7, true>(S2, Ab, 0, ib * cpb, (nbk - ib) * cpb, nch, t, NT, n, bw, nsrc, &fx);
+  } else if (prog) {  // both sides' first ib blocks in one batch
     stage_band2<7>(S2, Ab, 0, ib * cpb, (nbk - ib) * cpb, nch, t, NT, n, bw, nsrc);
   } else {
     stage_band<14>(S2, Ab, 0, nch, t, NT, n, bw, nsrc);
@@ -2279,7 +2314,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     s_mask = msk;
   }
   __syncthreads();
-  if (HEAD) {  // the camera blocks of the rows staged so far
+  if (HEAD && !(prog && LORB_CHOL_FFIX)) {  // the camera blocks of the rows staged so far
     if (prog) {
       if (fa0 >= 0) Ab[fa0] = Ab[fa0] + fv0;
       if (fa1 >= 0) Ab[fa1] = Ab[fa1] + fv1;
