@@ -16,4 +16,4 @@ for i in 1 2; do
     LORB_LIB_PATH=$L tools/gpu_step.sh 300 $O/x_$v$i.log rocprofv3 --kernel-trace --stats -d $P/$v$i -o x --output-format csv -- python3 $R/bench.py --workload c4 --no-cpu-baseline $NOSUB --steps 10 --warmup 2 || exit $?
   done
 done
-for f in $(find $P -name "*kernel_stats.csv" | sort); do echo "$f $(grep 'k_ba_chol_2s<true>' $f | cut -d, -f4)"; done > $O/x_summary.txt
+for f in $(find $P -name "*kernel_stats.csv" | sort); do echo "$f $(grep 'k_ba_chol_2s<true>' $f | cut -d, -f4) $(grep 'k_ba_lin(' $f | cut -d, -f4)"; done > $O/x_summary.txt
