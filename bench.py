@@ -55,7 +55,7 @@ K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_schur", 3: "k_ba
 # rocprofv3 short names (tools/pmc_traffic.py) of the same kernels, for the PMC traffic lookup
 K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_2s"}
 # committed PMC summaries, newest first; each is keyed by workload (tools/pmc_traffic.py)
-TRAFFIC = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r04", "r03", "r02", "r01")]
+TRAFFIC = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r05", "r04", "r03", "r02", "r01")]
 METRIC = "ORB matches/sec + local-BA iterations/sec (50 KF, 10k pts) at 1/2/4/8 MI355X"
 
 
@@ -195,6 +195,11 @@ def workload_c4(ctx, args, rank):
     t0 = time.perf_counter()
     maps = [LocalMap(ctx, s["init"]) for s in seqs]
     create_ms = (time.perf_counter() - t0) * 1e3
+    # the keyframes below are uploaded (synchronously) before any step: step t+1's match and append
+    # may run under step t's solve (lorb_map_set_overlap's requirement; tests/test_gpu_map.py checks
+    # the overlapped chain bit-for-bit against the serial one)
+    for m in maps:
+        m.set_overlap(True)
     fp = A.make_frame_params(synth.frame_params())
     # the keyframe stream, resident in HBM before the timed region
     kfs = [[(k["pose"], k["Tcw"], len(k["x"]), ctx.to_device(A.u8(k["desc"])), ctx.to_device(A.f32(k["x"])),
@@ -255,6 +260,33 @@ def workload_c4(ctx, args, rank):
                         "new_kf_keypoints": nq, "match": f"{nq}x~{n_pts} bf crossCheck",
                         "step": "match + unproject + append + slide/cull + device plan build + 10 LM its + write-back"},
                 cpu=lambda: cpu_baseline_c4(seqs[0], args.cpu_budget))
+
+
+def sub_c4x8(ctx, D, args):
+    """A filled GPU: the C4 chained step on 8 independent HBM-resident windows per
+    GPU, stepped together (each step issues one keyframe to every window; north_star shards
+    independent windows).  One window leaves most CUs idle during its Cholesky; this line shows
+    what one MI355X sustains with 8 in flight.  It does not replace the headline (one window)."""
+    import copy
+    a = copy.copy(args)
+    a.windows, a.steps, a.warmup = 8, max(10, min(args.steps, 20)), max(2, min(args.warmup, 3))
+    wl = workload_c4(ctx, a, D.rank)
+    elapsed = timed(ctx, D, wl, a.steps, a.warmup)
+    chk = wl["check"]()
+    rwin = chk.pop("_window", None)
+    kt, pn = profile_pass(ctx, wl, a.steps)
+    total = D.reduce(wl["ba_iters"] * a.steps, "SUM")
+    ms = elapsed / a.steps * 1e3
+    wl["traffic_key"] = "c4x8"
+    out = {"workload": "c4_local_mapping_step_chained_x8", "config": wl["config"], "value": total / elapsed,
+           "unit": "BA iterations/s", "steps": a.steps, "ms_per_step": ms,
+           "roofline": roofline_entry(kt, wl, pn),
+           # per window-iteration: the step's time / (10 iterations x 8 windows)
+           "roofline_iteration": roofline_iteration(rwin, wl["config"]["kf"], ms / (10.0 * a.windows), "c4x8")
+           if rwin is not None else None,
+           "check": {"windows": chk["windows"][:2], "keyframes_stepped": chk["keyframes_stepped"]}}
+    wl["cleanup"]()
+    return out
 
 
 def cpu_baseline_c4(seq, budget_s):
@@ -566,7 +598,7 @@ def workload_shared(ctx, args, rank, D, comm):
     # whole-job units: the shared window's iterations / matches are counted once (rank 0 only)
     return dict(step=step, check=check, ba_iters=10.0 if rank == 0 else 0.0, matches=float(nq) if rank == 0 else 0.0,
                 pairs=float(b - a) * nt, plan_ms=plan_ms, cleanup=cleanup, kspec=kspec,
-                traffic_key=f"shared_w{world}", n_ranks=world,
+                traffic_key=f"shared_w{world}", n_ranks=world, window=win, n_poses=50,
                 config={"workload": "c5_shared_window", "kf": 50, "fixed_kf": 5, "points": len(win["point_init"]),
                         "observations": n_obs, "lm_iterations": 10, "new_kf_keypoints": nq,
                         "match": f"{nq}x{nt} bf crossCheck, query rows sharded", "points_this_rank": len(sh["point_init"]),
@@ -576,13 +608,13 @@ def workload_shared(ctx, args, rank, D, comm):
 
 def workload_c2(ctx, args, rank):
     """BASELINE config 1: brute-force Hamming 2000x2000 random 256-bit + ratio test, batched
-    over `pairs` independent frame pairs per GPU (each pair is a full 2000x2000 problem; the
-    inputs cycle through `unique` generated pairs to keep input generation short)."""
+    over `pairs` independent frame pairs per GPU (each pair is a full 2000x2000 problem with its
+    own seeded descriptors: every problem of the batch is distinct)."""
     from lorb_slam_amd import _abi as A
     from lorb_slam_amd import synth
     from lorb_slam_amd.runtime import lib
     B = args.pairs
-    U = min(B, 64)
+    U = B
     gen = [synth.bf_problem(seed=1000 * rank + p, nq=2000, nt=2000, n_planted=1000, random_levels=True) for p in range(U)]
     qs = [gen[p % U][0] for p in range(B)]
     ts = [gen[p % U][1] for p in range(B)]
@@ -829,11 +861,16 @@ def sub_shared(ctx, D, args, comm):
     its = 10.0 * pn
     ar_ms = D.reduce(ar[0] / its if its else 0.0, "MAX")
     wl["cleanup"]()
+    ms = elapsed / steps * 1e3
+    # SURVEY 8(d)'s per-iteration figures of the WHOLE window (all ranks' points); the PMC bytes are
+    # this rank's (at one rank: the whole window)
+    rit = (roofline_iteration(wl["window"], wl["n_poses"], ms / 10.0, wl["traffic_key"])
+           if wl.get("window") is not None else None)
     return {"workload": wl["config"]["workload"], "n_ranks": wl["n_ranks"], "scaling": "strong",
-            "value": total / elapsed, "unit": "BA iterations/s", "steps": steps, "ms_per_step": elapsed / steps * 1e3,
+            "value": total / elapsed, "unit": "BA iterations/s", "steps": steps, "ms_per_step": ms,
             "plan_create_ms": wl["plan_ms"], "allreduce_ms_per_iteration": ar_ms,
             "allreduce_launches_per_iteration": (ar[1] / its) if its else 0.0,
-            "roofline": roofline_entry(kt, wl, pn), "config": wl["config"], "check": chk}
+            "roofline": roofline_entry(kt, wl, pn), "roofline_iteration": rit, "config": wl["config"], "check": chk}
 
 
 def sub_dropin(ctx, D, args):
@@ -894,6 +931,7 @@ def main():
     ap.add_argument("--no-shared", action="store_true", help="skip the shared-window (RCCL) sub-record")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 local-BA sub-record")
     ap.add_argument("--no-c1", action="store_true", help="skip the C1 per-frame tracking sub-record")
+    ap.add_argument("--no-c4x8", action="store_true", help="skip the 8-windows-per-GPU C4 sub-record")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -941,6 +979,7 @@ def main():
     dropin = sub_dropin(ctx, D, args) if (args.workload == "c4" and not args.no_dropin) else None
     c1 = sub_c1(ctx, D, args) if (args.workload == "c4" and not args.no_c1) else None
     c3 = sub_c3(ctx, D, args) if (args.workload == "c4" and not args.no_c3) else None
+    c4x8 = sub_c4x8(ctx, D, args) if (args.workload == "c4" and args.windows == 1 and not args.no_c4x8) else None
     shared = (sub_shared(ctx, D, args, comm) if (args.workload in ("c4", "rehearse") and not args.no_shared)
               else None)
     if D.rank == 0:
@@ -965,7 +1004,7 @@ def main():
                                                       elapsed / args.steps * 1e3 / max(wl["ba_iters"], 1.0),
                                                       wl["traffic_key"])
                                    if rwin is not None and wl["ba_iters"] > 0 else None),
-            "cpu_baseline": cpu, "c2": c2, "c3": c3, "dropin_local_ba": dropin, "shared": shared, "c1": c1,
+            "cpu_baseline": cpu, "c2": c2, "c3": c3, "c4x8": c4x8, "dropin_local_ba": dropin, "shared": shared, "c1": c1,
             "check": check,
         }
         if rehearse:

@@ -574,8 +574,21 @@ int lorb_map_create(lorb_ctx* ctx, const lorb_map_init* init, lorb_map** out);
 int lorb_map_step_dev(lorb_map* map, const lorb_frame_params* frame, const float pose[6], const float Tcw[16],
                       int32_t n, const uint8_t* d_desc, const float* d_x, const float* d_y, const float* d_depth,
                       const lorb_lm_options* opt);
+/* Overlap of consecutive steps (default off): with enable = 1, step t+1's match and append run on a
+ * stream the map owns, concurrently with step t's BA solve, ordered only after step t's plan build
+ * (they touch the map's descriptors, new slots and counts and the map's own key buffers -- nothing
+ * the solve or its write-back reads or writes).  Results are bit-identical to enable = 0.
+ * REQUIREMENT while enabled: the keyframe arrays handed to lorb_map_step_dev (d_desc, d_x, d_y,
+ * d_depth) must be complete when the call is made -- uploaded or produced by work the caller has
+ * already synchronised.  The map's stream is not ordered after work still queued on the ctx stream
+ * or any other stream, so inputs produced asynchronously need enable = 0 (then every kernel of a
+ * step runs on the ctx stream, in order).  The reference's LocalMapping::Run consumes keyframes the
+ * tracking thread has finished (src/local_mapping.cpp:19-40), which is the enabled case.  Per-kernel
+ * timing (lorb_kernel_timing_enable) runs the steps serially either way. */
+int lorb_map_set_overlap(lorb_map* map, int32_t enable);
 /* first n of: [0] points, [1] observations, [2] t0, [3] last step's keypoints, [4] its new points,
- * [5] its new observations (matches + new points), [6] its matches, [7] W.  Synchronises. */
+ * [5] its new observations (matches + new points), [6] its matches, [7] W, [8] steps whose match and
+ * append ran overlapped (lorb_map_set_overlap).  Synchronises. */
 int lorb_map_counts(lorb_map* map, int32_t* out, int32_t n);
 int lorb_map_read(lorb_map* map, const lorb_map_state* state);
 int lorb_map_plan(lorb_map* map, lorb_ba_plan** out);   /* the map's BA plan (owned by the map) */

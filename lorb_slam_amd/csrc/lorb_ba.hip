@@ -13,6 +13,13 @@
 //     fixed order (deterministic, no FP64 atomics), an envelope (profile) Cholesky of S per
 //     window in LDS, and per-point back-substitution.
 //   * all reductions are fixed-order trees (block partials reduced in index order).
+//
+// FP64 contraction: the BA arithmetic may fuse multiply-adds (v_fma_f64; its parity bar is 1e-5
+// relative, not bit-exactness -- VERDICT r04 item 3).  The Makefile's global -ffp-contract=off stays
+// for the float paths that must be bit-exact (projection, grid, unprojection, ORB, stereo: the other
+// translation units).  Everything in this file is deterministic either way (fixed reduction orders);
+// the host code here (cv::Rodrigues restated, x86-64 without FMA) is unaffected.
+#pragma clang fp contract(fast)
 #include "lorb_ba_math.h"
 #include "lorb_internal.h"
 

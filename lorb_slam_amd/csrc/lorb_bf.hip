@@ -609,15 +609,29 @@ int lorb::match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8
   hipStream_t st = stream ? stream : ctx->stream;
   unsigned long long* qkey = nullptr;
   LORB_TRY(lorb::scratch_t(ctx, S_BF_QKEY, (size_t)std::max(nq, 1), &qkey));
+  uint32_t* tkey = nullptr;
+  size_t ready = 0;
+  if (nt > 0 && nq > 0) {
+    LORB_TRY(tkeys1(ctx, nt, st, &tkey));
+    ready = ctx->tkey_ready;
+    ctx->tkey_ready = 0;  // until the merge has been enqueued (it restores the all-ones)
+  }
+  LORB_TRY(lorb::match1_keys_into(ctx, d_q, nq, d_t, nt, qkey, tkey, st));
+  if (tkey) ctx->tkey_ready = ready;
+  *qkey_out = qkey;
+  return LORB_OK;
+}
+
+// The same into caller-owned buffers: qkey (nq entries) and tkey (nt entries, all-ones on entry;
+// the merge restores the all-ones).  The LocalMapping step owns its pair, so its side-stream match
+// shares no scratch with matcher calls on the ctx stream.
+int lorb::match1_keys_into(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
+                           unsigned long long* qkey, uint32_t* tkey, hipStream_t st) {
   if (nt > 0 && nq > 0) {
     // reverse pass: lanes = trains, uniform = queries -> nearest query per train
     if (nq > (int)kIdxMask) return lorb::set_error(ctx, LORB_E_INVALID, "problem 0: %d uniform items > 2^23-1", nq);
     int qpl = 2;
     const BfGrid1 g = grid1_of(nq, nt, &qpl);
-    uint32_t* tkey = nullptr;
-    LORB_TRY(tkeys1(ctx, nt, st, &tkey));
-    const size_t ready = ctx->tkey_ready;
-    ctx->tkey_ready = 0;  // until the merge has been enqueued (it restores the all-ones)
     const unsigned nb = (unsigned)(g.lane_tiles * g.n_chunks);
     {
       lorb::KernelTimer kt(ctx, LORB_K_BF_SCAN_TOP1);
@@ -633,12 +647,10 @@ int lorb::match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8
     }
     hipLaunchKernelGGL(k_cc_merge1, dim3(lorb::ceil_div(nt, 256)), dim3(256), 0, st, tkey, nt, qkey);
     LORB_CHECK_LAUNCH(ctx);
-    ctx->tkey_ready = ready;
   } else if (nq > 0) {
     LORB_HIP(ctx, hipMemsetAsync(qkey, 0xff, sizeof(unsigned long long) * nq, st));
   }
   LORB_CHECK_LAUNCH(ctx);
-  *qkey_out = qkey;
   return LORB_OK;
 }
 

@@ -28,7 +28,6 @@ int comm_allreduce(lorb_comm* c, const double* d_send, double* d_recv, size_t n,
   }
   if (c->pinned_n < n) {
     if (c->pinned) (void)hipHostFree(c->pinned);
-  if (c->dbuf) (void)hipFree(c->dbuf);
     c->pinned = nullptr;
     c->pinned_n = 0;
     LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&c->pinned), n * sizeof(double)));
@@ -110,6 +109,7 @@ int lorb_comm_destroy(lorb_comm* c) {
   if (c->ctx && c->ctx->stream) (void)hipStreamSynchronize(c->ctx->stream);
   if (c->rccl && c->nccl) (void)ncclCommDestroy(static_cast<ncclComm_t>(c->nccl));
   if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->dbuf) (void)hipFree(c->dbuf);
   delete c;
   return LORB_OK;
 }

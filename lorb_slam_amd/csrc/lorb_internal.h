@@ -121,6 +121,10 @@ const int* ba_plan_point_offsets(const lorb_ba_plan* P);
 // query (dist << 32 | train) or all-ones; *qkey_out is ctx scratch valid until the next matcher call
 int match1_keys_dev(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
                     unsigned long long** qkey_out, hipStream_t stream = nullptr);  // null: ctx->stream
+// the same into caller-owned buffers: qkey (nq entries), tkey (nt entries, all-ones on entry and
+// again once the call's kernels have run), on stream st
+int match1_keys_into(lorb_ctx* ctx, const uint8_t* d_q, int nq, const uint8_t* d_t, int nt,
+                     unsigned long long* qkey, uint32_t* tkey, hipStream_t st);
 
 // grow-only scratch: returns device pointer in *out
 int scratch(lorb_ctx* ctx, int slot, size_t bytes, void** out);

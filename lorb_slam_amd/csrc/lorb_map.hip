@@ -324,17 +324,25 @@ struct lorb_map {
   double prof_ms[8] = {};
   int prof_n = 0;
   int* mt = nullptr;
+  // the step's crossCheck keys: per-query keys and per-train keys (all-ones between steps), owned by
+  // the map so that its side-stream match shares no scratch with matcher calls on the ctx stream
+  unsigned long long* qkey = nullptr;
+  uint32_t* tkey = nullptr;
   int* pinned = nullptr;
   lorb_ba_plan* plan = nullptr;
   bool plan_ok = false;  // plan built on the current slots (its point offsets serve the compaction)
   bool broken = false;   // a failed step whose counts could not be re-read: the map is unusable
-  // Overlap (LORB_MAP_OVERLAP, default on): a step's match and append touch only the map's point
-  // descriptors, its new slots / points and counts -- nothing the previous step's LM solve and
-  // write-back read or write -- so they run on a side stream as soon as the previous step's plan
-  // build has read the map (ev_built), concurrently with that solve; the slide waits for both.
+  // Overlap (lorb_map_set_overlap, default off): a step's match and append touch only the map's
+  // point descriptors, its new slots / points and counts, its own key buffers -- nothing the previous
+  // step's LM solve and write-back read or write -- so they run on a side stream as soon as the
+  // previous step's plan build has read the map (ev_built), concurrently with that solve; the slide
+  // waits for both.  The caller's keyframe arrays must be complete when the step is called (the side
+  // stream is not ordered after work the caller still has queued, lorb_c.h).
+  bool overlap = false;
   hipStream_t side = nullptr;
   hipEvent_t ev_built = nullptr, ev_app = nullptr;
   bool built = false;  // ev_built recorded by the previous step
+  int n_overlapped = 0;  // steps whose match + append ran on the side stream
   std::vector<void*> allocs;
   ~lorb_map() {
     if (prof && prof_n)
@@ -387,6 +395,9 @@ int map_alloc(lorb_map* M, const lorb_map_init* in) {
   const size_t n = (size_t)std::max(in->max_keypoints, 1);
   M->n_cap = (int)n;
   LORB_TRY(malloc_n(M, n, &M->mt));
+  LORB_TRY(malloc_n(M, n, &M->qkey));
+  LORB_TRY(malloc_n(M, P, &M->tkey));
+  LORB_HIP(M->ctx, hipMemsetAsync(M->tkey, 0xff, sizeof(uint32_t) * std::max<size_t>(P, 1), M->ctx->stream));
   LORB_HIP(M->ctx, hipHostMalloc(reinterpret_cast<void**>(&M->pinned), sizeof(int) * 8));
   return LORB_OK;
 }
@@ -524,19 +535,22 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
     return LORB_OK;
   };
   LORB_TRY(mark(7));
-  static const bool ovl_env = [] { const char* e = getenv("LORB_MAP_OVERLAP"); return !(e && e[0] == '0'); }();
-  const bool ovl = ovl_env && M->built && !M->prof && !ctx->ktime;
+  const bool ovl = M->overlap && M->built && !M->prof && !ctx->ktime;
   if (ovl && !M->side) {
     LORB_HIP(ctx, hipStreamCreateWithFlags(&M->side, hipStreamNonBlocking));
     LORB_HIP(ctx, hipEventCreateWithFlags(&M->ev_app, hipEventDisableTiming));
   }
   hipStream_t ms = ovl ? M->side : s;  // the match + append stream
+  M->n_overlapped += ovl;
   if (ovl) LORB_HIP(ctx, hipStreamWaitEvent(ms, M->ev_built, 0));
   // 1. SearchLocalPoints: the keyframe's descriptors against the map's points -- the crossCheck keys
   //    here, the finalisation (minDist filter) inside the append
   unsigned long long* qkey = nullptr;
   const bool has_t = M->h_P > 0;
-  if (n > 0 && has_t) LORB_TRY(lorb::match1_keys_dev(ctx, d_desc, n, m.desc, M->h_P, &qkey, ms));
+  if (n > 0 && has_t) {
+    LORB_TRY(lorb::match1_keys_into(ctx, d_desc, n, m.desc, M->h_P, M->qkey, M->tkey, ms));
+    qkey = M->qkey;
+  }
   LORB_TRY(mark(0));
   LORB_TRY(mark(1));
   // 2 + 3. AddObservation / new points at UnprojectStereo (Twc = mTcw.inv(), src/frame.cpp:350),
@@ -607,13 +621,23 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   return LORB_OK;
 }
 
+int lorb_map_set_overlap(lorb_map* M, int32_t enable) {
+  if (!M || (enable != 0 && enable != 1)) return LORB_E_INVALID;
+  M->overlap = enable == 1;
+  if (!M->overlap && M->side) {  // later steps run on the ctx stream only: drain the side stream's work
+    LORB_HIP(M->ctx, hipStreamSynchronize(M->side));
+  }
+  return LORB_OK;
+}
+
 int lorb_map_counts(lorb_map* M, int32_t* out, int32_t n) {
   if (!M || !out || n < 0) return LORB_E_INVALID;
   lorb_ctx* ctx = M->ctx;
   LORB_HIP(ctx, hipMemcpyAsync(M->pinned, M->m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, ctx->stream));
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  const int32_t v[8] = {M->pinned[0], M->pinned[1], M->t0, M->last_n, M->pinned[3], M->pinned[4], M->pinned[5], M->m.W};
-  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  const int32_t v[9] = {M->pinned[0], M->pinned[1], M->t0, M->last_n, M->pinned[3], M->pinned[4], M->pinned[5], M->m.W,
+                        M->n_overlapped};
+  for (int i = 0; i < n && i < 9; ++i) out[i] = v[i];
   return LORB_OK;
 }
 

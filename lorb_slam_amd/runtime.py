@@ -461,7 +461,8 @@ class LocalMap:
     SURVEY §8 a17 full step).  `init`: dict(pose_init W x 6, fixed_pose F x 6, point_init, point_desc,
     obs_point, obs_kf (keyframe ids in [-F, W)), obs_uv, intr) -- synth.mapping_sequence()["init"]."""
 
-    COUNT_KEYS = ("points", "observations", "t0", "keypoints", "new_points", "new_observations", "matches", "window")
+    COUNT_KEYS = ("points", "observations", "t0", "keypoints", "new_points", "new_observations", "matches", "window",
+                  "overlapped_steps")
 
     def __init__(self, ctx, init, max_points=None, max_obs=None, max_keypoints=4096):
         self.ctx, self._keep = ctx, A.KeepAlive()
@@ -485,6 +486,11 @@ class LocalMap:
         ctx.check(lib().lorb_map_create(ctx.handle, C.byref(s), C.byref(self._p)), "lorb_map_create")
         self._keep.clear()
 
+    def set_overlap(self, enable=True):
+        """lorb_map_set_overlap: step t+1's match + append on the map's own stream under step t's
+        solve.  The keyframe arrays of step_dev must then be complete when it is called."""
+        self.ctx.check(lib().lorb_map_set_overlap(self._p, C.c_int32(1 if enable else 0)), "lorb_map_set_overlap")
+
     def step_dev(self, fp, pose, Tcw, n, d_desc, d_x, d_y, d_depth, opt=None):
         """one step on device-resident keypoints (DeviceArrays); fp: FrameParams"""
         opt = opt or A.LMOptions.default()
@@ -506,8 +512,8 @@ class LocalMap:
                 a.free()
 
     def counts(self):
-        v = (C.c_int32 * 8)()
-        self.ctx.check(lib().lorb_map_counts(self._p, v, C.c_int32(8)), "lorb_map_counts")
+        v = (C.c_int32 * 9)()
+        self.ctx.check(lib().lorb_map_counts(self._p, v, C.c_int32(9)), "lorb_map_counts")
         return dict(zip(self.COUNT_KEYS, [int(x) for x in v]))
 
     def read(self):

@@ -115,3 +115,44 @@ def test_local_mapping_capacity_error(ctx):
         lm_match(g["summary"], r["summary"])
     finally:
         M.close()
+
+
+def test_local_mapping_overlapped_chain_bit_identical(ctx):
+    """The bench's timed regime: C4 keyframes issued back to back through
+    step_dev with the overlap on (step t+1's crossCheck + append on the map's own stream under step
+    t's LM solve and write-back) and no host synchronisation in between, then the map read once.  A
+    second map runs the same keyframes serially (overlap off) and is checked against the oracle after
+    every step (run_chain).  Done when the overlapped map equals the serial one bit for bit --
+    structure, descriptors, poses, points, LM summary -- and every serial step matches the oracle
+    (structure bit-exact, poses / points within 1e-5)."""
+    n = 6
+    seq = synth.mapping_sequence(steps=n)
+    fp = A.make_frame_params(synth.frame_params())
+    # the keyframe arrays, complete in HBM before the first step (lorb_map_set_overlap's requirement)
+    dev = [(k["pose"], k["Tcw"], len(k["x"]), ctx.to_device(A.u8(k["desc"])), ctx.to_device(A.f32(k["x"])),
+            ctx.to_device(A.f32(k["y"])), ctx.to_device(A.f32(k["depth"]))) for k in seq["steps"][:n]]
+    ctx.sync()
+    Mo = LocalMap(ctx, seq["init"])
+    Ms = None
+    try:
+        Mo.set_overlap(True)
+        for pose, Tcw, nk, dd, dx, dy, dz in dev:
+            Mo.step_dev(fp, pose, Tcw, nk, dd, dx, dy, dz, OPT10)
+        go = Mo.read()
+        # every step after the first found the previous step's plan built: n - 1 ran overlapped
+        assert go["overlapped_steps"] == n - 1, go["overlapped_steps"]
+        Ms, gs = run_chain(ctx, seq, OPT10, n)
+        assert gs["overlapped_steps"] == 0
+        for k in ("t0", "points", "observations", "keypoints", "new_points", "new_observations", "matches"):
+            assert go[k] == gs[k], k
+        for k in EXACT + ("point", "pose", "fixed_pose", "match_train"):
+            assert go[k].shape == gs[k].shape and np.array_equal(go[k].view(np.uint8), gs[k].view(np.uint8)), k
+        for k, v in gs["summary"].items():
+            assert go["summary"][k] == v, (k, go["summary"][k], v)
+    finally:
+        Mo.close()
+        if Ms is not None:
+            Ms.close()
+        for d in dev:
+            for a in d[3:]:
+                a.free()

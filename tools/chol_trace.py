@@ -1,5 +1,5 @@
 """Diagnostic: per-panel event timeline of k_ba_chol_2s on the C4 window (cycles, s_memtime).
-Needs LORB_LIB_PATH=liblorb_trace.so (tools/build_variant.sh trace -DLORB_CHOL_TRACE)."""
+Needs LORB_LIB_PATH=variants/liblorb_trace.so (tools/build_variant.sh trace -DLORB_CHOL_TRACE)."""
 import sys, os, ctypes as C
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
