@@ -51,9 +51,30 @@ HBM_PEAK = 8.0e12                            # HBM3E spec (MI355X_MICROARCH)
 OPS_PER_PAIR = 16                            # 8 x v_xor_b32 + 8 x v_bcnt_u32_b32 per 256-bit pair
 # the Cholesky id covers three kernels chosen by band shape; C3/C4/C5 windows
 # (band 47, n >= 128) run the two-sided k_ba_chol_2s
-K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_2s"}
+# Point-major BA path (the default; LORB_PM=0 selects the pair-major one): timer 3 is k_ba_ls
+# (linearisation + point elimination + per-group Schur partials), timer 2 k_ba_red (the partials'
+# fixed-order sum into the band)
+PM = os.environ.get("LORB_PM", "1") != "0"
+K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_red" if PM else "k_ba_schur",
+           3: "k_ba_ls" if PM else "k_ba_lin", 4: "k_ba_chol_2s"}
 # rocprofv3 short names (tools/pmc_traffic.py) of the same kernels, for the PMC traffic lookup
-K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: "k_ba_schur", 3: "k_ba_lin", 4: "k_ba_chol_2s"}
+K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: K_NAMES[2], 3: K_NAMES[3], 4: "k_ba_chol_2s"}
+
+
+def ba_kspec(W, n_obs, n_pts, F, bw):
+    """Algorithmic bytes per launch of the BA kernels of W windows (id -> (bound, amount, unit)).
+    Point-major: k_ba_ls reads per observation its uv (16 B) and three structure indices (12 B), per
+    point X (24 B), and writes per point the point-block inverse and rhs (72 B); k_ba_red writes the
+    band once.  Pair-major: k_ba_schur reads the W / Y tiles (2 x 18 doubles per observation) once
+    and writes the band; k_ba_lin writes 34 doubles per observation and reads uv + indices + X."""
+    band = W * (6 * F) * (bw + 1) * 8.0
+    if PM:
+        return {2: ("hbm", band, "GB/s"),
+                3: ("hbm", W * (n_obs * 28.0 + n_pts * 96.0), "GB/s"),
+                4: ("fp64", W * ((6 * F) * bw * bw + 4.0 * (6 * F) * bw), "TFLOP/s")}
+    return {2: ("hbm", W * n_obs * 36 * 8.0 + band, "GB/s"),
+            3: ("hbm", W * (n_obs * (34 * 8.0 + 16 + 12) + n_pts * 24.0), "GB/s"),
+            4: ("fp64", W * ((6 * F) * bw * bw + 4.0 * (6 * F) * bw), "TFLOP/s")}
 # committed PMC summaries, newest first; each is keyed by workload (tools/pmc_traffic.py)
 TRAFFIC = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r05", "r04", "r03", "r02", "r01")]
 METRIC = "ORB matches/sec + local-BA iterations/sec (50 KF, 10k pts) at 1/2/4/8 MI355X"
@@ -232,18 +253,7 @@ def workload_c4(ctx, args, rank):
     nq = len(seqs[0]["steps"][0]["x"])
     bw = 6 * 8 - 1
     opt_obs = n_obs  # window observations; the fixed ones (~4%) are in n_obs too
-    kspec = {
-        # Schur block accumulation: compulsory bytes = the W and Y tiles (2 x 18 doubles per
-        # optimised observation) read once + the S band written once
-        2: ("hbm", W * opt_obs * 36 * 8.0 + W * (6 * F) * (bw + 1) * 8.0, "GB/s"),
-        # linearisation with the point-block prep fused in (k_ba_lin): per observation it writes the
-        # residual (2), Jp (2x3) and Jc (2x6), and the Schur inputs Jps (2x3), Q (2x3), g (2) -- 34
-        # doubles (the camera-major residual copy, 2 more, is layout, not counted) -- and reads uv
-        # (16 B) and three structure indices (12 B); per point it reads X (24 B)
-        3: ("hbm", W * (n_obs * (34 * 8.0 + 16 + 12) + n_pts * 24.0), "GB/s"),
-        # banded Cholesky + 2 triangular solves: n*bw^2 + 4*n*bw flops
-        4: ("fp64", W * ((6 * F) * bw * bw + 4.0 * (6 * F) * bw), "TFLOP/s"),
-    }
+    kspec = ba_kspec(W, opt_obs, n_pts, F, bw)
 
     def cleanup():
         for m in maps:
@@ -485,11 +495,7 @@ def workload_c3(ctx, args, rank):
 
     n_obs, n_pts, F = len(w["obs_point"]), len(w["point_init"]), 20
     bw = 6 * 8 - 1
-    kspec = {  # the C4 figures of workload_c4 for this window
-        2: ("hbm", n_obs * 36 * 8.0 + (6 * F) * (bw + 1) * 8.0, "GB/s"),
-        3: ("hbm", n_obs * (34 * 8.0 + 16 + 12) + n_pts * 24.0, "GB/s"),
-        4: ("fp64", (6 * F) * bw * bw + 4.0 * (6 * F) * bw, "TFLOP/s"),
-    }
+    kspec = ba_kspec(1, n_obs, n_pts, F, bw)  # the C4 figures of workload_c4 for this window
 
     def cpu():
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -588,13 +594,7 @@ def workload_shared(ctx, args, rank, D, comm):
     n_obs = len(win["obs_point"])
     opt_obs = int((sh["obs_frame"] >= 0).sum())
     bw = 6 * 8 - 1
-    kspec = {
-        2: ("hbm", opt_obs * 36 * 8.0 + (6 * 50) * (bw + 1) * 8.0, "GB/s"),
-        # k_ba_lin with the point-block prep fused in: the C4 figure of workload_c4 (34 doubles
-        # written per observation, uv + three structure indices read; X read per point)
-        3: ("hbm", len(sh["obs_point"]) * (34 * 8.0 + 16 + 12) + len(sh["point_init"]) * 24.0, "GB/s"),
-        4: ("fp64", (6 * 50) * bw * bw + 4.0 * (6 * 50) * bw, "TFLOP/s"),
-    }
+    kspec = ba_kspec(1, len(sh["obs_point"]), len(sh["point_init"]), 50, bw)  # this rank's shard
     # whole-job units: the shared window's iterations / matches are counted once (rank 0 only)
     return dict(step=step, check=check, ba_iters=10.0 if rank == 0 else 0.0, matches=float(nq) if rank == 0 else 0.0,
                 pairs=float(b - a) * nt, plan_ms=plan_ms, cleanup=cleanup, kspec=kspec,

@@ -47,6 +47,10 @@ struct BaWin {
   int env_base, env_size, n, row_base, bw;  // S band: row i holds cols [i-bw, i]
   int obs_base, n_obs;
   int n_obs_all;  // observations of the window over all ranks (== n_obs unless sharded)
+  // point-major path: the window's group partials start at part_base, part_stride doubles per group
+  // (camera terms at part_cam within it); bwc = the camera-level half band
+  int part_stride, part_cam, bwc, pad_;
+  long long part_base;
   double fx, fy, cx, cy;
 };
 struct PBlk { int win, p0, cnt, o0, no; };  // point group: points [p0, p0+cnt), obs [o0, o0+no)
@@ -284,6 +288,10 @@ struct BaDev {
                              // ((row_base >> 4) + w) * 1024 doubles, top side's blocks then the
                              // bottom side's, [block][16][64] (BandSide::bsk_block)
   WinState* st;
+  // point-major path (PM): group partials, per group (first camera - pose_base, span); pm: plan uses it
+  double* gpart;
+  int2* gspan;
+  int pm;
   // [0] point groups, [1] block pairs in use.  Launch grids may be larger (device-built plans
   // launch at capacity so that the captured LM graph survives a rebuild); the extra workgroups exit.
   const int* live;
@@ -2137,11 +2145,12 @@ __device__ __forceinline__ void stage_fix(const BaDev& d, const LMOpt& o, double
   const int B1 = W.bw + 1;
   for (int q = tid; q < (r1 - r0) * 6; q += nthr) {
     const int i = r0 + q / 6, i6 = i % 6, j6 = q % 6;
-    if (j6 > i6) continue;
+    if (j6 > i6 || (d.pm && j6 != i6)) continue;
     const int c = W.pose_base + i / 6;
     const double* sc = d.scale_pose + 6 * c;
     double v = d.U[21 * c + u21(i6, j6)] * sc[i6] * sc[j6];
-    if (i6 == j6) v += fmin(fmax(v, o.min_diag), o.max_diag) / radius;
+    // point-major path: the staged diagonal blocks hold sc (U - A) sc^T already, only D^2 is added
+    if (i6 == j6) v = (d.pm ? 0.0 : v) + fmin(fmax(v, o.min_diag), o.max_diag) / radius;
     double& e = Ab[i * B1 + (j6 - i6 + W.bw)];
     e = e + v;
   }
@@ -2156,11 +2165,11 @@ __device__ __forceinline__ double stage_fix_val(const BaDev& d, const LMOpt& o, 
   at = -1;
   if (q >= (r1 - r0) * 6) return 0.0;
   const int i = r0 + q / 6, i6 = i % 6, j6 = q % 6;
-  if (j6 > i6) return 0.0;
+  if (j6 > i6 || (d.pm && j6 != i6)) return 0.0;
   const int c = W.pose_base + i / 6;
   const double* sc = d.scale_pose + 6 * c;
   double v = d.U[21 * c + u21(i6, j6)] * sc[i6] * sc[j6];
-  if (i6 == j6) v += fmin(fmax(v, o.min_diag), o.max_diag) / radius;
+  if (i6 == j6) v = (d.pm ? 0.0 : v) + fmin(fmax(v, o.min_diag), o.max_diag) / radius;
   at = i * (W.bw + 1) + (j6 - i6 + W.bw);
   return v;
 }
@@ -2290,8 +2299,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   {
     const int row = t < rt ? t : n16 - 1 - (t - rt);
     rz = (t < rt + rb && row < n) ? d.rhs[W.row_base + row] : 0.0;
-    // fused: the rhs holds -r; + V sc (k_ba_schur<false>'s vs - r, same bits)
-    if (HEAD && t < rt + rb && row < n) rz = rz + d.V[6 * W.pose_base + row] * d.scale_pose[6 * W.pose_base + row];
+    // fused: the rhs holds -r; + V sc (k_ba_schur<false>'s vs - r, same bits).  Point-major: the
+    // rhs is complete
+    if (HEAD && !d.pm && t < rt + rb && row < n)
+      rz = rz + d.V[6 * W.pose_base + row] * d.scale_pose[6 * W.pose_base + row];
   }
   if (prog && HEAD && LORB_CHOL_FFIX) {  // ... with the camera-block terms added as they are staged
     const StageFix fx{d.U, d.scale_pose, W.pose_base, o.min_diag, o.max_diag, S0.radius};
@@ -2306,7 +2317,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   for (int k = t + NT; k < rt + rb; k += NT) {  // (n16 > 464 only)
     const int row = k < rt ? k : n16 - 1 - (k - rt);
     double v = row < n ? d.rhs[W.row_base + row] : 0.0;
-    if (HEAD && row < n) v = v + d.V[6 * W.pose_base + row] * d.scale_pose[6 * W.pose_base + row];
+    if (HEAD && !d.pm && row < n) v = v + d.V[6 * W.pose_base + row] * d.scale_pose[6 * W.pose_base + row];
     if (k < rt) zt[k] = v; else zb[k - rt] = v;
   }
   if (t == 0) {
@@ -2954,43 +2965,638 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
   lm_end_run<SH>(d, o, blockIdx.x, threadIdx.x);
 }
 
+// ==========================================================================================
+// Point-major path ("PM").  The pair-major path above materialises 34 doubles
+// per observation (k_ba_lin) and re-reads them once per camera block pair a point takes part in
+// (k_ba_schur: k (k + 1) / 2 pairs for a point seen k times).  Here one kernel per point group
+// linearises its observations, eliminates its points and forms the group's contributions to the
+// reduced camera system on chip, and writes ONE partial per (group, camera block) of its camera
+// window; a second kernel sums the partials of each block in a fixed group order (deterministic, no
+// FP64 atomics).  Nothing is stored per observation: the back-substitution re-evaluates the
+// linearisation (the same expression on the same inputs: the same bits).
+//
+// Group window: the group's optimised observations see cameras [cmin, cmin + span) (plan order);
+// its blocks (a, b) (a >= b, local to cmin) lie in the band a - b <= bwc (the window's camera-level
+// half band), stored row by row: slot(a, dd = a - b).  Per local camera a the partial also holds
+// the camera terms diag(Jc^T Jc) (6), Jc^T r (6) and Jc^T g (6).  The diagonal blocks carry
+// Jc^T (I - Q Jps^T) Jc = U - A, the off-diagonal ones -A: band = sc (sum) sc^T, plus D^2 on the
+// diagonal; rhs = (Jc^T r - Jc^T g) sc.
+// ==========================================================================================
+
+__host__ __device__ __forceinline__ int pm_slot(int a, int dd, int bwc) {
+  return a <= bwc ? a * (a + 1) / 2 + dd : (bwc + 1) * (bwc + 2) / 2 + (a - bwc - 1) * (bwc + 1) + dd;
+}
+// slots of a window of `span` cameras
+__host__ __device__ __forceinline__ int pm_nslots(int span, int bwc) {
+  return span <= 0 ? 0 : pm_slot(span - 1, span - 1 < bwc ? span - 1 : bwc, bwc) + 1;
+}
+__device__ __forceinline__ void pm_slot_inv(int q, int bwc, int& a, int& dd) {
+  const int T = (bwc + 1) * (bwc + 2) / 2;
+  if (q < T) {
+    a = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+    while ((a + 1) * (a + 2) / 2 <= q) ++a;
+    while (a * (a + 1) / 2 > q) --a;
+    dd = q - a * (a + 1) / 2;
+  } else {
+    const int r = q - T;
+    a = bwc + 1 + r / (bwc + 1);
+    dd = r - (r / (bwc + 1)) * (bwc + 1);
+  }
+}
+
+// LORB_LS_SKIPD 1: phase D's point loop skipped (timing diagnostics only: wrong results)
+#ifndef LORB_LS_SKIPD
+#define LORB_LS_SKIPD 0
+#endif
+constexpr int kLsThreads = kGB;
+constexpr int kLsWaves = kLsThreads / 64;
+
+// three sums (M1: the second a max) over an NW-wave workgroup: per-wave butterfly, then the waves'
+// values in wave order (every thread must call it)
+template <int NW, bool M1>
+__device__ __forceinline__ void block_red3w(double& a, double& b, double& c, double (*red)[NW]) {
+  a = wave_sum(a); b = M1 ? wave_max(b) : wave_sum(b); c = wave_sum(c);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    red[0][w] = a; red[1][w] = b; red[2][w] = c;
+  }
+  __syncthreads();
+  a = red[0][0]; b = red[1][0]; c = red[2][0];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) { a += red[0][k]; b = M1 ? fmax(b, red[1][k]) : b + red[1][k]; c += red[2][k]; }
+}
+
+// The linearisation of one observation at the current linearisation point (k_ba_ls and k_ba_bs2
+// evaluate the same expression on the same inputs, so both see the same bits).
+__device__ __forceinline__ void pm_lin(const BaDev& d, const BaWin& W, int cur, int p, int c, int fx, double2 uv,
+                                       double (&r)[2], double (&Jp)[6], double (&Jc)[12]) {
+  double X[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) X[k] = d.x_pt[cur][3 * p + k];
+  if (c >= 0) {
+    double tr[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tr[k] = d.x_pose[cur][6 * c + 3 + k];
+    residual_jac_s(d.rot_lin[c], tr, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
+  } else {
+    double pose[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * fx + k];
+    residual_jac(pose, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
+  }
+}
+
+// PM-K1: one point group per workgroup (observation threads t < kGB; kLsThreads threads for the
+// block phase).  Phases:
+//   A (observation)  residual + Jacobians in registers, Jp^T Jp / Jp^T r terms to LDS;
+//   B (point)        E^T E, E^T r in observation order, Jacobi scale (iteration 0), the point-block
+//                    prep (prep_point); the group's camera window (min / max camera);
+//   C (observation)  Jps, Q = Jps E^-1, g = Q b; every optimised observation moves to its point's
+//                    camera-ordered slot (rank among the point's cameras: no table);
+//   D (block row)    thread = (slot, row i): sum over the group's points in point order of row i of
+//                    Jc_h^T K Jc_l (K = I - Q_h Jps_l^T on the diagonal, -Q_h Jps_l^T off it), plus
+//                    the camera terms on the diagonal; written to the group's partial.
+// Cost, point gradient max and |x|^2 partials as k_ba_lin (the head reads them when relinearising).
+__global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
+  __shared__ double s_jc[kGB][12];   // B / C: per point Ei (0..5), bs (6..8), sp (9..11); D: Jc per slot
+  __shared__ double s_qj[kGB][12];   // A / B: Jp^T Jp (6) | Jp^T r (3) per observation; D: Q | Jps per slot
+  __shared__ double s_rg[kGB][4];    // D: r | g per slot
+  __shared__ unsigned long long s_mask[kGB];
+  __shared__ int s_po[kGB];
+  __shared__ unsigned long long s_pts[64][kGB / 64];  // per local camera: the points that see it
+  __shared__ int s_mm[2][kLsWaves];
+  __shared__ double red3[3][kLsWaves];
+  if ((int)blockIdx.x >= d.live[0]) return;
+#ifdef LORB_LS_STAMPS
+  // dbg[8 g + k]: s_memtime at the kernel's entry (k 0) and after phase A (1), B (2), C (3), D (4),
+  // the partial sums (5) of group g (thread 0)
+#define LS_STAMP(k) do { if (threadIdx.x == 0) d.dbg[8 * blockIdx.x + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define LS_STAMP(k) do {} while (0)
+#endif
+  LS_STAMP(0);
+  const PBlk g = d.pblk[blockIdx.x];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const bool has = t < g.no;
+  const int of = g.o0 + min(t, max(g.no - 1, 0));
+  const int p_ = has ? d.obs_pt[of] : 0, c_ = has ? d.obs_cam[of] : -1;
+  const int fx_ = has ? d.obs_fix[of] : 0;
+  const double2 uv = has ? d.obs_uv[of] : make_double2(0.0, 0.0);
+  int po0 = 0, po1 = 0;
+  // the point phase's global inputs (both iterates: cur is not known yet) go out with the group's
+  double Xp[2][3] = {{0, 0, 0}, {0, 0, 0}}, spp[3] = {0, 0, 0};
+  if (t < g.cnt) {
+    const int p = g.p0 + t;
+    po0 = d.pt_obs_off[p]; po1 = d.pt_obs_off[p + 1];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { Xp[0][k] = d.x_pt[0][3 * p + k]; Xp[1][k] = d.x_pt[1][3 * p + k]; spp[k] = d.scale_pt[3 * p + k]; }
+  }
+  const WinState& S = d.st[g.win];
+  if (S.done) return;
+  const BaWin& W = d.win[g.win];
+  const int cur = S.cur;
+  const double rad = S.radius;
+  if (t < kGB) s_mask[t] = 0ull;
+  if (t < 64 * (kGB / 64)) s_pts[t / (kGB / 64)][t % (kGB / 64)] = 0ull;
+  // A
+  double r[2] = {0, 0}, Jp[6] = {0, 0, 0, 0, 0, 0}, Jc[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) Jc[k] = 0.0;
+  double cost = 0.0;
+  if (has) {
+    pm_lin(d, W, cur, p_, c_, fx_, uv, r, Jp, Jc);
+    cost = 0.5 * (r[0] * r[0] + r[1] * r[1]);
+    double* v = s_qj[t];
+    v[0] = Jp[0] * Jp[0] + Jp[3] * Jp[3]; v[1] = Jp[0] * Jp[1] + Jp[3] * Jp[4];
+    v[2] = Jp[0] * Jp[2] + Jp[3] * Jp[5]; v[3] = Jp[1] * Jp[1] + Jp[4] * Jp[4];
+    v[4] = Jp[1] * Jp[2] + Jp[4] * Jp[5]; v[5] = Jp[2] * Jp[2] + Jp[5] * Jp[5];
+    v[6] = Jp[0] * r[0] + Jp[3] * r[1]; v[7] = Jp[1] * r[0] + Jp[4] * r[1];
+    v[8] = Jp[2] * r[0] + Jp[5] * r[1];
+  }
+  {
+    int mn = has && c_ >= 0 ? c_ : 0x7fffffff, mx = has && c_ >= 0 ? c_ : -1;
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) { mn = min(mn, __shfl_xor(mn, s, 64)); mx = max(mx, __shfl_xor(mx, s, 64)); }
+    if (lane == 0) { s_mm[0][wv] = mn; s_mm[1][wv] = mx; }
+  }
+  __syncthreads();
+  LS_STAMP(1);
+  int cmin = s_mm[0][0], cmax = s_mm[1][0];
+#pragma unroll
+  for (int k = 1; k < kLsWaves; ++k) { cmin = min(cmin, s_mm[0][k]); cmax = max(cmax, s_mm[1][k]); }
+  const int span = cmax >= 0 ? cmax - cmin + 1 : 0;
+  // B (point t) -- and the observations' camera bits
+  double gm = 0.0, xn2 = 0.0;
+  if (t < g.cnt) {
+    const int p = g.p0 + t;
+    double E[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
+    for (int e = po0 - g.o0; e < po1 - g.o0; ++e) {
+      const double* v = s_qj[e];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) E[k] += v[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) b[k] += v[6 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d.etb[3 * p + k] = b[k];
+    double sp[3];
+    if (S.iter == 0) {
+      sp[0] = 1.0 / (1.0 + sqrt(E[0]));
+      sp[1] = 1.0 / (1.0 + sqrt(E[3]));
+      sp[2] = 1.0 / (1.0 + sqrt(E[5]));
+#pragma unroll
+      for (int k = 0; k < 3; ++k) d.scale_pt[3 * p + k] = sp[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) sp[k] = spp[k];
+    }
+    if (po1 > po0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double X = cur ? Xp[1][k] : Xp[0][k];
+        gm = fmax(gm, fabs(X - (X + -b[k])));
+        xn2 += X * X;
+      }
+    }
+    double Ei[6], bs[3];
+    if (!prep_point(E, b, sp, rad, o, Ei, bs)) prep_fail(d, g.win);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { d.pinv[6 * p + k] = Ei[k]; s_jc[t][k] = Ei[k]; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { s_jc[t][6 + k] = bs[k]; s_jc[t][9 + k] = sp[k]; }
+    s_po[t] = po0 - g.o0;
+  }
+  const int lp = p_ - g.p0;
+  const int a_ = c_ - cmin;
+  if (has && c_ >= 0) {
+    atomicOr(&s_mask[lp], 1ull << a_);
+    atomicOr(&s_pts[a_][lp >> 6], 1ull << (lp & 63));
+  }
+  __syncthreads();
+  LS_STAMP(2);
+  // C: Jps, Q, g (reads the point data), then the camera-ordered slot
+  double Q[6], Js[6], g0 = 0.0, g1 = 0.0;
+  int slot = -1;
+  if (has && c_ >= 0) {
+    const double* pt = s_jc[lp];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Js[k] = Jp[k] * pt[9 + k % 3];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        Q[3 * rr + j] = Js[3 * rr] * s3(pt, 0, j) + Js[3 * rr + 1] * s3(pt, 1, j) + Js[3 * rr + 2] * s3(pt, 2, j);
+    g0 = Q[0] * pt[6] + Q[1] * pt[7] + Q[2] * pt[8];
+    g1 = Q[3] * pt[6] + Q[4] * pt[7] + Q[5] * pt[8];
+    slot = s_po[lp] + __popcll(s_mask[lp] & ((1ull << a_) - 1ull));
+  }
+  __syncthreads();
+  if (slot >= 0) {
+#pragma unroll
+    for (int k = 0; k < 12; ++k) s_jc[slot][k] = Jc[k];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) { s_qj[slot][k] = Q[k]; s_qj[slot][6 + k] = Js[k]; }
+    s_rg[slot][0] = r[0]; s_rg[slot][1] = r[1]; s_rg[slot][2] = g0; s_rg[slot][3] = g1;
+  }
+  __syncthreads();
+  LS_STAMP(3);
+  // D
+  const int bwc = W.bwc, nsl = pm_nslots(span, bwc);
+  double* gp = d.gpart + W.part_base + (size_t)(blockIdx.x - W.pblk_base) * W.part_stride;
+  if (t == 0) d.gspan[blockIdx.x] = make_int2(span > 0 ? cmin - W.pose_base : 0, span);
+  // Lane = slot (its whole 6 x 6 block: the point's loads serve 36 outputs), wave = point subset:
+  // every lane of a wave walks the same points (k = wave, wave + 4, ...: a uniform loop, so the next
+  // point's mask / offset are requested before this point's FMAs), a lane whose two cameras the
+  // point does not share sits the point out.  The four waves' blocks are then summed in wave order
+  // through LDS (the observation data is dead by then).  More than 64 slots: waves take 64-slot
+  // chunks over all points instead (no point split, no cross-wave sum).
+  const bool split = nsl <= 64;
+  const int nrounds = split ? 1 : (nsl + 64 * kLsWaves - 1) / (64 * kLsWaves);
+  for (int rd = 0; rd < nrounds; ++rd) {
+    const int q = split ? lane : 64 * (kLsWaves * rd + wv) + lane;
+    const bool act = q < nsl;
+    int a = 0, dd = 0;
+    if (act) pm_slot_inv(q, bwc, a, dd);
+    const int b = a - dd;
+    const unsigned long long ba = act ? 1ull << a : 0ull, bb = 1ull << b;
+    const bool dg = dd == 0;
+    double acc[36], ex[18];
+#pragma unroll
+    for (int k = 0; k < 36; ++k) acc[k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 18; ++k) ex[k] = 0.0;
+    const int k0 = split ? wv : 0, kst = split ? kLsWaves : 1;
+    if (!LORB_LS_SKIPD && k0 < g.cnt) {
+      unsigned long long m = s_mask[k0];
+      int po = s_po[k0];
+      for (int k = k0; k < g.cnt; k += kst) {
+        const unsigned long long mc = m;
+        const int pc = po;
+        if (k + kst < g.cnt) { m = s_mask[k + kst]; po = s_po[k + kst]; }  // the next point's
+        if ((mc & ba) && (mc & bb)) {
+          const int eh = pc + __popcll(mc & (ba - 1ull)), el = pc + __popcll(mc & (bb - 1ull));
+          const double* Qh = s_qj[eh];
+          const double* Jl = s_qj[el] + 6;
+          const double* Ch = s_jc[eh];
+          const double* Cl = s_jc[el];
+          double k00 = -(Qh[0] * Jl[0] + Qh[1] * Jl[1] + Qh[2] * Jl[2]);
+          double k01 = -(Qh[0] * Jl[3] + Qh[1] * Jl[4] + Qh[2] * Jl[5]);
+          double k10 = -(Qh[3] * Jl[0] + Qh[4] * Jl[1] + Qh[5] * Jl[2]);
+          double k11 = -(Qh[3] * Jl[3] + Qh[4] * Jl[4] + Qh[5] * Jl[5]);
+          if (dg) { k00 += 1.0; k11 += 1.0; }
+          double cl[12], ch[12];
+#pragma unroll
+          for (int j = 0; j < 12; ++j) { cl[j] = Cl[j]; ch[j] = Ch[j]; }
+#pragma unroll
+          for (int i = 0; i < 6; ++i) {
+            const double z0 = ch[i] * k00 + ch[6 + i] * k10, z1 = ch[i] * k01 + ch[6 + i] * k11;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) acc[6 * i + j] = fma(z0, cl[j], fma(z1, cl[6 + j], acc[6 * i + j]));
+          }
+          if (dg) {
+            const double* rg = s_rg[eh];
+            const double g0r = rg[0], g1r = rg[1], g2r = rg[2], g3r = rg[3];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+              ex[i] = fma(ch[i], ch[i], fma(ch[6 + i], ch[6 + i], ex[i]));
+              ex[6 + i] = fma(ch[i], g0r, fma(ch[6 + i], g1r, ex[6 + i]));
+              ex[12 + i] = fma(ch[i], g2r, fma(ch[6 + i], g3r, ex[12 + i]));
+            }
+          }
+        }
+      }
+    }
+    if (split) {
+      // ((w0 + w1) + w2) + w3 through 64 x 36 + 64 x 18 buffers over the dead observation data
+      static_assert(64 * 36 <= kGB * 12 && 64 * 18 <= kGB * 12, "reduction buffers");
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < kLsWaves; ++w) {
+        if (wv == w && act) {
+          double* bl = &s_jc[0][0] + 36 * lane;
+          double* bx = &s_qj[0][0] + 18 * lane;
+#pragma unroll
+          for (int k = 0; k < 36; ++k) { if (w > 0) acc[k] += bl[k]; if (w + 1 < kLsWaves) bl[k] = acc[k]; }
+          if (dg) {
+#pragma unroll
+            for (int k = 0; k < 18; ++k) { if (w > 0) ex[k] += bx[k]; if (w + 1 < kLsWaves) bx[k] = ex[k]; }
+          }
+        }
+        if (w + 1 < kLsWaves) __syncthreads();
+      }
+    }
+    if (act && (!split || wv == kLsWaves - 1)) {
+      double* out = gp + 36 * q;
+#pragma unroll
+      for (int k = 0; k < 36; ++k) out[k] = acc[k];
+      if (dg) {
+        double* gc = gp + W.part_cam + 18 * a;
+#pragma unroll
+        for (int k = 0; k < 18; ++k) gc[k] = ex[k];
+      }
+    }
+  }
+  LS_STAMP(4);
+  block_red3w<kLsWaves, true>(cost, gm, xn2, red3);
+  if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[0] = cost; P[1] = gm; P[2] = xn2; }
+  LS_STAMP(5);
+#undef LS_STAMP
+}
+
+// PM-K2: one workgroup per camera block (h, l) of a window: the partials of the window's groups
+// whose camera window holds the block, summed in group order.  Thread = (entry e, subset s); the
+// candidate groups of each 256-group chunk are compacted in order, subset s takes every nsub-th.
+// MODE 0: the camera terms of the diagonal blocks only (U diag, V: the iteration head's inputs,
+//         before k_ba_lm_begin fixes the iteration-0 Jacobi scale);
+// MODE 1: the band with D^2 on the diagonal (rank 0) and the rhs (V - R) sc (k_ba_schur<false>'s
+//         result, for the Cholesky without a head);
+// MODE 2: the fused iteration: band without D^2 (k_ba_chol_2s<true> adds it), rhs, U diag and V.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_ba_red(BaDev d, LMOpt o) {
+  constexpr int kRc = 4;  // groups per thread per chunk: 1024 groups' windows requested at once
+  __shared__ int s_cand[256 * kRc];
+  __shared__ int s_a[256 * kRc];
+  __shared__ int s_wc[kRc][4];
+  __shared__ double s_acc[256];
+  __shared__ double s_tot[54];
+  if ((int)blockIdx.x >= d.live[1]) return;
+  const BlockPair bp = d.bp[blockIdx.x];
+  const bool diag = bp.ch == bp.cl;
+  if (MODE == 0 && !diag) return;
+  const WinState& S = d.st[bp.win];
+  const BaWin& W = d.win[bp.win];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // the finalisation's scales (and MODE 1's camera diagonal) go out with the state
+  const int fi = t < 36 ? t / 6 : (t < 42 ? t - 36 : 0), fj = t < 36 ? t % 6 : 0;
+  double sci = 1.0, scj = 1.0, udg = 0.0;
+  if (MODE != 0) {
+    sci = d.scale_pose[6 * bp.ch + fi];
+    scj = d.scale_pose[6 * bp.cl + fj];
+    if (MODE == 1 && diag) udg = d.U[21 * bp.ch + u21(fi, fi)];
+  }
+  if (S.done) return;
+  const int h = bp.ch - W.pose_base, l = bp.cl - W.pose_base, dd = h - l;
+  // entries: [0, 36) the block, [36, 54) the camera terms (U diag, V, R); MODE 0: U diag, V only
+  const int e0 = MODE == 0 ? 36 : 0, ne = MODE == 0 ? 12 : (diag ? 54 : 36);
+  const int nsub = 256 / ne, e = t % ne, sub = t / ne;
+  double acc = 0.0;
+  const int g0 = W.pblk_base, ng = W.n_pblk;
+  for (int c0 = 0; c0 < ng; c0 += 256 * kRc) {
+    int2 gs[kRc];
+#pragma unroll
+    for (int u = 0; u < kRc; ++u) {
+      const int gi = c0 + 256 * u + t;
+      gs[u] = gi < ng ? d.gspan[g0 + gi] : make_int2(0, 0);
+    }
+    unsigned long long bal[kRc];
+#pragma unroll
+    for (int u = 0; u < kRc; ++u) {
+      const bool cand = gs[u].y > 0 && gs[u].x <= l && h < gs[u].x + gs[u].y;
+      bal[u] = __ballot(cand);
+      if (lane == 0) s_wc[u][wv] = __popcll(bal[u]);
+    }
+    __syncthreads();
+    // candidates in group order: sub-chunk u, then wave, then lane
+    int pre = 0, nc = 0;
+#pragma unroll
+    for (int u = 0; u < kRc; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) nc += s_wc[u][k];
+#pragma unroll
+    for (int u = 0; u < kRc; ++u) {
+      int pu = pre;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pu += k < wv ? s_wc[u][k] : 0;
+      if ((bal[u] >> lane) & 1ull) {
+        const int j = pu + __popcll(bal[u] & ((1ull << lane) - 1ull));
+        s_cand[j] = c0 + 256 * u + t;
+        s_a[j] = h - gs[u].x;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pre += s_wc[u][k];
+    }
+    __syncthreads();
+    if (sub < nsub) {
+      const int ee = e0 + e;
+      auto at = [&](int j) -> const double* {
+        const double* gp = d.gpart + W.part_base + (size_t)s_cand[j] * W.part_stride;
+        const int a = s_a[j];
+        return ee < 36 ? gp + 36 * pm_slot(a, dd, W.bwc) + ee : gp + W.part_cam + 18 * a + (ee - 36);
+      };
+      // kRu candidates' loads in flight before they are added (in candidate order: the same sum)
+      constexpr int kRu = 8;
+      int j = sub;
+      for (; j + (kRu - 1) * nsub < nc; j += kRu * nsub) {
+        double v[kRu];
+#pragma unroll
+        for (int u = 0; u < kRu; ++u) v[u] = *at(j + u * nsub);
+#pragma unroll
+        for (int u = 0; u < kRu; ++u) acc += v[u];
+      }
+      for (; j < nc; j += nsub) acc += *at(j);
+    }
+    __syncthreads();
+  }
+  if (sub < nsub) s_acc[t] = acc;
+  __syncthreads();
+  if (t < ne) {
+    double v = s_acc[t];
+    for (int s = 1; s < nsub; ++s) v += s_acc[t + s * ne];
+    s_tot[t] = v;
+  }
+  __syncthreads();
+  const int c = bp.ch;
+  if (MODE == 0) {
+    if (t < 6) d.U_part[21 * c + u21(t, t)] = s_tot[t];
+    else if (t < 12) d.V_part[6 * c + t - 6] = s_tot[t];
+    return;
+  }
+  double* A = d.env_part + W.env_base;
+  if (t < 36) {
+    const int i = fi, j = fj;
+    if (!diag || j <= i) {
+      double v = s_tot[t] * sci * scj;
+      if (MODE == 1 && diag && i == j && d.rank0) {
+        const double u = udg * sci * sci;
+        v += fmin(fmax(u, o.min_diag), o.max_diag) / S.radius;
+      }
+      band(A, W.bw, 6 * h + i, 6 * l + j) = v;
+    }
+  } else if (diag && t < 42) {
+    const int i = fi;
+    d.rhs_part[W.row_base + 6 * h + i] = (s_tot[42 + i] - s_tot[48 + i]) * sci;
+    if (MODE == 2) { d.U_part[21 * c + u21(i, i)] = s_tot[36 + i]; d.V_part[6 * c + i] = s_tot[42 + i]; }
+  }
+}
+
+// PM-K3: point-group back-substitution (k_ba_backsub's phases) with the linearisation re-evaluated
+// in registers instead of read back: b_p -= sum_e Jps_e^T (Jc_e y_c(e)), the point step and
+// candidate, then the model cost change and the candidate cost per observation.
+__global__ __launch_bounds__(kGB) void k_ba_bs2(BaDev d) {
+  __shared__ double sh[kGB][3], sst[kGB][3], sxn[kGB][3], ssp[kGB][3];
+  __shared__ double red3[3][4];
+  if ((int)blockIdx.x >= d.live[0]) return;
+  const PBlk g = d.pblk[blockIdx.x];
+  const int t = threadIdx.x;
+  const bool has = t < g.no;
+  const int of = g.o0 + min(t, max(g.no - 1, 0));
+  const int p_ = has ? d.obs_pt[of] : 0, c_ = has ? d.obs_cam[of] : -1;
+  const int fx_ = has ? d.obs_fix[of] : 0;
+  const double2 uv = has ? d.obs_uv[of] : make_double2(0.0, 0.0);
+  double b[3] = {0, 0, 0}, sp[3] = {0, 0, 0}, Xa[3] = {0, 0, 0}, Xb[3] = {0, 0, 0};
+  double Ei[6] = {0, 0, 0, 0, 0, 0};
+  int po0 = 0, po1 = 0;
+  if (t < g.cnt) {
+    const int p = g.p0 + t;
+    po0 = d.pt_obs_off[p]; po1 = d.pt_obs_off[p + 1];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      sp[k] = d.scale_pt[3 * p + k];
+      b[k] = d.etb[3 * p + k] * sp[k];
+      Xa[k] = d.x_pt[0][3 * p + k];
+      Xb[k] = d.x_pt[1][3 * p + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Ei[k] = d.pinv[6 * p + k];
+  }
+  const WinState& S = d.st[g.win];
+  if (S.done || S.chol_fail) return;
+  const BaWin& W = d.win[g.win];
+  const int cur = S.cur;
+  if (t < g.cnt) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ssp[t][k] = sp[k];
+  }
+  // every camera-indexed input (the step y, the Jacobi scale, the candidate pose) goes out with the
+  // linearisation's: one dependent round trip after the observation's indices
+  double ys[6] = {0, 0, 0, 0, 0, 0}, tc[3] = {0, 0, 0};
+  lorb::RotVal Rc{};
+  if (has && c_ >= 0) {
+    const double* y = d.ycam + W.row_base + 6 * (c_ - W.pose_base);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) ys[i] = y[i] * d.scale_pose[6 * c_ + i];
+    Rc = d.rot_cand[c_];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) tc[k] = d.x_pose[cur ^ 1][6 * c_ + 3 + k];
+  }
+  double r[2] = {0, 0}, Jp[6] = {0, 0, 0, 0, 0, 0}, Jc[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) Jc[k] = 0.0;
+  if (has) pm_lin(d, W, cur, p_, c_, fx_, uv, r, Jp, Jc);
+  const int lp = p_ - g.p0;
+  __syncthreads();
+  // W^T y = Jps^T (Jcs y): this observation's push into its point's rhs
+  double ya0 = 0.0, ya1 = 0.0;
+  if (has) {
+    if (c_ >= 0) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        ya0 += Jc[i] * ys[i];
+        ya1 += Jc[6 + i] * ys[i];
+      }
+#pragma unroll
+      for (int j = 0; j < 3; ++j) sh[t][j] = (Jp[j] * ssp[lp][j]) * ya0 + (Jp[3 + j] * ssp[lp][j]) * ya1;
+    } else {
+      sh[t][0] = sh[t][1] = sh[t][2] = 0.0;
+    }
+  }
+  __syncthreads();
+  double sn2 = 0.0;
+  if (t < g.cnt) {
+    const int p = g.p0 + t;
+    for (int e = po0 - g.o0; e < po1 - g.o0; ++e) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) b[j] -= sh[e][j];
+    }
+    double X[3], step[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) X[k] = cur ? Xb[k] : Xa[k];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      step[j] = -(s3(Ei, j, 0) * b[0] + s3(Ei, j, 1) * b[1] + s3(Ei, j, 2) * b[2]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const double xn = X[j] + step[j] * sp[j];
+      d.x_pt[cur ^ 1][3 * p + j] = xn;
+      sxn[t][j] = xn;
+      sst[t][j] = step[j] * sp[j];
+      if (po1 > po0) sn2 += (X[j] - xn) * (X[j] - xn);
+    }
+  }
+  __syncthreads();
+  double mcc = 0.0, ncost = 0.0;
+  if (has) {
+    const double Xn[3] = {sxn[lp][0], sxn[lp][1], sxn[lp][2]};
+    double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      m0 += Jp[j] * sst[lp][j];
+      m1 += Jp[3 + j] * sst[lp][j];
+    }
+    double rn[2];
+    if (c_ >= 0) {
+      m0 -= ya0;
+      m1 -= ya1;
+      residual_s(Rc, tc, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
+    } else {
+      double pose[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * fx_ + k];
+      residual(pose, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
+    }
+    mcc = m0 * (r[0] + m0 / 2.0) + m1 * (r[1] + m1 / 2.0);
+    ncost = 0.5 * (rn[0] * rn[0] + rn[1] * rn[1]);
+  }
+  block_red3<false>(mcc, ncost, sn2, red3);
+  if (t == 0) {
+    double* P = d.part + 8 * blockIdx.x;
+    P[3] = mcc; P[4] = ncost; P[5] = sn2;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
-// pose-only LM (BA::ProjectPoseOptimization), one workgroup per frame, whole solve in-kernel
-// One WAVEFRONT per frame (a12 is the per-frame tracking call: a few hundred residuals): lanes stride
-// the frame's residuals (the first 256 held in registers for the whole solve), the 28 normal-equation
-// sums are one wave reduce-scatter (wave_sum_all), the candidate cost a butterfly (every lane ends
-// with the same bits), and every lane carries the frame's LM state and solves the 6 x 6 system
-// redundantly, so an iteration has no LDS traffic and no barrier.
-__global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__ res_off,
-                                                     const float* __restrict__ intr,
-                                                     const float* __restrict__ pose_init,
-                                                     const float* __restrict__ pts3d,
-                                                     const float* __restrict__ obs2d, LMOpt o,
-                                                     double* __restrict__ pose_out,
-                                                     lorb_ba_summary* __restrict__ sums) {
+// pose-only LM (BA::ProjectPoseOptimization), one workgroup per frame, whole solve in-kernel.
+// kPoW wavefronts per frame (a12 is the per-frame tracking call: a few hundred residuals): threads
+// stride the frame's residuals (the first kPoC per thread held in registers for the whole solve);
+// the 28 normal-equation sums are one reduce-scatter per wave (wave_sum_all) plus the waves' sums in
+// wave order through LDS, the candidate cost a butterfly plus the same; every thread then carries
+// the frame's LM state and solves the 6 x 6 system redundantly (identical bits everywhere, so the
+// control flow is uniform).  Two barriers per iteration; the LDS exchange is double-buffered.
+constexpr int kPoW = 4, kPoThreads = 64 * kPoW;
+__global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __restrict__ res_off,
+                                                             const float* __restrict__ intr,
+                                                             const float* __restrict__ pose_init,
+                                                             const float* __restrict__ pts3d,
+                                                             const float* __restrict__ obs2d, LMOpt o,
+                                                             double* __restrict__ pose_out,
+                                                             lorb_ba_summary* __restrict__ sums) {
+  __shared__ double s_nv[2][kPoW][28];
+  __shared__ double s_cv[2][kPoW];
   const int f = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int r0 = res_off[f], r1 = res_off[f + 1];
   const double fx = intr[4 * f], fyv = intr[4 * f + 1], cx = intr[4 * f + 2], cy = intr[4 * f + 3];
   double xs[6], xn[6], sc[6], JtJ[21], Jtr[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) { xs[k] = (double)pose_init[6 * f + k]; xn[k] = xs[k]; sc[k] = 1.0; }
   if (r1 == r0) {
-    if (lane < 6) pose_out[6 * f + lane] = xs[lane];
-    if (lane == 0) { lorb_ba_summary z = {}; sums[f] = z; }
+    if (t < 6) pose_out[6 * f + t] = xs[t];
+    if (t == 0) { lorb_ba_summary z = {}; sums[f] = z; }
     return;
   }
   double radius = o.init_radius, df = 2.0;
   int iter = 0, n_success = 0, n_invalid = 0, term = LORB_TERM_NO_CONVERGENCE, last_successful = 1;
   double initial_cost = 0.0, cost = 0.0, gmax = 0.0, xnorm = 0.0;
   bool relin = true;
-  // the lane's first kPoC residuals (r0 + lane + 64 q) stay in registers for the whole solve; a frame
-  // with more than 64 kPoC residuals reads the rest from memory in each pass (same per-lane order)
-  constexpr int kPoC = 4;
+  int buf = 0;
+  // the thread's first kPoC residuals (r0 + t + kPoThreads q) stay in registers for the whole solve;
+  // a frame with more reads the rest from memory in each pass (same per-thread order)
+  constexpr int kPoC = 2;
   double cX[kPoC][3], cuv[kPoC][2];
 #pragma unroll
   for (int q = 0; q < kPoC; ++q) {
-    const int r = min(r0 + lane + 64 * q, r1 - 1);
+    const int r = min(r0 + t + kPoThreads * q, r1 - 1);
 #pragma unroll
     for (int k = 0; k < 3; ++k) cX[q][k] = pts3d[3 * r + k];
     cuv[q][0] = obs2d[2 * r]; cuv[q][1] = obs2d[2 * r + 1];
@@ -3007,20 +3613,33 @@ __global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__
         int q = 0;
 #pragma unroll
         for (int a = 0; a < 6; ++a) {
-          v[21 + a] += Jc[a] * rr[0] + Jc[6 + a] * rr[1];
+          v[21 + a] = fma(Jc[a], rr[0], fma(Jc[6 + a], rr[1], v[21 + a]));
 #pragma unroll
-          for (int b = a; b < 6; ++b) v[q++] += Jc[a] * Jc[b] + Jc[6 + a] * Jc[6 + b];
+          for (int b = a; b < 6; ++b) { v[q] = fma(Jc[a], Jc[b], fma(Jc[6 + a], Jc[6 + b], v[q])); ++q; }
         }
         v[27] += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
       };
 #pragma unroll
       for (int q = 0; q < kPoC; ++q)
-        if (r0 + lane + 64 * q < r1) acc(cX[q], cuv[q][0], cuv[q][1]);
-      for (int r = r0 + lane + 64 * kPoC; r < r1; r += 64) {
+        if (r0 + t + kPoThreads * q < r1) acc(cX[q], cuv[q][0], cuv[q][1]);
+      for (int r = r0 + t + kPoThreads * kPoC; r < r1; r += kPoThreads) {
         const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
         acc(X, obs2d[2 * r], obs2d[2 * r + 1]);
       }
       wave_sum_all<28>(v);
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 28; ++k) s_nv[buf][wv][k] = v[k];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 28; ++k) {
+        double a = s_nv[buf][0][k];
+#pragma unroll
+        for (int w = 1; w < kPoW; ++w) a += s_nv[buf][w][k];
+        v[k] = a;
+      }
+      buf ^= 1;
 #pragma unroll
       for (int k = 0; k < 21; ++k) JtJ[k] = v[k];
 #pragma unroll
@@ -3105,12 +3724,12 @@ __global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__
       const lorb::RotVal R = lorb::rot_val(xn);
 #pragma unroll
       for (int q = 0; q < kPoC; ++q)
-        if (r0 + lane + 64 * q < r1) {
+        if (r0 + t + kPoThreads * q < r1) {
           double rr[2];
           residual_s(R, xn + 3, cX[q], fx, fyv, cx, cy, cuv[q][0], cuv[q][1], rr);
           cv += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
         }
-      for (int r = r0 + lane + 64 * kPoC; r < r1; r += 64) {
+      for (int r = r0 + t + kPoThreads * kPoC; r < r1; r += kPoThreads) {
         const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
         double rr[2];
         residual_s(R, xn + 3, X, fx, fyv, cx, cy, obs2d[2 * r], obs2d[2 * r + 1], rr);
@@ -3118,6 +3737,12 @@ __global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__
       }
     }
     cv = wave_sum(cv);
+    if (lane == 0) s_cv[buf][wv] = cv;
+    __syncthreads();
+    cv = s_cv[buf][0];
+#pragma unroll
+    for (int w = 1; w < kPoW; ++w) cv += s_cv[buf][w];
+    buf ^= 1;
     const double new_cost = isfinite(cv) ? cv : 1.7976931348623157e308;
     double sn2 = 0.0;
 #pragma unroll
@@ -3142,8 +3767,8 @@ __global__ __launch_bounds__(64) void k_ba_pose_only(const int32_t* __restrict__
   }
 #pragma unroll
   for (int k = 0; k < 6; ++k)
-    if (lane == k) pose_out[6 * f + k] = xs[k];
-  if (lane == 0) {
+    if (t == k) pose_out[6 * f + k] = xs[k];
+  if (t == 0) {
     lorb_ba_summary sm;
     sm.iterations = iter; sm.successful_steps = n_success; sm.termination = term; sm.pad_ = 0;
     sm.initial_cost = initial_cost; sm.final_cost = cost;
@@ -3179,7 +3804,8 @@ struct lorb_ba_devbuild {
   int* hist = nullptr; int hist_cap = 0;  // camera-major block histograms
   int* cam_pt = nullptr;      // K_cap: point of each camera-major slot
   int* perm = nullptr;        // C: input camera -> plan camera
-  int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0;
+  int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0, gspan_cap = 0;
+  int gpart_cap = 0;  // doubles of BaDev::gpart (point-major path)
   std::vector<int> h_hdr, h_cov, h_cam;
   int* pinned = nullptr; size_t pinned_n = 0;
   double* sol_part = nullptr; size_t sol_n = 0;  // this rank's solve block (== the global one unsharded)
@@ -3325,6 +3951,25 @@ std::vector<int> camera_order(int C, const std::vector<char>& adj) {
   return camera_band(C, adj, pos) < camera_band(C, adj, id) ? pos : id;
 }
 
+// Point-major path (PM): windows of at most 64 optimised cameras (a group's camera window is a 64-bit
+// mask) whose points fit one group (C + F <= kGB observations per point); LORB_PM=0 keeps the
+// pair-major path (A/B, diagnostics)
+bool pm_fits(int C, int F) { return C <= 64 && C + F <= kGB; }
+bool pm_enabled() {
+  static const bool on = [] { const char* e = getenv("LORB_PM"); return !(e && e[0] == '0'); }();
+  return on;
+}
+// a window's partial layout: camera half band, slots of a full-width window, the camera terms after
+// them; its groups' partials from `total` on (advanced)
+void pm_layout(BaWin& bw, long long& total) {
+  const int C = bw.n_poses;
+  bw.bwc = bw.n > 0 ? std::max(bw.bw - 5, 0) / 6 : 0;
+  bw.part_cam = 36 * pm_nslots(C, bw.bwc);
+  bw.part_stride = bw.part_cam + 18 * C;
+  bw.part_base = total;
+  total += (long long)bw.n_pblk * bw.part_stride;
+}
+
 int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan* P) {
   // camera relabelling per window (RCM), applied to copies of the pose / observation arrays; the
   // covisibility graph of a sharded window is all-reduced so every rank picks the same order
@@ -3415,8 +4060,11 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   std::vector<BlockPair> bps;
   std::vector<int2> pairs;
   int pose_base = 0, point_base = 0, fix_base = 0, env_base = 0, row_base = 0;
+  long long part_total = 0;
+  bool pm_ok = true;
   for (int w = 0; w < nw; ++w) {
     const lorb_ba_window& in = win[w];
+    pm_ok = pm_ok && pm_fits(in.n_poses, in.n_fixed);
     if (in.n_poses < 0 || in.n_points < 0 || in.n_obs < 0 || in.n_fixed < 0)
       return lorb::set_error(ctx, LORB_E_INVALID, "window %d: negative sizes", w);
     BaWin bw{};
@@ -3521,6 +4169,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
       pblk.push_back(g);
     }
     bw.n_pblk = (int)pblk.size() - bw.pblk_base;
+    pm_layout(bw, part_total);
     P->hwin.push_back(bw);
     pose_base += in.n_poses; point_base += in.n_points; fix_base += in.n_fixed;
   }
@@ -3613,11 +4262,18 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
 #ifdef LORB_CHOL_TRACE
   LORB_TRY(dalloc(P, (size_t)nw * 512, &d.dbg));
+#elif defined(LORB_LS_STAMPS)
+  LORB_TRY(dalloc(P, (size_t)std::max(P->n_pblk, nw) * 8, &d.dbg));
 #else
   LORB_TRY(dalloc(P, (size_t)nw * 8, &d.dbg));
 #endif
   LORB_TRY(dalloc(P, ((size_t)P->n_total / 16 + nw + 1) * 1024, &d.kco));
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
+  d.pm = pm_ok && pm_enabled() ? 1 : 0;
+  if (d.pm) {
+    LORB_TRY(dalloc(P, (size_t)std::max(part_total, 1ll), &d.gpart));
+    LORB_TRY(dalloc(P, (size_t)std::max(P->n_pblk, 1), &d.gspan));
+  }
   if (!obs_cam.empty()) { /* keep obs arrays alive via allocs */ }
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return LORB_OK;
@@ -3657,11 +4313,22 @@ lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
 int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = P->ctx->stream;
   const BaDev& d = P->dev;
-  if (P->grid_pblk) {
-    lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-    hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
+  if (d.pm) {  // point-major: the group partials, then the camera terms of the head
+    if (P->grid_pblk) {
+      lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
+      hipLaunchKernelGGL(k_ba_ls, dim3(P->grid_pblk), dim3(kLsThreads), 0, s, d, o);
+    }
+    if (P->grid_bp) {
+      lorb::KernelTimer kt(P->ctx, LORB_K_BA_SCHUR);
+      hipLaunchKernelGGL(k_ba_red<0>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
+    }
+  } else {
+    if (P->grid_pblk) {
+      lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
+      hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
+    }
+    if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(256), 0, s, d);
   }
-  if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(256), 0, s, d);
   if (P->comm) {  // exchange 1: camera blocks + cost / |x|^2 (sum), gradient max (max)
     hipLaunchKernelGGL(k_ba_win_reduce<0>, dim3(P->W), dim3(64), 0, s, d);
     {
@@ -3690,20 +4357,27 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
   if (fused) {
     if (P->grid_pblk) {
       lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-      hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
+      if (d.pm) hipLaunchKernelGGL(k_ba_ls, dim3(P->grid_pblk), dim3(kLsThreads), 0, s, d, o);
+      else hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
     }
   } else {
     LORB_TRY(enqueue_linearize(P, o));
   }
-  // The LDS Cholesky never writes env, and k_ba_schur rewrites every stored entry of every
-  // block each iteration, so the band's structural zeros (set at plan creation) persist; the
+  // The LDS Cholesky never writes env, and k_ba_schur / k_ba_red rewrite every stored entry of
+  // every block each iteration, so the band's structural zeros (set at plan creation) persist; the
   // in-place global variant needs them restored.
   const bool chol_in_lds = sizeof(double) * (size_t)P->max_env <= (size_t)kLdsBudget;
   if (P->env_total && !chol_in_lds && !P->comm) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   if (P->grid_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
-    if (fused) hipLaunchKernelGGL(k_ba_schur<true>, dim3(P->grid_bp + P->Ctot), dim3(256), 0, s, d, o, (int)P->grid_bp);
-    else hipLaunchKernelGGL(k_ba_schur<false>, dim3(P->grid_bp), dim3(256), 0, s, d, o, (int)P->grid_bp);
+    if (d.pm) {
+      if (fused) hipLaunchKernelGGL(k_ba_red<2>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
+      else hipLaunchKernelGGL(k_ba_red<1>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
+    } else if (fused) {
+      hipLaunchKernelGGL(k_ba_schur<true>, dim3(P->grid_bp + P->Ctot), dim3(256), 0, s, d, o, (int)P->grid_bp);
+    } else {
+      hipLaunchKernelGGL(k_ba_schur<false>, dim3(P->grid_bp), dim3(256), 0, s, d, o, (int)P->grid_bp);
+    }
   }
   if (P->comm && fused) {
     // the fused sharded iteration: the point partials of the head, then exchanges 1 and 2 as one
@@ -3741,7 +4415,10 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
     else { if (rpl == 1) LORB_CHOL(false, 1); else if (rpl == 2) LORB_CHOL(false, 2); else if (rpl == 4) LORB_CHOL(false, 4); else LORB_CHOL(false, 8); }
 #undef LORB_CHOL
   }
-  if (P->grid_pblk) hipLaunchKernelGGL(k_ba_backsub, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
+  if (P->grid_pblk) {
+    if (d.pm) hipLaunchKernelGGL(k_ba_bs2, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
+    else hipLaunchKernelGGL(k_ba_backsub, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
+  }
   if (P->comm) {  // exchange 3: model cost change, candidate cost, point |step|^2
     hipLaunchKernelGGL(k_ba_win_reduce<1>, dim3(P->W), dim3(64), 0, s, d);
     {
@@ -4583,6 +5260,7 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
 #endif
   LORB_TRY(dalloc(P, ((size_t)n / 16 + 2) * 1024, &d.kco));
   LORB_TRY(dalloc(P, (size_t)1, &P->d_state)); d.st = P->d_state;
+  d.pm = pm_fits(b.C, b.F) && pm_enabled() ? 1 : 0;
   P->W = 1;
   P->hwin.assign(1, BaWin{});
   P->pt_launch = b.P_cap;
@@ -4812,6 +5490,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   bw.env_base = 0; bw.env_size = n * (bwid + 1); bw.n = n; bw.row_base = 0; bw.bw = bwid;
   bw.obs_base = 0; bw.n_obs = K; bw.n_obs_all = K_all;
   bw.fx = w->fx; bw.fy = w->fy; bw.cx = w->cx; bw.cy = w->cy;
+  long long part_total = 0;
+  pm_layout(bw, part_total);
   P->hwin[0] = bw;
   P->Ctot = C; P->Ptot = Pn; P->K = K; P->NF = F; P->n_pblk = G; P->n_bp = (int)bps.size(); P->n_pairs = n_pairs;
   P->env_total = bw.env_size; P->n_total = n;
@@ -4842,6 +5522,12 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     d.part = pt;
   }
   P->grid_pblk = b.pblk_cap;
+  if (d.pm) {  // group partials (grow-only; a reallocation re-captures the LM graph)
+    LORB_TRY(grow(P, &d.gpart, &b.gpart_cap, (size_t)std::max(part_total, 1ll)));
+    int2* gsp = d.gspan;
+    LORB_TRY(grow(P, &gsp, &b.gspan_cap, (size_t)b.pblk_cap));
+    d.gspan = gsp;
+  }
   LORB_TRY(up_alloc(P, (int)bps.size()));
   hp_mark(3);
   // one upload (pinned staging, stream-ordered; the next build writes the staging only after its
@@ -4896,7 +5582,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   }
   if (K > 0 && !fuse)
     hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), sizeof(int) * std::max(C, 1), s, d, K, NB, C, b.hist, b.cam_pt);
-  if (!bps.empty())
+  // the block pair lists feed the pair-major Schur only (the point-major path reduces group partials)
+  if (!bps.empty() && !d.pm)
     hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), sizeof(int) * (C + 1), s, d, C, b.cam_pt);
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
@@ -5012,6 +5699,8 @@ int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8) {
   if (!plan || !out8) return LORB_E_INVALID;
 #ifdef LORB_CHOL_TRACE
   const size_t nst = 512;  // trace builds: the caller passes 512 entries
+#elif defined(LORB_LS_STAMPS)
+  const size_t nst = (size_t)std::max(plan->n_pblk, plan->W) * 8;  // host-built plans: 8 per point group
 #else
   const size_t nst = 8;
 #endif
@@ -5067,7 +5756,7 @@ int lorb_ba_pose_only(lorb_ctx* ctx, const lorb_pose_problem_batch* prob,
   lorb::OutPack out(ctx);
   const int o_pose = out.add(sizeof(double) * 6 * nf), o_sum = out.add(sizeof(lorb_ba_summary) * nf);
   LORB_TRY(out.alloc(true));  // the kernel stores poses and summaries into the mapped block
-  hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(64), 0, ctx->stream, in.dev<int32_t>(i_roff), in.dev<float>(i_intr),
+  hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(kPoThreads), 0, ctx->stream, in.dev<int32_t>(i_roff), in.dev<float>(i_intr),
                      in.dev<float>(i_pinit), in.dev<float>(i_pts), in.dev<float>(i_obs), to_dev_opt(opt),
                      out.dev<double>(o_pose), out.dev<lorb_ba_summary>(o_sum));
   LORB_CHECK_LAUNCH(ctx);

@@ -90,10 +90,13 @@ def Tcw_from(aa, t):
 
 # ------------------------------------------------------------------------------------------
 def ba_window(seed=3, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400, obs_lens=(7, 8),
-              noise_px=0.5, fx=FX, fy=FY, cx=CX, cy=CY, pert=(2e-3, 2e-2, 5e-2)):
+              noise_px=0.5, fx=FX, fy=FY, cx=CX, cy=CY, pert=(2e-3, 2e-2, 5e-2), point_order="first_kf"):
     """Local-BA window.  KF i: camera centre (0.1 i, 0, 0), yaw 0.01 i.
     Each point is seen by a contiguous KF range of length obs_lens[p % len]; n_fixed extra
     out-of-window KFs (MPCost, fixed pose) each observe ~fixed_obs_per_kf points to fix the gauge.
+    point_order "first_kf" numbers the points by their first observing keyframe (stable), the order
+    BA::LocalPoseOptimization collects them in -- keyframe by keyframe, each keyframe's map points not
+    seen before (src/bundle_adjust.cpp:224-241); "random" keeps the draw order (no camera locality).
     Returns the problem dict consumed by lorb_ba_local / or_ba_local plus ground truth."""
     rng = np.random.default_rng(seed)
 
@@ -118,6 +121,16 @@ def ba_window(seed=3, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400, obs_
         for p in np.sort(sel):
             obs_p.append(p); obs_f.append(-1 - j)
     obs_p = np.array(obs_p, np.int32); obs_f = np.array(obs_f, np.int32)
+    if point_order == "first_kf":  # relabel: point rank by (first window keyframe, draw index)
+        first = np.full(n_pts, n_kf, np.int64)
+        win = obs_f >= 0
+        np.minimum.at(first, obs_p[win], obs_f[win])
+        rank = np.empty(n_pts, np.int64)
+        rank[np.argsort(first, kind="stable")] = np.arange(n_pts)
+        pts = pts[np.argsort(rank)]
+        obs_p = rank[obs_p].astype(np.int32)
+    elif point_order != "random":
+        raise ValueError(point_order)
     allposes = np.concatenate([true_poses, fixed], 0)
     fidx = np.where(obs_f >= 0, obs_f, n_kf + (-1 - obs_f))
     uv = np.zeros((len(obs_p), 2))

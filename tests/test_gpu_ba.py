@@ -93,6 +93,22 @@ def test_local_ba_c3_ten_iterations(ctx):
     assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
 
 
+@pytest.mark.parametrize("n_kf,obs_lens", [(20, (7, 8)), (40, (2, 30))])
+def test_local_ba_point_order_without_camera_locality(ctx, n_kf, obs_lens):
+    """Points in draw order (no camera locality: a point group's camera window spans most of the
+    window) and, second case, points seen by 2 or 30 keyframes (a camera band of 29): the
+    point-major path's group windows are wide and its partials sparse -- the result must not depend
+    on the point order's locality, only its speed does."""
+    w = synth.ba_window(seed=17, n_kf=n_kf, n_pts=2000, n_fixed=2, fixed_obs_per_kf=200, obs_lens=obs_lens,
+                        point_order="random")
+    opt = A.LMOptions.default(max_num_iterations=8, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    Pg, Xg, sg = ctx.ba_local([w], opt)
+    Po, Xo, so = O.ba_local([w], opt)
+    lm_match(sg[0], so[0])
+    assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
+    assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
+
+
 def test_local_ba_batched_ragged_windows(ctx):
     wins = [synth.ba_window(seed=10 + i, n_kf=k, n_pts=p, n_fixed=nf, fixed_obs_per_kf=50)
             for i, (k, p, nf) in enumerate([(3, 100, 1), (8, 700, 2), (12, 900, 3), (5, 257, 1)])]
