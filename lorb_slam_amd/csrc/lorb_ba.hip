@@ -3076,6 +3076,14 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
 #define LS_STAMP(k) do {} while (0)
 #endif
   LS_STAMP(0);
+#ifdef LORB_LS_STAMPS
+  // where the group ran: HW_ID (hwreg 4) << 8 | XCC_ID (hwreg 20); when: the 100 MHz real-time
+  // counter at the start (<< 20) | the ticks to the end (slot 7, written at LS_STAMP(5))
+  const unsigned long long ls_rt0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0)
+    d.dbg[8 * blockIdx.x + 6] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 8) |
+                                (__builtin_amdgcn_s_getreg((31 << 11) | 20) & 255);
+#endif
   const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const bool has = t < g.no;
@@ -3211,10 +3219,16 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
   // point does not share sits the point out.  The four waves' blocks are then summed in wave order
   // through LDS (the observation data is dead by then).  More than 64 slots: waves take 64-slot
   // chunks over all points instead (no point split, no cross-wave sum).
+  // A group of few slots (a window's newest points: many points, 1 - 4 cameras) would leave most
+  // lanes idle through a long point loop: there R = 2^lr lanes share a slot (R nsl <= 64), lane =
+  // (slot, point subset), and their sums are combined by a butterfly (fixed order) first.
   const bool split = nsl <= 64;
+  int lr = 0;
+  if (split) while (lr < 6 && (nsl << (lr + 1)) <= 64) ++lr;
   const int nrounds = split ? 1 : (nsl + 64 * kLsWaves - 1) / (64 * kLsWaves);
   for (int rd = 0; rd < nrounds; ++rd) {
-    const int q = split ? lane : 64 * (kLsWaves * rd + wv) + lane;
+    const int q = split ? lane >> lr : 64 * (kLsWaves * rd + wv) + lane;
+    const int rr = split ? lane & ((1 << lr) - 1) : 0;
     const bool act = q < nsl;
     int a = 0, dd = 0;
     if (act) pm_slot_inv(q, bwc, a, dd);
@@ -3226,7 +3240,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
     for (int k = 0; k < 36; ++k) acc[k] = 0.0;
 #pragma unroll
     for (int k = 0; k < 18; ++k) ex[k] = 0.0;
-    const int k0 = split ? wv : 0, kst = split ? kLsWaves : 1;
+    const int k0 = split ? (wv << lr) + rr : 0, kst = split ? kLsWaves << lr : 1;
     if (!LORB_LS_SKIPD && k0 < g.cnt) {
       unsigned long long m = s_mask[k0];
       int po = s_po[k0];
@@ -3267,15 +3281,22 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
         }
       }
     }
+    for (int m = 1; m < (1 << lr); m <<= 1) {  // the slot's R subsets (lr = 0 unless split)
+#pragma unroll
+      for (int k = 0; k < 36; ++k) acc[k] += __shfl_xor(acc[k], m, 64);
+#pragma unroll
+      for (int k = 0; k < 18; ++k) ex[k] += __shfl_xor(ex[k], m, 64);
+    }
+    const bool own = act && rr == 0;  // the slot's lane after the butterfly
     if (split) {
       // ((w0 + w1) + w2) + w3 through 64 x 36 + 64 x 18 buffers over the dead observation data
       static_assert(64 * 36 <= kGB * 12 && 64 * 18 <= kGB * 12, "reduction buffers");
       __syncthreads();
 #pragma unroll
       for (int w = 0; w < kLsWaves; ++w) {
-        if (wv == w && act) {
-          double* bl = &s_jc[0][0] + 36 * lane;
-          double* bx = &s_qj[0][0] + 18 * lane;
+        if (wv == w && own) {
+          double* bl = &s_jc[0][0] + 36 * q;
+          double* bx = &s_qj[0][0] + 18 * q;
 #pragma unroll
           for (int k = 0; k < 36; ++k) { if (w > 0) acc[k] += bl[k]; if (w + 1 < kLsWaves) bl[k] = acc[k]; }
           if (dg) {
@@ -3286,7 +3307,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
         if (w + 1 < kLsWaves) __syncthreads();
       }
     }
-    if (act && (!split || wv == kLsWaves - 1)) {
+    if (own && (!split || wv == kLsWaves - 1)) {
       double* out = gp + 36 * q;
 #pragma unroll
       for (int k = 0; k < 36; ++k) out[k] = acc[k];
@@ -3301,6 +3322,9 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
   block_red3w<kLsWaves, true>(cost, gm, xn2, red3);
   if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[0] = cost; P[1] = gm; P[2] = xn2; }
   LS_STAMP(5);
+#ifdef LORB_LS_STAMPS
+  if (t == 0) d.dbg[8 * blockIdx.x + 7] = (ls_rt0 << 20) | ((__builtin_amdgcn_s_memrealtime() - ls_rt0) & 0xfffff);
+#endif
 #undef LS_STAMP
 }
 
@@ -3869,6 +3893,79 @@ struct lorb_ba_plan {
       fprintf(stderr, "lorb_ba_plan: host phase %.2f us per device build (%d builds): checks %.2f order %.2f blocks %.2f "
               "buffers %.2f staging %.2f launch %.2f\n", hp_us / hp_n, hp_n, hp_sec[0] / hp_n, hp_sec[1] / hp_n,
               hp_sec[2] / hp_n, hp_sec[3] / hp_n, hp_sec[4] / hp_n, hp_sec[5] / hp_n);
+    // LORB_PM_SPANS=1 (diagnostics): the point groups' camera spans of the last linearisation
+    if (dev.pm && dev.gspan && n_pblk > 0 && getenv("LORB_PM_SPANS")) {
+      std::vector<int2> gs(n_pblk);
+      if (hipStreamSynchronize(ctx->stream) == hipSuccess &&
+          hipMemcpy(gs.data(), dev.gspan, sizeof(int2) * n_pblk, hipMemcpyDeviceToHost) == hipSuccess) {
+        std::vector<int> sp;
+        for (const int2& g : gs) if (g.y > 0) sp.push_back(g.y);
+        std::sort(sp.begin(), sp.end());
+        if (!sp.empty())
+          fprintf(stderr, "lorb_ba_plan: %d point groups (%zu live), %d observations; camera span p50 %d p90 %d max %d\n",
+                  n_pblk, sp.size(), K, sp[sp.size() / 2], sp[sp.size() * 9 / 10], sp.back());
+      }
+    }
+#ifdef LORB_LS_STAMPS
+    // LORB_LS_PRINT=1: the last k_ba_ls launch's phase cycles (medians over the point groups)
+    if (dev.pm && dev.dbg && n_pblk > 0 && getenv("LORB_LS_PRINT")) {
+      std::vector<unsigned long long> st((size_t)n_pblk * 8);
+      if (hipStreamSynchronize(ctx->stream) == hipSuccess &&
+          hipMemcpy(st.data(), dev.dbg, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost) == hipSuccess) {
+        fprintf(stderr, "lorb_ba_plan: k_ba_ls phase cycles (median, p90):");
+        for (int k = 0; k < 5; ++k) {
+          std::vector<long long> v;
+          for (int g = 0; g < n_pblk; ++g)
+            if (st[8 * g]) v.push_back((long long)(st[8 * g + k + 1] - st[8 * g + k]));
+          std::sort(v.begin(), v.end());
+          if (!v.empty()) fprintf(stderr, " %c %lld %lld", "ABCDE"[k], v[v.size() / 2], v[v.size() * 9 / 10]);
+        }
+        fprintf(stderr, "\n");
+        // per XCC (s_memtime is per XCC): first start -> last end, and groups that shared a CU with
+        // an earlier one (same XCC / SE / SH / CU) -- started after it ended (serial) or not (co-resident)
+        std::map<unsigned long long, std::vector<int>> by_cu;
+        unsigned long long r0 = ~0ull, r1 = 0;
+        std::vector<long long> dur;
+        for (int g = 0; g < n_pblk; ++g) {
+          if (!st[8 * g]) continue;
+          const unsigned long long a = st[8 * g + 7] >> 20, b = a + (st[8 * g + 7] & 0xfffff);
+          r0 = std::min(r0, a); r1 = std::max(r1, b);
+          dur.push_back((long long)(b - a));
+          by_cu[st[8 * g + 6] & 0xff00ffull].push_back(g);  // XCC | CU / SH / SE of HW_ID
+        }
+        std::sort(dur.begin(), dur.end());
+        int shared = 0;
+        long long pair_max = 0;
+        for (auto& c : by_cu) {
+          if (c.second.size() < 2) continue;
+          ++shared;
+          unsigned long long a = ~0ull, b = 0;
+          for (int g : c.second) { a = std::min(a, st[8 * g + 7] >> 20); b = std::max(b, (st[8 * g + 7] >> 20) + (st[8 * g + 7] & 0xfffff)); }
+          pair_max = std::max(pair_max, (long long)(b - a));
+        }
+        if (!dur.empty())
+          fprintf(stderr, "lorb_ba_plan: k_ba_ls real time (us): first start -> last end %.2f; group p50 %.2f p90 %.2f max %.2f; "
+                  "%zu CUs, %d with > 1 group (their span max %.2f)\n", (r1 - r0) * 0.01, dur[dur.size() / 2] * 0.01,
+                  dur[dur.size() * 9 / 10] * 0.01, dur.back() * 0.01, by_cu.size(), shared, pair_max * 0.01);
+        // the slowest groups: phases, points / observations, camera span
+        std::vector<PBlk> pb(n_pblk);
+        std::vector<int2> gs(n_pblk);
+        if (hipMemcpy(pb.data(), dev.pblk, sizeof(PBlk) * n_pblk, hipMemcpyDeviceToHost) == hipSuccess &&
+            hipMemcpy(gs.data(), dev.gspan, sizeof(int2) * n_pblk, hipMemcpyDeviceToHost) == hipSuccess) {
+          std::vector<int> ord;
+          for (int g = 0; g < n_pblk; ++g) if (st[8 * g]) ord.push_back(g);
+          std::sort(ord.begin(), ord.end(), [&](int a, int b) { return (st[8 * a + 7] & 0xfffff) > (st[8 * b + 7] & 0xfffff); });
+          for (size_t i = 0; i < ord.size() && i < 6; ++i) {
+            const int g = ord[i];
+            fprintf(stderr, "  group %d: %.2f us, points %d obs %d span %d, phases", g, (st[8 * g + 7] & 0xfffff) * 0.01,
+                    pb[g].cnt, pb[g].no, gs[g].y);
+            for (int k = 0; k < 5; ++k) fprintf(stderr, " %lld", (long long)(st[8 * g + k + 1] - st[8 * g + k]));
+            fprintf(stderr, "\n");
+          }
+        }
+      }
+    }
+#endif
     if (devb) {
       if (devb->pinned) (void)hipHostFree(devb->pinned);
       if (devb->up_host) (void)hipHostFree(devb->up_host);
@@ -5255,6 +5352,8 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(dalloc(P, n, &d.ycam));
 #ifdef LORB_CHOL_TRACE
   LORB_TRY(dalloc(P, (size_t)512, &d.dbg));
+#elif defined(LORB_LS_STAMPS)
+  LORB_TRY(dalloc(P, (K + Pn + 1) * 8, &d.dbg));  // >= 8 per point group at any build
 #else
   LORB_TRY(dalloc(P, (size_t)8, &d.dbg));
 #endif
