@@ -19,7 +19,9 @@
 // for the float paths that must be bit-exact (projection, grid, unprojection, ORB, stereo: the other
 // translation units).  Everything in this file is deterministic either way (fixed reduction orders);
 // the host code here (cv::Rodrigues restated, x86-64 without FMA) is unaffected.
+#ifndef LORB_NO_CONTRACT  // A/B builds only (tools/isa_fma.py, tools/build_variant.sh nofma -DLORB_NO_CONTRACT)
 #pragma clang fp contract(fast)
+#endif
 #include "lorb_ba_math.h"
 #include "lorb_internal.h"
 
