@@ -3589,8 +3589,19 @@ __global__ __launch_bounds__(kGB) void k_ba_bs2(BaDev d) {
 // wave order through LDS, the candidate cost a butterfly plus the same; every thread then carries
 // the frame's LM state and solves the 6 x 6 system redundantly (identical bits everywhere, so the
 // control flow is uniform).  Two barriers per iteration; the LDS exchange is double-buffered.
+#ifdef LORB_PO_STAMPS
+// diagnostics (tools/po_stamps.py): s_memtime of frame 0's thread 0 at each phase, in order
+__device__ unsigned long long g_po_st[64];
+#define PO_STAMP(tag) do { if (blockIdx.x == 0 && threadIdx.x == 0 && po_n < 31) { g_po_st[2 * po_n] = __builtin_amdgcn_s_memtime(); g_po_st[2 * po_n + 1] = (tag); ++po_n; } } while (0)
+#else
+#define PO_STAMP(tag) do {} while (0)
+#endif
 constexpr int kPoW = 4, kPoThreads = 64 * kPoW;
-__global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __restrict__ res_off,
+constexpr int kPoRegRes = 2 * kPoThreads;  // residuals per frame held in registers (kPoC per thread)
+// a small batch's residual offsets as a kernel argument: the residual loads need no round trip first
+constexpr int kPoArgF = 16;
+struct PoOff { int n; int off[kPoArgF + 1]; };
+__global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(PoOff aoff, const int32_t* __restrict__ res_off,
                                                              const float* __restrict__ intr,
                                                              const float* __restrict__ pose_init,
                                                              const float* __restrict__ pts3d,
@@ -3601,7 +3612,11 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
   __shared__ double s_cv[2][kPoW];
   const int f = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int r0 = res_off[f], r1 = res_off[f + 1];
+#ifdef LORB_PO_STAMPS
+  int po_n = 0;
+#endif
+  PO_STAMP(0);
+  const int r0 = aoff.n ? aoff.off[f] : res_off[f], r1 = aoff.n ? aoff.off[f + 1] : res_off[f + 1];
   const double fx = intr[4 * f], fyv = intr[4 * f + 1], cx = intr[4 * f + 2], cy = intr[4 * f + 3];
   double xs[6], xn[6], sc[6], JtJ[21], Jtr[6];
 #pragma unroll
@@ -3618,7 +3633,7 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
   int buf = 0;
   // the thread's first kPoC residuals (r0 + t + kPoThreads q) stay in registers for the whole solve;
   // a frame with more reads the rest from memory in each pass (same per-thread order)
-  constexpr int kPoC = 2;
+  constexpr int kPoC = kPoRegRes / kPoThreads;
   double cX[kPoC][3], cuv[kPoC][2];
 #pragma unroll
   for (int q = 0; q < kPoC; ++q) {
@@ -3629,6 +3644,7 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
   }
   for (;;) {
     if (relin) {
+      PO_STAMP(1);
       double v[32];  // 21 JtJ + 6 Jtr + cost (+ wave_sum_all's padding)
 #pragma unroll
       for (int k = 0; k < 28; ++k) v[k] = 0.0;
@@ -3652,12 +3668,15 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
         const double X[3] = {pts3d[3 * r], pts3d[3 * r + 1], pts3d[3 * r + 2]};
         acc(X, obs2d[2 * r], obs2d[2 * r + 1]);
       }
+      PO_STAMP(2);
       wave_sum_all<28>(v);
+      PO_STAMP(3);
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < 28; ++k) s_nv[buf][wv][k] = v[k];
       }
       __syncthreads();
+      PO_STAMP(4);
 #pragma unroll
       for (int k = 0; k < 28; ++k) {
         double a = s_nv[buf][0][k];
@@ -3699,8 +3718,8 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
     }
 #pragma unroll
     for (int a = 0; a < 6; ++a) A[7 * a] += fmin(fmax(A[7 * a], o.min_diag), o.max_diag) / radius;
-    // the six pivots' reciprocals once (one IEEE division each); the column and both triangular
-    // solves multiply by them: the solve's dependent chain holds 6 divisions instead of 33
+    // the six pivots' reciprocal square roots once (v_rsq_f64 + two Newton steps, as k_ba_chol:
+    // no IEEE sqrt / division on the chain); the column and both triangular solves multiply by them
     bool ok = true;
     double il[6];
 #pragma unroll
@@ -3709,7 +3728,7 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
 #pragma unroll
       for (int k = 0; k < j; ++k) dd -= A[6 * j + k] * A[6 * j + k];
       ok = ok && dd > 0.0;
-      il[j] = 1.0 / sqrt(dd);
+      il[j] = rsqrt_refined(dd);
 #pragma unroll
       for (int i = j + 1; i < 6; ++i) {
         double sv = A[6 * i + j];
@@ -3725,14 +3744,20 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
 #pragma unroll
       for (int i = 5; i >= 0; --i) { double sv = y[i]; for (int k = i + 1; k < 6; ++k) sv -= A[6 * k + i] * y[k]; y[i] = sv * il[i]; }
       // model cost change = -(step.Js^T r + 0.5 step^T Js^T Js step), step = -y
-      double lin = 0.0, quad = 0.0;
+      // on the unscaled step z = sc (-y): lin = z . J^T r, quad = z^T (J^T J z) -- six independent
+      // row products, then two dot products (short dependent chains)
+      double z[6], w[6];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) z[a] = sc[a] * -y[a];
 #pragma unroll
       for (int a = 0; a < 6; ++a) {
-        const double sa = -y[a];
-        lin += sa * Jtr[a] * sc[a];
+        w[a] = 0.0;
 #pragma unroll
-        for (int b = 0; b < 6; ++b) quad += sa * JtJ[u21(a, b)] * sc[a] * sc[b] * (-y[b]);
+        for (int b = 0; b < 6; ++b) w[a] = fma(JtJ[u21(a, b)], z[b], w[a]);
       }
+      double lin = 0.0, quad = 0.0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) { lin = fma(z[a], Jtr[a], lin); quad = fma(z[a], w[a], quad); }
       mcc = -(lin + 0.5 * quad);
 #pragma unroll
       for (int a = 0; a < 6; ++a) xn[a] = xs[a] + (-y[a]) * sc[a];
@@ -3744,6 +3769,7 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
       continue;
     }
     n_invalid = 0;
+    PO_STAMP(5);
     // candidate cost
     double cv = 0.0;
     {
@@ -3762,9 +3788,11 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
         cv += 0.5 * (rr[0] * rr[0] + rr[1] * rr[1]);
       }
     }
+    PO_STAMP(6);
     cv = wave_sum(cv);
     if (lane == 0) s_cv[buf][wv] = cv;
     __syncthreads();
+    PO_STAMP(7);
     cv = s_cv[buf][0];
 #pragma unroll
     for (int w = 1; w < kPoW; ++w) cv += s_cv[buf][w];
@@ -3791,6 +3819,7 @@ __global__ __launch_bounds__(kPoThreads) void k_ba_pose_only(const int32_t* __re
       df *= 2.0;
     }
   }
+  PO_STAMP(8);
 #pragma unroll
   for (int k = 0; k < 6; ++k)
     if (t == k) pose_out[6 * f + k] = xs[k];
@@ -5848,16 +5877,26 @@ int lorb_ba_pose_only(lorb_ctx* ctx, const lorb_pose_problem_batch* prob,
   const int nf = prob->n_frames;
   if (nf <= 0) return LORB_OK;
   const int nr = prob->res_off[nf];
-  // every input in one pull, poses and summaries stored straight into pinned memory
+  // every input in one pinned staging, poses and summaries stored straight into pinned memory.  A
+  // batch whose frames all fit the kernel's register-resident residuals reads each input once: the
+  // kernel then reads the mapped staging directly (no pull launch); larger frames re-read theirs
+  // every pass, from HBM after a pull.
+  int max_res = 0;
+  for (int f = 0; f < nf; ++f) max_res = std::max(max_res, prob->res_off[f + 1] - prob->res_off[f]);
   lorb::InPack in(ctx);
   const int i_roff = in.add_t(prob->res_off, (size_t)nf + 1), i_intr = in.add_t(prob->intr, (size_t)nf * 4),
             i_pinit = in.add_t(prob->pose_init, (size_t)nf * 6), i_pts = in.add_t(prob->pts3d, (size_t)nr * 3),
             i_obs = in.add_t(prob->obs2d, (size_t)nr * 2);
-  LORB_TRY(in.commit());
+  LORB_TRY(in.commit(max_res <= kPoRegRes));
   lorb::OutPack out(ctx);
   const int o_pose = out.add(sizeof(double) * 6 * nf), o_sum = out.add(sizeof(lorb_ba_summary) * nf);
   LORB_TRY(out.alloc(true));  // the kernel stores poses and summaries into the mapped block
-  hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(kPoThreads), 0, ctx->stream, in.dev<int32_t>(i_roff), in.dev<float>(i_intr),
+  PoOff aoff{};
+  if (nf <= kPoArgF) {
+    aoff.n = nf;
+    for (int f = 0; f <= nf; ++f) aoff.off[f] = prob->res_off[f];
+  }
+  hipLaunchKernelGGL(k_ba_pose_only, dim3(nf), dim3(kPoThreads), 0, ctx->stream, aoff, in.dev<int32_t>(i_roff), in.dev<float>(i_intr),
                      in.dev<float>(i_pinit), in.dev<float>(i_pts), in.dev<float>(i_obs), to_dev_opt(opt),
                      out.dev<double>(o_pose), out.dev<lorb_ba_summary>(o_sum));
   LORB_CHECK_LAUNCH(ctx);
@@ -5872,6 +5911,12 @@ int lorb_ba_pose_only(lorb_ctx* ctx, const lorb_pose_problem_batch* prob,
     }
   return LORB_OK;
 }
+
+#ifdef LORB_PO_STAMPS
+int lorb_debug_po_stamps(unsigned long long* out64) {
+  return hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_po_st), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // cv::Rodrigues (vector -> matrix, double internally) + Frame::UpdatePoseMat write-back
 void lorb_pose_to_Tcw(const float rvec[3], const float tvec[3], float T[16]) {

@@ -167,7 +167,9 @@ class InPack {
   }
   template <typename T>
   int add_t(const T* host, size_t count) { return add(host, host ? count * sizeof(T) : 0); }
-  int commit();
+  // mapped: no pull -- dev<T>() then addresses the mapped staging itself (for a kernel that reads
+  // each input once: one PCIe round trip instead of a pull launch and its hand-off)
+  int commit(bool mapped = false);
   template <typename T>
   T* dev(int i) const { return parts[i].bytes ? reinterpret_cast<T*>(static_cast<unsigned char*>(base) + parts[i].off) : nullptr; }
 

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(256) void k_io_pull(const uint4* __restrict__ src, 
     dst[i] = src[i];
 }
 
-int InPack::commit() {
+int InPack::commit(bool mapped) {
   if (!total) return LORB_OK;
   // a call that failed after its commit may have left its copy in flight
   // every host-array call ends waiting for its stream (OutPack::fetch); only a call that failed
@@ -84,6 +84,11 @@ int InPack::commit() {
   unsigned char* h = static_cast<unsigned char*>(ctx->io_in);
   for (const Part& p : parts)
     if (p.bytes) std::memcpy(h + p.off, p.host, p.bytes);
+  if (mapped) {
+    base = ctx->io_in_dev;
+    ctx->io_pending = true;
+    return LORB_OK;
+  }
   LORB_TRY(scratch(ctx, S_IO_IN, total, &base));
   size_t used = 0;
   for (const Part& p : parts) used = std::max(used, p.off + p.bytes);
