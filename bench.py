@@ -31,6 +31,7 @@ timed region.  torch.distributed (gloo, CPU) provides the barrier, the max-over-
 timing and the RCCL unique id; the data-path collectives (shared workload) are RCCL.
 """
 import argparse
+import concurrent.futures
 import ctypes as C
 import json
 import os
@@ -207,14 +208,17 @@ def workload_c4(ctx, args, rank):
     the BA plan on the device and runs 10 LM iterations.  The plan build is inside the step."""
     from lorb_slam_amd import _abi as A
     from lorb_slam_amd import synth
-    from lorb_slam_amd.runtime import LocalMap
+    from lorb_slam_amd.runtime import Context, LocalMap
     W = args.windows
     n_kf_needed = args.warmup + args.steps + max(3, min(args.steps, 10)) + 2
     seqs = [synth.mapping_sequence(seed=4 + 1009 * rank + 17 * i, steps=n_kf_needed) for i in range(W)]
     opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
+    # one context (one stream) per window: the windows' steps run concurrently, each in its own
+    # stream order (the first window on the caller's context)
+    ctxs = [ctx] + [Context(ctx.device) for _ in range(W - 1)]
     t0 = time.perf_counter()
-    maps = [LocalMap(ctx, s["init"]) for s in seqs]
+    maps = [LocalMap(c, s["init"]) for c, s in zip(ctxs, seqs)]
     create_ms = (time.perf_counter() - t0) * 1e3
     # the keyframes below are uploaded (synchronously) before any step: step t+1's match and append
     # may run under step t's solve (lorb_map_set_overlap's requirement; tests/test_gpu_map.py checks
@@ -223,17 +227,27 @@ def workload_c4(ctx, args, rank):
         m.set_overlap(True)
     fp = A.make_frame_params(synth.frame_params())
     # the keyframe stream, resident in HBM before the timed region
-    kfs = [[(k["pose"], k["Tcw"], len(k["x"]), ctx.to_device(A.u8(k["desc"])), ctx.to_device(A.f32(k["x"])),
-             ctx.to_device(A.f32(k["y"])), ctx.to_device(A.f32(k["depth"]))) for k in s["steps"]] for s in seqs]
+    kfs = [[(k["pose"], k["Tcw"], len(k["x"]), c.to_device(A.u8(k["desc"])), c.to_device(A.f32(k["x"])),
+             c.to_device(A.f32(k["y"])), c.to_device(A.f32(k["depth"]))) for k in s["steps"]] for c, s in zip(ctxs, seqs)]
     pos = [0]
+
+    # several windows: one host thread per window (each window's step blocks on its own plan
+    # readback; ctypes releases the GIL inside the call), so the windows' host phases overlap
+    pool = concurrent.futures.ThreadPoolExecutor(max_workers=W) if W > 1 else None
 
     def step():
         i = pos[0]
         if i >= n_kf_needed:
             raise RuntimeError("bench keyframe stream exhausted")
-        for m, ks in zip(maps, kfs):
+
+        def one(m, ks):
             pose, Tcw, n, dd, dx, dy, dz = ks[i]
             m.step_dev(fp, pose, Tcw, n, dd, dx, dy, dz, opt)
+        if pool is None:
+            one(maps[0], kfs[0])
+        else:
+            for f in [pool.submit(one, m, ks) for m, ks in zip(maps, kfs)]:
+                f.result()
         pos[0] = i + 1
 
     def check():
@@ -262,8 +276,16 @@ def workload_c4(ctx, args, rank):
             for k in ks:
                 for a in k[3:]:
                     a.free()
+        for c in ctxs[1:]:
+            c.close()
+        if pool is not None:
+            pool.shutdown()
 
-    return dict(step=step, check=check, ba_iters=10.0 * W, matches=float(W * nq), pairs=float(W) * nq * n_pts,
+    def sync():
+        for c in ctxs:
+            c.sync()
+
+    return dict(step=step, check=check, sync=sync, ba_iters=10.0 * W, matches=float(W * nq), pairs=float(W) * nq * n_pts,
                 plan_ms=0.0, create_ms=create_ms, cleanup=cleanup, kspec=kspec, traffic_key="c4_chain",
                 config={"workload": "c4_local_mapping_step_chained", "windows_per_gpu": W, "kf": F,
                         "fixed_kf": maps[0].F, "points": n_pts, "observations": n_obs, "lm_iterations": 10,
@@ -275,7 +297,8 @@ def workload_c4(ctx, args, rank):
 def sub_c4x8(ctx, D, args):
     """A filled GPU: the C4 chained step on 8 independent HBM-resident windows per
     GPU, stepped together (each step issues one keyframe to every window; north_star shards
-    independent windows).  One window leaves most CUs idle during its Cholesky; this line shows
+    independent windows).  Each window has its own context (stream) and host thread, so the windows'
+    steps run concurrently.  One window leaves most CUs idle during its Cholesky; this line shows
     what one MI355X sustains with 8 in flight.  It does not replace the headline (one window)."""
     import copy
     a = copy.copy(args)
@@ -776,15 +799,16 @@ def roofline_iteration(win, n_poses, ms_per_iteration, traffic_key):
 
 def timed(ctx, D, wl, steps, warmup):
     """W untimed steps, then exactly K steps bracketed by barrier + device sync; max over ranks."""
+    sync = wl.get("sync", ctx.sync)  # every stream the workload runs on
     for _ in range(warmup):
         wl["step"]()
-    ctx.sync()
+    sync()
     D.barrier()
-    ctx.sync()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         wl["step"]()
-    ctx.sync()
+    sync()
     t1 = time.perf_counter()
     D.barrier()
     return D.reduce(t1 - t0, "MAX")
@@ -800,7 +824,7 @@ def profile_pass(ctx, wl, steps):
     n = max(3, min(steps, 10))
     for _ in range(n):
         wl["step"]()
-    ctx.sync()
+    wl.get("sync", ctx.sync)()
     kt = {k: v for k, v in kernel_times(ctx, range(8)).items() if v[1] > 0}
     L.lorb_kernel_timing_enable(ctx.handle, 0)
     return kt, n
