@@ -3338,13 +3338,16 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
 // MODE 1: the band with D^2 on the diagonal (rank 0) and the rhs (V - R) sc (k_ba_schur<false>'s
 //         result, for the Cholesky without a head);
 // MODE 2: the fused iteration: band without D^2 (k_ba_chol_2s<true> adds it), rhs, U diag and V.
-template <int MODE>
-__global__ __launch_bounds__(256) void k_ba_red(BaDev d, LMOpt o) {
-  constexpr int kRc = 4;  // groups per thread per chunk: 1024 groups' windows requested at once
-  __shared__ int s_cand[256 * kRc];
-  __shared__ int s_a[256 * kRc];
-  __shared__ int s_wc[kRc][4];
-  __shared__ double s_acc[256];
+// RT threads per block (256 or 1024: red_threads() picks per plan -- 1024 when a block has many
+// candidate groups, or the grid leaves CUs idle; 256 when many blocks share the GPU)
+template <int MODE, int RT>
+__global__ __launch_bounds__(RT) void k_ba_red(BaDev d, LMOpt o) {
+  constexpr int kRt = RT, kRw = kRt / 64;
+  constexpr int kRc = 1024 / kRt;  // groups per thread per chunk: 1024 groups' windows requested at once
+  __shared__ int s_cand[kRt * kRc];
+  __shared__ int s_a[kRt * kRc];
+  __shared__ int s_wc[kRc][kRw];
+  __shared__ double s_acc[kRt];
   __shared__ double s_tot[54];
   if ((int)blockIdx.x >= d.live[1]) return;
   const BlockPair bp = d.bp[blockIdx.x];
@@ -3365,14 +3368,14 @@ __global__ __launch_bounds__(256) void k_ba_red(BaDev d, LMOpt o) {
   const int h = bp.ch - W.pose_base, l = bp.cl - W.pose_base, dd = h - l;
   // entries: [0, 36) the block, [36, 54) the camera terms (U diag, V, R); MODE 0: U diag, V only
   const int e0 = MODE == 0 ? 36 : 0, ne = MODE == 0 ? 12 : (diag ? 54 : 36);
-  const int nsub = 256 / ne, e = t % ne, sub = t / ne;
+  const int nsub = kRt / ne, e = t % ne, sub = t / ne;
   double acc = 0.0;
   const int g0 = W.pblk_base, ng = W.n_pblk;
-  for (int c0 = 0; c0 < ng; c0 += 256 * kRc) {
+  for (int c0 = 0; c0 < ng; c0 += kRt * kRc) {
     int2 gs[kRc];
 #pragma unroll
     for (int u = 0; u < kRc; ++u) {
-      const int gi = c0 + 256 * u + t;
+      const int gi = c0 + kRt * u + t;
       gs[u] = gi < ng ? d.gspan[g0 + gi] : make_int2(0, 0);
     }
     unsigned long long bal[kRc];
@@ -3388,19 +3391,19 @@ __global__ __launch_bounds__(256) void k_ba_red(BaDev d, LMOpt o) {
 #pragma unroll
     for (int u = 0; u < kRc; ++u)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) nc += s_wc[u][k];
+      for (int k = 0; k < kRw; ++k) nc += s_wc[u][k];
 #pragma unroll
     for (int u = 0; u < kRc; ++u) {
       int pu = pre;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) pu += k < wv ? s_wc[u][k] : 0;
+      for (int k = 0; k < kRw; ++k) pu += k < wv ? s_wc[u][k] : 0;
       if ((bal[u] >> lane) & 1ull) {
         const int j = pu + __popcll(bal[u] & ((1ull << lane) - 1ull));
-        s_cand[j] = c0 + 256 * u + t;
+        s_cand[j] = c0 + kRt * u + t;
         s_a[j] = h - gs[u].x;
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) pre += s_wc[u][k];
+      for (int k = 0; k < kRw; ++k) pre += s_wc[u][k];
     }
     __syncthreads();
     if (sub < nsub) {
@@ -3411,25 +3414,25 @@ __global__ __launch_bounds__(256) void k_ba_red(BaDev d, LMOpt o) {
         return ee < 36 ? gp + 36 * pm_slot(a, dd, W.bwc) + ee : gp + W.part_cam + 18 * a + (ee - 36);
       };
       // kRu candidates' loads in flight before they are added (in candidate order: the same sum)
+      // (a short last batch adds exact zeros for its missing candidates: the same sum)
       constexpr int kRu = 8;
-      int j = sub;
-      for (; j + (kRu - 1) * nsub < nc; j += kRu * nsub) {
+      for (int j = sub; j < nc; j += kRu * nsub) {
         double v[kRu];
 #pragma unroll
-        for (int u = 0; u < kRu; ++u) v[u] = *at(j + u * nsub);
+        for (int u = 0; u < kRu; ++u) v[u] = j + u * nsub < nc ? *at(j + u * nsub) : 0.0;
 #pragma unroll
         for (int u = 0; u < kRu; ++u) acc += v[u];
       }
-      for (; j < nc; j += nsub) acc += *at(j);
     }
     __syncthreads();
   }
   if (sub < nsub) s_acc[t] = acc;
   __syncthreads();
-  if (t < ne) {
-    double v = s_acc[t];
-    for (int s = 1; s < nsub; ++s) v += s_acc[t + s * ne];
-    s_tot[t] = v;
+  if (t < ne) {  // the subsets' sums: four interleaved partial sums, then their pairs
+    double v4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+    for (int s = 0; s < nsub; ++s) v4[s & 3] += s_acc[t + s * ne];
+    s_tot[t] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
   }
   __syncthreads();
   const int c = bp.ch;
@@ -3901,6 +3904,7 @@ struct lorb_ba_plan {
   // point-group / block-pair kernels at capacity) replays the graph without a new capture
   struct GraphKey {
     int kind = -1, lds = 0, memset_env = 0, env_total = 0, grid_pblk = 0, grid_bp = 0, pt_launch = 0, x2_n = 0;
+    int red_wide = 0;
     bool operator==(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) == 0; }
   } gkey;
   int grid_pblk = 0, grid_bp = 0;  // launch grids of the point-group and block-pair kernels
@@ -4426,6 +4430,20 @@ size_t x2_count(const lorb_ba_plan* P) {
   return P->devb ? P->x2_off + (size_t)P->env_total : (size_t)P->env_total + P->n_total + P->W;
 }
 
+// k_ba_red's width: 1024 threads when a block has many candidate groups (a window's groups x the
+// cameras a group spans / the window's cameras >= 128: the shared window) or the grid leaves CUs
+// idle (<= 256 blocks: C3); 256 when many blocks share the GPU (C4, several windows per plan)
+int red_wide(const lorb_ba_plan* P) {
+  const double W = std::max(P->W, 1), cams = std::max((double)P->Ctot / W, 1.0);
+  const double cand = (double)P->n_pblk / W * ((P->max_bw + 1) / 6.0) / cams;
+  return P->grid_bp <= 256 || cand >= 128.0;
+}
+template <int MODE>
+void launch_red(const lorb_ba_plan* P, hipStream_t s, const BaDev& d, const LMOpt& o) {
+  if (red_wide(P)) hipLaunchKernelGGL((k_ba_red<MODE, 1024>), dim3(P->grid_bp), dim3(1024), 0, s, d, o);
+  else hipLaunchKernelGGL((k_ba_red<MODE, 256>), dim3(P->grid_bp), dim3(256), 0, s, d, o);
+}
+
 lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
   lorb_ba_plan::GraphKey k;
   k.kind = chol_kind_of(P);
@@ -4434,6 +4452,7 @@ lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
   k.env_total = k.memset_env ? P->env_total : 0;
   k.grid_pblk = P->grid_pblk; k.grid_bp = P->grid_bp; k.pt_launch = P->pt_launch;
   k.x2_n = P->comm ? (int)x2_count(P) : 0;  // the captured all-reduce's count
+  k.red_wide = red_wide(P);
   return k;
 }
 
@@ -4448,7 +4467,7 @@ int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
     }
     if (P->grid_bp) {
       lorb::KernelTimer kt(P->ctx, LORB_K_BA_SCHUR);
-      hipLaunchKernelGGL(k_ba_red<0>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
+      launch_red<0>(P, s, d, o);
     }
   } else {
     if (P->grid_pblk) {
@@ -4499,8 +4518,8 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
   if (P->grid_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
     if (d.pm) {
-      if (fused) hipLaunchKernelGGL(k_ba_red<2>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
-      else hipLaunchKernelGGL(k_ba_red<1>, dim3(P->grid_bp), dim3(256), 0, s, d, o);
+      if (fused) launch_red<2>(P, s, d, o);
+      else launch_red<1>(P, s, d, o);
     } else if (fused) {
       hipLaunchKernelGGL(k_ba_schur<true>, dim3(P->grid_bp + P->Ctot), dim3(256), 0, s, d, o, (int)P->grid_bp);
     } else {
