@@ -5865,8 +5865,9 @@ int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n) {
   int reordered = 0;
   for (const auto& m : plan->cam_map)
     for (size_t c = 0; c < m.size(); ++c) reordered |= m[c] != (int)c;
-  const int32_t v[8] = {bw, plan->chol_kind, plan->n_bp, plan->n_pblk, plan->K, plan->Ptot, plan->Ctot, reordered};
-  for (int i = 0; i < n && i < 8; ++i) info[i] = v[i];
+  const int32_t v[10] = {bw, plan->chol_kind, plan->n_bp, plan->n_pblk, plan->K, plan->Ptot, plan->Ctot, reordered,
+                         plan->dev.pm, plan->dev.pm ? (red_wide(plan) ? 1024 : 256) : 0};
+  for (int i = 0; i < n && i < 10; ++i) info[i] = v[i];
   return LORB_OK;
 }
 

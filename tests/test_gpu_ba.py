@@ -109,6 +109,30 @@ def test_local_ba_point_order_without_camera_locality(ctx, n_kf, obs_lens):
     assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
 
 
+@pytest.mark.parametrize("n_kf,n_pts,n_fixed,pm", [(70, 3000, 2, 0), (20, 4000, 2, 1), (50, 10000, 5, 1)])
+def test_local_ba_schur_path_by_window(ctx, n_kf, n_pts, n_fixed, pm):
+    """The Schur path each window shape takes, and its parity: more than 64 cameras (the point-major
+    kernels' camera masks are 64 bits) runs the pair-major k_ba_lin / k_ba_schur / k_ba_backsub; C3 /
+    C4 shapes run the point-major path, C3 with 1024-thread partial reductions (<= 256 blocks), C4
+    with 256 (372 blocks)."""
+    from lorb_slam_amd.runtime import BAPlan
+    w = synth.ba_window(seed=29, n_kf=n_kf, n_pts=n_pts, n_fixed=n_fixed, fixed_obs_per_kf=100)
+    opt = A.LMOptions.default(max_num_iterations=6, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    plan = BAPlan(ctx, [w])
+    try:
+        info = plan.info()
+        assert info["point_major"] == pm, info
+        if pm:
+            assert info["red_threads"] == (1024 if info["blocks"] <= 256 else 256), info
+    finally:
+        plan.close()
+    Pg, Xg, sg = ctx.ba_local([w], opt)
+    Po, Xo, so = O.ba_local([w], opt)
+    lm_match(sg[0], so[0])
+    assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
+    assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
+
+
 def test_local_ba_batched_ragged_windows(ctx):
     wins = [synth.ba_window(seed=10 + i, n_kf=k, n_pts=p, n_fixed=nf, fixed_obs_per_kf=50)
             for i, (k, p, nf) in enumerate([(3, 100, 1), (8, 700, 2), (12, 900, 3), (5, 257, 1)])]
