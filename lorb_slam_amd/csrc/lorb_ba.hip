@@ -2933,15 +2933,32 @@ __device__ __forceinline__ void lm_end_run(const BaDev& d, const LMOpt& o, int w
   double mccs = 0.0, ncost = 0.0, sn2 = 0.0;
   double xc[6] = {0, 0, 0, 0, 0, 0};  // candidate pose of camera pose_base + lane (kept for its jet)
   if (valid) {
-    if (!SH) group_partials<3, 4, 5, false>(d.part, W.pblk_base, W.n_pblk, lane, mccs, ncost, sn2);
     const int cur = S.cur;
-    for (int c = W.pose_base + lane; c < W.pose_base + W.n_poses; c += 64) {
+    // the first 64 cameras' poses are requested before the group partials (one round trip for both;
+    // the partials' loop would otherwise keep them behind it)
+    const int c0 = W.pose_base + lane;
+    const bool has0 = lane < W.n_poses;
+    double x0[6], xn0[6];
+    bool act0 = false;
+    if (has0) {
+      act0 = d.cam_active[c0];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) { x0[k] = d.x_pose[cur][6 * c0 + k]; xn0[k] = d.x_pose[cur ^ 1][6 * c0 + k]; }
+    }
+    if (!SH) group_partials<3, 4, 5, false>(d.part, W.pblk_base, W.n_pblk, lane, mccs, ncost, sn2);
+    if (has0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        if (act0) sn2 += (x0[k] - xn0[k]) * (x0[k] - xn0[k]);  // (the same order as the loop below)
+        xc[k] = xn0[k];
+      }
+    }
+    for (int c = c0 + 64; c < W.pose_base + W.n_poses; c += 64) {
       const bool active = d.cam_active[c];
       for (int k = 0; k < 6; ++k) {
         const double x = d.x_pose[cur][6 * c + k];
         const double xn = d.x_pose[cur ^ 1][6 * c + k];  // written by k_ba_chol
         if (active) sn2 += (x - xn) * (x - xn);
-        if (c == W.pose_base + lane) xc[k] = xn;
       }
     }
     mccs = wave_sum(mccs); ncost = wave_sum(ncost); sn2 = wave_sum(sn2);
