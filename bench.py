@@ -322,7 +322,40 @@ def sub_c4x8(ctx, D, args):
            if rwin is not None else None,
            "check": {"windows": chk["windows"][:2], "keyframes_stepped": chk["keyframes_stepped"]}}
     wl["cleanup"]()
+    out["one_plan"] = c4x8_one_plan(ctx, D, a.steps)
     return out
+
+
+def c4x8_one_plan(ctx, D, steps):
+    """The LM solve alone on 8 independent C4 windows in ONE plan (every point-group, block and
+    Cholesky kernel launched once for all 8 windows; tests/test_gpu_ba.py
+    test_local_ba_eight_c4_windows_independent checks it bit for bit against 8 one-window plans):
+    10 LM iterations per solve, the plan built once outside the timed solves."""
+    from lorb_slam_amd import _abi as A
+    from lorb_slam_amd import synth
+    from lorb_slam_amd.runtime import BAPlan
+    wins = [synth.ba_window(seed=40 + i, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400) for i in range(8)]
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    plan = BAPlan(ctx, wins)
+    try:
+        for _ in range(2):
+            plan.solve(opt)
+        ctx.sync()
+        D.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            plan.solve(opt)
+        ctx.sync()
+        el = D.reduce(time.perf_counter() - t0, "MAX")
+        s = plan.read()[2]
+    finally:
+        plan.close()
+    ms = el / steps * 1e3
+    return {"workload": "c4_local_ba_x8_one_plan", "value": D.reduce(80.0 * steps, "SUM") / el,
+            "unit": "BA iterations/s", "solves": steps, "ms_per_solve": ms,
+            "roofline_iteration": roofline_iteration(wins[0], 50, ms / 80.0, "c4x8"),
+            "check": {"final_cost_w0": s[0]["final_cost"], "iterations_w0": s[0]["iterations"]}}
 
 
 def sub_c4x8_run(ctx, D, args):
