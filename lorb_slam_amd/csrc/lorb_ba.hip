@@ -8,11 +8,17 @@
 //   * every LM scalar decision (accept/reject, radius, tolerances) is made ON THE DEVICE by a
 //     one-workgroup-per-window kernel, so an LM iteration is a fixed sequence of launches with
 //     no host round trip; it is captured once into a hipGraph and replayed.
-//   * per-observation linearisation, per-point Schur elimination (3x3 inverse, W / Y tiles),
-//     one wavefront per non-zero (camera, camera) block of S accumulating a CSR pair list in a
-//     fixed order (deterministic, no FP64 atomics), an envelope (profile) Cholesky of S per
-//     window in LDS, and per-point back-substitution.
-//   * all reductions are fixed-order trees (block partials reduced in index order).
+//   * point-major Schur (windows of <= 64 cameras, the default): one workgroup per point group
+//     linearises its observations, eliminates its points and forms its camera-block partials on
+//     chip (k_ba_ls); one workgroup per band block sums the groups' partials in group order
+//     (k_ba_red); the back-substitution re-evaluates the linearisation (k_ba_bs2).  Nothing is
+//     stored per observation.  Wider windows (and LORB_PM=0) take the pair-major kernels:
+//     per-observation tiles (k_ba_lin), one workgroup per (camera, camera) block over a CSR pair
+//     list (k_ba_schur), per-point back-substitution (k_ba_backsub).
+//   * the reduced camera system is banded (cameras in reverse Cuthill-McKee order): a two-sided
+//     band Cholesky with the LM head inside (k_ba_chol_2s), or the wider variants.
+//   * all reductions are fixed-order trees (block partials reduced in index order): deterministic,
+//     no FP64 atomics.
 //
 // FP64 contraction: the BA arithmetic may fuse multiply-adds (v_fma_f64; its parity bar is 1e-5
 // relative, not bit-exactness -- VERDICT r04 item 3).  The Makefile's global -ffp-contract=off stays
