@@ -512,7 +512,7 @@ int lorb_ctx_ba_solver(lorb_ctx* ctx, lorb_ba_solver** out);
  * blocks, [3] point groups, [4] observations, [5] points, [6] cameras, [7] 1 if some window's
  * cameras were reordered (reverse Cuthill-McKee on the covisibility graph; outputs keep the
  * caller's order), [8] 1 if the plan runs the point-major Schur path (every window <= 64 cameras;
- * else the pair-major kernels), [9] its partial-reduction width (threads per block, 0: pair-major) */
+ * else the pair-major kernels), [9] its partial-reduction width (threads per block: 256, 512 or 1024; 0: pair-major) */
 int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n);
 /* diagnostics: Cholesky phase stamps of window 0 (non-zero only in LORB_CHOL_STAMPS builds) */
 int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8);

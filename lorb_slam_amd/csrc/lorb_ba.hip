@@ -3370,7 +3370,7 @@ __global__ __launch_bounds__(RT) void k_ba_red(BaDev d, LMOpt o) {
   __shared__ int s_cand[kRt * kRc];
   __shared__ int s_a[kRt * kRc];
   __shared__ int s_wc[kRc][kRw];
-  __shared__ double s_acc[kRt];
+  __shared__ double s_acc[1024];
   __shared__ double s_tot[54];
   if ((int)blockIdx.x >= d.live[1]) return;
   const BlockPair bp = d.bp[blockIdx.x];
@@ -3391,8 +3391,17 @@ __global__ __launch_bounds__(RT) void k_ba_red(BaDev d, LMOpt o) {
   const int h = bp.ch - W.pose_base, l = bp.cl - W.pose_base, dd = h - l;
   // entries: [0, 36) the block, [36, 54) the camera terms (U diag, V, R); MODE 0: U diag, V only
   const int e0 = MODE == 0 ? 36 : 0, ne = MODE == 0 ? 12 : (diag ? 54 : 36);
+  // The sum's shape does not depend on the width: candidate j of a chunk belongs to subset j mod NS
+  // (NS = 1024 / ne, the subsets a 1024-thread block runs one per thread), each subset sums its
+  // candidates in order, and the subsets are combined in a fixed tree -- so the 256-, 512- and
+  // 1024-thread kernels give the same bits (a window solved alone or batched with others takes the
+  // same band).  A narrower block runs up to kSp subsets per thread.
+  const int NS = 1024 / ne;
   const int nsub = kRt / ne, e = t % ne, sub = t / ne;
-  double acc = 0.0;
+  constexpr int kSp = RT >= 1024 ? 1 : RT >= 512 ? 3 : 5;  // ceil(NS / nsub) for ne in {12, 36, 54}
+  double acc[kSp];
+#pragma unroll
+  for (int q = 0; q < kSp; ++q) acc[q] = 0.0;
   const int g0 = W.pblk_base, ng = W.n_pblk;
   for (int c0 = 0; c0 < ng; c0 += kRt * kRc) {
     int2 gs[kRc];
@@ -3438,23 +3447,43 @@ __global__ __launch_bounds__(RT) void k_ba_red(BaDev d, LMOpt o) {
       };
       // kRu candidates' loads in flight before they are added (in candidate order: the same sum)
       // (a short last batch adds exact zeros for its missing candidates: the same sum)
-      constexpr int kRu = 8;
-      for (int j = sub; j < nc; j += kRu * nsub) {
-        double v[kRu];
+      // the thread's subsets advance together, kRu candidates each per round (kSp x kRu loads in
+      // flight); every subset still adds its candidates in order
+      constexpr int kRu = RT >= 1024 ? 8 : RT >= 512 ? 4 : 2;
+      for (int b0 = 0;; b0 += kRu) {
+        double v[kSp][kRu];
+        bool more = false;
 #pragma unroll
-        for (int u = 0; u < kRu; ++u) v[u] = j + u * nsub < nc ? *at(j + u * nsub) : 0.0;
+        for (int q = 0; q < kSp; ++q) {
+          const int s0 = sub + q * nsub;
 #pragma unroll
-        for (int u = 0; u < kRu; ++u) acc += v[u];
+          for (int u = 0; u < kRu; ++u) {
+            const int j = s0 + (b0 + u) * NS;
+            v[q][u] = s0 < NS && j < nc ? *at(j) : 0.0;
+          }
+          more |= s0 < NS && s0 + (b0 + kRu) * NS < nc;
+        }
+#pragma unroll
+        for (int q = 0; q < kSp; ++q)
+#pragma unroll
+          for (int u = 0; u < kRu; ++u) acc[q] += v[q][u];
+        if (!more) break;
       }
     }
     __syncthreads();
   }
-  if (sub < nsub) s_acc[t] = acc;
+  if (sub < nsub) {
+#pragma unroll
+    for (int q = 0; q < kSp; ++q) {
+      const int s0 = sub + q * nsub;
+      if (s0 < NS) s_acc[e + s0 * ne] = acc[q];
+    }
+  }
   __syncthreads();
   if (t < ne) {  // the subsets' sums: four interleaved partial sums, then their pairs
     double v4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll 4
-    for (int s = 0; s < nsub; ++s) v4[s & 3] += s_acc[t + s * ne];
+    for (int s = 0; s < NS; ++s) v4[s & 3] += s_acc[t + s * ne];
     s_tot[t] = (v4[0] + v4[1]) + (v4[2] + v4[3]);
   }
   __syncthreads();
@@ -4455,15 +4484,19 @@ size_t x2_count(const lorb_ba_plan* P) {
 
 // k_ba_red's width: 1024 threads when a block has many candidate groups (a window's groups x the
 // cameras a group spans / the window's cameras >= 128: the shared window) or the grid leaves CUs
-// idle (<= 256 blocks: C3); 256 when many blocks share the GPU (C4, several windows per plan)
-int red_wide(const lorb_ba_plan* P) {
+// idle (<= 256 blocks: C3); 512 up to 1024 blocks (C4's 372: 9.8 -> 7.8 us); 256 when many blocks
+// share the GPU (several C4 windows per plan)
+int red_threads(const lorb_ba_plan* P) {
   const double W = std::max(P->W, 1), cams = std::max((double)P->Ctot / W, 1.0);
   const double cand = (double)P->n_pblk / W * ((P->max_bw + 1) / 6.0) / cams;
-  return P->grid_bp <= 256 || cand >= 128.0;
+  if (P->grid_bp <= 256 || cand >= 128.0) return 1024;
+  return P->grid_bp <= 1024 ? 512 : 256;
 }
 template <int MODE>
 void launch_red(const lorb_ba_plan* P, hipStream_t s, const BaDev& d, const LMOpt& o) {
-  if (red_wide(P)) hipLaunchKernelGGL((k_ba_red<MODE, 1024>), dim3(P->grid_bp), dim3(1024), 0, s, d, o);
+  const int rt = red_threads(P);
+  if (rt == 1024) hipLaunchKernelGGL((k_ba_red<MODE, 1024>), dim3(P->grid_bp), dim3(1024), 0, s, d, o);
+  else if (rt == 512) hipLaunchKernelGGL((k_ba_red<MODE, 512>), dim3(P->grid_bp), dim3(512), 0, s, d, o);
   else hipLaunchKernelGGL((k_ba_red<MODE, 256>), dim3(P->grid_bp), dim3(256), 0, s, d, o);
 }
 
@@ -4475,7 +4508,7 @@ lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
   k.env_total = k.memset_env ? P->env_total : 0;
   k.grid_pblk = P->grid_pblk; k.grid_bp = P->grid_bp; k.pt_launch = P->pt_launch;
   k.x2_n = P->comm ? (int)x2_count(P) : 0;  // the captured all-reduce's count
-  k.red_wide = red_wide(P);
+  k.red_wide = red_threads(P);
   return k;
 }
 
@@ -5889,7 +5922,7 @@ int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n) {
   for (const auto& m : plan->cam_map)
     for (size_t c = 0; c < m.size(); ++c) reordered |= m[c] != (int)c;
   const int32_t v[10] = {bw, plan->chol_kind, plan->n_bp, plan->n_pblk, plan->K, plan->Ptot, plan->Ctot, reordered,
-                         plan->dev.pm, plan->dev.pm ? (red_wide(plan) ? 1024 : 256) : 0};
+                         plan->dev.pm, plan->dev.pm ? red_threads(plan) : 0};
   for (int i = 0; i < n && i < 10; ++i) info[i] = v[i];
   return LORB_OK;
 }

@@ -114,7 +114,7 @@ def test_local_ba_schur_path_by_window(ctx, n_kf, n_pts, n_fixed, pm):
     """The Schur path each window shape takes, and its parity: more than 64 cameras (the point-major
     kernels' camera masks are 64 bits) runs the pair-major k_ba_lin / k_ba_schur / k_ba_backsub; C3 /
     C4 shapes run the point-major path, C3 with 1024-thread partial reductions (<= 256 blocks), C4
-    with 256 (372 blocks)."""
+    with 512 (372 blocks)."""
     from lorb_slam_amd.runtime import BAPlan
     w = synth.ba_window(seed=29, n_kf=n_kf, n_pts=n_pts, n_fixed=n_fixed, fixed_obs_per_kf=100)
     opt = A.LMOptions.default(max_num_iterations=6, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
@@ -123,7 +123,7 @@ def test_local_ba_schur_path_by_window(ctx, n_kf, n_pts, n_fixed, pm):
         info = plan.info()
         assert info["point_major"] == pm, info
         if pm:
-            assert info["red_threads"] == (1024 if info["blocks"] <= 256 else 256), info
+            assert info["red_threads"] == (1024 if info["blocks"] <= 256 else 512 if info["blocks"] <= 1024 else 256), info
     finally:
         plan.close()
     Pg, Xg, sg = ctx.ba_local([w], opt)
@@ -236,11 +236,20 @@ def test_local_ba_reference_camera_order(ctx, size):
     assert close(Pg[0], Pt[0][order]) and close(Xg[0], Xt[0])
 
 
-def test_local_ba_eight_c4_windows_independent(ctx):
+@pytest.mark.parametrize("shape", ["c4", "c3"])
+def test_local_ba_eight_c4_windows_independent(ctx, shape):
     """BASELINE config 4 shape on one GPU: 8 C4 windows in one plan.  Size-independent property:
-    batching never couples windows -- each window's result is bit-identical to its solo solve."""
-    wins = [synth.ba_window(seed=40 + i, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400) for i in range(8)]
+    batching never couples windows -- each window's result is bit-identical to its solo solve.  The
+    C3 case also crosses reduction widths (solo: 1024-thread k_ba_red, batched: 256), whose group
+    sums use the same fixed subsets and order."""
+    kw = dict(n_kf=50, n_pts=10000, n_fixed=5) if shape == "c4" else dict(n_kf=20, n_pts=4000, n_fixed=2)
+    wins = [synth.ba_window(seed=40 + i, fixed_obs_per_kf=400, **kw) for i in range(8)]
     opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    if shape == "c3":
+        from lorb_slam_amd.runtime import BAPlan
+        solo, batch = BAPlan(ctx, wins[:1]), BAPlan(ctx, wins)
+        assert solo.info()["red_threads"] == 1024 and batch.info()["red_threads"] < 1024
+        solo.close(); batch.close()
     Pb, Xb, sb = ctx.ba_local(wins, opt)
     for i in (0, 5):
         Ps, Xs, ss = ctx.ba_local([wins[i]], opt)
