@@ -19,17 +19,19 @@ def close(a, b, rtol=RTOL):
     return np.all(np.abs(a - b) <= rtol * np.maximum(np.abs(b), 1.0))
 
 
-def lm_match(g, o, cost_rtol=1e-8):
-    """The LM summaries agree to the north_star contract: same iteration count, final cost within
-    cost_rtol relative.  The count of ACCEPTED steps may differ only when a step's accept test sits
-    at round-off level, i.e. when the final costs still agree to cost_rtol (then the disagreement is
-    reported, not failed: the solution itself is checked to 1e-5 by the caller)."""
+def lm_match(g, o, cost_rtol=1e-8, roundoff_ok=False):
+    """The LM summaries agree to the north_star contract: same iteration count, same count of
+    accepted steps, final cost within cost_rtol relative.  roundoff_ok (a solve that runs into
+    machine-precision convergence, where a late step's accept test compares cost changes at
+    round-off level): the accepted counts may differ by one step when the final costs agree to
+    1e-12 (reported; the solution itself is checked to 1e-5 by the caller)."""
     assert g["iterations"] == o["iterations"], (g, o)
     assert abs(g["final_cost"] - o["final_cost"]) <= cost_rtol * abs(o["final_cost"]), (g, o)
     if g["successful_steps"] != o["successful_steps"]:
+        rel = abs(g["final_cost"] - o["final_cost"]) / abs(o["final_cost"])
+        assert roundoff_ok and abs(g["successful_steps"] - o["successful_steps"]) <= 1 and rel <= 1e-12, (g, o)
         print(f"round-off accept/reject difference: gpu {g['successful_steps']} vs oracle "
-              f"{o['successful_steps']} accepted steps, final cost rel diff "
-              f"{abs(g['final_cost'] - o['final_cost']) / abs(o['final_cost']):.2e}")
+              f"{o['successful_steps']} accepted steps, final cost rel diff {rel:.2e}")
 
 
 @pytest.mark.parametrize("quirk", [True, False])

@@ -18,10 +18,10 @@ OPT10 = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradi
                             parameter_tolerance=0.0)
 
 
-def check(solver, w, opt):
+def check(solver, w, opt, roundoff_ok=False):
     Pg, Xg, sg = solver.solve(w, opt)
     Po, Xo, so = O.ba_local([w], opt)
-    lm_match(sg, so[0])
+    lm_match(sg, so[0], roundoff_ok=roundoff_ok)
     assert close(Pg, Po[0]), np.abs(Pg - Po[0]).max()
     assert close(Xg, Xo[0]), np.abs(Xg - Xo[0]).max()
     return Pg, Xg, sg
@@ -30,14 +30,17 @@ def check(solver, w, opt):
 def test_solver_c4_reference_order_twice(ctx):
     """C4 window in the reference's camera order, solved twice (the second call with the first
     call's float write-back as its start, as the drop-in's next call sees it): one plan creation,
-    band 47 after the RCM relabelling, no host-built fallback."""
+    band 47 after the RCM relabelling, no host-built fallback.  At tolerance 0 this window's 10th
+    iteration compares cost changes at round-off level (the relative change is ~1e-14), so that
+    one accepted step may go either way (final costs agree to 1e-14); every other test asserts
+    the accepted-step count exactly."""
     w0 = synth.ba_window(seed=4, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400)
     w, _ = synth.reference_window_order(w0)
     s = BASolver(ctx)
     try:
-        P1, X1, _ = check(s, w, OPT10)
+        P1, X1, _ = check(s, w, OPT10, roundoff_ok=True)
         w2 = dict(w, pose_init=P1.astype(np.float32), point_init=X1.astype(np.float32))
-        check(s, w2, OPT10)
+        check(s, w2, OPT10, roundoff_ok=True)
         info = s.info()
         assert info["plan_creations"] == 1 and info["host_plan_fallback"] == 0, info
         assert info["band"] == 47 and info["cholesky"] == 2 and info["reordered"] == 1, info
