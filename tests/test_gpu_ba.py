@@ -43,6 +43,7 @@ def test_pose_only_default_options(ctx, quirk):
     assert np.allclose(Tg, To, rtol=1e-5, atol=1e-6)
     for a, b in zip(sg, so):
         assert a["termination"] == b["termination"] and a["iterations"] == b["iterations"]
+        assert a["successful_steps"] == b["successful_steps"], (a, b)
         assert abs(a["final_cost"] - b["final_cost"]) <= 1e-6 * b["final_cost"]
 
 
