@@ -408,6 +408,26 @@ typedef struct lorb_ba_summary {
   double final_cost;
 } lorb_ba_summary;
 
+/* Per-iteration record of a local-BA solve (diagnostics / parity): one record per
+ * LM iteration that computed a step, as Ceres' IterationSummary holds it (trust_region_minimizer.cc:
+ * cost, model cost change, the candidate's cost, the radius the step was computed with, |step|).
+ * The first LORB_LM_TRACE_CAP iterations of every window are recorded. */
+#define LORB_LM_STEP_INVALID   0   /* linear solve failed / non-positive model decrease */
+#define LORB_LM_STEP_ACCEPTED  1
+#define LORB_LM_STEP_REJECTED  2   /* relative decrease <= min_relative_decrease */
+#define LORB_LM_STEP_PARAM_TOL 3   /* solve ends: |step| <= parameter_tolerance * (|x| + ptol) */
+#define LORB_LM_STEP_FUNC_TOL  4   /* solve ends: |cost change| <= function_tolerance * cost */
+#define LORB_LM_TRACE_CAP 64
+typedef struct lorb_lm_iteration {
+  int32_t iteration;           /* 1-based */
+  int32_t outcome;             /* LORB_LM_STEP_* */
+  double cost;                 /* cost at the current point */
+  double model_cost_change;    /* -(J step)^T (r + J step / 2), the linear model's decrease */
+  double new_cost;             /* cost at the candidate x + step (valid steps) */
+  double radius;               /* trust-region radius the step was computed with */
+  double step_norm;            /* |x_candidate - x| (valid steps) */
+} lorb_lm_iteration;
+
 /* (a12) BA::ProjectPoseOptimization: pose-only, one PoseCost per matched map point.
  * The PoseCost quirk (v projected with fx, src/bundle_adjust.cpp:51) is reproduced by passing
  * fy_eff = fx; pass the real fy to get the "fixed" projection.  Batched over frames:
@@ -502,6 +522,9 @@ int lorb_ba_solver_solve(lorb_ba_solver* solver, const lorb_ba_window* window, c
 /* first n of: [0] resident plans, [1] plan creations so far, [2] 1 if the last call ran on the host-built
  * plan, [3] its S half band, [4] its Cholesky kernel, [5] 1 if its cameras were reordered (RCM) */
 int lorb_ba_solver_info(lorb_ba_solver* solver, int32_t* info, int32_t n);
+/* the last call's per-iteration records (lorb_ba_plan_trace of the resident plan it ran on; none after a
+ * call that took the host-built plan) */
+int lorb_ba_solver_trace(lorb_ba_solver* solver, lorb_lm_iteration* out, int32_t cap, int32_t* n_out);
 int lorb_ba_solver_destroy(lorb_ba_solver* solver);
 /* The ctx's own solver: created on the first call, destroyed by lorb_destroy(ctx) (so it never
  * outlives its ctx, and a new ctx never inherits it).  Not to be passed to lorb_ba_solver_destroy.
@@ -514,6 +537,9 @@ int lorb_ctx_ba_solver(lorb_ctx* ctx, lorb_ba_solver** out);
  * caller's order), [8] 1 if the plan runs the point-major Schur path (every window <= 64 cameras;
  * else the pair-major kernels), [9] its partial-reduction width (threads per block: 256, 512 or 1024; 0: pair-major) */
 int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n);
+/* the last solve's per-iteration records of window w (at most min(cap, LORB_LM_TRACE_CAP)); *n_out =
+ * records written.  Synchronises. */
+int lorb_ba_plan_trace(lorb_ba_plan* plan, int32_t window, lorb_lm_iteration* out, int32_t cap, int32_t* n_out);
 /* diagnostics: Cholesky phase stamps of window 0 (non-zero only in LORB_CHOL_STAMPS builds) */
 int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8);
 

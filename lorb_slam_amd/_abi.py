@@ -128,6 +128,25 @@ class BASummary(C.Structure):
                 "initial_cost": self.initial_cost, "final_cost": self.final_cost}
 
 
+LM_STEP_NAMES = {0: "invalid", 1: "accepted", 2: "rejected", 3: "parameter_tol", 4: "function_tol"}
+LM_TRACE_CAP = 64
+
+
+class LMIteration(C.Structure):  # lorb_lm_iteration
+    _fields_ = [("iteration", C.c_int32), ("outcome", C.c_int32), ("cost", C.c_double),
+                ("model_cost_change", C.c_double), ("new_cost", C.c_double), ("radius", C.c_double),
+                ("step_norm", C.c_double)]
+
+    def as_dict(self):
+        return {"iteration": self.iteration, "outcome": LM_STEP_NAMES.get(self.outcome, self.outcome),
+                "cost": self.cost, "model_cost_change": self.model_cost_change, "new_cost": self.new_cost,
+                "radius": self.radius, "step_norm": self.step_norm}
+
+
+def trace_list(buf, n):
+    return [buf[i].as_dict() for i in range(n)]
+
+
 class PoseProblemBatch(C.Structure):
     _fields_ = [("n_frames", C.c_int32), ("res_off", i32p), ("intr", f32p), ("pose_init", f32p),
                 ("pts3d", f32p), ("obs2d", f32p)]

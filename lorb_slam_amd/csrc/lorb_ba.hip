@@ -300,6 +300,7 @@ struct BaDev {
   double* gpart;
   int2* gspan;
   int pm;
+  lorb_lm_iteration* trace;  // per window LORB_LM_TRACE_CAP records (lm_decide)
   // [0] point groups, [1] block pairs in use.  Launch grids may be larger (device-built plans
   // launch at capacity so that the captured LM graph survives a rebuild); the extra workgroups exit.
   const int* live;
@@ -2875,12 +2876,23 @@ __global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
   }
 }
 
+// the iteration's record (lorb_lm_iteration; S is the state the step was computed from)
+__device__ __forceinline__ void lm_record(const BaDev& d, int w, const WinState& S, int outcome, double mcc,
+                                          double ncost, double step_norm) {
+  if (S.iter < 1 || S.iter > LORB_LM_TRACE_CAP) return;
+  lorb_lm_iteration r;
+  r.iteration = S.iter; r.outcome = outcome;
+  r.cost = S.cost; r.model_cost_change = mcc; r.new_cost = ncost; r.radius = S.radius; r.step_norm = step_norm;
+  d.trace[(size_t)w * LORB_LM_TRACE_CAP + S.iter - 1] = r;
+}
+
 // K8 decision (lane 0): step validity, tolerances, accept/reject; returns 1 if accepted
 __device__ int lm_decide(BaDev d, const LMOpt& o, int w, WinState S, bool valid, double mccs,
                          double ncost, double sn2) {
   const double model_cost_change = -mccs;
   valid = valid && isfinite(model_cost_change) && isfinite(sn2) && model_cost_change > 0.0;
   if (!valid) {
+    lm_record(d, w, S, LORB_LM_STEP_INVALID, model_cost_change, ncost, sqrt(sn2));
     if (++S.n_invalid >= o.max_invalid) {
       S.done = 1; S.term = LORB_TERM_FAILURE;
     } else {
@@ -2896,13 +2908,17 @@ __device__ int lm_decide(BaDev d, const LMOpt& o, int w, WinState S, bool valid,
   const double new_cost = isfinite(ncost) ? ncost : 1.7976931348623157e308;
   const double step_norm = sqrt(sn2);
   if (step_norm <= o.ptol * (S.x_norm + o.ptol)) {
+    lm_record(d, w, S, LORB_LM_STEP_PARAM_TOL, model_cost_change, new_cost, step_norm);
     S.done = 1; S.term = LORB_TERM_PARAMETER_TOL; d.st[w] = S; return 0;
   }
   const double cost_change = S.cost - new_cost;
   if (fabs(cost_change) <= o.ftol * S.cost) {
+    lm_record(d, w, S, LORB_LM_STEP_FUNC_TOL, model_cost_change, new_cost, step_norm);
     S.done = 1; S.term = LORB_TERM_FUNCTION_TOL; d.st[w] = S; return 0;
   }
   const double rel = cost_change / model_cost_change;
+  lm_record(d, w, S, rel > o.min_rel ? LORB_LM_STEP_ACCEPTED : LORB_LM_STEP_REJECTED, model_cost_change, new_cost,
+            step_norm);
   if (rel > o.min_rel) {
     S.cur ^= 1;
     S.relin = 1;
@@ -4453,6 +4469,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
 #endif
   LORB_TRY(dalloc(P, ((size_t)P->n_total / 16 + nw + 1) * 1024, &d.kco));
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
+  LORB_TRY(dalloc(P, (size_t)nw * LORB_LM_TRACE_CAP, &d.trace));
   d.pm = pm_ok && pm_enabled() ? 1 : 0;
   if (d.pm) {
     LORB_TRY(dalloc(P, (size_t)std::max(part_total, 1ll), &d.gpart));
@@ -5465,6 +5482,7 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
 #endif
   LORB_TRY(dalloc(P, ((size_t)n / 16 + 2) * 1024, &d.kco));
   LORB_TRY(dalloc(P, (size_t)1, &P->d_state)); d.st = P->d_state;
+  LORB_TRY(dalloc(P, (size_t)LORB_LM_TRACE_CAP, &d.trace));
   d.pm = pm_fits(b.C, b.F) && pm_enabled() ? 1 : 0;
   P->W = 1;
   P->hwin.assign(1, BaWin{});
@@ -5897,6 +5915,24 @@ int lorb_ba_plan_read(lorb_ba_plan* plan, double* const* pose_out, double* const
   if (!plan) return LORB_E_INVALID;
   if (plan->W == 0) return LORB_OK;
   return plan_read(plan, pose_out, point_out, summaries);
+}
+
+int lorb_ba_plan_trace(lorb_ba_plan* plan, int32_t window, lorb_lm_iteration* out, int32_t cap, int32_t* n_out) {
+  if (!plan || !n_out || cap < 0 || (cap > 0 && !out)) return LORB_E_INVALID;
+  *n_out = 0;
+  if (window < 0 || window >= std::max(plan->W, 0)) return plan->W == 0 ? LORB_OK : LORB_E_INVALID;
+  lorb_ctx* ctx = plan->ctx;
+  WinState st;
+  LORB_HIP(ctx, hipMemcpyAsync(&st, plan->d_state + window, sizeof(WinState), hipMemcpyDeviceToHost, ctx->stream));
+  LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const int n = std::min(std::min(st.iter, (int)LORB_LM_TRACE_CAP), (int)cap);
+  if (n > 0) {
+    LORB_HIP(ctx, hipMemcpyAsync(out, plan->dev.trace + (size_t)window * LORB_LM_TRACE_CAP, sizeof(lorb_lm_iteration) * n,
+                                 hipMemcpyDeviceToHost, ctx->stream));
+    LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  *n_out = std::max(n, 0);
+  return LORB_OK;
 }
 
 // diagnostic: copy the Cholesky phase stamps of window 0 (LORB_CHOL_STAMPS builds)

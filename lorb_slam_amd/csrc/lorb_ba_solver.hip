@@ -265,6 +265,13 @@ int lorb_ba_solver_info(lorb_ba_solver* S, int32_t* info, int32_t n) {
   return LORB_OK;
 }
 
+int lorb_ba_solver_trace(lorb_ba_solver* S, lorb_lm_iteration* out, int32_t cap, int32_t* n_out) {
+  if (!S || !n_out) return LORB_E_INVALID;
+  *n_out = 0;
+  if (S->last_fallback || S->last_slot < 0 || !S->slot[S->last_slot].plan) return LORB_OK;
+  return lorb_ba_plan_trace(S->slot[S->last_slot].plan, 0, out, cap, n_out);
+}
+
 int lorb_ba_solver_destroy(lorb_ba_solver* S) {
   delete S;
   return LORB_OK;

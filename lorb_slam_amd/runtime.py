@@ -327,6 +327,13 @@ class BAPlan:
         self.ctx.check(lib().lorb_ba_plan_read(self._p, pp, qp, summ), "lorb_ba_plan_read")
         return poses, pts, [summ[i].as_dict() for i in range(len(wins))]
 
+    def trace(self, w=0):
+        """lorb_ba_plan_trace: the last solve's per-iteration records of window w"""
+        buf, n = (A.LMIteration * A.LM_TRACE_CAP)(), C.c_int32()
+        self.ctx.check(lib().lorb_ba_plan_trace(self._p, C.c_int32(w), buf, C.c_int32(A.LM_TRACE_CAP), C.byref(n)),
+                       "lorb_ba_plan_trace")
+        return A.trace_list(buf, n.value)
+
     def info(self):
         """lorb_ba_plan_info: structure of the plan and the Cholesky kernel of the last solve."""
         v = (C.c_int32 * 10)()
@@ -375,6 +382,13 @@ class BASolver:
     def solve(self, w, opt=None):
         """(poses n_poses x 6, points n_points x 3, summary) of one window dict"""
         return self.solve_prepared(self.prepare(w), opt or A.LMOptions.default())
+
+    def trace(self):
+        """lorb_ba_solver_trace: the last call's per-iteration records"""
+        buf, n = (A.LMIteration * A.LM_TRACE_CAP)(), C.c_int32()
+        self.ctx.check(lib().lorb_ba_solver_trace(self._p, buf, C.c_int32(A.LM_TRACE_CAP), C.byref(n)),
+                       "lorb_ba_solver_trace")
+        return A.trace_list(buf, n.value)
 
     def info(self):
         v = (C.c_int32 * 6)()
@@ -539,6 +553,15 @@ class LocalMap:
         out["summary"] = summ.as_dict()
         out.update(c)
         return out
+
+    def trace(self):
+        """the last step's LM records (lorb_ba_plan_trace of the map's plan)"""
+        p = C.c_void_p()
+        self.ctx.check(lib().lorb_map_plan(self._p, C.byref(p)), "lorb_map_plan")
+        buf, n = (A.LMIteration * A.LM_TRACE_CAP)(), C.c_int32()
+        self.ctx.check(lib().lorb_ba_plan_trace(p, C.c_int32(0), buf, C.c_int32(A.LM_TRACE_CAP), C.byref(n)),
+                       "lorb_ba_plan_trace")
+        return A.trace_list(buf, n.value)
 
     def plan_info(self):
         p = C.c_void_p()

@@ -340,6 +340,20 @@ static int schur_solve(const or_prob* P, const lin_state* L, const double* D, do
   return ok;
 }
 
+/* Per-iteration records (lorb_lm_iteration) of the last lm_solve, when a sink is set: the iteration
+ * summary Ceres' TrustRegionMinimizer keeps (cost, model cost change, candidate cost, radius, |step|). */
+static lorb_lm_iteration* g_trace = NULL;
+static int g_trace_cap = 0, g_trace_n = 0;
+void or_lm_trace(lorb_lm_iteration* buf, int cap) { g_trace = buf; g_trace_cap = buf ? cap : 0; g_trace_n = 0; }
+int or_lm_trace_count(void) { return g_trace_n; }
+static void trace_put(int iter, int outcome, double cost, double mcc, double new_cost, double radius, double step_norm) {
+  if (!g_trace || iter < 1 || iter > g_trace_cap) return;
+  lorb_lm_iteration* r = &g_trace[iter - 1];
+  r->iteration = iter; r->outcome = outcome; r->cost = cost; r->model_cost_change = mcc;
+  r->new_cost = new_cost; r->radius = radius; r->step_norm = step_norm;
+  if (iter > g_trace_n) g_trace_n = iter;
+}
+
 /* The Ceres TrustRegionMinimizer + LevenbergMarquardtStrategy loop (Appendix B). */
 static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_ba_summary* sum,
                     const or_reducer* R) {
@@ -359,6 +373,7 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
     for (int k = 0; k < nr; k++) { const int p = P->res[k].point; if (p >= 0) L.pt_res[L.pt_res_off[p] + fill[p]++] = k; }
     free(fill);
   }
+  g_trace_n = 0;
   uint8_t* active = (uint8_t*)calloc((size_t)np + 1, 1);
   for (int k = 0; k < nr; k++) {
     if (P->res[k].pose >= 0) memset(active + 6 * P->res[k].pose, 1, 6);
@@ -483,6 +498,7 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
     }
     if (!valid) {
       /* HandleInvalidStep -> StepIsInvalid == StepRejected(0) */
+      trace_put(iter, LORB_LM_STEP_INVALID, cost, model_cost_change, 0.0, radius, 0.0);
       if (++n_invalid >= o->max_num_consecutive_invalid_steps) { term = LORB_TERM_FAILURE; break; }
       radius = radius / decrease_factor;
       decrease_factor *= 2.0;
@@ -497,10 +513,18 @@ static int lm_solve(const or_prob* P, const lorb_lm_options* o, double* x, lorb_
     for (int i = 0; i < nc; i++) if (active[i]) { const double d = x[i] - xn[i]; sp += d * d; }
     for (int i = nc; i < np; i++) if (active[i]) { const double d = x[i] - xn[i]; sq += d * d; }
     const double step_norm = sqrt(sp + ar1(R, sq, LORB_OP_SUM));
-    if (step_norm <= o->parameter_tolerance * (x_norm + o->parameter_tolerance)) { term = LORB_TERM_PARAMETER_TOL; break; }
+    if (step_norm <= o->parameter_tolerance * (x_norm + o->parameter_tolerance)) {
+      trace_put(iter, LORB_LM_STEP_PARAM_TOL, cost, model_cost_change, new_cost, radius, step_norm);
+      term = LORB_TERM_PARAMETER_TOL; break;
+    }
     const double cost_change = cost - new_cost;
-    if (fabs(cost_change) <= o->function_tolerance * cost) { term = LORB_TERM_FUNCTION_TOL; break; }
+    if (fabs(cost_change) <= o->function_tolerance * cost) {
+      trace_put(iter, LORB_LM_STEP_FUNC_TOL, cost, model_cost_change, new_cost, radius, step_norm);
+      term = LORB_TERM_FUNCTION_TOL; break;
+    }
     const double relative_decrease = cost_change / model_cost_change;
+    trace_put(iter, relative_decrease > o->min_relative_decrease ? LORB_LM_STEP_ACCEPTED : LORB_LM_STEP_REJECTED,
+              cost, model_cost_change, new_cost, radius, step_norm);
     if (relative_decrease > o->min_relative_decrease) {
       /* HandleSuccessfulStep */
       memcpy(x, xn, sizeof(double) * (size_t)np);

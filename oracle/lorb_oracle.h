@@ -86,6 +86,10 @@ int or_ba_pose_only(const lorb_pose_problem_batch* prob, const lorb_lm_options* 
                     double* pose_out, float* Tcw_out, lorb_ba_summary* summaries);
 int or_ba_local(int n_windows, const lorb_ba_window* windows, const lorb_lm_options* opt,
                 double* const* pose_out, double* const* point_out, lorb_ba_summary* summaries);
+/* Sink for the per-iteration records of the next LM solves (each solve restarts at record 0, so
+ * after a multi-window call it holds the last window's); NULL switches it off. */
+void or_lm_trace(lorb_lm_iteration* buf, int cap);
+int or_lm_trace_count(void);
 /* Point-partitioned local BA (the multi-GPU exchange pattern of SURVEY §8e, restated on the
  * CPU): each rank passes its shard; fn all-reduces `count` doubles in place (op LORB_OP_*). */
 typedef int (*or_allreduce_fn)(void* user, double* buf, int64_t count, int32_t op);

@@ -193,6 +193,18 @@ def ba_local(wins, opt=None):
     return poses, pts, [summ[i].as_dict() for i in range(len(wins))]
 
 
+def ba_local_traced(w, opt=None):
+    """ba_local of one window plus its per-iteration records (or_lm_trace)"""
+    buf = (A.LMIteration * A.LM_TRACE_CAP)()
+    lib().or_lm_trace(buf, C.c_int(A.LM_TRACE_CAP))
+    try:
+        poses, pts, summ = ba_local([w], opt)
+        n = lib().or_lm_trace_count()
+    finally:
+        lib().or_lm_trace(None, C.c_int(0))
+    return poses[0], pts[0], summ[0], A.trace_list(buf, n)
+
+
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.c_int32)
 
 

@@ -98,12 +98,12 @@ class MapOracle:
         self.ring[t_new] = np.asarray(kf["pose"], np.float32).copy()
         self._sort_obs()
         self._slide(self.t0 + 1)
-        poses, pts, summ = O.ba_local([self.window()], opt)
+        poses, pts, summ, trace = O.ba_local_traced(self.window(), opt)
         for j in range(self.W):
-            self.ring[self.t0 + j] = poses[0][j].astype(np.float32)
-        self.point = pts[0].astype(np.float32)
+            self.ring[self.t0 + j] = poses[j].astype(np.float32)
+        self.point = pts.astype(np.float32)
         return dict(match_train=mt, n_matches=int(nm), new_points=int(new.sum()), new_observations=int(sel.sum()),
-                    pose=poses[0], points=pts[0], summary=summ[0])
+                    pose=poses, points=pts, summary=summ, trace=trace)
 
     def state(self):
         w = self.window()

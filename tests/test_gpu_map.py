@@ -28,7 +28,7 @@ def same_structure(g, o):
         assert np.array_equal(g[k], o[k]), k
 
 
-def run_chain(ctx, seq, opt, n_steps):
+def run_chain(ctx, seq, opt, n_steps, label="chain", strict=True):
     fp = synth.frame_params()
     M = LocalMap(ctx, seq["init"])
     try:
@@ -50,7 +50,8 @@ def run_chain(ctx, seq, opt, n_steps):
             assert close(g["pose"], o["pose"]), np.abs(g["pose"] - o["pose"]).max()
             assert close(g["point"], o["point"]), np.abs(g["point"] - o["point"]).max()
             assert np.array_equal(g["fixed_pose"], o["fixed_pose"])
-            lm_match(g["summary"], r["summary"])
+            flip = lm_match(g["summary"], r["summary"], gt=M.trace(), ot=r["trace"], label=f"{label} step {i}")
+            assert not strict or flip is None, (label, i, flip)
         return M, g
     except BaseException:
         M.close()
@@ -65,6 +66,15 @@ def test_local_mapping_chain_c4(ctx):
     info = M.plan_info()
     assert info["cameras"] == 50 and info["band"] <= 47, info
     assert 9000 < g["points"] < 12000 and 60000 < g["observations"] < 90000
+    M.close()
+
+
+def test_local_mapping_chain_c4_ceres_defaults(ctx):
+    """the chained C4 step with the options LocalMapping's BA runs with (Ceres
+    defaults, src/bundle_adjust.cpp:308-314): 3 steps, each step's termination, accepted steps and
+    per-iteration outcomes as the oracle's (strict)."""
+    seq = synth.mapping_sequence(steps=3)
+    M, g = run_chain(ctx, seq, A.LMOptions.default(), 3, label="map c4 defaults")
     M.close()
 
 
@@ -149,6 +159,7 @@ def test_local_mapping_overlapped_chain_bit_identical(ctx):
             assert go[k].shape == gs[k].shape and np.array_equal(go[k].view(np.uint8), gs[k].view(np.uint8)), k
         for k, v in gs["summary"].items():
             assert go["summary"][k] == v, (k, go["summary"][k], v)
+        assert Mo.trace() == Ms.trace()  # the last step's per-iteration records, bit for bit
     finally:
         Mo.close()
         if Ms is not None:
