@@ -24,7 +24,8 @@
 // relative, not bit-exactness -- VERDICT r04 item 3).  The Makefile's global -ffp-contract=off stays
 // for the float paths that must be bit-exact (projection, grid, unprojection, ORB, stereo: the other
 // translation units).  Everything in this file is deterministic either way (fixed reduction orders);
-// the host code here (cv::Rodrigues restated, x86-64 without FMA) is unaffected.
+// the host restatement that must round like the reference (lorb_pose_to_Tcw, cv::Rodrigues) turns
+// contraction off in its own body.
 #ifndef LORB_NO_CONTRACT  // A/B builds only (tools/isa_fma.py, tools/build_variant.sh nofma -DLORB_NO_CONTRACT)
 #pragma clang fp contract(fast)
 #endif
@@ -36,6 +37,7 @@
 #include <chrono>
 #include <cmath>
 #include <map>
+#include <type_traits>
 
 namespace {
 
@@ -3103,9 +3105,8 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
   __shared__ double s_jc[kGB][12];   // B / C: per point Ei (0..5), bs (6..8), sp (9..11); D: Jc per slot
   __shared__ double s_qj[kGB][12];   // A / B: Jp^T Jp (6) | Jp^T r (3) per observation; D: Q | Jps per slot
   __shared__ double s_rg[kGB][4];    // D: r | g per slot
-  __shared__ unsigned long long s_mask[kGB];
+  __shared__ unsigned long long s_mask[2][kGB];  // per point: its cameras, bits a - cmin (two words: spans <= 128)
   __shared__ int s_po[kGB];
-  __shared__ unsigned long long s_pts[64][kGB / 64];  // per local camera: the points that see it
   __shared__ int s_mm[2][kLsWaves];
   __shared__ double red3[3][kLsWaves];
   if ((int)blockIdx.x >= d.live[0]) return;
@@ -3146,8 +3147,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
   const BaWin& W = d.win[g.win];
   const int cur = S.cur;
   const double rad = S.radius;
-  if (t < kGB) s_mask[t] = 0ull;
-  if (t < 64 * (kGB / 64)) s_pts[t / (kGB / 64)][t % (kGB / 64)] = 0ull;
+  if (t < kGB) { s_mask[0][t] = 0ull; s_mask[1][t] = 0ull; }
   // A
   double r[2] = {0, 0}, Jp[6] = {0, 0, 0, 0, 0, 0}, Jc[12];
 #pragma unroll
@@ -3218,10 +3218,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
   }
   const int lp = p_ - g.p0;
   const int a_ = c_ - cmin;
-  if (has && c_ >= 0) {
-    atomicOr(&s_mask[lp], 1ull << a_);
-    atomicOr(&s_pts[a_][lp >> 6], 1ull << (lp & 63));
-  }
+  if (has && c_ >= 0) atomicOr(&s_mask[a_ >> 6][lp], 1ull << (a_ & 63));
   __syncthreads();
   LS_STAMP(2);
   // C: Jps, Q, g (reads the point data), then the camera-ordered slot
@@ -3238,7 +3235,9 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
         Q[3 * rr + j] = Js[3 * rr] * s3(pt, 0, j) + Js[3 * rr + 1] * s3(pt, 1, j) + Js[3 * rr + 2] * s3(pt, 2, j);
     g0 = Q[0] * pt[6] + Q[1] * pt[7] + Q[2] * pt[8];
     g1 = Q[3] * pt[6] + Q[4] * pt[7] + Q[5] * pt[8];
-    slot = s_po[lp] + __popcll(s_mask[lp] & ((1ull << a_) - 1ull));
+    const unsigned long long m0 = s_mask[0][lp];
+    slot = s_po[lp] + (a_ < 64 ? __popcll(m0 & ((1ull << a_) - 1ull))
+                               : __popcll(m0) + __popcll(s_mask[1][lp] & ((1ull << (a_ - 64)) - 1ull)));
   }
   __syncthreads();
   if (slot >= 0) {
@@ -3274,7 +3273,6 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
     int a = 0, dd = 0;
     if (act) pm_slot_inv(q, bwc, a, dd);
     const int b = a - dd;
-    const unsigned long long ba = act ? 1ull << a : 0ull, bb = 1ull << b;
     const bool dg = dd == 0;
     double acc[36], ex[18];
 #pragma unroll
@@ -3282,15 +3280,26 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
 #pragma unroll
     for (int k = 0; k < 18; ++k) ex[k] = 0.0;
     const int k0 = split ? (wv << lr) + rr : 0, kst = split ? kLsWaves << lr : 1;
-    if (!LORB_LS_SKIPD && k0 < g.cnt) {
-      unsigned long long m = s_mask[k0];
+    // the point loop, for group windows of <= 64 cameras (one mask word) or up to 128 (two: the
+    // lane's two cameras pick their word, a rank in the high word adds the low word's count)
+    auto point_loop = [&](auto wide_tag) {
+      constexpr bool kWide = decltype(wide_tag)::value;
+      const int wa = kWide ? a >> 6 : 0, wb = kWide ? b >> 6 : 0;
+      const unsigned long long ba = act ? 1ull << (a & 63) : 0ull, bb = 1ull << (b & 63);
+      unsigned long long m = s_mask[0][k0], mh = kWide ? s_mask[1][k0] : 0ull;
       int po = s_po[k0];
       for (int k = k0; k < g.cnt; k += kst) {
-        const unsigned long long mc = m;
+        const unsigned long long mc = m, mch = mh;
         const int pc = po;
-        if (k + kst < g.cnt) { m = s_mask[k + kst]; po = s_po[k + kst]; }  // the next point's
-        if ((mc & ba) && (mc & bb)) {
-          const int eh = pc + __popcll(mc & (ba - 1ull)), el = pc + __popcll(mc & (bb - 1ull));
+        if (k + kst < g.cnt) {  // the next point's
+          m = s_mask[0][k + kst]; po = s_po[k + kst];
+          if (kWide) mh = s_mask[1][k + kst];
+        }
+        const unsigned long long ma = kWide && wa ? mch : mc, mb = kWide && wb ? mch : mc;
+        if ((ma & ba) && (mb & bb)) {
+          const int lo = kWide ? __popcll(mc) : 0;
+          const int eh = pc + (kWide && wa ? lo : 0) + __popcll(ma & (ba - 1ull));
+          const int el = pc + (kWide && wb ? lo : 0) + __popcll(mb & (bb - 1ull));
           const double* Qh = s_qj[eh];
           const double* Jl = s_qj[el] + 6;
           const double* Ch = s_jc[eh];
@@ -3321,6 +3330,10 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
           }
         }
       }
+    };
+    if (!LORB_LS_SKIPD && k0 < g.cnt) {
+      if (span > 64) point_loop(std::true_type{});
+      else point_loop(std::false_type{});
     }
     for (int m = 1; m < (1 << lr); m <<= 1) {  // the slot's R subsets (lr = 0 unless split)
 #pragma unroll
@@ -4154,7 +4167,7 @@ std::vector<int> camera_order(int C, const std::vector<char>& adj) {
 // Point-major path (PM): windows of at most 64 optimised cameras (a group's camera window is a 64-bit
 // mask) whose points fit one group (C + F <= kGB observations per point); LORB_PM=0 keeps the
 // pair-major path (A/B, diagnostics)
-bool pm_fits(int C, int F) { return C <= 64 && C + F <= kGB; }
+bool pm_fits(int C, int F) { return C <= 128 && C + F <= kGB; }
 bool pm_enabled() {
   static const bool on = [] { const char* e = getenv("LORB_PM"); return !(e && e[0] == '0'); }();
   return on;
@@ -6031,7 +6044,10 @@ int lorb_debug_po_stamps(unsigned long long* out64) {
 #endif
 
 // cv::Rodrigues (vector -> matrix, double internally) + Frame::UpdatePoseMat write-back
+// (the file-scope contraction pragma must not reach this restatement: it rounds like the
+// reference's un-contracted host build whatever -march the library is built with)
 void lorb_pose_to_Tcw(const float rvec[3], const float tvec[3], float T[16]) {
+#pragma clang fp contract(off)
   double rx = rvec[0], ry = rvec[1], rz = rvec[2];
   const double theta = std::sqrt(rx * rx + ry * ry + rz * rz);
   double R[9];

@@ -37,14 +37,15 @@ __device__ __forceinline__ RotVal rot_val(const double aa[3]) {
   R.aa0 = aa[0]; R.aa1 = aa[1]; R.aa2 = aa[2];
   const double theta2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
   R.big = theta2 > kAarpEps;
-  if (R.big) {
-    const double th = sqrt(theta2);
-    sincos(th, &R.sn, &R.cs);
-    const double ti = 1.0 / th;
-    R.w0 = aa[0] * ti; R.w1 = aa[1] * ti; R.w2 = aa[2] * ti;
-  } else {
-    R.sn = R.cs = R.w0 = R.w1 = R.w2 = 0.0;
-  }
+  // evaluated on both branches and selected by value: stores through &R.sn / &R.cs on one branch
+  // and plain zero stores on the other were merged into one store through a selected address,
+  // which put R in scratch (24 B per lane in k_ba_bs2 / k_ba_chol_2s)
+  const double th = sqrt(theta2);
+  double sn, cs;
+  sincos(th, &sn, &cs);
+  const double ti = 1.0 / th;
+  R.sn = R.big ? sn : 0.0; R.cs = R.big ? cs : 0.0;
+  R.w0 = R.big ? aa[0] * ti : 0.0; R.w1 = R.big ? aa[1] * ti : 0.0; R.w2 = R.big ? aa[2] * ti : 0.0;
   return R;
 }
 __device__ __forceinline__ void aarp_s(const RotVal& R, const double pt[3], double out[3]) {

@@ -548,7 +548,13 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   unsigned long long* qkey = nullptr;
   const bool has_t = M->h_P > 0;
   if (n > 0 && has_t) {
-    LORB_TRY(lorb::match1_keys_into(ctx, d_desc, n, m.desc, M->h_P, M->qkey, M->tkey, ms));
+    // the per-train keys are restored to all-ones by the append's merge (k_cc_merge1); a failure
+    // between the scan and that merge would leave stale keys for the next step: reset them here, or
+    // mark the map unusable when even that fails
+    if (const int rc = lorb::match1_keys_into(ctx, d_desc, n, m.desc, M->h_P, M->qkey, M->tkey, ms); rc != LORB_OK) {
+      if (hipMemsetAsync(M->tkey, 0xff, sizeof(uint32_t) * std::max<size_t>(m.P_cap, 1), ms) != hipSuccess) M->broken = true;
+      return rc;
+    }
     qkey = M->qkey;
   }
   LORB_TRY(mark(0));
@@ -568,7 +574,10 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   else if (n <= 4096) LORB_APPEND(4);
   else LORB_APPEND(0);
 #undef LORB_APPEND
-  LORB_CHECK_LAUNCH(ctx);
+  if (hipGetLastError() != hipSuccess) {  // the append (and its key merge) did not run: see above
+    M->broken = true;
+    return lorb::set_error(ctx, LORB_E_DEVICE, "k_map_append launch failed; the map is unusable");
+  }
   if (ovl) {  // the rest of the step follows the previous step's write-back on the main stream
     LORB_HIP(ctx, hipEventRecord(M->ev_app, ms));
     LORB_HIP(ctx, hipStreamWaitEvent(s, M->ev_app, 0));

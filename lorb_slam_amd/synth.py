@@ -94,9 +94,14 @@ def ba_window(seed=3, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400, obs_
     """Local-BA window.  KF i: camera centre (0.1 i, 0, 0), yaw 0.01 i.
     Each point is seen by a contiguous KF range of length obs_lens[p % len]; n_fixed extra
     out-of-window KFs (MPCost, fixed pose) each observe ~fixed_obs_per_kf points to fix the gauge.
-    point_order "first_kf" numbers the points by their first observing keyframe (stable), the order
-    BA::LocalPoseOptimization collects them in -- keyframe by keyframe, each keyframe's map points not
-    seen before (src/bundle_adjust.cpp:224-241); "random" keeps the draw order (no camera locality).
+    point_order "first_kf" numbers the points by their first observing window keyframe, oldest
+    first (stable).  That is a synthetic order with camera locality, NOT the reference's order:
+    BA::LocalPoseOptimization collects points frame by frame starting from the CURRENT frame, then
+    its covisible frames in GetCovisibleFrames() order (src/bundle_adjust.cpp:208-241,
+    src/frame.cpp:729), each frame's map points not seen before.  The device-built plans of the
+    chained map step take the reference's order (tests/test_gpu_ba.py reference_camera_order);
+    "random" keeps the draw order (no camera locality; test_local_ba_point_order_without_camera_
+    locality).  Bench windows before round 5 used "random".
     Returns the problem dict consumed by lorb_ba_local / or_ba_local plus ground truth."""
     rng = np.random.default_rng(seed)
 
