@@ -52,12 +52,9 @@ HBM_PEAK = 8.0e12                            # HBM3E spec (MI355X_MICROARCH)
 OPS_PER_PAIR = 16                            # 8 x v_xor_b32 + 8 x v_bcnt_u32_b32 per 256-bit pair
 # the Cholesky id covers three kernels chosen by band shape; C3/C4/C5 windows
 # (band 47, n >= 128) run the two-sided k_ba_chol_2s
-# Point-major BA path (the default; LORB_PM=0 selects the pair-major one): timer 3 is k_ba_ls
-# (linearisation + point elimination + per-group Schur partials), timer 2 k_ba_red (the partials'
-# fixed-order sum into the band)
-PM = os.environ.get("LORB_PM", "1") != "0"
-K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_red" if PM else "k_ba_schur",
-           3: "k_ba_ls" if PM else "k_ba_lin", 4: "k_ba_chol_2s"}
+# Point-major BA path (the only Schur path since round 6): timer 3 is k_ba_ls (linearisation + point
+# elimination + per-group Schur partials), timer 2 k_ba_red (the partials' fixed-order sum into the band)
+K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_red", 3: "k_ba_ls", 4: "k_ba_chol_2s"}
 # rocprofv3 short names (tools/pmc_traffic.py) of the same kernels, for the PMC traffic lookup
 K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: K_NAMES[2], 3: K_NAMES[3], 4: "k_ba_chol_2s"}
 
@@ -66,15 +63,10 @@ def ba_kspec(W, n_obs, n_pts, F, bw):
     """Algorithmic bytes per launch of the BA kernels of W windows (id -> (bound, amount, unit)).
     Point-major: k_ba_ls reads per observation its uv (16 B) and three structure indices (12 B), per
     point X (24 B), and writes per point the point-block inverse and rhs (72 B); k_ba_red writes the
-    band once.  Pair-major: k_ba_schur reads the W / Y tiles (2 x 18 doubles per observation) once
-    and writes the band; k_ba_lin writes 34 doubles per observation and reads uv + indices + X."""
+    band once."""
     band = W * (6 * F) * (bw + 1) * 8.0
-    if PM:
-        return {2: ("hbm", band, "GB/s"),
-                3: ("hbm", W * (n_obs * 28.0 + n_pts * 96.0), "GB/s"),
-                4: ("fp64", W * ((6 * F) * bw * bw + 4.0 * (6 * F) * bw), "TFLOP/s")}
-    return {2: ("hbm", W * n_obs * 36 * 8.0 + band, "GB/s"),
-            3: ("hbm", W * (n_obs * (34 * 8.0 + 16 + 12) + n_pts * 24.0), "GB/s"),
+    return {2: ("hbm", band, "GB/s"),
+            3: ("hbm", W * (n_obs * 28.0 + n_pts * 96.0), "GB/s"),
             4: ("fp64", W * ((6 * F) * bw * bw + 4.0 * (6 * F) * bw), "TFLOP/s")}
 # committed PMC summaries, newest first; each is keyed by workload (tools/pmc_traffic.py)
 TRAFFIC = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r05", "r04", "r03", "r02", "r01")]

@@ -534,8 +534,8 @@ int lorb_ctx_ba_solver(lorb_ctx* ctx, lorb_ba_solver** out);
  * the last solve (0 k_ba_chol, 1 k_ba_chol_w, 2 k_ba_chol_2s, -1 none yet), [2] (camera, camera)
  * blocks, [3] point groups, [4] observations, [5] points, [6] cameras, [7] 1 if some window's
  * cameras were reordered (reverse Cuthill-McKee on the covisibility graph; outputs keep the
- * caller's order), [8] 1 if the plan runs the point-major Schur path (every window <= 64 cameras;
- * else the pair-major kernels), [9] its partial-reduction width (threads per block: 256, 512 or 1024; 0: pair-major) */
+ * caller's order), [8] 1: the point-major Schur path (the only one since round 6; point groups span
+ * <= 128 cameras), [9] its partial-reduction width (threads per block: 256, 512 or 1024) */
 int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n);
 /* the last solve's per-iteration records of window w (at most min(cap, LORB_LM_TRACE_CAP)); *n_out =
  * records written.  Synchronises. */

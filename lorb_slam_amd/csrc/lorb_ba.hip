@@ -8,13 +8,12 @@
 //   * every LM scalar decision (accept/reject, radius, tolerances) is made ON THE DEVICE by a
 //     one-workgroup-per-window kernel, so an LM iteration is a fixed sequence of launches with
 //     no host round trip; it is captured once into a hipGraph and replayed.
-//   * point-major Schur (windows of <= 64 cameras, the default): one workgroup per point group
-//     linearises its observations, eliminates its points and forms its camera-block partials on
-//     chip (k_ba_ls); one workgroup per band block sums the groups' partials in group order
-//     (k_ba_red); the back-substitution re-evaluates the linearisation (k_ba_bs2).  Nothing is
-//     stored per observation.  Wider windows (and LORB_PM=0) take the pair-major kernels:
-//     per-observation tiles (k_ba_lin), one workgroup per (camera, camera) block over a CSR pair
-//     list (k_ba_schur), per-point back-substitution (k_ba_backsub).
+//   * point-major Schur: one workgroup per point group linearises its observations, eliminates its
+//     points and forms its camera-block partials on chip (k_ba_ls; a group spans <= 128 cameras);
+//     one workgroup per band block sums the groups' partials in group order (k_ba_red); the
+//     back-substitution re-evaluates the linearisation (k_ba_bs2).  Nothing is stored per
+//     observation.  (Round 4's pair-major path -- per-observation tiles, one workgroup per camera
+//     block pair over a CSR pair list -- was removed in round 6.)
 //   * the reduced camera system is banded (cameras in reverse Cuthill-McKee order): a two-sided
 //     band Cholesky with the LM head inside (k_ba_chol_2s), or the wider variants.
 //   * all reductions are fixed-order trees (block partials reduced in index order): deterministic,
@@ -173,21 +172,6 @@ __device__ __forceinline__ void wave_sum_all(double (&v)[32]) {
 #pragma unroll
   for (int k = 0; k < N; ++k) v[k] = readlane_d(r, 2 * k);
 }
-__device__ __forceinline__ int wave_isum(int v) {
-  {
-    const auto p = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
-    v = (int)(p[0] + p[1]);  // v_i + v_(i^32), whichever copy holds which
-  }
-  {
-    const auto p = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
-    v = (int)(p[0] + p[1]);
-  }
-  v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xF, 0xF, false);
-  v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xF, 0xF, false);
-  v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
-  v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
-  return v;
-}
 template <int N>
 __device__ __forceinline__ void block_sum(double (&v)[N], double* sh /* [N*256] */) {
   // deterministic fixed tree over a 256-thread block
@@ -247,18 +231,10 @@ struct BaDev {
   const PBlk* pblk;
   const int* obs_pt;         // K  (global point of each observation)
   const BlockPair* bp;
-  const int2* pairs;
   const int* pt_obs_off;     // Ptot+1
   const int* obs_cam;        // K  (global optimised camera or -1)
   const int* obs_fix;        // K  (global fixed pose or -1)
   const double2* obs_uv;     // K
-  const int* cam_obs_off;    // Ctot+1
-  const int* cam_obs;        // camera-major obs list
-  const int* obs_cm;         // K: camera-major slot of an optimised obs (-1: fixed camera).
-                             //    Camera-side tiles (obs_Jc, cam_r, obs_Jps, obs_Q, obs_g) are
-                             //    stored in camera-major order so camera and Schur kernels
-                             //    read contiguous runs.
-  const int* cam_win;        // Ctot
   const double* fixed_pose;  // NF*6
   double* x_init_pose;       // Ctot*6 (initial values, never written)
   double* x_init_pt;         // Ptot*3
@@ -266,20 +242,10 @@ struct BaDev {
   double* x_pt[2];           // Ptot*3
   double* scale_pose;        // Ctot*6
   double* scale_pt;          // Ptot*3
-  double* ete;               // Ptot*6 (unscaled)
   double* etb;               // Ptot*3 (unscaled)
   double* pinv;              // Ptot*6
   double* U;                 // Ctot*21 (unscaled, packed upper row-major)
   double* V;                 // Ctot*6
-  double* cam_gmax;          // Ctot
-  double* obs_r;             // K*2
-  double* obs_Jp;            // K*6
-  double* obs_Jc;            // K*12, camera-major slots
-  double* cam_r;             // K*2: residuals in camera-major slots
-  double* obs_Jps;           // K*6: Jp scaled by the point's Jacobi scale (2x3)
-  double* obs_Q;             // K*6: Q = Jps E^-1 (2x3); W = Jcs^T Jps is rank 2, so the Schur
-                             //      block Y_h W_l^T = Jcs_h^T (Q_h Jps_l^T) Jcs_l
-  double* obs_g;             // K*2: g = Q b_p  (rhs: Y_h b_p = Jcs_h^T g)
   double* env;               // S envelopes (all-reduced when sharded)
   double* rhs;               // sum n
   // sharded plans: kernels write the *_part buffers, the all-reduce produces the
@@ -298,10 +264,9 @@ struct BaDev {
                              // ((row_base >> 4) + w) * 1024 doubles, top side's blocks then the
                              // bottom side's, [block][16][64] (BandSide::bsk_block)
   WinState* st;
-  // point-major path (PM): group partials, per group (first camera - pose_base, span); pm: plan uses it
+  // group partials (k_ba_ls -> k_ba_red), per group (first camera - pose_base, span)
   double* gpart;
   int2* gspan;
-  int pm;
   lorb_lm_iteration* trace;  // per window LORB_LM_TRACE_CAP records (lm_decide)
   // [0] point groups, [1] block pairs in use.  Launch grids may be larger (device-built plans
   // launch at capacity so that the captured LM graph survives a rebuild); the extra workgroups exit.
@@ -325,7 +290,7 @@ __global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n
     s.done = d.win[i].n_obs_all == 0 ? 1 : 0;
     s.relin = 1; s.cur = 0; s.last_successful = 1; s.term = 0; s.chol_fail = 0; s.pad = 0;
     d.st[i] = s;
-    if (d.sharded) d.wfail_part[i] = 0.0;  // point-block failures (set by k_ba_lin, cleared by k_ba_lm_end)
+    if (d.sharded) d.wfail_part[i] = 0.0;  // point-block failures (set by k_ba_ls, cleared by k_ba_lm_end)
   }
   if (i < ctot) {
     double x[6];
@@ -364,10 +329,8 @@ __device__ __forceinline__ void block_red3(double& a, double& b, double& c, doub
   for (int k = 1; k < kGW; ++k) { a += red[0][k]; b = M1 ? fmax(b, red[1][k]) : b + red[1][k]; c += red[2][k]; }
 }
 
-// Point-block prep of k_ba_lin (from on-chip values when it relinearises, from the stored
-// linearisation after a rejected step, where only the radius changed): the point's scaled
-// E^T E + D^2 inverted, and per optimised observation Jps (scaled Jp), Q = Jps E^-1, g = Q b.
-// Returns false when the 3x3 block is not invertible (Ei = 0).
+// Point-block prep (k_ba_ls phase B): the point's scaled E^T E + D^2 inverted at the current
+// radius.  Returns false when the 3x3 block is not invertible (Ei = 0).
 __device__ __forceinline__ bool prep_point(const double (&Eu)[6], const double (&bu)[3], const double (&sp)[3],
                                            double rad, const LMOpt& o, double (&Ei)[6], double (&b)[3]) {
   double E[6];
@@ -387,259 +350,11 @@ __device__ __forceinline__ bool prep_point(const double (&Eu)[6], const double (
 }
 __device__ __forceinline__ void prep_fail(const BaDev& d, int win) {
   // benign race: every writer stores the same value; sharded plans reduce the flag (K5).  The
-  // flag is cleared by k_ba_lm_end (and k_ba_init), not by k_ba_lm_begin: k_ba_lin sets it
+  // flag is cleared by k_ba_lm_end (and k_ba_init), not by k_ba_lm_begin: k_ba_ls sets it
   // before k_ba_lm_begin runs.
   if (d.sharded) d.wfail_part[win] = 1.0;
   else d.st[win].chol_fail = 1;
 }
-__device__ __forceinline__ void prep_obs(const BaDev& d, int m, const double (&Jp)[6], const double* Ei,
-                                         const double* b, const double* sp) {
-  double Jps[6], Q[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) Jps[k] = Jp[k] * sp[k % 3];
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      Q[3 * r + j] = Jps[3 * r] * s3(Ei, 0, j) + Jps[3 * r + 1] * s3(Ei, 1, j) + Jps[3 * r + 2] * s3(Ei, 2, j);
-#pragma unroll
-  for (int k = 0; k < 6; ++k) { d.obs_Jps[6 * m + k] = Jps[k]; d.obs_Q[6 * m + k] = Q[k]; }
-  d.obs_g[2 * m] = Q[0] * b[0] + Q[1] * b[1] + Q[2] * b[2];
-  d.obs_g[2 * m + 1] = Q[3] * b[0] + Q[4] * b[1] + Q[5] * b[2];
-}
-
-// Point-group Schur prep after a rejected step (only the radius changed since the last
-// linearisation): scaled E^T E + D^2 -> inverse (point phase), then per optimised observation
-// Jps, Q = Jps E^-1 and g = Q b (observation phase).  Runs inside k_ba_lin, whose relinearising
-// iterations do the same prep from on-chip values; sh[t] holds Ei (0..5) and b (6..8).
-__device__ __forceinline__ void prep_after_reject(const BaDev& d, const LMOpt& o, const PBlk& g, int t, double rad,
-                                                  double (*sh)[9], double (*ssp)[3]) {
-  const int pf = g.p0 + min(t, max(g.cnt - 1, 0));
-  double sp[3] = {0, 0, 0}, b[3] = {0, 0, 0}, Eu[6] = {0, 0, 0, 0, 0, 0};
-  if (g.cnt > 0) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { sp[k] = d.scale_pt[3 * pf + k]; b[k] = d.etb[3 * pf + k]; }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Eu[k] = d.ete[6 * pf + k];
-  }
-  const int ef = g.o0 + min(t, max(g.no - 1, 0));
-  int m_f = -1, pt_f = 0;
-  double Jp_f[6] = {0, 0, 0, 0, 0, 0};
-  if (g.no > 0) {
-    m_f = d.obs_cm[ef]; pt_f = d.obs_pt[ef];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Jp_f[k] = d.obs_Jp[6 * ef + k];
-  }
-  if (t < g.cnt) {
-    const int p = g.p0 + t;
-    double Ei[6], bs[3];
-    if (!prep_point(Eu, b, sp, rad, o, Ei, bs)) prep_fail(d, g.win);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { d.pinv[6 * p + k] = Ei[k]; sh[t][k] = Ei[k]; }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { sh[t][6 + k] = bs[k]; ssp[t][k] = sp[k]; }
-  }
-  __syncthreads();
-  for (int c0 = t; c0 < g.no; c0 += kGB) {
-    const int e = g.o0 + c0;
-    const bool first = c0 == t;
-    const int m = first ? m_f : d.obs_cm[e];
-    if (m < 0) continue;
-    const int lp = (first ? pt_f : d.obs_pt[e]) - g.p0;
-    double Jp[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Jp[k] = first ? Jp_f[k] : d.obs_Jp[6 * e + k];
-    prep_obs(d, m, Jp, sh[lp], sh[lp] + 6, ssp[lp]);
-  }
-}
-
-// K1: linearisation of a point group (windows that (re)linearise this iteration): per
-// observation residual + Jacobians, per point E^T E / E^T r (unscaled), Jacobi scale
-// (iteration 0), gradient-max / point-norm / cost partials, and the point-block prep of this
-// iteration (prep_point / prep_obs at the current radius: the radius only changes in
-// k_ba_lm_end), so the observations' Jp and the point's E, b never make an HBM round trip.  After
-// a rejected step it only redoes the prep at the new radius (prep_after_reject).
-__global__ __launch_bounds__(kGB) void k_ba_lin(BaDev d, LMOpt o) {
-  __shared__ double sh[kGB][9];   // observation terms; then the points' Ei (6) and b (3)
-  __shared__ double ssp[kGB][3];
-  __shared__ double red3[3][4];
-  if ((int)blockIdx.x >= d.live[0]) return;
-  const PBlk g = d.pblk[blockIdx.x];
-  const int t = threadIdx.x;
-  // plan-structure loads of the first chunk go out together with the window state
-  const int of = g.o0 + min(t, max(g.no - 1, 0));
-  const int p_f = g.no > 0 ? d.obs_pt[of] : 0, c_f = g.no > 0 ? d.obs_cam[of] : -1;
-  int po0 = 0, po1 = 0;
-  if (t < g.cnt) { po0 = d.pt_obs_off[g.p0 + t]; po1 = d.pt_obs_off[g.p0 + t + 1]; }
-  const WinState& S = d.st[g.win];
-  if (S.done) return;
-  if (!S.relin) {  // after a rejected step: the prep at the new radius only
-    prep_after_reject(d, o, g, t, S.radius, sh, ssp);
-    return;
-  }
-  const BaWin& W = d.win[g.win];
-  const int cur = S.cur;
-  const double rad = S.radius;
-  double cost = 0.0;
-  double E[6] = {0, 0, 0, 0, 0, 0}, b[3] = {0, 0, 0};
-  double Jp_f[6] = {0, 0, 0, 0, 0, 0};  // the first chunk's Jp (this thread's observation)
-  int m_f = -1;
-  for (int c0 = 0; c0 < g.no; c0 += kGB) {
-    if (c0 + t < g.no) {
-      const int o = g.o0 + c0 + t;
-      const int p = c0 == 0 ? p_f : d.obs_pt[o];
-      const int c = c0 == 0 ? c_f : d.obs_cam[o];
-      if (c0 == 0) m_f = d.obs_cm[o];
-      double X[3], pose[6];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) X[k] = d.x_pt[cur][3 * p + k];
-      if (c >= 0) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) pose[k] = d.x_pose[cur][6 * c + k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * d.obs_fix[o] + k];
-      }
-      const double2 uv = d.obs_uv[o];
-      double r[2], Jp[6], Jc[12];
-      if (c >= 0) residual_jac_s(d.rot_lin[c], pose + 3, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
-      else residual_jac(pose, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
-      d.obs_r[2 * o] = r[0]; d.obs_r[2 * o + 1] = r[1];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) d.obs_Jp[6 * o + k] = Jp[k];
-      if (c0 == 0) {
-#pragma unroll
-        for (int k = 0; k < 6; ++k) Jp_f[k] = Jp[k];
-      }
-      if (c >= 0) {
-        const int m = c0 == 0 ? m_f : d.obs_cm[o];
-#pragma unroll
-        for (int k = 0; k < 12; ++k) d.obs_Jc[12 * m + k] = Jc[k];
-        d.cam_r[2 * m] = r[0]; d.cam_r[2 * m + 1] = r[1];
-      }
-      cost += 0.5 * (r[0] * r[0] + r[1] * r[1]);
-      sh[t][0] = Jp[0] * Jp[0] + Jp[3] * Jp[3]; sh[t][1] = Jp[0] * Jp[1] + Jp[3] * Jp[4];
-      sh[t][2] = Jp[0] * Jp[2] + Jp[3] * Jp[5]; sh[t][3] = Jp[1] * Jp[1] + Jp[4] * Jp[4];
-      sh[t][4] = Jp[1] * Jp[2] + Jp[4] * Jp[5]; sh[t][5] = Jp[2] * Jp[2] + Jp[5] * Jp[5];
-      sh[t][6] = Jp[0] * r[0] + Jp[3] * r[1]; sh[t][7] = Jp[1] * r[0] + Jp[4] * r[1];
-      sh[t][8] = Jp[2] * r[0] + Jp[5] * r[1];
-    }
-    __syncthreads();
-    if (t < g.cnt) {
-      const int a = max(po0, g.o0 + c0), z = min(po1, g.o0 + c0 + kGB);
-      for (int e = a; e < z; ++e) {
-        const double* v = sh[e - g.o0 - c0];
-#pragma unroll
-        for (int k = 0; k < 6; ++k) E[k] += v[k];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) b[k] += v[6 + k];
-      }
-    }
-    __syncthreads();
-  }
-  double gm = 0.0, xn2 = 0.0;
-  if (t < g.cnt) {
-    const int p = g.p0 + t;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) d.ete[6 * p + k] = E[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) d.etb[3 * p + k] = b[k];
-    double sp[3];
-    if (S.iter == 0) {
-      sp[0] = 1.0 / (1.0 + sqrt(E[0]));
-      sp[1] = 1.0 / (1.0 + sqrt(E[3]));
-      sp[2] = 1.0 / (1.0 + sqrt(E[5]));
-#pragma unroll
-      for (int k = 0; k < 3; ++k) d.scale_pt[3 * p + k] = sp[k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) sp[k] = d.scale_pt[3 * p + k];
-    }
-    if (po1 > po0) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double X = d.x_pt[cur][3 * p + k];
-        gm = fmax(gm, fabs(X - (X + -b[k])));
-        xn2 += X * X;
-      }
-    }
-    // point-block prep (point phase)
-    double Ei[6], bs[3];
-    if (!prep_point(E, b, sp, rad, o, Ei, bs)) prep_fail(d, g.win);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) { d.pinv[6 * p + k] = Ei[k]; sh[t][k] = Ei[k]; }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) { sh[t][6 + k] = bs[k]; ssp[t][k] = sp[k]; }
-  }
-  __syncthreads();
-  // point-block prep (observation phase): the first chunk's Jp from registers
-  for (int c0 = t; c0 < g.no; c0 += kGB) {
-    const int e = g.o0 + c0;
-    const bool first = c0 == t;
-    const int m = first ? m_f : d.obs_cm[e];
-    if (m < 0) continue;
-    const int lp = (first ? p_f : d.obs_pt[e]) - g.p0;
-    double Jp[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Jp[k] = first ? Jp_f[k] : d.obs_Jp[6 * e + k];
-    prep_obs(d, m, Jp, sh[lp], sh[lp] + 6, ssp[lp]);
-  }
-  block_red3<true>(cost, gm, xn2, red3);
-  if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[0] = cost; P[1] = gm; P[2] = xn2; }
-}
-
-// K2: per-camera normal blocks U = Jc^T Jc (21, packed upper), V = Jc^T r (6): one 256-thread
-// workgroup per optimised camera, lanes stride the camera's slots, fixed-order wave + LDS reduction.
-// Also the trailing workgroups of the fused iteration's k_ba_schur<true>.
-template <bool FU>
-__device__ __forceinline__ void camera_block(const BaDev& d, int c, double (&red)[4][27]) {
-  const int w = d.cam_win[c];
-  const int a0 = d.cam_obs_off[c], a1 = d.cam_obs_off[c + 1];  // issued with cam_win
-  const WinState& S = d.st[w];
-  // FU: also after a rejected step (same U, V: the tiles are the linearisation's), since the
-  // diagonal Schur block is combined with them every iteration
-  if (S.done || (!FU && !S.relin)) return;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  double U[21], V[6];
-#pragma unroll
-  for (int k = 0; k < 21; ++k) U[k] = 0.0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) V[k] = 0.0;
-  for (int e = a0 + t; e < a1; e += 256) {
-    double J[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) J[k] = d.obs_Jc[12 * e + k];
-    const double r0 = d.cam_r[2 * e], r1 = d.cam_r[2 * e + 1];
-    int q = 0;
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      V[a] += J[a] * r0 + J[6 + a] * r1;
-#pragma unroll
-      for (int b = a; b < 6; ++b) U[q++] += J[a] * J[b] + J[6 + a] * J[6 + b];
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 21; ++k) {
-    const double v = wave_sum(U[k]);
-    if (lane == 0) red[wv][k] = v;
-  }
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const double v = wave_sum(V[k]);
-    if (lane == 0) red[wv][21 + k] = v;
-  }
-  __syncthreads();
-  if (t < 27) {
-    const double v = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
-    if (t < 21) d.U_part[21 * c + t] = v;
-    else d.V_part[6 * c + t - 21] = v;
-  }
-}
-__global__ __launch_bounds__(256) void k_ba_camera(BaDev d) {
-  __shared__ double red[4][27];
-  camera_block<false>(d, blockIdx.x, red);
-}
-
 // Lane-strided partial sums over a window's point groups (b = lane, lane + 64, ... in that order,
 // the per-lane order of a plain loop) with the loads of kPU groups issued before any is added: the
 // partials come from the previous kernel (another XCD's L2), so a load-add loop pays one memory
@@ -743,153 +458,6 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double& band(double* A, int bw, int i, int j) {
   return A[(size_t)i * (bw + 1) + (j - i + bw)];
-}
-
-// K5: reduced camera system S (band storage) + rhs: one 256-thread workgroup per non-zero
-// camera block pair; lanes stride the pair list, fixed-order wave + LDS reduction.  Each
-// (obs_h, obs_l) term is Jc_h^T M Jc_l with the 2x2 M = Q_h Jps_l^T (108 FMA, 36 doubles read);
-// the camera Jacobi scales are applied once per block.  Block pairs are sorted by camera and
-// remapped so that each XCD (blockIdx % 8 group) takes a contiguous run: the tiles of a camera
-// are re-read from that XCD's L2 instead of from the fabric.
-// DIAG (a diagonal block: pr.x == pr.y, pairs in camera-slot order): the camera's rhs term
-// Jc^T g of the same observation is accumulated from the tiles already loaded
-template <bool DIAG>
-__device__ __forceinline__ void schur_pair(const BaDev& d, int2 pr, double (&acc)[36], double (&r6)[6]) {
-  double Qh[6], Jl[6], Ch[12], Cl[12], g0 = 0.0, g1 = 0.0;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) { Qh[k] = d.obs_Q[6 * pr.x + k]; Jl[k] = d.obs_Jps[6 * pr.y + k]; }
-#pragma unroll
-  for (int k = 0; k < 12; ++k) { Ch[k] = d.obs_Jc[12 * pr.x + k]; Cl[k] = DIAG ? Ch[k] : d.obs_Jc[12 * pr.y + k]; }
-  if (DIAG) {
-    g0 = d.obs_g[2 * pr.x]; g1 = d.obs_g[2 * pr.x + 1];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) r6[k] += Ch[k] * g0 + Ch[6 + k] * g1;
-  }
-
-  double M[4], N[12];
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-      M[2 * r + s] = Qh[3 * r] * Jl[3 * s] + Qh[3 * r + 1] * Jl[3 * s + 1] + Qh[3 * r + 2] * Jl[3 * s + 2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) N[6 * r + j] = M[2 * r] * Cl[j] + M[2 * r + 1] * Cl[6 + j];
-#pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) acc[6 * i + j] += Ch[i] * N[j] + Ch[6 + i] * N[6 + j];
-}
-
-// K5: reduced camera system S (band storage) + rhs: one 256-thread workgroup per non-zero camera
-// block pair; threads stride the pair list two pairs at a time (both pairs' loads are in flight
-// before either is accumulated: the loop is load-latency bound), fixed-order wave + LDS
-// reduction.  Each (obs_h, obs_l) term is Jc_h^T M Jc_l with the 2x2 M = Q_h Jps_l^T (108 FMA,
-// 36 doubles read); the camera Jacobi scales are applied once per block.  Block pairs are sorted
-// by camera and remapped so that each XCD (blockIdx % 8 group) takes a contiguous run: the tiles
-// of a camera are re-read from that XCD's L2 instead of from the fabric.
-// FU (the fused iteration of unsharded plans, after the first): Ctot trailing workgroups do
-// k_ba_camera's work (U, V for the head of the iteration, which runs inside the Cholesky kernel,
-// lm_head) concurrently with the pair blocks.  The diagonal blocks write -a and -r only; the
-// Cholesky (k_ba_chol_2s<true>) adds U sc sc^T + D^2 and V sc as it stages the band and loads the
-// rhs: (-a) + v == v - a exactly, so the bits are those of k_ba_schur<false>.  The Jacobi scale is
-// iteration 0's.
-template <bool FU>
-__global__ __launch_bounds__(256) void k_ba_schur(BaDev d, LMOpt o, int grid_bp) {
-  __shared__ double red[4][37];
-  if (FU && (int)blockIdx.x >= grid_bp) {  // the trailing workgroups: k_ba_camera's work
-    __shared__ double redu[4][27];
-    camera_block<true>(d, blockIdx.x - grid_bp, redu);
-    return;
-  }
-  const int n_bp = d.live[1];
-  if ((int)blockIdx.x >= n_bp) return;
-  int bid;
-  {
-    const int nwg = n_bp, q = nwg / 8, r = nwg % 8, x = blockIdx.x % 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blockIdx.x / 8;
-  }
-  if (bid >= n_bp) return;
-  const BlockPair bp = d.bp[bid];
-  const WinState& S = d.st[bp.win];
-  if (S.done) return;
-  const BaWin& W = d.win[bp.win];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  double acc[36];
-#pragma unroll
-  for (int k = 0; k < 36; ++k) acc[k] = 0.0;
-  const int end = bp.off + bp.cnt;
-  // camera-major slots (obs in camera ch, obs in camera cl) of one point; the next step's pair
-  // indices are read while this step's tiles load (same pairs, same order)
-  const bool diag = bp.ch == bp.cl;
-  double r6[6] = {0, 0, 0, 0, 0, 0};
-  // A diagonal block's pairs are (e, e) for the camera's slots e in order (both plan builders),
-  // so thread t meets the observations a0 + t, a0 + t + 256, ... of the rhs sum in its order.
-  auto run = [&](auto diag_c) {
-    constexpr bool DG = decltype(diag_c)::value;
-    int q = bp.off + t;
-    int2 p0n = make_int2(0, 0), p1n = make_int2(0, 0);
-    if (q < end) { p0n = d.pairs[q]; p1n = d.pairs[q + 256 < end ? q + 256 : q]; }
-    for (; q < end; q += 512) {
-      const int2 p0 = p0n, p1 = p1n;
-      const bool two = q + 256 < end;
-      const int qn = q + 512;
-      if (qn < end) { p0n = d.pairs[qn]; p1n = d.pairs[qn + 256 < end ? qn + 256 : qn]; }
-      schur_pair<DG>(d, p0, acc, r6);
-      if (two) schur_pair<DG>(d, p1, acc, r6);
-    }
-  };
-  if (diag) run(std::true_type{});
-  else run(std::false_type{});
-#pragma unroll
-  for (int k = 0; k < 36; ++k) {
-    const double v = wave_sum(acc[k]);
-    if (lane == 0) red[wv][k] = v;
-  }
-  __syncthreads();
-  if (t < 36) {
-    const int i = t / 6, j = t % 6;
-    const double a = (((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]) *
-                     d.scale_pose[6 * bp.ch + i] * d.scale_pose[6 * bp.cl + j];
-    const int lh = bp.ch - W.pose_base, ll = bp.cl - W.pose_base;
-    double* A = d.env_part + W.env_base;
-    if (diag) {
-      if (j <= i) {
-        if (FU) {  // -a: k_ba_chol_2s<true> adds the camera block while staging the band
-          band(A, W.bw, 6 * lh + i, 6 * lh + j) = -a;
-        } else {
-          double v = 0.0;
-          if (d.rank0) {  // camera block J^T J + D^2 once (sharded: U is already global)
-            const double* sc = d.scale_pose + 6 * bp.ch;
-            v = d.U[21 * bp.ch + u21(i, j)] * sc[i] * sc[j];
-            if (i == j) v += fmin(fmax(v, o.min_diag), o.max_diag) / S.radius;
-          }
-          band(A, W.bw, 6 * lh + i, 6 * lh + j) = v - a;
-        }
-      }
-    } else {
-      band(A, W.bw, 6 * lh + i, 6 * ll + j) = -a;
-    }
-  }
-  if (diag) {
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const double v = wave_sum(r6[k]);
-      if (lane == 0) red[wv][k] = v;
-    }
-    __syncthreads();
-    if (t < 6) {
-      const double r = (((red[0][t] + red[1][t]) + red[2][t]) + red[3][t]) * d.scale_pose[6 * bp.ch + t];
-      if (FU) {  // -r: k_ba_chol_2s<true> adds V sc when it loads the rhs
-        d.rhs_part[W.row_base + 6 * (bp.ch - W.pose_base) + t] = -r;
-      } else {
-        const double vs = d.rank0 ? d.V[6 * bp.ch + t] * d.scale_pose[6 * bp.ch + t] : 0.0;
-        d.rhs_part[W.row_base + 6 * (bp.ch - W.pose_base) + t] = vs - r;
-      }
-    }
-  }
 }
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -2054,10 +1622,6 @@ struct BandSide {
 // threads, U chunks per thread per batch with all loads of a batch issued before any store.
 // Element (i, off) keeps S's value inside the matrix; the left triangle of the first bw rows is
 // zeroed and rows n .. n16-1 are an identity pad.
-struct StageFix;
-template <int U, bool FIX = false>
-__device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, double* Ab, int a0, int a1, int b0, int b1,
-                                            int tid, int nthr, int n, int bw, int nsrc, const StageFix* fx = nullptr);
 template <int U>
 __device__ __forceinline__ void stage_band(const double2* __restrict__ S2, double* Ab, int j0, int j1, int tid,
                                            int nthr, int n, int bw, int nsrc) {
@@ -2089,44 +1653,19 @@ __device__ __forceinline__ void stage_band(const double2* __restrict__ S2, doubl
 
 
 // the fused iteration's camera-block terms (stage_fix's), added by the staging thread itself
-struct StageFix {
-  const double* U; const double* sc; int pose_base; double min_diag, max_diag, radius;
-  // element (i, j), i < n: the term of its camera block (0 off the 6 x 6 diagonal blocks); the
-  // loads go out with the band chunk's
-  __device__ __forceinline__ double term(int i, int j) const {
-    const int i6 = i % 6, cb = i - i6;
-    if (j < cb) return 0.0;
-    const int j6 = j - cb, c = pose_base + i / 6;
-    double v = U[21 * c + u21(i6, j6)] * sc[6 * c + i6] * sc[6 * c + j6];
-    if (i6 == j6) v += fmin(fmax(v, min_diag), max_diag) / radius;
-    return v;
-  }
-};
-
 // the same over two chunk ranges [a0, a1) and [b0, b1), all loads of a batch before any store;
-// FIX: every element of the batch also gets its camera-block term (e + v: stage_fix's bits)
-template <int U, bool FIX>
+template <int U>
 __device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, double* Ab, int a0, int a1, int b0, int b1,
-                                            int tid, int nthr, int n, int bw, int nsrc, const StageFix* fx) {
+                                            int tid, int nthr, int n, int bw, int nsrc) {
   const int B1 = bw + 1, la = a1 - a0, tot = la + (b1 - b0);
   for (int vb = tid; vb < tot; vb += nthr * U) {
     double2 v[U];
     int jj[U];
-    double fv[FIX ? U : 1][2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int vv = vb + nthr * u;
       jj[u] = vv < la ? a0 + vv : b0 + (vv - la);
       v[u] = S2[(vv < tot && jj[u] < nsrc) ? jj[u] : 0];
-      if (FIX) {
-        int i = (2 * jj[u]) / B1, off = (2 * jj[u]) % B1;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const bool in = vv < tot && i < n && i - (bw - off) >= 0;
-          fv[u][h] = in ? fx->term(i, i + off - bw) : 0.0;
-          if (++off == B1) { off = 0; ++i; }
-        }
-      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -2138,7 +1677,6 @@ __device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, doub
         for (int h = 0; h < 2; ++h) {
           const bool in = i < n && i - (bw - off) >= 0;
           e[h] = in ? e[h] : ((i >= n && off == bw) ? 1.0 : 0.0);
-          if (FIX && in) e[h] = e[h] + fv[u][h];
           if (++off == B1) { off = 0; ++i; }
         }
         reinterpret_cast<double2*>(Ab)[j] = double2{e[0], e[1]};
@@ -2147,21 +1685,20 @@ __device__ __forceinline__ void stage_band2(const double2* __restrict__ S2, doub
   }
 }
 
-// The fused iteration's camera blocks (k_ba_schur<true> leaves -a on the diagonal camera blocks):
-// rows [r0, r1) of the staged band get v = U sc sc^T (+ D^2 on the diagonal), k_ba_schur<false>'s
-// expression, added as (-a) + v == v - a.  Threads tid, tid + nthr, ... of the caller.
+// The fused iteration's camera blocks: k_ba_red<2> stages sc (U - A) sc^T on the diagonal camera
+// blocks, so rows [r0, r1) of the staged band only get D^2 = clamp(U_ii sc_i^2) / radius on the
+// diagonal.  Threads tid, tid + nthr, ... of the caller.
 __device__ __forceinline__ void stage_fix(const BaDev& d, const LMOpt& o, double* Ab, const BaWin& W, double radius,
                                           int r0, int r1, int tid, int nthr) {
   r1 = min(r1, W.n);
   const int B1 = W.bw + 1;
   for (int q = tid; q < (r1 - r0) * 6; q += nthr) {
     const int i = r0 + q / 6, i6 = i % 6, j6 = q % 6;
-    if (j6 > i6 || (d.pm && j6 != i6)) continue;
+    if (j6 != i6) continue;
     const int c = W.pose_base + i / 6;
     const double* sc = d.scale_pose + 6 * c;
     double v = d.U[21 * c + u21(i6, j6)] * sc[i6] * sc[j6];
-    // point-major path: the staged diagonal blocks hold sc (U - A) sc^T already, only D^2 is added
-    if (i6 == j6) v = (d.pm ? 0.0 : v) + fmin(fmax(v, o.min_diag), o.max_diag) / radius;
+    v = 0.0 + fmin(fmax(v, o.min_diag), o.max_diag) / radius;
     double& e = Ab[i * B1 + (j6 - i6 + W.bw)];
     e = e + v;
   }
@@ -2176,21 +1713,16 @@ __device__ __forceinline__ double stage_fix_val(const BaDev& d, const LMOpt& o, 
   at = -1;
   if (q >= (r1 - r0) * 6) return 0.0;
   const int i = r0 + q / 6, i6 = i % 6, j6 = q % 6;
-  if (j6 > i6 || (d.pm && j6 != i6)) return 0.0;
+  if (j6 != i6) return 0.0;
   const int c = W.pose_base + i / 6;
   const double* sc = d.scale_pose + 6 * c;
   double v = d.U[21 * c + u21(i6, j6)] * sc[i6] * sc[j6];
-  if (i6 == j6) v = (d.pm ? 0.0 : v) + fmin(fmax(v, o.min_diag), o.max_diag) / radius;
+  v = 0.0 + fmin(fmax(v, o.min_diag), o.max_diag) / radius;
   at = i * (W.bw + 1) + (j6 - i6 + W.bw);
   return v;
 }
 
 constexpr int kChol2sThreads = 512;
-// 1: the first batch's camera-block terms added by the staging threads (no fix pass + barrier;
-// three more scattered loads per staged element: same-box A/B 46.2 / 46.1 -> 50.0 / 50.1 us: off)
-#ifndef LORB_CHOL_FFIX
-#define LORB_CHOL_FFIX 0
-#endif
 // 1: the epilogue's pose state loaded at the kernel's start (registers live through the kernel:
 // 232 -> 256 VGPRs of k_ba_chol_2s<true>; same-box A/B 46.4 / 45.8 vs 46.4 / 45.9 us: off)
 #ifndef LORB_CHOL_EPI_PREFETCH
@@ -2292,7 +1824,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   static_assert(16 * 4 * 6 <= kChol2sThreads, "one stage_fix item per thread");
   int fa0 = -1, fa1 = -1;
   double fv0 = 0.0, fv1 = 0.0;
-  if (HEAD && prog && !LORB_CHOL_FFIX) {
+  if (HEAD && prog) {
     fv0 = stage_fix_val(d, o, W, S0.radius, 0, 16 * ib, t, fa0);
     fv1 = stage_fix_val(d, o, W, S0.radius, 16 * (nbk - ib), n16, t, fa1);
   }
@@ -2310,15 +1842,9 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   {
     const int row = t < rt ? t : n16 - 1 - (t - rt);
     rz = (t < rt + rb && row < n) ? d.rhs[W.row_base + row] : 0.0;
-    // fused: the rhs holds -r; + V sc (k_ba_schur<false>'s vs - r, same bits).  Point-major: the
-    // rhs is complete
-    if (HEAD && !d.pm && t < rt + rb && row < n)
-      rz = rz + d.V[6 * W.pose_base + row] * d.scale_pose[6 * W.pose_base + row];
+    // (the rhs is complete: k_ba_red writes (V - R) sc)
   }
-  if (prog && HEAD && LORB_CHOL_FFIX) {  // ... with the camera-block terms added as they are staged
-    const StageFix fx{d.U, d.scale_pose, W.pose_base, o.min_diag, o.max_diag, S0.radius};
-    stage_band2<7, true>(S2, Ab, 0, ib * cpb, (nbk - ib) * cpb, nch, t, NT, n, bw, nsrc, &fx);
-  } else if (prog) {  // both sides' first ib blocks in one batch
+  if (prog) {  // both sides' first ib blocks in one batch
     stage_band2<7>(S2, Ab, 0, ib * cpb, (nbk - ib) * cpb, nch, t, NT, n, bw, nsrc);
   } else {
     stage_band<14>(S2, Ab, 0, nch, t, NT, n, bw, nsrc);
@@ -2328,7 +1854,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   for (int k = t + NT; k < rt + rb; k += NT) {  // (n16 > 464 only)
     const int row = k < rt ? k : n16 - 1 - (k - rt);
     double v = row < n ? d.rhs[W.row_base + row] : 0.0;
-    if (HEAD && !d.pm && row < n) v = v + d.V[6 * W.pose_base + row] * d.scale_pose[6 * W.pose_base + row];
     if (k < rt) zt[k] = v; else zb[k - rt] = v;
   }
   if (t == 0) {
@@ -2346,7 +1871,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     s_mask = msk;
   }
   __syncthreads();
-  if (HEAD && !(prog && LORB_CHOL_FFIX)) {  // the camera blocks of the rows staged so far
+  if (HEAD) {  // the camera blocks of the rows staged so far
     if (prog) {
       if (fa0 >= 0) Ab[fa0] = Ab[fa0] + fv0;
       if (fa1 >= 0) Ab[fa1] = Ab[fa1] + fv1;
@@ -2715,169 +2240,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
 #endif
 }
 
-// K7: point-group back-substitution: b_p -= sum_e W_e^T y_c(e) (observation phase + ordered
-// point reduction), point step / candidate (point phase), model cost change and candidate cost
-// per observation (observation phase).
-__global__ __launch_bounds__(kGB) void k_ba_backsub(BaDev d) {
-  __shared__ double sh[kGB][3], sst[kGB][3], sxn[kGB][3];
-  __shared__ double red3[3][4];
-  if ((int)blockIdx.x >= d.live[0]) return;
-  const PBlk g = d.pblk[blockIdx.x];
-  const int t = threadIdx.x;
-  // plan-structure loads of the first chunk and the point's terms go out with the window state
-  const int of = g.o0 + min(t, max(g.no - 1, 0));
-  const int c_f = g.no > 0 ? d.obs_cam[of] : -1, m_f = g.no > 0 ? d.obs_cm[of] : -1;
-  // ... and so do the point phase's terms (both iterates: cur is not known yet) and the cost
-  // phase's first-chunk observation terms, so the kernel pays three dependent round trips (the
-  // group, these, the camera-indexed ones) instead of six
-  double b[3] = {0, 0, 0}, sp[3] = {0, 0, 0}, Xa[3] = {0, 0, 0}, Xb[3] = {0, 0, 0};
-  double Ei[6] = {0, 0, 0, 0, 0, 0};
-  int po0 = 0, po1 = 0;
-  if (t < g.cnt) {
-    const int p = g.p0 + t;
-    po0 = d.pt_obs_off[p]; po1 = d.pt_obs_off[p + 1];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      sp[k] = d.scale_pt[3 * p + k];
-      b[k] = d.etb[3 * p + k] * sp[k];
-      Xa[k] = d.x_pt[0][3 * p + k];
-      Xb[k] = d.x_pt[1][3 * p + k];
-    }
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Ei[k] = d.pinv[6 * p + k];
-  }
-  const bool has_f = t < g.no;
-  const int lp_f = has_f ? d.obs_pt[of] - g.p0 : 0, fix_f = has_f ? d.obs_fix[of] : 0;
-  double Jp_f[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) Jp_f[k] = has_f ? d.obs_Jp[6 * of + k] : 0.0;
-  const double2 uv_f = has_f ? d.obs_uv[of] : double2{0.0, 0.0};
-  const double r0_f = has_f ? d.obs_r[2 * of] : 0.0, r1_f = has_f ? d.obs_r[2 * of + 1] : 0.0;
-  const WinState& S = d.st[g.win];
-  if (S.done || S.chol_fail) return;
-  const BaWin& W = d.win[g.win];
-  const int cur = S.cur;
-  // the first chunk's camera for the cost phase: the candidate pose (rotation state + translation,
-  // written by the Cholesky) or the fixed pose
-  lorb::RotVal R_f{};
-  double pc_f[6] = {0, 0, 0, 0, 0, 0};
-  if (has_f) {
-    if (c_f >= 0) {
-      R_f = d.rot_cand[c_f];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) pc_f[3 + k] = d.x_pose[cur ^ 1][6 * c_f + 3 + k];
-    } else {
-#pragma unroll
-      for (int k = 0; k < 6; ++k) pc_f[k] = d.fixed_pose[6 * fix_f + k];
-    }
-  }
-  // Jcs y of this thread's first-chunk observation, kept for the model cost change below (the
-  // camera part of J step is -Jcs y): Jc is read once
-  double ya0 = 0.0, ya1 = 0.0;
-  for (int c0 = 0; c0 < g.no; c0 += kGB) {
-    if (c0 + t < g.no) {
-      const int e = g.o0 + c0 + t;
-      const int c = c0 == 0 ? c_f : d.obs_cam[e];
-      if (c >= 0) {
-        // W^T y = Jps^T (Jcs y), W = Jcs^T Jps
-        const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
-        const int m = c0 == 0 ? m_f : d.obs_cm[e];
-        double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          const double ys = y[i] * d.scale_pose[6 * c + i];
-          a0 += d.obs_Jc[12 * m + i] * ys;
-          a1 += d.obs_Jc[12 * m + 6 + i] * ys;
-        }
-        if (c0 == 0) { ya0 = a0; ya1 = a1; }
-#pragma unroll
-        for (int j = 0; j < 3; ++j) sh[t][j] = d.obs_Jps[6 * m + j] * a0 + d.obs_Jps[6 * m + 3 + j] * a1;
-      } else {
-        sh[t][0] = sh[t][1] = sh[t][2] = 0.0;
-      }
-    }
-    __syncthreads();
-    if (t < g.cnt) {
-      const int a = max(po0, g.o0 + c0), z = min(po1, g.o0 + c0 + kGB);
-      for (int e = a; e < z; ++e) {
-        if (d.obs_cam[e] < 0) continue;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) b[j] -= sh[e - g.o0 - c0][j];
-      }
-    }
-    __syncthreads();
-  }
-  double sn2 = 0.0;
-  if (t < g.cnt) {
-    const int p = g.p0 + t;
-    double X[3], step[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) X[k] = cur ? Xb[k] : Xa[k];
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      step[j] = -(s3(Ei, j, 0) * b[0] + s3(Ei, j, 1) * b[1] + s3(Ei, j, 2) * b[2]);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const double xn = X[j] + step[j] * sp[j];
-      d.x_pt[cur ^ 1][3 * p + j] = xn;
-      sxn[t][j] = xn;
-      sst[t][j] = step[j] * sp[j];
-      if (po1 > po0) sn2 += (X[j] - xn) * (X[j] - xn);
-    }
-  }
-  __syncthreads();
-  double mcc = 0.0, ncost = 0.0;
-  for (int c0 = t; c0 < g.no; c0 += kGB) {
-    const int e = g.o0 + c0;
-    const bool first = c0 == t;  // (the prefetched terms: e == of)
-    const int c = first ? c_f : d.obs_cam[e];
-    const int lp = first ? lp_f : d.obs_pt[e] - g.p0;
-    const double Xn[3] = {sxn[lp][0], sxn[lp][1], sxn[lp][2]};
-    double m0 = 0.0, m1 = 0.0;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      m0 += (first ? Jp_f[j] : d.obs_Jp[6 * e + j]) * sst[lp][j];
-      m1 += (first ? Jp_f[3 + j] : d.obs_Jp[6 * e + 3 + j]) * sst[lp][j];
-    }
-    const double2 uv = first ? uv_f : d.obs_uv[e];
-    double rn[2];
-    if (c >= 0) {
-      if (first) {
-        m0 -= ya0;
-        m1 -= ya1;
-      } else {  // observations beyond the first chunk (points with > kGB observations)
-        const double* y = d.ycam + W.row_base + 6 * (c - W.pose_base);
-        const int m = d.obs_cm[e];
-        double a0 = 0.0, a1 = 0.0;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          const double ys = y[k] * d.scale_pose[6 * c + k];
-          a0 += d.obs_Jc[12 * m + k] * ys;
-          a1 += d.obs_Jc[12 * m + 6 + k] * ys;
-        }
-        m0 -= a0;
-        m1 -= a1;
-      }
-      // candidate camera (end of k_ba_chol): x_pose[cur ^ 1] with its rotation state
-      if (first) residual_s(R_f, pc_f + 3, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
-      else residual_s(d.rot_cand[c], d.x_pose[cur ^ 1] + 6 * c + 3, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
-    } else {
-      double pose[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) pose[k] = first ? pc_f[k] : d.fixed_pose[6 * d.obs_fix[e] + k];
-      residual(pose, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
-    }
-    const double r0 = first ? r0_f : d.obs_r[2 * e], r1 = first ? r1_f : d.obs_r[2 * e + 1];
-    mcc += m0 * (r0 + m0 / 2.0) + m1 * (r1 + m1 / 2.0);
-    ncost += 0.5 * (rn[0] * rn[0] + rn[1] * rn[1]);
-  }
-  block_red3<false>(mcc, ncost, sn2, red3);
-  if (t == 0) {
-    double* P = d.part + 8 * blockIdx.x;
-    P[3] = mcc; P[4] = ncost; P[5] = sn2;
-  }
-}
-
 // the iteration's record (lorb_lm_iteration; S is the state the step was computed from)
 __device__ __forceinline__ void lm_record(const BaDev& d, int w, const WinState& S, int outcome, double mcc,
                                           double ncost, double step_norm) {
@@ -2944,7 +2306,7 @@ __device__ int lm_decide(BaDev d, const LMOpt& o, int w, WinState S, bool valid,
 
 // K8: per-window iteration tail: camera candidate, step validity, tolerances, accept/reject, on one
 // wavefront (no workgroup barrier: the decision is broadcast with readfirstlane).  (Run instead by
-// the last-finishing point group of k_ba_backsub -- a per-window counter behind agent-scope
+// the last-finishing point group of the back-substitution -- a per-window counter behind agent-scope
 // release / acquire fences -- it measured far slower: on the 8-XCD device those fences write back
 // and invalidate L2, C4 step 1.076 -> 1.294 ms.)
 template <bool SH>
@@ -2988,14 +2350,14 @@ __device__ __forceinline__ void lm_end_run(const BaDev& d, const LMOpt& o, int w
     mccs = wave_sum(mccs); ncost = wave_sum(ncost); sn2 = wave_sum(sn2);
     if (SH) { mccs += d.wstep[3 * w]; ncost += d.wstep[3 * w + 1]; sn2 += d.wstep[3 * w + 2]; }
   }
-  // point-block / Cholesky failures are per iteration: cleared here for the next one (k_ba_lin
+  // point-block / Cholesky failures are per iteration: cleared here for the next one (k_ba_ls
   // sets them before k_ba_lm_begin runs)
   S.chol_fail = 0;
   if (SH && lane == 0) d.wfail_part[w] = 0.0;
   int acc = 0;
   if (lane == 0) acc = lm_decide(d, o, w, S, valid, mccs, ncost, sn2);
   acc = __builtin_amdgcn_readfirstlane(acc);  // lane 0's decision, wave-uniform
-  // accepted: the candidate is the new linearisation point -> its rotation states for k_ba_lin
+  // accepted: the candidate is the new linearisation point -> its rotation states for k_ba_ls
   // (an accepted step is a valid one, so the first 64 candidates are already in registers)
   if (acc) {
     if (lane < W.n_poses) d.rot_lin[W.pose_base + lane] = lorb::rot_jet(xc);
@@ -3009,9 +2371,9 @@ __global__ __launch_bounds__(64) void k_ba_lm_end(BaDev d, LMOpt o) {
 }
 
 // ==========================================================================================
-// Point-major path ("PM").  The pair-major path above materialises 34 doubles
-// per observation (k_ba_lin) and re-reads them once per camera block pair a point takes part in
-// (k_ba_schur: k (k + 1) / 2 pairs for a point seen k times).  Here one kernel per point group
+// Point-major Schur path ("PM"; the only one since round 6).  Round 4's
+// pair-major path materialised 34 doubles per observation and re-read them once per camera block
+// pair a point takes part in (k (k + 1) / 2 pairs for a point seen k times).  Here one kernel per point group
 // linearises its observations, eliminates its points and forms the group's contributions to the
 // reduced camera system on chip, and writes ONE partial per (group, camera block) of its camera
 // window; a second kernel sums the partials of each block in a fixed group order (deterministic, no
@@ -3100,7 +2462,7 @@ __device__ __forceinline__ void pm_lin(const BaDev& d, const BaWin& W, int cur, 
 //   D (block row)    thread = (slot, row i): sum over the group's points in point order of row i of
 //                    Jc_h^T K Jc_l (K = I - Q_h Jps_l^T on the diagonal, -Q_h Jps_l^T off it), plus
 //                    the camera terms on the diagonal; written to the group's partial.
-// Cost, point gradient max and |x|^2 partials as k_ba_lin (the head reads them when relinearising).
+// Cost, point gradient max and |x|^2 partials per group (the head reads them when relinearising).
 __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
   __shared__ double s_jc[kGB][12];   // B / C: per point Ei (0..5), bs (6..8), sp (9..11); D: Jc per slot
   __shared__ double s_qj[kGB][12];   // A / B: Jp^T Jp (6) | Jp^T r (3) per observation; D: Q | Jps per slot
@@ -3387,7 +2749,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
 // candidate groups of each 256-group chunk are compacted in order, subset s takes every nsub-th.
 // MODE 0: the camera terms of the diagonal blocks only (U diag, V: the iteration head's inputs,
 //         before k_ba_lm_begin fixes the iteration-0 Jacobi scale);
-// MODE 1: the band with D^2 on the diagonal (rank 0) and the rhs (V - R) sc (k_ba_schur<false>'s
+// MODE 1: the band with D^2 on the diagonal (rank 0) and the rhs (V - R) sc (round 4's pair-major
 //         result, for the Cholesky without a head);
 // MODE 2: the fused iteration: band without D^2 (k_ba_chol_2s<true> adds it), rhs, U diag and V.
 // RT threads per block (256 or 1024: red_threads() picks per plan -- 1024 when a block has many
@@ -3540,7 +2902,7 @@ __global__ __launch_bounds__(RT) void k_ba_red(BaDev d, LMOpt o) {
   }
 }
 
-// PM-K3: point-group back-substitution (k_ba_backsub's phases) with the linearisation re-evaluated
+// PM-K3: point-group back-substitution with the linearisation re-evaluated
 // in registers instead of read back: b_p -= sum_e Jps_e^T (Jc_e y_c(e)), the point step and
 // candidate, then the model cost change and the candidate cost per observation.
 __global__ __launch_bounds__(kGB) void k_ba_bs2(BaDev d) {
@@ -3940,21 +3302,19 @@ struct lorb_ba_devbuild {
   int* cov = nullptr;         // C * C
   int* cam_cnt = nullptr;     // C
   unsigned long long* bits = nullptr;
-  int* hist = nullptr; int hist_cap = 0;  // camera-major block histograms
-  int* cam_pt = nullptr;      // K_cap: point of each camera-major slot
   int* perm = nullptr;        // C: input camera -> plan camera
-  int pblk_cap = 0, bp_cap = 0, pairs_cap = 0, part_cap = 0, gspan_cap = 0;
-  int gpart_cap = 0;  // doubles of BaDev::gpart (point-major path)
+  int pblk_cap = 0, bp_cap = 0, part_cap = 0, gspan_cap = 0;
+  size_t gpart_cap = 0;  // doubles of BaDev::gpart (the point groups' partials)
   std::vector<int> h_hdr, h_cov, h_cam;
   int* pinned = nullptr; size_t pinned_n = 0;
   double* sol_part = nullptr; size_t sol_n = 0;  // this rank's solve block (== the global one unsharded)
   bool dirty = true;  // the build scratch needs a clearing fill (first build, or after a failed one)
   bool sorted_hint = false;  // the caller's slots are sorted by point: try k_db_sorted first
   std::vector<double> h_red;                     // sharded: the build's host all-reduce
-  // per-build structure uploaded in one copy: [BaWin | live (2) | perm (C) | cam_obs_off (C+1) | bp (up_bp_cap)]
+  // per-build structure uploaded in one copy: [BaWin | live (2) | perm (C) | gcam (C) | bp (up_bp_cap)]
   unsigned char* up_dev = nullptr; unsigned char* up_host = nullptr; int up_bp_cap = 0;
   const unsigned char* up_host_dev = nullptr;  // up_host as the device reads it (pinned, mapped)
-  size_t off_live = 0, off_perm = 0, off_camoff = 0, off_gcam = 0, off_bp = 0, up_bytes = 0;
+  size_t off_live = 0, off_perm = 0, off_gcam = 0, off_bp = 0, up_bytes = 0;
   int* gcam = nullptr;  // device: observations per input camera over all ranks (camera activity)
   // camera_order is a function of the adjacency pattern alone: a build whose pattern equals the
   // previous one's (a sliding window usually keeps its banded pattern) reuses that order
@@ -4010,7 +3370,7 @@ struct lorb_ba_plan {
               "buffers %.2f staging %.2f launch %.2f\n", hp_us / hp_n, hp_n, hp_sec[0] / hp_n, hp_sec[1] / hp_n,
               hp_sec[2] / hp_n, hp_sec[3] / hp_n, hp_sec[4] / hp_n, hp_sec[5] / hp_n);
     // LORB_PM_SPANS=1 (diagnostics): the point groups' camera spans of the last linearisation
-    if (dev.pm && dev.gspan && n_pblk > 0 && getenv("LORB_PM_SPANS")) {
+    if (dev.gspan && n_pblk > 0 && getenv("LORB_PM_SPANS")) {
       std::vector<int2> gs(n_pblk);
       if (hipStreamSynchronize(ctx->stream) == hipSuccess &&
           hipMemcpy(gs.data(), dev.gspan, sizeof(int2) * n_pblk, hipMemcpyDeviceToHost) == hipSuccess) {
@@ -4024,7 +3384,7 @@ struct lorb_ba_plan {
     }
 #ifdef LORB_LS_STAMPS
     // LORB_LS_PRINT=1: the last k_ba_ls launch's phase cycles (medians over the point groups)
-    if (dev.pm && dev.dbg && n_pblk > 0 && getenv("LORB_LS_PRINT")) {
+    if (dev.dbg && n_pblk > 0 && getenv("LORB_LS_PRINT")) {
       std::vector<unsigned long long> st((size_t)n_pblk * 8);
       if (hipStreamSynchronize(ctx->stream) == hipSuccess &&
           hipMemcpy(st.data(), dev.dbg, sizeof(unsigned long long) * st.size(), hipMemcpyDeviceToHost) == hipSuccess) {
@@ -4164,23 +3524,30 @@ std::vector<int> camera_order(int C, const std::vector<char>& adj) {
   return camera_band(C, adj, pos) < camera_band(C, adj, id) ? pos : id;
 }
 
-// Point-major path (PM): windows of at most 64 optimised cameras (a group's camera window is a 64-bit
-// mask) whose points fit one group (C + F <= kGB observations per point); LORB_PM=0 keeps the
-// pair-major path (A/B, diagnostics)
-bool pm_fits(int C, int F) { return C <= 128 && C + F <= kGB; }
-bool pm_enabled() {
-  static const bool on = [] { const char* e = getenv("LORB_PM"); return !(e && e[0] == '0'); }();
-  return on;
-}
-// a window's partial layout: camera half band, slots of a full-width window, the camera terms after
-// them; its groups' partials from `total` on (advanced)
-void pm_layout(BaWin& bw, long long& total) {
-  const int C = bw.n_poses;
+// Point groups and their partials.  A group's camera window [cmin, cmin + span) is held by
+// k_ba_ls as two 64-bit words per point, so a group spans at most kPmSpan cameras: device-built
+// plans (one window of C cameras) take C <= kPmSpan; host-built plans cut a group where the next
+// point would widen it past kPmSpan (any C, as long as no single point's cameras lie more than
+// kPmSpan apart in the plan's camera order).
+constexpr int kPmSpan = 128;
+// the partial budget of one plan: a group's partial holds the camera blocks of a
+// window of `span_max` cameras; far above every workload here (C4: 5 MB, the shared window: 0.3 GB)
+constexpr size_t kPartBudgetBytes = (size_t)16 << 30;
+// a window's partial layout: camera half band, the slots of a group window of span_max cameras, the
+// camera terms after them; its groups' partials from `total` on (advanced)
+void pm_layout(BaWin& bw, int span_max, long long& total) {
   bw.bwc = bw.n > 0 ? std::max(bw.bw - 5, 0) / 6 : 0;
-  bw.part_cam = 36 * pm_nslots(C, bw.bwc);
-  bw.part_stride = bw.part_cam + 18 * C;
+  span_max = std::max(std::min(span_max, bw.n_poses), 0);
+  bw.part_cam = 36 * pm_nslots(span_max, bw.bwc);
+  bw.part_stride = bw.part_cam + 18 * span_max;
   bw.part_base = total;
   total += (long long)bw.n_pblk * bw.part_stride;
+}
+int part_budget_check(lorb_ctx* ctx, long long total) {
+  if ((size_t)std::max(total, 1ll) * sizeof(double) > kPartBudgetBytes)
+    return lorb::set_error(ctx, LORB_E_NOMEM, "point-group partials need %.1f GB (> %.0f GB budget)",
+                           (double)total * sizeof(double) / 1e9, (double)kPartBudgetBytes / 1e9);
+  return LORB_OK;
 }
 
 int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan* P) {
@@ -4266,18 +3633,15 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
     }
   }
   std::vector<int> cam_active;
-  std::vector<int> pt_obs_off(1, 0), obs_cam, obs_fix, obs_pt, cam_obs_off(1, 0), cam_obs, cam_win, obs_cm;
+  std::vector<int> pt_obs_off(1, 0), obs_cam, obs_fix, obs_pt;
   std::vector<double2> obs_uv;
   std::vector<double> fixed, xpose, xpt;
   std::vector<PBlk> pblk;
   std::vector<BlockPair> bps;
-  std::vector<int2> pairs;
-  int pose_base = 0, point_base = 0, fix_base = 0, env_base = 0, row_base = 0;
+  int pose_base = 0, point_base = 0, fix_base = 0, env_base = 0, row_base = 0, n_pairs = 0;
   long long part_total = 0;
-  bool pm_ok = true;
   for (int w = 0; w < nw; ++w) {
     const lorb_ba_window& in = win[w];
-    pm_ok = pm_ok && pm_fits(in.n_poses, in.n_fixed);
     if (in.n_poses < 0 || in.n_points < 0 || in.n_obs < 0 || in.n_fixed < 0)
       return lorb::set_error(ctx, LORB_E_INVALID, "window %d: negative sizes", w);
     BaWin bw{};
@@ -4309,19 +3673,16 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
     for (int i = 0; i < 6 * in.n_fixed; ++i) fixed.push_back(in.fixed_pose[i]);
     for (int i = 0; i < 6 * in.n_poses; ++i) xpose.push_back(in.pose_init[i]);
     for (int i = 0; i < 3 * in.n_points; ++i) xpt.push_back(in.point_init[i]);
-    // camera-major obs lists (sorted by point == by sorted obs index)
-    std::vector<std::vector<int>> co(in.n_poses);
-    for (int e = 0; e < in.n_obs; ++e) { const int c = obs_cam[ob0 + e]; if (c >= 0) co[c - pose_base].push_back(ob0 + e); }
-    obs_cm.resize(obs_cam.size(), -1);
-    for (int c = 0; c < in.n_poses; ++c) {
-      for (int e : co[c]) { obs_cm[e] = (int)cam_obs.size(); cam_obs.push_back(e); }
-      cam_obs_off.push_back((int)cam_obs.size());
-      cam_win.push_back(w);
-      cam_active.push_back(comm ? (g_cam_obs[w][c] > 0) : !co[c].empty());
+    // camera activity: observed by this rank (sharded: by some rank)
+    {
+      std::vector<int> n_cam(in.n_poses, 0);
+      for (int e = 0; e < in.n_obs; ++e) { const int c = obs_cam[ob0 + e]; if (c >= 0) n_cam[c - pose_base]++; }
+      for (int c = 0; c < in.n_poses; ++c) cam_active.push_back(comm ? (g_cam_obs[w][c] > 0) : n_cam[c] > 0);
     }
-    // block pairs: for each point, all ordered (obs_h, obs_l) with cam(h) >= cam(l)
-    std::map<std::pair<int, int>, std::vector<int2>> bmap;
-    for (int c = 0; c < in.n_poses; ++c) bmap[{c, c}];  // every diagonal block exists
+    // camera blocks (ch, cl), ch >= cl, that some point couples, with their observation-pair counts
+    // (every diagonal block exists); the first coupled camera of each row for the band
+    std::map<std::pair<int, int>, int> bmap;
+    for (int c = 0; c < in.n_poses; ++c) bmap[{c, c}];
     std::vector<int> fc(in.n_poses);
     for (int c = 0; c < in.n_poses; ++c) fc[c] = c;
     for (int p = 0; p < in.n_points; ++p) {
@@ -4333,20 +3694,17 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
           const int cb = obs_cam[b];
           if (cb < 0 || cb > ca) continue;
           // the reference keys a point's observations by Frame* (include/map_point.h:83): one per
-          // camera; the diagonal blocks rely on it (their pairs are (e, e))
+          // camera (k_ba_ls places a point's observations by camera rank)
           if (cb == ca && a != b)
             return lorb::set_error(ctx, LORB_E_INVALID, "window %d: a point observed twice by one camera", w);
-          bmap[{ca - pose_base, cb - pose_base}].push_back(make_int2(obs_cm[a], obs_cm[b]));
+          bmap[{ca - pose_base, cb - pose_base}]++;
           fc[ca - pose_base] = std::min(fc[ca - pose_base], cb - pose_base);
         }
       }
     }
     for (auto& kv : bmap) {
-      BlockPair b;
-      b.win = w; b.ch = pose_base + kv.first.first; b.cl = pose_base + kv.first.second;
-      b.off = (int)pairs.size(); b.cnt = (int)kv.second.size();
-      pairs.insert(pairs.end(), kv.second.begin(), kv.second.end());
-      bps.push_back(b);
+      bps.push_back(BlockPair{w, pose_base + kv.first.first, pose_base + kv.first.second, n_pairs, kv.second});
+      n_pairs += kv.second;
     }
     // uniform band of S: bw = max_i (i - first_nonzero_col(i)); exact for Cholesky (no fill
     // outside the envelope, and the zero padding never changes a value)
@@ -4370,46 +3728,45 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
       if (n16 > 0) P->min_n16 = std::min(P->min_n16, n16);
     }
     env_base += bw.env_size; row_base += n;
-    // point groups: consecutive points with <= kGB observations (and <= kGB points) in total
+    // point groups: consecutive points with <= kGB observations (and <= kGB points) in total whose
+    // optimised cameras span <= kPmSpan (k_ba_ls's camera masks); the widest group sizes the partials
     bw.pblk_base = (int)pblk.size();
+    int span_max = 0;
     for (int p = 0; p < in.n_points;) {
       PBlk g{w, point_base + p, 0, ob0 + cnt[p], 0};
+      int gmin = INT32_MAX, gmax = -1;
       while (p < in.n_points && g.cnt < kGB) {
         const int k = cnt[p + 1] - cnt[p];
-        if (g.cnt > 0 && g.no + k > kGB) break;
+        int pmin = INT32_MAX, pmax = -1;
+        for (int e = ob0 + cnt[p]; e < ob0 + cnt[p + 1]; ++e)
+          if (obs_cam[e] >= 0) { pmin = std::min(pmin, obs_cam[e]); pmax = std::max(pmax, obs_cam[e]); }
+        if (k > kGB)
+          return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "window %d: point %d has %d observations (a point group holds %d)",
+                                 w, p, k, kGB);
+        if (pmax - pmin >= kPmSpan)
+          return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "window %d: point %d is seen by cameras %d apart (at most %d)",
+                                 w, p, pmax - pmin, kPmSpan - 1);
+        const int nmin = std::min(gmin, pmin), nmax = std::max(gmax, pmax);
+        if (g.cnt > 0 && (g.no + k > kGB || (nmax >= 0 && nmax - nmin >= kPmSpan))) break;
         g.cnt++; g.no += k; ++p;
+        gmin = nmin; gmax = nmax;
       }
+      if (gmax >= 0) span_max = std::max(span_max, gmax - gmin + 1);
       pblk.push_back(g);
     }
     bw.n_pblk = (int)pblk.size() - bw.pblk_base;
-    pm_layout(bw, part_total);
+    pm_layout(bw, span_max, part_total);
     P->hwin.push_back(bw);
     pose_base += in.n_poses; point_base += in.n_points; fix_base += in.n_fixed;
   }
   P->Ctot = pose_base; P->Ptot = point_base; P->K = (int)obs_cam.size(); P->NF = fix_base;
-  {
-    // k_ba_schur gives XCD x a contiguous run of block pairs (camera locality in its L2).  When
-    // the pairs fill the CUs once but not twice (256 < n <= 512, one C4 window: 372), sort each
-    // run heaviest first, so the workgroups that double up on a CU are the light ones.  Fewer
-    // pairs never share a CU; with many (8 windows) the camera order of the runs matters more
-    // (measured: C4 Schur 27.1 -> 23.4 us, 8 x C4 86.7 -> 111.5 us if sorted).
-    const int nwg = (int)bps.size(), q = nwg / 8, r = nwg % 8;
-    std::vector<int> cam_n(cam_obs_off.size() > 0 ? cam_obs_off.size() - 1 : 0);
-    for (size_t c = 0; c + 1 < cam_obs_off.size(); ++c) cam_n[c] = cam_obs_off[c + 1] - cam_obs_off[c];
-    auto weight = [&](const BlockPair& b) { return (int64_t)b.cnt + (b.ch == b.cl ? cam_n[b.ch] / 2 : 0); };
-    for (int x = 0; x < 8 && nwg > 256 && nwg <= 512; ++x) {
-      const int a = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
-      const int len = x < r ? q + 1 : q;
-      std::stable_sort(bps.begin() + a, bps.begin() + a + len,
-                       [&](const BlockPair& u, const BlockPair& v) { return weight(u) > weight(v); });
-    }
-  }
-  P->n_pblk = (int)pblk.size(); P->n_bp = (int)bps.size(); P->n_pairs = (int)pairs.size();
+  LORB_TRY(part_budget_check(ctx, part_total));
+  P->n_pblk = (int)pblk.size(); P->n_bp = (int)bps.size(); P->n_pairs = n_pairs;
   P->env_total = env_base; P->n_total = row_base;
   P->grid_pblk = P->n_pblk; P->grid_bp = P->n_bp; P->pt_launch = P->Ptot;
   BaDev& d = P->dev;
-  BaWin* dwin; PBlk* dpb; BlockPair* dbp; int2* dpairs; double2* duv;
-  int *a1, *a2, *a3, *a4, *a5, *a6;
+  BaWin* dwin; PBlk* dpb; BlockPair* dbp; double2* duv;
+  int *a1, *a2, *a3;
   double* dfix;
   LORB_TRY(dupload(P, P->hwin, &dwin)); d.win = dwin;
   LORB_TRY(dupload(P, std::vector<int>{P->n_pblk, P->n_bp}, &P->live)); d.live = P->live;
@@ -4417,16 +3774,10 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   int* dopt;
   LORB_TRY(dupload(P, obs_pt, &dopt)); d.obs_pt = dopt;
   LORB_TRY(dupload(P, bps, &dbp)); d.bp = dbp;
-  LORB_TRY(dupload(P, pairs, &dpairs)); d.pairs = dpairs;
   LORB_TRY(dupload(P, pt_obs_off, &a1)); d.pt_obs_off = a1;
   LORB_TRY(dupload(P, obs_cam, &a2)); d.obs_cam = a2;
   LORB_TRY(dupload(P, obs_fix, &a3)); d.obs_fix = a3;
   LORB_TRY(dupload(P, obs_uv, &duv)); d.obs_uv = duv;
-  LORB_TRY(dupload(P, cam_obs_off, &a4)); d.cam_obs_off = a4;
-  LORB_TRY(dupload(P, cam_obs, &a5)); d.cam_obs = a5;
-  int* acm = nullptr;
-  LORB_TRY(dupload(P, obs_cm, &acm)); d.obs_cm = acm;
-  LORB_TRY(dupload(P, cam_win, &a6)); d.cam_win = a6;
   LORB_TRY(dupload(P, fixed, &dfix)); d.fixed_pose = dfix;
   LORB_TRY(dupload(P, xpose, &d.x_init_pose));
   LORB_TRY(dupload(P, xpt, &d.x_init_pt));
@@ -4434,9 +3785,9 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   LORB_TRY(dupload(P, xpose, &d.x_pose[1]));
   LORB_TRY(dupload(P, xpt, &d.x_pt[0]));
   LORB_TRY(dupload(P, xpt, &d.x_pt[1]));
-  const size_t C = P->Ctot, Pn = P->Ptot, K = P->K;
+  const size_t C = P->Ctot, Pn = P->Ptot;
   LORB_TRY(dalloc(P, C * 6, &d.scale_pose)); LORB_TRY(dalloc(P, Pn * 3, &d.scale_pt));
-  LORB_TRY(dalloc(P, Pn * 6, &d.ete)); LORB_TRY(dalloc(P, Pn * 3, &d.etb)); LORB_TRY(dalloc(P, Pn * 6, &d.pinv));
+  LORB_TRY(dalloc(P, Pn * 3, &d.etb)); LORB_TRY(dalloc(P, Pn * 6, &d.pinv));
   int* dact = nullptr;
   LORB_TRY(dupload(P, cam_active, &dact)); d.cam_active = dact;
   // exchange buffers (see BaDev); unsharded plans alias *_part to the global buffers
@@ -4465,12 +3816,8 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   d.wstep = stp; d.wstep_part = stpp;
   d.sharded = comm ? 1 : 0;
   d.rank0 = comm ? (comm->rank == 0) : 1;
-  LORB_TRY(dalloc(P, C, &d.cam_gmax));
-  LORB_TRY(dalloc(P, K * 2, &d.obs_r)); LORB_TRY(dalloc(P, K * 6, &d.obs_Jp)); LORB_TRY(dalloc(P, K * 12, &d.obs_Jc));
-  LORB_TRY(dalloc(P, K * 2, &d.cam_r));
   LORB_TRY(dalloc(P, (size_t)P->Ctot, &d.rot_lin));
   LORB_TRY(dalloc(P, (size_t)P->Ctot, &d.rot_cand));
-  LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
   if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, ctx->stream));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
 #ifdef LORB_CHOL_TRACE
@@ -4483,12 +3830,8 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   LORB_TRY(dalloc(P, ((size_t)P->n_total / 16 + nw + 1) * 1024, &d.kco));
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
   LORB_TRY(dalloc(P, (size_t)nw * LORB_LM_TRACE_CAP, &d.trace));
-  d.pm = pm_ok && pm_enabled() ? 1 : 0;
-  if (d.pm) {
-    LORB_TRY(dalloc(P, (size_t)std::max(part_total, 1ll), &d.gpart));
-    LORB_TRY(dalloc(P, (size_t)std::max(P->n_pblk, 1), &d.gspan));
-  }
-  if (!obs_cam.empty()) { /* keep obs arrays alive via allocs */ }
+  LORB_TRY(dalloc(P, (size_t)std::max(part_total, 1ll), &d.gpart));
+  LORB_TRY(dalloc(P, (size_t)std::max(P->n_pblk, 1), &d.gspan));
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return LORB_OK;
 }
@@ -4546,21 +3889,14 @@ lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
 int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = P->ctx->stream;
   const BaDev& d = P->dev;
-  if (d.pm) {  // point-major: the group partials, then the camera terms of the head
-    if (P->grid_pblk) {
-      lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-      hipLaunchKernelGGL(k_ba_ls, dim3(P->grid_pblk), dim3(kLsThreads), 0, s, d, o);
-    }
-    if (P->grid_bp) {
-      lorb::KernelTimer kt(P->ctx, LORB_K_BA_SCHUR);
-      launch_red<0>(P, s, d, o);
-    }
-  } else {
-    if (P->grid_pblk) {
-      lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-      hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
-    }
-    if (P->Ctot) hipLaunchKernelGGL(k_ba_camera, dim3(P->Ctot), dim3(256), 0, s, d);
+  // the group partials, then the camera terms of the head
+  if (P->grid_pblk) {
+    lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
+    hipLaunchKernelGGL(k_ba_ls, dim3(P->grid_pblk), dim3(kLsThreads), 0, s, d, o);
+  }
+  if (P->grid_bp) {
+    lorb::KernelTimer kt(P->ctx, LORB_K_BA_SCHUR);
+    launch_red<0>(P, s, d, o);
   }
   if (P->comm) {  // exchange 1: camera blocks + cost / |x|^2 (sum), gradient max (max)
     hipLaunchKernelGGL(k_ba_win_reduce<0>, dim3(P->W), dim3(64), 0, s, d);
@@ -4576,11 +3912,11 @@ int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   return LORB_OK;
 }
 
-// one LM iteration on the ctx stream.  first: the full sequence lin -> camera -> lm_begin -> schur
-// -> chol -> backsub -> lm_end.  Later iterations of an unsharded plan on the two-sided Cholesky run
-// fused: the diagonal Schur blocks form the camera normal blocks (k_ba_camera's work; the Jacobi
-// scale is iteration 0's) and the head runs inside the Cholesky (k_ba_lm_begin's work), so lin ->
-// schur -> chol -> backsub -> lm_end -- five launches instead of seven, the same bits.
+// one LM iteration on the ctx stream.  first: k_ba_ls -> k_ba_red<0> (camera terms) -> k_ba_lm_begin
+// -> k_ba_red<1> -> Cholesky -> k_ba_bs2 -> k_ba_lm_end.  Later iterations of an unsharded plan on
+// the two-sided Cholesky run fused: k_ba_red<2> writes the band, rhs and camera terms at once (the
+// Jacobi scale is iteration 0's) and the head runs inside the Cholesky (k_ba_lm_begin's work), so
+// k_ba_ls -> k_ba_red<2> -> k_ba_chol_2s<true> -> k_ba_bs2 -> k_ba_lm_end: five launches.
 int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
   lorb_ctx* ctx = P->ctx;
   hipStream_t s = ctx->stream;
@@ -4590,27 +3926,20 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
   if (fused) {
     if (P->grid_pblk) {
       lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-      if (d.pm) hipLaunchKernelGGL(k_ba_ls, dim3(P->grid_pblk), dim3(kLsThreads), 0, s, d, o);
-      else hipLaunchKernelGGL(k_ba_lin, dim3(P->grid_pblk), dim3(kGB), 0, s, d, o);
+      hipLaunchKernelGGL(k_ba_ls, dim3(P->grid_pblk), dim3(kLsThreads), 0, s, d, o);
     }
   } else {
     LORB_TRY(enqueue_linearize(P, o));
   }
-  // The LDS Cholesky never writes env, and k_ba_schur / k_ba_red rewrite every stored entry of
+  // The LDS Cholesky never writes env, and k_ba_red rewrites every stored entry of
   // every block each iteration, so the band's structural zeros (set at plan creation) persist; the
   // in-place global variant needs them restored.
   const bool chol_in_lds = sizeof(double) * (size_t)P->max_env <= (size_t)kLdsBudget;
   if (P->env_total && !chol_in_lds && !P->comm) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, s));
   if (P->grid_bp) {
     lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
-    if (d.pm) {
-      if (fused) launch_red<2>(P, s, d, o);
-      else launch_red<1>(P, s, d, o);
-    } else if (fused) {
-      hipLaunchKernelGGL(k_ba_schur<true>, dim3(P->grid_bp + P->Ctot), dim3(256), 0, s, d, o, (int)P->grid_bp);
-    } else {
-      hipLaunchKernelGGL(k_ba_schur<false>, dim3(P->grid_bp), dim3(256), 0, s, d, o, (int)P->grid_bp);
-    }
+    if (fused) launch_red<2>(P, s, d, o);
+    else launch_red<1>(P, s, d, o);
   }
   if (P->comm && fused) {
     // the fused sharded iteration: the point partials of the head, then exchanges 1 and 2 as one
@@ -4648,10 +3977,7 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
     else { if (rpl == 1) LORB_CHOL(false, 1); else if (rpl == 2) LORB_CHOL(false, 2); else if (rpl == 4) LORB_CHOL(false, 4); else LORB_CHOL(false, 8); }
 #undef LORB_CHOL
   }
-  if (P->grid_pblk) {
-    if (d.pm) hipLaunchKernelGGL(k_ba_bs2, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
-    else hipLaunchKernelGGL(k_ba_backsub, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
-  }
+  if (P->grid_pblk) hipLaunchKernelGGL(k_ba_bs2, dim3(P->grid_pblk), dim3(kGB), 0, s, d);
   if (P->comm) {  // exchange 3: model cost change, candidate cost, point |step|^2
     hipLaunchKernelGGL(k_ba_win_reduce<1>, dim3(P->W), dim3(64), 0, s, d);
     {
@@ -4759,13 +4085,9 @@ int plan_read(lorb_ba_plan* P, double* const* pose_out, double* const* point_out
 //   k_db_scatter counting sort by point: slot order within a point restored by k_db_segsort
 //                (stable: the caller's order within a point, as a stable radix sort gives it)
 //   k_db_cov     covisibility counts of camera pairs = popcount(bits_a & bits_b), per-camera counts
-//   k_db_gather  point-sorted structure arrays, per-block camera histograms (RCM labels), initial
-//                values (float -> double, camera relabelling), point groups of <= kGB observations
-//                (weights k + 1, fixed-size bins), and the zeros the next build starts from
-//   k_db_scan1   camera-major block offsets
-//   k_db_place   counting sort of the optimised observations by camera (stable), camera slots
-//   k_db_pairs   per block pair: the points both cameras observe (binary search of the lower
-//                camera's point list staged in LDS)
+//   k_db_gather  point-sorted observation records (RCM camera labels), initial values (float ->
+//                double, camera relabelling), point groups of <= kGB observations (weights k + 1,
+//                fixed-size bins), and the zeros the next build starts from
 // ==========================================================================================
 
 namespace {
@@ -4829,12 +4151,10 @@ constexpr int kDbFuseLds = 64 * 1024;  // LDS bytes the FUSE tables may take
 template <bool FUSE>
 __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, int F, int Wd, int* __restrict__ pt_off,
                                                    int* __restrict__ hdr, unsigned long long* __restrict__ bits,
-                                                   int* __restrict__ cov, int* __restrict__ cam_cnt,
-                                                   int* __restrict__ hist) {
-  extern __shared__ unsigned long long s_bits[];  // C * kDbWords; FUSE: then cov C * C | cam C | hist C (ints)
+                                                   int* __restrict__ cov, int* __restrict__ cam_cnt) {
+  extern __shared__ unsigned long long s_bits[];  // C * kDbWords; FUSE: then cov C * C | cam C (ints)
   int* s_cov = reinterpret_cast<int*>(s_bits + C * kDbWords);
   int* s_cam = s_cov + C * C;
-  int* s_hist = s_cam + C;
   __shared__ int s_cnt, s_err;
   const int t = threadIdx.x, lane = t & 63;
   const int i = blockIdx.x * 256 + t;
@@ -4844,7 +4164,7 @@ __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, 
   const int* __restrict__ of = w.d_obs_frame;
   for (int k = t; k < C * kDbWords; k += 256) s_bits[k] = 0ull;
   if (FUSE)
-    for (int k = t; k < C * C + 2 * C; k += 256) s_cov[k] = 0;
+    for (int k = t; k < C * C + C; k += 256) s_cov[k] = 0;
   if (t == 0) { s_cnt = 0; s_err = 0; }
   const int i0 = blockIdx.x * 256;
   const int w0 = i0 < n_obs ? max(op[i0], 0) >> 6 : 0;  // the workgroup's first word
@@ -4865,7 +4185,6 @@ __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, 
     else if (f >= C) err |= 2;
     else if (q < 0 || q >= n_pt) err |= 1;
     else if (f >= 0) {
-      if (FUSE) atomicAdd(&s_hist[f], 1);
       const unsigned long long m = 1ull << (q & 63);
       const int wl = (q >> 6) - w0;
       if (wl >= 0 && wl < kDbWords) atomicOr(&s_bits[f * kDbWords + wl], m);
@@ -4953,9 +4272,6 @@ __global__ __launch_bounds__(256) void k_db_sorted(lorb_ba_window_dev w, int C, 
       const int v = s_cov[k];  // (cam_cnt follows cov in LDS and in the scratch)
       if (v) __hip_atomic_fetch_add(k < C * C ? &cov[k] : &cam_cnt[k - C * C], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const int NB = (n_obs + 255) / 256;
-    if ((int)blockIdx.x < NB)
-      for (int k = t; k < C; k += 256) hist[(size_t)k * NB + blockIdx.x] = s_hist[k];
   }
   if (t == 0) {
     if (s_cnt > __hip_atomic_load(&hdr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(&hdr[1], s_cnt);
@@ -5060,28 +4376,21 @@ __global__ __launch_bounds__(256) void k_db_cov(int C, int Wd, const unsigned lo
 //  * zeros: this rank's band, and the build scratch the next build accumulates into (camera x point
 //    bitsets, header max / error words, cov / cam_cnt; pt_cnt is left zero by k_db_scatter), so the
 //    next build needs no clearing fill.
-// FUSE (after k_db_sorted<true>): also k_db_place's work -- the block's first slot per camera from
-// the camera offsets and the column prefix of k_db_sorted's input-camera histogram, then the rank
-// of each observation among the block's earlier ones of its camera.
 struct DbFused {
-  const int* perm;   // input camera -> plan camera
-  const int* gcam;   // observations per input camera, all ranks
   int C, F, P, G, S, env_n, bits_n;
   int sorted;        // the slots were sorted by point (k_db_sorted): slot e is sorted position e
   unsigned long long* bits;
   int* hdr;
   int* cov;          // cov | cam_cnt (C * C + C ints): zeroed for the next build's k_db_sorted<true>
   int cov_n;
-  // ARGS (C <= kDbArgC): the upload is not copied before the launch -- the workgroups copy it from
-  // the mapped pinned staging (src -> dst, words), and read perm / gcam / cam_obs_off from `cams`
-  // (kernel arguments), not from the copy
+  // the upload is not copied before the launch -- the workgroups copy it from the mapped pinned
+  // staging (src -> dst, words), and read perm / gcam from `cams` (kernel arguments), not from the copy
   const int* up_src;
   int* up_dst;
   int up_words;
 };
-constexpr int kDbArgC = 160;
-struct DbCams {
-  int perm[kDbArgC], gcam[kDbArgC], coff[kDbArgC + 1];
+struct DbCams {  // kernel arguments: device plans hold <= kPmSpan cameras
+  int perm[kPmSpan], gcam[kPmSpan];
 };
 // Point groups: group g = points [start(g), start(g + 1)), start(g) = the smallest p with
 // off[p] + p >= g S (P if none), found by one wavefront, 32-ary: each half-wave probes 32 points spread over its
@@ -5115,19 +4424,13 @@ __device__ __forceinline__ void group_bounds(const int* __restrict__ off, int P,
   s0 = __shfl(lo, 0, 64);
   s1 = __shfl(lo, 32, 64);
 }
-template <bool FUSE, bool ARGS>
-__global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d, int K, int C, int NB,
-                                                   const int* __restrict__ key, const int* __restrict__ val,
-                                                   const int* __restrict__ perm_dev, int* __restrict__ hist, DbFused f,
-                                                   int* __restrict__ cam_pt, DbCams cams) {
-  extern __shared__ int s_h[];  // C: histogram; FUSE: first slot per input camera (-1: absent)
-  __shared__ int s_c[FUSE ? 256 : 1];
+__global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d, int K, const int* __restrict__ key,
+                                                   const int* __restrict__ val, DbFused f, DbCams cams) {
   const int gt = blockIdx.x * 256 + threadIdx.x, gs = gridDim.x * 256;
-  if (ARGS)  // the upload, from the mapped staging (PCIe reads, no copy launch before this kernel)
-    for (int i = gt; i < f.up_words; i += gs) f.up_dst[i] = f.up_src[i];
-  const int* __restrict__ perm = ARGS ? cams.perm : perm_dev;
-  const int* __restrict__ gcam = ARGS ? cams.gcam : f.gcam;
-  const int* __restrict__ coff = ARGS ? cams.coff : d.cam_obs_off;
+  // the upload, from the mapped staging (PCIe reads, no copy launch before this kernel)
+  for (int i = gt; i < f.up_words; i += gs) f.up_dst[i] = f.up_src[i];
+  const int* __restrict__ perm = cams.perm;
+  const int* __restrict__ gcam = cams.gcam;
   {  // initial values and camera activity
     const int m = max(max(6 * f.C, 6 * f.F), 3 * f.P);
     for (int i = gt; i < m; i += gs) {
@@ -5135,7 +4438,6 @@ __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d
         const int c = i / 6, q = i - 6 * c;
         d.x_init_pose[6 * perm[c] + q] = (double)w.d_pose_init[i];
         if (q == 0) const_cast<int*>(d.cam_active)[perm[c]] = gcam[c] > 0;
-        if (q == 0) const_cast<int*>(d.cam_win)[c] = 0;
       }
       if (i < 6 * f.F) const_cast<double*>(d.fixed_pose)[i] = (double)w.d_fixed_pose[i];
       if (i < 3 * f.P) d.x_init_pt[i] = (double)w.d_point_init[i];
@@ -5154,166 +4456,16 @@ __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d
   for (int i = gt; i < f.bits_n; i += gs) f.bits[i] = 0ull;
   for (int i = gt; i < f.cov_n; i += gs) f.cov[i] = 0;
   if (gt == 0) { f.hdr[1] = 0; f.hdr[2] = 0; }
-  if ((int)blockIdx.x >= NB) return;  // uniform per workgroup
-  const int t = threadIdx.x;
-  for (int i = t; i < C; i += 256) s_h[i] = FUSE ? -1 : 0;
-  __syncthreads();
-  const int e = blockIdx.x * 256 + t;
-  int c = -1, fr = -1, pt = 0;
-  if (e < K) {
+  // the point-sorted observation records
+  for (int e = gt; e < K; e += gs) {
     const int k = f.sorted ? e : val[e];
-    fr = w.d_obs_frame[k];
-    c = fr >= 0 ? perm[fr] : -1;
-    pt = f.sorted ? w.d_obs_point[e] : key[e];
-    const_cast<int*>(d.obs_pt)[e] = pt;
-    const_cast<int*>(d.obs_cam)[e] = c;
+    const int fr = w.d_obs_frame[k];
+    const_cast<int*>(d.obs_pt)[e] = f.sorted ? w.d_obs_point[e] : key[e];
+    const_cast<int*>(d.obs_cam)[e] = fr >= 0 ? perm[fr] : -1;
     const_cast<int*>(d.obs_fix)[e] = fr >= 0 ? -1 : -1 - fr;
     const_cast<double2*>(d.obs_uv)[e] = make_double2(w.d_obs_uv[2 * k], w.d_obs_uv[2 * k + 1]);
-    if (!FUSE || c < 0) const_cast<int*>(d.obs_cm)[e] = -1;
-    if (!FUSE && c >= 0) atomicAdd(&s_h[c], 1);
-  }
-  if (!FUSE) {
-    __syncthreads();
-    for (int i = t; i < C; i += 256) hist[(size_t)i * NB + blockIdx.x] = s_h[i];
-    return;
-  }
-  s_c[t] = c;
-  if (c >= 0) s_h[fr] = 0;
-  __syncthreads();
-  // column prefixes of the present cameras, one wavefront per camera (lanes stride the blocks)
-  const int lane = t & 63;
-  for (int cc = t >> 6; cc < C; cc += 4) {
-    if (s_h[cc] < 0) continue;  // uniform per wavefront
-    const int* h = hist + (size_t)cc * NB;
-    int v = 0;
-    for (int i = lane; i < (int)blockIdx.x; i += 64) v += h[i];
-    v = wave_isum(v);
-    if (lane == 0) s_h[cc] = coff[perm[cc]] + v;
-  }
-  __syncthreads();
-  if (c < 0) return;
-  int rank = 0;
-  for (int u = 0; u < t; ++u) rank += s_c[u] == c;
-  const int j = s_h[fr] + rank;
-  const_cast<int*>(d.cam_obs)[j] = e;
-  const_cast<int*>(d.obs_cm)[e] = j;
-  cam_pt[j] = pt;
-}
-
-// counting sort of the optimised observations by plan camera, stable: slot = camera offset (the
-// uploaded cam_obs_off: observations of the plan cameras before c) + this camera's observations in
-// the earlier blocks (a column prefix of the camera-major histogram, summed here by one wavefront
-// per camera present in the block -- no separate scan launch) + rank among the block's earlier
-// observations of the same camera.  Writes the camera-major list, its point ids and each
-// observation's camera slot.
-__global__ __launch_bounds__(256) void k_db_place(BaDev d, int K, int NB, int C, const int* __restrict__ hist,
-                                                  int* __restrict__ cam_pt) {
-  extern __shared__ int s_off[];  // C: this block's first slot per camera (-1: camera absent)
-  __shared__ int s_c[256];
-  const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const int e = b * 256 + t;
-  for (int i = t; i < C; i += 256) s_off[i] = -1;
-  __syncthreads();
-  const int c = e < K ? d.obs_cam[e] : -1;
-  s_c[t] = c;
-  if (c >= 0) s_off[c] = 0;
-  __syncthreads();
-  for (int cc = wv; cc < C; cc += 4) {
-    if (s_off[cc] < 0) continue;  // uniform per wavefront
-    const int* h = hist + (size_t)cc * NB;
-    int v = 0;
-    for (int i = lane; i < b; i += 64) v += h[i];
-    v = wave_isum(v);
-    if (lane == 0) s_off[cc] = d.cam_obs_off[cc] + v;
-  }
-  __syncthreads();
-  if (c < 0) return;
-  int rank = 0;
-  for (int u = 0; u < t; ++u) rank += s_c[u] == c;
-  const int j = s_off[c] + rank;
-  const_cast<int*>(d.cam_obs)[j] = e;
-  const_cast<int*>(d.obs_cm)[e] = j;
-  cam_pt[j] = d.obs_pt[e];
-}
-
-// one workgroup per (camera, camera) block: its pair list in point order.  A diagonal block's pairs
-// are (e, e) over the camera's slots.  Otherwise the lower camera's point ids (ascending) are staged
-// in LDS for the binary searches when they fit; each thread owns a run of up to kPR consecutive
-// slots of the higher camera, loads their point ids together (one memory round trip per batch, not
-// one per 256 slots; the first batch's go out with the staging loads), searches them and places its
-// matches after one block scan of the run counts.  The camera offsets come in whole (C + 1 ints,
-// issued with the block pair) so the slot ranges cost no dependent load.
-constexpr int kPairsLds = 8192, kPR = 8;
-__global__ __launch_bounds__(256) void k_db_pairs(BaDev d, int C, const int* __restrict__ cam_pt) {
-  __shared__ int wsum[4];
-  __shared__ int s_pt[kPairsLds];
-  extern __shared__ int s_co[];  // C + 1 camera offsets
-  const BlockPair B = d.bp[blockIdx.x];
-  const int t = threadIdx.x;
-  for (int i = t; i <= C; i += 256) s_co[i] = d.cam_obs_off[i];
-  __syncthreads();
-  const int h0 = s_co[B.ch], h1 = s_co[B.ch + 1];
-  const int l0 = s_co[B.cl], l1 = s_co[B.cl + 1];
-  const int nl = l1 - l0;
-  int2* out = const_cast<int2*>(d.pairs) + B.off;
-  if (B.ch == B.cl) {
-    for (int i = h0 + t; i < h1 && i - h0 < B.cnt; i += 256) out[i - h0] = make_int2(i, i);
-    return;
-  }
-  const bool lds = nl <= kPairsLds;
-  int p[kPR], jv[kPR];
-  {  // the first batch's point ids, issued before the staging waits
-    const int nb = min(h1 - h0, 256 * kPR), r0 = h0 + t * kPR;
-#pragma unroll
-    for (int u = 0; u < kPR; ++u) p[u] = r0 + u < h0 + nb ? cam_pt[r0 + u] : -1;
-  }
-  if (lds) {
-    for (int i = t; i < nl; i += 256) s_pt[i] = cam_pt[l0 + i];
-    __syncthreads();
-  }
-  const int* lp = lds ? s_pt : cam_pt + l0;
-  int run = 0;
-  for (int base = h0; base < h1; base += 256 * kPR) {
-    const int nb = min(h1 - base, 256 * kPR), r0 = base + t * kPR;
-    if (base != h0) {
-#pragma unroll
-      for (int u = 0; u < kPR; ++u) p[u] = r0 + u < base + nb ? cam_pt[r0 + u] : -1;
-    }
-    // the kPR lower bounds advance together, one halving per step (the step lengths depend on nl
-    // only), so each step's kPR LDS reads are in flight at once instead of kPR serial searches
-    int bs[kPR];
-#pragma unroll
-    for (int u = 0; u < kPR; ++u) bs[u] = 0;
-    for (int len = nl; len > 1;) {
-      const int half = len >> 1;
-#pragma unroll
-      for (int u = 0; u < kPR; ++u) bs[u] = lp[bs[u] + half] < p[u] ? bs[u] + half : bs[u];
-      len -= half;
-    }
-    int c = 0;
-#pragma unroll
-    for (int u = 0; u < kPR; ++u) {
-      int j = -1;
-      if (p[u] >= 0 && nl > 0) {
-        const int v = lp[bs[u]];
-        const int lo = bs[u] + (v < p[u] ? 1 : 0);
-        if (lo < nl && (v < p[u] ? lp[lo] : v) == p[u]) j = l0 + lo;
-      }
-      jv[u] = j;
-      c += j >= 0;
-    }
-    int tot;
-    int o = run + lorb::block_excl_scan<256>(c, wsum, &tot);
-#pragma unroll
-    for (int u = 0; u < kPR; ++u)
-      if (jv[u] >= 0) {
-        if (o < B.cnt) out[o] = make_int2(r0 + u, jv[u]);
-        ++o;
-      }
-    run += tot;
   }
 }
-
 
 // plan camera order -> caller order, as float (Frame::SetPose / MapPoint::SetWorldPos write-back).
 // ring (the LocalMapping map's keyframe ring of R slots): caller pose c goes to slot (t0 + c) mod R.
@@ -5391,8 +4543,8 @@ int ba_plan_result64_dev(lorb_ba_plan* P, double* d_out) {
 
 namespace {
 
-template <typename T>
-int grow(lorb_ba_plan* P, T** ptr, int* cap, size_t need) {
+template <typename T, typename Cap>
+int grow(lorb_ba_plan* P, T** ptr, Cap* cap, size_t need) {
   if (*ptr && (size_t)*cap >= need) return LORB_OK;
   if (*ptr) {
     LORB_HIP(P->ctx, hipStreamSynchronize(P->ctx->stream));
@@ -5402,7 +4554,7 @@ int grow(lorb_ba_plan* P, T** ptr, int* cap, size_t need) {
   }
   const size_t n = std::max<size_t>(need + need / 4, 16);
   LORB_TRY(dalloc(P, n, ptr));
-  *cap = (int)n;
+  *cap = (Cap)n;
   P->has_graph = false;  // kernel arguments changed
   return LORB_OK;
 }
@@ -5414,7 +4566,9 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   b.Wd = (std::max(b.P_cap, 1) + 63) / 64;
   const size_t K = (size_t)std::max(b.K_cap, 1), Pn = (size_t)std::max(b.P_cap, 1), C = (size_t)std::max(b.C, 1);
   BaDev& d = P->dev;
-  LORB_TRY(dalloc(P, K, &b.key_out)); LORB_TRY(dalloc(P, K, &b.val_out)); LORB_TRY(dalloc(P, K, &b.cam_pt));
+  if (b.C > kPmSpan)
+    return lorb::set_error(ctx, LORB_E_UNSUPPORTED, "device-built plans hold windows of <= %d cameras (%d)", kPmSpan, b.C);
+  LORB_TRY(dalloc(P, K, &b.key_out)); LORB_TRY(dalloc(P, K, &b.val_out));
   {
     const size_t ints = ((Pn + 1 + 8 + C * C + C) + 1) & ~(size_t)1;  // the u64 bitsets 8-byte aligned
     b.scr_bytes = sizeof(int) * ints + sizeof(unsigned long long) * C * (size_t)b.Wd;
@@ -5424,24 +4578,19 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     b.pt_cnt = b.scr; b.hdr = b.pt_cnt + Pn + 1; b.cov = b.hdr + 8; b.cam_cnt = b.cov + C * C;
     b.bits = reinterpret_cast<unsigned long long*>(b.scr + ints);
   }
-  {  // camera-major block histograms: k_db_sorted<true> writes them before the readback
-    const size_t nb = (K + 1 + 255) / 256;
-    LORB_TRY(grow(P, &b.hist, &b.hist_cap, nb * C));
-  }
-  int *a_pt, *a_cam, *a_fix, *a_cm, *a_camobs, *a_win, *a_act, *a_ptoff;
+  int *a_pt, *a_cam, *a_fix, *a_act, *a_ptoff;
   double2* a_uv;
   double* a_fixp;
   LORB_TRY(dalloc(P, K, &a_pt)); LORB_TRY(dalloc(P, K, &a_cam)); LORB_TRY(dalloc(P, K, &a_fix));
-  LORB_TRY(dalloc(P, K, &a_uv)); LORB_TRY(dalloc(P, K, &a_cm)); LORB_TRY(dalloc(P, K, &a_camobs));
-  LORB_TRY(dalloc(P, C, &a_win)); LORB_TRY(dalloc(P, C, &a_act));
+  LORB_TRY(dalloc(P, K, &a_uv)); LORB_TRY(dalloc(P, C, &a_act));
   LORB_TRY(dalloc(P, Pn + 1, &a_ptoff)); LORB_TRY(dalloc(P, (size_t)std::max(b.F, 1) * 6, &a_fixp));
-  d.obs_pt = a_pt; d.obs_cam = a_cam; d.obs_fix = a_fix; d.obs_uv = a_uv; d.obs_cm = a_cm; d.cam_obs = a_camobs;
-  d.cam_win = a_win; d.cam_active = a_act; d.pt_obs_off = a_ptoff; d.fixed_pose = a_fixp;
+  d.obs_pt = a_pt; d.obs_cam = a_cam; d.obs_fix = a_fix; d.obs_uv = a_uv;
+  d.cam_active = a_act; d.pt_obs_off = a_ptoff; d.fixed_pose = a_fixp;
   LORB_TRY(dalloc(P, C * 6, &d.x_init_pose)); LORB_TRY(dalloc(P, Pn * 3, &d.x_init_pt));
   LORB_TRY(dalloc(P, C * 6, &d.x_pose[0])); LORB_TRY(dalloc(P, C * 6, &d.x_pose[1]));
   LORB_TRY(dalloc(P, Pn * 3, &d.x_pt[0])); LORB_TRY(dalloc(P, Pn * 3, &d.x_pt[1]));
   LORB_TRY(dalloc(P, C * 6, &d.scale_pose)); LORB_TRY(dalloc(P, Pn * 3, &d.scale_pt));
-  LORB_TRY(dalloc(P, Pn * 6, &d.ete)); LORB_TRY(dalloc(P, Pn * 3, &d.etb)); LORB_TRY(dalloc(P, Pn * 6, &d.pinv));
+  LORB_TRY(dalloc(P, Pn * 3, &d.etb)); LORB_TRY(dalloc(P, Pn * 6, &d.pinv));
   // the solve block is rhs (n) | wfail (1) | pad | env (up to the dense n x n): rhs and wfail at fixed
   // places, so the captured solve survives a rebuild that changes the band, and a sharded plan's
   // exchange 2 is one contiguous all-reduce of x2_off + env_total doubles
@@ -5480,11 +4629,7 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   P->x2_send = b.sol_part; P->x2_recv = sol;
   d.sharded = comm ? 1 : 0;
   d.rank0 = comm ? (comm->rank == 0) : 1;
-  LORB_TRY(dalloc(P, C, &d.cam_gmax));
-  LORB_TRY(dalloc(P, K * 2, &d.obs_r)); LORB_TRY(dalloc(P, K * 6, &d.obs_Jp)); LORB_TRY(dalloc(P, K * 12, &d.obs_Jc));
-  LORB_TRY(dalloc(P, K * 2, &d.cam_r));
   LORB_TRY(dalloc(P, C, &d.rot_lin)); LORB_TRY(dalloc(P, C, &d.rot_cand));
-  LORB_TRY(dalloc(P, K * 6, &d.obs_Jps)); LORB_TRY(dalloc(P, K * 6, &d.obs_Q)); LORB_TRY(dalloc(P, K * 2, &d.obs_g));
   LORB_TRY(dalloc(P, n, &d.ycam));
 #ifdef LORB_CHOL_TRACE
   LORB_TRY(dalloc(P, (size_t)512, &d.dbg));
@@ -5496,7 +4641,6 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(dalloc(P, ((size_t)n / 16 + 2) * 1024, &d.kco));
   LORB_TRY(dalloc(P, (size_t)1, &P->d_state)); d.st = P->d_state;
   LORB_TRY(dalloc(P, (size_t)LORB_LM_TRACE_CAP, &d.trace));
-  d.pm = pm_fits(b.C, b.F) && pm_enabled() ? 1 : 0;
   P->W = 1;
   P->hwin.assign(1, BaWin{});
   P->pt_launch = b.P_cap;
@@ -5513,8 +4657,7 @@ int up_alloc(lorb_ba_plan* P, int bp_need) {
   const size_t C = (size_t)std::max(b.C, 1);
   b.off_live = al(sizeof(BaWin));
   b.off_perm = b.off_live + 256;
-  b.off_camoff = b.off_perm + al(4 * C);
-  b.off_gcam = b.off_camoff + al(4 * (C + 1));
+  b.off_gcam = b.off_perm + al(4 * C);
   b.off_bp = b.off_gcam + al(4 * C);
   b.up_bytes = b.off_bp + sizeof(BlockPair) * (size_t)cap;
   if (b.up_dev) {
@@ -5538,7 +4681,6 @@ int up_alloc(lorb_ba_plan* P, int bp_need) {
   d.live = reinterpret_cast<const int*>(b.up_dev + b.off_live);
   b.perm = reinterpret_cast<int*>(b.up_dev + b.off_perm);
   b.gcam = reinterpret_cast<int*>(b.up_dev + b.off_gcam);
-  d.cam_obs_off = reinterpret_cast<const int*>(b.up_dev + b.off_camoff);
   d.bp = reinterpret_cast<const BlockPair*>(b.up_dev + b.off_bp);
   P->grid_bp = cap;
   P->has_graph = false;
@@ -5574,16 +4716,16 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   for (;;) {
     if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
     b.dirty = true;
-    fuse = sorted && C > 0 && sizeof(int) * ((size_t)C * C + 2 * C) <= (size_t)kDbFuseLds;
+    fuse = sorted && C > 0 && sizeof(int) * ((size_t)C * C + C) <= (size_t)kDbFuseLds;
     if (sorted) {
       const size_t lds = sizeof(unsigned long long) * kDbWords * std::max(C, 1) +
-                         (fuse ? sizeof(int) * ((size_t)C * C + 2 * C) : 0);
+                         (fuse ? sizeof(int) * ((size_t)C * C + C) : 0);
       if (fuse)
         hipLaunchKernelGGL(k_db_sorted<true>, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), lds, s, *w, C, F, b.Wd,
-                           const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt, b.hist);
+                           const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt);
       else
         hipLaunchKernelGGL(k_db_sorted<false>, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), lds, s, *w, C, F, b.Wd,
-                           const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt, b.hist);
+                           const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt);
     } else {
       hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);
       hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1,
@@ -5700,8 +4842,6 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   std::vector<int> inv(C);
   for (int c = 0; c < C; ++c) inv[map[c]] = c;
   P->cam_map.assign(1, map);
-  std::vector<int> cam_off(C + 1, 0);
-  for (int c = 0; c < C; ++c) cam_off[c + 1] = cam_off[c] + cam_cnt[inv[c]];
   std::vector<BlockPair> bps;
   std::vector<int> fc(C);
   int n_pairs = 0;
@@ -5727,7 +4867,8 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   bw.obs_base = 0; bw.n_obs = K; bw.n_obs_all = K_all;
   bw.fx = w->fx; bw.fy = w->fy; bw.cx = w->cx; bw.cy = w->cy;
   long long part_total = 0;
-  pm_layout(bw, part_total);
+  pm_layout(bw, C, part_total);  // a group spans at most the window's C <= kPmSpan cameras
+  LORB_TRY(part_budget_check(ctx, part_total));
   P->hwin[0] = bw;
   P->Ctot = C; P->Ptot = Pn; P->K = K; P->NF = F; P->n_pblk = G; P->n_bp = (int)bps.size(); P->n_pairs = n_pairs;
   P->env_total = bw.env_size; P->n_total = n;
@@ -5748,17 +4889,15 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   hp_mark(2);
   // grow-only structure buffers; the point-group kernels launch at capacity
   PBlk* pb = const_cast<PBlk*>(d.pblk);
-  int2* pr = const_cast<int2*>(d.pairs);
   LORB_TRY(grow(P, &pb, &b.pblk_cap, (size_t)std::max(G, 1)));
-  LORB_TRY(grow(P, &pr, &b.pairs_cap, (size_t)std::max(n_pairs, 1)));
-  d.pblk = pb; d.pairs = pr;
+  d.pblk = pb;
   {
     double* pt = d.part;
     LORB_TRY(grow(P, &pt, &b.part_cap, (size_t)b.pblk_cap * 8));
     d.part = pt;
   }
   P->grid_pblk = b.pblk_cap;
-  if (d.pm) {  // group partials (grow-only; a reallocation re-captures the LM graph)
+  {  // group partials (grow-only; a reallocation re-captures the LM graph)
     LORB_TRY(grow(P, &d.gpart, &b.gpart_cap, (size_t)std::max(part_total, 1ll)));
     int2* gsp = d.gspan;
     LORB_TRY(grow(P, &gsp, &b.gspan_cap, (size_t)b.pblk_cap));
@@ -5767,9 +4906,9 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   LORB_TRY(up_alloc(P, (int)bps.size()));
   hp_mark(3);
   // one upload (pinned staging, stream-ordered; the next build writes the staging only after its
-  // own readback synchronised the stream).  C <= kDbArgC: no copy launch -- k_db_gather copies the
-  // staging over the bus and takes the camera tables as kernel arguments (the step's host phase
-  // ends with the gather's launch)
+  // own readback synchronised the stream).  No copy launch: k_db_gather copies the staging over the
+  // bus and takes the camera tables as kernel arguments (the step's host phase ends with the
+  // gather's launch)
   int up_words = 0;
   {
     unsigned char* h = b.up_host;
@@ -5777,38 +4916,23 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
     const int live[2] = {G, (int)bps.size()};
     memcpy(h + b.off_live, live, sizeof(live));
     memcpy(h + b.off_perm, map.data(), sizeof(int) * C);
-    memcpy(h + b.off_camoff, cam_off.data(), sizeof(int) * (C + 1));
     memcpy(h + b.off_gcam, gcam, sizeof(int) * C);
     if (!bps.empty()) memcpy(h + b.off_bp, bps.data(), sizeof(BlockPair) * bps.size());
     const size_t bytes = b.off_bp + sizeof(BlockPair) * bps.size();
     up_words = (int)((bytes + 3) / 4);
-    if (C > kDbArgC) LORB_HIP(ctx, hipMemcpyAsync(b.up_dev, h, bytes, hipMemcpyHostToDevice, s));
   }
   hp_mark(4);
-  // 4. structure kernels: gather (+ initial values, point groups, zeros), the camera-major block
-  //    offsets, the stable placement by camera, the block pair lists
+  // 4. structure kernel: gather (point-sorted observation records, initial values, point groups,
+  //    the zeros the next build starts from)
   const int NB = lorb::ceil_div(K, 256);
-  if ((size_t)std::max(NB, 1) * C > (size_t)b.hist_cap) {
-    LORB_TRY(grow(P, &b.hist, &b.hist_cap, (size_t)std::max(NB, 1) * C));
-  }
   {
     // this rank's band starts from zeros (blocks it has no pairs of stay zero; sharded: the
     // all-reduce writes the global band every iteration)
-    const bool args = C <= kDbArgC;
-    DbFused f{b.perm, b.gcam, C, F, Pn, G, S, P->env_total, C * b.Wd, sorted ? 1 : 0, b.bits, b.hdr, b.cov, C * C + C,
-              reinterpret_cast<const int*>(b.up_host_dev), reinterpret_cast<int*>(b.up_dev), args ? up_words : 0};
+    DbFused f{C, F, Pn, G, S, P->env_total, C * b.Wd, sorted ? 1 : 0, b.bits, b.hdr, b.cov, C * C + C,
+              reinterpret_cast<const int*>(b.up_host_dev), reinterpret_cast<int*>(b.up_dev), up_words};
     DbCams cams;
-    if (args) {
-      for (int c = 0; c < C; ++c) { cams.perm[c] = map[c]; cams.gcam[c] = gcam[c]; }
-      for (int c = 0; c <= C; ++c) cams.coff[c] = cam_off[c];
-    }
-    const size_t lds = sizeof(int) * std::max(C, 1);
-    const dim3 g(std::max(NB, 1));
-#define LORB_GATHER(FU, AR) hipLaunchKernelGGL((k_db_gather<FU, AR>), g, dim3(256), lds, s, *w, d, K, C, NB, b.key_out, \
-                                                b.val_out, b.perm, b.hist, f, b.cam_pt, cams)
-    if (fuse) { if (args) LORB_GATHER(true, true); else LORB_GATHER(true, false); }
-    else { if (args) LORB_GATHER(false, true); else LORB_GATHER(false, false); }
-#undef LORB_GATHER
+    for (int c = 0; c < C; ++c) { cams.perm[c] = map[c]; cams.gcam[c] = gcam[c]; }
+    hipLaunchKernelGGL(k_db_gather, dim3(std::max(NB, 1)), dim3(256), 0, s, *w, d, K, b.key_out, b.val_out, f, cams);
     b.dirty = false;
     if (hp_log) {
       hp_mark(5);
@@ -5816,11 +4940,6 @@ int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
       P->hp_n++;
     }
   }
-  if (K > 0 && !fuse)
-    hipLaunchKernelGGL(k_db_place, dim3(NB), dim3(256), sizeof(int) * std::max(C, 1), s, d, K, NB, C, b.hist, b.cam_pt);
-  // the block pair lists feed the pair-major Schur only (the point-major path reduces group partials)
-  if (!bps.empty() && !d.pm)
-    hipLaunchKernelGGL(k_db_pairs, dim3((unsigned)bps.size()), dim3(256), sizeof(int) * (C + 1), s, d, C, b.cam_pt);
   LORB_CHECK_LAUNCH(ctx);
   return LORB_OK;
 }
@@ -5971,7 +5090,7 @@ int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n) {
   for (const auto& m : plan->cam_map)
     for (size_t c = 0; c < m.size(); ++c) reordered |= m[c] != (int)c;
   const int32_t v[10] = {bw, plan->chol_kind, plan->n_bp, plan->n_pblk, plan->K, plan->Ptot, plan->Ctot, reordered,
-                         plan->dev.pm, plan->dev.pm ? red_threads(plan) : 0};
+                         1, red_threads(plan)};
   for (int i = 0; i < n && i < 10; ++i) info[i] = v[i];
   return LORB_OK;
 }

@@ -49,8 +49,13 @@ def trace_match(gt, ot, cost_rtol=1e-10, strict_to=1e-12, flip_at=1e-13, label="
                       f"{rc_g:.2e}; max differences before {worst}")
                 return i
             continue
-        assert g["outcome"] == o["outcome"], (label, i, rc_o, g, o)
         assert _rel(g["cost"], o["cost"]) <= cost_rtol, (label, i, g, o)
+        if g["outcome"] != o["outcome"]:  # the first round-off-level iteration may already part
+            assert min(rc_o, rc_g) <= flip_at, (label, i, rc_o, rc_g, g, o)
+            print(f"{label}: outcomes agree through iteration {i}; they part at iteration {i + 1}: "
+                  f"{g['outcome']} (gpu) vs {o['outcome']} (oracle), relative cost change {rc_o:.2e} / {rc_g:.2e}; "
+                  f"max differences before {worst}")
+            return i
         assert abs(g["model_cost_change"] - o["model_cost_change"]) <= cost_rtol * abs(o["cost"]), (label, i, g, o)
         assert _rel(g["radius"], o["radius"]) <= 1e-6, (label, i, g, o)
         if o["outcome"] != "invalid":
@@ -75,10 +80,15 @@ def lm_match(g, o, cost_rtol=1e-8, gt=None, ot=None, label=""):
     accepted steps, final cost within cost_rtol relative.  With the per-iteration records (gt, ot) the
     traces are compared too (trace_match); a differing accepted-step count is then allowed only when
     the traces show the outcomes parting at a round-off-level cost change (the solution itself is
-    checked to 1e-5 by the caller)."""
-    assert g["iterations"] == o["iterations"], (g, o)
+    checked to 1e-5 by the caller).  The same holds for the iteration count: at tolerance 0 a solve
+    may stop on an exactly-zero cost change (function tolerance 0), which one summation order reaches
+    and the other does not -- allowed only behind such a round-off-level parting."""
     assert abs(g["final_cost"] - o["final_cost"]) <= cost_rtol * abs(o["final_cost"]), (g, o)
     flip = trace_match(gt, ot, label=label) if gt is not None else None
+    if g["iterations"] != o["iterations"]:
+        assert flip is not None, (g, o)
+        print(f"{label}: iterations gpu {g['iterations']} vs oracle {o['iterations']} after the round-off "
+              f"parting at iteration {flip + 1}")
     if g["successful_steps"] != o["successful_steps"]:
         assert flip is not None, (g, o)
         print(f"{label}: accepted steps gpu {g['successful_steps']} vs oracle {o['successful_steps']} after the "
@@ -148,12 +158,13 @@ def test_local_ba_c3_ten_iterations(ctx):
     assert close(Xg, Xo), np.abs(Xg - Xo).max()
 
 
-@pytest.mark.parametrize("n_kf,obs_lens", [(20, (7, 8)), (40, (2, 30))])
+@pytest.mark.parametrize("n_kf,obs_lens", [(20, (7, 8)), (40, (2, 30)), (100, (7, 8))])
 def test_local_ba_point_order_without_camera_locality(ctx, n_kf, obs_lens):
     """Points in draw order (no camera locality: a point group's camera window spans most of the
     window) and, second case, points seen by 2 or 30 keyframes (a camera band of 29): the
     point-major path's group windows are wide and its partials sparse -- the result must not depend
-    on the point order's locality, only its speed does."""
+    on the point order's locality, only its speed does.  The 100-camera case gives group windows
+    wider than 64 cameras (k_ba_ls's two-word camera masks)."""
     w = synth.ba_window(seed=17, n_kf=n_kf, n_pts=2000, n_fixed=2, fixed_obs_per_kf=200, obs_lens=obs_lens,
                         point_order="random")
     opt = A.LMOptions.default(max_num_iterations=8, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
@@ -164,12 +175,12 @@ def test_local_ba_point_order_without_camera_locality(ctx, n_kf, obs_lens):
     assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
 
 
-@pytest.mark.parametrize("n_kf,n_pts,n_fixed,pm", [(70, 3000, 2, 0), (20, 4000, 2, 1), (50, 10000, 5, 1)])
+@pytest.mark.parametrize("n_kf,n_pts,n_fixed,pm", [(70, 3000, 2, 1), (100, 5000, 2, 1), (128, 6000, 3, 1),
+                                                   (20, 4000, 2, 1), (50, 10000, 5, 1)])
 def test_local_ba_schur_path_by_window(ctx, n_kf, n_pts, n_fixed, pm):
-    """The Schur path each window shape takes, and its parity: more than 64 cameras (the point-major
-    kernels' camera masks are 64 bits) runs the pair-major k_ba_lin / k_ba_schur / k_ba_backsub; C3 /
-    C4 shapes run the point-major path, C3 with 1024-thread partial reductions (<= 256 blocks), C4
-    with 512 (372 blocks)."""
+    """The Schur path each window shape takes, and its parity: every window runs the point-major path
+    (k_ba_ls / k_ba_red / k_ba_bs2; camera masks of two words: windows of up to 128 cameras), C3 with
+    1024-thread partial reductions (<= 256 blocks), C4 with 512 (372 blocks)."""
     from lorb_slam_amd.runtime import BAPlan
     w = synth.ba_window(seed=29, n_kf=n_kf, n_pts=n_pts, n_fixed=n_fixed, fixed_obs_per_kf=100)
     opt = A.LMOptions.default(max_num_iterations=6, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
@@ -186,6 +197,48 @@ def test_local_ba_schur_path_by_window(ctx, n_kf, n_pts, n_fixed, pm):
     lm_match(sg[0], so[0])
     assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
     assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
+
+
+@pytest.mark.parametrize("order", ["first_kf", "random"])
+def test_local_ba_window_over_128_cameras(ctx, order):
+    """A 150-camera window (host-built plan): point groups are cut where a group's camera window
+    would pass 128 cameras (k_ba_ls's two-word masks; with random point order that cuts most groups
+    early), and the solve still matches the oracle."""
+    from lorb_slam_amd.runtime import BAPlan
+    w = synth.ba_window(seed=41, n_kf=150, n_pts=4000, n_fixed=2, fixed_obs_per_kf=100, point_order=order)
+    opt = A.LMOptions.default(max_num_iterations=5, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    plan = BAPlan(ctx, [w])
+    try:
+        info = plan.info()
+        assert info["cameras"] == 150 and info["point_major"] == 1, info
+        if order == "random":  # groups end at the span limit long before 256 observations
+            assert info["point_groups"] > len(w["obs_point"]) // 256 + 1, info
+    finally:
+        plan.close()
+    Pg, Xg, sg = ctx.ba_local([w], opt)
+    Po, Xo, so = O.ba_local([w], opt)
+    lm_match(sg[0], so[0])
+    assert close(Pg[0], Po[0]), np.abs(Pg[0] - Po[0]).max()
+    assert close(Xg[0], Xo[0]), np.abs(Xg[0] - Xo[0]).max()
+
+
+def test_local_ba_plan_limits(ctx):
+    """What the point-major path refuses, loudly (LORB_E_UNSUPPORTED): a point whose cameras lie more
+    than 127 apart in every camera order (seen by all 140 cameras) in a host-built plan, and a
+    device-built plan of more than 128 cameras (the drop-in solver falls back to a host-built plan
+    for it, lorb_ba_solver.hip)."""
+    from lorb_slam_amd.runtime import BAPlan, BAPlanDev, LorbError
+    w = synth.ba_window(seed=42, n_kf=140, n_pts=300, n_fixed=1, fixed_obs_per_kf=20, obs_lens=(140, 7))
+    with pytest.raises(LorbError, match="apart"):
+        BAPlan(ctx, [w])
+    w2 = synth.ba_window(seed=43, n_kf=130, n_pts=2000, n_fixed=1, fixed_obs_per_kf=50)
+    arrays = BAPlanDev.upload(ctx, w2)
+    try:
+        with pytest.raises(LorbError, match="128 cameras"):
+            BAPlanDev(ctx, arrays, 130, 1, w2["intr"])
+    finally:
+        for a in arrays.values():
+            a.free()
 
 
 def test_local_ba_batched_ragged_windows(ctx):

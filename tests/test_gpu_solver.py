@@ -116,17 +116,24 @@ def test_solver_sorted_duplicate(ctx):
 
 
 def test_solver_many_cameras(ctx):
-    """a window of more cameras than the device build passes as kernel arguments (kDbArgC = 160) and
-    than its fused covisibility tables hold in LDS: the upload goes by copy, k_db_cov and k_db_place
-    run -- in caller order and point-sorted, both against the oracle"""
+    """the widest device-built window (128 cameras: past the fused covisibility tables' LDS, so
+    k_db_cov runs), in caller order and point-sorted, then a 170-camera window, which the device
+    build refuses (its camera tables are kernel arguments of <= 128 cameras) and the solver runs on
+    a host-built plan -- the same point-major kernels, point groups cut at a 128-camera span; every
+    call against the oracle"""
     s = BASolver(ctx)
     try:
-        w = synth.ba_window(seed=26, n_kf=170, n_pts=2500, n_fixed=2, fixed_obs_per_kf=40)
+        w = synth.ba_window(seed=26, n_kf=128, n_pts=2500, n_fixed=2, fixed_obs_per_kf=40)
         check(s, w, OPT10)
         o = np.argsort(np.asarray(w["obs_point"]), kind="stable")
         uv = np.asarray(w["obs_uv"]).reshape(-1, 2)
         ws = dict(w, obs_point=np.asarray(w["obs_point"])[o], obs_frame=np.asarray(w["obs_frame"])[o], obs_uv=uv[o])
         check(s, ws, OPT10)
+        assert s.info()["host_plan_fallback"] == 0
+        w170 = synth.ba_window(seed=27, n_kf=170, n_pts=2500, n_fixed=2, fixed_obs_per_kf=40)
+        check(s, w170, OPT10)
+        assert s.info()["host_plan_fallback"] == 1
+        check(s, w, OPT10)
         assert s.info()["host_plan_fallback"] == 0
     finally:
         s.close()
@@ -193,9 +200,9 @@ def wide_window(seed, n_kf, n_pts, obs_len, n_fixed=2, fixed_obs=60, fx=435.2, f
 
 def test_solver_kgb_fallback_between_normal_windows(ctx):
     """a resident plan, then a window with one point observed by 260 cameras (>= kGB = 256
-    observations: the device plan refuses it, LORB_E_UNSUPPORTED -> lorb_ba_local's host-built plan on
-    the same GPU kernels), then the first window again on its resident plan: every result against
-    the oracle, and the failed build leaves no stale plan or scratch behind"""
+    observations, cameras 259 apart: a point group holds neither, so both plan builders refuse it
+    with LORB_E_UNSUPPORTED -- DESIGN §7), then the first window again on its resident plan: the
+    failed builds leave no stale plan or scratch behind, every result against the oracle"""
     opt = A.LMOptions.default(max_num_iterations=3, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
     s = BASolver(ctx)
@@ -204,8 +211,8 @@ def test_solver_kgb_fallback_between_normal_windows(ctx):
         check(s, a, opt)
         big = wide_window(seed=32, n_kf=260, n_pts=1200, obs_len=3)
         assert int(np.sum(np.asarray(big["obs_point"]) == 0)) == 260
-        check(s, big, opt)
-        assert s.info()["host_plan_fallback"] == 1, s.info()
+        with pytest.raises(LorbError, match="observations"):
+            s.solve(big, opt)
         check(s, a, opt)
         info = s.info()
         assert info["host_plan_fallback"] == 0 and info["plan_creations"] == 1, info

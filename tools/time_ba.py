@@ -1,6 +1,6 @@
 """Quick GPU timing of the local-BA plan (C3 / C4 / 8 x C4 / the 80k-point shared window), 10 LM
-iterations, tolerances 0; per-kernel ms of the linearisation (k_ba_lin / k_ba_ls), the Schur
-(k_ba_schur / k_ba_red) and the Cholesky.  LORB_PM=0 runs the pair-major path (A/B)."""
+iterations, tolerances 0; per-kernel ms of the linearisation (k_ba_ls), the partial reduction
+(k_ba_red) and the Cholesky."""
 import sys, os, time, ctypes as C
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -29,6 +29,6 @@ for name, kw, W in [("C3", dict(n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf
         ms, n = C.c_double(0), C.c_int(0)
         L.lorb_kernel_timing_read(ctx.handle, k, C.byref(ms), C.byref(n)); res[nm] = (ms.value / max(n.value, 1), n.value)
     L.lorb_kernel_timing_enable(ctx.handle, 0)
-    print(os.environ.get("LORB_PM", "1"), name, "W", W, "plan %.1f ms" % ((t1 - t0) * 1e3), "solve med %.3f ms" % (np.median(ts) * 1e3),
+    print("pm", name, "W", W, "plan %.1f ms" % ((t1 - t0) * 1e3), "solve med %.3f ms" % (np.median(ts) * 1e3),
           "it/s %.0f" % (10 * W / np.median(ts)), s[0], "per-kernel ms", res, flush=True)
     plan.close()
