@@ -280,7 +280,7 @@ def workload_c4(ctx, args, rank):
         for c in ctxs:
             c.sync()
 
-    return dict(step=step, check=check, sync=sync, ba_iters=10.0 * W, matches=float(W * nq), pairs=float(W) * nq * n_pts,
+    return dict(step=step, check=check, sync=sync, maps=maps, ba_iters=10.0 * W, matches=float(W * nq), pairs=float(W) * nq * n_pts,
                 plan_ms=0.0, create_ms=create_ms, cleanup=cleanup, kspec=kspec, traffic_key="c4_chain",
                 config={"workload": "c4_local_mapping_step_chained", "windows_per_gpu": W, "kf": F,
                         "fixed_kf": maps[0].F, "points": n_pts, "observations": n_obs, "lm_iterations": 10,

@@ -311,11 +311,11 @@ __global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n
 // deterministic point-group reductions (fixed butterfly per wave, fixed wave order) over the
 // kGB / 64 waves of a point-group workgroup
 constexpr int kGW = kGB / 64;
-static_assert(kGW >= 1 && kGW <= 4, "point groups of 64..256 observations (red3 holds 4 waves)");
+static_assert(kGW >= 1 && kGW <= 16 && kGB % 64 == 0, "point groups of 64..1024 observations, whole waves");
 // three block reductions behind one LDS exchange (M1: the second is a max): per-wave butterfly,
 // then the waves' values in wave order
 template <bool M1>
-__device__ __forceinline__ void block_red3(double& a, double& b, double& c, double (*red)[4]) {
+__device__ __forceinline__ void block_red3(double& a, double& b, double& c, double (*red)[kGW]) {
   a = wave_sum(a); b = M1 ? wave_max(b) : wave_sum(b); c = wave_sum(c);
   if (kGW == 1) return;
   __syncthreads();
@@ -2907,7 +2907,7 @@ __global__ __launch_bounds__(RT) void k_ba_red(BaDev d, LMOpt o) {
 // candidate, then the model cost change and the candidate cost per observation.
 __global__ __launch_bounds__(kGB) void k_ba_bs2(BaDev d) {
   __shared__ double sh[kGB][3], sst[kGB][3], sxn[kGB][3], ssp[kGB][3];
-  __shared__ double red3[3][4];
+  __shared__ double red3[3][kGW];
   if ((int)blockIdx.x >= d.live[0]) return;
   const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x;
