@@ -69,7 +69,7 @@ def ba_kspec(W, n_obs, n_pts, F, bw):
             3: ("hbm", W * (n_obs * 28.0 + n_pts * 96.0), "GB/s"),
             4: ("fp64", W * ((6 * F) * bw * bw + 4.0 * (6 * F) * bw), "TFLOP/s")}
 # committed PMC summaries, newest first; each is keyed by workload (tools/pmc_traffic.py)
-TRAFFIC = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r05", "r04", "r03", "r02", "r01")]
+TRAFFIC = [os.path.join(ROOT, "profiles", r, "traffic.json") for r in ("r06", "r05", "r04", "r03", "r02", "r01")]
 METRIC = "ORB matches/sec + local-BA iterations/sec (50 KF, 10k pts) at 1/2/4/8 MI355X"
 
 
