@@ -463,6 +463,10 @@ typedef struct lorb_ba_window {
   const float* obs_uv;         /* n_obs x 2 */
 } lorb_ba_window;
 
+/* (a13) BA::LocalPoseOptimization (src/bundle_adjust.cpp:207-330) over independent windows.  Any
+ * number of cameras; LORB_E_UNSUPPORTED for a point observed by more than 256 cameras, or by two
+ * cameras more than 127 apart in the plan's camera order (the point-major Schur's point groups,
+ * DESIGN.md §7). */
 int lorb_ba_local(lorb_ctx* ctx, int32_t n_windows, const lorb_ba_window* windows,
                   const lorb_lm_options* opt, double* const* pose_out,
                   double* const* point_out, lorb_ba_summary* summaries);
@@ -485,7 +489,7 @@ int lorb_ba_plan_destroy(lorb_ba_plan* plan);
  * may be observed at most once per camera (the reference keys observations by Frame*,
  * include/map_point.h:83).  create: capacity allocations + the first build; update: rebuild from
  * the arrays' current contents (one small readback of counts and the camera covisibility, then
- * sorting, point groups and Schur pair lists on the device).  solve / read / info / destroy as
+ * sorting and point groups on the device).  solve / read / info / destroy as
  * lorb_ba_plan_*; result_dev writes the solution as float in the caller's pose order (device
  * pointers, either may be NULL; async). */
 typedef struct lorb_ba_window_dev {
@@ -501,6 +505,7 @@ typedef struct lorb_ba_window_dev {
   const int32_t* d_obs_frame;        /* max_obs: >= 0 optimised pose, -1-j fixed pose j, < -n_fixed unused */
   const float* d_obs_uv;             /* max_obs x 2 */
 } lorb_ba_window_dev;
+/* n_poses <= 128 (the camera tables travel as kernel arguments; LORB_E_UNSUPPORTED above) */
 int lorb_ba_plan_create_dev(lorb_ctx* ctx, const lorb_ba_window_dev* win, lorb_ba_plan** out);
 int lorb_ba_plan_update_dev(lorb_ba_plan* plan, const lorb_ba_window_dev* win);
 int lorb_ba_plan_result_dev(lorb_ba_plan* plan, float* d_pose_out, float* d_point_out);
@@ -511,7 +516,7 @@ int lorb_ba_plan_result_dev(lorb_ba_plan* plan, float* d_pose_out, float* d_poin
  * that grow, so a call costs one host-to-device copy of the window, the device plan build (one small
  * readback), the captured LM graph and one device-to-host copy of the solution -- no per-call plan
  * construction, allocation or graph capture.  Windows the device plans do not take (no cameras /
- * points / observations, a point with 256 or more observations) run through lorb_ba_local's
+ * points / observations, more than 128 cameras, a point with 256 or more observations) run through lorb_ba_local's
  * host-built plan on the same GPU kernels.  A point observed twice by one camera is an error (both
  * plan builders; the reference keys observations by Frame*).  One solver per ctx / thread.
  * pose_out: n_poses x 6 doubles (caller order), point_out: n_points x 3 doubles.  Synchronous. */
@@ -570,7 +575,7 @@ int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8);
  * ---------------------------------------------------------------------------------------- */
 typedef struct lorb_map lorb_map;
 typedef struct lorb_map_init {
-  int32_t n_window, n_fixed;          /* W optimised keyframes (ids 0..W-1), F fixed (ids -1..-F) */
+  int32_t n_window, n_fixed;          /* W <= 128 optimised keyframes (ids 0..W-1), F fixed (ids -1..-F) */
   int32_t max_points, max_obs, max_keypoints;   /* capacities */
   float fx, fy, cx, cy;
   const float* pose;                  /* W x 6 (mRvec | mTvec), row j = keyframe j */
