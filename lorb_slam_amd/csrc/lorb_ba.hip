@@ -227,6 +227,8 @@ __device__ __forceinline__ double s3(const double m[6], int a, int b) {
 struct BaDev {
   lorb::RotJet* rot_lin;           // Ctot: rotation state (with d/daa) of x_pose[cur], per linearisation
   lorb::RotVal* rot_cand;          // Ctot: rotation state of the candidate pose x_pose[cur ^ 1]
+  lorb::RotJet* rot_fix;           // NF: rotation states of the fixed poses (k_ba_init; they never change)
+  lorb::RotVal* rotv_fix;          // NF: the same, value only (the candidate cost)
   const BaWin* win;
   const PBlk* pblk;
   const int* obs_pt;         // K  (global point of each observation)
@@ -281,7 +283,7 @@ __device__ __forceinline__ int u21(int a, int b) {  // packed upper index of 6x6
 // K0: start of a solve, one launch: window states, x[0] <- the initial values, and the
 // per-camera rotation states of that first linearisation point (transcendentals once per
 // camera; later ones come from k_ba_lm_end on acceptance).
-__global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n_pt, LMOpt o) {
+__global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n_pt, int nf, LMOpt o) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < W) {
     WinState s;
@@ -297,6 +299,13 @@ __global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n
 #pragma unroll
     for (int k = 0; k < 6; ++k) { x[k] = d.x_init_pose[6 * i + k]; d.x_pose[0][6 * i + k] = x[k]; }
     d.rot_lin[i] = lorb::rot_jet(x);
+  }
+  if (i < nf) {  // the fixed poses' rotation states, once per solve (k_ba_ls / k_ba_bs2 read them)
+    double x[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) x[k] = d.fixed_pose[6 * i + k];
+    d.rot_fix[i] = lorb::rot_jet(x);
+    d.rotv_fix[i] = lorb::rot_val(x);
   }
   for (int k = i; k < 3 * n_pt; k += gridDim.x * blockDim.x) d.x_pt[0][k] = d.x_init_pt[k];
 }
@@ -2444,11 +2453,11 @@ __device__ __forceinline__ void pm_lin(const BaDev& d, const BaWin& W, int cur, 
 #pragma unroll
     for (int k = 0; k < 3; ++k) tr[k] = d.x_pose[cur][6 * c + 3 + k];
     residual_jac_s(d.rot_lin[c], tr, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
-  } else {
-    double pose[6];
+  } else {  // a fixed keyframe: its rotation state from k_ba_init (rot_jet of the same pose: the same bits)
+    double tr[3];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * fx + k];
-    residual_jac(pose, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
+    for (int k = 0; k < 3; ++k) tr[k] = d.fixed_pose[6 * fx + 3 + k];
+    residual_jac_s(d.rot_fix[fx], tr, X, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, r, Jp, Jc);
   }
 }
 
@@ -3012,10 +3021,10 @@ __global__ __launch_bounds__(kGB) void k_ba_bs2(BaDev d) {
       m1 -= ya1;
       residual_s(Rc, tc, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
     } else {
-      double pose[6];
+      double tr[3];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) pose[k] = d.fixed_pose[6 * fx_ + k];
-      residual(pose, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
+      for (int k = 0; k < 3; ++k) tr[k] = d.fixed_pose[6 * fx_ + 3 + k];
+      residual_s(d.rotv_fix[fx_], tr, Xn, W.fx, W.fy, W.cx, W.cy, uv.x, uv.y, rn);
     }
     mcc = m0 * (r[0] + m0 / 2.0) + m1 * (r[1] + m1 / 2.0);
     ncost = 0.5 * (rn[0] * rn[0] + rn[1] * rn[1]);
@@ -3818,6 +3827,8 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   d.rank0 = comm ? (comm->rank == 0) : 1;
   LORB_TRY(dalloc(P, (size_t)P->Ctot, &d.rot_lin));
   LORB_TRY(dalloc(P, (size_t)P->Ctot, &d.rot_cand));
+  LORB_TRY(dalloc(P, (size_t)std::max(P->NF, 1), &d.rot_fix));
+  LORB_TRY(dalloc(P, (size_t)std::max(P->NF, 1), &d.rotv_fix));
   if (P->env_total) LORB_HIP(ctx, hipMemsetAsync(d.env, 0, sizeof(double) * P->env_total, ctx->stream));
   LORB_TRY(dalloc(P, (size_t)P->n_total, &d.ycam)); LORB_TRY(dalloc(P, (size_t)P->n_pblk * 8, &d.part));
 #ifdef LORB_CHOL_TRACE
@@ -3997,9 +4008,9 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
 int enqueue_solve(lorb_ba_plan* P, const LMOpt& o) {
   lorb_ctx* ctx = P->ctx;
   {
-    const int n = std::max(std::max(P->W, P->Ctot), std::min(3 * P->pt_launch, 256 * 1024));
+    const int n = std::max(std::max(std::max(P->W, P->Ctot), P->NF), std::min(3 * P->pt_launch, 256 * 1024));
     hipLaunchKernelGGL(k_ba_init, dim3(lorb::ceil_div(std::max(n, 1), 256)), dim3(256), 0, ctx->stream, P->dev, P->W,
-                       P->Ctot, P->pt_launch, o);
+                       P->Ctot, P->pt_launch, P->NF, o);
   }
   LORB_CHECK_LAUNCH(ctx);
   // no iterations: one linearisation (cost, termination) as the head of a first iteration
@@ -4630,6 +4641,7 @@ int dev_alloc(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   d.sharded = comm ? 1 : 0;
   d.rank0 = comm ? (comm->rank == 0) : 1;
   LORB_TRY(dalloc(P, C, &d.rot_lin)); LORB_TRY(dalloc(P, C, &d.rot_cand));
+  LORB_TRY(dalloc(P, (size_t)std::max(b.F, 1), &d.rot_fix)); LORB_TRY(dalloc(P, (size_t)std::max(b.F, 1), &d.rotv_fix));
   LORB_TRY(dalloc(P, n, &d.ycam));
 #ifdef LORB_CHOL_TRACE
   LORB_TRY(dalloc(P, (size_t)512, &d.dbg));
