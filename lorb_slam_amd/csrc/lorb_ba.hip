@@ -1053,9 +1053,6 @@ __device__ __forceinline__ void wait_ge(int* c, int v) {
 
 // 1: the update waves spin on the chain's L post instead of sleeping between polls (same-box A/B
 // 46.2 / 46.1 vs 46.1 / 45.5 us: inside the noise, off)
-#ifndef LORB_UPD_SPIN
-#define LORB_UPD_SPIN 0
-#endif
 // Column stride of the chain's L columns in xch, padded against bank conflicts when the update
 // wave reads them in MFMA operand layout.
 constexpr int kCS = 65;
@@ -1245,7 +1242,7 @@ struct BandSide {
       tn_addr += dstep;
       const bool nxt = kb + 16 < kend;
       tr(0);
-      wait_ge<!LORB_UPD_SPIN>(lrd, ++lwant);
+      wait_ge<true>(lrd, ++lwant);
       tr(1);
       double opA[4][4];
 #pragma unroll
@@ -1534,97 +1531,6 @@ struct BandSide {
       for (int k = 0; k < 16; ++k) cf[k] = cg[k];
     }
   }
-  // LORB_BSG: this side's coupling to M solved ahead of y_M.  With R = this side's rows, the back-
-  // substitution of rows < R is y_R = L_R^-T (z_R - L_MR^T y_M) = w - G y_M, w = L_R^-T z_R and
-  // G = L_R^-T C, C(i, k) = L(R + k, i) (k < 48: M's rows).  Both need only L_R and the inverted
-  // diagonal blocks X, final when this side's panels are, so they run during the M phase; after
-  // y_M only the 48-term product G y_M per row remains (bsg_combine).  G's 16-column tiles k0[q]
-  // on the matrix cores, block by block from the bottom: the window of rows c0-48 .. c0+15 as four
-  // 16-row accumulator tiles (row c0-48+16t + (lane>>4) + 4r in register r of tile t, column k0 +
-  // (lane&15)), then G_b = X_b^T R_b (4 v_mfma_f64_16x16x4f64; R_b's register st is exactly the B
-  // operand of step st), R_above -= L_b,above^T G_b (12; bsk_block's L operand), and the window
-  // slides (rows entering above are zero: C's rows start at R - 47).  G row i at G[64 i + k];
-  // tile q's columns start at k0 = kb + 16 q.
-  template <int NTL>
-  __device__ __forceinline__ void bsg_tiles(int R, int kb, double* G) const {
-    const int ci = lane & 15, ck = lane >> 4;
-    v4d acc[NTL][4];
-    // C's window of block R - 16, branch-free (out-of-band / negative rows read the zero word)
-#pragma unroll
-    for (int q = 0; q < NTL; ++q)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = R - 64 + 16 * t + ck + 4 * r, k = R + kb + 16 * q + ci;
-          acc[q][t][r] = A[(i >= 0 && k - i <= bw) ? idx(k, i) : zslot];
-        }
-    // a block's operands, at addresses linear in c0 (per-lane offsets and validity fixed):
-    // X(c0 + j, c0 + ci) = (X^T)(ci, j), j = 4 st + ck >= ci, and L(c0 + j, r), r = c0 - 48 + 16 t
-    // + ci above the block, 1 <= j + 48 - 16 t - ci <= bw, r >= 0
-    const int dstep = si + sj;
-    int oX[4], oL[3][4];
-    bool vL[3][4];
-#pragma unroll
-    for (int st = 0; st < 4; ++st) {
-      const int j = 4 * st + ck;
-      oX[st] = j >= ci ? base + si * j + sj * ci : -1;
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-        const int dd = j + 48 - 16 * t - ci;
-        vL[t][st] = dd >= 1 && dd <= bw;
-        oL[t][st] = base + si * j + sj * (16 * t + ci - 48);
-      }
-    }
-    auto ld = [&](int c0, double (&xa)[4], double (&la)[3][4]) {
-      const int a0 = dstep * c0;
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        xa[st] = A[oX[st] >= 0 ? a0 + oX[st] : zslot];
-#pragma unroll
-        for (int t = 0; t < 3; ++t)
-          la[t][st] = A[(vL[t][st] && c0 - 48 + 16 * t + ci >= 0) ? a0 + oL[t][st] : zslot];
-      }
-    };
-    auto step = [&](int c0, const double (&xa)[4], const double (&la)[3][4]) {
-      tr_bs(0);
-      const_cast<BandSide*>(this)->bslot += 1;
-      v4d y[NTL];
-#pragma unroll
-      for (int q = 0; q < NTL; ++q) {
-        y[q] = v4d{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int st = 0; st < 4; ++st) y[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[st], acc[q][3][st], y[q], 0, 0, 0);
-      }
-#pragma unroll
-      for (int t = 2; t >= 0; --t)  // tile 2 first: the next block's chain waits on it
-#pragma unroll
-        for (int q = 0; q < NTL; ++q)
-#pragma unroll
-          for (int st = 0; st < 4; ++st)
-            acc[q][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(-la[t][st], y[q][st], acc[q][t], 0, 0, 0);
-#pragma unroll
-      for (int q = 0; q < NTL; ++q) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) G[64 * (c0 + ck + 4 * r) + kb + 16 * q + ci] = y[q][r];
-        acc[q][3] = acc[q][2];
-        acc[q][2] = acc[q][1];
-        acc[q][1] = acc[q][0];
-        acc[q][0] = v4d{0.0, 0.0, 0.0, 0.0};
-      }
-    };
-    // two operand sets alternate (no copies: a copy would wait for the loads in flight)
-    double xa[4], la[3][4], xb[4], lb[3][4];
-    ld(R - 16, xa, la);
-    for (int c0 = R - 16;; c0 -= 32) {
-      ld(max(c0 - 16, 0), xb, lb);
-      step(c0, xa, la);
-      if (c0 - 16 < 0) break;
-      ld(max(c0 - 32, 0), xa, la);
-      step(c0 - 16, xb, lb);
-      if (c0 - 32 < 0) break;
-    }
-  }
 };
 
 // Flat copy of band chunks [j0, j1) (16-byte chunks of the row-major n x (bw + 1) band) by nthr
@@ -1732,23 +1638,10 @@ __device__ __forceinline__ double stage_fix_val(const BaDev& d, const LMOpt& o, 
 }
 
 constexpr int kChol2sThreads = 512;
-// 1: the epilogue's pose state loaded at the kernel's start (registers live through the kernel:
-// 232 -> 256 VGPRs of k_ba_chol_2s<true>; same-box A/B 46.4 / 45.8 vs 46.4 / 45.9 us: off)
-#ifndef LORB_CHOL_EPI_PREFETCH
-#define LORB_CHOL_EPI_PREFETCH 0
-#endif
-// LORB_BSK 1: the T / B back-substitution runs one LDS round trip per block (BandSide::bsk_block /
-// bs_run_k).  LORB_BSG 1 (measured slower, kept for the record): y_T / y_B as w - G y_M, with G
-// and w computed during the M phase (BandSide::bsg_tiles); replaces LORB_BSK's operators.  G's 768
-// f64 matrix ops per window (~49k SIMD cycles at 64 each) do not fit the M phase's ~21k cycles on
-// the two SIMDs the M phase leaves free, and the extra live registers (250 VGPRs, SGPR spills)
-// slow the T / B chains: the Cholesky measured 115k cycles against 97k.
-#ifndef LORB_BSG
-#define LORB_BSG 0
-#endif
-#ifndef LORB_BSK
-#define LORB_BSK (!LORB_BSG)
-#endif
+// The T / B back-substitution runs one LDS round trip per block (BandSide::bsk_block / bs_run_k).
+// (Measured and removed: the epilogue's pose state loaded at the kernel's start, 232 -> 256 VGPRs,
+// no gain; y_T / y_B as w - G y_M with G and w formed during the M phase, 115 k cycles against
+// 97 k -- DESIGN §4.)
 
 // LDS words of k_ba_chol_2s: band (n16 rows), both sides' rhs (n16 + 48), two 64 x 18 exchanges
 // (together the 48 x 48 combine), zX (48), two 64 x 17 panel hand-off buffers, a zero word
@@ -1812,11 +1705,10 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   // of L as the panels finish, for the back-substitution.
   __shared__ unsigned long long s_mask;
   __shared__ int s_pdone[2];
-  __shared__ int s_linv[2];           // diagonal-block inverses done, per side (LORB_BSK)
+  __shared__ int s_linv[2];           // diagonal-block inverses done, per side
   __shared__ int s_lrd[2], s_prd[2];  // per side: L panels posted (chain), panel columns posted (update)
   __shared__ int s_hand[3];           // T / B -> M hand-over (below)
-  __shared__ int s_cz, s_gd[2], s_wd[2];  // LORB_BSG: top z final; G tiles / w done, per side
-  __shared__ int s_kdone[2];          // LORB_BSK: operator builders done, per side
+  __shared__ int s_kdone[2];          // operator builders done, per side
   const double2* __restrict__ S2 = reinterpret_cast<const double2*>(d.env + W.env_base);
   const int nch = n16 * B1 / 2, nsrc = n * B1 / 2;  // chunks (n is a multiple of 6: even)
   const int nbk = n16 / 16, ib = 4;
@@ -1838,15 +1730,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     fv1 = stage_fix_val(d, o, W, S0.radius, 16 * (nbk - ib), n16, t, fa1);
   }
   const int cur = S0.cur, ep = t - (NT - 128);  // epilogue: camera ep (+ 128 k) of the window
-  double xp0[6] = {0, 0, 0, 0, 0, 0}, sp0[6] = {0, 0, 0, 0, 0, 0};
-  if (LORB_CHOL_EPI_PREFETCH && ep >= 0) {  // (waves 6 / 7: uniform)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const int c = W.pose_base + (ep < W.n_poses ? ep : 0);
-      xp0[k] = d.x_pose[cur][6 * c + k];
-      sp0[k] = d.scale_pose[6 * c + k];
-    }
-  }
   double rz;
   {
     const int row = t < rt ? t : n16 - 1 - (t - rt);
@@ -1873,7 +1756,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     s_linv[0] = 0; s_linv[1] = 0;
     s_lrd[0] = 0; s_lrd[1] = 0; s_prd[0] = 0; s_prd[1] = 0;
     s_hand[0] = 0; s_hand[1] = 0; s_hand[2] = 0;
-    s_cz = 0; s_gd[0] = 0; s_gd[1] = 0; s_wd[0] = 0; s_wd[1] = 0;
     s_kdone[0] = 0; s_kdone[1] = 0;
     unsigned long long msk = 0;
     for (int b = 0; b < nbk; ++b) msk |= (unsigned long long)(!prog || b < ib || b >= nbk - ib) << (b & 63);
@@ -1956,9 +1838,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
       while (__hip_atomic_load(pd, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= p) __builtin_amdgcn_s_sleep(1);
       TR1(56 + 32 * side + 2 * p);   // dbg[256 + 32 side + 2 p]
       me.linv(16 * p);
-#if LORB_BSK || LORB_BSG
       if (lane == 0) __hip_atomic_fetch_add(&s_linv[side], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
       TR1(57 + 32 * side + 2 * p);
     }
     TR1(10 + side);
@@ -1969,31 +1849,11 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     if (wv == 0) { if (lane == 0) { phv[0] = phv[1] = phv[2] = 0; } const_cast<BandSide&>(me).phases = phv; }
 #endif
     me.chain(P, zr, bad, 0, side == 0 ? m : nB, true, lrd, prd, pwant, pb);
-#if LORB_BSG
-    if (wv == 0 && lane == 0) __hip_atomic_fetch_add(&s_cz, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
   } else if (wv < 4) {
     me.init_tiles(T);
     me.update(T, 0, side == 0 ? m : nB, lrd, prd, lwant, pb);
   }
   if (wv < 6) C2_STAMP(wv);
-#if LORB_BSG
-  // G's three 16-column tiles per side, once the side's panels and diagonal inverses are done
-  // (bsg_tiles), on SIMDs 1 and 3: the f64 matrix ops share the DP pipe with the M phase's chain
-  // (SIMD 0) and update (SIMD 2) waves.  Wave 5 the top side's, wave 7 the bottom side's.
-  auto gtiles = [&](int gs) {
-    const BandSide& g = gs == 0 ? top : bot;
-    const int R = gs == 0 ? m : nB;
-    wait_ge<true>(&s_linv[gs], R / 16);
-    TR1(16 + 2 * gs);
-    g.bsg_tiles<3>(R, 0, g.kco);
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): G is in L2 before the post
-    if (lane == 0) __hip_atomic_fetch_add(&s_gd[gs], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    TR1(17 + 2 * gs);
-  };
-  if (wv == 5 || wv == 7) gtiles(wv == 7);
-#endif
-#if LORB_BSK
   // The T / B back-substitution operators (bsk_block, on the matrix cores), once a side's diagonal
   // inverses are done, on SIMDs 1 and 3 (the M phase's chain and update waves are on 0 and 2): waves
   // 5 / 7 build the top side's (alternate blocks, in the order the back-substitution needs them),
@@ -2010,7 +1870,6 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     TR1(17 + 2 * ks);
   };
   if (wv == 5 || wv == 7) build_ops(0, wv == 7);
-#endif
   // Hand-over to the M phase by flags, not barriers (the diagonal-block inverses of waves 4 / 5
   // may still be running): wave 2 posts that it has read its last L from xt, wave 3 then writes
   // the bottom side's window on M into X = xt (+ xb) and posts it, wave 1 posts zX.
@@ -2036,25 +1895,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     if (bad) s_bad = 1;
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[2], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-#if LORB_BSK
   if (wv == 1 || wv == 3) build_ops(1, wv == 3);
-#endif
-#if LORB_BSG
-  // w = L_R^-T z_R (bs_run on the inverted diagonal blocks, in place in z's rows < R): wave 3 the
-  // top side's after its hand-over, wave 1 the bottom side's after its chain
-  if (wv == 1 || wv == 3) {
-    const int ws = wv == 3 ? 0 : 1;
-    const BandSide& g = ws == 0 ? top : bot;
-    const int R = ws == 0 ? m : nB;
-    if (ws == 0) wait_ge<true>(&s_cz, 1);
-    wait_ge<true>(&s_linv[ws], R / 16);
-    TR1(22 + 2 * ws);
-    BandSide::BsWin S{g.bs_init(R - 16, 0)};
-    g.bs_run<true>(S, R - 16, 0);
-    if (lane == 0) __hip_atomic_fetch_add(&s_wd[ws], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    TR1(23 + 2 * ws);
-  }
-#endif
   if (wv == 2) {
     TR1(0);
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2099,14 +1940,7 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     if (bad) s_bad = 1;
     C2_STAMP(6);
   }
-#if LORB_BSG
-  __syncthreads();
-  if (s_bad) {
-    if (t == 0) d.st[w].chol_fail = 1;
-    return;
-  }
-#endif
-  // (LORB_BSK: no barrier here.  Wave 0 goes from M's factor straight into the back-substitution,
+  // (No barrier here.  Wave 0 goes from M's factor straight into the back-substitution,
   // wave 1 waits for y_M by flag, the operators are complete by their builders' flags; a failed
   // factorization (s_bad) only computes values nobody reads and is caught after the last barrier.)
 #ifdef LORB_CHOL_PHASES
@@ -2114,59 +1948,15 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
 #else
 #define BS_PH(k) do {} while (0)
 #endif
-  // non-LORB_BSG: the side's operator set and window (wave 0 top, wave 1 bottom), then ONE call site
+  // the side's operator set and window (wave 0 top, wave 1 bottom), then ONE call site
   // of the unrolled T / B back-substitution for both waves (one copy of its code in the
   // instruction cache: the bottom side's copy missed it, 4 k cycles before its first block)
   double cf[16];
   BandSide::BsWin S{0.0};
   if (wv == 0) {
     BS_PH(3);
-#if LORB_BSK
     wait_ge<true>(&s_kdone[0], 2);
     top.bsk_load(m - 16, cf);  // the first T block's operator, loaded under the M blocks
-#endif
-#if LORB_BSG
-    S = BandSide::BsWin{top.bs_init(m + 32, 0)};
-    TR1(5);
-    top.bs_run<false>(S, m + 32, m);                   // y_M (chained triangles)
-    BS_PH(4);
-    TR1(6);
-    if (lane < 48) zb[nB + 47 - lane] = zt[m + lane];  // into the reversed bottom rows
-    if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    TR1(7);
-  } else if (wv >= 4) {
-    // y_R = w - G y_M, rows 64 h + lane (+ 128 q) of side wv & 1 (waves 4 / 6 top, 5 / 7 bottom):
-    // the first row's G (L2) is loaded before the waits, so after y_M only its 48 broadcast reads
-    // and the FMAs remain
-    const BandSide& g = side == 0 ? top : bot;
-    const int R = side == 0 ? m : nB;
-    wait_ge<true>(&s_gd[side], 1);
-    int i = 64 * (wv >> 1 & 1) + lane;
-    double2 gr[24];
-    const double2* G2 = reinterpret_cast<const double2*>(g.kco);
-#pragma unroll
-    for (int k2 = 0; k2 < 24; ++k2) gr[k2] = G2[32 * min(i, R - 1) + k2];
-    wait_ge<true>(&s_wd[side], 1);
-    wait_ge<true>(&s_hand[0], 2);
-    TR1(26 + (wv - 4));
-    const double2* zm = reinterpret_cast<const double2*>(g.z + R);
-    for (;;) {
-      double a4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int k2 = 0; k2 < 24; ++k2) {
-        const double2 v = zm[k2];
-        a4[(2 * k2) & 3] = fma(gr[k2].x, v.x, a4[(2 * k2) & 3]);
-        a4[(2 * k2 + 1) & 3] = fma(gr[k2].y, v.y, a4[(2 * k2 + 1) & 3]);
-      }
-      if (i < R) g.z[i] = g.z[i] - ((a4[0] + a4[1]) + (a4[2] + a4[3]));
-      i += 128;
-      if (i - lane >= R) break;
-#pragma unroll
-      for (int k2 = 0; k2 < 24; ++k2) gr[k2] = G2[32 * min(i, R - 1) + k2];
-    }
-    TR1(30 + (wv - 4));
-  }
-#else
     S = BandSide::BsWin{top.bs_init(m + 32, 0)};
     TR1(5);
     top.bs_run<false>(S, m + 32, m);                   // y_M (chained triangles)
@@ -2175,10 +1965,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     if (lane < 48) zb[nB + 47 - lane] = zt[m + lane];  // into the reversed bottom rows
     if (lane == 0) __hip_atomic_fetch_add(&s_hand[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   } else if (wv == 1) {
-#if LORB_BSK
     wait_ge<true>(&s_kdone[1], 2);
     bot.bsk_load(nB - 16, cf);
-#endif
     // the bottom window's pushes from M's 48 rows: L is final since the B phase, so its 48 entries
     // per lane are loaded before the wait; after it only y_M's broadcast reads and the FMAs remain
     // (four partial sums: a 48-long dependent FMA chain cost ~2 k cycles)
@@ -2209,22 +1997,17 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
   }
   if (wv < 2) {  // y_T (wave 0) / y_B (wave 1, reversed)
     const BandSide g = wv == 0 ? top : bot;
-#if LORB_BSK
     g.bs_run_k(S, (wv == 0 ? m : nB) - 16, 0, cf);  // one product per block
-#else
-    g.bs_run<true>(S, (wv == 0 ? m : nB) - 16, 0);  // inverted diagonal blocks
-#endif
     BS_PH(5 + 2 * wv);
     TR1(wv == 0 ? 7 : 12);
   }
-#endif
 #undef BS_PH
   if (wv == 0) C2_STAMP(7);
   __syncthreads();
   TR1(13);
 #undef C2_STAMP
 #undef TR1
-  if (!LORB_BSG && s_bad) {
+  if (s_bad) {
     if (t == 0) d.st[w].chol_fail = 1;
     return;
   }
@@ -2237,8 +2020,8 @@ __global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o)
     for (int k = 0; k < 6; ++k) {
       const int row = 6 * ci2 + k;
       const double y = row < rt ? zt[row] : zb[n16 - 1 - row];
-      const double xp = LORB_CHOL_EPI_PREFETCH && ci2 == ep ? xp0[k] : d.x_pose[cur][6 * c + k];
-      const double sp = LORB_CHOL_EPI_PREFETCH && ci2 == ep ? sp0[k] : d.scale_pose[6 * c + k];
+      const double xp = d.x_pose[cur][6 * c + k];
+      const double sp = d.scale_pose[6 * c + k];
       xn[k] = xp + (-y) * sp;
       d.x_pose[cur ^ 1][6 * c + k] = xn[k];
     }
