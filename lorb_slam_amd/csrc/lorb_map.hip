@@ -574,7 +574,7 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   else if (n <= 4096) LORB_APPEND(4);
   else LORB_APPEND(0);
 #undef LORB_APPEND
-  if (hipGetLastError() != hipSuccess) {  // the append (and its key merge) did not run: see above
+  if (hipGetLastError() != hipSuccess) {  // the append did not run: the map's counts are unknown
     M->broken = true;
     return lorb::set_error(ctx, LORB_E_DEVICE, "k_map_append launch failed; the map is unusable");
   }
