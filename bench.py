@@ -200,48 +200,54 @@ def workload_c4(ctx, args, rank):
     the BA plan on the device and runs 10 LM iterations.  The plan build is inside the step."""
     from lorb_slam_amd import _abi as A
     from lorb_slam_amd import synth
-    from lorb_slam_amd.runtime import Context, LocalMap
+    from lorb_slam_amd.runtime import Context, LocalMap, MapGroup
     W = args.windows
     n_kf_needed = args.warmup + args.steps + max(3, min(args.steps, 10)) + 2
     seqs = [synth.mapping_sequence(seed=4 + 1009 * rank + 17 * i, steps=n_kf_needed) for i in range(W)]
     opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
-    # one context (one stream) per window: the windows' steps run concurrently, each in its own
-    # stream order (the first window on the caller's context).  How HIP deals these streams (and the
-    # maps' side streams) to its 4 hardware queues matters: this layout in a fresh process measured
-    # 2.6 ms per 8-window step, 8 new contexts (or one more stream created first) 3.4 ms
-    # (tools/c4x8_host.py) -- hence sub_c4x8_run's child process
-    ctxs = [ctx] + [Context(ctx.device) for _ in range(W - 1)]
+    # Several windows: map groups of G = 2 maps (lorb_map_group: per step the maps' match, append,
+    # slide and plan build, then ONE set of BA launches for both windows), one context (stream) and
+    # one host thread per group, so W / G groups step concurrently (the first on the caller's
+    # context).  Measured on 8 C4 windows (tools/x8_chain_split.py, DESIGN §8): 4 groups of 2 1.97 ms
+    # per 8-window step, 2 of 4 2.20, 1 of 8 3.43, and the round-5 layout -- one map, stream and
+    # thread per window -- 2.44 (overlap off) / 2.62 ms (overlap on): HIP deals the streams to 4
+    # hardware queues, and one group's Cholesky (one CU per window) runs beside another group's
+    # point-group kernels.  One window: the map alone with the overlap of consecutive steps.
+    G = 2 if W > 1 else 1
+    ctxs = [ctx] + [Context(ctx.device) for _ in range((W + G - 1) // G - 1)]
+    owner = [i // G for i in range(W)]
     t0 = time.perf_counter()
-    maps = [LocalMap(c, s["init"]) for c, s in zip(ctxs, seqs)]
+    maps = [LocalMap(ctxs[owner[i]], s["init"]) for i, s in enumerate(seqs)]
+    groups = [MapGroup([maps[i] for i in range(W) if owner[i] == k]) for k in range(len(ctxs))] if W > 1 else None
     create_ms = (time.perf_counter() - t0) * 1e3
     # the keyframes below are uploaded (synchronously) before any step: step t+1's match and append
     # may run under step t's solve (lorb_map_set_overlap's requirement; tests/test_gpu_map.py checks
     # the overlapped chain bit-for-bit against the serial one)
-    for m in maps:
-        m.set_overlap(True)
+    if W == 1:
+        maps[0].set_overlap(True)
     fp = A.make_frame_params(synth.frame_params())
     # the keyframe stream, resident in HBM before the timed region
     kfs = [[(k["pose"], k["Tcw"], len(k["x"]), c.to_device(A.u8(k["desc"])), c.to_device(A.f32(k["x"])),
-             c.to_device(A.f32(k["y"])), c.to_device(A.f32(k["depth"]))) for k in s["steps"]] for c, s in zip(ctxs, seqs)]
+             c.to_device(A.f32(k["y"])), c.to_device(A.f32(k["depth"]))) for k in s["steps"]]
+           for c, s in zip([ctxs[o] for o in owner], seqs)]
     pos = [0]
 
-    # several windows: one host thread per window (each window's step blocks on its own plan
-    # readback; ctypes releases the GIL inside the call), so the windows' host phases overlap
-    pool = concurrent.futures.ThreadPoolExecutor(max_workers=W) if W > 1 else None
+    # one host thread per group (each group's step blocks on its plans' readbacks; ctypes releases
+    # the GIL inside the call), so the groups' host phases overlap
+    pool = concurrent.futures.ThreadPoolExecutor(max_workers=len(groups)) if groups else None
 
     def step():
         i = pos[0]
         if i >= n_kf_needed:
             raise RuntimeError("bench keyframe stream exhausted")
-
-        def one(m, ks):
-            pose, Tcw, n, dd, dx, dy, dz = ks[i]
-            m.step_dev(fp, pose, Tcw, n, dd, dx, dy, dz, opt)
         if pool is None:
-            one(maps[0], kfs[0])
+            pose, Tcw, n, dd, dx, dy, dz = kfs[0][i]
+            maps[0].step_dev(fp, pose, Tcw, n, dd, dx, dy, dz, opt)
         else:
-            for f in [pool.submit(one, m, ks) for m, ks in zip(maps, kfs)]:
+            def one(k):
+                groups[k].step_dev(fp, [kfs[j][i] for j in range(W) if owner[j] == k], opt)
+            for f in [pool.submit(one, k) for k in range(len(groups))]:
                 f.result()
         pos[0] = i + 1
 
@@ -265,6 +271,8 @@ def workload_c4(ctx, args, rank):
     kspec = ba_kspec(W, opt_obs, n_pts, F, bw)
 
     def cleanup():
+        for g in groups or []:
+            g.close()
         for m in maps:
             m.close()
         for ks in kfs:
@@ -283,6 +291,7 @@ def workload_c4(ctx, args, rank):
     return dict(step=step, check=check, sync=sync, maps=maps, ba_iters=10.0 * W, matches=float(W * nq), pairs=float(W) * nq * n_pts,
                 plan_ms=0.0, create_ms=create_ms, cleanup=cleanup, kspec=kspec, traffic_key="c4_chain",
                 config={"workload": "c4_local_mapping_step_chained", "windows_per_gpu": W, "kf": F,
+                        **({"map_groups": f"{len(groups)} x {G} windows (lorb_map_group), one stream each"} if groups else {}),
                         "fixed_kf": maps[0].F, "points": n_pts, "observations": n_obs, "lm_iterations": 10,
                         "new_kf_keypoints": nq, "match": f"{nq}x~{n_pts} bf crossCheck",
                         "step": "match + unproject + append + slide/cull + device plan build + 10 LM its + write-back"},
@@ -292,9 +301,12 @@ def workload_c4(ctx, args, rank):
 def sub_c4x8(ctx, D, args):
     """A filled GPU: the C4 chained step on 8 independent HBM-resident windows per
     GPU, stepped together (each step issues one keyframe to every window; north_star shards
-    independent windows).  Each window has its own context (stream) and host thread, so the windows'
-    steps run concurrently.  One window leaves most CUs idle during its Cholesky; this line shows
-    what one MI355X sustains with 8 in flight.  It does not replace the headline (one window)."""
+    independent windows).  The windows run as 4 map groups of 2 (lorb_map_group: one set of BA
+    launches per group and step), one context (stream) and host thread per group,
+    so the groups' steps run concurrently.  One window leaves most CUs idle during its Cholesky; this
+    line shows what one MI355X sustains with 8 in flight.  It does not replace the headline (one
+    window).  Its roofline comes from the profile pass, where per-kernel events make each group
+    solve its plans one after another (the same kernels per window)."""
     import copy
     a = copy.copy(args)
     a.windows, a.steps, a.warmup = 8, max(10, min(args.steps, 20)), max(2, min(args.warmup, 3))
@@ -322,32 +334,55 @@ def c4x8_one_plan(ctx, D, steps):
     """The LM solve alone on 8 independent C4 windows in ONE plan (every point-group, block and
     Cholesky kernel launched once for all 8 windows; tests/test_gpu_ba.py
     test_local_ba_eight_c4_windows_independent checks it bit for bit against 8 one-window plans):
-    10 LM iterations per solve, the plan built once outside the timed solves."""
+    10 LM iterations per solve, the plan built once outside the timed solves.  `four_plans_x2`: the
+    same 8 windows as 4 plans of 2 on 4 contexts (streams), the 4 solves enqueued back to back --
+    the layout of the c4x8 map groups."""
     from lorb_slam_amd import _abi as A
     from lorb_slam_amd import synth
-    from lorb_slam_amd.runtime import BAPlan
+    from lorb_slam_amd.runtime import BAPlan, Context
     wins = [synth.ba_window(seed=40 + i, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400) for i in range(8)]
     opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
-    plan = BAPlan(ctx, wins)
-    try:
+
+    def timed_solves(plans, ctxs):
         for _ in range(2):
-            plan.solve(opt)
-        ctx.sync()
+            for p in plans:
+                p.solve(opt)
+        for c in ctxs:
+            c.sync()
         D.barrier()
         t0 = time.perf_counter()
         for _ in range(steps):
-            plan.solve(opt)
-        ctx.sync()
-        el = D.reduce(time.perf_counter() - t0, "MAX")
+            for p in plans:
+                p.solve(opt)
+        for c in ctxs:
+            c.sync()
+        return D.reduce(time.perf_counter() - t0, "MAX")
+
+    plan = BAPlan(ctx, wins)
+    try:
+        el = timed_solves([plan], [ctx])
         s = plan.read()[2]
     finally:
         plan.close()
-    ms = el / steps * 1e3
+    ctxs = [ctx] + [Context(ctx.device) for _ in range(3)]
+    plans = [BAPlan(c, wins[2 * k:2 * k + 2]) for k, c in enumerate(ctxs)]
+    try:
+        el4 = timed_solves(plans, ctxs)
+        s4 = plans[0].read()[2]
+    finally:
+        for p in plans:
+            p.close()
+        for c in ctxs[1:]:
+            c.close()
+    ms, ms4 = el / steps * 1e3, el4 / steps * 1e3
     return {"workload": "c4_local_ba_x8_one_plan", "value": D.reduce(80.0 * steps, "SUM") / el,
             "unit": "BA iterations/s", "solves": steps, "ms_per_solve": ms,
             "roofline_iteration": roofline_iteration(wins[0], 50, ms / 80.0, "c4x8"),
-            "check": {"final_cost_w0": s[0]["final_cost"], "iterations_w0": s[0]["iterations"]}}
+            "check": {"final_cost_w0": s[0]["final_cost"], "iterations_w0": s[0]["iterations"]},
+            "four_plans_x2": {"value": D.reduce(80.0 * steps, "SUM") / el4, "unit": "BA iterations/s",
+                              "ms_per_8_windows": ms4, "final_cost_w0": s4[0]["final_cost"],
+                              "same_as_one_plan": s4[0]["final_cost"] == s[0]["final_cost"]}}
 
 
 def sub_c4x8_run(ctx, D, args):

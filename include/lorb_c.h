@@ -547,6 +547,22 @@ int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n);
 int lorb_ba_plan_trace(lorb_ba_plan* plan, int32_t window, lorb_lm_iteration* out, int32_t cap, int32_t* n_out);
 /* diagnostics: Cholesky phase stamps of window 0 (non-zero only in LORB_CHOL_STAMPS builds) */
 int lorb_ba_plan_debug_stamps(lorb_ba_plan* plan, unsigned long long* out8);
+/* Plan group: the LM solves of several plans on ONE ctx launched as one set of kernels (one launch per
+ * kernel for all members, one captured graph), as a plan of several windows is -- for independent
+ * windows whose plans are built separately (the device-built plans of several lorb_map windows:
+ * lorb_map_group_*).  No reference counterpart (the reference solves one window per call,
+ * src/bundle_adjust.cpp:308-314).  Each member's results (poses, points, summary, trace) are
+ * bit-identical to lorb_ba_plan_solve of that plan.  Up to 4 members run fused when every member is
+ * an unsharded plan on the two-sided Cholesky (lorb_ba_plan_info [1] == 2 after a solve; C3 / C4
+ * windows); otherwise the members are solved one after another.  The group does not own its plans:
+ * they must outlive it, and may be rebuilt (lorb_ba_plan_update_dev) between solves.  solve is
+ * asynchronous (read the members with lorb_ba_plan_read). */
+typedef struct lorb_ba_group lorb_ba_group;
+int lorb_ba_group_create(lorb_ctx* ctx, int32_t n_plans, lorb_ba_plan* const* plans, lorb_ba_group** out);
+int lorb_ba_group_solve(lorb_ba_group* group, const lorb_lm_options* opt);
+/* first n of: [0] member plans, [1] solves that ran as one set of launches, [2] graph captures */
+int lorb_ba_group_info(lorb_ba_group* group, int32_t* info, int32_t n);
+int lorb_ba_group_destroy(lorb_ba_group* group);
 
 /* ----------------------------------------------------------------------------------------
  * SURVEY §8 a17, the LocalMapping "full step" (SURVEY §7 item 8): a local map resident in HBM and
@@ -625,6 +641,30 @@ int lorb_map_counts(lorb_map* map, int32_t* out, int32_t n);
 int lorb_map_read(lorb_map* map, const lorb_map_state* state);
 int lorb_map_plan(lorb_map* map, lorb_ba_plan** out);   /* the map's BA plan (owned by the map) */
 int lorb_map_destroy(lorb_map* map);
+/* Several maps stepped together (independent LocalMapping windows on one GPU, north_star's sharding
+ * unit): every map on the same ctx.  A group step gives each map its keyframe (kfs[i] for maps[i]) and
+ * runs steps 1-3 and the plan build of every map, then ONE BA solve over all of their plans
+ * (lorb_ba_group, fused for up to 4 maps per group of launches), then the write-backs.  Each map's
+ * state after the step is bit-identical to lorb_map_step_dev of that map alone.  Errors: a map whose
+ * steps 1-3 or plan build fail returns the error as lorb_map_step_dev does; the maps before it in the
+ * group complete their step (solve and write-back), the maps after it are not stepped. */
+typedef struct lorb_map_group lorb_map_group;
+typedef struct lorb_map_keyframe {
+  const lorb_frame_params* frame;
+  const float* pose;                  /* 6 (host) */
+  const float* Tcw;                   /* 16 (host) */
+  int32_t n;
+  const uint8_t* d_desc;              /* device arrays of n keypoints, as lorb_map_step_dev */
+  const float* d_x;
+  const float* d_y;
+  const float* d_depth;
+} lorb_map_keyframe;
+int lorb_map_group_create(int32_t n_maps, lorb_map* const* maps, lorb_map_group** out);
+int lorb_map_group_step_dev(lorb_map_group* group, const lorb_map_keyframe* kfs, const lorb_lm_options* opt);
+/* first n of: [0] maps, [1] plan groups, [2] steps whose solves all ran as one set of launches per plan
+ * group, [3] graph captures over the plan groups */
+int lorb_map_group_info(lorb_map_group* group, int32_t* info, int32_t n);
+int lorb_map_group_destroy(lorb_map_group* group);
 
 /* ----------------------------------------------------------------------------------------
  * Multi-GPU: point-partitioned ("sharded") local BA.  No reference counterpart:

@@ -282,6 +282,12 @@ class MapInit(C.Structure):
                 ("obs_uv", f32p)]
 
 
+class MapKeyframe(C.Structure):
+    """lorb_map_keyframe: one map's keyframe of a lorb_map_group step (host pose / Tcw, device keypoints)."""
+    _fields_ = [("frame", C.POINTER(FrameParams)), ("pose", f32p), ("Tcw", f32p), ("n", C.c_int32),
+                ("d_desc", C.c_void_p), ("d_x", C.c_void_p), ("d_y", C.c_void_p), ("d_depth", C.c_void_p)]
+
+
 class MapState(C.Structure):
     """lorb_map_state: host buffers lorb_map_read fills (NULL = skip)."""
     _fields_ = [("point", f32p), ("point_desc", C.POINTER(C.c_uint8)), ("obs_point", i32p), ("obs_kf", i32p),

@@ -323,6 +323,7 @@ struct lorb_map {
   bool prof = false;
   double prof_ms[8] = {};
   int prof_n = 0;
+  std::chrono::steady_clock::time_point prof_clk{};
   int* mt = nullptr;
   // the step's crossCheck keys: per-query keys and per-train keys (all-ones between steps), owned by
   // the map so that its side-stream match shares no scratch with matcher calls on the ctx stream
@@ -514,10 +515,24 @@ int lorb_map_create(lorb_ctx* ctx, const lorb_map_init* in, lorb_map** out) {
   return LORB_OK;
 }
 
-int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float pose[6], const float Tcw[16], int32_t n,
-                      const uint8_t* d_desc, const float* d_x, const float* d_y, const float* d_depth,
-                      const lorb_lm_options* opt) {
-  if (!M || !frame || !pose || !Tcw || !opt || n < 0) return LORB_E_INVALID;
+}  // extern "C"
+
+namespace {
+
+// LORB_MAP_PROFILE: host wall time since the last mark into phase i, after a stream sync
+int map_mark(lorb_map* M, int i) {
+  if (!M->prof) return LORB_OK;
+  LORB_HIP(M->ctx, hipStreamSynchronize(M->ctx->stream));
+  const auto now = std::chrono::steady_clock::now();
+  M->prof_ms[i] += std::chrono::duration<double, std::milli>(now - M->prof_clk).count();
+  M->prof_clk = now;
+  return LORB_OK;
+}
+
+// steps 1-5 of lorb_map_step_dev: everything before the BA solve
+int map_prepare(lorb_map* M, const lorb_frame_params* frame, const float pose[6], const float Tcw[16], int32_t n,
+                const uint8_t* d_desc, const float* d_x, const float* d_y, const float* d_depth) {
+  if (!M || !frame || !pose || !Tcw || n < 0) return LORB_E_INVALID;
   lorb_ctx* ctx = M->ctx;
   if (n > M->n_cap) return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints > the map's max_keypoints %d", n, M->n_cap);
   if (n > 0 && (!d_desc || !d_x || !d_y || !d_depth)) return LORB_E_INVALID;
@@ -525,15 +540,8 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   hipStream_t s = ctx->stream;
   MapDev& m = M->m;
   const int kf = M->t0 + m.W;  // the new keyframe's id
-  auto clk = std::chrono::steady_clock::now();
-  auto mark = [&](int i) -> int {
-    if (!M->prof) return LORB_OK;
-    LORB_HIP(ctx, hipStreamSynchronize(s));
-    const auto now = std::chrono::steady_clock::now();
-    M->prof_ms[i] += std::chrono::duration<double, std::milli>(now - clk).count();
-    clk = now;
-    return LORB_OK;
-  };
+  M->prof_clk = std::chrono::steady_clock::now();
+  auto mark = [&](int i) { return map_mark(M, i); };
   LORB_TRY(mark(7));
   const bool ovl = M->overlap && M->built && !M->prof && !ctx->ktime;
   if (ovl && !M->side) {
@@ -620,14 +628,43 @@ int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float p
   M->built = true;
   LORB_TRY(mark(4));
   lorb::ba_plan_window_counts(M->plan, &M->h_P, &M->h_K);
-  // 6. LocalPoseOptimization + float write-back of poses (ring) and points (map)
-  LORB_TRY(lorb_ba_plan_solve(M->plan, opt));
-  LORB_TRY(mark(5));
-  // float write-back: poses straight into the ring (Frame::SetPose), points into the map
-  LORB_TRY(lorb::ba_plan_result_ring_dev(M->plan, m.ring, m.R, M->t0, m.pos));
-  LORB_TRY(mark(6));
+  return LORB_OK;
+}
+
+// 6b. after the solve: float write-back of the window's poses straight into the ring (Frame::SetPose)
+// and of the points into the map
+int map_finish(lorb_map* M) {
+  LORB_TRY(lorb::ba_plan_result_ring_dev(M->plan, M->m.ring, M->m.R, M->t0, M->m.pos));
+  LORB_TRY(map_mark(M, 6));
   if (M->prof) M->prof_n++;
   return LORB_OK;
+}
+
+}  // namespace
+
+// a group of maps on one ctx stepped together (lorb_map_group_*): their BA plans solved by plan
+// groups of up to kMapGrp maps
+constexpr int kMapGrp = 4;
+struct lorb_map_group {
+  std::vector<lorb_map*> maps;
+  std::vector<lorb_ba_group*> bag;
+  int n_steps_fused = 0;
+  ~lorb_map_group() {
+    for (lorb_ba_group* g : bag) (void)lorb_ba_group_destroy(g);
+  }
+};
+
+extern "C" {
+
+int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float pose[6], const float Tcw[16], int32_t n,
+                      const uint8_t* d_desc, const float* d_x, const float* d_y, const float* d_depth,
+                      const lorb_lm_options* opt) {
+  if (!M || !opt) return LORB_E_INVALID;
+  LORB_TRY(map_prepare(M, frame, pose, Tcw, n, d_desc, d_x, d_y, d_depth));
+  // 6. LocalPoseOptimization, then the float write-back
+  LORB_TRY(lorb_ba_plan_solve(M->plan, opt));
+  LORB_TRY(map_mark(M, 5));
+  return map_finish(M);
 }
 
 int lorb_map_set_overlap(lorb_map* M, int32_t enable) {
@@ -693,6 +730,80 @@ int lorb_map_destroy(lorb_map* M) {
   if (!M) return LORB_E_INVALID;
   (void)hipStreamSynchronize(M->ctx->stream);
   delete M;
+  return LORB_OK;
+}
+
+int lorb_map_group_create(int32_t n_maps, lorb_map* const* maps, lorb_map_group** out) {
+  if (n_maps < 1 || !maps || !out || !maps[0]) return LORB_E_INVALID;
+  *out = nullptr;
+  lorb_ctx* ctx = maps[0]->ctx;
+  for (int i = 0; i < n_maps; ++i) {
+    if (!maps[i]) return lorb::set_error(ctx, LORB_E_INVALID, "lorb_map_group_create: map %d is null", i);
+    if (maps[i]->ctx != ctx) return lorb::set_error(ctx, LORB_E_INVALID, "lorb_map_group_create: map %d is on another context", i);
+    for (int j = 0; j < i; ++j)
+      if (maps[j] == maps[i]) return lorb::set_error(ctx, LORB_E_INVALID, "lorb_map_group_create: map %d appears twice", i);
+  }
+  lorb_map_group* G = new (std::nothrow) lorb_map_group();
+  if (!G) return LORB_E_NOMEM;
+  G->maps.assign(maps, maps + n_maps);
+  for (int i0 = 0; i0 < n_maps; i0 += kMapGrp) {
+    std::vector<lorb_ba_plan*> plans;
+    for (int i = i0; i < std::min(n_maps, i0 + kMapGrp); ++i) plans.push_back(maps[i]->plan);
+    lorb_ba_group* g = nullptr;
+    if (const int rc = lorb_ba_group_create(ctx, (int32_t)plans.size(), plans.data(), &g); rc != LORB_OK) {
+      delete G;
+      return rc;
+    }
+    G->bag.push_back(g);
+  }
+  *out = G;
+  return LORB_OK;
+}
+
+int lorb_map_group_step_dev(lorb_map_group* G, const lorb_map_keyframe* kfs, const lorb_lm_options* opt) {
+  if (!G || !kfs || !opt) return LORB_E_INVALID;
+  const int n = (int)G->maps.size();
+  int rc = LORB_OK, ready = n;
+  for (int i = 0; i < n; ++i) {
+    const lorb_map_keyframe& k = kfs[i];
+    rc = map_prepare(G->maps[i], k.frame, k.pose, k.Tcw, k.n, k.d_desc, k.d_x, k.d_y, k.d_depth);
+    if (rc != LORB_OK) { ready = i; break; }
+  }
+  // 6. the BA solves: one plan group per kMapGrp maps; after a failure, the maps before the failing
+  //    one complete their step on their own plans
+  if (ready == n) {
+    bool fused = true;
+    for (lorb_ba_group* g : G->bag) {
+      int32_t before[2], after[2];
+      LORB_TRY(lorb_ba_group_info(g, before, 2));
+      LORB_TRY(lorb_ba_group_solve(g, opt));
+      LORB_TRY(lorb_ba_group_info(g, after, 2));
+      fused = fused && after[1] > before[1];
+    }
+    G->n_steps_fused += fused;
+  } else {
+    for (int i = 0; i < ready; ++i) LORB_TRY(lorb_ba_plan_solve(G->maps[i]->plan, opt));
+  }
+  for (int i = 0; i < ready; ++i) LORB_TRY(map_finish(G->maps[i]));
+  return rc;
+}
+
+int lorb_map_group_info(lorb_map_group* G, int32_t* info, int32_t n) {
+  if (!G || !info || n < 0) return LORB_E_INVALID;
+  int32_t caps = 0;
+  for (lorb_ba_group* g : G->bag) {
+    int32_t v[3];
+    LORB_TRY(lorb_ba_group_info(g, v, 3));
+    caps += v[2];
+  }
+  const int32_t v[4] = {(int32_t)G->maps.size(), (int32_t)G->bag.size(), G->n_steps_fused, caps};
+  for (int i = 0; i < n && i < 4; ++i) info[i] = v[i];
+  return LORB_OK;
+}
+
+int lorb_map_group_destroy(lorb_map_group* G) {
+  if (!G) return LORB_E_INVALID;
+  delete G;
   return LORB_OK;
 }
 

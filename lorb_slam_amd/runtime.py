@@ -583,6 +583,80 @@ class LocalMap:
             pass
 
 
+class BAGroup:
+    """lorb_ba_group: the LM solves of several plans on one context as one set of launches (each
+    plan's results bit-identical to its own solve).  The plans are not owned and must outlive it."""
+
+    def __init__(self, ctx, plans):
+        self.ctx, self.plans = ctx, list(plans)
+        arr = (C.c_void_p * len(self.plans))(*[p._p for p in self.plans])
+        self._p = C.c_void_p()
+        ctx.check(lib().lorb_ba_group_create(ctx.handle, C.c_int32(len(self.plans)), arr, C.byref(self._p)),
+                  "lorb_ba_group_create")
+
+    def solve(self, opt=None):
+        opt = opt or A.LMOptions.default()
+        self.ctx.check(lib().lorb_ba_group_solve(self._p, C.byref(opt)), "lorb_ba_group_solve")
+
+    def info(self):
+        v = (C.c_int32 * 3)()
+        self.ctx.check(lib().lorb_ba_group_info(self._p, v, C.c_int32(3)), "lorb_ba_group_info")
+        return dict(zip(("plans", "fused_solves", "captures"), [int(x) for x in v]))
+
+    def close(self):
+        if self._p:
+            lib().lorb_ba_group_destroy(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MapGroup:
+    """lorb_map_group: several LocalMaps on one context stepped together -- per map steps 1-3 and
+    the plan build, then one BA solve over all of their plans (lorb_ba_group), then the write-backs.
+    Each map's state is bit-identical to stepping it alone."""
+
+    def __init__(self, maps):
+        self.maps = list(maps)
+        self.ctx = self.maps[0].ctx
+        arr = (C.c_void_p * len(self.maps))(*[m._p for m in self.maps])
+        self._p = C.c_void_p()
+        self.ctx.check(lib().lorb_map_group_create(C.c_int32(len(self.maps)), arr, C.byref(self._p)),
+                       "lorb_map_group_create")
+
+    def step_dev(self, fp, kfs, opt=None):
+        """kfs: per map (pose, Tcw, n, d_desc, d_x, d_y, d_depth) with DeviceArrays; fp: FrameParams"""
+        opt = opt or A.LMOptions.default()
+        arr = (A.MapKeyframe * len(self.maps))()
+        keep = []
+        for k, (pose, Tcw, n, dd, dx, dy, dz) in zip(arr, kfs):
+            pose = A.f32(pose).reshape(6); T = A.f32(Tcw).reshape(16)
+            keep += [pose, T]
+            k.frame = C.pointer(fp); k.pose = A.ptr(pose, C.c_float); k.Tcw = A.ptr(T, C.c_float); k.n = int(n)
+            k.d_desc, k.d_x, k.d_y, k.d_depth = dd.ptr, dx.ptr, dy.ptr, dz.ptr
+        self.ctx.check(lib().lorb_map_group_step_dev(self._p, arr, C.byref(opt)), "lorb_map_group_step_dev")
+
+    def info(self):
+        v = (C.c_int32 * 4)()
+        self.ctx.check(lib().lorb_map_group_info(self._p, v, C.c_int32(4)), "lorb_map_group_info")
+        return dict(zip(("maps", "plan_groups", "fused_steps", "captures"), [int(x) for x in v]))
+
+    def close(self):
+        if self._p:
+            lib().lorb_map_group_destroy(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 Context.ba_pose_only = _ba_pose_only
 Context.ba_local = _ba_local
 

@@ -167,3 +167,89 @@ def test_local_mapping_overlapped_chain_bit_identical(ctx):
         for d in dev:
             for a in d[3:]:
                 a.free()
+
+
+def _dev_keyframes(ctx, seq, n):
+    return [(k["pose"], k["Tcw"], len(k["x"]), ctx.to_device(A.u8(k["desc"])), ctx.to_device(A.f32(k["x"])),
+             ctx.to_device(A.f32(k["y"])), ctx.to_device(A.f32(k["depth"]))) for k in seq["steps"][:n]]
+
+
+def _bitwise_same(a, b, label):
+    for k in ("t0", "points", "observations", "keypoints", "new_points", "new_observations", "matches"):
+        assert a[k] == b[k], (label, k, a[k], b[k])
+    for k in EXACT + ("point", "pose", "fixed_pose", "match_train"):
+        assert a[k].shape == b[k].shape and np.array_equal(a[k].view(np.uint8), b[k].view(np.uint8)), (label, k)
+    for k, v in b["summary"].items():
+        assert a["summary"][k] == v, (label, k, a["summary"][k], v)
+
+
+def _group_vs_solo(ctx, seqs, n_steps, expect_fused):
+    """maps stepped together (lorb_map_group, one ctx) vs the same maps stepped one by one
+    (lorb_map_step_dev, a second set of maps): bit for bit after every step, LM traces included"""
+    from lorb_slam_amd.runtime import MapGroup
+    fp = A.make_frame_params(synth.frame_params())
+    devs = [_dev_keyframes(ctx, s, n_steps) for s in seqs]
+    ctx.sync()
+    Mg = [LocalMap(ctx, s["init"]) for s in seqs]
+    Ms = [LocalMap(ctx, s["init"]) for s in seqs]
+    G = MapGroup(Mg)
+    try:
+        for t in range(n_steps):
+            G.step_dev(fp, [d[t] for d in devs], OPT10)
+            for m, d in zip(Ms, devs):
+                m.step_dev(fp, *d[t], OPT10)
+            for i, (a, b) in enumerate(zip(Mg, Ms)):
+                _bitwise_same(a.read(), b.read(), f"map {i} step {t}")
+                assert a.trace() == b.trace(), (i, t)
+        info = G.info()
+        assert info["maps"] == len(seqs) and info["plan_groups"] == (len(seqs) + 3) // 4, info
+        assert info["fused_steps"] == (n_steps if expect_fused else 0), info
+        return info
+    finally:
+        G.close()
+        for m in Mg + Ms:
+            m.close()
+        for d in devs:
+            for k in d:
+                for a in k[3:]:
+                    a.free()
+
+
+def test_local_mapping_group_bit_identical(ctx):
+    """several windows stepped through ONE set of BA launches per step (the
+    maps' device-built plans solved as a lorb_ba_group: every point-group, block and Cholesky kernel
+    launched once for all of them).  Two C4 windows and a 24-keyframe one, 3 steps: each map equals
+    the same map stepped alone, bit for bit (structure, poses, points, LM summary and per-iteration
+    trace), and every group step ran fused; the solo chain itself is the oracle-checked one
+    (test_local_mapping_chain_c4)."""
+    seqs = [synth.mapping_sequence(seed=4, steps=3), synth.mapping_sequence(seed=21, steps=3),
+            synth.mapping_sequence(seed=9, n_kf=24, n_fixed=3, n_new=90, obs_lens=(4, 5), steps=3, n_kps=800)]
+    info = _group_vs_solo(ctx, seqs, 3, expect_fused=True)
+    assert info["captures"] <= 3, info
+
+
+def test_local_mapping_group_chunks_and_fallback(ctx):
+    """Six small windows: two plan groups (4 + 2 maps).  With a 12-keyframe window among them (too
+    narrow for the two-sided Cholesky) its plan group solves its members one by one; the results
+    are bit-identical either way."""
+    small = [synth.mapping_sequence(seed=30 + i, n_kf=24, n_fixed=3, n_new=90, obs_lens=(4, 5), steps=2, n_kps=800)
+             for i in range(5)]
+    tiny = synth.mapping_sequence(seed=9, n_kf=12, n_fixed=3, n_new=60, obs_lens=(4, 5), steps=2, n_kps=600)
+    _group_vs_solo(ctx, small + [tiny], 2, expect_fused=False)
+
+
+def test_local_mapping_group_errors(ctx):
+    """a group's maps share one context and appear once"""
+    from lorb_slam_amd.runtime import Context, MapGroup
+    seq = synth.mapping_sequence(seed=9, n_kf=12, n_fixed=3, n_new=60, obs_lens=(4, 5), steps=1, n_kps=600)
+    c2 = Context(0)
+    a, b, c = LocalMap(ctx, seq["init"]), LocalMap(ctx, seq["init"]), LocalMap(c2, seq["init"])
+    try:
+        with pytest.raises(LorbError, match="another context"):
+            MapGroup([a, c])
+        with pytest.raises(LorbError, match="twice"):
+            MapGroup([a, b, a])
+    finally:
+        for m in (a, b, c):
+            m.close()
+        c2.close()
