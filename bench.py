@@ -322,7 +322,7 @@ def sub_c4x8(ctx, D, args):
            "unit": "BA iterations/s", "steps": a.steps, "ms_per_step": ms,
            "roofline": roofline_entry(kt, wl, pn),
            # per window-iteration: the step's time / (10 iterations x 8 windows)
-           "roofline_iteration": roofline_iteration(rwin, wl["config"]["kf"], ms / (10.0 * a.windows), "c4x8")
+           "roofline_iteration": roofline_iteration(rwin, wl["config"]["kf"], ms / (10.0 * a.windows), "c4x8", 2)
            if rwin is not None else None,
            "check": {"windows": chk["windows"][:2], "keyframes_stepped": chk["keyframes_stepped"]}}
     wl["cleanup"]()
@@ -834,10 +834,11 @@ def roofline_entry(kt, wl, steps):
             "all_kernels_ms_per_step": {K_NAMES.get(kk, str(kk)): v[0] / steps for kk, v in kt.items()}}
 
 
-def pmc_bytes_per_iteration(workload):
+def pmc_bytes_per_iteration(workload, group=1):
     """HBM bytes per LM iteration of the BA kernels (k_ba_*: every launch of a solve, k_ba_init's
     amortised) from this round's committed PMC summary, with the per-kernel breakdown; None when the
-    workload has no summary.  Iterations = k_ba_lm_end launches (one per LM iteration)."""
+    workload has no summary.  Iterations = k_ba_lm_end launches (one per LM iteration), plus `group`
+    window-iterations per k_ba_lm_end_g launch (a plan group's)."""
     for path in TRAFFIC:
         try:
             with open(path) as f:
@@ -845,7 +846,7 @@ def pmc_bytes_per_iteration(workload):
         except (OSError, ValueError):
             continue
         ks = (tab.get("workloads") or {}).get(workload, {}).get("kernels", {})
-        its = ks.get("k_ba_lm_end", {}).get("calls", 0)
+        its = ks.get("k_ba_lm_end", {}).get("calls", 0) + group * ks.get("k_ba_lm_end_g", {}).get("calls", 0)
         if not its:
             continue
         per = {k: e["calls"] * e["hbm_bytes_per_launch"] / its for k, e in ks.items()
@@ -854,7 +855,7 @@ def pmc_bytes_per_iteration(workload):
     return None
 
 
-def roofline_iteration(win, n_poses, ms_per_iteration, traffic_key):
+def roofline_iteration(win, n_poses, ms_per_iteration, traffic_key, group=1):
     """SURVEY §8(d)'s whole-iteration roofline of one LM iteration on a window:
        F_it = sum_obs 380 + sum_pts (60 + 108 k_p + 108 k_p (k_p + 1)) + (6F)^3 / 3 + 4 (6F)^2 + sum_obs 40
        B_it = 24 N_obs + 48 N_pts + 16 (6F)^2
@@ -871,7 +872,7 @@ def roofline_iteration(win, n_poses, ms_per_iteration, traffic_key):
     f_it = 420.0 * n_obs + float(np.sum(60.0 + 108.0 * kp + 108.0 * kp * (kp + 1.0))) + n6 ** 3 / 3.0 + 4.0 * n6 ** 2
     b_it = 24.0 * n_obs + 48.0 * n_pts + 16.0 * n6 ** 2
     t = ms_per_iteration * 1e-3
-    pmc = pmc_bytes_per_iteration(traffic_key)
+    pmc = pmc_bytes_per_iteration(traffic_key, group)
     return {"flop_per_iteration": f_it, "bytes_per_iteration": b_it, "ms_per_iteration": ms_per_iteration,
             "achieved_tflops": f_it / t / 1e12, "peak_tflops": FP64_PEAK / 1e12, "frac_fp64": f_it / t / FP64_PEAK,
             "achieved_gbs": b_it / t / 1e9, "peak_gbs": HBM_PEAK / 1e9, "frac_hbm": b_it / t / HBM_PEAK,

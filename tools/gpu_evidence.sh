@@ -5,7 +5,7 @@
 #   passes (tools/pmc_traffic.py -> gpurun_out/ROUND_traffic.json) for the C4 chained step, the shared
 #   window, C3 and C2, and one SQ MFMA pass.
 # Switches: NO_TESTS, NO_BENCH, NO_PROF=1 skip a part; TESTS="test_gpu_x ..." narrows the tests;
-# WORKLOADS="c4_chain shared_w1 c3 c2" narrows the profiled workloads; TRACE=1 adds the Cholesky trace
+# WORKLOADS="c4_chain shared_w1 c3 c2 c4x8" narrows the profiled workloads; TRACE=1 adds the Cholesky trace
 # (needs variants/liblorb_trace.so: tools/build_variant.sh trace -DLORB_CHOL_TRACE); C1=1 the C1 trace.
 RD=${1:-r05}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -15,7 +15,7 @@ P=$O/prof_$RD
 mkdir -p $O $P
 export TMPDIR=/tmp
 TESTS=${TESTS:-"test_gpu_solver test_gpu_map test_gpu_ba test_gpu_host_cpp test_gpu_window test_gpu_bf test_gpu_shard test_compute_descriptor test_golden"}
-WORKLOADS=${WORKLOADS:-"c4_chain shared_w1 c3 c2"}
+WORKLOADS=${WORKLOADS:-"c4_chain shared_w1 c3 c2 c4x8"}
 fail=0
 if [ -z "$NO_TESTS" ]; then
   for t in $TESTS; do
