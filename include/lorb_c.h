@@ -646,8 +646,9 @@ int lorb_map_destroy(lorb_map* map);
  * runs steps 1-3 and the plan build of every map, then ONE BA solve over all of their plans
  * (lorb_ba_group, fused for up to 4 maps per group of launches), then the write-backs.  Each map's
  * state after the step is bit-identical to lorb_map_step_dev of that map alone.  Errors: a map whose
- * steps 1-3 or plan build fail returns the error as lorb_map_step_dev does; the maps before it in the
- * group complete their step (solve and write-back), the maps after it are not stepped. */
+ * steps 1-3 or plan build fail is left as lorb_map_step_dev leaves it after that error; when a map's
+ * steps 1-3 fail, the maps after it in the group are not stepped; every other map completes its step
+ * (solve and write-back).  The first error is returned. */
 typedef struct lorb_map_group lorb_map_group;
 typedef struct lorb_map_keyframe {
   const lorb_frame_params* frame;

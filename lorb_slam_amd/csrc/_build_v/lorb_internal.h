@@ -55,16 +55,12 @@ namespace lorb {
 // Wait for the stream by polling an event from the host instead of a blocking synchronize: the
 // device plan build's one readback sits on the step's critical path, and a blocked host thread
 // wakes up tens of microseconds after the copy lands.
-inline hipError_t spin_wait(hipEvent_t ev) {
-  hipError_t e;
-  while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
-  }
-  return e;
-}
 inline hipError_t spin_sync(lorb_ctx* ctx) {
   hipError_t e = hipEventRecord(ctx->spin_ev, ctx->stream);
   if (e != hipSuccess) return e;
-  return spin_wait(ctx->spin_ev);
+  while ((e = hipEventQuery(ctx->spin_ev)) == hipErrorNotReady) {
+  }
+  return e;
 }
 }  // namespace lorb
 
@@ -116,11 +112,6 @@ int ba_plan_result_ring_dev(lorb_ba_plan* P, float* ring, int R, int t0, float* 
 // a device-built plan whose callers keep the observation slots sorted by point (stably, no unused
 // slots) builds without the counting sort; slots found out of order fall back to it (same result)
 void ba_plan_sorted_hint(lorb_ba_plan* P, bool sorted);
-// lorb_ba_plan_update_dev in two halves (unsharded device-built plans): issue queues the build's
-// first phase and its readback on the ctx stream; finish waits for that readback and completes the
-// build.  Work for other plans may be queued in between (lorb_map_group builds its maps this way).
-int ba_plan_update_dev_issue(lorb_ba_plan* P, const lorb_ba_window_dev* w);
-int ba_plan_update_dev_finish(lorb_ba_plan* P, const lorb_ba_window_dev* w);
 // the window's live point / observation counts as the last lorb_ba_plan_update_dev read them
 void ba_plan_window_counts(const lorb_ba_plan* P, int* n_points, int* n_obs);
 // the last device build's per-point observation offsets (point-sorted slots), device pointer

@@ -283,8 +283,8 @@ __device__ __forceinline__ int u21(int a, int b) {  // packed upper index of 6x6
 // K0: start of a solve, one launch: window states, x[0] <- the initial values, and the
 // per-camera rotation states of that first linearisation point (transcendentals once per
 // camera; later ones come from k_ba_lm_end on acceptance).
-__device__ __forceinline__ void init_run(const BaDev& d, int W, int ctot, int n_pt, int nf, const LMOpt& o, const int i,
-                                         const int stride) {
+__global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n_pt, int nf, LMOpt o) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < W) {
     WinState s;
     s.radius = o.init_radius; s.decrease_factor = 2.0; s.cost = 0.0; s.x_norm = 0.0; s.gmax = 0.0;
@@ -307,10 +307,7 @@ __device__ __forceinline__ void init_run(const BaDev& d, int W, int ctot, int n_
     d.rot_fix[i] = lorb::rot_jet(x);
     d.rotv_fix[i] = lorb::rot_val(x);
   }
-  for (int k = i; k < 3 * n_pt; k += stride) d.x_pt[0][k] = d.x_init_pt[k];
-}
-__global__ __launch_bounds__(256) void k_ba_init(BaDev d, int W, int ctot, int n_pt, int nf, LMOpt o) {
-  init_run(d, W, ctot, n_pt, nf, o, blockIdx.x * blockDim.x + threadIdx.x, gridDim.x * blockDim.x);
+  for (int k = i; k < 3 * n_pt; k += gridDim.x * blockDim.x) d.x_pt[0][k] = d.x_init_pt[k];
 }
 
 // Point groups (PBlk): consecutive points of one window whose observations (contiguous, sorted
@@ -457,16 +454,13 @@ __device__ __forceinline__ WinState lm_head(const BaDev& d, const LMOpt& o, int 
 }
 
 template <bool SH>
-__device__ __forceinline__ void lm_begin_run(const BaDev& d, const LMOpt& o, const int w) {
+__global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
+  const int w = blockIdx.x;
   const WinState* Sp = d.st + w;
   const WinState S = *Sp;
   const BaWin W = d.win[w];  // issued with the state, before the done test
   if (S.done) return;
   (void)lm_head<SH>(d, o, w, threadIdx.x, S, W);
-}
-template <bool SH>
-__global__ __launch_bounds__(64) void k_ba_lm_begin(BaDev d, LMOpt o) {
-  lm_begin_run<SH>(d, o, blockIdx.x);
 }
 
 typedef double v4d __attribute__((ext_vector_type(4)));
@@ -1660,7 +1654,7 @@ __host__ __device__ constexpr int chol2s_words(int n16, int bw) {
 // HEAD (the fused iteration): wave 4 first runs the iteration head (lm_head, k_ba_lm_begin's work)
 // while the first panels factor; a head that ends the solve leaves the candidate unwritten.
 template <bool HEAD>
-__device__ __forceinline__ void chol_2s_run(const BaDev& d, const LMOpt& o, const int w) {
+__global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int s_bad;
   __shared__ int s_head_done;
@@ -1668,6 +1662,7 @@ __device__ __forceinline__ void chol_2s_run(const BaDev& d, const LMOpt& o, cons
   const unsigned long long st_entry = __builtin_amdgcn_s_memtime();
 #endif
 
+  const int w = blockIdx.x;
   // window, state and failure flag requested together (one round trip before the band copy)
   const BaWin W = d.win[w];
   const WinState S0 = d.st[w];
@@ -1686,7 +1681,7 @@ __device__ __forceinline__ void chol_2s_run(const BaDev& d, const LMOpt& o, cons
     return;
   }
 #ifdef LORB_CHOL_TRACE
-  if (threadIdx.x == 0) d.dbg[512 * w + 250] = __builtin_amdgcn_s_memtime();  // raw: state loaded
+  if (threadIdx.x == 0) d.dbg[512 * blockIdx.x + 250] = __builtin_amdgcn_s_memtime();  // raw: state loaded
 #endif
   constexpr int NT = kChol2sThreads;
   const int n = W.n, bw = W.bw, B1 = bw + 1;
@@ -2036,8 +2031,6 @@ __device__ __forceinline__ void chol_2s_run(const BaDev& d, const LMOpt& o, cons
   if (t == 0) d.dbg[512 * w + 251] = __builtin_amdgcn_s_memtime();  // raw: epilogue issued (thread 0)
 #endif
 }
-template <bool HEAD>
-__global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s(BaDev d, LMOpt o) { chol_2s_run<HEAD>(d, o, blockIdx.x); }
 
 // the iteration's record (lorb_lm_iteration; S is the state the step was computed from)
 __device__ __forceinline__ void lm_record(const BaDev& d, int w, const WinState& S, int outcome, double mcc,
@@ -2262,7 +2255,7 @@ __device__ __forceinline__ void pm_lin(const BaDev& d, const BaWin& W, int cur, 
 //                    Jc_h^T K Jc_l (K = I - Q_h Jps_l^T on the diagonal, -Q_h Jps_l^T off it), plus
 //                    the camera terms on the diagonal; written to the group's partial.
 // Cost, point gradient max and |x|^2 partials per group (the head reads them when relinearising).
-__device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const unsigned bid) {
+__global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) {
   __shared__ double s_jc[kGB][12];   // B / C: per point Ei (0..5), bs (6..8), sp (9..11); D: Jc per slot
   __shared__ double s_qj[kGB][12];   // A / B: Jp^T Jp (6) | Jp^T r (3) per observation; D: Q | Jps per slot
   __shared__ double s_rg[kGB][4];    // D: r | g per slot
@@ -2270,11 +2263,11 @@ __device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const uns
   __shared__ int s_po[kGB];
   __shared__ int s_mm[2][kLsWaves];
   __shared__ double red3[3][kLsWaves];
-  if ((int)bid >= d.live[0]) return;
+  if ((int)blockIdx.x >= d.live[0]) return;
 #ifdef LORB_LS_STAMPS
   // dbg[8 g + k]: s_memtime at the kernel's entry (k 0) and after phase A (1), B (2), C (3), D (4),
   // the partial sums (5) of group g (thread 0)
-#define LS_STAMP(k) do { if (threadIdx.x == 0) d.dbg[8 * bid + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#define LS_STAMP(k) do { if (threadIdx.x == 0) d.dbg[8 * blockIdx.x + (k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define LS_STAMP(k) do {} while (0)
 #endif
@@ -2284,10 +2277,10 @@ __device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const uns
   // counter at the start (<< 20) | the ticks to the end (slot 7, written at LS_STAMP(5))
   const unsigned long long ls_rt0 = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0)
-    d.dbg[8 * bid + 6] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 8) |
+    d.dbg[8 * blockIdx.x + 6] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) << 8) |
                                 (__builtin_amdgcn_s_getreg((31 << 11) | 20) & 255);
 #endif
-  const PBlk g = d.pblk[bid];
+  const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const bool has = t < g.no;
   const int of = g.o0 + min(t, max(g.no - 1, 0));
@@ -2412,8 +2405,8 @@ __device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const uns
   LS_STAMP(3);
   // D
   const int bwc = W.bwc, nsl = pm_nslots(span, bwc);
-  double* gp = d.gpart + W.part_base + (size_t)(bid - W.pblk_base) * W.part_stride;
-  if (t == 0) d.gspan[bid] = make_int2(span > 0 ? cmin - W.pose_base : 0, span);
+  double* gp = d.gpart + W.part_base + (size_t)(blockIdx.x - W.pblk_base) * W.part_stride;
+  if (t == 0) d.gspan[blockIdx.x] = make_int2(span > 0 ? cmin - W.pose_base : 0, span);
   // Lane = slot (its whole 6 x 6 block: the point's loads serve 36 outputs), wave = point subset:
   // every lane of a wave walks the same points (k = wave, wave + 4, ...: a uniform loop, so the next
   // point's mask / offset are requested before this point's FMAs), a lane whose two cameras the
@@ -2535,14 +2528,13 @@ __device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const uns
   }
   LS_STAMP(4);
   block_red3w<kLsWaves, true>(cost, gm, xn2, red3);
-  if (t == 0) { double* P = d.part + 8 * bid; P[0] = cost; P[1] = gm; P[2] = xn2; }
+  if (t == 0) { double* P = d.part + 8 * blockIdx.x; P[0] = cost; P[1] = gm; P[2] = xn2; }
   LS_STAMP(5);
 #ifdef LORB_LS_STAMPS
-  if (t == 0) d.dbg[8 * bid + 7] = (ls_rt0 << 20) | ((__builtin_amdgcn_s_memrealtime() - ls_rt0) & 0xfffff);
+  if (t == 0) d.dbg[8 * blockIdx.x + 7] = (ls_rt0 << 20) | ((__builtin_amdgcn_s_memrealtime() - ls_rt0) & 0xfffff);
 #endif
 #undef LS_STAMP
 }
-__global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) { ls_run(d, o, blockIdx.x); }
 
 // PM-K2: one workgroup per camera block (h, l) of a window: the partials of the window's groups
 // whose camera window holds the block, summed in group order.  Thread = (entry e, subset s); the
@@ -2555,7 +2547,7 @@ __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) { ls_run
 // RT threads per block (256 or 1024: red_threads() picks per plan -- 1024 when a block has many
 // candidate groups, or the grid leaves CUs idle; 256 when many blocks share the GPU)
 template <int MODE, int RT>
-__device__ __forceinline__ void red_run(const BaDev& d, const LMOpt& o, const unsigned bid) {
+__global__ __launch_bounds__(RT) void k_ba_red(BaDev d, LMOpt o) {
   constexpr int kRt = RT, kRw = kRt / 64;
   constexpr int kRc = 1024 / kRt;  // groups per thread per chunk: 1024 groups' windows requested at once
   __shared__ int s_cand[kRt * kRc];
@@ -2563,8 +2555,8 @@ __device__ __forceinline__ void red_run(const BaDev& d, const LMOpt& o, const un
   __shared__ int s_wc[kRc][kRw];
   __shared__ double s_acc[1024];
   __shared__ double s_tot[54];
-  if ((int)bid >= d.live[1]) return;
-  const BlockPair bp = d.bp[bid];
+  if ((int)blockIdx.x >= d.live[1]) return;
+  const BlockPair bp = d.bp[blockIdx.x];
   const bool diag = bp.ch == bp.cl;
   if (MODE == 0 && !diag) return;
   const WinState& S = d.st[bp.win];
@@ -2701,17 +2693,15 @@ __device__ __forceinline__ void red_run(const BaDev& d, const LMOpt& o, const un
     if (MODE == 2) { d.U_part[21 * c + u21(i, i)] = s_tot[36 + i]; d.V_part[6 * c + i] = s_tot[42 + i]; }
   }
 }
-template <int MODE, int RT>
-__global__ __launch_bounds__(RT) void k_ba_red(BaDev d, LMOpt o) { red_run<MODE, RT>(d, o, blockIdx.x); }
 
 // PM-K3: point-group back-substitution with the linearisation re-evaluated
 // in registers instead of read back: b_p -= sum_e Jps_e^T (Jc_e y_c(e)), the point step and
 // candidate, then the model cost change and the candidate cost per observation.
-__device__ __forceinline__ void bs2_run(const BaDev& d, const unsigned bid) {
+__global__ __launch_bounds__(kGB) void k_ba_bs2(BaDev d) {
   __shared__ double sh[kGB][3], sst[kGB][3], sxn[kGB][3], ssp[kGB][3];
   __shared__ double red3[3][kGW];
-  if ((int)bid >= d.live[0]) return;
-  const PBlk g = d.pblk[bid];
+  if ((int)blockIdx.x >= d.live[0]) return;
+  const PBlk g = d.pblk[blockIdx.x];
   const int t = threadIdx.x;
   const bool has = t < g.no;
   const int of = g.o0 + min(t, max(g.no - 1, 0));
@@ -2824,77 +2814,9 @@ __device__ __forceinline__ void bs2_run(const BaDev& d, const unsigned bid) {
   }
   block_red3<false>(mcc, ncost, sn2, red3);
   if (t == 0) {
-    double* P = d.part + 8 * bid;
+    double* P = d.part + 8 * blockIdx.x;
     P[3] = mcc; P[4] = ncost; P[5] = sn2;
   }
-}
-__global__ __launch_bounds__(kGB) void k_ba_bs2(BaDev d) { bs2_run(d, blockIdx.x); }
-
-// ==========================================================================================
-// Plan groups (lorb_ba_group_*): the LM solves of up to kGrpMax plans -- the device-built plans of
-// several LocalMapping windows -- launched as ONE set of kernels on one stream, the way a plan of
-// several windows is.  Each launch deals its workgroups to the member plans by a block prefix
-// (GrpGrid); a workgroup runs the one-plan kernel's code on its member's BaDev (kernel arguments),
-// so every member's results are bit-identical to its own solve (the block-pair sums do not depend
-// on the k_ba_red width, k_ba_red's note).
-// ==========================================================================================
-constexpr int kGrpMax = 4;
-struct BaGrp {
-  BaDev d[kGrpMax];
-  int n;
-};
-struct GrpGrid {
-  int pre[kGrpMax + 1];  // workgroups of members [0, k); pre[n] = the launch's workgroups
-};
-struct GrpInit {  // k_ba_init's per-plan arguments
-  int W[kGrpMax], ctot[kGrpMax], n_pt[kGrpMax], nf[kGrpMax];
-};
-// the member running workgroup b, and b's index in that member's own launch (members without
-// workgroups in this launch are skipped: the last member whose prefix is <= b)
-__device__ __forceinline__ int grp_member(const GrpGrid& G, int n, unsigned b, unsigned& lb) {
-  int k = 0;
-#pragma unroll
-  for (int i = 1; i < kGrpMax; ++i) k += (i < n && (int)b >= G.pre[i]) ? 1 : 0;
-  lb = b - (unsigned)G.pre[k];
-  return k;
-}
-__global__ __launch_bounds__(256) void k_ba_init_g(BaGrp g, GrpGrid G, GrpInit a, LMOpt o) {
-  unsigned lb;
-  const int k = grp_member(G, g.n, blockIdx.x, lb);
-  init_run(g.d[k], a.W[k], a.ctot[k], a.n_pt[k], a.nf[k], o, (int)(lb * 256 + threadIdx.x),
-           (G.pre[k + 1] - G.pre[k]) * 256);
-}
-__global__ __launch_bounds__(kLsThreads) void k_ba_ls_g(BaGrp g, GrpGrid G, LMOpt o) {
-  unsigned lb;
-  const int k = grp_member(G, g.n, blockIdx.x, lb);
-  ls_run(g.d[k], o, lb);
-}
-template <int MODE, int RT>
-__global__ __launch_bounds__(RT) void k_ba_red_g(BaGrp g, GrpGrid G, LMOpt o) {
-  unsigned lb;
-  const int k = grp_member(G, g.n, blockIdx.x, lb);
-  red_run<MODE, RT>(g.d[k], o, lb);
-}
-__global__ __launch_bounds__(64) void k_ba_lm_begin_g(BaGrp g, GrpGrid G, LMOpt o) {
-  unsigned lb;
-  const int k = grp_member(G, g.n, blockIdx.x, lb);
-  lm_begin_run<false>(g.d[k], o, (int)lb);
-}
-template <bool HEAD>
-__global__ __launch_bounds__(kChol2sThreads) void k_ba_chol_2s_g(BaGrp g, GrpGrid G, LMOpt o) {
-  unsigned lb;
-  const int k = grp_member(G, g.n, blockIdx.x, lb);
-  chol_2s_run<HEAD>(g.d[k], o, (int)lb);
-}
-__global__ __launch_bounds__(kGB) void k_ba_bs2_g(BaGrp g, GrpGrid G) {
-  unsigned lb;
-  const int k = grp_member(G, g.n, blockIdx.x, lb);
-  bs2_run(g.d[k], lb);
-}
-__global__ __launch_bounds__(64) void k_ba_lm_end_g(BaGrp g, GrpGrid G, LMOpt o) {
-  unsigned lb;
-  const int k = grp_member(G, g.n, blockIdx.x, lb);
-  lm_end_run<false>(g.d[k], o, (int)lb, threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3156,12 +3078,6 @@ LMOpt to_dev_opt(const lorb_lm_options* o) {
   d.min_rel = o->min_relative_decrease; d.min_diag = o->min_lm_diagonal; d.max_diag = o->max_lm_diagonal;
   return d;
 }
-// field by field (LMOpt has padding after its ints: a memcmp would see whatever those bytes hold)
-bool same_opt(const LMOpt& a, const LMOpt& b) {
-  return a.max_iter == b.max_iter && a.max_invalid == b.max_invalid && a.jacobi == b.jacobi && a.ftol == b.ftol &&
-         a.gtol == b.gtol && a.ptol == b.ptol && a.init_radius == b.init_radius && a.max_radius == b.max_radius &&
-         a.min_radius == b.min_radius && a.min_rel == b.min_rel && a.min_diag == b.min_diag && a.max_diag == b.max_diag;
-}
 
 }  // namespace
 
@@ -3197,9 +3113,6 @@ struct lorb_ba_devbuild {
   std::vector<char> last_adj;
   std::vector<int> h_copy;  // host copy of the build's readback
   std::vector<int> last_map;
-  // a build issued (dev_build_issue: phase 1 and the readback queued) and not yet finished
-  hipEvent_t rb_ev = nullptr;
-  bool rb_pending = false, rb_sorted = false, rb_fuse = false;
 };
 
 struct lorb_ba_plan {
@@ -3220,7 +3133,6 @@ struct lorb_ba_plan {
   hipGraphExec_t gexec = nullptr;
   LMOpt graph_opt{};
   bool has_graph = false;
-  unsigned gen = 0;  // bumped whenever the plan's buffers move (a lorb_ba_group's graph then re-captures)
   // launch shape of the captured solve: a rebuild that keeps it (device-built plans launch the
   // point-group / block-pair kernels at capacity) replays the graph without a new capture
   struct GraphKey {
@@ -3323,7 +3235,6 @@ struct lorb_ba_plan {
     }
 #endif
     if (devb) {
-      if (devb->rb_ev) (void)hipEventDestroy(devb->rb_ev);
       if (devb->pinned) (void)hipHostFree(devb->pinned);
       if (devb->up_host) (void)hipHostFree(devb->up_host);
       delete devb;
@@ -3899,7 +3810,7 @@ int plan_solve(lorb_ba_plan* P, const lorb_lm_options* opt) {
   const bool timing = ctx->ktime || no_graph || (P->comm && !P->comm->rccl);
   if (timing) return enqueue_solve(P, o);
   const lorb_ba_plan::GraphKey key = graph_key(P);
-  if (!P->has_graph || !(key == P->gkey) || !same_opt(P->graph_opt, o)) {
+  if (!P->has_graph || !(key == P->gkey) || memcmp(&P->graph_opt, &o, sizeof(LMOpt)) != 0) {
     if (P->gexec) { (void)hipGraphExecDestroy(P->gexec); P->gexec = nullptr; }
     if (P->graph) { (void)hipGraphDestroy(P->graph); P->graph = nullptr; }
     LORB_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
@@ -3950,162 +3861,6 @@ int plan_read(lorb_ba_plan* P, double* const* pose_out, double* const* point_out
       for (int q = 0; q < 6; ++q)
         pose_out[w][6 * (size_t)c + q] = hp[w][6 * (size_t)(map.empty() ? c : map[c]) + q];
   }
-  return LORB_OK;
-}
-
-}  // namespace
-
-// A plan group (lorb_ba_group_*): member plans (not owned) on one context, solved by one set of
-// launches (k_ba_*_g) captured in one graph.  The graph holds the members' BaDev and launch shapes:
-// it is re-captured when a member's buffers moved (lorb_ba_plan::gen), its launch shape changed or
-// the options differ.
-struct lorb_ba_group {
-  lorb_ctx* ctx = nullptr;
-  std::vector<lorb_ba_plan*> plans;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t gexec = nullptr;
-  bool has_graph = false;
-  LMOpt graph_opt{};
-  std::vector<unsigned> gens;
-  std::vector<lorb_ba_plan::GraphKey> keys;
-  int n_fused = 0, n_captures = 0;  // solves run as one set of launches; graph captures
-  ~lorb_ba_group() {
-    if (gexec) (void)hipGraphExecDestroy(gexec);
-    if (graph) (void)hipGraphDestroy(graph);
-  }
-};
-
-namespace {
-
-// a group runs as one set of launches when every member is an unsharded plan on the two-sided
-// Cholesky (the fused iteration); otherwise its members are solved one after another, each by its
-// own path (the same bits either way)
-bool group_fused(const lorb_ba_group* G) {
-  static const bool no_fuse = [] { const char* e = getenv("LORB_NO_FUSE"); return e && e[0] == '1'; }();
-  if (no_fuse || G->ctx->ktime || G->plans.size() > (size_t)kGrpMax) return false;
-  for (const lorb_ba_plan* P : G->plans)
-    if (P->W == 0 || P->comm || chol_kind_of(P) != 2) return false;
-  return true;
-}
-
-// block prefix of one launch: f(P) workgroups per member
-template <typename F>
-GrpGrid grp_grid(const lorb_ba_group* G, F f) {
-  GrpGrid g{};
-  for (size_t k = 0; k < G->plans.size(); ++k) g.pre[k + 1] = g.pre[k] + f(G->plans[k]);
-  for (size_t k = G->plans.size() + 1; k <= (size_t)kGrpMax; ++k) g.pre[k] = g.pre[G->plans.size()];
-  return g;
-}
-
-template <int MODE>
-void launch_red_g(const lorb_ba_group* G, hipStream_t s, const BaGrp& bg, const LMOpt& o) {
-  const GrpGrid gg = grp_grid(G, [](const lorb_ba_plan* P) { return P->grid_bp; });
-  const int n = (int)G->plans.size(), nb = gg.pre[n];
-  if (nb == 0) return;
-  // the width rule of red_threads over the whole launch (the sums do not depend on it)
-  bool wide = nb <= 256;
-  for (const lorb_ba_plan* P : G->plans) wide = wide || (red_threads(P) == 1024 && P->grid_bp > 256);
-  const int rt = wide ? 1024 : nb <= 1024 ? 512 : 256;
-  if (rt == 1024) hipLaunchKernelGGL((k_ba_red_g<MODE, 1024>), dim3(nb), dim3(1024), 0, s, bg, gg, o);
-  else if (rt == 512) hipLaunchKernelGGL((k_ba_red_g<MODE, 512>), dim3(nb), dim3(512), 0, s, bg, gg, o);
-  else hipLaunchKernelGGL((k_ba_red_g<MODE, 256>), dim3(nb), dim3(256), 0, s, bg, gg, o);
-}
-
-// the group's whole solve on the ctx stream (enqueue_solve / enqueue_iteration of every member at once)
-int enqueue_group_solve(lorb_ba_group* G, const LMOpt& o) {
-  lorb_ctx* ctx = G->ctx;
-  hipStream_t s = ctx->stream;
-  const int n = (int)G->plans.size();
-  BaGrp bg{};
-  bg.n = n;
-  for (int k = 0; k < n; ++k) bg.d[k] = G->plans[k]->dev;
-  {
-    GrpInit a{};
-    for (int k = 0; k < n; ++k) {
-      const lorb_ba_plan* P = G->plans[k];
-      a.W[k] = P->W; a.ctot[k] = P->Ctot; a.n_pt[k] = P->pt_launch; a.nf[k] = P->NF;
-    }
-    const GrpGrid gg = grp_grid(G, [](const lorb_ba_plan* P) {
-      const int m = std::max(std::max(std::max(P->W, P->Ctot), P->NF), std::min(3 * P->pt_launch, 256 * 1024));
-      return lorb::ceil_div(std::max(m, 1), 256);
-    });
-    hipLaunchKernelGGL(k_ba_init_g, dim3(gg.pre[n]), dim3(256), 0, s, bg, gg, a, o);
-  }
-  const GrpGrid g_pb = grp_grid(G, [](const lorb_ba_plan* P) { return P->grid_pblk; });
-  const GrpGrid g_w = grp_grid(G, [](const lorb_ba_plan* P) { return P->W; });
-  size_t lds = 0;
-  for (const lorb_ba_plan* P : G->plans) lds = std::max(lds, sizeof(double) * (size_t)P->max_env_w);
-  auto linearise = [&]() {
-    if (g_pb.pre[n]) hipLaunchKernelGGL(k_ba_ls_g, dim3(g_pb.pre[n]), dim3(kLsThreads), 0, s, bg, g_pb, o);
-  };
-  if (o.max_iter <= 0) {  // one linearisation (cost, termination) as the head of a first iteration
-    linearise();
-    launch_red_g<0>(G, s, bg, o);
-    hipLaunchKernelGGL(k_ba_lm_begin_g, dim3(g_w.pre[n]), dim3(64), 0, s, bg, g_w, o);
-    LORB_CHECK_LAUNCH(ctx);
-    return LORB_OK;
-  }
-  for (int it = 0; it < o.max_iter; ++it) {
-    const bool first = it == 0;
-    linearise();
-    if (first) {
-      launch_red_g<0>(G, s, bg, o);
-      hipLaunchKernelGGL(k_ba_lm_begin_g, dim3(g_w.pre[n]), dim3(64), 0, s, bg, g_w, o);
-    }
-    for (const lorb_ba_plan* P : G->plans)  // (the two-sided Cholesky holds its band in LDS: none)
-      if (P->env_total && sizeof(double) * (size_t)P->max_env > (size_t)kLdsBudget)
-        LORB_HIP(ctx, hipMemsetAsync(P->dev.env, 0, sizeof(double) * P->env_total, s));
-    if (first) launch_red_g<1>(G, s, bg, o);
-    else launch_red_g<2>(G, s, bg, o);
-    if (first)
-      hipLaunchKernelGGL(k_ba_chol_2s_g<false>, dim3(g_w.pre[n]), dim3(kChol2sThreads), lds, s, bg, g_w, o);
-    else
-      hipLaunchKernelGGL(k_ba_chol_2s_g<true>, dim3(g_w.pre[n]), dim3(kChol2sThreads), lds, s, bg, g_w, o);
-    if (g_pb.pre[n]) hipLaunchKernelGGL(k_ba_bs2_g, dim3(g_pb.pre[n]), dim3(kGB), 0, s, bg, g_pb);
-    hipLaunchKernelGGL(k_ba_lm_end_g, dim3(g_w.pre[n]), dim3(64), 0, s, bg, g_w, o);
-  }
-  for (lorb_ba_plan* P : G->plans) P->chol_kind = 2;
-  LORB_CHECK_LAUNCH(ctx);
-  return LORB_OK;
-}
-
-int group_solve(lorb_ba_group* G, const lorb_lm_options* opt) {
-  lorb_ctx* ctx = G->ctx;
-  if (!group_fused(G)) {
-    for (lorb_ba_plan* P : G->plans)
-      if (P->W > 0) LORB_TRY(plan_solve(P, opt));
-    return LORB_OK;
-  }
-  const LMOpt o = to_dev_opt(opt);
-  static const bool no_graph = [] { const char* e = getenv("LORB_NO_GRAPH"); return e && e[0] == '1'; }();
-  if (no_graph) {
-    LORB_TRY(enqueue_group_solve(G, o));
-    G->n_fused++;
-    return LORB_OK;
-  }
-  bool same = G->has_graph && same_opt(G->graph_opt, o);
-  for (size_t k = 0; k < G->plans.size() && same; ++k)
-    same = G->gens[k] == G->plans[k]->gen && G->keys[k] == graph_key(G->plans[k]);
-  if (!same) {
-    if (G->gexec) { (void)hipGraphExecDestroy(G->gexec); G->gexec = nullptr; }
-    if (G->graph) { (void)hipGraphDestroy(G->graph); G->graph = nullptr; }
-    G->has_graph = false;
-    LORB_HIP(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
-    const int rc = enqueue_group_solve(G, o);
-    hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
-    if (rc != LORB_OK) { if (g) (void)hipGraphDestroy(g); return rc; }
-    if (e != hipSuccess) return lorb::set_error(ctx, LORB_E_DEVICE, "group graph capture failed: %s", hipGetErrorString(e));
-    G->graph = g;
-    LORB_HIP(ctx, hipGraphInstantiate(&G->gexec, G->graph, nullptr, nullptr, 0));
-    G->graph_opt = o;
-    G->gens.clear(); G->keys.clear();
-    for (const lorb_ba_plan* P : G->plans) { G->gens.push_back(P->gen); G->keys.push_back(graph_key(P)); }
-    G->has_graph = true;
-    G->n_captures++;
-  }
-  LORB_HIP(ctx, hipGraphLaunch(G->gexec, ctx->stream));
-  G->n_fused++;
   return LORB_OK;
 }
 
@@ -4545,22 +4300,9 @@ __global__ __launch_bounds__(256) void k_db_result64(BaDev d, int C, int P, cons
   }
 }
 
-int dev_build_issue(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P, int* lerr_out);
-int dev_build_finish(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P, int lerr);
-
 }  // namespace
 
 namespace lorb {
-int ba_plan_update_dev_issue(lorb_ba_plan* P, const lorb_ba_window_dev* w) {
-  if (!P || !w || !P->devb || P->comm) return LORB_E_INVALID;
-  int lerr = 0;
-  return dev_build_issue(P->ctx, w, P, &lerr);
-}
-int ba_plan_update_dev_finish(lorb_ba_plan* P, const lorb_ba_window_dev* w) {
-  if (!P || !w || !P->devb || P->comm) return LORB_E_INVALID;
-  return dev_build_finish(P->ctx, w, P, 0);
-}
-
 void ba_plan_sorted_hint(lorb_ba_plan* P, bool sorted) {
   if (P && P->devb) P->devb->sorted_hint = sorted;
 }
@@ -4608,7 +4350,6 @@ int grow(lorb_ba_plan* P, T** ptr, Cap* cap, size_t need) {
   LORB_TRY(dalloc(P, n, ptr));
   *cap = (Cap)n;
   P->has_graph = false;  // kernel arguments changed
-  P->gen++;
   return LORB_OK;
 }
 
@@ -4738,21 +4479,28 @@ int up_alloc(lorb_ba_plan* P, int bp_need) {
   d.bp = reinterpret_cast<const BlockPair*>(b.up_dev + b.off_bp);
   P->grid_bp = cap;
   P->has_graph = false;
-  P->gen++;
   return LORB_OK;
 }
 
-// phase 1 of a build on the ctx stream: per-point counts, camera x point bitsets, point offsets,
-// the counting sort by point when the slots are not sorted, covisibility counts; then the one
-// readback (hdr | cov | cam_cnt are contiguous in the scratch: one copy) and an event behind it.
-// The scratch is left clear by the previous build's k_db_gather; only a build that stopped before it
-// (an error) leaves it dirty.
-int db_phase1_issue(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P, bool sorted) {
+int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
   lorb_ba_devbuild& b = *P->devb;
+  const bool shape_ok = w->n_poses == b.C && w->n_fixed == b.F && w->max_obs <= b.K_cap && w->max_points <= b.P_cap;
+  // Sharded plans are collective: a rank-local failure before the exchange below (a shape that
+  // differs from the plan's, a failed allocation or copy) is not returned here -- it becomes an
+  // error bit of the all-reduce, so every rank reaches the exchange and every rank returns the error.
+  if (!shape_ok && !P->comm)
+    return lorb::set_error(ctx, LORB_E_INVALID, "window shape differs from the plan's (cameras %d/%d, fixed %d/%d)",
+                           w->n_poses, b.C, w->n_fixed, b.F);
   hipStream_t s = ctx->stream;
   BaDev& d = P->dev;
   const int C = b.C, F = b.F, Kc = w->max_obs;
   const size_t nrb = 8 + (size_t)C + (size_t)C * C;
+  bool sorted = b.sorted_hint, fuse = false;
+  int lerr = shape_ok ? 0 : 32;  // rank-local failures (bits 5, 6 of the exchanged error word)
+  // 1. per-point counts and camera x point bitsets; point offsets; counting sort by point
+  //    (stable); covisibility counts from the bitsets.  The scratch is left clear by the previous
+  //    build's k_db_gather; only a build that stopped before it (an error) leaves it dirty.
+  const int phase_rc = !shape_ok ? LORB_OK : [&]() -> int {
   const int nb_obs = lorb::ceil_div(std::max(Kc, 1), 256), nb_pt = lorb::ceil_div(std::max(b.P_cap, 1), 256);
   if (b.pinned_n < nrb) {
     if (b.pinned) (void)hipHostFree(b.pinned);
@@ -4760,90 +4508,42 @@ int db_phase1_issue(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P,
     LORB_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&b.pinned), sizeof(int) * nrb));
     b.pinned_n = nrb;
   }
-  if (!b.rb_ev) LORB_HIP(ctx, hipEventCreateWithFlags(&b.rb_ev, hipEventDisableTiming));
-  if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
-  b.dirty = true;
-  const bool fuse = sorted && C > 0 && sizeof(int) * ((size_t)C * C + C) <= (size_t)kDbFuseLds;
-  if (sorted) {
-    const size_t lds = sizeof(unsigned long long) * kDbWords * std::max(C, 1) +
-                       (fuse ? sizeof(int) * ((size_t)C * C + C) : 0);
-    if (fuse)
-      hipLaunchKernelGGL(k_db_sorted<true>, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), lds, s, *w, C, F, b.Wd,
-                         const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt);
-    else
-      hipLaunchKernelGGL(k_db_sorted<false>, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), lds, s, *w, C, F, b.Wd,
-                         const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt);
-  } else {
-    hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);
-    hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1,
-                       w->d_n_points, b.hdr);
-    if (Kc > 0) {
-      hipLaunchKernelGGL(k_db_scatter, dim3(nb_obs), dim3(256), 0, s, *w, C, F, d.pt_obs_off, b.pt_cnt, b.val_out);
-      hipLaunchKernelGGL(k_db_segsort, dim3(nb_pt), dim3(256), 0, s, *w, d.pt_obs_off, b.val_out, b.key_out);
-    }
-  }
-  if (C > 0 && !fuse)
-    hipLaunchKernelGGL(k_db_cov, dim3(lorb::ceil_div(C * (C + 1) / 2, 4)), dim3(256), 0, s, C, b.Wd, b.bits, b.cov,
-                       b.cam_cnt);
-  LORB_CHECK_LAUNCH(ctx);
-  LORB_HIP(ctx, hipMemcpyAsync(b.pinned, b.hdr, sizeof(int) * nrb, hipMemcpyDeviceToHost, s));
-  LORB_HIP(ctx, hipEventRecord(b.rb_ev, s));
-  b.rb_sorted = sorted;
-  b.rb_fuse = fuse;
-  b.rb_pending = true;
-  return LORB_OK;
-}
-
-// the readback of an issued phase 1 landed (polled); slots found out of order on the sorted path
-// (or unused) rerun the general phase from a cleared scratch
-int db_phase1_wait(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
-  lorb_ba_devbuild& b = *P->devb;
   for (;;) {
-    b.rb_pending = false;
-    LORB_HIP(ctx, lorb::spin_wait(b.rb_ev));
-    if (!(b.rb_sorted && (b.pinned[2] & 16))) return LORB_OK;
+    if (b.dirty) LORB_HIP(ctx, hipMemsetAsync(b.scr, 0, b.scr_bytes, s));
+    b.dirty = true;
+    fuse = sorted && C > 0 && sizeof(int) * ((size_t)C * C + C) <= (size_t)kDbFuseLds;
+    if (sorted) {
+      const size_t lds = sizeof(unsigned long long) * kDbWords * std::max(C, 1) +
+                         (fuse ? sizeof(int) * ((size_t)C * C + C) : 0);
+      if (fuse)
+        hipLaunchKernelGGL(k_db_sorted<true>, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), lds, s, *w, C, F, b.Wd,
+                           const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt);
+      else
+        hipLaunchKernelGGL(k_db_sorted<false>, dim3(lorb::ceil_div(Kc + 1, 256)), dim3(256), lds, s, *w, C, F, b.Wd,
+                           const_cast<int*>(d.pt_obs_off), b.hdr, b.bits, b.cov, b.cam_cnt);
+    } else {
+      hipLaunchKernelGGL(k_db_keys, dim3(nb_obs), dim3(256), 0, s, *w, C, F, b.Wd, b.pt_cnt, b.hdr, b.bits);
+      hipLaunchKernelGGL(k_db_scan1, dim3(1), dim3(1024), 0, s, b.pt_cnt, const_cast<int*>(d.pt_obs_off), b.P_cap + 1,
+                         w->d_n_points, b.hdr);
+      if (Kc > 0) {
+        hipLaunchKernelGGL(k_db_scatter, dim3(nb_obs), dim3(256), 0, s, *w, C, F, d.pt_obs_off, b.pt_cnt, b.val_out);
+        hipLaunchKernelGGL(k_db_segsort, dim3(nb_pt), dim3(256), 0, s, *w, d.pt_obs_off, b.val_out, b.key_out);
+      }
+    }
+    if (C > 0 && !fuse)
+      hipLaunchKernelGGL(k_db_cov, dim3(lorb::ceil_div(C * (C + 1) / 2, 4)), dim3(256), 0, s, C, b.Wd, b.bits, b.cov,
+                         b.cam_cnt);
+    LORB_CHECK_LAUNCH(ctx);
+    // 2. the one readback: counts and the covisibility structure (hdr | cov | cam_cnt are
+    //    contiguous in the scratch: one copy)
+    LORB_HIP(ctx, hipMemcpyAsync(b.pinned, b.hdr, sizeof(int) * nrb, hipMemcpyDeviceToHost, s));
+    LORB_HIP(ctx, lorb::spin_sync(ctx));
+    if (!(sorted && (b.pinned[2] & 16))) break;
+    sorted = false;  // slots out of order (or unused): the general phase, from a cleared scratch
     b.sorted_hint = false;
-    LORB_TRY(db_phase1_issue(ctx, w, P, false));
   }
-}
-
-// the first half of a build: the shape check and phase 1 with its readback queued (no wait).  A
-// rank-local failure of a sharded plan is kept for dev_build_finish (see there).
-int dev_build_issue(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P, int* lerr_out) {
-  lorb_ba_devbuild& b = *P->devb;
-  const bool shape_ok = w->n_poses == b.C && w->n_fixed == b.F && w->max_obs <= b.K_cap && w->max_points <= b.P_cap;
-  *lerr_out = shape_ok ? 0 : 32;
-  if (!shape_ok && !P->comm)
-    return lorb::set_error(ctx, LORB_E_INVALID, "window shape differs from the plan's (cameras %d/%d, fixed %d/%d)",
-                           w->n_poses, b.C, w->n_fixed, b.F);
-  if (!shape_ok) return LORB_OK;
-  const int rc = db_phase1_issue(ctx, w, P, b.sorted_hint);
-  if (rc != LORB_OK && P->comm) { *lerr_out |= 64; return LORB_OK; }
-  return rc;
-}
-
-int dev_build_finish(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P, int lerr);
-
-// a whole build: dev_build_issue + dev_build_finish
-int dev_build(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P) {
-  int lerr = 0;
-  LORB_TRY(dev_build_issue(ctx, w, P, &lerr));
-  return dev_build_finish(ctx, w, P, lerr);
-}
-
-// the second half: wait for the readback, then the host phase and the structure kernel.
-// Sharded plans are collective: a rank-local failure before the exchange below (a shape that
-// differs from the plan's, a failed allocation or copy) is not returned here -- it becomes an
-// error bit of the all-reduce, so every rank reaches the exchange and every rank returns the error.
-int dev_build_finish(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P, int lerr) {
-  lorb_ba_devbuild& b = *P->devb;
-  const bool shape_ok = !(lerr & 32);
-  hipStream_t s = ctx->stream;
-  BaDev& d = P->dev;
-  const int C = b.C, F = b.F;
-  const size_t nrb = 8 + (size_t)C + (size_t)C * C;
-  const int phase_rc = (lerr || !b.rb_pending) ? LORB_OK : db_phase1_wait(ctx, w, P);
-  const bool sorted = b.rb_sorted, fuse = b.rb_fuse;
+  return LORB_OK;
+  }();
   static const bool hp_log = [] { const char* e = getenv("LORB_HOST_PHASE"); return e && e[0] == '1'; }();
   const auto hp_t0 = std::chrono::steady_clock::now();
   auto hp_last = hp_t0;
@@ -5194,43 +4894,6 @@ int lorb_ba_plan_destroy(lorb_ba_plan* plan) {
   if (!plan) return LORB_OK;
   if (plan->ctx) (void)hipStreamSynchronize(plan->ctx->stream);
   delete plan;
-  return LORB_OK;
-}
-
-int lorb_ba_group_create(lorb_ctx* ctx, int32_t n_plans, lorb_ba_plan* const* plans, lorb_ba_group** out) {
-  if (!ctx || !out || n_plans < 1 || !plans) return LORB_E_INVALID;
-  *out = nullptr;
-  for (int k = 0; k < n_plans; ++k) {
-    if (!plans[k]) return lorb::set_error(ctx, LORB_E_INVALID, "lorb_ba_group_create: plan %d is null", k);
-    if (plans[k]->ctx != ctx)
-      return lorb::set_error(ctx, LORB_E_INVALID, "lorb_ba_group_create: plan %d belongs to another context", k);
-    for (int j = 0; j < k; ++j)
-      if (plans[j] == plans[k]) return lorb::set_error(ctx, LORB_E_INVALID, "lorb_ba_group_create: plan %d appears twice", k);
-  }
-  lorb_ba_group* G = new (std::nothrow) lorb_ba_group();
-  if (!G) return LORB_E_NOMEM;
-  G->ctx = ctx;
-  G->plans.assign(plans, plans + n_plans);
-  *out = G;
-  return LORB_OK;
-}
-
-int lorb_ba_group_solve(lorb_ba_group* group, const lorb_lm_options* opt) {
-  if (!group || !opt) return LORB_E_INVALID;
-  return group_solve(group, opt);
-}
-
-int lorb_ba_group_info(lorb_ba_group* group, int32_t* info, int32_t n) {
-  if (!group || !info || n < 0) return LORB_E_INVALID;
-  const int32_t v[3] = {(int32_t)group->plans.size(), group->n_fused, group->n_captures};
-  for (int i = 0; i < n && i < 3; ++i) info[i] = v[i];
-  return LORB_OK;
-}
-
-int lorb_ba_group_destroy(lorb_ba_group* group) {
-  if (!group) return LORB_OK;
-  (void)hipStreamSynchronize(group->ctx->stream);
-  delete group;
   return LORB_OK;
 }
 

@@ -323,7 +323,6 @@ struct lorb_map {
   bool prof = false;
   double prof_ms[8] = {};
   int prof_n = 0;
-  std::chrono::steady_clock::time_point prof_clk{};
   int* mt = nullptr;
   // the step's crossCheck keys: per-query keys and per-train keys (all-ones between steps), owned by
   // the map so that its side-stream match shares no scratch with matcher calls on the ctx stream
@@ -515,51 +514,10 @@ int lorb_map_create(lorb_ctx* ctx, const lorb_map_init* in, lorb_map** out) {
   return LORB_OK;
 }
 
-}  // extern "C"
-
-namespace {
-
-// LORB_MAP_PROFILE: host wall time since the last mark into phase i, after a stream sync
-int map_mark(lorb_map* M, int i) {
-  if (!M->prof) return LORB_OK;
-  LORB_HIP(M->ctx, hipStreamSynchronize(M->ctx->stream));
-  const auto now = std::chrono::steady_clock::now();
-  M->prof_ms[i] += std::chrono::duration<double, std::milli>(now - M->prof_clk).count();
-  M->prof_clk = now;
-  return LORB_OK;
-}
-
-// a failed plan build (step 5): the append and the slide have run, so the live counts are the
-// device's now, and the next slide takes h_K as the end of the point-sorted slots -- re-read them, or
-// mark the map unusable
-int map_build_fail(lorb_map* M, int rc) {
-  M->built = false;  // the next step's match waits for this step's kernels on the main stream
-  hipStream_t s = M->ctx->stream;
-  if (hipMemcpyAsync(M->pinned, M->m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
-      hipStreamSynchronize(s) == hipSuccess) {
-    M->h_P = M->pinned[0]; M->h_K = M->pinned[1];
-  } else {
-    M->broken = true;
-  }
-  return rc;
-}
-
-int map_build_done(lorb_map* M) {
-  lorb_ctx* ctx = M->ctx;
-  M->plan_ok = true;
-  // the plan build has read the map: the next step's match and append may start (see `side`)
-  if (!M->ev_built) LORB_HIP(ctx, hipEventCreateWithFlags(&M->ev_built, hipEventDisableTiming));
-  LORB_HIP(ctx, hipEventRecord(M->ev_built, ctx->stream));
-  M->built = true;
-  LORB_TRY(map_mark(M, 4));
-  lorb::ba_plan_window_counts(M->plan, &M->h_P, &M->h_K);
-  return LORB_OK;
-}
-
-// steps 1-5 of lorb_map_step_dev: everything before the BA solve
-int map_prepare(lorb_map* M, const lorb_frame_params* frame, const float pose[6], const float Tcw[16], int32_t n,
-                const uint8_t* d_desc, const float* d_x, const float* d_y, const float* d_depth, bool split = false) {
-  if (!M || !frame || !pose || !Tcw || n < 0) return LORB_E_INVALID;
+int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float pose[6], const float Tcw[16], int32_t n,
+                      const uint8_t* d_desc, const float* d_x, const float* d_y, const float* d_depth,
+                      const lorb_lm_options* opt) {
+  if (!M || !frame || !pose || !Tcw || !opt || n < 0) return LORB_E_INVALID;
   lorb_ctx* ctx = M->ctx;
   if (n > M->n_cap) return lorb::set_error(ctx, LORB_E_INVALID, "%d keypoints > the map's max_keypoints %d", n, M->n_cap);
   if (n > 0 && (!d_desc || !d_x || !d_y || !d_depth)) return LORB_E_INVALID;
@@ -567,8 +525,15 @@ int map_prepare(lorb_map* M, const lorb_frame_params* frame, const float pose[6]
   hipStream_t s = ctx->stream;
   MapDev& m = M->m;
   const int kf = M->t0 + m.W;  // the new keyframe's id
-  M->prof_clk = std::chrono::steady_clock::now();
-  auto mark = [&](int i) { return map_mark(M, i); };
+  auto clk = std::chrono::steady_clock::now();
+  auto mark = [&](int i) -> int {
+    if (!M->prof) return LORB_OK;
+    LORB_HIP(ctx, hipStreamSynchronize(s));
+    const auto now = std::chrono::steady_clock::now();
+    M->prof_ms[i] += std::chrono::duration<double, std::milli>(now - clk).count();
+    clk = now;
+    return LORB_OK;
+  };
   LORB_TRY(mark(7));
   const bool ovl = M->overlap && M->built && !M->prof && !ctx->ktime;
   if (ovl && !M->side) {
@@ -633,59 +598,36 @@ int map_prepare(lorb_map* M, const lorb_frame_params* frame, const float pose[6]
   LORB_TRY(map_slide(M, M->t0 + 1, std::min(M->h_P + n, m.P_cap), std::min(M->h_K + n, m.K_cap), M->h_K, M->h_P,
                       M->plan_ok ? lorb::ba_plan_point_offsets(M->plan) : nullptr));
   LORB_TRY(mark(3));
-  // 5. BA plan of the slid window; its one readback carries the window's live counts too (split:
-  //    only the build's first phase and readback are queued here, map_build_finish completes it)
+  // 5. BA plan of the slid window; its one readback carries the window's live counts too
   const lorb_ba_window_dev w = window_of(M);
   M->plan_ok = false;
-  if (split) {
-    if (const int rc = lorb::ba_plan_update_dev_issue(M->plan, &w); rc != LORB_OK) return map_build_fail(M, rc);
-    return LORB_OK;
+  if (const int rc = lorb_ba_plan_update_dev(M->plan, &w); rc != LORB_OK) {
+    M->built = false;  // the next step's match waits for this step's kernels on the main stream
+    // the append and the slide have run: the live counts are the device's now, and the next slide
+    // takes h_K as the end of the point-sorted slots -- re-read them, or mark the map unusable
+    if (hipMemcpyAsync(M->pinned, m.cnt, sizeof(int) * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+        hipStreamSynchronize(s) == hipSuccess) {
+      M->h_P = M->pinned[0]; M->h_K = M->pinned[1];
+    } else {
+      M->broken = true;
+    }
+    return rc;
   }
-  if (const int rc = lorb_ba_plan_update_dev(M->plan, &w); rc != LORB_OK) return map_build_fail(M, rc);
-  return map_build_done(M);
-}
-
-// the second half of a split step 5
-int map_build_finish(lorb_map* M) {
-  const lorb_ba_window_dev w = window_of(M);
-  if (const int rc = lorb::ba_plan_update_dev_finish(M->plan, &w); rc != LORB_OK) return map_build_fail(M, rc);
-  return map_build_done(M);
-}
-
-// 6b. after the solve: float write-back of the window's poses straight into the ring (Frame::SetPose)
-// and of the points into the map
-int map_finish(lorb_map* M) {
-  LORB_TRY(lorb::ba_plan_result_ring_dev(M->plan, M->m.ring, M->m.R, M->t0, M->m.pos));
-  LORB_TRY(map_mark(M, 6));
+  M->plan_ok = true;
+  // the plan build has read the map: the next step's match and append may start (see `side`)
+  if (!M->ev_built) LORB_HIP(ctx, hipEventCreateWithFlags(&M->ev_built, hipEventDisableTiming));
+  LORB_HIP(ctx, hipEventRecord(M->ev_built, s));
+  M->built = true;
+  LORB_TRY(mark(4));
+  lorb::ba_plan_window_counts(M->plan, &M->h_P, &M->h_K);
+  // 6. LocalPoseOptimization + float write-back of poses (ring) and points (map)
+  LORB_TRY(lorb_ba_plan_solve(M->plan, opt));
+  LORB_TRY(mark(5));
+  // float write-back: poses straight into the ring (Frame::SetPose), points into the map
+  LORB_TRY(lorb::ba_plan_result_ring_dev(M->plan, m.ring, m.R, M->t0, m.pos));
+  LORB_TRY(mark(6));
   if (M->prof) M->prof_n++;
   return LORB_OK;
-}
-
-}  // namespace
-
-// a group of maps on one ctx stepped together (lorb_map_group_*): their BA plans solved by plan
-// groups of up to kMapGrp maps
-constexpr int kMapGrp = 4;
-struct lorb_map_group {
-  std::vector<lorb_map*> maps;
-  std::vector<lorb_ba_group*> bag;
-  int n_steps_fused = 0;
-  ~lorb_map_group() {
-    for (lorb_ba_group* g : bag) (void)lorb_ba_group_destroy(g);
-  }
-};
-
-extern "C" {
-
-int lorb_map_step_dev(lorb_map* M, const lorb_frame_params* frame, const float pose[6], const float Tcw[16], int32_t n,
-                      const uint8_t* d_desc, const float* d_x, const float* d_y, const float* d_depth,
-                      const lorb_lm_options* opt) {
-  if (!M || !opt) return LORB_E_INVALID;
-  LORB_TRY(map_prepare(M, frame, pose, Tcw, n, d_desc, d_x, d_y, d_depth));
-  // 6. LocalPoseOptimization, then the float write-back
-  LORB_TRY(lorb_ba_plan_solve(M->plan, opt));
-  LORB_TRY(map_mark(M, 5));
-  return map_finish(M);
 }
 
 int lorb_map_set_overlap(lorb_map* M, int32_t enable) {
@@ -751,95 +693,6 @@ int lorb_map_destroy(lorb_map* M) {
   if (!M) return LORB_E_INVALID;
   (void)hipStreamSynchronize(M->ctx->stream);
   delete M;
-  return LORB_OK;
-}
-
-int lorb_map_group_create(int32_t n_maps, lorb_map* const* maps, lorb_map_group** out) {
-  if (n_maps < 1 || !maps || !out || !maps[0]) return LORB_E_INVALID;
-  *out = nullptr;
-  lorb_ctx* ctx = maps[0]->ctx;
-  for (int i = 0; i < n_maps; ++i) {
-    if (!maps[i]) return lorb::set_error(ctx, LORB_E_INVALID, "lorb_map_group_create: map %d is null", i);
-    if (maps[i]->ctx != ctx) return lorb::set_error(ctx, LORB_E_INVALID, "lorb_map_group_create: map %d is on another context", i);
-    for (int j = 0; j < i; ++j)
-      if (maps[j] == maps[i]) return lorb::set_error(ctx, LORB_E_INVALID, "lorb_map_group_create: map %d appears twice", i);
-  }
-  lorb_map_group* G = new (std::nothrow) lorb_map_group();
-  if (!G) return LORB_E_NOMEM;
-  G->maps.assign(maps, maps + n_maps);
-  for (int i0 = 0; i0 < n_maps; i0 += kMapGrp) {
-    std::vector<lorb_ba_plan*> plans;
-    for (int i = i0; i < std::min(n_maps, i0 + kMapGrp); ++i) plans.push_back(maps[i]->plan);
-    lorb_ba_group* g = nullptr;
-    if (const int rc = lorb_ba_group_create(ctx, (int32_t)plans.size(), plans.data(), &g); rc != LORB_OK) {
-      delete G;
-      return rc;
-    }
-    G->bag.push_back(g);
-  }
-  *out = G;
-  return LORB_OK;
-}
-
-int lorb_map_group_step_dev(lorb_map_group* G, const lorb_map_keyframe* kfs, const lorb_lm_options* opt) {
-  if (!G || !kfs || !opt) return LORB_E_INVALID;
-  const int n = (int)G->maps.size();
-  int rc = LORB_OK, ready = n;
-  // steps 1-4 and the first half of every map's plan build (its readback queued), then the second
-  // halves: a map's host phase runs while the next maps' kernels execute, and the builds wait for
-  // their readbacks one after another instead of once per map between the maps' kernels
-  for (int i = 0; i < n; ++i) {
-    const lorb_map_keyframe& k = kfs[i];
-    rc = map_prepare(G->maps[i], k.frame, k.pose, k.Tcw, k.n, k.d_desc, k.d_x, k.d_y, k.d_depth, true);
-    if (rc != LORB_OK) { ready = i; break; }
-  }
-  std::vector<char> built(ready, 0);
-  bool all = ready == n;
-  for (int i = 0; i < ready; ++i) {
-    const int r = map_build_finish(G->maps[i]);
-    built[i] = r == LORB_OK;
-    if (r != LORB_OK) {
-      all = false;
-      if (rc == LORB_OK) rc = r;
-    }
-  }
-  // 6. the BA solves: one plan group per kMapGrp maps; after a failure, the maps whose builds
-  //    completed finish their step on their own plans
-  if (all) {
-    bool fused = true;
-    for (lorb_ba_group* g : G->bag) {
-      int32_t before[2], after[2];
-      LORB_TRY(lorb_ba_group_info(g, before, 2));
-      LORB_TRY(lorb_ba_group_solve(g, opt));
-      LORB_TRY(lorb_ba_group_info(g, after, 2));
-      fused = fused && after[1] > before[1];
-    }
-    G->n_steps_fused += fused;
-  } else {
-    for (int i = 0; i < ready; ++i)
-      if (built[i]) LORB_TRY(lorb_ba_plan_solve(G->maps[i]->plan, opt));
-  }
-  for (int i = 0; i < ready; ++i)
-    if (built[i]) LORB_TRY(map_finish(G->maps[i]));
-  return rc;
-}
-
-int lorb_map_group_info(lorb_map_group* G, int32_t* info, int32_t n) {
-  if (!G || !info || n < 0) return LORB_E_INVALID;
-  int32_t caps = 0;
-  for (lorb_ba_group* g : G->bag) {
-    int32_t v[3];
-    LORB_TRY(lorb_ba_group_info(g, v, 3));
-    caps += v[2];
-  }
-  const int32_t v[4] = {(int32_t)G->maps.size(), (int32_t)G->bag.size(), G->n_steps_fused, caps};
-  for (int i = 0; i < n && i < 4; ++i) info[i] = v[i];
-  return LORB_OK;
-}
-
-int lorb_map_group_destroy(lorb_map_group* G) {
-  if (!G) return LORB_E_INVALID;
-  delete G;
   return LORB_OK;
 }
 

@@ -238,6 +238,41 @@ def test_local_mapping_group_chunks_and_fallback(ctx):
     _group_vs_solo(ctx, small + [tiny], 2, expect_fused=False)
 
 
+def test_local_mapping_group_step_error(ctx):
+    """a group step where the second of three maps overflows its point capacity: that map is left as
+    it was (as lorb_map_step_dev leaves it), the first completes its step (bit-identical to a solo
+    step), the third is not stepped"""
+    from lorb_slam_amd.runtime import MapGroup
+    seq = synth.mapping_sequence(seed=5, n_kf=24, n_fixed=3, n_new=90, obs_lens=(4, 5), steps=2, n_kps=800)
+    n_pts = len(seq["init"]["point_init"])
+    fp = A.make_frame_params(synth.frame_params())
+    dev = _dev_keyframes(ctx, seq, 2)
+    ctx.sync()
+    maps = [LocalMap(ctx, seq["init"]), LocalMap(ctx, seq["init"], max_points=n_pts + 5, max_keypoints=1024),
+            LocalMap(ctx, seq["init"])]
+    solo = LocalMap(ctx, seq["init"])
+    G = MapGroup(maps)
+    try:
+        before = [m.read() for m in maps]
+        with pytest.raises(LorbError, match="capacity"):
+            G.step_dev(fp, [dev[0]] * 3, OPT10)
+        solo.step_dev(fp, *dev[0], OPT10)
+        _bitwise_same(maps[0].read(), solo.read(), "completed map")
+        for i in (1, 2):
+            after = maps[i].read()
+            same_structure(after, before[i])
+            for k in ("point", "pose", "fixed_pose"):
+                assert np.array_equal(after[k], before[i][k]), (i, k)
+        assert G.info()["fused_steps"] == 0
+    finally:
+        G.close()
+        for m in maps + [solo]:
+            m.close()
+        for k in dev:
+            for a in k[3:]:
+                a.free()
+
+
 def test_local_mapping_group_errors(ctx):
     """a group's maps share one context and appear once"""
     from lorb_slam_amd.runtime import Context, MapGroup
