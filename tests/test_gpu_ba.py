@@ -427,6 +427,39 @@ def test_plan_group_bit_identical(ctx):
             p.close()
 
 
+def test_plan_group_members_stop_at_different_iterations(ctx):
+    """Ceres-default options (tolerances on, 50 iterations): the group's members terminate at different
+    iterations (a converged window early-exits every later launch while the others go on); each one
+    still equals its own solve bit for bit, termination and trace included, and the oracle's summary."""
+    from lorb_slam_amd.runtime import BAGroup, BAPlan
+    wins = [synth.ba_window(seed=7, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400),
+            synth.ba_window(seed=41, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400),
+            synth.ba_window(seed=8, n_kf=24, n_pts=3000, n_fixed=2, fixed_obs_per_kf=300)]
+    opt = A.LMOptions.default()
+    gp = [BAPlan(ctx, [w]) for w in wins]
+    sp = [BAPlan(ctx, [w]) for w in wins]
+    G = BAGroup(ctx, gp)
+    try:
+        G.solve(opt)
+        for p in sp:
+            p.solve(opt)
+        its = []
+        for i, (a, b) in enumerate(zip(gp, sp)):
+            ra, rb = a.read(), b.read()
+            assert np.array_equal(ra[0][0], rb[0][0]) and np.array_equal(ra[1][0], rb[1][0]), i
+            assert ra[2][0] == rb[2][0], (i, ra[2][0], rb[2][0])
+            assert a.trace(0) == b.trace(0), i
+            its.append(ra[2][0]["iterations"])
+            _, _, so, ot = O.ba_local_traced(wins[i], opt)
+            lm_match(ra[2][0], so, gt=a.trace(0), ot=ot, label=f"group member {i}")
+        assert G.info()["fused_solves"] == 1, G.info()
+        assert len(set(its)) > 1, its  # the members did stop at different iterations
+    finally:
+        G.close()
+        for p in gp + sp:
+            p.close()
+
+
 def _dev_window(ctx, w, extra_pts=37, extra_obs=500, shuffle_seed=None, holes=0):
     """Upload window w into device arrays with spare capacity, optionally with the observations in
     a shuffled slot order and `holes` unused slots (frame < -n_fixed) spread among them."""
