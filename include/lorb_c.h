@@ -648,7 +648,8 @@ int lorb_map_destroy(lorb_map* map);
  * state after the step is bit-identical to lorb_map_step_dev of that map alone.  Errors: a map whose
  * steps 1-3 or plan build fail is left as lorb_map_step_dev leaves it after that error; when a map's
  * steps 1-3 fail, the maps after it in the group are not stepped; every other map completes its step
- * (solve and write-back).  The first error is returned. */
+ * (solve and write-back).  The first error is returned.  The group does not own its maps: they must
+ * outlive it. */
 typedef struct lorb_map_group lorb_map_group;
 typedef struct lorb_map_keyframe {
   const lorb_frame_params* frame;

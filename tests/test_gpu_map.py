@@ -183,15 +183,18 @@ def _bitwise_same(a, b, label):
         assert a["summary"][k] == v, (label, k, a["summary"][k], v)
 
 
-def _group_vs_solo(ctx, seqs, n_steps, expect_fused):
+def _group_vs_solo(ctx, seqs, n_steps, expect_fused, overlap=False):
     """maps stepped together (lorb_map_group, one ctx) vs the same maps stepped one by one
-    (lorb_map_step_dev, a second set of maps): bit for bit after every step, LM traces included"""
+    (lorb_map_step_dev, a second set of maps): bit for bit after every step, LM traces included.
+    overlap: the group's maps with lorb_map_set_overlap on (the keyframes are resident beforehand)"""
     from lorb_slam_amd.runtime import MapGroup
     fp = A.make_frame_params(synth.frame_params())
     devs = [_dev_keyframes(ctx, s, n_steps) for s in seqs]
     ctx.sync()
     Mg = [LocalMap(ctx, s["init"]) for s in seqs]
     Ms = [LocalMap(ctx, s["init"]) for s in seqs]
+    for m in Mg:
+        m.set_overlap(overlap)
     G = MapGroup(Mg)
     try:
         for t in range(n_steps):
@@ -215,7 +218,8 @@ def _group_vs_solo(ctx, seqs, n_steps, expect_fused):
                     a.free()
 
 
-def test_local_mapping_group_bit_identical(ctx):
+@pytest.mark.parametrize("overlap", [False, True])
+def test_local_mapping_group_bit_identical(ctx, overlap):
     """several windows stepped through ONE set of BA launches per step (the
     maps' device-built plans solved as a lorb_ba_group: every point-group, block and Cholesky kernel
     launched once for all of them).  Two C4 windows and a 24-keyframe one, 3 steps: each map equals
@@ -224,7 +228,7 @@ def test_local_mapping_group_bit_identical(ctx):
     (test_local_mapping_chain_c4)."""
     seqs = [synth.mapping_sequence(seed=4, steps=3), synth.mapping_sequence(seed=21, steps=3),
             synth.mapping_sequence(seed=9, n_kf=24, n_fixed=3, n_new=90, obs_lens=(4, 5), steps=3, n_kps=800)]
-    info = _group_vs_solo(ctx, seqs, 3, expect_fused=True)
+    info = _group_vs_solo(ctx, seqs, 3, expect_fused=True, overlap=overlap)
     assert info["captures"] <= 3, info
 
 
