@@ -540,7 +540,9 @@ int lorb_ctx_ba_solver(lorb_ctx* ctx, lorb_ba_solver** out);
  * blocks, [3] point groups, [4] observations, [5] points, [6] cameras, [7] 1 if some window's
  * cameras were reordered (reverse Cuthill-McKee on the covisibility graph; outputs keep the
  * caller's order), [8] 1: the point-major Schur path (the only one since round 6; point groups span
- * <= 128 cameras), [9] its partial-reduction width (threads per block: 256, 512 or 1024) */
+ * <= 128 cameras), [9] its partial-reduction width (threads per block: 256, 512 or 1024), [10] partial
+ * runs of the last build (0: one partial per point group; else the runs of several groups that
+ * k_ba_ls_sup folds into one partial each -- windows of more than 512 point groups) */
 int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n);
 /* the last solve's per-iteration records of window w (at most min(cap, LORB_LM_TRACE_CAP)); *n_out =
  * records written.  Synchronises. */

@@ -59,6 +59,9 @@ struct BaWin {
   // point-major path: the window's group partials start at part_base, part_stride doubles per group
   // (camera terms at part_cam within it); bwc = the camera-level half band
   int part_stride, part_cam, bwc, pad_;
+  // partial runs ("super-groups"): F consecutive point groups of the window processed by one
+  // k_ba_ls workgroup into ONE partial (F = 1: one per group); super-groups [sg_base, sg_base + n_sg)
+  int sg_base, n_sg;
   long long part_base;
   double fx, fy, cx, cy;
 };
@@ -266,11 +269,12 @@ struct BaDev {
                              // ((row_base >> 4) + w) * 1024 doubles, top side's blocks then the
                              // bottom side's, [block][16][64] (BandSide::bsk_block)
   WinState* st;
-  // group partials (k_ba_ls -> k_ba_red), per group (first camera - pose_base, span)
+  // partials (k_ba_ls -> k_ba_red), per super-group (its first camera - pose_base, camera span)
   double* gpart;
   int2* gspan;
+  const int4* sgrp;          // per super-group: window, first point group, point groups
   lorb_lm_iteration* trace;  // per window LORB_LM_TRACE_CAP records (lm_decide)
-  // [0] point groups, [1] block pairs in use.  Launch grids may be larger (device-built plans
+  // [0] point groups, [1] block pairs, [2] super-groups in use.  Launch grids may be larger (device-built plans
   // launch at capacity so that the captured LM graph survives a rebuild); the extra workgroups exit.
   const int* live;
 };
@@ -2262,7 +2266,14 @@ __device__ __forceinline__ void pm_lin(const BaDev& d, const BaWin& W, int cur, 
 //                    Jc_h^T K Jc_l (K = I - Q_h Jps_l^T on the diagonal, -Q_h Jps_l^T off it), plus
 //                    the camera terms on the diagonal; written to the group's partial.
 // Cost, point gradient max and |x|^2 partials per group (the head reads them when relinearising).
-__device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const unsigned bid) {
+// SUP (ls_run_sup): the group is one of a super-group's; phase D adds its blocks into the
+// super-group's partial (its camera window at the super-group's offset) instead of writing its own.
+struct LsSup {
+  double* gsp;  // the super-group's partial
+  int cmin;     // its first camera (plan numbering)
+};
+template <bool SUP>
+__device__ __forceinline__ void ls_group(const BaDev& d, const LMOpt& o, const unsigned bid, const LsSup& su) {
   __shared__ double s_jc[kGB][12];   // B / C: per point Ei (0..5), bs (6..8), sp (9..11); D: Jc per slot
   __shared__ double s_qj[kGB][12];   // A / B: Jp^T Jp (6) | Jp^T r (3) per observation; D: Q | Jps per slot
   __shared__ double s_rg[kGB][4];    // D: r | g per slot
@@ -2270,7 +2281,6 @@ __device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const uns
   __shared__ int s_po[kGB];
   __shared__ int s_mm[2][kLsWaves];
   __shared__ double red3[3][kLsWaves];
-  if ((int)bid >= d.live[0]) return;
 #ifdef LORB_LS_STAMPS
   // dbg[8 g + k]: s_memtime at the kernel's entry (k 0) and after phase A (1), B (2), C (3), D (4),
   // the partial sums (5) of group g (thread 0)
@@ -2412,8 +2422,9 @@ __device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const uns
   LS_STAMP(3);
   // D
   const int bwc = W.bwc, nsl = pm_nslots(span, bwc);
-  double* gp = d.gpart + W.part_base + (size_t)(bid - W.pblk_base) * W.part_stride;
-  if (t == 0) d.gspan[bid] = make_int2(span > 0 ? cmin - W.pose_base : 0, span);
+  double* gp = SUP ? su.gsp : d.gpart + W.part_base + (size_t)(bid - W.sg_base) * W.part_stride;
+  const int aoff = SUP ? cmin - su.cmin : 0;  // the group's first camera in the super-group's window
+  if (!SUP && t == 0) d.gspan[bid] = make_int2(span > 0 ? cmin - W.pose_base : 0, span);
   // Lane = slot (its whole 6 x 6 block: the point's loads serve 36 outputs), wave = point subset:
   // every lane of a wave walks the same points (k = wave, wave + 4, ...: a uniform loop, so the next
   // point's mask / offset are requested before this point's FMAs), a lane whose two cameras the
@@ -2523,13 +2534,24 @@ __device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const uns
       }
     }
     if (own && (!split || wv == kLsWaves - 1)) {
-      double* out = gp + 36 * q;
+      if (SUP) {  // added in group order into the super-group's partial (zeroed by ls_run_sup)
+        double* out = gp + 36 * pm_slot(a + aoff, dd, bwc);
 #pragma unroll
-      for (int k = 0; k < 36; ++k) out[k] = acc[k];
-      if (dg) {
-        double* gc = gp + W.part_cam + 18 * a;
+        for (int k = 0; k < 36; ++k) out[k] = out[k] + acc[k];
+        if (dg) {
+          double* gc = gp + W.part_cam + 18 * (a + aoff);
 #pragma unroll
-        for (int k = 0; k < 18; ++k) gc[k] = ex[k];
+          for (int k = 0; k < 18; ++k) gc[k] = gc[k] + ex[k];
+        }
+      } else {
+        double* out = gp + 36 * q;
+#pragma unroll
+        for (int k = 0; k < 36; ++k) out[k] = acc[k];
+        if (dg) {
+          double* gc = gp + W.part_cam + 18 * a;
+#pragma unroll
+          for (int k = 0; k < 18; ++k) gc[k] = ex[k];
+        }
       }
     }
   }
@@ -2542,7 +2564,49 @@ __device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const uns
 #endif
 #undef LS_STAMP
 }
+__device__ __forceinline__ void ls_run(const BaDev& d, const LMOpt& o, const unsigned bid) {
+  if ((int)bid >= d.live[0]) return;
+  ls_group<false>(d, o, bid, LsSup{nullptr, 0});
+}
 __global__ __launch_bounds__(kLsThreads) void k_ba_ls(BaDev d, LMOpt o) { ls_run(d, o, blockIdx.x); }
+
+// Super-group sid: its point groups one after another in one workgroup, their camera-block sums
+// added in group order into ONE partial over the union of their camera windows (a window with more
+// point groups than two workgroups per CU take in one round: VERDICT r05 item 2, the partials' HBM
+// round trip).  The union window comes from the super-group's observations (one pass); its region
+// of the partial is zeroed first.
+__device__ __forceinline__ void ls_run_sup(const BaDev& d, const LMOpt& o, const unsigned sid) {
+  __shared__ int s_r[2][kLsWaves];
+  if ((int)sid >= d.live[2]) return;
+  const int4 sg = d.sgrp[sid];
+  const WinState& S = d.st[sg.x];
+  if (S.done) return;
+  const BaWin& W = d.win[sg.x];
+  const PBlk gf = d.pblk[sg.y], gl = d.pblk[sg.y + sg.z - 1];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  int mn = 0x7fffffff, mx = -1;
+  for (int e = gf.o0 + t; e < gl.o0 + gl.no; e += kLsThreads) {
+    const int c = d.obs_cam[e];
+    if (c >= 0) { mn = min(mn, c); mx = max(mx, c); }
+  }
+#pragma unroll
+  for (int k = 32; k > 0; k >>= 1) { mn = min(mn, __shfl_xor(mn, k, 64)); mx = max(mx, __shfl_xor(mx, k, 64)); }
+  if (lane == 0) { s_r[0][wv] = mn; s_r[1][wv] = mx; }
+  __syncthreads();
+  int cmin = s_r[0][0], cmax = s_r[1][0];
+#pragma unroll
+  for (int k = 1; k < kLsWaves; ++k) { cmin = min(cmin, s_r[0][k]); cmax = max(cmax, s_r[1][k]); }
+  const int span = cmax >= 0 ? cmax - cmin + 1 : 0;
+  double* gsp = d.gpart + W.part_base + (size_t)(sid - W.sg_base) * W.part_stride;
+  const int nb = 36 * pm_nslots(span, W.bwc), nc = 18 * span;
+  for (int i = t; i < nb + nc; i += kLsThreads) gsp[i < nb ? i : W.part_cam + (i - nb)] = 0.0;
+  if (t == 0) d.gspan[sid] = make_int2(span > 0 ? cmin - W.pose_base : 0, span);
+  __syncthreads();
+  for (int k = 0; k < sg.z; ++k) ls_group<true>(d, o, sg.y + k, LsSup{gsp, cmin});
+}
+__global__ __launch_bounds__(kLsThreads) __attribute__((amdgpu_waves_per_eu(2))) void k_ba_ls_sup(BaDev d, LMOpt o) {
+  ls_run_sup(d, o, blockIdx.x);
+}
 
 // PM-K2: one workgroup per camera block (h, l) of a window: the partials of the window's groups
 // whose camera window holds the block, summed in group order.  Thread = (entry e, subset s); the
@@ -2593,7 +2657,7 @@ __device__ __forceinline__ void red_run(const BaDev& d, const LMOpt& o, const un
   double acc[kSp];
 #pragma unroll
   for (int q = 0; q < kSp; ++q) acc[q] = 0.0;
-  const int g0 = W.pblk_base, ng = W.n_pblk;
+  const int g0 = W.sg_base, ng = W.n_sg;
   for (int c0 = 0; c0 < ng; c0 += kRt * kRc) {
     int2 gs[kRc];
 #pragma unroll
@@ -3179,7 +3243,7 @@ struct lorb_ba_devbuild {
   int* cam_cnt = nullptr;     // C
   unsigned long long* bits = nullptr;
   int* perm = nullptr;        // C: input camera -> plan camera
-  int pblk_cap = 0, bp_cap = 0, part_cap = 0, gspan_cap = 0;
+  int pblk_cap = 0, bp_cap = 0, part_cap = 0, gspan_cap = 0, sgrp_cap = 0;
   size_t gpart_cap = 0;  // doubles of BaDev::gpart (the point groups' partials)
   std::vector<int> h_hdr, h_cov, h_cam;
   int* pinned = nullptr; size_t pinned_n = 0;
@@ -3225,10 +3289,12 @@ struct lorb_ba_plan {
   // point-group / block-pair kernels at capacity) replays the graph without a new capture
   struct GraphKey {
     int kind = -1, lds = 0, memset_env = 0, env_total = 0, grid_pblk = 0, grid_bp = 0, pt_launch = 0, x2_n = 0;
-    int red_wide = 0;
+    int red_wide = 0, sup = 0, grid_sg = 0;
     bool operator==(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) == 0; }
   } gkey;
   int grid_pblk = 0, grid_bp = 0;  // launch grids of the point-group and block-pair kernels
+  int grid_sg = 0;                 // k_ba_ls_sup's grid (partial runs)
+  bool has_super = false;          // some window's partial runs hold more than one point group
   int pt_launch = 0;               // points k_ba_init copies (Ptot, or the capacity)
   int* live = nullptr;             // device [n_pblk, n_bp] (BaDev::live)
   lorb_comm* comm = nullptr;  // sharded plan (not owned)
@@ -3422,7 +3488,16 @@ void pm_layout(BaWin& bw, int span_max, long long& total) {
   bw.part_cam = 36 * pm_nslots(span_max, bw.bwc);
   bw.part_stride = bw.part_cam + 18 * span_max;
   bw.part_base = total;
-  total += (long long)bw.n_pblk * bw.part_stride;
+  total += (long long)bw.n_sg * bw.part_stride;
+}
+// Partial runs: F consecutive point groups per k_ba_ls workgroup, one partial per run, when a window
+// has more point groups than one round of two workgroups per CU takes (F = 1 otherwise: C3 / C4
+// windows, alone or batched -- F depends on the window only, so a window's bits do not depend on its
+// plan's other windows).  LORB_SG_F=k forces k (tests).
+int sg_factor(int n_pblk) {
+  const char* e = getenv("LORB_SG_F");
+  if (e && atoi(e) >= 1) return n_pblk > 1 ? atoi(e) : 1;
+  return n_pblk > 512 ? (n_pblk + 479) / 480 : 1;
 }
 int part_budget_check(lorb_ctx* ctx, long long total) {
   if ((size_t)std::max(total, 1ll) * sizeof(double) > kPartBudgetBytes)
@@ -3518,6 +3593,8 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   std::vector<double2> obs_uv;
   std::vector<double> fixed, xpose, xpt;
   std::vector<PBlk> pblk;
+  std::vector<int2> gcam;   // per point group: first / last optimised camera (plan numbering)
+  std::vector<int4> sgrp;   // partial runs
   std::vector<BlockPair> bps;
   int pose_base = 0, point_base = 0, fix_base = 0, env_base = 0, row_base = 0, n_pairs = 0;
   long long part_total = 0;
@@ -3634,8 +3711,26 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
       }
       if (gmax >= 0) span_max = std::max(span_max, gmax - gmin + 1);
       pblk.push_back(g);
+      gcam.push_back(make_int2(gmin, gmax));
     }
     bw.n_pblk = (int)pblk.size() - bw.pblk_base;
+    {  // partial runs (super-groups) and the widest run's camera window
+      const int F = sg_factor(bw.n_pblk);
+      bw.sg_base = (int)sgrp.size();
+      if (F > 1) span_max = 0;
+      for (int g = 0; g < bw.n_pblk; g += F) {
+        const int ng = std::min(F, bw.n_pblk - g);
+        sgrp.push_back(make_int4(w, bw.pblk_base + g, ng, 0));
+        int umin = INT32_MAX, umax = -1;
+        for (int k = 0; k < ng; ++k) {
+          const int2 c = gcam[bw.pblk_base + g + k];
+          if (c.y >= 0) { umin = std::min(umin, c.x); umax = std::max(umax, c.y); }
+        }
+        if (F > 1 && umax >= 0) span_max = std::max(span_max, umax - umin + 1);
+      }
+      bw.n_sg = (int)sgrp.size() - bw.sg_base;
+      P->has_super = P->has_super || F > 1;
+    }
     pm_layout(bw, span_max, part_total);
     P->hwin.push_back(bw);
     pose_base += in.n_poses; point_base += in.n_points; fix_base += in.n_fixed;
@@ -3645,12 +3740,18 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   P->n_pblk = (int)pblk.size(); P->n_bp = (int)bps.size(); P->n_pairs = n_pairs;
   P->env_total = env_base; P->n_total = row_base;
   P->grid_pblk = P->n_pblk; P->grid_bp = P->n_bp; P->pt_launch = P->Ptot;
+  P->grid_sg = (int)sgrp.size();
   BaDev& d = P->dev;
   BaWin* dwin; PBlk* dpb; BlockPair* dbp; double2* duv;
   int *a1, *a2, *a3;
   double* dfix;
   LORB_TRY(dupload(P, P->hwin, &dwin)); d.win = dwin;
-  LORB_TRY(dupload(P, std::vector<int>{P->n_pblk, P->n_bp}, &P->live)); d.live = P->live;
+  LORB_TRY(dupload(P, std::vector<int>{P->n_pblk, P->n_bp, (int)sgrp.size()}, &P->live)); d.live = P->live;
+  {
+    int4* dsg;
+    LORB_TRY(dupload(P, sgrp.empty() ? std::vector<int4>{make_int4(0, 0, 0, 0)} : sgrp, &dsg));
+    d.sgrp = dsg;
+  }
   LORB_TRY(dupload(P, pblk, &dpb)); d.pblk = dpb;
   int* dopt;
   LORB_TRY(dupload(P, obs_pt, &dopt)); d.obs_pt = dopt;
@@ -3714,7 +3815,7 @@ int build_plan(lorb_ctx* ctx, int nw, const lorb_ba_window* win_in, lorb_ba_plan
   LORB_TRY(dalloc(P, (size_t)nw, &P->d_state)); d.st = P->d_state;
   LORB_TRY(dalloc(P, (size_t)nw * LORB_LM_TRACE_CAP, &d.trace));
   LORB_TRY(dalloc(P, (size_t)std::max(part_total, 1ll), &d.gpart));
-  LORB_TRY(dalloc(P, (size_t)std::max(P->n_pblk, 1), &d.gspan));
+  LORB_TRY(dalloc(P, (size_t)std::max(P->grid_sg, 1), &d.gspan));
   LORB_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return LORB_OK;
 }
@@ -3756,6 +3857,16 @@ void launch_red(const lorb_ba_plan* P, hipStream_t s, const BaDev& d, const LMOp
   else hipLaunchKernelGGL((k_ba_red<MODE, 256>), dim3(P->grid_bp), dim3(256), 0, s, d, o);
 }
 
+// the linearisation: one workgroup per point group, or per partial run (k_ba_ls_sup)
+void launch_ls(const lorb_ba_plan* P, hipStream_t s, const BaDev& d, const LMOpt& o) {
+  lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
+  if (P->has_super) {
+    if (P->grid_sg) hipLaunchKernelGGL(k_ba_ls_sup, dim3(P->grid_sg), dim3(kLsThreads), 0, s, d, o);
+  } else if (P->grid_pblk) {
+    hipLaunchKernelGGL(k_ba_ls, dim3(P->grid_pblk), dim3(kLsThreads), 0, s, d, o);
+  }
+}
+
 lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
   lorb_ba_plan::GraphKey k;
   k.kind = chol_kind_of(P);
@@ -3765,6 +3876,8 @@ lorb_ba_plan::GraphKey graph_key(const lorb_ba_plan* P) {
   k.grid_pblk = P->grid_pblk; k.grid_bp = P->grid_bp; k.pt_launch = P->pt_launch;
   k.x2_n = P->comm ? (int)x2_count(P) : 0;  // the captured all-reduce's count
   k.red_wide = red_threads(P);
+  k.sup = P->has_super ? 1 : 0;
+  k.grid_sg = P->grid_sg;
   return k;
 }
 
@@ -3773,10 +3886,7 @@ int enqueue_linearize(lorb_ba_plan* P, const LMOpt& o) {
   hipStream_t s = P->ctx->stream;
   const BaDev& d = P->dev;
   // the group partials, then the camera terms of the head
-  if (P->grid_pblk) {
-    lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-    hipLaunchKernelGGL(k_ba_ls, dim3(P->grid_pblk), dim3(kLsThreads), 0, s, d, o);
-  }
+  launch_ls(P, s, d, o);
   if (P->grid_bp) {
     lorb::KernelTimer kt(P->ctx, LORB_K_BA_SCHUR);
     launch_red<0>(P, s, d, o);
@@ -3807,10 +3917,7 @@ int enqueue_iteration(lorb_ba_plan* P, const LMOpt& o, bool first) {
   static const bool no_fuse = [] { const char* e = getenv("LORB_NO_FUSE"); return e && e[0] == '1'; }();
   const bool fused = !first && chol_kind_of(P) == 2 && !no_fuse;
   if (fused) {
-    if (P->grid_pblk) {
-      lorb::KernelTimer kt(P->ctx, LORB_K_BA_LINEARIZE);
-      hipLaunchKernelGGL(k_ba_ls, dim3(P->grid_pblk), dim3(kLsThreads), 0, s, d, o);
-    }
+    launch_ls(P, s, d, o);
   } else {
     LORB_TRY(enqueue_linearize(P, o));
   }
@@ -3984,7 +4091,7 @@ bool group_fused(const lorb_ba_group* G) {
   static const bool no_fuse = [] { const char* e = getenv("LORB_NO_FUSE"); return e && e[0] == '1'; }();
   if (no_fuse || G->ctx->ktime || G->plans.size() > (size_t)kGrpMax) return false;
   for (const lorb_ba_plan* P : G->plans)
-    if (P->W == 0 || P->comm || chol_kind_of(P) != 2) return false;
+    if (P->W == 0 || P->comm || P->has_super || chol_kind_of(P) != 2) return false;
   return true;
 }
 
@@ -4427,6 +4534,8 @@ struct DbFused {
   const int* up_src;
   int* up_dst;
   int up_words;
+  int sgf = 1, nsg = 0;  // partial runs: groups per run, runs
+  int4* sgrp = nullptr;
 };
 struct DbCams {  // kernel arguments: device plans hold <= kPmSpan cameras
   int perm[kPmSpan], gcam[kPmSpan];
@@ -4491,6 +4600,7 @@ __global__ __launch_bounds__(256) void k_db_gather(lorb_ba_window_dev w, BaDev d
       const_cast<PBlk*>(d.pblk)[g] = b;
     }
   }
+  for (int i = gt; i < f.nsg; i += gs) f.sgrp[i] = make_int4(0, i * f.sgf, min(f.sgf, f.G - i * f.sgf), 0);
   for (int i = gt; i < f.env_n; i += gs) d.env_part[i] = 0.0;
   for (int i = gt; i < f.bits_n; i += gs) f.bits[i] = 0ull;
   for (int i = gt; i < f.cov_n; i += gs) f.cov[i] = 0;
@@ -4961,8 +5071,10 @@ int dev_build_finish(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P
   bw.env_base = 0; bw.env_size = n * (bwid + 1); bw.n = n; bw.row_base = 0; bw.bw = bwid;
   bw.obs_base = 0; bw.n_obs = K; bw.n_obs_all = K_all;
   bw.fx = w->fx; bw.fy = w->fy; bw.cx = w->cx; bw.cy = w->cy;
+  const int SF = sg_factor(G), NSG = G > 0 ? (G + SF - 1) / SF : 0;  // partial runs (k_db_gather fills them)
+  bw.sg_base = 0; bw.n_sg = NSG;
   long long part_total = 0;
-  pm_layout(bw, C, part_total);  // a group spans at most the window's C <= kPmSpan cameras
+  pm_layout(bw, C, part_total);  // a group (or run) spans at most the window's C <= kPmSpan cameras
   LORB_TRY(part_budget_check(ctx, part_total));
   P->hwin[0] = bw;
   P->Ctot = C; P->Ptot = Pn; P->K = K; P->NF = F; P->n_pblk = G; P->n_bp = (int)bps.size(); P->n_pairs = n_pairs;
@@ -4997,7 +5109,12 @@ int dev_build_finish(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P
     int2* gsp = d.gspan;
     LORB_TRY(grow(P, &gsp, &b.gspan_cap, (size_t)b.pblk_cap));
     d.gspan = gsp;
+    int4* sgp = const_cast<int4*>(d.sgrp);
+    LORB_TRY(grow(P, &sgp, &b.sgrp_cap, (size_t)b.pblk_cap));
+    d.sgrp = sgp;
   }
+  P->has_super = SF > 1;
+  P->grid_sg = b.pblk_cap;  // runs <= groups: launched at the groups' capacity, live[2] in use
   LORB_TRY(up_alloc(P, (int)bps.size()));
   hp_mark(3);
   // one upload (pinned staging, stream-ordered; the next build writes the staging only after its
@@ -5008,7 +5125,7 @@ int dev_build_finish(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P
   {
     unsigned char* h = b.up_host;
     memcpy(h, &P->hwin[0], sizeof(BaWin));
-    const int live[2] = {G, (int)bps.size()};
+    const int live[3] = {G, (int)bps.size(), NSG};
     memcpy(h + b.off_live, live, sizeof(live));
     memcpy(h + b.off_perm, map.data(), sizeof(int) * C);
     memcpy(h + b.off_gcam, gcam, sizeof(int) * C);
@@ -5025,6 +5142,7 @@ int dev_build_finish(lorb_ctx* ctx, const lorb_ba_window_dev* w, lorb_ba_plan* P
     // all-reduce writes the global band every iteration)
     DbFused f{C, F, Pn, G, S, P->env_total, C * b.Wd, sorted ? 1 : 0, b.bits, b.hdr, b.cov, C * C + C,
               reinterpret_cast<const int*>(b.up_host_dev), reinterpret_cast<int*>(b.up_dev), up_words};
+    f.sgf = SF; f.nsg = NSG; f.sgrp = const_cast<int4*>(d.sgrp);
     DbCams cams;
     for (int c = 0; c < C; ++c) { cams.perm[c] = map[c]; cams.gcam[c] = gcam[c]; }
     hipLaunchKernelGGL(k_db_gather, dim3(std::max(NB, 1)), dim3(256), 0, s, *w, d, K, b.key_out, b.val_out, f, cams);
@@ -5184,9 +5302,11 @@ int lorb_ba_plan_info(lorb_ba_plan* plan, int32_t* info, int32_t n) {
   int reordered = 0;
   for (const auto& m : plan->cam_map)
     for (size_t c = 0; c < m.size(); ++c) reordered |= m[c] != (int)c;
-  const int32_t v[10] = {bw, plan->chol_kind, plan->n_bp, plan->n_pblk, plan->K, plan->Ptot, plan->Ctot, reordered,
-                         1, red_threads(plan)};
-  for (int i = 0; i < n && i < 10; ++i) info[i] = v[i];
+  int runs = 0;
+  for (const BaWin& w : plan->hwin) runs += w.n_sg;
+  const int32_t v[11] = {bw, plan->chol_kind, plan->n_bp, plan->n_pblk, plan->K, plan->Ptot, plan->Ctot, reordered,
+                         1, red_threads(plan), plan->has_super ? runs : 0};
+  for (int i = 0; i < n && i < 11; ++i) info[i] = v[i];
   return LORB_OK;
 }
 

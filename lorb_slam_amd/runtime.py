@@ -336,10 +336,10 @@ class BAPlan:
 
     def info(self):
         """lorb_ba_plan_info: structure of the plan and the Cholesky kernel of the last solve."""
-        v = (C.c_int32 * 10)()
-        self.ctx.check(lib().lorb_ba_plan_info(self._p, v, C.c_int32(10)), "lorb_ba_plan_info")
+        v = (C.c_int32 * 11)()
+        self.ctx.check(lib().lorb_ba_plan_info(self._p, v, C.c_int32(11)), "lorb_ba_plan_info")
         keys = ("band", "cholesky", "blocks", "point_groups", "observations", "points", "cameras", "reordered",
-                "point_major", "red_threads")
+                "point_major", "red_threads", "partial_runs")
         return dict(zip(keys, [int(x) for x in v]))
 
     def close(self):

@@ -460,6 +460,49 @@ def test_plan_group_members_stop_at_different_iterations(ctx):
             p.close()
 
 
+@pytest.mark.parametrize("f", [2, 5])
+def test_local_ba_partial_runs(ctx, f, monkeypatch):
+    """partial runs -- f consecutive point groups per k_ba_ls_sup workgroup, their
+    camera-block sums added into ONE partial (the path of windows with more than 512 point groups;
+    LORB_SG_F forces it here on C4 / C3 windows).  Oracle parity iteration by iteration, poses and
+    points within 1e-5; a window batched with another equals its solo solve bit for bit; the
+    device-built plan takes the same path."""
+    from lorb_slam_amd.runtime import BAPlan, BAPlanDev
+    monkeypatch.setenv("LORB_SG_F", str(f))
+    opt = A.LMOptions.default(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0)
+    w = synth.ba_window(seed=40, n_kf=50, n_pts=10000, n_fixed=5, fixed_obs_per_kf=400)
+    w3 = synth.ba_window(seed=3, n_kf=20, n_pts=4000, n_fixed=2, fixed_obs_per_kf=400)
+    plan = BAPlan(ctx, [w])
+    try:
+        plan.solve(opt)
+        (Pg,), (Xg,), (sg,) = plan.read()
+        gt, info = plan.trace(0), plan.info()
+    finally:
+        plan.close()
+    assert info["partial_runs"] == (info["point_groups"] + f - 1) // f, info
+    Po, Xo, so, ot = O.ba_local_traced(w, opt)
+    lm_match(sg, so, gt=gt, ot=ot, label=f"partial runs of {f}")
+    assert close(Pg, Po), np.abs(Pg - Po).max()
+    assert close(Xg, Xo), np.abs(Xg - Xo).max()
+    Pb, Xb, sb = ctx.ba_local([w3, w], opt)
+    Ps, Xs, ss = ctx.ba_local([w], opt)
+    assert np.array_equal(Pb[1], Ps[0]) and np.array_equal(Xb[1], Xs[0]) and sb[1] == ss[0]
+    arrays, order = _dev_window(ctx, w3)
+    dplan = BAPlanDev(ctx, arrays, len(w3["pose_init"]), len(w3["fixed_pose"]), w3["intr"])
+    try:
+        dplan.solve(opt)
+        Pd, Xd, sd = dplan.read()
+        dinfo = dplan.info()
+    finally:
+        dplan.close()
+        for a in arrays.values():
+            a.free()
+    assert dinfo["partial_runs"] == (dinfo["point_groups"] + f - 1) // f, dinfo
+    Po3, Xo3, so3 = O.ba_local([w3], opt)
+    lm_match(sd[0], so3[0])
+    assert close(Pd[0], Po3[0]) and close(Xd[0], Xo3[0])
+
+
 def _dev_window(ctx, w, extra_pts=37, extra_obs=500, shuffle_seed=None, holes=0):
     """Upload window w into device arrays with spare capacity, optionally with the observations in
     a shuffled slot order and `holes` unused slots (frame < -n_fixed) spread among them."""
