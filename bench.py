@@ -56,7 +56,7 @@ OPS_PER_PAIR = 16                            # 8 x v_xor_b32 + 8 x v_bcnt_u32_b3
 # elimination + per-group Schur partials), timer 2 k_ba_red (the partials' fixed-order sum into the band)
 K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_red", 3: "k_ba_ls", 4: "k_ba_chol_2s"}
 # rocprofv3 short names (tools/pmc_traffic.py) of the same kernels, for the PMC traffic lookup
-K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: K_NAMES[2], 3: K_NAMES[3], 4: "k_ba_chol_2s"}
+K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: K_NAMES[2], 3: ("k_ba_ls_sup", K_NAMES[3]), 4: "k_ba_chol_2s"}
 
 
 def ba_kspec(W, n_obs, n_pts, F, bw):
@@ -799,9 +799,11 @@ def pmc_traffic(workload, kernel):
         except (OSError, ValueError):
             continue
         wls = tab.get("workloads") or {"c4": tab}  # r01 files hold the c4 workload only
-        ent = wls.get(workload, {}).get("kernels", {}).get(kernel)
-        if ent is not None and ent.get("hbm_bytes_per_launch") is not None:
-            return {"hbm_bytes_per_launch": ent["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
+        for name in (kernel if isinstance(kernel, tuple) else (kernel,)):
+            ent = wls.get(workload, {}).get("kernels", {}).get(name)
+            if ent is not None and ent.get("hbm_bytes_per_launch") is not None:
+                return {"hbm_bytes_per_launch": ent["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT),
+                        "kernel": name}
     return None
 
 
@@ -829,7 +831,7 @@ def roofline_entry(kt, wl, steps):
     tr = pmc_traffic(wl["traffic_key"], K_PROF.get(k, name)) if wl.get("traffic_key") else None
     return {"bound": bound, "achieved": achieved / scale, "peak": peak / scale, "unit": unit,
             "frac": achieved / peak, "traffic": tr["hbm_bytes_per_launch"] if tr else None,
-            "traffic_source": tr["source"] if tr else None, "kernel": name,
+            "traffic_source": tr["source"] if tr else None, "kernel": tr["kernel"] if tr else name,
             "algorithmic_per_launch": amount, "avg_kernel_us": avg_s * 1e6, "launches_per_step": per_step,
             "all_kernels_ms_per_step": {K_NAMES.get(kk, str(kk)): v[0] / steps for kk, v in kt.items()}}
 
