@@ -56,7 +56,9 @@ OPS_PER_PAIR = 16                            # 8 x v_xor_b32 + 8 x v_bcnt_u32_b3
 # elimination + per-group Schur partials), timer 2 k_ba_red (the partials' fixed-order sum into the band)
 K_NAMES = {0: "k_bf_scan<top2>", 1: "k_bf_scan<top1>", 2: "k_ba_red", 3: "k_ba_ls", 4: "k_ba_chol_2s"}
 # rocprofv3 short names (tools/pmc_traffic.py) of the same kernels, for the PMC traffic lookup
-K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: K_NAMES[2], 3: ("k_ba_ls_sup", K_NAMES[3]), 4: "k_ba_chol_2s"}
+# (the plan-group launches of map groups first, then partial runs, then the one-plan kernels)
+K_PROF = {0: "k_bf_scan", 1: "k_bf_scan", 2: ("k_ba_red_g", K_NAMES[2]), 3: ("k_ba_ls_g", "k_ba_ls_sup", K_NAMES[3]),
+          4: ("k_ba_chol_2s_g", "k_ba_chol_2s")}
 
 
 def ba_kspec(W, n_obs, n_pts, F, bw):
@@ -268,7 +270,8 @@ def workload_c4(ctx, args, rank):
     nq = len(seqs[0]["steps"][0]["x"])
     bw = 6 * 8 - 1
     opt_obs = n_obs  # window observations; the fixed ones (~4%) are in n_obs too
-    kspec = ba_kspec(W, opt_obs, n_pts, F, bw)
+    # per launch: the profile pass times the first context's launches, each over its group's G windows
+    kspec = ba_kspec(G, opt_obs, n_pts, F, bw)
 
     def cleanup():
         for g in groups or []:

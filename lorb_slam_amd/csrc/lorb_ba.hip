@@ -4089,7 +4089,7 @@ namespace {
 // own path (the same bits either way)
 bool group_fused(const lorb_ba_group* G) {
   static const bool no_fuse = [] { const char* e = getenv("LORB_NO_FUSE"); return e && e[0] == '1'; }();
-  if (no_fuse || G->ctx->ktime || G->plans.size() > (size_t)kGrpMax) return false;
+  if (no_fuse || G->plans.size() > (size_t)kGrpMax) return false;
   for (const lorb_ba_plan* P : G->plans)
     if (P->W == 0 || P->comm || P->has_super || chol_kind_of(P) != 2) return false;
   return true;
@@ -4143,6 +4143,7 @@ int enqueue_group_solve(lorb_ba_group* G, const LMOpt& o) {
   size_t lds = 0;
   for (const lorb_ba_plan* P : G->plans) lds = std::max(lds, sizeof(double) * (size_t)P->max_env_w);
   auto linearise = [&]() {
+    lorb::KernelTimer kt(ctx, LORB_K_BA_LINEARIZE);
     if (g_pb.pre[n]) hipLaunchKernelGGL(k_ba_ls_g, dim3(g_pb.pre[n]), dim3(kLsThreads), 0, s, bg, g_pb, o);
   };
   if (o.max_iter <= 0) {  // one linearisation (cost, termination) as the head of a first iteration
@@ -4156,18 +4157,27 @@ int enqueue_group_solve(lorb_ba_group* G, const LMOpt& o) {
     const bool first = it == 0;
     linearise();
     if (first) {
-      launch_red_g<0>(G, s, bg, o);
+      {
+        lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
+        launch_red_g<0>(G, s, bg, o);
+      }
       hipLaunchKernelGGL(k_ba_lm_begin_g, dim3(g_w.pre[n]), dim3(64), 0, s, bg, g_w, o);
     }
     for (const lorb_ba_plan* P : G->plans)  // (the two-sided Cholesky holds its band in LDS: none)
       if (P->env_total && sizeof(double) * (size_t)P->max_env > (size_t)kLdsBudget)
         LORB_HIP(ctx, hipMemsetAsync(P->dev.env, 0, sizeof(double) * P->env_total, s));
-    if (first) launch_red_g<1>(G, s, bg, o);
-    else launch_red_g<2>(G, s, bg, o);
-    if (first)
-      hipLaunchKernelGGL(k_ba_chol_2s_g<false>, dim3(g_w.pre[n]), dim3(kChol2sThreads), lds, s, bg, g_w, o);
-    else
-      hipLaunchKernelGGL(k_ba_chol_2s_g<true>, dim3(g_w.pre[n]), dim3(kChol2sThreads), lds, s, bg, g_w, o);
+    {
+      lorb::KernelTimer kt(ctx, LORB_K_BA_SCHUR);
+      if (first) launch_red_g<1>(G, s, bg, o);
+      else launch_red_g<2>(G, s, bg, o);
+    }
+    {
+      lorb::KernelTimer kt(ctx, LORB_K_BA_CHOLESKY);
+      if (first)
+        hipLaunchKernelGGL(k_ba_chol_2s_g<false>, dim3(g_w.pre[n]), dim3(kChol2sThreads), lds, s, bg, g_w, o);
+      else
+        hipLaunchKernelGGL(k_ba_chol_2s_g<true>, dim3(g_w.pre[n]), dim3(kChol2sThreads), lds, s, bg, g_w, o);
+    }
     if (g_pb.pre[n]) hipLaunchKernelGGL(k_ba_bs2_g, dim3(g_pb.pre[n]), dim3(kGB), 0, s, bg, g_pb);
     hipLaunchKernelGGL(k_ba_lm_end_g, dim3(g_w.pre[n]), dim3(64), 0, s, bg, g_w, o);
   }
@@ -4185,7 +4195,7 @@ int group_solve(lorb_ba_group* G, const lorb_lm_options* opt) {
   }
   const LMOpt o = to_dev_opt(opt);
   static const bool no_graph = [] { const char* e = getenv("LORB_NO_GRAPH"); return e && e[0] == '1'; }();
-  if (no_graph) {
+  if (no_graph || ctx->ktime) {  // per-kernel timing: eager launches (events cannot live in a graph)
     LORB_TRY(enqueue_group_solve(G, o));
     G->n_fused++;
     return LORB_OK;
