@@ -53,6 +53,15 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
   return r;
 }
 
+// (dist << kIdxBits) + idx as ONE v_lshl_add_u32 with the index in an SGPR: the index goes through
+// an opaque scalar move (written as plain C++, the compiler folds the step offset into an immediate
+// and splits all but one key per step into v_lshlrev + v_add3)
+__device__ __forceinline__ uint32_t make_key(uint32_t d, uint32_t idx) {
+  asm("s_mov_b32 %0, %0" : "+s"(idx));
+  return (d << kIdxBits) + idx;
+}
+static_assert(kIdxBits == 23, "make_key's shift");
+
 __device__ __forceinline__ uint32_t hamming256(const uint4& a0, const uint4& a1, const uint4& b0,
                                                const uint4& b1) {
   uint32_t d = __builtin_popcount(a0.x ^ b0.x);
@@ -92,35 +101,43 @@ __device__ __forceinline__ void scan_tile(const uint4* __restrict__ lane_desc, c
   const int n = tl.uni_count;
   int j = 0;
   // 4 train descriptors per step in SGPRs (s_load); the next step's are requested before this
-  // step's 19 x 4 x QPL VALU ops, so the scalar-cache / L2 latency hides behind them
-  uint4 bn[8];
-  if (n >= 4) {
-#pragma unroll
-    for (int s = 0; s < 8; ++s) bn[s] = u[s];
-  }
-  for (; j + 4 <= n; j += 4) {
-    uint4 b[8];
-#pragma unroll
-    for (int s = 0; s < 8; ++s) b[s] = bn[s];
-    if (j + 8 <= n) {
-#pragma unroll
-      for (int s = 0; s < 8; ++s) bn[s] = u[2 * (j + 4) + s];
-    }
+  // step's 18 x 4 x QPL VALU ops, so the scalar-cache / L2 latency hides behind them.  Two steps
+  // per iteration on two register sets, so no set is copied into the other between steps.
+  auto step = [&](const uint4 (&b)[8], int js) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
 #pragma unroll
       for (int r = 0; r < QPL; ++r) {
-        const uint32_t key = (hamming256(a[r][0], a[r][1], b[2 * s], b[2 * s + 1]) << kIdxBits) + kb + (uint32_t)(j + s);
+        const uint32_t key = make_key(hamming256(a[r][0], a[r][1], b[2 * s], b[2 * s + 1]), kb + (uint32_t)(js + s));
         if (TOP2) k2[r] = umed3(k1[r], key, k2[r]);
         k1[r] = min(k1[r], key);
       }
     }
+  };
+  uint4 bA[8], bB[8];
+  if (n >= 4) {  // bA: the descriptors of step j whenever j + 4 <= n at the loop head
+#pragma unroll
+    for (int s = 0; s < 8; ++s) bA[s] = u[s];
+  }
+  for (; j + 8 <= n; j += 8) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s) bB[s] = u[2 * (j + 4) + s];
+    step(bA, j);
+    if (j + 12 <= n) {
+#pragma unroll
+      for (int s = 0; s < 8; ++s) bA[s] = u[2 * (j + 8) + s];
+    }
+    step(bB, j + 4);
+  }
+  if (j + 4 <= n) {
+    step(bA, j);
+    j += 4;
   }
   for (; j < n; ++j) {
     const uint4 b0 = u[2 * j], b1 = u[2 * j + 1];
 #pragma unroll
     for (int r = 0; r < QPL; ++r) {
-      const uint32_t key = (hamming256(a[r][0], a[r][1], b0, b1) << kIdxBits) + kb + (uint32_t)j;
+      const uint32_t key = make_key(hamming256(a[r][0], a[r][1], b0, b1), kb + (uint32_t)j);
       if (TOP2) k2[r] = umed3(k1[r], key, k2[r]);
       k1[r] = min(k1[r], key);
     }
