@@ -22,6 +22,24 @@ def test_top2_single(ctx, nq, nt, random_levels):
         assert (got[k] == ref[k]).all(), k
 
 
+@pytest.mark.parametrize("nt", [2, 3, 4, 5, 8, 11, 12, 13, 19, 28])
+def test_top2_scan_remainders(ctx, nt):
+    """Train counts around the scan loop's shape (two 4-descriptor steps per iteration, then one
+    step, then single descriptors): every remainder path, bit-exact."""
+    q, t, lev = synth.bf_problem(seed=700 + nt, nq=70, nt=nt, n_planted=min(70, nt) // 2, random_levels=True)
+    got, _ = ctx.bf_top2([q], [t], [lev])
+    ref = _oracle_top2(q, t, lev)
+    for k in ref:
+        assert (got[k] == ref[k]).all(), k
+    got, _ = ctx.bf_match([q], [t])  # the top-1 scans (crossCheck, both directions)
+    ref = O.bf_match(q, t)
+    m = ref["cc_train"] >= 0
+    assert (got["cc_train"] == ref["cc_train"]).all()
+    assert (got["cc_dist"][m] == ref["cc_dist"][m]).all()
+    assert (got["match_train"] == ref["match_train"]).all()
+    assert got["n_matches"][0] == ref["n_matches"]
+
+
 def test_top2_batched_ragged(ctx):
     rng = np.random.default_rng(11)
     qs, ts, ls = [], [], []
